@@ -1,0 +1,575 @@
+// gc_core.h -- bitboard chess core for the batched env (gfx950 device code; also
+// host-compilable so tests/ can differential-test it against the C oracle).
+//
+// Semantics are the reference engine's, /root/reference/src/lib.rs, NOT FIDE chess
+// (SURVEY.md §0 Q1-Q10).  Square numbering is the reference's flat index
+// sq = row*8 + col with row 0 = rank 8 (lib.rs:1235-1238); bit sq of a bitboard is
+// that square.  Board state per lane: 7 bitboards (K,Q,R,B,N,P by type, both colours,
+// plus white occupancy) and a 32-bit meta word.
+//
+// Every function is a pure function of its arguments (no tables, no memory):
+// slider attacks use hyperbola quintessence with a full 64-bit bit reversal
+// (v_bfrev_b32 x2), line masks are computed arithmetically, so one lane = one board
+// needs no LDS and no cache traffic beyond its own state.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define GC_HD __host__ __device__ __forceinline__
+#else
+#define GC_HD static inline
+#endif
+
+namespace gc {
+
+typedef uint64_t u64;
+typedef uint32_t u32;
+
+// ---- piece ids (lib.rs:11-17) and values (lib.rs:19-25) ------------------------
+enum { EMPTY = 0, KING = 1, QUEEN = 2, ROOK = 3, BISHOP = 4, KNIGHT = 5, PAWN = 6 };
+// actions (chess_v2.py:492-506)
+enum { A_KSW = 4096, A_QSW = 4097, A_KSB = 4098, A_QSB = 4099, A_RESIGN = 4100, A_NONE = 0xFFFF };
+
+// ---- meta word layout ----------------------------------------------------------
+// bit 0      side to move (1 = WHITE)
+// bits 1..4  castle rights wkc, wqc, bkc, bqc (as the reference's state dict stores them)
+// bit 5      white_king_is_checked     bit 6  black_king_is_checked
+// bit 7      env done flag (chess_v2.py self.done)
+// bits 8..15 env move_count (chess_v2.py:194, 291-292; <= 150)
+// bits 16..24 repetition-window length (<= 300)
+enum : u32 {
+    M_WHITE = 1u, M_WKC = 2u, M_WQC = 4u, M_BKC = 8u, M_BQC = 16u, M_RIGHTS = 30u,
+    M_WCHK = 32u, M_BCHK = 64u, M_DONE = 128u,
+    M_MC_SHIFT = 8, M_MC_MASK = 0xFFu << 8,
+    M_HL_SHIFT = 16, M_HL_MASK = 0x1FFu << 16,
+};
+
+// ---- step reasons (per-ply info code) -------------------------------------------
+enum { R_NONE = 0, R_MATE = 1, R_REPETITION = 2, R_MOVE_CAP = 3, R_NO_MOVES = 4, R_BOTH_CHECKED = 5,
+       R_INVALID = 6, R_DONE_ALREADY = 7 };
+
+struct Pos {
+    u64 k, q, r, b, n, p, w;  // by type (both colours) + white occupancy
+    u32 meta;
+};
+
+static constexpr u64 FILE_A = 0x0101010101010101ull;  // col 0
+static constexpr u64 FILE_H = 0x8080808080808080ull;  // col 7
+static constexpr u64 DIAG = 0x8040201008040201ull;    // row == col
+static constexpr u64 ANTI = 0x0102040810204080ull;    // row + col == 7
+
+GC_HD int popc(u64 x) { return __builtin_popcountll(x); }
+GC_HD int ctz(u64 x) { return __builtin_ctzll(x); }
+GC_HD int msb(u64 x) { return 63 - __builtin_clzll(x); }
+GC_HD u64 bit(int s) { return 1ull << s; }
+
+GC_HD u64 rbit(u64 x) {
+#if defined(__clang__)
+    return __builtin_bitreverse64(x);
+#else
+    x = ((x >> 1) & 0x5555555555555555ull) | ((x & 0x5555555555555555ull) << 1);
+    x = ((x >> 2) & 0x3333333333333333ull) | ((x & 0x3333333333333333ull) << 2);
+    x = ((x >> 4) & 0x0F0F0F0F0F0F0F0Full) | ((x & 0x0F0F0F0F0F0F0F0Full) << 4);
+    return __builtin_bswap64(x);
+#endif
+}
+
+GC_HD u64 occ_of(const Pos& s) { return s.k | s.q | s.r | s.b | s.n | s.p; }
+
+// ---- line masks (arithmetic) ------------------------------------------------------
+GC_HD u64 file_mask(int sq) { return FILE_A << (sq & 7); }
+GC_HD u64 row_mask(int sq) { return 0xFFull << (sq & 56); }
+GC_HD u64 diag_mask(int sq) {  // row - col = d
+    int d = (sq >> 3) - (sq & 7);
+    return d >= 0 ? DIAG << (8 * d) : DIAG >> (-8 * d);
+}
+GC_HD u64 anti_mask(int sq) {  // row + col = s
+    int s = (sq >> 3) + (sq & 7);
+    return s >= 7 ? ANTI << (8 * (s - 7)) : ANTI >> (8 * (7 - s));
+}
+
+// hyperbola quintessence on one line (mask includes the slider square)
+GC_HD u64 line_att(u64 occ, u64 mask, u64 s) {
+    u64 m = mask ^ s;
+    u64 o = occ & m;
+    u64 fwd = o - s;
+    u64 rev = rbit(o) - rbit(s);
+    return (fwd ^ rbit(rev)) & m;
+}
+GC_HD u64 rook_att(int sq, u64 occ) {
+    u64 s = bit(sq);
+    return line_att(occ, file_mask(sq), s) | line_att(occ, row_mask(sq), s);
+}
+GC_HD u64 bishop_att(int sq, u64 occ) {
+    u64 s = bit(sq);
+    return line_att(occ, diag_mask(sq), s) | line_att(occ, anti_mask(sq), s);
+}
+
+// leapers (set-wise; wrap masks per direction)
+GC_HD u64 knight_set(u64 x) {
+    u64 l1 = (x >> 1) & ~FILE_H, l2 = (x >> 2) & ~(FILE_H | (FILE_H >> 1));
+    u64 r1 = (x << 1) & ~FILE_A, r2 = (x << 2) & ~(FILE_A | (FILE_A << 1));
+    u64 h1 = l1 | r1, h2 = l2 | r2;
+    return (h1 << 16) | (h1 >> 16) | (h2 << 8) | (h2 >> 8);
+}
+GC_HD u64 king_set(u64 x) {
+    u64 h = ((x >> 1) & ~FILE_H) | ((x << 1) & ~FILE_A);
+    u64 row = x | h;
+    return h | (row << 8) | (row >> 8);
+}
+// pawn capture squares (r-p, c+1) and (r-p, c-1), p=+1 white (lib.rs:921-924)
+GC_HD u64 pawn_att_set(u64 x, bool white) {
+    return white ? (((x >> 7) & ~FILE_A) | ((x >> 9) & ~FILE_H))
+                 : (((x << 9) & ~FILE_A) | ((x << 7) & ~FILE_H));
+}
+
+// in-between squares (exclusive) on a shared line, else 0 (branch-free, CPW formula)
+GC_HD u64 between(int sq1, int sq2) {
+    const u64 m1 = ~0ull;
+    const u64 a2a7 = 0x0001010101010100ull;
+    const u64 b2g7 = 0x0040201008040200ull;
+    const u64 h1b7 = 0x0002040810204080ull;
+    u64 btwn = (m1 << sq1) ^ (m1 << sq2);
+    u64 file = (u64)((sq2 & 7) - (sq1 & 7));
+    u64 rank = (u64)(((sq2 | 7) - sq1) >> 3);
+    u64 line = ((file & 7) - 1) & a2a7;
+    line += 2 * (((rank & 7) - 1) >> 58);
+    line += (((rank - file) & 15) - 1) & b2g7;
+    line += (((rank + file) & 15) - 1) & h1b7;
+    line *= btwn & (0 - btwn);
+    return line & btwn;
+}
+// the full line through a and b (a != b, aligned); isolates one pin segment from the union
+GC_HD u64 line_through(int a, int b) {
+    int dr = (b >> 3) - (a >> 3), dc = (b & 7) - (a & 7);
+    if (dc == 0) return file_mask(a);
+    if (dr == 0) return row_mask(a);
+    if (dr == dc) return diag_mask(a);
+    if (dr == -dc) return anti_mask(a);
+    return 0;
+}
+
+// ---- piece lookup -------------------------------------------------------------------
+GC_HD int type_at(const Pos& s, int sq) {
+    u64 m = bit(sq);
+    if (s.p & m) return PAWN;
+    if (s.n & m) return KNIGHT;
+    if (s.b & m) return BISHOP;
+    if (s.r & m) return ROOK;
+    if (s.q & m) return QUEEN;
+    if (s.k & m) return KING;
+    return EMPTY;
+}
+GC_HD int id_at(const Pos& s, int sq) {
+    int t = type_at(s, sq);
+    return (s.w >> sq) & 1 ? t : -t;
+}
+GC_HD void clear_sq(Pos& s, int sq) {
+    u64 m = ~bit(sq);
+    s.k &= m; s.q &= m; s.r &= m; s.b &= m; s.n &= m; s.p &= m; s.w &= m;
+}
+GC_HD void put(Pos& s, int sq, int id) {  // square must be clear
+    if (id == 0) return;
+    u64 m = bit(sq);
+    int t = id < 0 ? -id : id;
+    switch (t) {
+        case KING: s.k |= m; break;
+        case QUEEN: s.q |= m; break;
+        case ROOK: s.r |= m; break;
+        case BISHOP: s.b |= m; break;
+        case KNIGHT: s.n |= m; break;
+        default: s.p |= m; break;
+    }
+    if (id > 0) s.w |= m;
+}
+
+// ---- attack map of one side (lib.rs:669-677, attack mode, 1089-1104/1147-1174/928-933)
+// Sliders stop at and include the first piece of either colour (so a slider ray ends AT a
+// king: Q6); knights/kings every on-board target; pawns both diagonals except squares
+// holding the pawn owner's own king (lib.rs:930).
+GC_HD u64 side_attacks(const Pos& s, bool white) {
+    u64 occ = occ_of(s);
+    u64 mine = white ? s.w : (occ & ~s.w);
+    u64 a = pawn_att_set(s.p & mine, white) & ~(s.k & mine);
+    a |= knight_set(s.n & mine) | king_set(s.k & mine);
+    u64 rq = (s.r | s.q) & mine;
+    while (rq) { int sq = ctz(rq); rq &= rq - 1; a |= rook_att(sq, occ); }
+    u64 bq = (s.b | s.q) & mine;
+    while (bq) { int sq = ctz(bq); bq &= bq - 1; a |= bishop_att(sq, occ); }
+    return a;
+}
+
+// is square `sq` in `by_white`'s attack map? (the map membership test of lib.rs:661)
+GC_HD bool sq_attacked(const Pos& s, int sq, bool by_white) {
+    u64 occ = occ_of(s);
+    u64 them = by_white ? s.w : (occ & ~s.w);
+    u64 m = bit(sq);
+    // pawn attack squares exclude squares holding the pawn owner's own king
+    if (!(s.k & them & m) && (pawn_att_set(m, !by_white) & s.p & them)) return true;
+    if (knight_set(m) & s.n & them) return true;
+    if (king_set(m) & s.k & them) return true;
+    if (rook_att(sq, occ) & (s.r | s.q) & them) return true;
+    if (bishop_att(sq, occ) & (s.b | s.q) & them) return true;
+    return false;
+}
+
+// tracked king square of a colour, or -1 (lib.rs:641-653: the `break` leaves only the
+// inner loop, so the LAST row holding a king wins, first column within it)
+GC_HD int tracked_king(const Pos& s, bool white) {
+    u64 occ = occ_of(s);
+    u64 kk = s.k & (white ? s.w : (occ & ~s.w));
+    if (!kk) return -1;
+    int row = msb(kk) >> 3;
+    return ctz(kk & (0xFFull << (8 * row)));
+}
+
+// castle rights as the engine sees them on every call: State::new forces a colour's
+// rights false when it has no king (lib.rs:315-322)
+GC_HD u32 eff_rights(const Pos& s) {
+    u64 occ = occ_of(s);
+    u32 r = s.meta & M_RIGHTS;
+    if (!(s.k & s.w)) r &= ~(M_WKC | M_WQC);
+    if (!(s.k & occ & ~s.w)) r &= ~(M_BKC | M_BQC);
+    return r;
+}
+
+// update_state (lib.rs:1386-1393): both check flags from the board
+GC_HD u32 check_flags(const Pos& s) {
+    u32 f = 0;
+    int wk = tracked_king(s, true), bk = tracked_king(s, false);
+    if (wk >= 0 && sq_attacked(s, wk, false)) f |= M_WCHK;
+    if (bk >= 0 && sq_attacked(s, bk, true)) f |= M_BCHK;
+    return f;
+}
+
+// ---- legal move generation context ----------------------------------------------------
+struct Gen {
+    u64 own, opp, occ;
+    u64 checkmask;  // non-king targets must lie in it
+    u64 pinned;     // own non-king pieces pinned to the tracked king
+    u64 pinrays;    // union over pinners of between(king, pinner) | pinner
+    u64 enemy_att;  // enemy attack map (king moves, castling); 0 if we have no king
+    int ks;         // tracked king square or -1 (no legality filter)
+    u32 castles;    // bit0 = queen side, bit1 = king side (reference order QS, KS)
+    bool white;
+};
+
+// Legality: the reference filters every non-king move by next_state + a full enemy
+// attack-map recompute + "is my (tracked) king in it" (lib.rs:561, 612-632).  For
+// en-passant-free rules that is exactly "target in checkmask AND (not pinned OR on the
+// pin segment king..pinner)".  The segment, not the whole line: a pinned pawn's double
+// push jumps blockers (Q1) and can land beyond its pinner or beyond its own king.  King moves are filtered by the pre-move enemy map instead (lib.rs:613-619,
+// 1125-1128), which keeps the Q6 retreat-along-the-ray quirk.
+GC_HD void gen_init(const Pos& s, Gen& g) {
+    bool white = s.meta & M_WHITE;
+    g.white = white;
+    g.occ = occ_of(s);
+    g.own = white ? s.w : (g.occ & ~s.w);
+    g.opp = g.occ ^ g.own;
+    g.ks = tracked_king(s, white);
+    g.checkmask = ~0ull;
+    g.pinned = 0;
+    g.pinrays = 0;
+    g.enemy_att = 0;
+    g.castles = 0;
+    if (g.ks < 0) return;  // "King not present": no filter, no castling, no king moves
+    int ks = g.ks;
+    u64 kb = bit(ks);
+    u64 opp = g.opp;
+    u64 rq = (s.r | s.q) & opp, bq = (s.b | s.q) & opp;
+    u64 checkers = (pawn_att_set(kb, white) & s.p & opp) | (knight_set(kb) & s.n & opp) |
+                   (king_set(kb) & s.k & opp) | (rook_att(ks, g.occ) & rq) | (bishop_att(ks, g.occ) & bq);
+    if (checkers) {
+        if (checkers & (checkers - 1)) g.checkmask = 0;
+        else g.checkmask = checkers | between(ks, ctz(checkers));
+    }
+    u64 snipers = (rook_att(ks, opp) & rq) | (bishop_att(ks, opp) & bq);
+    while (snipers) {
+        int sq = ctz(snipers);
+        snipers &= snipers - 1;
+        u64 bw = between(ks, sq) & g.occ;
+        if (bw && !(bw & (bw - 1)) && (bw & g.own)) {
+            g.pinned |= bw;
+            g.pinrays |= between(ks, sq) | bit(sq);
+        }
+    }
+    g.enemy_att = side_attacks(s, !white);
+    // castling (lib.rs:578-610 gate = OR of the colour's rights + king on board;
+    // geometry lib.rs:966-1056 tests the POSITIVE ids for black too: Q4)
+    u32 er = eff_rights(s);
+    bool gate = white ? (er & (M_WKC | M_WQC)) : (er & (M_BKC | M_BQC));
+    if (gate) {
+        u64 wr = s.r & s.w, wk = s.k & s.w, A = g.enemy_att, occ = g.occ;
+        int base = white ? 56 : 0;
+        u64 qs_empty = 7ull << (base + 1), ks_empty = 3ull << (base + 5);
+        u64 qs_safe = 7ull << (base + 2), ks_safe = 7ull << (base + 4);
+        bool kpos = wk & bit(base + 4);
+        if (kpos && (wr & bit(base)) && !(occ & qs_empty) && !(A & qs_safe)) g.castles |= 1;
+        if (kpos && (wr & bit(base + 7)) && !(occ & ks_empty) && !(A & ks_safe)) g.castles |= 2;
+    }
+}
+
+// pseudo targets (non-attack mode) of the own piece on `sq` of type `t`, before legality
+GC_HD u64 pseudo_targets(const Pos& s, const Gen& g, int sq, int t) {
+    u64 notown = ~g.own;
+    switch (t) {
+        case QUEEN: return (rook_att(sq, g.occ) | bishop_att(sq, g.occ)) & notown;
+        case ROOK: return rook_att(sq, g.occ) & notown;
+        case BISHOP: return bishop_att(sq, g.occ) & notown;
+        case KNIGHT: return knight_set(bit(sq)) & notown;
+        case PAWN: {
+            // lib.rs:935-958: one step if empty; two step from the start row if the
+            // DESTINATION is empty (Q1); diagonal captures of any enemy piece (incl. king)
+            u64 m = bit(sq), empty = ~g.occ, tg = 0;
+            int row = sq >> 3;
+            if (g.white) {
+                tg |= (m >> 8) & empty;
+                if (row == 6) tg |= (m >> 16) & empty;
+            } else {
+                tg |= (m << 8) & empty;
+                if (row == 1) tg |= (m << 16) & empty;
+            }
+            return tg | (pawn_att_set(m, g.white) & g.opp);
+        }
+        default: return 0;
+    }
+}
+
+GC_HD u64 legal_targets(const Pos& s, const Gen& g, int sq, int t) {
+    if (t == KING) return king_set(bit(sq)) & ~g.own & ~g.enemy_att;
+    u64 tg = pseudo_targets(s, g, sq, t);
+    if (g.ks < 0) return tg;
+    tg &= g.checkmask;
+    if (g.pinned & bit(sq)) tg &= g.pinrays & line_through(g.ks, sq);
+    return tg;
+}
+
+// attack-mode targets (get_possible_moves(attack=True), lib.rs:556-557)
+GC_HD u64 attack_targets(const Pos& s, const Gen& g, int sq, int t) {
+    u64 m = bit(sq);
+    switch (t) {
+        case KING: return king_set(m);
+        case QUEEN: return rook_att(sq, g.occ) | bishop_att(sq, g.occ);
+        case ROOK: return rook_att(sq, g.occ);
+        case BISHOP: return bishop_att(sq, g.occ);
+        case KNIGHT: return knight_set(m);
+        case PAWN: return pawn_att_set(m, g.white) & ~(s.k & g.own);
+        default: return 0;
+    }
+}
+
+// ---- reference move ORDER within one piece ---------------------------------------------
+// Returns the k-th target (0-based) of piece (sq, t) in the reference emission order.
+//   K: (1,0),(-1,0),(0,1),(0,-1),(1,1),(1,-1),(-1,1),(-1,-1)   lib.rs:797-806
+//   N: (-2,-1),(-2,1),(2,-1),(2,1),(-1,-2),(-1,2),(1,-2),(1,2)  lib.rs:891-900
+//   P: one, two, (r-p,c+1), (r-p,c-1)                            lib.rs:921-958
+//   R: rays (-1,0),(1,0),(0,-1),(0,1) outward                    lib.rs:835
+//   B: rays (-1,-1),(-1,1),(1,-1),(1,1) outward                  lib.rs:845
+//   Q: rook rays then bishop rays                                 lib.rs:824-831
+GC_HD int kth_bit_desc(u64 x, int k) {
+    for (int i = 0; i < k; i++) x &= ~bit(msb(x));
+    return msb(x);
+}
+GC_HD int kth_bit_asc(u64 x, int k) {
+    for (int i = 0; i < k; i++) x &= x - 1;
+    return ctz(x);
+}
+GC_HD int ray_pick(u64 tg, int sq, u64 fm, u64 rm, u64 dm, u64 am, bool rook, bool bish, int& k) {
+    // outward from sq: rays toward lower indices are walked high->low ("desc")
+    u64 below = bit(sq) - 1, above = ~below & ~bit(sq);
+    u64 grp[8];
+    bool desc[8];
+    int n = 0;
+    if (rook) {
+        grp[n] = tg & fm & below; desc[n++] = true;   // (-1, 0)
+        grp[n] = tg & fm & above; desc[n++] = false;  // (+1, 0)
+        grp[n] = tg & rm & below; desc[n++] = true;   // (0, -1)
+        grp[n] = tg & rm & above; desc[n++] = false;  // (0, +1)
+    }
+    if (bish) {
+        grp[n] = tg & dm & below; desc[n++] = true;   // (-1, -1)
+        grp[n] = tg & am & below; desc[n++] = true;   // (-1, +1)
+        grp[n] = tg & am & above; desc[n++] = false;  // (+1, -1)
+        grp[n] = tg & dm & above; desc[n++] = false;  // (+1, +1)
+    }
+    for (int i = 0; i < n; i++) {
+        int c = popc(grp[i]);
+        if (k < c) return desc[i] ? kth_bit_desc(grp[i], k) : kth_bit_asc(grp[i], k);
+        k -= c;
+    }
+    return -1;
+}
+GC_HD int offset_pick(u64 tg, int sq, const signed char* offs, int k) {
+    for (int i = 0; i < 8; i++) {
+        int t = sq + offs[i];
+        if (t >= 0 && t < 64 && (tg >> t) & 1) {
+            if (k == 0) return t;
+            k--;
+        }
+    }
+    return -1;
+}
+GC_HD int kth_target(u64 tg, int sq, int t, bool white, int k) {
+    const signed char KO[8] = {8, -8, 1, -1, 9, 7, -7, -9};
+    const signed char NO[8] = {-17, -15, 15, 17, -10, -6, 6, 10};
+    const signed char PW[8] = {-8, -16, -7, -9, 99, 99, 99, 99};
+    const signed char PB[8] = {8, 16, 9, 7, 99, 99, 99, 99};
+    switch (t) {
+        case KING: return offset_pick(tg, sq, KO, k);
+        case KNIGHT: return offset_pick(tg, sq, NO, k);
+        case PAWN: return offset_pick(tg, sq, white ? PW : PB, k);
+        default: {
+            bool rook = (t == ROOK || t == QUEEN), bish = (t == BISHOP || t == QUEEN);
+            return ray_pick(tg, sq, file_mask(sq), row_mask(sq), diag_mask(sq), anti_mask(sq), rook, bish, k);
+        }
+    }
+}
+
+// ---- whole-position enumeration --------------------------------------------------------
+GC_HD int count_legal(const Pos& s, const Gen& g) {
+    int n = 0;
+    u64 pcs = g.own;
+    while (pcs) {
+        int sq = ctz(pcs);
+        pcs &= pcs - 1;
+        n += popc(legal_targets(s, g, sq, type_at(s, sq)));
+    }
+    return n + popc(g.castles);
+}
+
+// k-th legal action in reference order (normal moves row-major, castles QS then KS)
+GC_HD int select_legal(const Pos& s, const Gen& g, int k) {
+    u64 pcs = g.own;
+    while (pcs) {
+        int sq = ctz(pcs);
+        pcs &= pcs - 1;
+        int t = type_at(s, sq);
+        u64 tg = legal_targets(s, g, sq, t);
+        int c = popc(tg);
+        if (k < c) return sq * 64 + kth_target(tg, sq, t, g.white, k);
+        k -= c;
+    }
+    if (g.castles & 1) { if (k == 0) return g.white ? A_QSW : A_QSB; k--; }
+    if (g.castles & 2) { if (k == 0) return g.white ? A_KSW : A_KSB; }
+    return A_NONE;
+}
+
+// is `action` in the legal list? (chess_v2.py:240 `action not in self.possible_actions`)
+GC_HD bool action_legal(const Pos& s, const Gen& g, int action) {
+    if (action < 0 || action > A_RESIGN) return false;
+    if (action >= 4096) {
+        if (g.white) return (action == A_QSW && (g.castles & 1)) || (action == A_KSW && (g.castles & 2));
+        return (action == A_QSB && (g.castles & 1)) || (action == A_KSB && (g.castles & 2));
+    }
+    int f = action >> 6, t = action & 63;
+    if (!((g.own >> f) & 1)) return false;
+    return (legal_targets(s, g, f, type_at(s, f)) >> t) & 1;
+}
+
+// ---- transition: next_state (lib.rs:679-784) ------------------------------------------
+// `white_player` is the caller's player argument (it selects promotion colour and which
+// rights are revoked), not necessarily the piece's colour.  Returns 0 ok, -1 if the from
+// square is empty (the reference panics), -2 bad action.  *reward = captured value
+// (+10 on the dead promotion branch); *irrev = pawn move or capture (repetition window).
+GC_HD int apply_move(Pos& s, bool white_player, int action, int* reward, bool* irrev) {
+    const int VAL[7] = {0, 0, 10, 5, 3, 3, 1};
+    *reward = 0;
+    *irrev = false;
+    if (action < 4096) {
+        int f = action >> 6, t = action & 63;
+        int pid = id_at(s, f);
+        if (pid == 0) return -1;
+        int cid = id_at(s, t);
+        int pt = pid < 0 ? -pid : pid, ct = cid < 0 ? -cid : cid;
+        clear_sq(s, f);
+        clear_sq(s, t);
+        int nid = pid;
+        *reward = VAL[ct];
+        if (pt == PAWN && ((white_player && (t >> 3) == 7) || (!white_player && (t >> 3) == 0))) {
+            nid = white_player ? QUEEN : -QUEEN;  // QUEEN_ID * player (lib.rs:706)
+            *reward += 10;
+        }
+        put(s, t, nid);
+        *irrev = (pt == PAWN) || (cid != 0);
+        if (pid == KING) {  // positive id only (Q5)
+            s.meta &= white_player ? ~(u32)(M_WKC | M_WQC) : ~(u32)(M_BKC | M_BQC);
+        } else if (pid == ROOK) {
+            if ((f & 7) == 0) s.meta &= white_player ? ~(u32)M_WQC : ~(u32)M_BQC;
+            else if ((f & 7) == 7) s.meta &= white_player ? ~(u32)M_WKC : ~(u32)M_BKC;
+        }
+    } else {
+        switch (action) {  // lib.rs:740-773
+            case A_KSW:
+                clear_sq(s, 60); clear_sq(s, 61); clear_sq(s, 62); clear_sq(s, 63);
+                put(s, 61, ROOK); put(s, 62, KING);
+                s.meta &= ~(u32)(M_WKC | M_WQC);
+                break;
+            case A_QSW:
+                clear_sq(s, 56); clear_sq(s, 57); clear_sq(s, 58); clear_sq(s, 59); clear_sq(s, 60);
+                put(s, 58, KING); put(s, 59, ROOK);
+                s.meta &= ~(u32)(M_WKC | M_WQC);
+                break;
+            case A_KSB:
+                clear_sq(s, 4); clear_sq(s, 5); clear_sq(s, 6); clear_sq(s, 7);
+                put(s, 5, -ROOK); put(s, 6, -KING);
+                s.meta &= ~(u32)(M_BKC | M_BQC);
+                break;
+            case A_QSB:
+                clear_sq(s, 0); clear_sq(s, 1); clear_sq(s, 2); clear_sq(s, 3); clear_sq(s, 4);
+                put(s, 2, -KING); put(s, 3, -ROOK);
+                s.meta &= ~(u32)(M_BKC | M_BQC);
+                break;
+            default: return -2;
+        }
+    }
+    // current_player = other (lib.rs:778-780)
+    s.meta = white_player ? (s.meta & ~(u32)M_WHITE) : (s.meta | M_WHITE);
+    return 0;
+}
+
+// ---- board-only key for 3-fold repetition (chess_v2.py:599-602) -------------------------
+// A filter only: every hash hit is confirmed against the stored board, so collisions
+// cannot change results.
+GC_HD u64 mix64(u64 x) {
+    x ^= x >> 31; x *= 0x7FB5D329728EA185ull;
+    x ^= x >> 27; x *= 0x81DADEF4BC2DD44Dull;
+    x ^= x >> 33;
+    return x;
+}
+GC_HD u32 board_key(const Pos& s) {
+    u64 h = mix64(s.k ^ 0x9E3779B97F4A7C15ull) ^ mix64(s.q + 0x632BE59BD9B4E019ull) ^
+            mix64(s.r ^ 0x85157AF5ull) ^ mix64(s.b + 0xD6E8FEB86659FD93ull) ^
+            mix64(s.n ^ 0xA0761D6478BD642Full) ^ mix64(s.p + 0xE7037ED1A0B428DBull) ^ mix64(s.w ^ 0x8EBC6AF09C88C6E3ull);
+    return (u32)(h ^ (h >> 32));
+}
+
+// ---- mailbox <-> bitboards ------------------------------------------------------------
+GC_HD Pos from_mailbox(const int8_t* b, u32 meta) {
+    Pos s = {0, 0, 0, 0, 0, 0, 0, meta};
+    for (int i = 0; i < 64; i++) put(s, i, b[i]);
+    return s;
+}
+GC_HD void to_mailbox(const Pos& s, int8_t* b) {
+    for (int i = 0; i < 64; i++) b[i] = (int8_t)id_at(s, i);
+}
+
+// ---- Philox4x32-10 random policy (same stream as the test oracle's policy draw) -----------
+GC_HD u32 policy_index(u64 seed, u32 board, u32 draw, u32 n) {
+    u32 k0 = (u32)seed, k1 = (u32)(seed >> 32);
+    u32 x0 = board, x1 = draw, x2 = 0x5EEDu, x3 = 0u;
+    for (int i = 0; i < 10; i++) {
+        u64 p0 = (u64)0xD2511F53u * x0;
+        u64 p1 = (u64)0xCD9E8D57u * x2;
+        u32 y0 = (u32)(p1 >> 32) ^ x1 ^ k0;
+        u32 y1 = (u32)p1;
+        u32 y2 = (u32)(p0 >> 32) ^ x3 ^ k1;
+        u32 y3 = (u32)p0;
+        x0 = y0; x1 = y1; x2 = y2; x3 = y3;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    return (u32)(((u64)x0 * n) >> 32);
+}
+
+}  // namespace gc

@@ -1,0 +1,989 @@
+// gymchess.hip -- HIP kernels (gfx950) + the extern "C" boundary (include/gymchess.h).
+//
+// One lane = one board.  Board state lives in HBM as structure-of-arrays: bitboard j of
+// board i at bb[j*N + i] (j = K,Q,R,B,N,P,W), meta[i], so every wave's loads and stores
+// of one field are 512 contiguous bytes.  All move generation is register-resident
+// integer/bitwise work (gc_core.h); the only other HBM traffic is the 3-fold repetition
+// window hkey[slot*N + i] (u32) + hboard[(slot*7 + j)*N + i] (read only on key hits).
+//
+// The C-ABI replaces the reference's FFI (the PyO3 ChessEngine, lib.rs:1412-1512) for the
+// engine calls, plus a device-resident batched env for chess_v2.py's reset()/step().
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "gc_core.h"
+#include "gc_env.h"
+#include "../../include/gymchess.h"
+
+using namespace gc;
+
+#define NBB 7
+#define BLOCK 256
+
+// ----------------------------------------------------------------------------- errors
+static thread_local std::string g_err;
+static int fail(const std::string& m) {
+    g_err = m;
+    return -1;
+}
+#define HIPCHK(x)                                                                   \
+    do {                                                                            \
+        hipError_t e_ = (x);                                                        \
+        if (e_ != hipSuccess) return fail(std::string(#x) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+extern "C" const char* gc_last_error(void) { return g_err.c_str(); }
+extern "C" int gc_version(void) { return GC_ABI_VERSION; }
+extern "C" int gc_get_device_count(int* n) {
+    if (!n) return fail("null out pointer");
+    HIPCHK(hipGetDeviceCount(n));
+    return 0;
+}
+
+// ----------------------------------------------------------------------------- SoA access
+struct SoA {
+    u64* bb;   // [7][N]
+    u32* meta; // [N]
+    int n;
+    __device__ Pos load(int i) const {
+        Pos s;
+        s.k = bb[0 * (size_t)n + i]; s.q = bb[1 * (size_t)n + i]; s.r = bb[2 * (size_t)n + i];
+        s.b = bb[3 * (size_t)n + i]; s.n = bb[4 * (size_t)n + i]; s.p = bb[5 * (size_t)n + i];
+        s.w = bb[6 * (size_t)n + i];
+        s.meta = meta[i];
+        return s;
+    }
+    __device__ void store(int i, const Pos& s) const {
+        bb[0 * (size_t)n + i] = s.k; bb[1 * (size_t)n + i] = s.q; bb[2 * (size_t)n + i] = s.r;
+        bb[3 * (size_t)n + i] = s.b; bb[4 * (size_t)n + i] = s.n; bb[5 * (size_t)n + i] = s.p;
+        bb[6 * (size_t)n + i] = s.w;
+        meta[i] = s.meta;
+    }
+};
+
+struct DevHist {  // repetition window of board i
+    u32* hkey;
+    u64* hboard;
+    int n, i;
+    __device__ u32 key(int slot) const { return hkey[(size_t)slot * n + i]; }
+    __device__ bool same(int slot, const Pos& s) const {
+        const u64* h = hboard + (size_t)slot * NBB * n + i;
+        return h[0] == s.k && h[(size_t)n] == s.q && h[2 * (size_t)n] == s.r && h[3 * (size_t)n] == s.b &&
+               h[4 * (size_t)n] == s.n && h[5 * (size_t)n] == s.p && h[6 * (size_t)n] == s.w;
+    }
+    __device__ void put(int slot, u32 k, const Pos& s) const {
+        hkey[(size_t)slot * n + i] = k;
+        u64* h = hboard + (size_t)slot * NBB * n + i;
+        h[0] = s.k; h[(size_t)n] = s.q; h[2 * (size_t)n] = s.r; h[3 * (size_t)n] = s.b;
+        h[4 * (size_t)n] = s.n; h[5 * (size_t)n] = s.p; h[6 * (size_t)n] = s.w;
+    }
+};
+
+// ----------------------------------------------------------------------------- engine kernels
+// import: mailbox int8[64] + meta8 {side, wkc, wqc, bkc, bqc, ...} -> bitboards, with the
+// State::new rights forcing (lib.rs:295-336).  `side` may override meta8[0] (player arg).
+__global__ void k_import(const int8_t* __restrict__ boards, const uint8_t* __restrict__ meta8,
+                         const uint8_t* __restrict__ side, SoA out) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= out.n) return;
+    const uint8_t* m = meta8 + 8 * (size_t)i;
+    bool white = side ? side[i] != 0 : m[0] != 0;
+    u32 meta = (white ? M_WHITE : 0u) | (m[1] ? M_WKC : 0u) | (m[2] ? M_WQC : 0u) | (m[3] ? M_BKC : 0u) |
+               (m[4] ? M_BQC : 0u) | (m[5] ? M_WCHK : 0u) | (m[6] ? M_BCHK : 0u) | ((u32)m[7] << M_MC_SHIFT);
+    Pos s = from_mailbox(boards + 64 * (size_t)i, meta);
+    s.meta = (s.meta & ~(u32)M_RIGHTS) | eff_rights(s);
+    out.store(i, s);
+}
+
+__global__ void k_export(SoA in, int8_t* __restrict__ boards, uint8_t* __restrict__ meta8) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= in.n) return;
+    Pos s = in.load(i);
+    if (boards) to_mailbox(s, boards + 64 * (size_t)i);
+    if (meta8) {
+        uint8_t* m = meta8 + 8 * (size_t)i;
+        m[0] = (s.meta & M_WHITE) != 0; m[1] = (s.meta & M_WKC) != 0; m[2] = (s.meta & M_WQC) != 0;
+        m[3] = (s.meta & M_BKC) != 0; m[4] = (s.meta & M_BQC) != 0; m[5] = (s.meta & M_WCHK) != 0;
+        m[6] = (s.meta & M_BCHK) != 0; m[7] = (uint8_t)mc_of(s.meta);
+    }
+}
+
+// ordered move list in reference order (lib.rs:460-563 + 1468-1479); attack mode lists the
+// unfiltered attack-mode moves and no castles.  count may exceed cap (list truncated).
+__global__ void k_list(SoA in, int attack, int cap, uint16_t* __restrict__ out, int32_t* __restrict__ counts) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= in.n) return;
+    Pos s = in.load(i);
+    Gen g;
+    gen_init(s, g);
+    uint16_t* o = out + (size_t)cap * i;
+    int n = 0;
+    u64 pcs = g.own;
+    while (pcs) {
+        int sq = ctz(pcs);
+        pcs &= pcs - 1;
+        int t = type_at(s, sq);
+        u64 tg = attack ? attack_targets(s, g, sq, t) : legal_targets(s, g, sq, t);
+        int c = popc(tg);
+        for (int k = 0; k < c; k++) {
+            if (n < cap) o[n] = (uint16_t)(sq * 64 + kth_target(tg, sq, t, g.white, k));
+            n++;
+        }
+    }
+    if (!attack) {
+        if (g.castles & 1) { if (n < cap) o[n] = g.white ? A_QSW : A_QSB; n++; }
+        if (g.castles & 2) { if (n < cap) o[n] = g.white ? A_KSW : A_KSB; n++; }
+    }
+    counts[i] = n;
+}
+
+// legal action mask: 64 words (from-square -> target bitboard) + 1 word of castle bits
+// (bit c set <=> action 4096+c legal)
+__global__ void k_mask(SoA in, u64* __restrict__ mask, int32_t* __restrict__ counts) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= in.n) return;
+    Pos s = in.load(i);
+    Gen g;
+    gen_init(s, g);
+    u64* o = mask + 65 * (size_t)i;
+    int n = 0;
+    for (int sq = 0; sq < 64; sq++) {
+        u64 tg = ((g.own >> sq) & 1) ? legal_targets(s, g, sq, type_at(s, sq)) : 0;
+        o[sq] = tg;
+        n += popc(tg);
+    }
+    u64 c = 0;
+    if (g.castles & 1) c |= g.white ? (1ull << 1) : (1ull << 3);
+    if (g.castles & 2) c |= g.white ? (1ull << 0) : (1ull << 2);
+    o[64] = c;
+    if (counts) counts[i] = n + popc(c);
+}
+
+// next_state (lib.rs:1422-1452): move + update_state; status 0 ok, 1 both kings checked,
+// -1 empty from-square (reference panics), -2 bad action
+__global__ void k_next_state(SoA in, const uint8_t* __restrict__ player_white, const uint16_t* __restrict__ actions,
+                             SoA out, int32_t* __restrict__ rewards, int32_t* __restrict__ status) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= in.n) return;
+    Pos s = in.load(i);
+    int rw = 0;
+    bool irrev;
+    int rc = apply_move(s, player_white[i] != 0, actions[i], &rw, &irrev);
+    if (rc == 0) {
+        u32 chk = check_flags(s);
+        s.meta = (s.meta & ~(u32)(M_WCHK | M_BCHK)) | chk;
+        if ((chk & (M_WCHK | M_BCHK)) == (M_WCHK | M_BCHK)) rc = 1;
+    }
+    out.store(i, s);
+    rewards[i] = rw;
+    status[i] = rc;
+}
+
+// update_state (lib.rs:1502-1511)
+__global__ void k_update_state(SoA st) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= st.n) return;
+    Pos s = st.load(i);
+    s.meta = (s.meta & ~(u32)(M_WCHK | M_BCHK)) | check_flags(s);
+    st.store(i, s);
+}
+
+// ----------------------------------------------------------------------------- perft
+// perft(s, d) = sum over get_all_possible_moves of perft(next_state, d-1), perft(s,1) = #moves
+// (SURVEY §3.4).  Per-lane iterative DFS; bulk count at depth 1.
+#define PERFT_MAXD 8
+struct Frame {
+    Pos s;
+    Gen g;
+    u64 pcs;   // own pieces not yet expanded
+    u64 tg;    // remaining targets of the current piece
+    int sq;    // current piece square
+    u32 cast;  // remaining castle bits
+};
+
+__device__ Pos child_of(const Pos& s, bool white, int action) {
+    Pos c = s;
+    int rw;
+    bool irrev;
+    apply_move(c, white, action, &rw, &irrev);
+    // each engine call re-reads the dict: State::new forces rights by king presence
+    c.meta = (c.meta & ~(u32)M_RIGHTS) | eff_rights(c);
+    return c;
+}
+
+__device__ uint64_t perft_lane(const Pos& root, int depth) {
+    if (depth <= 0) return 1;
+    Frame st[PERFT_MAXD];
+    uint64_t nodes = 0;
+    int top = 0;
+    st[0].s = root;
+    gen_init(st[0].s, st[0].g);
+    if (depth == 1) return (uint64_t)count_legal(st[0].s, st[0].g);
+    st[0].pcs = st[0].g.own;
+    st[0].tg = 0;
+    st[0].sq = -1;
+    st[0].cast = st[0].g.castles;
+    while (top >= 0) {
+        Frame& f = st[top];
+        int action = -1;
+        if (f.tg) {
+            int t = ctz(f.tg);
+            f.tg &= f.tg - 1;
+            action = f.sq * 64 + t;
+        } else if (f.pcs) {
+            f.sq = ctz(f.pcs);
+            f.pcs &= f.pcs - 1;
+            f.tg = legal_targets(f.s, f.g, f.sq, type_at(f.s, f.sq));
+            continue;
+        } else if (f.cast) {
+            int c = ctz((u64)f.cast);
+            f.cast &= f.cast - 1;
+            action = c == 0 ? (f.g.white ? A_QSW : A_QSB) : (f.g.white ? A_KSW : A_KSB);
+        } else {
+            top--;
+            continue;
+        }
+        Pos c = child_of(f.s, f.g.white, action);
+        int remaining = depth - 1 - top;  // depth of the child subtree
+        if (remaining == 1) {
+            Gen g;
+            gen_init(c, g);
+            nodes += (uint64_t)count_legal(c, g);
+        } else {
+            Frame& nf = st[top + 1];
+            nf.s = c;
+            gen_init(nf.s, nf.g);
+            nf.pcs = nf.g.own;
+            nf.tg = 0;
+            nf.sq = -1;
+            nf.cast = nf.g.castles;
+            top++;
+        }
+    }
+    return nodes;
+}
+
+__global__ void k_perft(SoA in, int depth, uint64_t* __restrict__ nodes) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= in.n) return;
+    nodes[i] = perft_lane(in.load(i), depth);
+}
+
+// split: children of every root, written at offs[i] .. offs[i]+cnt[i] (offs = exclusive scan)
+__global__ void k_count_children(SoA in, int32_t* __restrict__ cnt) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= in.n) return;
+    Pos s = in.load(i);
+    Gen g;
+    gen_init(s, g);
+    cnt[i] = count_legal(s, g);
+}
+__global__ void k_expand(SoA in, const int32_t* __restrict__ offs, SoA out, int32_t* __restrict__ parent) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= in.n) return;
+    Pos s = in.load(i);
+    Gen g;
+    gen_init(s, g);
+    int o = offs[i];
+    u64 pcs = g.own;
+    while (pcs) {
+        int sq = ctz(pcs);
+        pcs &= pcs - 1;
+        u64 tg = legal_targets(s, g, sq, type_at(s, sq));
+        while (tg) {
+            int t = ctz(tg);
+            tg &= tg - 1;
+            out.store(o, child_of(s, g.white, sq * 64 + t));
+            parent[o++] = i;
+        }
+    }
+    if (g.castles & 1) { out.store(o, child_of(s, g.white, g.white ? A_QSW : A_QSB)); parent[o++] = i; }
+    if (g.castles & 2) { out.store(o, child_of(s, g.white, g.white ? A_KSW : A_KSB)); parent[o++] = i; }
+}
+// per-task perft + deterministic per-root sum (tasks of one root are contiguous)
+__global__ void k_perft_tasks(SoA tasks, int depth, uint64_t* __restrict__ nodes) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= tasks.n) return;
+    nodes[i] = perft_lane(tasks.load(i), depth);
+}
+__global__ void k_sum_tasks(const int32_t* __restrict__ offs, const int32_t* __restrict__ cnt,
+                            const uint64_t* __restrict__ tnodes, int n, uint64_t* __restrict__ out) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint64_t s = 0;
+    for (int k = 0; k < cnt[i]; k++) s += tnodes[offs[i] + k];
+    out[i] = s;
+}
+
+// ----------------------------------------------------------------------------- env kernels
+struct EnvDev {
+    SoA st;
+    u32* hkey;
+    u64* hboard;
+    u32* draw;       // policy draws per board (Philox counter)
+    uint16_t* act;   // next action per board (A_NONE = no legal move)
+    int32_t* reward;
+    uint8_t* done;
+    uint8_t* reason;
+    u32* nsteps;     // env.step() calls that applied the step logic, per board
+    const u64* init; // 7 bitboards of the initial board
+    uint64_t seed;
+    int n;
+};
+
+__device__ Pos init_pos(const u64* init) {
+    Pos s = {init[0], init[1], init[2], init[3], init[4], init[5], init[6], 0};
+    return env_reset_pos(s);
+}
+
+// policy: uniform choice among the reference-ordered legal list (test_benchmark.py:22-27)
+__device__ uint16_t pick(const Pos& s, const Gen& g, int n, uint64_t seed, int i, u32& draw) {
+    if (n == 0) return (uint16_t)A_NONE;
+    u32 k = policy_index(seed, (u32)i, draw++, (u32)n);
+    return (uint16_t)select_legal(s, g, (int)k);
+}
+
+__global__ void k_env_reset(EnvDev e, const uint8_t* __restrict__ mask, int select) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= e.n) return;
+    if (mask && !mask[i]) return;
+    Pos s = init_pos(e.init);
+    e.st.store(i, s);
+    if (select) {
+        Gen g;
+        gen_init(s, g);
+        u32 d = e.draw[i];
+        e.act[i] = pick(s, g, count_legal(s, g), e.seed, i, d);
+        e.draw[i] = d;
+    }
+}
+
+// One env ply per board.
+//  POLICY=false: external action e.act[i], validated like chess_v2.py:240; no auto-reset.
+//  POLICY=true : the random-self-play driver of test_benchmark.py -- act[i] was picked by
+//                the policy from this state; A_NONE (empty move list) -> driver reset
+//                without a step; done -> reset; then pick the next action.
+template <bool POLICY>
+__global__ void __launch_bounds__(BLOCK) k_env_step(EnvDev e) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= e.n) return;
+    Pos s = e.st.load(i);
+    DevHist h{e.hkey, e.hboard, e.n, i};
+    int a = e.act[i];
+    StepOut o = {0, 0, R_NONE, 0};
+    Gen g;
+    bool have_gen = false;
+    if (POLICY && a == A_NONE) {
+        s = init_pos(e.init);
+        o.reason = R_NO_MOVES;
+    } else {
+        if (POLICY) {
+            o = env_step<false>(s, h, a, nullptr);
+        } else {
+            Gen g0;
+            gen_init(s, g0);
+            o = env_step<true>(s, h, a, &g0);
+        }
+        if (o.moved) {
+            gen_init(s, g);
+            have_gen = true;
+            env_finish(s, o, count_legal(s, g));
+        }
+        e.nsteps[i] += 1;
+        if (POLICY && o.done) {
+            s = init_pos(e.init);
+            have_gen = false;
+        }
+    }
+    if (POLICY) {
+        if (!have_gen) gen_init(s, g);
+        u32 d = e.draw[i];
+        e.act[i] = pick(s, g, count_legal(s, g), e.seed, i, d);
+        e.draw[i] = d;
+    }
+    e.st.store(i, s);
+    e.reward[i] = o.reward;
+    e.done[i] = (uint8_t)o.done;
+    e.reason[i] = (uint8_t)o.reason;
+}
+
+// Fused K-ply random self-play: state in registers for the whole launch.  Optional per-ply
+// trace [ply][N] (tests).  stats per board: [steps, reward_sum(two's complement), ends[1..5]]
+__global__ void __launch_bounds__(BLOCK) k_env_rollout(EnvDev e, int plies, int16_t* tr_action, int16_t* tr_reward,
+                                                       uint8_t* tr_done, uint8_t* tr_reason, uint64_t* stats) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= e.n) return;
+    Pos s = e.st.load(i);
+    DevHist h{e.hkey, e.hboard, e.n, i};
+    u32 d = e.draw[i];
+    int a = e.act[i];
+    uint64_t steps = 0, rsum = 0, ends[6] = {0, 0, 0, 0, 0, 0};
+    for (int p = 0; p < plies; p++) {
+        StepOut o = {0, 0, R_NONE, 0};
+        Gen g;
+        bool have_gen = false;
+        int played = a;
+        if (a == A_NONE) {
+            s = init_pos(e.init);
+            o.reason = R_NO_MOVES;
+            ends[R_NO_MOVES]++;
+            played = -1;
+        } else {
+            o = env_step<false>(s, h, a, nullptr);
+            if (o.moved) {
+                gen_init(s, g);
+                have_gen = true;
+                env_finish(s, o, count_legal(s, g));
+            }
+            steps++;
+            rsum += (uint64_t)(int64_t)o.reward;
+            if (o.done) {
+                ends[o.reason < 6 ? o.reason : 0]++;
+                s = init_pos(e.init);
+                have_gen = false;
+            }
+        }
+        if (!have_gen) gen_init(s, g);
+        if (tr_action) {
+            size_t t = (size_t)p * e.n + i;
+            tr_action[t] = (int16_t)played;
+            tr_reward[t] = (int16_t)o.reward;
+            tr_done[t] = (uint8_t)o.done;
+            tr_reason[t] = (uint8_t)o.reason;
+        }
+        a = pick(s, g, count_legal(s, g), e.seed, i, d);
+    }
+    e.st.store(i, s);
+    e.draw[i] = d;
+    e.act[i] = (uint16_t)a;
+    e.nsteps[i] += (u32)steps;
+    if (stats) {
+        uint64_t* o = stats + 8 * (size_t)i;
+        o[0] += steps; o[1] += rsum;
+        for (int k = 0; k < 6; k++) o[2 + k] += ends[k];
+    }
+}
+
+// ----------------------------------------------------------------------------- host side
+static inline int grid_for(int n) { return (n + BLOCK - 1) / BLOCK; }
+
+template <class T>
+static int dalloc(T** p, size_t count) {
+    if (count == 0) count = 1;
+    hipError_t e = hipMalloc((void**)p, count * sizeof(T));
+    if (e != hipSuccess) return fail(std::string("hipMalloc: ") + hipGetErrorString(e));
+    return 0;
+}
+
+struct gc_engine {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int cap_n = 0, cap_list = 0;
+    u64* bb = nullptr; u32* meta = nullptr;       // input states
+    u64* bb2 = nullptr; u32* meta2 = nullptr;     // output states
+    int8_t* mbox = nullptr; uint8_t* m8 = nullptr; uint8_t* side = nullptr;
+    uint16_t* acts = nullptr; int32_t* i32a = nullptr; int32_t* i32b = nullptr;
+    uint16_t* list = nullptr; uint64_t* u64o = nullptr;
+};
+
+static void engine_free_bufs(gc_engine* e) {
+    void* ps[] = {e->bb, e->meta, e->bb2, e->meta2, e->mbox, e->m8, e->side, e->acts, e->i32a, e->i32b, e->list, e->u64o};
+    for (void* p : ps) if (p) (void)hipFree(p);
+    e->bb = nullptr; e->meta = nullptr; e->bb2 = nullptr; e->meta2 = nullptr; e->mbox = nullptr; e->m8 = nullptr;
+    e->side = nullptr; e->acts = nullptr; e->i32a = nullptr; e->i32b = nullptr; e->list = nullptr; e->u64o = nullptr;
+    e->cap_n = 0; e->cap_list = 0;
+}
+
+static int engine_reserve(gc_engine* e, int n, int listcap) {
+    if (n <= e->cap_n && listcap <= e->cap_list) return 0;
+    int nn = n > e->cap_n ? n : e->cap_n, lc = listcap > e->cap_list ? listcap : e->cap_list;
+    engine_free_bufs(e);
+    if (dalloc(&e->bb, (size_t)NBB * nn) || dalloc(&e->meta, nn) || dalloc(&e->bb2, (size_t)NBB * nn) ||
+        dalloc(&e->meta2, nn) || dalloc(&e->mbox, (size_t)64 * nn) || dalloc(&e->m8, (size_t)8 * nn) ||
+        dalloc(&e->side, nn) || dalloc(&e->acts, nn) || dalloc(&e->i32a, nn) || dalloc(&e->i32b, nn) ||
+        dalloc(&e->list, (size_t)lc * nn) || dalloc(&e->u64o, nn))
+        return -1;
+    e->cap_n = nn;
+    e->cap_list = lc;
+    return 0;
+}
+
+static int check_boards(int n, const int8_t* boards) {
+    for (size_t k = 0; k < (size_t)64 * n; k++)
+        if (boards[k] < -6 || boards[k] > 6) return fail("piece id out of range [-6, 6] at index " + std::to_string(k));
+    return 0;
+}
+
+static int engine_upload(gc_engine* e, int n, const int8_t* boards, const uint8_t* meta, const uint8_t* side) {
+    if (n <= 0) return fail("n must be > 0");
+    if (!boards || !meta) return fail("null boards/meta");
+    if (check_boards(n, boards)) return -1;
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipMemcpyAsync(e->mbox, boards, (size_t)64 * n, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(hipMemcpyAsync(e->m8, meta, (size_t)8 * n, hipMemcpyHostToDevice, e->stream));
+    if (side) HIPCHK(hipMemcpyAsync(e->side, side, n, hipMemcpyHostToDevice, e->stream));
+    SoA st{e->bb, e->meta, n};
+    k_import<<<grid_for(n), BLOCK, 0, e->stream>>>(e->mbox, e->m8, side ? e->side : nullptr, st);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+extern "C" int gc_engine_create(int device, gc_engine** out) {
+    if (!out) return fail("null out pointer");
+    int nd = 0;
+    HIPCHK(hipGetDeviceCount(&nd));
+    if (device < 0 || device >= nd) return fail("device index out of range");
+    gc_engine* e = new gc_engine();
+    e->device = device;
+    HIPCHK(hipSetDevice(device));
+    HIPCHK(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+    if (engine_reserve(e, 256, 256)) { delete e; return -1; }
+    *out = e;
+    return 0;
+}
+
+extern "C" int gc_engine_destroy(gc_engine* e) {
+    if (!e) return 0;
+    (void)hipSetDevice(e->device);
+    (void)hipStreamSynchronize(e->stream);
+    engine_free_bufs(e);
+    (void)hipStreamDestroy(e->stream);
+    delete e;
+    return 0;
+}
+
+extern "C" int gc_engine_get_possible_moves(gc_engine* e, int n, const int8_t* boards, const uint8_t* meta,
+                                            const uint8_t* player_white, int attack, uint16_t* moves, int cap,
+                                            int32_t* counts) {
+    if (!e || !moves || !counts || !player_white) return fail("null argument");
+    if (cap <= 0) return fail("cap must be > 0");
+    if (engine_reserve(e, n, cap)) return -1;
+    if (engine_upload(e, n, boards, meta, player_white)) return -1;
+    k_list<<<grid_for(n), BLOCK, 0, e->stream>>>(SoA{e->bb, e->meta, n}, attack ? 1 : 0, cap, e->list, e->i32a);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(moves, e->list, (size_t)2 * cap * n, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(counts, e->i32a, (size_t)4 * n, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return 0;
+}
+
+extern "C" int gc_engine_get_castle_moves(gc_engine* e, int n, const int8_t* boards, const uint8_t* meta,
+                                          const uint8_t* player_white, uint16_t* moves, int32_t* counts) {
+    if (!e || !moves || !counts || !player_white) return fail("null argument");
+    if (engine_reserve(e, n, 2)) return -1;
+    if (engine_upload(e, n, boards, meta, player_white)) return -1;
+    std::vector<u64> mask((size_t)65 * n);
+    u64* dmask = nullptr;
+    if (dalloc(&dmask, (size_t)65 * n)) return -1;
+    k_mask<<<grid_for(n), BLOCK, 0, e->stream>>>(SoA{e->bb, e->meta, n}, dmask, nullptr);
+    hipError_t le = hipGetLastError();
+    hipError_t ce = hipMemcpyAsync(mask.data(), dmask, (size_t)8 * 65 * n, hipMemcpyDeviceToHost, e->stream);
+    hipError_t se = hipStreamSynchronize(e->stream);
+    (void)hipFree(dmask);
+    if (le != hipSuccess || ce != hipSuccess || se != hipSuccess) return fail("castle mask kernel failed");
+    for (int i = 0; i < n; i++) {  // unpack in reference order (QS then KS, lib.rs:992,1011)
+        u64 c = mask[(size_t)65 * i + 64];
+        int k = 0;
+        uint16_t* o = moves + 2 * (size_t)i;
+        if (c & (1ull << 1)) o[k++] = A_QSW;
+        if (c & (1ull << 0)) o[k++] = A_KSW;
+        if (c & (1ull << 3)) o[k++] = A_QSB;
+        if (c & (1ull << 2)) o[k++] = A_KSB;
+        counts[i] = k;
+    }
+    return 0;
+}
+
+extern "C" int gc_engine_next_state(gc_engine* e, int n, const int8_t* boards, const uint8_t* meta,
+                                    const uint8_t* player_white, const uint16_t* actions, int8_t* out_boards,
+                                    uint8_t* out_meta, int32_t* rewards, int32_t* status) {
+    if (!e || !player_white || !actions || !out_boards || !out_meta || !rewards || !status) return fail("null argument");
+    for (int i = 0; i < n; i++)
+        if (actions[i] > A_QSB) return fail("action out of range at index " + std::to_string(i));
+    if (engine_reserve(e, n, 1)) return -1;
+    if (engine_upload(e, n, boards, meta, nullptr)) return -1;
+    HIPCHK(hipMemcpyAsync(e->side, player_white, n, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(hipMemcpyAsync(e->acts, actions, (size_t)2 * n, hipMemcpyHostToDevice, e->stream));
+    SoA in{e->bb, e->meta, n}, out{e->bb2, e->meta2, n};
+    k_next_state<<<grid_for(n), BLOCK, 0, e->stream>>>(in, e->side, e->acts, out, e->i32a, e->i32b);
+    HIPCHK(hipGetLastError());
+    k_export<<<grid_for(n), BLOCK, 0, e->stream>>>(out, e->mbox, e->m8);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(out_boards, e->mbox, (size_t)64 * n, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(out_meta, e->m8, (size_t)8 * n, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(rewards, e->i32a, (size_t)4 * n, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(status, e->i32b, (size_t)4 * n, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return 0;
+}
+
+extern "C" int gc_engine_update_state(gc_engine* e, int n, const int8_t* boards, const uint8_t* meta,
+                                      int8_t* out_boards, uint8_t* out_meta) {
+    if (!e || !out_boards || !out_meta) return fail("null argument");
+    if (engine_reserve(e, n, 1)) return -1;
+    if (engine_upload(e, n, boards, meta, nullptr)) return -1;
+    SoA st{e->bb, e->meta, n};
+    k_update_state<<<grid_for(n), BLOCK, 0, e->stream>>>(st);
+    HIPCHK(hipGetLastError());
+    k_export<<<grid_for(n), BLOCK, 0, e->stream>>>(st, e->mbox, e->m8);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(out_boards, e->mbox, (size_t)64 * n, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(out_meta, e->m8, (size_t)8 * n, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return 0;
+}
+
+// perft over n roots.  split_depth > 0 expands every root into its children first (one
+// lane per child subtree) so that few roots still fill the chip.
+extern "C" int gc_engine_perft(gc_engine* e, int n, const int8_t* boards, const uint8_t* meta, int depth,
+                               uint64_t* nodes) {
+    if (!e || !nodes) return fail("null argument");
+    if (depth < 0 || depth > PERFT_MAXD) return fail("depth must be in [0, 8]");
+    if (engine_reserve(e, n, 1)) return -1;
+    if (engine_upload(e, n, boards, meta, nullptr)) return -1;
+    SoA roots{e->bb, e->meta, n};
+    if (depth <= 2) {
+        k_perft<<<grid_for(n), BLOCK, 0, e->stream>>>(roots, depth, e->u64o);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(nodes, e->u64o, (size_t)8 * n, hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream));
+        return 0;
+    }
+    // split at depth 1: tasks = children of every root
+    int32_t *cnt = e->i32a, *offs = e->i32b;
+    k_count_children<<<grid_for(n), BLOCK, 0, e->stream>>>(roots, cnt);
+    HIPCHK(hipGetLastError());
+    size_t tmp_bytes = 0;
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, cnt, offs, n, e->stream));
+    void* tmp = nullptr;
+    if (dalloc((char**)&tmp, tmp_bytes)) return -1;
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, cnt, offs, n, e->stream));
+    int32_t last_off = 0, last_cnt = 0;
+    HIPCHK(hipMemcpyAsync(&last_off, offs + n - 1, 4, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(&last_cnt, cnt + n - 1, 4, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    (void)hipFree(tmp);
+    int nt = last_off + last_cnt;
+    if (nt == 0) {
+        for (int i = 0; i < n; i++) nodes[i] = 0;
+        return 0;
+    }
+    u64* tbb = nullptr; u32* tmeta = nullptr; int32_t* parent = nullptr; uint64_t* tnodes = nullptr;
+    if (dalloc(&tbb, (size_t)NBB * nt) || dalloc(&tmeta, nt) || dalloc(&parent, nt) || dalloc(&tnodes, nt)) return -1;
+    SoA tasks{tbb, tmeta, nt};
+    k_expand<<<grid_for(n), BLOCK, 0, e->stream>>>(roots, offs, tasks, parent);
+    k_perft_tasks<<<grid_for(nt), BLOCK, 0, e->stream>>>(tasks, depth - 1, tnodes);
+    k_sum_tasks<<<grid_for(n), BLOCK, 0, e->stream>>>(offs, cnt, tnodes, n, e->u64o);
+    hipError_t le = hipGetLastError();
+    hipError_t ce = hipMemcpyAsync(nodes, e->u64o, (size_t)8 * n, hipMemcpyDeviceToHost, e->stream);
+    hipError_t se = hipStreamSynchronize(e->stream);
+    (void)hipFree(tbb); (void)hipFree(tmeta); (void)hipFree(parent); (void)hipFree(tnodes);
+    if (le != hipSuccess || ce != hipSuccess || se != hipSuccess)
+        return fail(std::string("perft kernels failed: ") + hipGetErrorString(le != hipSuccess ? le : (ce != hipSuccess ? ce : se)));
+    return 0;
+}
+
+// ----------------------------------------------------------------------------- env API
+struct gc_env {
+    int device = 0, n = 0;
+    uint64_t seed = 0;
+    hipStream_t stream = nullptr;
+    EnvDev d{};
+    u64* bb = nullptr; u32* meta = nullptr; u64* init = nullptr;
+    int8_t* mbox = nullptr; uint8_t* m8 = nullptr; uint8_t* mask = nullptr;
+    uint16_t* list = nullptr; int list_cap = 0; int32_t* counts = nullptr; u64* lmask = nullptr;
+    uint64_t* stats = nullptr;
+    hipEvent_t ev[8] = {};
+    bool policy_ready = false;  // act[] holds policy picks for the current states
+};
+
+static void env_free(gc_env* e) {
+    void* ps[] = {e->bb, e->meta, e->init, e->d.hkey, e->d.hboard, e->d.draw, e->d.act, e->d.reward, e->d.done,
+                  e->d.reason, e->d.nsteps, e->mbox, e->m8, e->mask, e->list, e->counts, e->lmask, e->stats};
+    for (void* p : ps) if (p) (void)hipFree(p);
+    for (auto& v : e->ev) if (v) (void)hipEventDestroy(v);
+    if (e->stream) (void)hipStreamDestroy(e->stream);
+}
+
+extern "C" int gc_env_create(int device, int n_boards, uint64_t seed, const int8_t* initial_board, gc_env** out) {
+    if (!out) return fail("null out pointer");
+    if (n_boards <= 0) return fail("n_boards must be > 0");
+    int nd = 0;
+    HIPCHK(hipGetDeviceCount(&nd));
+    if (device < 0 || device >= nd) return fail("device index out of range");
+    static const int8_t DEF[64] = {-3, -5, -4, -2, -1, -4, -5, -3, -6, -6, -6, -6, -6, -6, -6, -6,
+                                   0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,
+                                   0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,
+                                   6,  6,  6,  6,  6,  6,  6,  6,  3,  5,  4,  2,  1,  4,  5,  3};
+    const int8_t* ib = initial_board ? initial_board : DEF;
+    if (check_boards(1, ib)) return -1;
+    gc_env* e = new gc_env();
+    e->device = device;
+    e->n = n_boards;
+    e->seed = seed;
+    int n = n_boards;
+    hipError_t he = hipSetDevice(device);
+    if (he == hipSuccess) he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
+    if (he != hipSuccess) { env_free(e); delete e; return fail(std::string("stream: ") + hipGetErrorString(he)); }
+    if (dalloc(&e->bb, (size_t)NBB * n) || dalloc(&e->meta, n) || dalloc(&e->init, NBB) ||
+        dalloc(&e->d.hkey, (size_t)HIST_CAP * n) || dalloc(&e->d.hboard, (size_t)HIST_CAP * NBB * n) ||
+        dalloc(&e->d.draw, n) || dalloc(&e->d.act, n) || dalloc(&e->d.reward, n) || dalloc(&e->d.done, n) ||
+        dalloc(&e->d.reason, n) || dalloc(&e->d.nsteps, n) || dalloc(&e->mbox, (size_t)64 * n) ||
+        dalloc(&e->m8, (size_t)8 * n) || dalloc(&e->mask, n) || dalloc(&e->counts, n) || dalloc(&e->stats, (size_t)8 * n)) {
+        std::string m = g_err;
+        env_free(e); delete e;
+        return fail(m);
+    }
+    // initial board bitboards (pure data conversion of the caller's input; no engine work)
+    Pos ip = from_mailbox(ib, 0);
+    u64 ibb[NBB] = {ip.k, ip.q, ip.r, ip.b, ip.n, ip.p, ip.w};
+    he = hipMemcpyAsync(e->init, ibb, sizeof(ibb), hipMemcpyHostToDevice, e->stream);
+    if (he == hipSuccess) he = hipMemsetAsync(e->d.draw, 0, (size_t)4 * n, e->stream);
+    if (he == hipSuccess) he = hipMemsetAsync(e->d.nsteps, 0, (size_t)4 * n, e->stream);
+    if (he == hipSuccess) he = hipMemsetAsync(e->d.reward, 0, (size_t)4 * n, e->stream);
+    if (he == hipSuccess) he = hipMemsetAsync(e->d.done, 0, (size_t)n, e->stream);
+    if (he == hipSuccess) he = hipMemsetAsync(e->d.reason, 0, (size_t)n, e->stream);
+    if (he == hipSuccess) he = hipMemsetAsync(e->stats, 0, (size_t)64 * n, e->stream);
+    for (auto& v : e->ev) if (he == hipSuccess) he = hipEventCreate(&v);
+    if (he != hipSuccess) { env_free(e); delete e; return fail(std::string("env init: ") + hipGetErrorString(he)); }
+    e->d.st = SoA{e->bb, e->meta, n};
+    e->d.init = e->init;
+    e->d.seed = seed;
+    e->d.n = n;
+    k_env_reset<<<grid_for(n), BLOCK, 0, e->stream>>>(e->d, nullptr, 1);
+    he = hipGetLastError();
+    if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
+    if (he != hipSuccess) { env_free(e); delete e; return fail(std::string("reset: ") + hipGetErrorString(he)); }
+    e->policy_ready = true;
+    *out = e;
+    return 0;
+}
+
+extern "C" int gc_env_destroy(gc_env* e) {
+    if (!e) return 0;
+    (void)hipSetDevice(e->device);
+    (void)hipStreamSynchronize(e->stream);
+    env_free(e);
+    delete e;
+    return 0;
+}
+
+extern "C" int gc_env_num_boards(gc_env* e) { return e ? e->n : -1; }
+
+extern "C" int gc_env_reset(gc_env* e, const uint8_t* mask) {
+    if (!e) return fail("null env");
+    HIPCHK(hipSetDevice(e->device));
+    if (mask) HIPCHK(hipMemcpyAsync(e->mask, mask, e->n, hipMemcpyHostToDevice, e->stream));
+    k_env_reset<<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d, mask ? e->mask : nullptr, 1);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(e->stream));
+    e->policy_ready = true;
+    return 0;
+}
+
+extern "C" int gc_env_step(gc_env* e, const uint16_t* actions, int32_t* reward, uint8_t* done, uint8_t* reason) {
+    if (!e || !actions) return fail("null argument");
+    for (int i = 0; i < e->n; i++)
+        if (actions[i] > A_RESIGN) return fail("action out of range [0, 4100] at index " + std::to_string(i));
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipMemcpyAsync(e->d.act, actions, (size_t)2 * e->n, hipMemcpyHostToDevice, e->stream));
+    k_env_step<false><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d);
+    HIPCHK(hipGetLastError());
+    e->policy_ready = false;
+    if (reward) HIPCHK(hipMemcpyAsync(reward, e->d.reward, (size_t)4 * e->n, hipMemcpyDeviceToHost, e->stream));
+    if (done) HIPCHK(hipMemcpyAsync(done, e->d.done, e->n, hipMemcpyDeviceToHost, e->stream));
+    if (reason) HIPCHK(hipMemcpyAsync(reason, e->d.reason, e->n, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return 0;
+}
+
+// device-resident random self-play: n_plies launches of the one-ply step kernel (no host
+// traffic, no sync).  Outputs of the LAST ply stay in device buffers (gc_env_get_outputs).
+extern "C" int gc_env_step_random(gc_env* e, int n_plies) {
+    if (!e) return fail("null env");
+    if (!e->policy_ready) return fail("policy actions stale: call gc_env_reset or gc_env_select_random first");
+    HIPCHK(hipSetDevice(e->device));
+    for (int p = 0; p < n_plies; p++) {
+        k_env_step<true><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d);
+        HIPCHK(hipGetLastError());
+    }
+    return 0;
+}
+
+__global__ void k_select(EnvDev e) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= e.n) return;
+    Pos s = e.st.load(i);
+    Gen g;
+    gen_init(s, g);
+    u32 d = e.draw[i];
+    e.act[i] = pick(s, g, count_legal(s, g), e.seed, i, d);
+    e.draw[i] = d;
+}
+
+extern "C" int gc_env_select_random(gc_env* e) {
+    if (!e) return fail("null env");
+    HIPCHK(hipSetDevice(e->device));
+    k_select<<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d);
+    HIPCHK(hipGetLastError());
+    e->policy_ready = true;
+    return 0;
+}
+
+extern "C" int gc_env_rollout(gc_env* e, int n_plies, int16_t* tr_action, int16_t* tr_reward, uint8_t* tr_done,
+                              uint8_t* tr_reason, uint64_t* stats8) {
+    if (!e) return fail("null env");
+    if (n_plies < 0) return fail("n_plies must be >= 0");
+    if (!e->policy_ready) return fail("policy actions stale: call gc_env_reset or gc_env_select_random first");
+    HIPCHK(hipSetDevice(e->device));
+    bool trace = tr_action || tr_reward || tr_done || tr_reason;
+    int16_t *da = nullptr, *dr = nullptr;
+    uint8_t *dd = nullptr, *dq = nullptr;
+    size_t cnt = (size_t)n_plies * e->n;
+    if (trace && (dalloc(&da, cnt) || dalloc(&dr, cnt) || dalloc(&dd, cnt) || dalloc(&dq, cnt))) return -1;
+    HIPCHK(hipMemsetAsync(e->stats, 0, (size_t)64 * e->n, e->stream));
+    k_env_rollout<<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d, n_plies, da, dr, dd, dq, e->stats);
+    hipError_t le = hipGetLastError();
+    if (le != hipSuccess) return fail(std::string("rollout launch: ") + hipGetErrorString(le));
+    if (trace) {
+        if (tr_action) HIPCHK(hipMemcpyAsync(tr_action, da, cnt * 2, hipMemcpyDeviceToHost, e->stream));
+        if (tr_reward) HIPCHK(hipMemcpyAsync(tr_reward, dr, cnt * 2, hipMemcpyDeviceToHost, e->stream));
+        if (tr_done) HIPCHK(hipMemcpyAsync(tr_done, dd, cnt, hipMemcpyDeviceToHost, e->stream));
+        if (tr_reason) HIPCHK(hipMemcpyAsync(tr_reason, dq, cnt, hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream));
+        (void)hipFree(da); (void)hipFree(dr); (void)hipFree(dd); (void)hipFree(dq);
+    }
+    if (stats8) {
+        std::vector<uint64_t> st((size_t)8 * e->n);
+        HIPCHK(hipMemcpyAsync(st.data(), e->stats, st.size() * 8, hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream));
+        for (int k = 0; k < 8; k++) stats8[k] = 0;
+        for (int i = 0; i < e->n; i++)
+            for (int k = 0; k < 8; k++) stats8[k] += st[(size_t)8 * i + k];
+    }
+    return 0;
+}
+
+extern "C" int gc_env_get_outputs(gc_env* e, int32_t* reward, uint8_t* done, uint8_t* reason, uint16_t* next_action,
+                                  uint32_t* nsteps) {
+    if (!e) return fail("null env");
+    HIPCHK(hipSetDevice(e->device));
+    if (reward) HIPCHK(hipMemcpyAsync(reward, e->d.reward, (size_t)4 * e->n, hipMemcpyDeviceToHost, e->stream));
+    if (done) HIPCHK(hipMemcpyAsync(done, e->d.done, e->n, hipMemcpyDeviceToHost, e->stream));
+    if (reason) HIPCHK(hipMemcpyAsync(reason, e->d.reason, e->n, hipMemcpyDeviceToHost, e->stream));
+    if (next_action) HIPCHK(hipMemcpyAsync(next_action, e->d.act, (size_t)2 * e->n, hipMemcpyDeviceToHost, e->stream));
+    if (nsteps) HIPCHK(hipMemcpyAsync(nsteps, e->d.nsteps, (size_t)4 * e->n, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return 0;
+}
+
+extern "C" int gc_env_get_states(gc_env* e, int8_t* boards, uint8_t* meta) {
+    if (!e) return fail("null env");
+    HIPCHK(hipSetDevice(e->device));
+    k_export<<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d.st, e->mbox, e->m8);
+    HIPCHK(hipGetLastError());
+    if (boards) HIPCHK(hipMemcpyAsync(boards, e->mbox, (size_t)64 * e->n, hipMemcpyDeviceToHost, e->stream));
+    if (meta) HIPCHK(hipMemcpyAsync(meta, e->m8, (size_t)8 * e->n, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return 0;
+}
+
+// set states (FEN/dict ingest). meta8[7] = move_count; repetition windows are cleared.
+extern "C" int gc_env_set_states(gc_env* e, const int8_t* boards, const uint8_t* meta) {
+    if (!e || !boards || !meta) return fail("null argument");
+    if (check_boards(e->n, boards)) return -1;
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipMemcpyAsync(e->mbox, boards, (size_t)64 * e->n, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(hipMemcpyAsync(e->m8, meta, (size_t)8 * e->n, hipMemcpyHostToDevice, e->stream));
+    k_import<<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->mbox, e->m8, nullptr, e->d.st);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(e->stream));
+    e->policy_ready = false;
+    return 0;
+}
+
+extern "C" int gc_env_legal_moves(gc_env* e, uint16_t* moves, int cap, int32_t* counts) {
+    if (!e || !moves || !counts) return fail("null argument");
+    if (cap <= 0) return fail("cap must be > 0");
+    HIPCHK(hipSetDevice(e->device));
+    if (cap > e->list_cap) {
+        if (e->list) (void)hipFree(e->list);
+        e->list = nullptr;
+        e->list_cap = 0;
+        if (dalloc(&e->list, (size_t)cap * e->n)) return -1;
+        e->list_cap = cap;
+    }
+    k_list<<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d.st, 0, cap, e->list, e->counts);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(moves, e->list, (size_t)2 * cap * e->n, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(counts, e->counts, (size_t)4 * e->n, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return 0;
+}
+
+extern "C" int gc_env_legal_mask(gc_env* e, uint64_t* mask, int32_t* counts) {
+    if (!e || !mask) return fail("null argument");
+    HIPCHK(hipSetDevice(e->device));
+    if (!e->lmask && dalloc(&e->lmask, (size_t)65 * e->n)) return -1;
+    k_mask<<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d.st, e->lmask, e->counts);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(mask, e->lmask, (size_t)8 * 65 * e->n, hipMemcpyDeviceToHost, e->stream));
+    if (counts) HIPCHK(hipMemcpyAsync(counts, e->counts, (size_t)4 * e->n, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return 0;
+}
+
+extern "C" int gc_env_synchronize(gc_env* e) {
+    if (!e) return fail("null env");
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return 0;
+}
+
+extern "C" int gc_env_record_event(gc_env* e, int slot) {
+    if (!e || slot < 0 || slot >= 8) return fail("bad env or event slot");
+    HIPCHK(hipEventRecord(e->ev[slot], e->stream));
+    return 0;
+}
+
+extern "C" int gc_env_elapsed_ms(gc_env* e, int a, int b, float* ms) {
+    if (!e || !ms || a < 0 || a >= 8 || b < 0 || b >= 8) return fail("bad argument");
+    HIPCHK(hipEventSynchronize(e->ev[b]));
+    HIPCHK(hipEventElapsedTime(ms, e->ev[a], e->ev[b]));
+    return 0;
+}
+
+// sum over boards of the repetition-window length (bytes accounting in bench.py)
+__global__ void k_window_sum(SoA st, unsigned long long* out) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    unsigned long long v = i < st.n ? (unsigned long long)hl_of(st.meta[i]) : 0ull;
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd(out, v);
+}
+
+extern "C" int gc_env_window_sum(gc_env* e, uint64_t* sum) {
+    if (!e || !sum) return fail("null argument");
+    HIPCHK(hipSetDevice(e->device));
+    unsigned long long* d = nullptr;
+    if (dalloc(&d, 1)) return -1;
+    HIPCHK(hipMemsetAsync(d, 0, 8, e->stream));
+    k_window_sum<<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d.st, d);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(sum, d, 8, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    (void)hipFree(d);
+    return 0;
+}
+
+// bytes of device memory held by the env (for reports)
+extern "C" uint64_t gc_env_device_bytes(gc_env* e) {
+    if (!e) return 0;
+    uint64_t n = (uint64_t)e->n;
+    return n * (NBB * 8 + 4) + n * HIST_CAP * (4 + NBB * 8) + n * (4 + 2 + 4 + 1 + 1 + 4) + n * (64 + 8 + 1 + 4 + 64);
+}

@@ -1,0 +1,87 @@
+"""ctypes binding of libgymchess.so (include/gymchess.h).
+
+The shared library holds the HIP kernels for gfx950 and the extern "C" launch shim.
+There is no CPU fallback: if the library is missing or no GPU is visible every call
+fails loudly.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libgymchess.so")
+
+# every symbol declared in include/gymchess.h: name -> (restype, argtypes)
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_U64 = ctypes.c_uint64
+SIGNATURES = {
+    "gc_last_error": (ctypes.c_char_p, []),
+    "gc_version": (_I, []),
+    "gc_get_device_count": (_I, [_P]),
+    "gc_engine_create": (_I, [_I, _P]),
+    "gc_engine_destroy": (_I, [_P]),
+    "gc_engine_get_possible_moves": (_I, [_P, _I, _P, _P, _P, _I, _P, _I, _P]),
+    "gc_engine_get_castle_moves": (_I, [_P, _I, _P, _P, _P, _P, _P]),
+    "gc_engine_next_state": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "gc_engine_update_state": (_I, [_P, _I, _P, _P, _P, _P]),
+    "gc_engine_perft": (_I, [_P, _I, _P, _P, _I, _P]),
+    "gc_env_create": (_I, [_I, _I, _U64, _P, _P]),
+    "gc_env_destroy": (_I, [_P]),
+    "gc_env_num_boards": (_I, [_P]),
+    "gc_env_reset": (_I, [_P, _P]),
+    "gc_env_step": (_I, [_P, _P, _P, _P, _P]),
+    "gc_env_step_random": (_I, [_P, _I]),
+    "gc_env_select_random": (_I, [_P]),
+    "gc_env_rollout": (_I, [_P, _I, _P, _P, _P, _P, _P]),
+    "gc_env_get_outputs": (_I, [_P, _P, _P, _P, _P, _P]),
+    "gc_env_get_states": (_I, [_P, _P, _P]),
+    "gc_env_set_states": (_I, [_P, _P, _P]),
+    "gc_env_legal_moves": (_I, [_P, _P, _I, _P]),
+    "gc_env_legal_mask": (_I, [_P, _P, _P]),
+    "gc_env_synchronize": (_I, [_P]),
+    "gc_env_record_event": (_I, [_P, _I]),
+    "gc_env_elapsed_ms": (_I, [_P, _I, _I, _P]),
+    "gc_env_device_bytes": (_U64, [_P]),
+    "gc_env_window_sum": (_I, [_P, _P]),
+}
+
+_lib = None
+
+
+class GymChessError(RuntimeError):
+    pass
+
+
+def load(path=LIB_PATH):
+    """Load libgymchess.so (raises if it was not built: run __graft_entry__.build())."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise GymChessError(
+            f"{path} not found: the HIP extension is not built (python -c 'import __graft_entry__ as g; g.build()')"
+        )
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc):
+    if rc != 0:
+        msg = load().gc_last_error()
+        raise GymChessError(msg.decode() if msg else f"gymchess call failed ({rc})")
+
+
+def ptr(a):
+    """numpy array -> void* (the array must stay alive for the call)."""
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def device_count():
+    n = ctypes.c_int(0)
+    check(load().gc_get_device_count(ctypes.byref(n)))
+    return n.value

@@ -1,0 +1,155 @@
+"""Engine API on the GPU.
+
+* `Engine`      -- batched numpy API over gc_engine_* (many positions per launch).
+* `ChessEngine` -- drop-in for the reference's PyO3 class `gym_chess.ChessEngine`
+                   (/root/reference/src/lib.rs:1412-1512): same four methods, same dict /
+                   "e2e4"-string conventions, same error behaviour, one GPU launch per call.
+
+Reference call sites this replaces: chess_v2.py:146 (construction), 204 (update_state),
+419 (next_state), 579 (get_possible_moves), 590 (get_castle_moves).
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from . import codec as C
+
+MAX_LIST = 320  # > the largest legal move list of any position reachable by the engine
+
+
+class Engine:
+    """Batched stateless engine on one device.  States are (boards int8[n,64], meta uint8[n,8])."""
+
+    def __init__(self, device=0):
+        self._L = _lib.load()
+        h = ctypes.c_void_p()
+        _lib.check(self._L.gc_engine_create(int(device), ctypes.byref(h)))
+        self._h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.gc_engine_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @staticmethod
+    def _prep(boards, meta):
+        b = np.ascontiguousarray(boards, dtype=np.int8).reshape(-1, 64)
+        m = np.ascontiguousarray(meta, dtype=np.uint8).reshape(-1, 8)
+        if b.shape[0] != m.shape[0]:
+            raise ValueError("boards and meta must have the same batch size")
+        return b, m
+
+    @staticmethod
+    def _players(player_white, n):
+        p = np.ascontiguousarray(np.broadcast_to(np.asarray(player_white, dtype=np.uint8), (n,)))
+        return p
+
+    def possible_moves(self, boards, meta, player_white, attack=False, cap=MAX_LIST):
+        """-> (moves uint16[n, cap], counts int32[n]) in reference order."""
+        b, m = self._prep(boards, meta)
+        n = b.shape[0]
+        p = self._players(player_white, n)
+        out = np.zeros((n, cap), dtype=np.uint16)
+        cnt = np.zeros(n, dtype=np.int32)
+        _lib.check(self._L.gc_engine_get_possible_moves(self._h, n, _lib.ptr(b), _lib.ptr(m), _lib.ptr(p),
+                                                        int(bool(attack)), _lib.ptr(out), int(cap), _lib.ptr(cnt)))
+        return out, cnt
+
+    def castle_moves(self, boards, meta, player_white):
+        b, m = self._prep(boards, meta)
+        n = b.shape[0]
+        p = self._players(player_white, n)
+        out = np.zeros((n, 2), dtype=np.uint16)
+        cnt = np.zeros(n, dtype=np.int32)
+        _lib.check(self._L.gc_engine_get_castle_moves(self._h, n, _lib.ptr(b), _lib.ptr(m), _lib.ptr(p),
+                                                      _lib.ptr(out), _lib.ptr(cnt)))
+        return out, cnt
+
+    def next_state(self, boards, meta, player_white, actions):
+        """-> (boards, meta, rewards int32[n], status int32[n])"""
+        b, m = self._prep(boards, meta)
+        n = b.shape[0]
+        p = self._players(player_white, n)
+        a = np.ascontiguousarray(np.broadcast_to(np.asarray(actions, dtype=np.uint16), (n,)))
+        ob = np.zeros((n, 64), dtype=np.int8)
+        om = np.zeros((n, 8), dtype=np.uint8)
+        rw = np.zeros(n, dtype=np.int32)
+        st = np.zeros(n, dtype=np.int32)
+        _lib.check(self._L.gc_engine_next_state(self._h, n, _lib.ptr(b), _lib.ptr(m), _lib.ptr(p), _lib.ptr(a),
+                                                _lib.ptr(ob), _lib.ptr(om), _lib.ptr(rw), _lib.ptr(st)))
+        return ob, om, rw, st
+
+    def update_state(self, boards, meta):
+        b, m = self._prep(boards, meta)
+        n = b.shape[0]
+        ob = np.zeros((n, 64), dtype=np.int8)
+        om = np.zeros((n, 8), dtype=np.uint8)
+        _lib.check(self._L.gc_engine_update_state(self._h, n, _lib.ptr(b), _lib.ptr(m), _lib.ptr(ob), _lib.ptr(om)))
+        return ob, om
+
+    def perft(self, boards, meta, depth):
+        b, m = self._prep(boards, meta)
+        n = b.shape[0]
+        out = np.zeros(n, dtype=np.uint64)
+        _lib.check(self._L.gc_engine_perft(self._h, n, _lib.ptr(b), _lib.ptr(m), int(depth), _lib.ptr(out)))
+        return out
+
+
+class ChessEngine:
+    """Drop-in replacement for the reference's `gym_chess.ChessEngine` (lib.rs:1412-1512).
+
+    Errors mirror the reference: a missing state key raises (the Rust side unwrap()s);
+    a bad colour or a both-kings-checked result raises SystemError (PyO3 returns Ok with a
+    Python exception set, lib.rs:434-437, 1442-1446); an empty from-square raises
+    (Rust panic, lib.rs:693-695).
+    """
+
+    def __init__(self, device=0):
+        self._e = Engine(device)
+
+    def next_state(self, state, player, move):
+        b, m = C.dict_to_arrays(state)
+        white = self._player(player)
+        a = C.str_to_action(move)
+        ob, om, rw, st = self._e.next_state(b, m, white, a)
+        if st[0] == -1:
+            raise RuntimeError("Bad move - piece is empty !")
+        if st[0] == 1:
+            raise SystemError("Both Kings are in check: this position is impossible")
+        if st[0] != 0:
+            raise ValueError(f"bad move {move!r}")
+        return C.arrays_to_dict(ob[0], om[0]), int(rw[0])
+
+    def get_possible_moves(self, state, player, attack=False):
+        b, m = C.dict_to_arrays(state)
+        white = self._player(player)
+        out, cnt = self._e.possible_moves(b, m, white, attack)
+        n = int(cnt[0])
+        if n > out.shape[1]:
+            out, cnt = self._e.possible_moves(b, m, white, attack, cap=n)
+        return [C.action_to_str(x) for x in out[0, :n]]
+
+    def get_castle_moves(self, state, player):
+        b, m = C.dict_to_arrays(state)
+        out, cnt = self._e.castle_moves(b, m, self._player(player))
+        return [C.action_to_str(x) for x in out[0, : int(cnt[0])]]
+
+    def update_state(self, state):
+        b, m = C.dict_to_arrays(state)
+        ob, om = self._e.update_state(b, m)
+        return C.arrays_to_dict(ob[0], om[0])
+
+    @staticmethod
+    def _player(player):
+        try:
+            return C.player_to_white(player)
+        except ValueError as ex:  # lib.rs:433-437
+            raise SystemError(str(ex)) from None

@@ -1,0 +1,162 @@
+"""Batched ChessEnvV2 on one GPU (chess_v2.py:132-602 semantics, opponent="none").
+
+`BatchedChessEnv(num_boards)` keeps N boards resident in HBM (bitboard SoA) and exposes
+the reference env surface vectorised over boards:
+
+    reset(mask=None)            chess_v2.py:183-217
+    step(actions)               chess_v2.py:219-294 -> (reward int32[N], done bool[N], reason uint8[N])
+    possible_moves / possible_actions / legal_mask / state / board arrays
+
+plus the device-resident random self-play driver of test_benchmark.py
+(`step_random`, `rollout`) used by bench.py.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from . import codec as C
+
+REASONS = {0: "none", 1: "mate", 2: "repetition", 3: "move_cap", 4: "no_moves", 5: "both_kings_checked",
+           6: "invalid_action", 7: "already_done"}
+
+
+class BatchedChessEnv:
+    def __init__(self, num_boards, device=0, seed=0, initial_board=None):
+        self._L = _lib.load()
+        self.num_boards = int(num_boards)
+        self.device = int(device)
+        self.seed = int(seed)
+        ib = None
+        if initial_board is not None:
+            ib = C.board_to_array(initial_board)
+        h = ctypes.c_void_p()
+        _lib.check(self._L.gc_env_create(self.device, self.num_boards, ctypes.c_uint64(self.seed),
+                                         _lib.ptr(ib) if ib is not None else None, ctypes.byref(h)))
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.gc_env_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ gym surface
+    def reset(self, mask=None):
+        m = None
+        if mask is not None:
+            m = np.ascontiguousarray(mask, dtype=np.uint8).reshape(self.num_boards)
+        _lib.check(self._L.gc_env_reset(self._h, _lib.ptr(m) if m is not None else None))
+        return self.state()
+
+    def step(self, actions):
+        a = np.ascontiguousarray(actions, dtype=np.int64).reshape(self.num_boards)
+        if (a < 0).any() or (a >= C.N_ACTIONS).any():  # action_space.contains (chess_v2.py:237)
+            raise AssertionError(f"ACTION ERROR {a[(a < 0) | (a >= C.N_ACTIONS)][0]}")
+        a = a.astype(np.uint16)
+        rw = np.zeros(self.num_boards, dtype=np.int32)
+        dn = np.zeros(self.num_boards, dtype=np.uint8)
+        why = np.zeros(self.num_boards, dtype=np.uint8)
+        _lib.check(self._L.gc_env_step(self._h, _lib.ptr(a), _lib.ptr(rw), _lib.ptr(dn), _lib.ptr(why)))
+        return rw, dn.astype(bool), why
+
+    def possible_actions(self, cap=320):
+        """list of per-board action lists in reference order (chess_v2.py:333-335)."""
+        moves, cnt = self.legal_moves(cap)
+        return [[int(x) for x in moves[i, : cnt[i]]] for i in range(self.num_boards)]
+
+    def possible_moves(self, cap=320):
+        """per-board move lists in the env's coordinate form (chess_v2.py:573-582)."""
+        return [[C.action_to_move(a) for a in acts] for acts in self.possible_actions(cap)]
+
+    def legal_moves(self, cap=320):
+        moves = np.zeros((self.num_boards, cap), dtype=np.uint16)
+        cnt = np.zeros(self.num_boards, dtype=np.int32)
+        _lib.check(self._L.gc_env_legal_moves(self._h, _lib.ptr(moves), int(cap), _lib.ptr(cnt)))
+        return moves, cnt
+
+    def legal_mask(self):
+        """bool[N, 4101] action mask (RL form of possible_actions)."""
+        raw = np.zeros((self.num_boards, 65), dtype=np.uint64)
+        cnt = np.zeros(self.num_boards, dtype=np.int32)
+        _lib.check(self._L.gc_env_legal_mask(self._h, _lib.ptr(raw), _lib.ptr(cnt)))
+        bits = np.unpackbits(raw[:, :64].view(np.uint8).reshape(self.num_boards, 64, 8), axis=2, bitorder="little")
+        out = np.zeros((self.num_boards, C.N_ACTIONS), dtype=bool)
+        out[:, :4096] = bits.reshape(self.num_boards, 4096).astype(bool)
+        for c in range(4):
+            out[:, 4096 + c] = (raw[:, 64] >> np.uint64(c)) & np.uint64(1) != 0
+        return out
+
+    def boards(self):
+        b = np.zeros((self.num_boards, 64), dtype=np.int8)
+        m = np.zeros((self.num_boards, 8), dtype=np.uint8)
+        _lib.check(self._L.gc_env_get_states(self._h, _lib.ptr(b), _lib.ptr(m)))
+        return b, m
+
+    def state(self, i=None):
+        """state dict(s) in the reference format (chess_v2.py:301-313)."""
+        b, m = self.boards()
+        if i is not None:
+            return C.arrays_to_dict(b[i], m[i])
+        return [C.arrays_to_dict(b[k], m[k]) for k in range(self.num_boards)]
+
+    def set_states(self, boards, meta):
+        b = np.ascontiguousarray(boards, dtype=np.int8).reshape(self.num_boards, 64)
+        m = np.ascontiguousarray(meta, dtype=np.uint8).reshape(self.num_boards, 8)
+        _lib.check(self._L.gc_env_set_states(self._h, _lib.ptr(b), _lib.ptr(m)))
+
+    # ------------------------------------------------------------------ device-resident driver
+    def select_random(self):
+        _lib.check(self._L.gc_env_select_random(self._h))
+
+    def step_random(self, n_plies=1):
+        _lib.check(self._L.gc_env_step_random(self._h, int(n_plies)))
+
+    def outputs(self):
+        n = self.num_boards
+        rw = np.zeros(n, dtype=np.int32)
+        dn = np.zeros(n, dtype=np.uint8)
+        why = np.zeros(n, dtype=np.uint8)
+        act = np.zeros(n, dtype=np.uint16)
+        ns = np.zeros(n, dtype=np.uint32)
+        _lib.check(self._L.gc_env_get_outputs(self._h, _lib.ptr(rw), _lib.ptr(dn), _lib.ptr(why), _lib.ptr(act),
+                                              _lib.ptr(ns)))
+        return dict(reward=rw, done=dn, reason=why, next_action=act, nsteps=ns)
+
+    def rollout(self, n_plies, trace=False):
+        n = self.num_boards
+        st = np.zeros(8, dtype=np.uint64)
+        if trace:
+            ta = np.zeros((n_plies, n), dtype=np.int16)
+            tr = np.zeros((n_plies, n), dtype=np.int16)
+            td = np.zeros((n_plies, n), dtype=np.uint8)
+            tq = np.zeros((n_plies, n), dtype=np.uint8)
+            _lib.check(self._L.gc_env_rollout(self._h, int(n_plies), _lib.ptr(ta), _lib.ptr(tr), _lib.ptr(td),
+                                              _lib.ptr(tq), _lib.ptr(st)))
+            return st, dict(action=ta, reward=tr, done=td, reason=tq)
+        _lib.check(self._L.gc_env_rollout(self._h, int(n_plies), None, None, None, None, _lib.ptr(st)))
+        return st, None
+
+    def synchronize(self):
+        _lib.check(self._L.gc_env_synchronize(self._h))
+
+    def record_event(self, slot):
+        _lib.check(self._L.gc_env_record_event(self._h, int(slot)))
+
+    def elapsed_ms(self, a, b):
+        ms = ctypes.c_float()
+        _lib.check(self._L.gc_env_elapsed_ms(self._h, int(a), int(b), ctypes.byref(ms)))
+        return ms.value
+
+    def window_sum(self):
+        v = ctypes.c_uint64()
+        _lib.check(self._L.gc_env_window_sum(self._h, ctypes.byref(v)))
+        return int(v.value)
+
+    def device_bytes(self):
+        return int(self._L.gc_env_device_bytes(self._h))

@@ -1,0 +1,111 @@
+/* gymchess.h -- C-ABI of libgymchess.so, the MI355X-native drop-in for the gym-chess
+ * hot path (reference: /root/reference, bobu36000/gym-chess).
+ *
+ * Plain pointers and sizes only.  All host buffers are caller-owned; device memory is
+ * owned by the handles.  Every function returns 0 on success, non-zero on failure with a
+ * message in gc_last_error() (per calling thread).  One handle per host thread/stream.
+ *
+ * Conventions (identical to the reference):
+ *   board   int8[64], sq = row*8 + col, row 0 = rank 8 (lib.rs:1235-1238);
+ *           ids +-1..6 = K,Q,R,B,N,P, positive = WHITE (lib.rs:11-17, 41-50)
+ *   meta    uint8[8] = {white_to_move, white_king_castle_is_possible,
+ *           white_queen_castle_is_possible, black_king_castle_is_possible,
+ *           black_queen_castle_is_possible, white_king_is_checked,
+ *           black_king_is_checked, move_count}  (the state dict, lib.rs:355-395)
+ *   action  uint16: from*64 + to; 4096 CASTLE_KING_SIDE_WHITE, 4097 ..._QUEEN_SIDE_WHITE,
+ *           4098 ..._KING_SIDE_BLACK, 4099 ..._QUEEN_SIDE_BLACK, 4100 RESIGN
+ *           (chess_v2.py:492-532); 0xFFFF = "no legal move" in policy buffers.
+ */
+#ifndef GYMCHESS_H
+#define GYMCHESS_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GC_ABI_VERSION 1
+
+const char* gc_last_error(void);
+int gc_version(void);
+int gc_get_device_count(int* n);
+
+/* ---------------------------------------------------------------------------------
+ * Stateless engine: batched form of the reference FFI class `ChessEngine`
+ * (#[pyclass] at /root/reference/src/lib.rs:1412-1512, bound in Python at
+ * gym_chess/__init__.py:1, used at chess_v2.py:146, 204, 419, 579, 590).
+ * ------------------------------------------------------------------------------- */
+typedef struct gc_engine gc_engine;
+int gc_engine_create(int device, gc_engine** out);
+int gc_engine_destroy(gc_engine* e);
+
+/* replaces ChessEngine.get_possible_moves(state, player, attack=False) (lib.rs:1454-1480):
+ * per board the ordered action list (normal moves in reference order, then castles QS, KS;
+ * attack != 0: attack-mode moves, no castles).  moves is n*cap; counts[i] may exceed cap
+ * (list truncated). player_white[i] is the `player` argument. */
+int gc_engine_get_possible_moves(gc_engine* e, int n, const int8_t* boards, const uint8_t* meta,
+                                 const uint8_t* player_white, int attack, uint16_t* moves, int cap,
+                                 int32_t* counts);
+/* replaces ChessEngine.get_castle_moves(state, player) (lib.rs:1482-1500); moves is n*2 */
+int gc_engine_get_castle_moves(gc_engine* e, int n, const int8_t* boards, const uint8_t* meta,
+                               const uint8_t* player_white, uint16_t* moves, int32_t* counts);
+/* replaces ChessEngine.next_state(state, player, move) (lib.rs:1422-1452): move, reward,
+ * update_state.  status[i]: 0 ok; 1 both kings checked (the reference sets a Python
+ * exception); -1 empty from-square (the reference panics); -2 bad action. */
+int gc_engine_next_state(gc_engine* e, int n, const int8_t* boards, const uint8_t* meta,
+                         const uint8_t* player_white, const uint16_t* actions, int8_t* out_boards,
+                         uint8_t* out_meta, int32_t* rewards, int32_t* status);
+/* replaces ChessEngine.update_state(state) (lib.rs:1502-1511) */
+int gc_engine_update_state(gc_engine* e, int n, const int8_t* boards, const uint8_t* meta,
+                           int8_t* out_boards, uint8_t* out_meta);
+/* perft by composition of get_all_possible_moves and next_state; the side
+ * to move is meta[0]. depth in [0, 8]. */
+int gc_engine_perft(gc_engine* e, int n, const int8_t* boards, const uint8_t* meta, int depth,
+                    uint64_t* nodes);
+
+/* ---------------------------------------------------------------------------------
+ * Batched env: N independent ChessEnvV2(opponent="none") boards resident on one device
+ * (chess_v2.py:132-602 reset()/step()/possible_moves).
+ * ------------------------------------------------------------------------------- */
+typedef struct gc_env gc_env;
+/* initial_board: int8[64] or NULL for DEFAULT_BOARD (chess_v2.py:98-107) */
+int gc_env_create(int device, int n_boards, uint64_t seed, const int8_t* initial_board, gc_env** out);
+int gc_env_destroy(gc_env* e);
+int gc_env_num_boards(gc_env* e);
+/* reset() (chess_v2.py:183-217) of the boards with mask[i] != 0 (mask NULL = all) */
+int gc_env_reset(gc_env* e, const uint8_t* mask);
+/* step(action) (chess_v2.py:219-294) for every board; host buffers of n entries.
+ * reason[i]: 0 none, 1 mate (+100), 2 3-fold repetition, 3 move cap, 5 both kings checked
+ * (reference raises; state unchanged), 6 invalid action (-10), 7 step after done. */
+int gc_env_step(gc_env* e, const uint16_t* actions, int32_t* reward, uint8_t* done, uint8_t* reason);
+/* Device-resident random self-play (the test_benchmark.py driver): n_plies one-ply kernel
+ * launches; each ply = one env.step() with a uniform Philox pick over the legal list, a
+ * reset when done, a reset without a step when the list is empty (reason 4). */
+int gc_env_step_random(gc_env* e, int n_plies);
+/* re-pick policy actions for the current states (after set_states / external steps) */
+int gc_env_select_random(gc_env* e);
+/* Same driver fused into ONE launch of n_plies plies (state kept in registers).  Optional
+ * host traces of n_plies*n entries ([ply][board]); stats8 = {steps, sum(reward), ends by
+ * reason 0..5} summed over boards (may be NULL). */
+int gc_env_rollout(gc_env* e, int n_plies, int16_t* tr_action, int16_t* tr_reward, uint8_t* tr_done,
+                   uint8_t* tr_reason, uint64_t* stats8);
+int gc_env_get_outputs(gc_env* e, int32_t* reward, uint8_t* done, uint8_t* reason, uint16_t* next_action,
+                       uint32_t* nsteps);
+int gc_env_get_states(gc_env* e, int8_t* boards, uint8_t* meta);
+int gc_env_set_states(gc_env* e, const int8_t* boards, const uint8_t* meta);
+/* possible_moves of every board, reference order; moves is n*cap */
+int gc_env_legal_moves(gc_env* e, uint16_t* moves, int cap, int32_t* counts);
+/* legal action mask per board: 64 words (from -> targets) + 1 word (bit c: action 4096+c) */
+int gc_env_legal_mask(gc_env* e, uint64_t* mask, int32_t* counts);
+int gc_env_synchronize(gc_env* e);
+/* HIP events on the env's stream (8 slots) for in-process kernel timing */
+int gc_env_record_event(gc_env* e, int slot);
+int gc_env_elapsed_ms(gc_env* e, int a, int b, float* ms);
+uint64_t gc_env_device_bytes(gc_env* e);
+/* sum over boards of the current 3-fold repetition-window length (traffic accounting) */
+int gc_env_window_sum(gc_env* e, uint64_t* sum);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,223 @@
+// TEST INFRASTRUCTURE ONLY: the product's bitboard core (gym-chess_amd/csrc/gc_core.h,
+// gc_env.h) compiled for the HOST with g++, so the CPU test suite can differential-test
+// the exact device logic against the C oracle without a GPU.  Never shipped or loaded by
+// the product (the product .so contains only device kernels + the launch shim).
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include "../../gym-chess_amd/csrc/gc_core.h"
+#include "../../gym-chess_amd/csrc/gc_env.h"
+
+using namespace gc;
+
+static Pos import_state(const int8_t* b, const uint8_t* m, int side_override) {
+    bool white = side_override >= 0 ? side_override != 0 : m[0] != 0;
+    u32 meta = (white ? M_WHITE : 0u) | (m[1] ? M_WKC : 0u) | (m[2] ? M_WQC : 0u) | (m[3] ? M_BKC : 0u) |
+               (m[4] ? M_BQC : 0u) | (m[5] ? M_WCHK : 0u) | (m[6] ? M_BCHK : 0u) | ((u32)m[7] << M_MC_SHIFT);
+    Pos s = from_mailbox(b, meta);
+    s.meta = (s.meta & ~(u32)M_RIGHTS) | eff_rights(s);
+    return s;
+}
+static void export_state(const Pos& s, int8_t* b, uint8_t* m) {
+    to_mailbox(s, b);
+    m[0] = (s.meta & M_WHITE) != 0; m[1] = (s.meta & M_WKC) != 0; m[2] = (s.meta & M_WQC) != 0;
+    m[3] = (s.meta & M_BKC) != 0; m[4] = (s.meta & M_BQC) != 0; m[5] = (s.meta & M_WCHK) != 0;
+    m[6] = (s.meta & M_BCHK) != 0; m[7] = (uint8_t)mc_of(s.meta);
+}
+
+extern "C" int host_list(const int8_t* b, const uint8_t* m, int white, int attack, uint16_t* out, int cap) {
+    Pos s = import_state(b, m, white);
+    Gen g;
+    gen_init(s, g);
+    int n = 0;
+    u64 pcs = g.own;
+    while (pcs) {
+        int sq = ctz(pcs);
+        pcs &= pcs - 1;
+        int t = type_at(s, sq);
+        u64 tg = attack ? attack_targets(s, g, sq, t) : legal_targets(s, g, sq, t);
+        int c = popc(tg);
+        for (int k = 0; k < c; k++) {
+            if (n < cap) out[n] = (uint16_t)(sq * 64 + kth_target(tg, sq, t, g.white, k));
+            n++;
+        }
+    }
+    if (!attack) {
+        if (g.castles & 1) { if (n < cap) out[n] = g.white ? A_QSW : A_QSB; n++; }
+        if (g.castles & 2) { if (n < cap) out[n] = g.white ? A_KSW : A_KSB; n++; }
+    }
+    return n;
+}
+
+extern "C" int host_count(const int8_t* b, const uint8_t* m, int white) {
+    Pos s = import_state(b, m, white);
+    Gen g;
+    gen_init(s, g);
+    return count_legal(s, g);
+}
+
+extern "C" int host_select(const int8_t* b, const uint8_t* m, int white, int k) {
+    Pos s = import_state(b, m, white);
+    Gen g;
+    gen_init(s, g);
+    return select_legal(s, g, k);
+}
+
+extern "C" int host_action_legal(const int8_t* b, const uint8_t* m, int white, int a) {
+    Pos s = import_state(b, m, white);
+    Gen g;
+    gen_init(s, g);
+    return action_legal(s, g, a) ? 1 : 0;
+}
+
+extern "C" int host_next_state(const int8_t* b, const uint8_t* m, int white, int action, int8_t* ob, uint8_t* om,
+                               int* reward) {
+    Pos s = import_state(b, m, -1);
+    bool irrev;
+    int rc = apply_move(s, white != 0, action, reward, &irrev);
+    if (rc == 0) {
+        u32 chk = check_flags(s);
+        s.meta = (s.meta & ~(u32)(M_WCHK | M_BCHK)) | chk;
+        if ((chk & (M_WCHK | M_BCHK)) == (M_WCHK | M_BCHK)) rc = 1;
+    }
+    export_state(s, ob, om);
+    return rc;
+}
+
+extern "C" void host_update_state(const int8_t* b, const uint8_t* m, int8_t* ob, uint8_t* om) {
+    Pos s = import_state(b, m, -1);
+    s.meta = (s.meta & ~(u32)(M_WCHK | M_BCHK)) | check_flags(s);
+    export_state(s, ob, om);
+}
+
+extern "C" uint64_t host_between(int a, int b) { return between(a, b); }
+extern "C" uint64_t host_rook_att(int sq, uint64_t occ) { return rook_att(sq, occ); }
+extern "C" uint64_t host_bishop_att(int sq, uint64_t occ) { return bishop_att(sq, occ); }
+extern "C" uint64_t host_side_attacks(const int8_t* b, int white) {
+    uint8_t m[8] = {0};
+    Pos s = import_state(b, m, 1);
+    return side_attacks(s, white != 0);
+}
+
+static uint64_t perft_rec(const Pos& s, int d) {
+    Gen g;
+    gen_init(s, g);
+    if (d <= 1) return (uint64_t)count_legal(s, g);
+    uint64_t tot = 0;
+    int n = count_legal(s, g);
+    for (int k = 0; k < n; k++) {
+        int a = select_legal(s, g, k);
+        Pos c = s;
+        int rw;
+        bool irrev;
+        apply_move(c, g.white, a, &rw, &irrev);
+        c.meta = (c.meta & ~(u32)M_RIGHTS) | eff_rights(c);
+        tot += perft_rec(c, d - 1);
+    }
+    return tot;
+}
+extern "C" uint64_t host_perft(const int8_t* b, const uint8_t* m, int depth) {
+    Pos s = import_state(b, m, -1);
+    if (depth <= 0) return 1;
+    return perft_rec(s, depth);
+}
+
+// ---- env rollout on the host with the same driver as k_env_rollout ----------------------
+struct HostHist {
+    std::vector<u32> keys;
+    std::vector<Pos> boards;
+    HostHist() : keys(HIST_CAP), boards(HIST_CAP) {}
+    u32 key(int i) const { return keys[i]; }
+    bool same(int i, const Pos& s) const {
+        const Pos& h = boards[i];
+        return h.k == s.k && h.q == s.q && h.r == s.r && h.b == s.b && h.n == s.n && h.p == s.p && h.w == s.w;
+    }
+    void put(int i, u32 k, const Pos& s) { keys[i] = k; boards[i] = s; }
+};
+
+extern "C" void host_rollout_trace(const int8_t* init, uint64_t seed, uint32_t board, int plies, int16_t* tr_action,
+                                   int16_t* tr_reward, uint8_t* tr_done, uint8_t* tr_reason, int8_t* final_board,
+                                   uint8_t* final_meta, uint64_t* stats8) {
+    Pos ip = from_mailbox(init, 0);
+    Pos s = env_reset_pos(ip);
+    HostHist h;
+    u32 draw = 0;
+    Gen g;
+    gen_init(s, g);
+    int n = count_legal(s, g);
+    int a = n ? select_legal(s, g, (int)policy_index(seed, board, draw++, (u32)n)) : A_NONE;
+    uint64_t steps = 0, rsum = 0, ends[6] = {0, 0, 0, 0, 0, 0};
+    for (int p = 0; p < plies; p++) {
+        StepOut o = {0, 0, R_NONE, 0};
+        bool have_gen = false;
+        int played = a;
+        if (a == A_NONE) {
+            s = env_reset_pos(ip);
+            o.reason = R_NO_MOVES;
+            ends[R_NO_MOVES]++;
+            played = -1;
+        } else {
+            o = env_step<false>(s, h, a, nullptr);
+            if (o.moved) {
+                gen_init(s, g);
+                have_gen = true;
+                env_finish(s, o, count_legal(s, g));
+            }
+            steps++;
+            rsum += (uint64_t)(int64_t)o.reward;
+            if (o.done) {
+                ends[o.reason < 6 ? o.reason : 0]++;
+                s = env_reset_pos(ip);
+                have_gen = false;
+            }
+        }
+        if (!have_gen) gen_init(s, g);
+        tr_action[p] = (int16_t)played;
+        tr_reward[p] = (int16_t)o.reward;
+        tr_done[p] = (uint8_t)o.done;
+        tr_reason[p] = (uint8_t)o.reason;
+        n = count_legal(s, g);
+        a = n ? select_legal(s, g, (int)policy_index(seed, board, draw++, (u32)n)) : A_NONE;
+    }
+    export_state(s, final_board, final_meta);
+    stats8[0] = steps; stats8[1] = rsum;
+    for (int k = 0; k < 6; k++) stats8[2 + k] = ends[k];
+}
+
+// external-action env for step-by-step replay of the reference env traces
+struct HostEnv {
+    Pos init, s;
+    HostHist h;
+};
+extern "C" void* host_env_new(const int8_t* init) {
+    HostEnv* e = new HostEnv();
+    e->init = from_mailbox(init, 0);
+    e->s = env_reset_pos(e->init);
+    return e;
+}
+extern "C" void host_env_free(void* p) { delete (HostEnv*)p; }
+extern "C" void host_env_reset(void* p) { HostEnv* e = (HostEnv*)p; e->s = env_reset_pos(e->init); }
+extern "C" int host_env_step(void* p, int action, int* reward, int* done, int* reason) {
+    HostEnv* e = (HostEnv*)p;
+    Gen g0;
+    gen_init(e->s, g0);
+    StepOut o = env_step<true>(e->s, e->h, action, &g0);
+    if (o.moved) {
+        Gen g;
+        gen_init(e->s, g);
+        env_finish(e->s, o, count_legal(e->s, g));
+    }
+    *reward = o.reward;
+    *done = o.done;
+    *reason = o.reason;
+    return o.reason == R_BOTH_CHECKED ? 1 : 0;
+}
+extern "C" void host_env_state(void* p, int8_t* b, uint8_t* m) { export_state(((HostEnv*)p)->s, b, m); }
+extern "C" int host_env_moves(void* p, uint16_t* out, int cap) {
+    HostEnv* e = (HostEnv*)p;
+    int8_t b[64];
+    uint8_t m[8];
+    export_state(e->s, b, m);
+    return host_list(b, m, -1, 0, out, cap);
+}

@@ -1,0 +1,142 @@
+"""TEST INFRASTRUCTURE ONLY -- ctypes view of the host build of the product's bitboard core
+(gym-chess_amd/csrc/gc_core.h + gc_env.h compiled by g++), for CPU differential tests."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_SO = os.path.join(_HERE, "_build", "libcorehost.so")
+_L = None
+P = ctypes.c_void_p
+
+
+def lib():
+    global _L
+    if _L is None:
+        src = os.path.join(_HERE, "core_host.cpp")
+        hdr = [os.path.join(_HERE, "..", "..", "gym-chess_amd", "csrc", h) for h in ("gc_core.h", "gc_env.h")]
+        if not os.path.exists(_SO) or os.path.getmtime(_SO) < max(os.path.getmtime(p) for p in [src] + hdr):
+            os.makedirs(os.path.dirname(_SO), exist_ok=True)
+            subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-o", _SO, src], check=True)
+        L = ctypes.CDLL(_SO)
+        L.host_between.restype = ctypes.c_uint64
+        L.host_rook_att.restype = ctypes.c_uint64
+        L.host_rook_att.argtypes = [ctypes.c_int, ctypes.c_uint64]
+        L.host_bishop_att.restype = ctypes.c_uint64
+        L.host_bishop_att.argtypes = [ctypes.c_int, ctypes.c_uint64]
+        L.host_side_attacks.restype = ctypes.c_uint64
+        L.host_side_attacks.argtypes = [P, ctypes.c_int]
+        L.host_perft.restype = ctypes.c_uint64
+        L.host_perft.argtypes = [P, P, ctypes.c_int]
+        L.host_list.argtypes = [P, P, ctypes.c_int, ctypes.c_int, P, ctypes.c_int]
+        L.host_count.argtypes = [P, P, ctypes.c_int]
+        L.host_select.argtypes = [P, P, ctypes.c_int, ctypes.c_int]
+        L.host_action_legal.argtypes = [P, P, ctypes.c_int, ctypes.c_int]
+        L.host_next_state.argtypes = [P, P, ctypes.c_int, ctypes.c_int, P, P, P]
+        L.host_update_state.argtypes = [P, P, P, P]
+        L.host_rollout_trace.argtypes = [P, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, P, P, P, P, P, P, P]
+        L.host_env_new.restype = P
+        L.host_env_new.argtypes = [P]
+        L.host_env_free.argtypes = [P]
+        L.host_env_reset.argtypes = [P]
+        L.host_env_step.argtypes = [P, ctypes.c_int, P, P, P]
+        L.host_env_state.argtypes = [P, P, P]
+        L.host_env_moves.argtypes = [P, P, ctypes.c_int]
+        _L = L
+    return _L
+
+
+def _p(a):
+    return a.ctypes.data_as(P)
+
+
+def _bm(b, m):
+    return np.ascontiguousarray(b, dtype=np.int8).reshape(64), np.ascontiguousarray(m, dtype=np.uint8).reshape(8)
+
+
+def get_list(board, meta, white, attack=False):
+    b, m = _bm(board, meta)
+    out = np.zeros(1024, dtype=np.uint16)
+    n = lib().host_list(_p(b), _p(m), int(white), int(bool(attack)), _p(out), 1024)
+    return [int(x) for x in out[:n]]
+
+
+def count(board, meta, white):
+    b, m = _bm(board, meta)
+    return lib().host_count(_p(b), _p(m), int(white))
+
+
+def select(board, meta, white, k):
+    b, m = _bm(board, meta)
+    return lib().host_select(_p(b), _p(m), int(white), int(k))
+
+
+def action_legal(board, meta, white, a):
+    b, m = _bm(board, meta)
+    return bool(lib().host_action_legal(_p(b), _p(m), int(white), int(a)))
+
+
+def next_state(board, meta, white, action):
+    b, m = _bm(board, meta)
+    ob = np.zeros(64, dtype=np.int8)
+    om = np.zeros(8, dtype=np.uint8)
+    rw = ctypes.c_int()
+    rc = lib().host_next_state(_p(b), _p(m), int(white), int(action), _p(ob), _p(om), ctypes.byref(rw))
+    return rc, ob, om, rw.value
+
+
+def update_state(board, meta):
+    b, m = _bm(board, meta)
+    ob = np.zeros(64, dtype=np.int8)
+    om = np.zeros(8, dtype=np.uint8)
+    lib().host_update_state(_p(b), _p(m), _p(ob), _p(om))
+    return ob, om
+
+
+def perft(board, meta, depth):
+    b, m = _bm(board, meta)
+    return int(lib().host_perft(_p(b), _p(m), int(depth)))
+
+
+def rollout_trace(seed, board_id, plies, init):
+    init = np.ascontiguousarray(init, dtype=np.int8).reshape(64)
+    a = np.zeros(plies, dtype=np.int16)
+    r = np.zeros(plies, dtype=np.int16)
+    d = np.zeros(plies, dtype=np.uint8)
+    q = np.zeros(plies, dtype=np.uint8)
+    fb = np.zeros(64, dtype=np.int8)
+    fm = np.zeros(8, dtype=np.uint8)
+    st = np.zeros(8, dtype=np.uint64)
+    lib().host_rollout_trace(_p(init), seed, board_id, plies, _p(a), _p(r), _p(d), _p(q), _p(fb), _p(fm), _p(st))
+    return dict(action=a, reward=r, done=d, reason=q, final_board=fb, final_meta=fm, stats=st)
+
+
+class HostEnv:
+    def __init__(self, init):
+        self._init = np.ascontiguousarray(init, dtype=np.int8).reshape(64)
+        self.h = lib().host_env_new(_p(self._init))
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().host_env_free(self.h)
+
+    def reset(self):
+        lib().host_env_reset(self.h)
+
+    def step(self, a):
+        rw, dn, why = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        rc = lib().host_env_step(self.h, int(a), ctypes.byref(rw), ctypes.byref(dn), ctypes.byref(why))
+        return rc, rw.value, dn.value, why.value
+
+    def state(self):
+        b = np.zeros(64, dtype=np.int8)
+        m = np.zeros(8, dtype=np.uint8)
+        lib().host_env_state(self.h, _p(b), _p(m))
+        return b, m
+
+    def moves(self):
+        out = np.zeros(1024, dtype=np.uint16)
+        n = lib().host_env_moves(self.h, _p(out), 1024)
+        return [int(x) for x in out[:n]]

@@ -1,0 +1,514 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures under tests/golden/ from the reference itself.
+
+Runs ONLY in the build container (needs /root/reference, which never travels).
+What it runs and why:
+  * the pure-Python v1 engine (gym_chess/envs/chess_v1.py), loaded by path with a
+    stub `gym` -- the only part of the reference that executes here (the Rust v2
+    engine, src/lib.rs, cannot be built: no cargo/rustc, crates not vendored);
+  * the v2 env (gym_chess/envs/chess_v2.py) and the reference's own v2 tests
+    (gym_chess/test/v2/*.py), with `gym_chess.ChessEngine` bound to a stub that
+    speaks lib.rs's dict/str protocol over the C oracle (oracle/gc_oracle.c).
+
+Outputs (data only -- inputs + expected outputs, no reference source):
+  perft_startpos.json      v1 perft(1..4) [+5 with --deep] from DEFAULT_BOARD
+  v1_games.json.gz         ordered move lists + next boards + rewards along seeded
+                           v1 random games, v1->v2 transformed (D4) and filtered
+                           (D1/D2/D3/D10) as SURVEY §8c prescribes
+  v1_perft_midgame.json    v1 perft(1..3) from mid-game positions of those games
+  v2_known_answers.json    every engine call made by the reference's v2 tests
+                           (whose asserts passed) with its inputs and outputs
+  v2_env_traces.json.gz    ChessEnvV2 step() traces (reward/done/move_count/3-fold/
+                           invalid actions; opponent "none" and "random")
+
+Usage:  python tests/golden/make_golden.py [--deep]
+"""
+import argparse
+import gzip
+import importlib.util
+import inspect
+import json
+import multiprocessing as mp
+import os
+import sys
+import types
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+sys.path.insert(0, os.path.join(REPO, "gym-chess_amd"))
+
+import oracle as O  # noqa: E402
+from gym_chess_amd import codec as C  # noqa: E402
+
+
+# --------------------------------------------------------------------------- stubs
+def install_gym_stub():
+    gym = types.ModuleType("gym")
+
+    class Env:
+        pass
+
+    gym.Env = Env
+    spaces = types.ModuleType("gym.spaces")
+
+    class Box:
+        def __init__(self, *a, **k):
+            pass
+
+    class Discrete:
+        def __init__(self, n):
+            self.n = n
+
+        def contains(self, x):
+            return 0 <= int(x) < self.n
+
+    spaces.Box, spaces.Discrete = Box, Discrete
+    error = types.ModuleType("gym.error")
+
+    class Error(Exception):
+        pass
+
+    error.Error = Error
+    utils = types.ModuleType("gym.utils")
+    utils.colorize = lambda s, *a, **k: s
+    seeding = types.ModuleType("gym.utils.seeding")
+    seeding.np_random = lambda seed=None: (np.random.RandomState(seed), seed)
+    utils.seeding = seeding
+    gym.spaces, gym.error, gym.utils = spaces, error, utils
+    for n, m in [("gym", gym), ("gym.spaces", spaces), ("gym.error", error), ("gym.utils", utils),
+                 ("gym.utils.seeding", seeding)]:
+        sys.modules[n] = m
+
+
+def load(name, path):
+    spec = importlib.util.spec_from_file_location(name, path)
+    m = importlib.util.module_from_spec(spec)
+    sys.modules[name] = m
+    spec.loader.exec_module(m)
+    return m
+
+
+CALL_LOG = []
+
+
+class OracleChessEngine:
+    """lib.rs:1412-1512 protocol (dicts + 'e2e4' strings) over the C oracle."""
+
+    def next_state(self, state, player, move):
+        b, m = C.dict_to_arrays(state)
+        white = C.player_to_white(player)
+        a = C.str_to_action(move)
+        rc, nb, nm, rw = O.next_state(b, m, white, a)
+        if rc == -1:
+            raise BaseException("Bad move - piece is empty !")  # Rust panic
+        CALL_LOG.append(dict(op="next_state", board=C.board_to_text(b), meta=[int(x) for x in m[:5]],
+                             white=white, action=a, out_board=C.board_to_text(nb),
+                             out_meta=[int(x) for x in nm[:7]], reward=rw, both_checked=rc == 1))
+        if rc == 1:
+            raise SystemError("Both Kings are in check: this position is impossible")
+        return C.arrays_to_dict(nb, nm), rw
+
+    def get_possible_moves(self, state, player, attack=False):
+        b, m = C.dict_to_arrays(state)
+        white = C.player_to_white(player)
+        acts = O.get_possible_moves(b, m, white, attack)
+        CALL_LOG.append(dict(op="get_possible_moves", board=C.board_to_text(b), meta=[int(x) for x in m[:5]],
+                             white=white, attack=bool(attack), out=acts))
+        return [C.action_to_str(x) for x in acts]
+
+    def get_castle_moves(self, state, player):
+        b, m = C.dict_to_arrays(state)
+        white = C.player_to_white(player)
+        acts = O.get_castle_moves(b, m, white)
+        CALL_LOG.append(dict(op="get_castle_moves", board=C.board_to_text(b), meta=[int(x) for x in m[:5]],
+                             white=white, out=acts))
+        return [C.action_to_str(x) for x in acts]
+
+    def update_state(self, state):
+        b, m = C.dict_to_arrays(state)
+        nb, nm = O.update_state(b, m)
+        CALL_LOG.append(dict(op="update_state", board=C.board_to_text(b), meta=[int(x) for x in m[:5]],
+                             out_meta=[int(x) for x in nm[:7]]))
+        return C.arrays_to_dict(nb, nm)
+
+
+def load_reference():
+    install_gym_stub()
+    v1 = load("ref_chess_v1", f"{REF}/gym_chess/envs/chess_v1.py")
+    # numpy-2 int8 overflow in move_to_action (chess_v1.py:524-526): cast to int
+    orig = v1.ChessEnvV1.move_to_action
+
+    def move_to_action(self, move):
+        if type(move) is list:
+            return (int(move[0][0]) * 8 + int(move[0][1])) * 64 + int(move[1][0]) * 8 + int(move[1][1])
+        return orig(self, move)
+
+    v1.ChessEnvV1.move_to_action = move_to_action
+    pkg = types.ModuleType("gym_chess")
+    pkg.__path__ = []
+    pkg.ChessEngine = OracleChessEngine
+    sys.modules["gym_chess"] = pkg
+    envs = types.ModuleType("gym_chess.envs")
+    envs.__path__ = []
+    sys.modules["gym_chess.envs"] = envs
+    v2 = load("gym_chess.envs.chess_v2", f"{REF}/gym_chess/envs/chess_v2.py")
+    sys.modules["gym_chess.envs.chess_v1"] = v1
+    pkg.ChessEnvV2 = v2.ChessEnvV2
+    pkg.ChessEnvV1 = v1.ChessEnvV1
+    tpkg = types.ModuleType("gym_chess.test")
+    tpkg.__path__ = []
+    sys.modules["gym_chess.test"] = tpkg
+    load("gym_chess.test.utils", f"{REF}/gym_chess/test/utils.py")
+    return v1, v2
+
+
+# --------------------------------------------------------------------------- v1 helpers
+def v1_list_to_actions(moves):
+    out = []
+    for m in moves:
+        if isinstance(m, str):
+            out.append(C.CASTLE_TO_ACTION[m])
+        else:
+            out.append((int(m[0][0]) * 8 + int(m[0][1])) * 64 + int(m[1][0]) * 8 + int(m[1][1]))
+    return out
+
+
+def d4_transform(actions, board):
+    """v1 emits black pawn captures c-1 then c+1 (chess_v1.py:761-764); v2 emits c+1
+    then c-1 (lib.rs:921-924).  Swap adjacent capture pairs of black pawns."""
+    acts = list(actions)
+    i = 0
+    while i < len(acts):
+        a = acts[i]
+        if a < 4096:
+            f, t = divmod(a, 64)
+            if board[f] == -6 and t // 8 == f // 8 + 1 and t % 8 == f % 8 - 1:
+                if i + 1 < len(acts) and acts[i + 1] < 4096:
+                    f2, t2 = divmod(acts[i + 1], 64)
+                    if f2 == f and t2 % 8 == f % 8 + 1 and t2 // 8 == f // 8 + 1:
+                        acts[i], acts[i + 1] = acts[i + 1], acts[i]
+                        i += 2
+                        continue
+        i += 1
+    return acts
+
+
+def v1_perft(env, state, player, depth, other):
+    env.state = state  # D5: v1 pawn pushes read self.state
+    moves = env.get_possible_moves(state=state, player=player)
+    if depth == 1:
+        return len(moves)
+    tot = 0
+    for m in moves:
+        ns, _ = env.next_state(state, player, m, commit=False)
+        tot += v1_perft(env, ns, other(player), depth - 1, other)
+    return tot
+
+
+_V1 = None
+
+
+def _v1_subtree(args):
+    idx, depth = args
+    global _V1
+    if _V1 is None:
+        _V1 = load_reference()[0]
+    env = _V1.ChessEnvV1(opponent="none", log=False)
+    state = env.state.copy()
+    env.state = state
+    moves = env.get_possible_moves(state=state, player="WHITE")
+    ns, _ = env.next_state(state, "WHITE", moves[idx], commit=False)
+    return v1_perft(env, ns, "BLACK", depth - 1, env.get_other_player)
+
+
+def gen_perft_startpos(v1, deep):
+    env = v1.ChessEnvV1(opponent="none", log=False)
+    res = {}
+    top = 5 if deep else 4
+    st0 = env.state.copy()
+    for d in range(1, min(top, 3) + 1):
+        st = st0.copy()
+        res[d] = v1_perft(env, st, "WHITE", d, env.get_other_player)
+        print("v1 perft", d, res[d], flush=True)
+    for d in range(4, top + 1):
+        with mp.Pool(8) as pool:
+            parts = pool.map(_v1_subtree, [(i, d) for i in range(20)])
+        res[d] = int(sum(parts))
+        print("v1 perft", d, res[d], flush=True)
+    return {"board": C.board_to_text(O.DEFAULT_BOARD), "meta": [1, 1, 1, 1, 1],
+            "perft": {str(k): int(v) for k, v in res.items()},
+            "source": "v1 reference (gym_chess/envs/chess_v1.py) via stub gym"}
+
+
+def attack_hits_king(board, white):
+    """D1 filter: can the mover capture the enemy king (v2 allows, v1 refuses)?"""
+    meta = O.make_meta(white, 0, 0, 0, 0)
+    att = O.get_possible_moves(board, meta, white, attack=True)
+    ek = -1 if white else 1
+    return any(board[a % 64] == ek for a in att if a < 4096)
+
+
+def kings_adjacent(board):
+    wk = [i for i in range(64) if board[i] == 1]
+    bk = [i for i in range(64) if board[i] == -1]
+    for a in wk:
+        for b in bk:
+            if max(abs(a // 8 - b // 8), abs(a % 8 - b % 8)) == 1:
+                return True
+    return False
+
+
+def gen_v1_games(v1, n_games, max_plies):
+    games = []
+    midgame = []
+    for g in range(n_games):
+        rng = np.random.RandomState(1000 + g)
+        env = v1.ChessEnvV1(opponent="none", log=False)
+        env.reset()
+        plies = []
+        for ply in range(max_plies):
+            board = env.state.copy().reshape(64)
+            white = env.current_player == "WHITE"
+            rights = [env.white_king_castle_possible, env.white_queen_castle_possible,
+                      env.black_king_castle_possible, env.black_queen_castle_possible]
+            try:
+                moves = env.possible_moves
+                acts = d4_transform(v1_list_to_actions(moves), board)
+            except Exception:
+                break
+            if not moves:
+                break
+            mr = rights[0:2] if white else rights[2:4]
+            skip = (attack_hits_king(board, white) or kings_adjacent(board) or mr[0] != mr[1]
+                    or 1 not in board or -1 not in board)
+            idx = int(rng.choice(np.arange(len(moves))))
+            move = moves[idx]
+            action = env.move_to_action(move)
+            try:
+                ns, rew = env.next_state(env.state, env.current_player, move, commit=False)
+            except Exception:
+                break
+            if not skip:
+                plies.append(dict(board=C.board_to_text(board), white=bool(white),
+                                  rights=[int(bool(x)) for x in rights], moves=acts, action=int(action),
+                                  next_board=C.board_to_text(np.asarray(ns).reshape(64)), reward=int(rew)))
+                if ply in (8, 20, 40) and not any(mr):
+                    midgame.append(dict(board=C.board_to_text(board), white=bool(white)))
+            try:
+                _, _, done, _ = env.step(action)
+            except Exception:
+                break
+            if done:
+                break
+        games.append(dict(seed=1000 + g, plies=plies))
+        print(f"v1 game {g}: {len(plies)} plies recorded", flush=True)
+    return games, midgame
+
+
+def v1_divergences(v1, board, white, depth):
+    """Walk the tree and list every node where the v1 move set differs from the oracle's.
+    Returns (divergences, all_are_D1).  D1 = v2-only moves whose target holds the enemy king
+    (lib.rs:1074, 1130 allow them; chess_v1.py:887-888, 927-928 refuse)."""
+    env = v1.ChessEnvV1(opponent="none", log=False)
+    env.white_king_castle_possible = env.white_queen_castle_possible = False
+    env.black_king_castle_possible = env.black_queen_castle_possible = False
+    divs = []
+
+    def walk(b, wh, d, path):
+        st = b.reshape(8, 8).copy()
+        env.state = st
+        try:
+            m1 = set(v1_list_to_actions(env.get_possible_moves(state=st, player="WHITE" if wh else "BLACK")))
+        except Exception:
+            divs.append(dict(path=path, v1="raised"))
+            return
+        m2 = O.get_possible_moves(b, O.make_meta(wh, 0, 0, 0, 0), wh)
+        if m1 != set(m2):
+            divs.append(dict(path=path, board=C.board_to_text(b), white=wh,
+                             v2_only=sorted(set(m2) - m1), v1_only=sorted(m1 - set(m2))))
+        if d == 1:
+            return
+        for a in m2:
+            if a not in m1:
+                continue  # v1 cannot follow a D1 king capture (D10 afterwards)
+            _, nb, _, _ = O.next_state(b, O.make_meta(wh, 0, 0, 0, 0), wh, a)
+            walk(nb, not wh, d - 1, path + [a])
+
+    walk(board, white, depth, [])
+    ek_ok = True
+    for dv in divs:
+        if dv.get("v1") == "raised" or dv["v1_only"]:
+            ek_ok = False
+            continue
+        bb = C.text_to_board(dv["board"])
+        ek = -1 if dv["white"] else 1
+        if not all(bb[a % 64] == ek for a in dv["v2_only"]):
+            ek_ok = False
+    return divs, ek_ok
+
+
+def gen_v1_perft_midgame(v1, positions, depth):
+    out = []
+    for p in positions:
+        env = v1.ChessEnvV1(opponent="none", log=False)
+        env.white_king_castle_possible = env.white_queen_castle_possible = False
+        env.black_king_castle_possible = env.black_queen_castle_possible = False
+        board = C.text_to_board(p["board"])
+        st = board.reshape(8, 8).copy()
+        player = "WHITE" if p["white"] else "BLACK"
+        res = {}
+        try:
+            for d in range(1, depth + 1):
+                res[str(d)] = int(v1_perft(env, st.copy(), player, d, env.get_other_player))
+        except Exception as ex:  # D2/D10 inside the tree: v1 cannot arbitrate
+            print("skip midgame perft:", type(ex).__name__, flush=True)
+            continue
+        meta = O.make_meta(p["white"], 0, 0, 0, 0)
+        ok = all(O.perft(board, meta, int(d)) == v for d, v in res.items())
+        entry = dict(board=p["board"], meta=[int(p["white"]), 0, 0, 0, 0], v1_perft=res, v1_equals_v2=ok)
+        if not ok:
+            # never dropped silently: record where and why v1 cannot arbitrate
+            divs, all_d1 = v1_divergences(v1, board, p["white"], depth)
+            entry["d1_divergences"] = divs
+            entry["all_divergences_are_D1"] = all_d1
+        print("midgame perft", res, "v1==oracle" if ok else f"differs (all D1: {entry['all_divergences_are_D1']})",
+              flush=True)
+        out.append(entry)
+    return out
+
+
+# --------------------------------------------------------------------------- v2 tests + env
+def gen_v2_known_answers():
+    cases = []
+    for fn in ["test_basic_moves", "test_capture_moves", "test_king_moves", "test_castle_moves",
+               "test_squares_under_attack", "test_run_moves"]:
+        mod = load(f"gym_chess.test.v2.{fn}", f"{REF}/gym_chess/test/v2/{fn}.py")
+        for name, f in inspect.getmembers(mod, inspect.isfunction):
+            if not name.startswith("test_") or f.__module__ != mod.__name__:
+                continue
+            CALL_LOG.clear()
+            import io
+            import contextlib
+            with contextlib.redirect_stdout(io.StringIO()):
+                f()  # the reference's own asserts run here
+            cases.append(dict(module=fn, test=name, calls=list(CALL_LOG)))
+            print(f"v2 test {fn}.{name}: passed, {len(CALL_LOG)} engine calls", flush=True)
+    return cases
+
+
+def trace_env(v2, seed, n_steps, opponent, invalid_every=0, initial_board=None):
+    np.random.seed(seed)
+    kw = dict(opponent=opponent, log=False)
+    if initial_board is not None:
+        kw["initial_board"] = initial_board
+    env = v2.ChessEnvV2(**kw)
+    steps = []
+    resets = 0
+    rng = np.random.RandomState(seed + 7)
+    for i in range(n_steps):
+        moves = env.possible_moves
+        if not moves:
+            env.reset()
+            resets += 1
+            steps.append(dict(kind="reset"))
+            continue
+        if invalid_every and i % invalid_every == invalid_every - 1:
+            action = int(rng.randint(0, 4100))
+        else:
+            idx = np.random.choice(np.arange(len(moves)))
+            action = env.move_to_action(moves[idx])
+        try:
+            state, reward, done, info = env.step(action)
+        except SystemError:
+            steps.append(dict(kind="error", action=int(action)))
+            env.reset()
+            continue
+        steps.append(dict(kind="step", action=int(action), reward=float(reward), done=bool(done),
+                          board=C.board_to_text(np.asarray(state["board"]).reshape(64)),
+                          meta=[int(env.current_player == "WHITE"),
+                                int(state["white_king_castle_is_possible"]),
+                                int(state["white_queen_castle_is_possible"]),
+                                int(state["black_king_castle_is_possible"]),
+                                int(state["black_queen_castle_is_possible"]),
+                                int(bool(state["white_king_is_checked"])),
+                                int(bool(state["black_king_is_checked"]))],
+                          move_count=int(info["move_count"]),
+                          n_moves=len(env.possible_moves)))
+        if done:
+            env.reset()
+            steps.append(dict(kind="reset"))
+    return dict(seed=seed, opponent=opponent, invalid_every=invalid_every,
+                initial_board=None if initial_board is None else C.board_to_text(np.asarray(initial_board).reshape(64)),
+                steps=steps)
+
+
+def trace_scripted(v2, actions, initial_board=None):
+    kw = dict(opponent="none", log=False)
+    if initial_board is not None:
+        kw["initial_board"] = initial_board
+    env = v2.ChessEnvV2(**kw)
+    steps = []
+    for a in actions:
+        state, reward, done, info = env.step(int(a))
+        steps.append(dict(kind="step", action=int(a), reward=float(reward), done=bool(done),
+                          board=C.board_to_text(np.asarray(state["board"]).reshape(64)),
+                          move_count=int(info["move_count"]), n_moves=len(env.possible_moves)))
+    return dict(scripted=True, actions=[int(a) for a in actions],
+                initial_board=None if initial_board is None else C.board_to_text(np.asarray(initial_board).reshape(64)),
+                steps=steps)
+
+
+def gen_env_traces(v2):
+    traces = []
+    for s in range(4):
+        traces.append(trace_env(v2, 2000 + s, 700, "none"))
+    traces.append(trace_env(v2, 2100, 400, "none", invalid_every=5))
+    for s in range(2):
+        traces.append(trace_env(v2, 2200 + s, 400, "random"))
+    # 3-fold by knight shuffle Nf3 Nf6 Ng1 Ng8 (x2) + Nf3, then steps after done
+    sq = lambda s: (8 - int(s[1])) * 8 + "abcdefgh".index(s[0])  # noqa: E731
+    mv = lambda a, b: sq(a) * 64 + sq(b)  # noqa: E731
+    shuffle = [mv("g1", "f3"), mv("g8", "f6"), mv("f3", "g1"), mv("f6", "g8")] * 2 + [mv("g1", "f3")]
+    traces.append(trace_scripted(v2, shuffle + [mv("g8", "f6"), mv("e2", "e4"), 0]))
+    # king capture / kingless continuation (Q6/Q7): white king a5 checked by rook a1 retreats to a6
+    b = np.zeros((8, 8), dtype=np.int8)
+    b[3, 0] = 1      # Ka5
+    b[7, 0] = -3     # ra1
+    b[0, 7] = -1     # kh8
+    b[6, 7] = 6      # Ph2
+    traces.append(trace_env(v2, 2300, 200, "none", initial_board=b))
+    return traces
+
+
+def dump(name, obj, gz=False):
+    path = os.path.join(HERE, name)
+    data = json.dumps(obj, separators=(",", ":")).encode()
+    if gz:
+        with gzip.open(path, "wb", compresslevel=9) as f:
+            f.write(data)
+    else:
+        with open(path, "wb") as f:
+            f.write(data)
+    print("wrote", path, os.path.getsize(path), "bytes", flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--deep", action="store_true", help="also v1 perft(5) (~4 min on 8 cores)")
+    ap.add_argument("--games", type=int, default=10)
+    args = ap.parse_args()
+    v1, v2 = load_reference()
+    dump("perft_startpos.json", gen_perft_startpos(v1, args.deep))
+    games, mid = gen_v1_games(v1, args.games, 320)
+    dump("v1_games.json.gz", games, gz=True)
+    dump("v1_perft_midgame.json", gen_v1_perft_midgame(v1, mid[:12], 3))
+    dump("v2_known_answers.json", gen_v2_known_answers())
+    dump("v2_env_traces.json.gz", gen_env_traces(v2), gz=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,305 @@
+"""GPU parity: the HIP kernels (through the C-ABI) vs the oracle and the golden fixtures.
+
+Bar: bit-exact (integer work) -- ordered move lists, next states, rewards, check flags,
+perft counts, step() rewards/done/reasons and whole random-self-play trajectories.
+"""
+import numpy as np
+import pytest
+
+from conftest import load_golden, random_positions
+
+pytestmark = pytest.mark.gpu
+
+
+def _text_board(t):
+    from gym_chess_amd import codec as C
+
+    return C.text_to_board(t)
+
+
+# ------------------------------------------------------------------ engine: move lists
+def test_v1_games_ordered_lists(engine):
+    """1888 positions along seeded v1 reference games (D4-transformed, D-filtered)."""
+    games = load_golden("v1_games.json.gz")
+    plies = [p for g in games for p in g["plies"]]
+    b = np.stack([_text_board(p["board"]) for p in plies])
+    m = np.zeros((len(plies), 8), dtype=np.uint8)
+    m[:, 0] = [p["white"] for p in plies]
+    m[:, 1:5] = [p["rights"] for p in plies]
+    out, cnt = engine.possible_moves(b, m, m[:, 0])
+    for i, p in enumerate(plies):
+        assert [int(x) for x in out[i, : cnt[i]]] == p["moves"], f"ply {i}"
+    # next boards and rewards of the chosen actions
+    acts = np.array([p["action"] for p in plies], dtype=np.uint16)
+    nb, nm, rw, st = engine.next_state(b, m, m[:, 0], acts)
+    assert (st == 0).all()
+    for i, p in enumerate(plies):
+        assert (nb[i] == _text_board(p["next_board"])).all(), f"ply {i}"
+        assert rw[i] == p["reward"]
+
+
+def test_v2_known_answers(engine):
+    """Every engine call the reference's own v2 tests made (their asserts passed)."""
+    cases = load_golden("v2_known_answers.json")
+    n = 0
+    for case in cases:
+        for c in case["calls"]:
+            b = _text_board(c["board"])[None]
+            m = np.zeros((1, 8), dtype=np.uint8)
+            m[0, :5] = c["meta"]
+            if c["op"] == "get_possible_moves":
+                out, cnt = engine.possible_moves(b, m, c["white"], attack=c["attack"])
+                assert [int(x) for x in out[0, : cnt[0]]] == c["out"], (case["test"], c)
+            elif c["op"] == "get_castle_moves":
+                out, cnt = engine.castle_moves(b, m, c["white"])
+                assert [int(x) for x in out[0, : cnt[0]]] == c["out"], case["test"]
+            elif c["op"] == "update_state":
+                ob, om = engine.update_state(b, m)
+                assert list(om[0, :7]) == c["out_meta"], case["test"]
+            elif c["op"] == "next_state":
+                ob, om, rw, st = engine.next_state(b, m, c["white"], c["action"])
+                assert (ob[0] == _text_board(c["out_board"])).all()
+                assert list(om[0, :7]) == c["out_meta"] and rw[0] == c["reward"]
+                assert bool(st[0] == 1) == c["both_checked"]
+            n += 1
+    assert n >= 60
+
+
+@pytest.mark.parametrize("seed", [11, 12, 13])
+def test_random_positions_vs_oracle(engine, oracle, seed):
+    """Fuzz: legal + attack-mode lists, castle lists, update_state, next_state of every
+    legal move and of arbitrary (also illegal / wrong-player) moves."""
+    boards, metas = random_positions(400, seed)
+    for attack in (False, True):
+        for white in (0, 1):
+            out, cnt = engine.possible_moves(boards, metas, white, attack=attack)
+            for i in range(len(boards)):
+                ref = oracle.get_possible_moves(boards[i], metas[i], white, attack)
+                assert [int(x) for x in out[i, : cnt[i]]] == ref, (i, attack, white)
+    cm, cc = engine.castle_moves(boards, metas, metas[:, 0])
+    ob, om = engine.update_state(boards, metas)
+    rng = np.random.RandomState(seed)
+    acts = np.zeros(len(boards), dtype=np.uint16)
+    players = rng.randint(2, size=len(boards)).astype(np.uint8)
+    for i in range(len(boards)):
+        assert [int(x) for x in cm[i, : cc[i]]] == oracle.get_castle_moves(boards[i], metas[i], metas[i, 0])
+        rb, rm = oracle.update_state(boards[i], metas[i])
+        assert (ob[i] == rb).all() and list(om[i, :7]) == list(rm[:7]), i
+        occupied = np.nonzero(boards[i])[0]
+        if rng.rand() < 0.2:
+            acts[i] = 4096 + rng.randint(4)
+        else:
+            acts[i] = int(rng.choice(occupied)) * 64 + rng.randint(64)
+    nb, nm, rw, st = engine.next_state(boards, metas, players, acts)
+    for i in range(len(boards)):
+        rc, rb, rm, rr = oracle.next_state(boards[i], metas[i], players[i], int(acts[i]))
+        assert st[i] == rc, i
+        if rc in (0, 1):
+            assert (nb[i] == rb).all() and list(nm[i, :7]) == list(rm[:7]) and rw[i] == rr, i
+
+
+def test_next_state_every_legal_move(engine, oracle):
+    boards, metas = random_positions(150, 21)
+    B, M, P, A = [], [], [], []
+    for i in range(len(boards)):
+        w = int(metas[i, 0])
+        for a in oracle.get_possible_moves(boards[i], metas[i], w):
+            B.append(boards[i]); M.append(metas[i]); P.append(w); A.append(a)
+    B, M = np.stack(B), np.stack(M)
+    nb, nm, rw, st = engine.next_state(B, M, np.array(P, np.uint8), np.array(A, np.uint16))
+    for k in range(len(A)):
+        rc, rb, rm, rr = oracle.next_state(B[k], M[k], P[k], A[k])
+        assert st[k] == rc and (nb[k] == rb).all() and list(nm[k, :7]) == list(rm[:7]) and rw[k] == rr, k
+
+
+def test_empty_from_square_status(engine):
+    b = np.zeros((1, 64), dtype=np.int8)
+    b[0, 60] = 1
+    m = np.zeros((1, 8), dtype=np.uint8)
+    _, _, _, st = engine.next_state(b, m, 1, 36 * 64 + 28)
+    assert st[0] == -1  # the reference panics: "Bad move - piece is empty !"
+
+
+# ------------------------------------------------------------------ perft
+def test_perft_startpos_4096_boards(engine):
+    """BASELINE configs[1]: 4 096 startpos boards, perft(3) = 8 982 each (reference rules)."""
+    from oracle import DEFAULT_BOARD, make_meta
+
+    b = np.tile(DEFAULT_BOARD, (4096, 1))
+    m = np.tile(make_meta(), (4096, 1))
+    assert (engine.perft(b, m, 3) == 8982).all()
+    golden = load_golden("perft_startpos.json")["perft"]
+    got = [int(engine.perft(b[:1], m[:1], d)[0]) for d in range(1, 6)]
+    assert got == [golden[str(d)] for d in range(1, 6)] == [20, 400, 8982, 200915, 5018995]
+
+
+def test_perft_midgame_vs_v1(engine, oracle):
+    for p in load_golden("v1_perft_midgame.json"):
+        b = _text_board(p["board"])[None]
+        m = np.zeros((1, 8), dtype=np.uint8)
+        m[0, :5] = p["meta"]
+        for d, v in p["v1_perft"].items():
+            got = int(engine.perft(b, m, int(d))[0])
+            if p["v1_equals_v2"]:
+                assert got == v
+            assert got == oracle.perft(b[0], m[0], int(d))
+
+
+def test_perft_random_positions(engine, oracle):
+    boards, metas = random_positions(48, 31)
+    for d in (1, 2, 3):
+        got = engine.perft(boards, metas, d)
+        ref = oracle.perft_batch(boards, metas, d, threads=8)
+        assert (got == ref).all(), d
+
+
+# ------------------------------------------------------------------ env
+def _replay_trace(env, oracle_env, steps):
+    """Drive the batched env (1 board) with the recorded actions; compare to the golden."""
+    from gym_chess_amd import codec as C
+
+    for s in steps:
+        if s["kind"] == "reset":
+            env.reset()
+            continue
+        rw, dn, why = env.step([s["action"]])
+        if s["kind"] == "error":
+            assert why[0] == 5
+            env.reset()
+            continue
+        assert rw[0] == s["reward"] and bool(dn[0]) == s["done"], s
+        b, m = env.boards()
+        assert C.board_to_text(b[0]) == s["board"]
+        if "meta" in s:
+            assert list(m[0, :7]) == s["meta"]
+        assert m[0, 7] == s["move_count"]
+        _, cnt = env.legal_moves()
+        assert cnt[0] == s["n_moves"]
+
+
+def test_env_traces_of_reference_env():
+    """step() traces of the reference's ChessEnvV2 (opponent none; invalid actions; 3-fold;
+    king capture / kingless play) replayed through gc_env_step."""
+    from gym_chess_amd import codec as C
+    from gym_chess_amd.env import BatchedChessEnv
+
+    for t in load_golden("v2_env_traces.json.gz"):
+        if t.get("opponent") == "random":
+            continue
+        ib = None if t["initial_board"] is None else C.text_to_board(t["initial_board"])
+        env = BatchedChessEnv(1, device=0, seed=1, initial_board=ib)
+        _replay_trace(env, None, t["steps"])
+
+
+def test_env_batch_step_vs_oracle_env(oracle):
+    """Many boards stepped in lockstep with external actions (valid and invalid)."""
+    from gym_chess_amd.env import BatchedChessEnv
+
+    n = 64
+    env = BatchedChessEnv(n, device=0, seed=3)
+    refs = [oracle.OracleEnv() for _ in range(n)]
+    rng = np.random.RandomState(5)
+    for ply in range(260):
+        acts = np.zeros(n, dtype=np.int64)
+        for i, r in enumerate(refs):
+            mv = r.moves()
+            if not mv or rng.rand() < 0.05:
+                acts[i] = rng.randint(0, 4101)
+            else:
+                acts[i] = mv[rng.randint(len(mv))]
+        rw, dn, why = env.step(acts)
+        for i, r in enumerate(refs):
+            rc, rr, rd, rq = r.step(int(acts[i]))
+            if rc == 1:
+                assert why[i] == 5
+            else:
+                assert rw[i] == rr and bool(dn[i]) == bool(rd), (ply, i)
+        b, m = env.boards()
+        for i, r in enumerate(refs):
+            rb, rm = r.state()
+            assert (b[i] == rb).all() and list(m[i]) == list(rm), (ply, i)
+            if dn[i] or why[i] == 5:
+                r.reset()
+        resets = np.array([bool(dn[i]) or why[i] == 5 for i in range(n)], dtype=np.uint8)
+        if resets.any():
+            env.reset(resets)
+
+
+@pytest.mark.parametrize("plies", [700])
+def test_rollout_trajectories_vs_oracle(oracle, plies):
+    """Fused rollout kernel: whole random self-play trajectories (incl. 3-fold, mate, move
+    cap, no-move resets, king captures) bit-exact vs the oracle driver."""
+    from gym_chess_amd.env import BatchedChessEnv
+
+    n = 256
+    env = BatchedChessEnv(n, device=0, seed=0xABCD)
+    st, tr = env.rollout(plies, trace=True)
+    ref_stats = np.zeros(8, dtype=np.uint64)
+    for i in range(n):
+        ref = oracle.rollout_trace(0xABCD, i, plies)
+        for k in ("action", "reward", "done", "reason"):
+            assert (tr[k][:, i] == ref[k]).all(), (i, k, np.nonzero(tr[k][:, i] != ref[k])[0][:3])
+        ref_stats += ref["stats"]
+    assert (st == ref_stats).all()
+    b, m = env.boards()
+
+
+def test_step_random_matches_fused_rollout():
+    """The one-ply step kernel (bench path) and the fused rollout kernel are the same driver."""
+    from gym_chess_amd.env import BatchedChessEnv
+
+    n, plies = 512, 400
+    a = BatchedChessEnv(n, device=0, seed=99)
+    bq = BatchedChessEnv(n, device=0, seed=99)
+    a.step_random(plies)
+    bq.rollout(plies)
+    ba, ma = a.boards()
+    bb, mb = bq.boards()
+    assert (ba == bb).all() and (ma == mb).all()
+    oa, ob = a.outputs(), bq.outputs()
+    assert (oa["next_action"] == ob["next_action"]).all() and (oa["nsteps"] == ob["nsteps"]).all()
+
+
+def test_step_random_vs_oracle_final_state(oracle):
+    from gym_chess_amd.env import BatchedChessEnv
+
+    n, plies = 128, 333
+    env = BatchedChessEnv(n, device=0, seed=4242)
+    env.step_random(plies)
+    b, m = env.boards()
+    for i in range(n):
+        ref = oracle.rollout_trace(4242, i, plies)
+        assert (b[i] == ref["final_board"]).all() and list(m[i]) == list(ref["final_meta"]), i
+
+
+def test_legal_mask_matches_list():
+    from gym_chess_amd.env import BatchedChessEnv
+
+    env = BatchedChessEnv(256, device=0, seed=8)
+    env.step_random(57)
+    mask = env.legal_mask()
+    acts = env.possible_actions()
+    for i in range(256):
+        assert sorted(np.nonzero(mask[i])[0].tolist()) == sorted(acts[i])
+
+
+def test_chess_engine_compat_dict_api(oracle):
+    """The drop-in ChessEngine: same dict/str protocol as lib.rs."""
+    from gym_chess_amd import codec as C
+    from gym_chess_amd.engine import ChessEngine
+
+    eng = ChessEngine()
+    state = dict(board=C.DEFAULT_BOARD, current_player="WHITE", white_king_castle_is_possible=True,
+                 white_queen_castle_is_possible=True, black_king_castle_is_possible=True,
+                 black_queen_castle_is_possible=True)
+    st = eng.update_state(state)
+    assert st["white_king_is_checked"] is False and st["board"] == C.DEFAULT_BOARD
+    moves = eng.get_possible_moves(st, "WHITE")
+    assert moves[:4] == ["a2a3", "a2a4", "b2b3", "b2b4"] and len(moves) == 20
+    ns, rw = eng.next_state(st, "WHITE", "e2e4")
+    assert ns["current_player"] == "BLACK" and rw == 0 and ns["board"][4][4] == 6
+    with pytest.raises(SystemError):
+        eng.get_possible_moves(st, "RED")
+    with pytest.raises(KeyError):
+        eng.get_possible_moves({"board": C.DEFAULT_BOARD}, "WHITE")
+    assert eng.get_castle_moves(st, "WHITE") == []

@@ -1,0 +1,30 @@
+#!/bin/bash
+# One gpurun session: each GPU step under its own timeout; stop at the first fault,
+# abort, segfault, timeout or hang (any exit code other than 0 / 1 = test failure).
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
+export TMPDIR=/tmp
+OUT=gpurun_out
+mkdir -p $OUT
+: > $OUT/steps.log
+step() {
+  local name=$1 secs=$2; shift 2
+  echo "[$(date +%T)] start $name" >> $OUT/steps.log
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "[$(date +%T)] $name rc=$rc" >> $OUT/steps.log
+  tail -5 "$OUT/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP after $name rc=$rc"; exit $rc; fi
+}
+for s in ${STEPS:-smoke pytest bench prof}; do
+  case $s in
+    smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    pytest) step pytest 1200 python -m pytest tests -x -q -m gpu ;;
+    bench)  step bench 600 python bench.py ${BENCH_ARGS:-} ;;
+    prof)   step prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 100 --warmup 20 ;;
+    pmcf)   step pmcf 600 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 20 --warmup 20 --fused-plies 0 ;;
+    pmcw)   step pmcw 600 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 20 --warmup 20 --fused-plies 0 ;;
+    pmcv)   step pmcv 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES -d $OUT/pmc_valu -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 20 --warmup 20 --fused-plies 0 ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo ALLDONE
