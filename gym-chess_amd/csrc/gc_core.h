@@ -17,8 +17,10 @@
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
 #define GC_HD __host__ __device__ __forceinline__
+#define GC_HDM __host__ __device__ __forceinline__
 #else
 #define GC_HD static inline
+#define GC_HDM inline
 #endif
 
 namespace gc {
@@ -253,14 +255,16 @@ struct Gen {
     int ks;         // tracked king square or -1 (no legality filter)
     u32 castles;    // bit0 = queen side, bit1 = king side (reference order QS, KS)
     bool white;
+    bool in_check;  // tracked king in the enemy attack map (_king_is_checked, lib.rs:634-667)
 };
 
 // Legality: the reference filters every non-king move by next_state + a full enemy
 // attack-map recompute + "is my (tracked) king in it" (lib.rs:561, 612-632).  For
 // en-passant-free rules that is exactly "target in checkmask AND (not pinned OR on the
 // pin segment king..pinner)".  The segment, not the whole line: a pinned pawn's double
-// push jumps blockers (Q1) and can land beyond its pinner or beyond its own king.  King moves are filtered by the pre-move enemy map instead (lib.rs:613-619,
-// 1125-1128), which keeps the Q6 retreat-along-the-ray quirk.
+// push jumps blockers (Q1) and can land beyond its pinner or beyond its own king.  King
+// moves are filtered by the pre-move enemy map instead (lib.rs:613-619, 1125-1128), which
+// keeps the Q6 retreat-along-the-ray quirk.
 GC_HD void gen_init(const Pos& s, Gen& g) {
     bool white = s.meta & M_WHITE;
     g.white = white;
@@ -273,6 +277,7 @@ GC_HD void gen_init(const Pos& s, Gen& g) {
     g.pinrays = 0;
     g.enemy_att = 0;
     g.castles = 0;
+    g.in_check = false;
     if (g.ks < 0) return;  // "King not present": no filter, no castling, no king moves
     int ks = g.ks;
     u64 kb = bit(ks);
@@ -280,6 +285,7 @@ GC_HD void gen_init(const Pos& s, Gen& g) {
     u64 rq = (s.r | s.q) & opp, bq = (s.b | s.q) & opp;
     u64 checkers = (pawn_att_set(kb, white) & s.p & opp) | (knight_set(kb) & s.n & opp) |
                    (king_set(kb) & s.k & opp) | (rook_att(ks, g.occ) & rq) | (bishop_att(ks, g.occ) & bq);
+    g.in_check = checkers != 0;
     if (checkers) {
         if (checkers & (checkers - 1)) g.checkmask = 0;
         else g.checkmask = checkers | between(ks, ctz(checkers));
@@ -378,31 +384,32 @@ GC_HD int kth_bit_asc(u64 x, int k) {
 GC_HD int ray_pick(u64 tg, int sq, u64 fm, u64 rm, u64 dm, u64 am, bool rook, bool bish, int& k) {
     // outward from sq: rays toward lower indices are walked high->low ("desc")
     u64 below = bit(sq) - 1, above = ~below & ~bit(sq);
-    u64 grp[8];
-    bool desc[8];
-    int n = 0;
+#define GC_RAY(G, DESC)                                                      \
+    {                                                                        \
+        u64 gg = (G);                                                        \
+        int c = popc(gg);                                                    \
+        if (k < c) return DESC ? kth_bit_desc(gg, k) : kth_bit_asc(gg, k);  \
+        k -= c;                                                              \
+    }
     if (rook) {
-        grp[n] = tg & fm & below; desc[n++] = true;   // (-1, 0)
-        grp[n] = tg & fm & above; desc[n++] = false;  // (+1, 0)
-        grp[n] = tg & rm & below; desc[n++] = true;   // (0, -1)
-        grp[n] = tg & rm & above; desc[n++] = false;  // (0, +1)
+        GC_RAY(tg & fm & below, true)   // (-1, 0)
+        GC_RAY(tg & fm & above, false)  // (+1, 0)
+        GC_RAY(tg & rm & below, true)   // (0, -1)
+        GC_RAY(tg & rm & above, false)  // (0, +1)
     }
     if (bish) {
-        grp[n] = tg & dm & below; desc[n++] = true;   // (-1, -1)
-        grp[n] = tg & am & below; desc[n++] = true;   // (-1, +1)
-        grp[n] = tg & am & above; desc[n++] = false;  // (+1, -1)
-        grp[n] = tg & dm & above; desc[n++] = false;  // (+1, +1)
+        GC_RAY(tg & dm & below, true)   // (-1, -1)
+        GC_RAY(tg & am & below, true)   // (-1, +1)
+        GC_RAY(tg & am & above, false)  // (+1, -1)
+        GC_RAY(tg & dm & above, false)  // (+1, +1)
     }
-    for (int i = 0; i < n; i++) {
-        int c = popc(grp[i]);
-        if (k < c) return desc[i] ? kth_bit_desc(grp[i], k) : kth_bit_asc(grp[i], k);
-        k -= c;
-    }
+#undef GC_RAY
     return -1;
 }
-GC_HD int offset_pick(u64 tg, int sq, const signed char* offs, int k) {
+// offsets packed as 8 signed bytes (no per-lane arrays -> no scratch memory)
+GC_HD int offset_pick(u64 tg, int sq, u64 packed, int k) {
     for (int i = 0; i < 8; i++) {
-        int t = sq + offs[i];
+        int t = sq + (int)(signed char)(packed >> (8 * i));
         if (t >= 0 && t < 64 && (tg >> t) & 1) {
             if (k == 0) return t;
             k--;
@@ -410,15 +417,16 @@ GC_HD int offset_pick(u64 tg, int sq, const signed char* offs, int k) {
     }
     return -1;
 }
+GC_HD u64 pack8(int a, int b, int c, int d, int e, int f, int g, int h) {
+    return (u64)(uint8_t)a | (u64)(uint8_t)b << 8 | (u64)(uint8_t)c << 16 | (u64)(uint8_t)d << 24 |
+           (u64)(uint8_t)e << 32 | (u64)(uint8_t)f << 40 | (u64)(uint8_t)g << 48 | (u64)(uint8_t)h << 56;
+}
 GC_HD int kth_target(u64 tg, int sq, int t, bool white, int k) {
-    const signed char KO[8] = {8, -8, 1, -1, 9, 7, -7, -9};
-    const signed char NO[8] = {-17, -15, 15, 17, -10, -6, 6, 10};
-    const signed char PW[8] = {-8, -16, -7, -9, 99, 99, 99, 99};
-    const signed char PB[8] = {8, 16, 9, 7, 99, 99, 99, 99};
     switch (t) {
-        case KING: return offset_pick(tg, sq, KO, k);
-        case KNIGHT: return offset_pick(tg, sq, NO, k);
-        case PAWN: return offset_pick(tg, sq, white ? PW : PB, k);
+        case KING: return offset_pick(tg, sq, pack8(8, -8, 1, -1, 9, 7, -7, -9), k);
+        case KNIGHT: return offset_pick(tg, sq, pack8(-17, -15, 15, 17, -10, -6, 6, 10), k);
+        case PAWN: return offset_pick(tg, sq, white ? pack8(-8, -16, -7, -9, 99, 99, 99, 99)
+                                                    : pack8(8, 16, 9, 7, 99, 99, 99, 99), k);
         default: {
             bool rook = (t == ROOK || t == QUEEN), bish = (t == BISHOP || t == QUEEN);
             return ray_pick(tg, sq, file_mask(sq), row_mask(sq), diag_mask(sq), anti_mask(sq), rook, bish, k);
@@ -449,6 +457,156 @@ GC_HD int select_legal(const Pos& s, const Gen& g, int k) {
         int c = popc(tg);
         if (k < c) return sq * 64 + kth_target(tg, sq, t, g.white, k);
         k -= c;
+    }
+    if (g.castles & 1) { if (k == 0) return g.white ? A_QSW : A_QSB; k--; }
+    if (g.castles & 2) { if (k == 0) return g.white ? A_KSW : A_KSB; }
+    return A_NONE;
+}
+
+// ---- type-uniform generation (the hot path) -------------------------------------------
+// Lanes of a wave hold different boards, so a per-square loop that dispatches on the piece
+// type serialises every type's code on every iteration.  Here each loop handles ONE piece
+// type (lanes differ only in trip count) and pawns are done set-wise.  The targets of every
+// other piece are parked in a per-lane scratch slot (LDS on the device) under the piece's
+// ordinal among the side's pieces -- its position in the reference's row-major scan
+// (lib.rs:510-511) -- so the ordered pick reads them back instead of regenerating them.
+static constexpr int SCRATCH_SLOTS = 16;
+static constexpr u64 ROW1 = 0xFFull << 8;   // black pawns' start row (lib.rs:947)
+static constexpr u64 ROW6 = 0xFFull << 48;  // white pawns' start row (lib.rs:946)
+
+struct MoveSet {
+    u64 fastp;            // own pawns handled set-wise (the unpinned ones)
+    u64 o1, o2, ol, orr;  // fast pawns with: single push, double push, capture c+1, capture c-1
+    int total;            // legal move count including castles
+    bool big;             // more own pieces than scratch slots: per-square fallback
+};
+
+struct NoScratch {  // count-only callers (perft leaves)
+    GC_HDM void put(int, u64) {}
+    GC_HDM u64 get(int) const { return 0; }
+};
+
+GC_HD int ordinal(u64 own, int sq) { return popc(own & (bit(sq) - 1)); }
+
+template <class S>
+GC_HD void gen_moves(const Pos& s, const Gen& g, MoveSet& ms, S& scr) {
+    ms.fastp = ms.o1 = ms.o2 = ms.ol = ms.orr = 0;
+    ms.big = popc(g.own) > SCRATCH_SLOTS;
+    if (ms.big) {
+        ms.total = count_legal(s, g);
+        return;
+    }
+    const u64 own = g.own, cm = g.checkmask, notown_cm = ~own & cm;
+    int total = popc(g.castles);
+    // pawns, set-wise (lib.rs:935-958; Q1: the double push tests only the destination)
+    u64 P = s.p & own, fp = P & ~g.pinned, empty = ~g.occ;
+    if (g.white) {
+        ms.o1 = ((fp >> 8) & empty & cm) << 8;
+        ms.o2 = (((fp & ROW6) >> 16) & empty & cm) << 16;
+        ms.ol = (((fp >> 7) & ~FILE_A) & g.opp & cm) << 7;
+        ms.orr = (((fp >> 9) & ~FILE_H) & g.opp & cm) << 9;
+    } else {
+        ms.o1 = ((fp << 8) & empty & cm) >> 8;
+        ms.o2 = (((fp & ROW1) << 16) & empty & cm) >> 16;
+        ms.ol = (((fp << 9) & ~FILE_A) & g.opp & cm) >> 9;
+        ms.orr = (((fp << 7) & ~FILE_H) & g.opp & cm) >> 7;
+    }
+    ms.fastp = fp;
+    total += popc(ms.o1) + popc(ms.o2) + popc(ms.ol) + popc(ms.orr);
+    u64 pp = P & g.pinned;  // pinned pawns: rare, per piece
+    while (pp) {
+        int sq = ctz(pp);
+        pp &= pp - 1;
+        u64 tg = legal_targets(s, g, sq, PAWN);
+        scr.put(ordinal(own, sq), tg);
+        total += popc(tg);
+    }
+    u64 x = s.n & own;  // a pinned knight never has a move on its pin segment
+    while (x) {
+        int sq = ctz(x);
+        x &= x - 1;
+        u64 tg = ((g.pinned >> sq) & 1) ? 0 : knight_set(bit(sq)) & notown_cm;
+        scr.put(ordinal(own, sq), tg);
+        total += popc(tg);
+    }
+    x = s.b & own;
+    while (x) {
+        int sq = ctz(x);
+        x &= x - 1;
+        u64 tg = bishop_att(sq, g.occ) & notown_cm;
+        if ((g.pinned >> sq) & 1) tg &= g.pinrays & line_through(g.ks, sq);
+        scr.put(ordinal(own, sq), tg);
+        total += popc(tg);
+    }
+    x = s.r & own;
+    while (x) {
+        int sq = ctz(x);
+        x &= x - 1;
+        u64 tg = rook_att(sq, g.occ) & notown_cm;
+        if ((g.pinned >> sq) & 1) tg &= g.pinrays & line_through(g.ks, sq);
+        scr.put(ordinal(own, sq), tg);
+        total += popc(tg);
+    }
+    x = s.q & own;
+    while (x) {
+        int sq = ctz(x);
+        x &= x - 1;
+        u64 tg = (rook_att(sq, g.occ) | bishop_att(sq, g.occ)) & notown_cm;
+        if ((g.pinned >> sq) & 1) tg &= g.pinrays & line_through(g.ks, sq);
+        scr.put(ordinal(own, sq), tg);
+        total += popc(tg);
+    }
+    x = s.k & own;  // every own king; filtered by the pre-move enemy map only (lib.rs:613-619)
+    while (x) {
+        int sq = ctz(x);
+        x &= x - 1;
+        u64 tg = king_set(bit(sq)) & ~own & ~g.enemy_att;
+        scr.put(ordinal(own, sq), tg);
+        total += popc(tg);
+    }
+    ms.total = total;
+}
+
+// k-th legal action (0 <= k < ms.total) in reference order, from gen_moves' results
+template <class S>
+GC_HD int select_move(const Pos& s, const Gen& g, const MoveSet& ms, const S& scr, int k) {
+    if (ms.big) return select_legal(s, g, k);
+    u64 t[SCRATCH_SLOTS];
+#pragma unroll
+    for (int j = 0; j < SCRATCH_SLOTS; j++) t[j] = scr.get(j);  // all reads in flight at once
+    u64 pcs = g.own;
+    int res = -1, rsq = 0, rk = 0;
+    u64 rtg = 0;
+    bool pawn = false;
+#pragma unroll
+    for (int j = 0; j < SCRATCH_SLOTS; j++) {  // single-exit, fully unrolled scan in square order
+        if (pcs && res < 0) {
+            int sq = ctz(pcs);
+            pcs &= pcs - 1;
+            bool fast = (ms.fastp >> sq) & 1;
+            int c = fast ? (int)(((ms.o1 >> sq) & 1) + ((ms.o2 >> sq) & 1) + ((ms.ol >> sq) & 1) + ((ms.orr >> sq) & 1))
+                         : popc(t[j]);
+            if (k < c) {
+                res = j;
+                rsq = sq;
+                rk = k;
+                rtg = t[j];
+                pawn = fast;
+            } else {
+                k -= c;
+            }
+        }
+    }
+    if (res >= 0) {
+        int sq = rsq;
+        k = rk;
+        if (pawn) {  // one, two, (r-p,c+1), (r-p,c-1)  (lib.rs:921-958)
+            if ((ms.o1 >> sq) & 1) { if (k == 0) return sq * 64 + (g.white ? sq - 8 : sq + 8); k--; }
+            if ((ms.o2 >> sq) & 1) { if (k == 0) return sq * 64 + (g.white ? sq - 16 : sq + 16); k--; }
+            if ((ms.ol >> sq) & 1) { if (k == 0) return sq * 64 + (g.white ? sq - 7 : sq + 9); k--; }
+            return sq * 64 + (g.white ? sq - 9 : sq + 7);
+        }
+        return sq * 64 + kth_target(rtg, sq, type_at(s, sq), g.white, k);
     }
     if (g.castles & 1) { if (k == 0) return g.white ? A_QSW : A_QSB; k--; }
     if (g.castles & 2) { if (k == 0) return g.white ? A_KSW : A_KSB; }
@@ -538,9 +696,10 @@ GC_HD u64 mix64(u64 x) {
     return x;
 }
 GC_HD u32 board_key(const Pos& s) {
-    u64 h = mix64(s.k ^ 0x9E3779B97F4A7C15ull) ^ mix64(s.q + 0x632BE59BD9B4E019ull) ^
-            mix64(s.r ^ 0x85157AF5ull) ^ mix64(s.b + 0xD6E8FEB86659FD93ull) ^
-            mix64(s.n ^ 0xA0761D6478BD642Full) ^ mix64(s.p + 0xE7037ED1A0B428DBull) ^ mix64(s.w ^ 0x8EBC6AF09C88C6E3ull);
+    u64 h = s.k * 0x9E3779B97F4A7C15ull + s.q * 0xC2B2AE3D27D4EB4Full + s.r * 0x165667B19E3779F9ull +
+            s.b * 0xD6E8FEB86659FD93ull + s.n * 0xA0761D6478BD642Full + s.p * 0xE7037ED1A0B428DBull +
+            s.w * 0x8EBC6AF09C88C6E3ull;
+    h = mix64(h);
     return (u32)(h ^ (h >> 32));
 }
 

@@ -3,8 +3,9 @@
 // One lane = one board.  Board state lives in HBM as structure-of-arrays: bitboard j of
 // board i at bb[j*N + i] (j = K,Q,R,B,N,P,W), meta[i], so every wave's loads and stores
 // of one field are 512 contiguous bytes.  All move generation is register-resident
-// integer/bitwise work (gc_core.h); the only other HBM traffic is the 3-fold repetition
-// window hkey[slot*N + i] (u32) + hboard[(slot*7 + j)*N + i] (read only on key hits).
+// integer/bitwise work (gc_core.h), with per-piece move targets parked in LDS for the
+// ordered policy pick; the only other HBM traffic is the 3-fold repetition window
+// (gc_env.h): one or two probes of a per-board hash table + a board compare on tag hits.
 //
 // The C-ABI replaces the reference's FFI (the PyO3 ChessEngine, lib.rs:1412-1512) for the
 // engine calls, plus a device-resident batched env for chess_v2.py's reset()/step().
@@ -67,23 +68,41 @@ struct SoA {
     }
 };
 
-struct DevHist {  // repetition window of board i
-    u32* hkey;
+// repetition window of board i (gc_env.h rep_count): table [HTAB][N] u64, window boards
+// [HIST_CAP][7][N] u64, occurrence counts [HIST_CAP][N] u8, generation [N] u32
+struct DevHist {
+    u64* htab;
     u64* hboard;
+    uint8_t* hcnt;
+    u32* hgen;
+    u32 g;
     int n, i;
-    __device__ u32 key(int slot) const { return hkey[(size_t)slot * n + i]; }
+    __device__ u32 gen() const { return g; }
+    __device__ void bump_gen() { g++; hgen[i] = g; }
+    __device__ u64 tab(int pos) const { return htab[(size_t)pos * n + i]; }
+    __device__ void set_tab(int pos, u64 v) { htab[(size_t)pos * n + i] = v; }
     __device__ bool same(int slot, const Pos& s) const {
         const u64* h = hboard + (size_t)slot * NBB * n + i;
         return h[0] == s.k && h[(size_t)n] == s.q && h[2 * (size_t)n] == s.r && h[3 * (size_t)n] == s.b &&
                h[4 * (size_t)n] == s.n && h[5 * (size_t)n] == s.p && h[6 * (size_t)n] == s.w;
     }
-    __device__ void put(int slot, u32 k, const Pos& s) const {
-        hkey[(size_t)slot * n + i] = k;
+    __device__ void put(int slot, const Pos& s) {
         u64* h = hboard + (size_t)slot * NBB * n + i;
         h[0] = s.k; h[(size_t)n] = s.q; h[2 * (size_t)n] = s.r; h[3 * (size_t)n] = s.b;
         h[4 * (size_t)n] = s.n; h[5 * (size_t)n] = s.p; h[6 * (size_t)n] = s.w;
     }
+    __device__ int cnt(int slot) const { return hcnt[(size_t)slot * n + i]; }
+    __device__ void set_cnt(int slot, int c) { hcnt[(size_t)slot * n + i] = (uint8_t)c; }
 };
+
+// per-lane move-target scratch in LDS: slot j of lane t at lds[j*BLOCK + t] (each wave's
+// ds_read_b64/ds_write_b64 touches 512 contiguous bytes: conflict-free)
+struct LdsScratch {
+    u64* base;
+    __device__ void put(int j, u64 v) { base[j * BLOCK] = v; }
+    __device__ u64 get(int j) const { return base[j * BLOCK]; }
+};
+#define LDS_SCRATCH_DECL __shared__ u64 lds_scr[SCRATCH_SLOTS * BLOCK]; LdsScratch scr{lds_scr + threadIdx.x}
 
 // ----------------------------------------------------------------------------- engine kernels
 // import: mailbox int8[64] + meta8 {side, wkc, wqc, bkc, bqc, ...} -> bitboards, with the
@@ -224,7 +243,12 @@ __device__ uint64_t perft_lane(const Pos& root, int depth) {
     int top = 0;
     st[0].s = root;
     gen_init(st[0].s, st[0].g);
-    if (depth == 1) return (uint64_t)count_legal(st[0].s, st[0].g);
+    NoScratch ns;
+    MoveSet ms;
+    if (depth == 1) {
+        gen_moves(st[0].s, st[0].g, ms, ns);
+        return (uint64_t)ms.total;
+    }
     st[0].pcs = st[0].g.own;
     st[0].tg = 0;
     st[0].sq = -1;
@@ -254,7 +278,8 @@ __device__ uint64_t perft_lane(const Pos& root, int depth) {
         if (remaining == 1) {
             Gen g;
             gen_init(c, g);
-            nodes += (uint64_t)count_legal(c, g);
+            gen_moves(c, g, ms, ns);
+            nodes += (uint64_t)ms.total;
         } else {
             Frame& nf = st[top + 1];
             nf.s = c;
@@ -324,17 +349,20 @@ __global__ void k_sum_tasks(const int32_t* __restrict__ offs, const int32_t* __r
 // ----------------------------------------------------------------------------- env kernels
 struct EnvDev {
     SoA st;
-    u32* hkey;
+    u64* htab;
     u64* hboard;
+    uint8_t* hcnt;
+    u32* hgen;
     u32* draw;       // policy draws per board (Philox counter)
     uint16_t* act;   // next action per board (A_NONE = no legal move)
     int32_t* reward;
     uint8_t* done;
     uint8_t* reason;
-    u32* nsteps;     // env.step() calls that applied the step logic, per board
+    u32* nsteps;     // env.step() calls, per board
     const u64* init; // 7 bitboards of the initial board
     uint64_t seed;
     int n;
+    __device__ DevHist hist(int i) const { return DevHist{htab, hboard, hcnt, hgen, hgen[i], n, i}; }
 };
 
 __device__ Pos init_pos(const u64* init) {
@@ -342,26 +370,51 @@ __device__ Pos init_pos(const u64* init) {
     return env_reset_pos(s);
 }
 
-// policy: uniform choice among the reference-ordered legal list (test_benchmark.py:22-27)
-__device__ uint16_t pick(const Pos& s, const Gen& g, int n, uint64_t seed, int i, u32& draw) {
-    if (n == 0) return (uint16_t)A_NONE;
-    u32 k = policy_index(seed, (u32)i, draw++, (u32)n);
-    return (uint16_t)select_legal(s, g, (int)k);
+// reset (chess_v2.py:183-206); the generation bump empties the repetition window
+__device__ void reset_board(Pos& s, DevHist& h, const u64* init) {
+    s = init_pos(init);
+    h.bump_gen();
 }
 
-__global__ void k_env_reset(EnvDev e, const uint8_t* __restrict__ mask, int select) {
+// policy: uniform choice among the reference-ordered legal list (test_benchmark.py:22-27)
+__device__ uint16_t pick(const Pos& s, const Gen& g, const MoveSet& ms, const LdsScratch& scr, uint64_t seed,
+                         int i, u32& draw) {
+    if (ms.total == 0) return (uint16_t)A_NONE;
+    u32 k = policy_index(seed, (u32)i, draw++, (u32)ms.total);
+    return (uint16_t)select_move(s, g, ms, scr, (int)k);
+}
+
+__global__ void __launch_bounds__(BLOCK) k_env_reset(EnvDev e, const uint8_t* __restrict__ mask, int select) {
+    LDS_SCRATCH_DECL;
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= e.n) return;
     if (mask && !mask[i]) return;
-    Pos s = init_pos(e.init);
+    DevHist h = e.hist(i);
+    Pos s;
+    reset_board(s, h, e.init);
     e.st.store(i, s);
     if (select) {
         Gen g;
+        MoveSet ms;
         gen_init(s, g);
+        gen_moves(s, g, ms, scr);
         u32 d = e.draw[i];
-        e.act[i] = pick(s, g, count_legal(s, g), e.seed, i, d);
+        e.act[i] = pick(s, g, ms, scr, e.seed, i, d);
         e.draw[i] = d;
     }
+}
+
+// set_states ingest for the env: import + empty window
+__global__ void k_env_import(const int8_t* __restrict__ boards, const uint8_t* __restrict__ meta8, EnvDev e) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= e.n) return;
+    const uint8_t* m = meta8 + 8 * (size_t)i;
+    u32 meta = (m[0] ? M_WHITE : 0u) | (m[1] ? M_WKC : 0u) | (m[2] ? M_WQC : 0u) | (m[3] ? M_BKC : 0u) |
+               (m[4] ? M_BQC : 0u) | (m[5] ? M_WCHK : 0u) | (m[6] ? M_BCHK : 0u) | ((u32)m[7] << M_MC_SHIFT);
+    Pos s = from_mailbox(boards + 64 * (size_t)i, meta);
+    e.st.store(i, s);
+    DevHist h = e.hist(i);
+    h.bump_gen();
 }
 
 // One env ply per board.
@@ -371,40 +424,41 @@ __global__ void k_env_reset(EnvDev e, const uint8_t* __restrict__ mask, int sele
 //                without a step; done -> reset; then pick the next action.
 template <bool POLICY>
 __global__ void __launch_bounds__(BLOCK) k_env_step(EnvDev e) {
+    LDS_SCRATCH_DECL;
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= e.n) return;
     Pos s = e.st.load(i);
-    DevHist h{e.hkey, e.hboard, e.n, i};
+    DevHist h = e.hist(i);
     int a = e.act[i];
     StepOut o = {0, 0, R_NONE, 0};
     Gen g;
-    bool have_gen = false;
+    MoveSet ms;
+    bool have = false;
     if (POLICY && a == A_NONE) {
-        s = init_pos(e.init);
+        reset_board(s, h, e.init);
         o.reason = R_NO_MOVES;
     } else {
         if (POLICY) {
-            o = env_step<false>(s, h, a, nullptr);
+            o = env_step<false>(s, h, a, nullptr, g, ms, scr);
         } else {
             Gen g0;
             gen_init(s, g0);
-            o = env_step<true>(s, h, a, &g0);
+            o = env_step<true>(s, h, a, &g0, g, ms, scr);
         }
-        if (o.moved) {
-            gen_init(s, g);
-            have_gen = true;
-            env_finish(s, o, count_legal(s, g));
-        }
+        have = o.moved;
         e.nsteps[i] += 1;
         if (POLICY && o.done) {
-            s = init_pos(e.init);
-            have_gen = false;
+            reset_board(s, h, e.init);
+            have = false;
         }
     }
     if (POLICY) {
-        if (!have_gen) gen_init(s, g);
+        if (!have) {
+            gen_init(s, g);
+            gen_moves(s, g, ms, scr);
+        }
         u32 d = e.draw[i];
-        e.act[i] = pick(s, g, count_legal(s, g), e.seed, i, d);
+        e.act[i] = pick(s, g, ms, scr, e.seed, i, d);
         e.draw[i] = d;
     }
     e.st.store(i, s);
@@ -414,42 +468,47 @@ __global__ void __launch_bounds__(BLOCK) k_env_step(EnvDev e) {
 }
 
 // Fused K-ply random self-play: state in registers for the whole launch.  Optional per-ply
-// trace [ply][N] (tests).  stats per board: [steps, reward_sum(two's complement), ends[1..5]]
+// trace [ply][N] (tests).  stats per board: [steps, reward_sum(two's complement), ends[0..5]]
 __global__ void __launch_bounds__(BLOCK) k_env_rollout(EnvDev e, int plies, int16_t* tr_action, int16_t* tr_reward,
                                                        uint8_t* tr_done, uint8_t* tr_reason, uint64_t* stats) {
+    LDS_SCRATCH_DECL;
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= e.n) return;
     Pos s = e.st.load(i);
-    DevHist h{e.hkey, e.hboard, e.n, i};
+    DevHist h = e.hist(i);
     u32 d = e.draw[i];
     int a = e.act[i];
-    uint64_t steps = 0, rsum = 0, ends[6] = {0, 0, 0, 0, 0, 0};
+    uint64_t steps = 0, rsum = 0;
+    u32 e_mate = 0, e_rep = 0, e_cap = 0, e_nomove = 0, e_err = 0;
     for (int p = 0; p < plies; p++) {
         StepOut o = {0, 0, R_NONE, 0};
         Gen g;
-        bool have_gen = false;
+        MoveSet ms;
+        bool have = false;
         int played = a;
         if (a == A_NONE) {
-            s = init_pos(e.init);
+            reset_board(s, h, e.init);
             o.reason = R_NO_MOVES;
-            ends[R_NO_MOVES]++;
+            e_nomove++;
             played = -1;
         } else {
-            o = env_step<false>(s, h, a, nullptr);
-            if (o.moved) {
-                gen_init(s, g);
-                have_gen = true;
-                env_finish(s, o, count_legal(s, g));
-            }
+            o = env_step<false>(s, h, a, nullptr, g, ms, scr);
+            have = o.moved;
             steps++;
             rsum += (uint64_t)(int64_t)o.reward;
             if (o.done) {
-                ends[o.reason < 6 ? o.reason : 0]++;
-                s = init_pos(e.init);
-                have_gen = false;
+                e_mate += o.reason == R_MATE;
+                e_rep += o.reason == R_REPETITION;
+                e_cap += o.reason == R_MOVE_CAP;
+                e_err += o.reason == R_BOTH_CHECKED;
+                reset_board(s, h, e.init);
+                have = false;
             }
         }
-        if (!have_gen) gen_init(s, g);
+        if (!have) {
+            gen_init(s, g);
+            gen_moves(s, g, ms, scr);
+        }
         if (tr_action) {
             size_t t = (size_t)p * e.n + i;
             tr_action[t] = (int16_t)played;
@@ -457,7 +516,7 @@ __global__ void __launch_bounds__(BLOCK) k_env_rollout(EnvDev e, int plies, int1
             tr_done[t] = (uint8_t)o.done;
             tr_reason[t] = (uint8_t)o.reason;
         }
-        a = pick(s, g, count_legal(s, g), e.seed, i, d);
+        a = pick(s, g, ms, scr, e.seed, i, d);
     }
     e.st.store(i, s);
     e.draw[i] = d;
@@ -466,8 +525,23 @@ __global__ void __launch_bounds__(BLOCK) k_env_rollout(EnvDev e, int plies, int1
     if (stats) {
         uint64_t* o = stats + 8 * (size_t)i;
         o[0] += steps; o[1] += rsum;
-        for (int k = 0; k < 6; k++) o[2 + k] += ends[k];
+        o[2 + R_MATE] += e_mate; o[2 + R_REPETITION] += e_rep; o[2 + R_MOVE_CAP] += e_cap;
+        o[2 + R_NO_MOVES] += e_nomove; o[2 + R_BOTH_CHECKED] += e_err;
     }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_select(EnvDev e) {
+    LDS_SCRATCH_DECL;
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= e.n) return;
+    Pos s = e.st.load(i);
+    Gen g;
+    MoveSet ms;
+    gen_init(s, g);
+    gen_moves(s, g, ms, scr);
+    u32 d = e.draw[i];
+    e.act[i] = pick(s, g, ms, scr, e.seed, i, d);
+    e.draw[i] = d;
 }
 
 // ----------------------------------------------------------------------------- host side
@@ -704,8 +778,9 @@ struct gc_env {
 };
 
 static void env_free(gc_env* e) {
-    void* ps[] = {e->bb, e->meta, e->init, e->d.hkey, e->d.hboard, e->d.draw, e->d.act, e->d.reward, e->d.done,
-                  e->d.reason, e->d.nsteps, e->mbox, e->m8, e->mask, e->list, e->counts, e->lmask, e->stats};
+    void* ps[] = {e->bb, e->meta, e->init, e->d.htab, e->d.hboard, e->d.hcnt, e->d.hgen, e->d.draw, e->d.act,
+                  e->d.reward, e->d.done, e->d.reason, e->d.nsteps, e->mbox, e->m8, e->mask, e->list, e->counts,
+                  e->lmask, e->stats};
     for (void* p : ps) if (p) (void)hipFree(p);
     for (auto& v : e->ev) if (v) (void)hipEventDestroy(v);
     if (e->stream) (void)hipStreamDestroy(e->stream);
@@ -732,7 +807,8 @@ extern "C" int gc_env_create(int device, int n_boards, uint64_t seed, const int8
     if (he == hipSuccess) he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
     if (he != hipSuccess) { env_free(e); delete e; return fail(std::string("stream: ") + hipGetErrorString(he)); }
     if (dalloc(&e->bb, (size_t)NBB * n) || dalloc(&e->meta, n) || dalloc(&e->init, NBB) ||
-        dalloc(&e->d.hkey, (size_t)HIST_CAP * n) || dalloc(&e->d.hboard, (size_t)HIST_CAP * NBB * n) ||
+        dalloc(&e->d.htab, (size_t)HTAB * n) || dalloc(&e->d.hboard, (size_t)HIST_CAP * NBB * n) ||
+        dalloc(&e->d.hcnt, (size_t)HIST_CAP * n) || dalloc(&e->d.hgen, n) ||
         dalloc(&e->d.draw, n) || dalloc(&e->d.act, n) || dalloc(&e->d.reward, n) || dalloc(&e->d.done, n) ||
         dalloc(&e->d.reason, n) || dalloc(&e->d.nsteps, n) || dalloc(&e->mbox, (size_t)64 * n) ||
         dalloc(&e->m8, (size_t)8 * n) || dalloc(&e->mask, n) || dalloc(&e->counts, n) || dalloc(&e->stats, (size_t)8 * n)) {
@@ -745,6 +821,8 @@ extern "C" int gc_env_create(int device, int n_boards, uint64_t seed, const int8
     u64 ibb[NBB] = {ip.k, ip.q, ip.r, ip.b, ip.n, ip.p, ip.w};
     he = hipMemcpyAsync(e->init, ibb, sizeof(ibb), hipMemcpyHostToDevice, e->stream);
     if (he == hipSuccess) he = hipMemsetAsync(e->d.draw, 0, (size_t)4 * n, e->stream);
+    if (he == hipSuccess) he = hipMemsetAsync(e->d.htab, 0, (size_t)8 * HTAB * n, e->stream);
+    if (he == hipSuccess) he = hipMemsetAsync(e->d.hgen, 0, (size_t)4 * n, e->stream);
     if (he == hipSuccess) he = hipMemsetAsync(e->d.nsteps, 0, (size_t)4 * n, e->stream);
     if (he == hipSuccess) he = hipMemsetAsync(e->d.reward, 0, (size_t)4 * n, e->stream);
     if (he == hipSuccess) he = hipMemsetAsync(e->d.done, 0, (size_t)n, e->stream);
@@ -814,17 +892,6 @@ extern "C" int gc_env_step_random(gc_env* e, int n_plies) {
         HIPCHK(hipGetLastError());
     }
     return 0;
-}
-
-__global__ void k_select(EnvDev e) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= e.n) return;
-    Pos s = e.st.load(i);
-    Gen g;
-    gen_init(s, g);
-    u32 d = e.draw[i];
-    e.act[i] = pick(s, g, count_legal(s, g), e.seed, i, d);
-    e.draw[i] = d;
 }
 
 extern "C" int gc_env_select_random(gc_env* e) {
@@ -901,7 +968,7 @@ extern "C" int gc_env_set_states(gc_env* e, const int8_t* boards, const uint8_t*
     HIPCHK(hipSetDevice(e->device));
     HIPCHK(hipMemcpyAsync(e->mbox, boards, (size_t)64 * e->n, hipMemcpyHostToDevice, e->stream));
     HIPCHK(hipMemcpyAsync(e->m8, meta, (size_t)8 * e->n, hipMemcpyHostToDevice, e->stream));
-    k_import<<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->mbox, e->m8, nullptr, e->d.st);
+    k_env_import<<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->mbox, e->m8, e->d);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(e->stream));
     e->policy_ready = false;
@@ -985,5 +1052,6 @@ extern "C" int gc_env_window_sum(gc_env* e, uint64_t* sum) {
 extern "C" uint64_t gc_env_device_bytes(gc_env* e) {
     if (!e) return 0;
     uint64_t n = (uint64_t)e->n;
-    return n * (NBB * 8 + 4) + n * HIST_CAP * (4 + NBB * 8) + n * (4 + 2 + 4 + 1 + 1 + 4) + n * (64 + 8 + 1 + 4 + 64);
+    return n * (NBB * 8 + 4) + n * HTAB * 8 + n * HIST_CAP * (1 + NBB * 8) + n * (4 + 4 + 2 + 4 + 1 + 1 + 4) +
+           n * (64 + 8 + 1 + 4 + 64);
 }

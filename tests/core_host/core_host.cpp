@@ -124,61 +124,99 @@ extern "C" uint64_t host_perft(const int8_t* b, const uint8_t* m, int depth) {
 }
 
 // ---- env rollout on the host with the same driver as k_env_rollout ----------------------
-struct HostHist {
-    std::vector<u32> keys;
+struct HostHist {  // same contract as the device DevHist (gc_env.h rep_count)
+    std::vector<u64> tabv;
     std::vector<Pos> boards;
-    HostHist() : keys(HIST_CAP), boards(HIST_CAP) {}
-    u32 key(int i) const { return keys[i]; }
+    std::vector<int> cnts;
+    u32 g = 1;
+    HostHist() : tabv(HTAB, 0), boards(HIST_CAP), cnts(HIST_CAP, 0) {}
+    u32 gen() const { return g; }
+    void bump_gen() { g++; }
+    u64 tab(int p) const { return tabv[p]; }
+    void set_tab(int p, u64 v) { tabv[p] = v; }
     bool same(int i, const Pos& s) const {
         const Pos& h = boards[i];
         return h.k == s.k && h.q == s.q && h.r == s.r && h.b == s.b && h.n == s.n && h.p == s.p && h.w == s.w;
     }
-    void put(int i, u32 k, const Pos& s) { keys[i] = k; boards[i] = s; }
+    void put(int i, const Pos& s) { boards[i] = s; }
+    int cnt(int i) const { return cnts[i]; }
+    void set_cnt(int i, int c) { cnts[i] = c; }
 };
+
+struct HostScratch {
+    u64 v[SCRATCH_SLOTS];
+    void put(int j, u64 x) { v[j] = x; }
+    u64 get(int j) const { return v[j]; }
+};
+
+extern "C" int host_count2(const int8_t* b, const uint8_t* m, int white) {
+    Pos s = import_state(b, m, white);
+    Gen g;
+    gen_init(s, g);
+    MoveSet ms;
+    HostScratch scr;
+    gen_moves(s, g, ms, scr);
+    return ms.total;
+}
+extern "C" int host_select2(const int8_t* b, const uint8_t* m, int white, int k) {
+    Pos s = import_state(b, m, white);
+    Gen g;
+    gen_init(s, g);
+    MoveSet ms;
+    HostScratch scr;
+    gen_moves(s, g, ms, scr);
+    return select_move(s, g, ms, scr, k);
+}
+
+static void host_reset(Pos& s, HostHist& h, const Pos& ip) {
+    s = env_reset_pos(ip);
+    h.bump_gen();
+}
 
 extern "C" void host_rollout_trace(const int8_t* init, uint64_t seed, uint32_t board, int plies, int16_t* tr_action,
                                    int16_t* tr_reward, uint8_t* tr_done, uint8_t* tr_reason, int8_t* final_board,
                                    uint8_t* final_meta, uint64_t* stats8) {
     Pos ip = from_mailbox(init, 0);
-    Pos s = env_reset_pos(ip);
+    Pos s;
     HostHist h;
+    HostScratch scr;
+    host_reset(s, h, ip);
     u32 draw = 0;
     Gen g;
+    MoveSet ms;
     gen_init(s, g);
-    int n = count_legal(s, g);
-    int a = n ? select_legal(s, g, (int)policy_index(seed, board, draw++, (u32)n)) : A_NONE;
+    gen_moves(s, g, ms, scr);
+    int a = ms.total ? select_move(s, g, ms, scr, (int)policy_index(seed, board, draw++, (u32)ms.total)) : A_NONE;
     uint64_t steps = 0, rsum = 0, ends[6] = {0, 0, 0, 0, 0, 0};
     for (int p = 0; p < plies; p++) {
         StepOut o = {0, 0, R_NONE, 0};
-        bool have_gen = false;
+        bool have = false;
         int played = a;
         if (a == A_NONE) {
-            s = env_reset_pos(ip);
+            host_reset(s, h, ip);
             o.reason = R_NO_MOVES;
             ends[R_NO_MOVES]++;
             played = -1;
         } else {
-            o = env_step<false>(s, h, a, nullptr);
-            if (o.moved) {
-                gen_init(s, g);
-                have_gen = true;
-                env_finish(s, o, count_legal(s, g));
-            }
+            o = env_step<false>(s, h, a, nullptr, g, ms, scr);
+            have = o.moved;
             steps++;
             rsum += (uint64_t)(int64_t)o.reward;
             if (o.done) {
                 ends[o.reason < 6 ? o.reason : 0]++;
-                s = env_reset_pos(ip);
-                have_gen = false;
+                host_reset(s, h, ip);
+                have = false;
             }
         }
-        if (!have_gen) gen_init(s, g);
+        if (!have) {
+            gen_init(s, g);
+            gen_moves(s, g, ms, scr);
+        }
         tr_action[p] = (int16_t)played;
         tr_reward[p] = (int16_t)o.reward;
         tr_done[p] = (uint8_t)o.done;
         tr_reason[p] = (uint8_t)o.reason;
-        n = count_legal(s, g);
-        a = n ? select_legal(s, g, (int)policy_index(seed, board, draw++, (u32)n)) : A_NONE;
+        a = ms.total ? select_move(s, g, ms, scr, (int)policy_index(seed, board, draw++, (u32)ms.total)) : A_NONE;
     }
     export_state(s, final_board, final_meta);
     stats8[0] = steps; stats8[1] = rsum;
@@ -189,25 +227,22 @@ extern "C" void host_rollout_trace(const int8_t* init, uint64_t seed, uint32_t b
 struct HostEnv {
     Pos init, s;
     HostHist h;
+    HostScratch scr;
 };
 extern "C" void* host_env_new(const int8_t* init) {
     HostEnv* e = new HostEnv();
     e->init = from_mailbox(init, 0);
-    e->s = env_reset_pos(e->init);
+    host_reset(e->s, e->h, e->init);
     return e;
 }
 extern "C" void host_env_free(void* p) { delete (HostEnv*)p; }
-extern "C" void host_env_reset(void* p) { HostEnv* e = (HostEnv*)p; e->s = env_reset_pos(e->init); }
+extern "C" void host_env_reset(void* p) { HostEnv* e = (HostEnv*)p; host_reset(e->s, e->h, e->init); }
 extern "C" int host_env_step(void* p, int action, int* reward, int* done, int* reason) {
     HostEnv* e = (HostEnv*)p;
-    Gen g0;
+    Gen g0, g;
+    MoveSet ms;
     gen_init(e->s, g0);
-    StepOut o = env_step<true>(e->s, e->h, action, &g0);
-    if (o.moved) {
-        Gen g;
-        gen_init(e->s, g);
-        env_finish(e->s, o, count_legal(e->s, g));
-    }
+    StepOut o = env_step<true>(e->s, e->h, action, &g0, g, ms, e->scr);
     *reward = o.reward;
     *done = o.done;
     *reason = o.reason;

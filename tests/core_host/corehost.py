@@ -32,6 +32,8 @@ def lib():
         L.host_perft.argtypes = [P, P, ctypes.c_int]
         L.host_list.argtypes = [P, P, ctypes.c_int, ctypes.c_int, P, ctypes.c_int]
         L.host_count.argtypes = [P, P, ctypes.c_int]
+        L.host_count2.argtypes = [P, P, ctypes.c_int]
+        L.host_select2.argtypes = [P, P, ctypes.c_int, ctypes.c_int]
         L.host_select.argtypes = [P, P, ctypes.c_int, ctypes.c_int]
         L.host_action_legal.argtypes = [P, P, ctypes.c_int, ctypes.c_int]
         L.host_next_state.argtypes = [P, P, ctypes.c_int, ctypes.c_int, P, P, P]
@@ -66,6 +68,16 @@ def get_list(board, meta, white, attack=False):
 def count(board, meta, white):
     b, m = _bm(board, meta)
     return lib().host_count(_p(b), _p(m), int(white))
+
+
+def count2(board, meta, white):
+    b, m = _bm(board, meta)
+    return lib().host_count2(_p(b), _p(m), int(white))
+
+
+def select2(board, meta, white, k):
+    b, m = _bm(board, meta)
+    return lib().host_select2(_p(b), _p(m), int(white), int(k))
 
 
 def select(board, meta, white, k):

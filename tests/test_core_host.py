@@ -84,8 +84,10 @@ def test_fuzz_positions(oracle, seed):
             ref = oracle.get_possible_moves(b, m, white)
             assert H.get_list(b, m, white) == ref, (i, white)
             assert H.count(b, m, white) == len(ref)
+            assert H.count2(b, m, white) == len(ref)
             for k in range(len(ref)):
                 assert H.select(b, m, white, k) == ref[k]
+                assert H.select2(b, m, white, k) == ref[k]
             legal = set(ref)
             for a in list(legal)[:5] + [int(x) for x in rng.randint(0, 4101, size=5)]:
                 assert H.action_legal(b, m, white, a) == (a in legal)
