@@ -574,28 +574,29 @@ GC_HD int select_move(const Pos& s, const Gen& g, const MoveSet& ms, const S& sc
     u64 t[SCRATCH_SLOTS];
 #pragma unroll
     for (int j = 0; j < SCRATCH_SLOTS; j++) t[j] = scr.get(j);  // all reads in flight at once
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+    for (int j = 0; j < SCRATCH_SLOTS; j++) asm volatile("" : "+v"(t[j]));  // one wait, not sixteen
+#endif
     u64 pcs = g.own;
     int res = -1, rsq = 0, rk = 0;
     u64 rtg = 0;
     bool pawn = false;
 #pragma unroll
-    for (int j = 0; j < SCRATCH_SLOTS; j++) {  // single-exit, fully unrolled scan in square order
-        if (pcs && res < 0) {
-            int sq = ctz(pcs);
-            pcs &= pcs - 1;
-            bool fast = (ms.fastp >> sq) & 1;
-            int c = fast ? (int)(((ms.o1 >> sq) & 1) + ((ms.o2 >> sq) & 1) + ((ms.ol >> sq) & 1) + ((ms.orr >> sq) & 1))
-                         : popc(t[j]);
-            if (k < c) {
-                res = j;
-                rsq = sq;
-                rk = k;
-                rtg = t[j];
-                pawn = fast;
-            } else {
-                k -= c;
-            }
-        }
+    for (int j = 0; j < SCRATCH_SLOTS; j++) {  // predicated, fully unrolled scan in square order
+        bool live = pcs != 0 && res < 0;
+        int sq = pcs ? ctz(pcs) : 0;
+        pcs &= pcs - 1;
+        bool fast = (ms.fastp >> sq) & 1;
+        int pc = (int)(((ms.o1 >> sq) & 1) + ((ms.o2 >> sq) & 1) + ((ms.ol >> sq) & 1) + ((ms.orr >> sq) & 1));
+        int c = fast ? pc : popc(t[j]);
+        bool hit = live && k < c;
+        res = hit ? j : res;
+        rsq = hit ? sq : rsq;
+        rk = hit ? k : rk;
+        rtg = hit ? t[j] : rtg;
+        pawn = hit ? fast : pawn;
+        k = (live && !hit) ? k - c : k;
     }
     if (res >= 0) {
         int sq = rsq;
@@ -631,7 +632,7 @@ GC_HD bool action_legal(const Pos& s, const Gen& g, int action) {
 // square is empty (the reference panics), -2 bad action.  *reward = captured value
 // (+10 on the dead promotion branch); *irrev = pawn move or capture (repetition window).
 GC_HD int apply_move(Pos& s, bool white_player, int action, int* reward, bool* irrev) {
-    const int VAL[7] = {0, 0, 10, 5, 3, 3, 1};
+    // piece values by |id| (lib.rs:19-25) as 4-bit fields: 0,0,10,5,3,3,1 -- no memory table
     *reward = 0;
     *irrev = false;
     if (action < 4096) {
@@ -643,7 +644,7 @@ GC_HD int apply_move(Pos& s, bool white_player, int action, int* reward, bool* i
         clear_sq(s, f);
         clear_sq(s, t);
         int nid = pid;
-        *reward = VAL[ct];
+        *reward = (int)((0x1335A00u >> (4 * ct)) & 0xFu);
         if (pt == PAWN && ((white_player && (t >> 3) == 7) || (!white_player && (t >> 3) == 0))) {
             nid = white_player ? QUEEN : -QUEEN;  // QUEEN_ID * player (lib.rs:706)
             *reward += 10;

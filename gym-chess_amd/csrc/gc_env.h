@@ -11,13 +11,18 @@
 // move backwards and no move adds a piece, so a pawn move or a capture strictly decreases
 // a monotone potential and no later board equals an earlier one.  The window therefore
 // holds the distinct boards since the last pawn move / capture (<= 300: the move cap,
-// chess_v2.py:141, 252) with their occurrence counts.  Lookup is O(1): a per-board
-// open-addressed table of 1024 entries {generation u32 | window slot u9 | key tag u22};
-// an entry is live only if its generation equals the board's current one, so clearing
-// the window (irreversible move, reset) is a single generation bump.  Every tag hit is
-// confirmed against the stored 7-bitboard board, so the count is exact.
+// chess_v2.py:141, 252) with their occurrence counts, in a per-board open-addressed table
+// of HTAB 64-byte entries {generation u32 | key tag u22 | count u8, 7 bitboards}: one
+// entry = one cache line, so a single probe both finds and verifies a board.  An entry is
+// live only if its generation equals the board's current one, so clearing the window
+// (irreversible move, reset) is a single generation bump.  The count is exact (full-board
+// compare); the first probe is issued before move generation so its latency overlaps it.
 #pragma once
 #include "gc_core.h"
+
+#ifndef GC_STAMP
+#define GC_STAMP(k)  // diagnostic builds (-DGC_STAMPS) record s_memtime at phase boundaries
+#endif
 
 namespace gc {
 
@@ -47,27 +52,43 @@ GC_HD Pos env_reset_pos(const Pos& init) {
     return s;
 }
 
-// H (per-board window storage) provides:
-//   u32 gen(); void bump_gen();  u64 tab(int); void set_tab(int, u64);
-//   bool same(int slot, const Pos&); void put(int slot, const Pos&);
-//   int cnt(int slot); void set_cnt(int slot, int)
+// one table entry
+struct RepEntry {
+    u64 hdr;  // gen (bits 0..31) | tag (32..53) | count (56..63)
+    u64 k, q, r, b, n, p, w;
+};
+GC_HD bool rep_same(const RepEntry& e, const Pos& s) {
+    return e.k == s.k && e.q == s.q && e.r == s.r && e.b == s.b && e.n == s.n && e.p == s.p && e.w == s.w;
+}
+
+// H (per-board table storage) provides:
+//   u32 gen(); void bump_gen(); RepEntry load(int pos); void store_hdr(int pos, u64);
+//   void store(int pos, const RepEntry&)
+struct RepProbe {
+    u32 key;
+    RepEntry e0;  // the first probe, loaded early
+};
+
+template <class H>
+GC_HD void rep_prefetch(H& h, const Pos& s, RepProbe& pr) {
+    pr.key = board_key(s);
+    pr.e0 = h.load((int)(pr.key & (HTAB - 1)));
+}
+
 // Returns how many times the board has been the pre-move board so far, this one included.
 template <class H>
-GC_HD int rep_count(H& h, const Pos& s, u32& hl, bool irrev) {
-    u32 key = board_key(s);
+GC_HD int rep_commit(H& h, const Pos& s, const RepProbe& pr, u32& hl, bool irrev) {
     u32 gen = h.gen();
-    u32 pos = key & (HTAB - 1), tag = key >> HTAB_BITS;
+    u32 pos = pr.key & (HTAB - 1), tag = pr.key >> HTAB_BITS;
     int c = 0;
+    RepEntry e = pr.e0;
     for (int probe = 0; probe < HTAB; probe++) {
-        u64 e = h.tab(pos);
-        if ((u32)e != gen) break;  // free for this generation
-        if ((u32)(e >> 41) == tag) {
-            int slot = (int)((e >> 32) & 511);
-            if (h.same(slot, s)) {
-                c = h.cnt(slot) + 1;
-                h.set_cnt(slot, c);
-                break;
-            }
+        if (probe) e = h.load((int)pos);
+        if ((u32)e.hdr != gen) break;  // free for this generation
+        if ((u32)((e.hdr >> 32) & 0x3FFFFF) == tag && rep_same(e, s)) {
+            c = (int)(e.hdr >> 56) + 1;
+            h.store_hdr((int)pos, (e.hdr & ~(0xFFull << 56)) | ((u64)c << 56));
+            break;
         }
         pos = (pos + 1) & (HTAB - 1);
     }
@@ -78,9 +99,8 @@ GC_HD int rep_count(H& h, const Pos& s, u32& hl, bool irrev) {
     }
     if (c) return c;
     if (hl < HIST_CAP) {
-        h.put(hl, s);
-        h.set_cnt(hl, 1);
-        h.set_tab(pos, (u64)gen | ((u64)hl << 32) | ((u64)tag << 41));
+        RepEntry ne = {(u64)gen | ((u64)tag << 32) | (1ull << 56), s.k, s.q, s.r, s.b, s.n, s.p, s.w};
+        h.store((int)pos, ne);
         hl++;
     }
     return 1;
@@ -100,6 +120,9 @@ GC_HD StepOut env_step(Pos& s, H& hist, int action, const Gen* g0, Gen& g, MoveS
     }
     if (s.meta & M_DONE) { o.done = 1; o.reason = R_DONE_ALREADY; return o; }       // 245-251
     if (mc_of(s.meta) > MOVES_MAX) { o.done = 1; o.reason = R_MOVE_CAP; return o; }  // 252-258
+    RepProbe pr;
+    rep_prefetch(hist, s, pr);  // in flight during the move generation below
+    GC_STAMP(2);
     bool white = s.meta & M_WHITE;
     Pos ns = s;
     ns.meta = (ns.meta & ~(u32)M_RIGHTS) | eff_rights(s);  // State::new
@@ -112,28 +135,31 @@ GC_HD StepOut env_step(Pos& s, H& hist, int action, const Gen* g0, Gen& g, MoveS
     bool opp_chk = g.in_check;
     int mk = tracked_king(ns, white);
     bool my_chk = mk >= 0 && sq_attacked(ns, mk, !white);
+    GC_STAMP(3);
     if (opp_chk && my_chk) {  // lib.rs:1442-1446
         o.reason = R_BOTH_CHECKED;
         o.done = 1;
         return o;
     }
+    // the opponent's possible moves (chess_v2.py:268)
+    gen_moves(ns, g, ms, scr);
+    GC_STAMP(4);
     u32 chk = white ? ((my_chk ? M_WCHK : 0u) | (opp_chk ? M_BCHK : 0u))
                     : ((opp_chk ? M_WCHK : 0u) | (my_chk ? M_BCHK : 0u));
     u32 hl = hl_of(s.meta);
-    bool rep = rep_count(hist, s, hl, irrev) >= 3;  // chess_v2.py:404-407
+    bool rep = rep_commit(hist, s, pr, hl, irrev) >= 3;  // chess_v2.py:404-407
+    GC_STAMP(5);
     ns.meta = with_hl((ns.meta & ~(u32)(M_WCHK | M_BCHK | M_DONE)) | chk | (rep ? M_DONE : 0u), hl);
     o.reward = -10 + mr;  // INVALID_ACTION_REWARD + move reward (Q9)
     o.moved = 1;
     if (rep) { o.done = 1; o.reason = R_REPETITION; }
-    // the opponent's possible moves (chess_v2.py:268), mate (270-272), move_count (291-292)
-    gen_moves(ns, g, ms, scr);
-    if (ms.total == 0 && opp_chk) {
+    if (ms.total == 0 && opp_chk) {  // 270-272
         ns.meta |= M_DONE;
         o.done = 1;
         o.reward += 100;
         o.reason = R_MATE;
     }
-    if (!o.done && !white) ns.meta += (1u << M_MC_SHIFT);
+    if (!o.done && !white) ns.meta += (1u << M_MC_SHIFT);  // 291-292
     s = ns;
     return o;
 }

@@ -5,7 +5,8 @@
 // of one field are 512 contiguous bytes.  All move generation is register-resident
 // integer/bitwise work (gc_core.h), with per-piece move targets parked in LDS for the
 // ordered policy pick; the only other HBM traffic is the 3-fold repetition window
-// (gc_env.h): one or two probes of a per-board hash table + a board compare on tag hits.
+// (gc_env.h): usually one 64-byte probe of a per-board hash table, issued before move
+// generation so that its latency overlaps it.
 //
 // The C-ABI replaces the reference's FFI (the PyO3 ChessEngine, lib.rs:1412-1512) for the
 // engine calls, plus a device-resident batched env for chess_v2.py's reset()/step().
@@ -18,6 +19,18 @@
 #include <string>
 #include <vector>
 
+#ifdef GC_STAMPS
+// diagnostic build only: per-wave s_memtime stamps (MI355X guide, "In-kernel stamps")
+__shared__ unsigned long long gc_stamp_lds[4][8];
+__device__ __forceinline__ void gc_stamp(int k) {
+    __builtin_amdgcn_sched_barrier(0);
+    unsigned long long t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if ((threadIdx.x & 63) == 0) gc_stamp_lds[threadIdx.x >> 6][k] = t;
+}
+#define GC_STAMP(k) gc_stamp(k)
+#endif
 #include "gc_core.h"
 #include "gc_env.h"
 #include "../../include/gymchess.h"
@@ -68,31 +81,30 @@ struct SoA {
     }
 };
 
-// repetition window of board i (gc_env.h rep_count): table [HTAB][N] u64, window boards
-// [HIST_CAP][7][N] u64, occurrence counts [HIST_CAP][N] u8, generation [N] u32
+// repetition window of board i (gc_env.h rep_prefetch / rep_commit): HTAB 64-byte entries
+// per board at htab[(i*HTAB + pos)*8 ..], one cache line each (4 x 16-B loads); generation [N]
 struct DevHist {
     u64* htab;
-    u64* hboard;
-    uint8_t* hcnt;
     u32* hgen;
     u32 g;
-    int n, i;
+    int i;
     __device__ u32 gen() const { return g; }
-    __device__ void bump_gen() { g++; hgen[i] = g; }
-    __device__ u64 tab(int pos) const { return htab[(size_t)pos * n + i]; }
-    __device__ void set_tab(int pos, u64 v) { htab[(size_t)pos * n + i] = v; }
-    __device__ bool same(int slot, const Pos& s) const {
-        const u64* h = hboard + (size_t)slot * NBB * n + i;
-        return h[0] == s.k && h[(size_t)n] == s.q && h[2 * (size_t)n] == s.r && h[3 * (size_t)n] == s.b &&
-               h[4 * (size_t)n] == s.n && h[5 * (size_t)n] == s.p && h[6 * (size_t)n] == s.w;
+    __device__ void bump_gen() { g++; }                // written back by flush()
+    __device__ void flush(u32 g0) const { if (g != g0) hgen[i] = g; }
+    __device__ RepEntry load(int pos) const {
+        const ulonglong2* p = reinterpret_cast<const ulonglong2*>(htab + ((size_t)i * HTAB + pos) * 8);
+        ulonglong2 a = p[0], b = p[1], c = p[2], d = p[3];
+        RepEntry e = {a.x, a.y, b.x, b.y, c.x, c.y, d.x, d.y};
+        return e;
     }
-    __device__ void put(int slot, const Pos& s) {
-        u64* h = hboard + (size_t)slot * NBB * n + i;
-        h[0] = s.k; h[(size_t)n] = s.q; h[2 * (size_t)n] = s.r; h[3 * (size_t)n] = s.b;
-        h[4 * (size_t)n] = s.n; h[5 * (size_t)n] = s.p; h[6 * (size_t)n] = s.w;
+    __device__ void store_hdr(int pos, u64 h) { htab[((size_t)i * HTAB + pos) * 8] = h; }
+    __device__ void store(int pos, const RepEntry& e) {
+        ulonglong2* p = reinterpret_cast<ulonglong2*>(htab + ((size_t)i * HTAB + pos) * 8);
+        p[0] = make_ulonglong2(e.hdr, e.k);
+        p[1] = make_ulonglong2(e.q, e.r);
+        p[2] = make_ulonglong2(e.b, e.n);
+        p[3] = make_ulonglong2(e.p, e.w);
     }
-    __device__ int cnt(int slot) const { return hcnt[(size_t)slot * n + i]; }
-    __device__ void set_cnt(int slot, int c) { hcnt[(size_t)slot * n + i] = (uint8_t)c; }
 };
 
 // per-lane move-target scratch in LDS: slot j of lane t at lds[j*BLOCK + t] (each wave's
@@ -349,9 +361,7 @@ __global__ void k_sum_tasks(const int32_t* __restrict__ offs, const int32_t* __r
 // ----------------------------------------------------------------------------- env kernels
 struct EnvDev {
     SoA st;
-    u64* htab;
-    u64* hboard;
-    uint8_t* hcnt;
+    u64* htab;       // [N][HTAB][8] repetition tables (gc_env.h)
     u32* hgen;
     u32* draw;       // policy draws per board (Philox counter)
     uint16_t* act;   // next action per board (A_NONE = no legal move)
@@ -359,11 +369,21 @@ struct EnvDev {
     uint8_t* done;
     uint8_t* reason;
     u32* nsteps;     // env.step() calls, per board
-    const u64* init; // 7 bitboards of the initial board
+    u64 init[NBB];   // 7 bitboards of the initial board (kernel argument: scalar loads)
     uint64_t seed;
     int n;
-    __device__ DevHist hist(int i) const { return DevHist{htab, hboard, hcnt, hgen, hgen[i], n, i}; }
+    __device__ DevHist hist(int i, u32 g) const { return DevHist{htab, hgen, g, i}; }
 };
+
+// Keep a loaded value in a VGPR from here on.  The per-board inputs are all loaded at kernel
+// entry and pinned, so they cost ONE round trip; otherwise the compiler sinks each load to
+// its first use, and because vmcnt retires in order, the wait for such a late load also
+// drains the repetition-table probe that is meant to stay in flight during move generation.
+__device__ __forceinline__ void pin(u64& x) { asm volatile("" : "+v"(x)); }
+__device__ __forceinline__ void pin(u32& x) { asm volatile("" : "+v"(x)); }
+__device__ __forceinline__ void pin(Pos& s) {
+    pin(s.k); pin(s.q); pin(s.r); pin(s.b); pin(s.n); pin(s.p); pin(s.w); pin(s.meta);
+}
 
 __device__ Pos init_pos(const u64* init) {
     Pos s = {init[0], init[1], init[2], init[3], init[4], init[5], init[6], 0};
@@ -389,9 +409,11 @@ __global__ void __launch_bounds__(BLOCK) k_env_reset(EnvDev e, const uint8_t* __
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= e.n) return;
     if (mask && !mask[i]) return;
-    DevHist h = e.hist(i);
+    u32 g0 = e.hgen[i];
+    DevHist h = e.hist(i, g0);
     Pos s;
     reset_board(s, h, e.init);
+    h.flush(g0);
     e.st.store(i, s);
     if (select) {
         Gen g;
@@ -413,8 +435,7 @@ __global__ void k_env_import(const int8_t* __restrict__ boards, const uint8_t* _
                (m[4] ? M_BQC : 0u) | (m[5] ? M_WCHK : 0u) | (m[6] ? M_BCHK : 0u) | ((u32)m[7] << M_MC_SHIFT);
     Pos s = from_mailbox(boards + 64 * (size_t)i, meta);
     e.st.store(i, s);
-    DevHist h = e.hist(i);
-    h.bump_gen();
+    e.hgen[i] += 1;  // empty the repetition window
 }
 
 // One env ply per board.
@@ -422,14 +443,21 @@ __global__ void k_env_import(const int8_t* __restrict__ boards, const uint8_t* _
 //  POLICY=true : the random-self-play driver of test_benchmark.py -- act[i] was picked by
 //                the policy from this state; A_NONE (empty move list) -> driver reset
 //                without a step; done -> reset; then pick the next action.
+#ifdef GC_STAMPS
+__device__ unsigned long long* g_stamp_out;
+#endif
 template <bool POLICY>
 __global__ void __launch_bounds__(BLOCK) k_env_step(EnvDev e) {
     LDS_SCRATCH_DECL;
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= e.n) return;
+    GC_STAMP(0);
     Pos s = e.st.load(i);
-    DevHist h = e.hist(i);
-    int a = e.act[i];
+    u32 g0 = e.hgen[i], d = POLICY ? e.draw[i] : 0u, nst = e.nsteps[i], ua = e.act[i];
+    pin(s); pin(g0); pin(d); pin(nst); pin(ua);
+    GC_STAMP(1);
+    DevHist h = e.hist(i, g0);
+    int a = (int)ua;
     StepOut o = {0, 0, R_NONE, 0};
     Gen g;
     MoveSet ms;
@@ -446,7 +474,7 @@ __global__ void __launch_bounds__(BLOCK) k_env_step(EnvDev e) {
             o = env_step<true>(s, h, a, &g0, g, ms, scr);
         }
         have = o.moved;
-        e.nsteps[i] += 1;
+        nst += 1;
         if (POLICY && o.done) {
             reset_board(s, h, e.init);
             have = false;
@@ -457,11 +485,18 @@ __global__ void __launch_bounds__(BLOCK) k_env_step(EnvDev e) {
             gen_init(s, g);
             gen_moves(s, g, ms, scr);
         }
-        u32 d = e.draw[i];
+        GC_STAMP(6);
         e.act[i] = pick(s, g, ms, scr, e.seed, i, d);
         e.draw[i] = d;
     }
+    GC_STAMP(7);
+#ifdef GC_STAMPS
+    if (POLICY && g_stamp_out != nullptr && (threadIdx.x & 63) == 0)
+        for (int k = 0; k < 8; k++) g_stamp_out[(size_t)(i >> 6) * 8 + k] = gc_stamp_lds[threadIdx.x >> 6][k];
+#endif
     e.st.store(i, s);
+    h.flush(g0);
+    e.nsteps[i] = nst;
     e.reward[i] = o.reward;
     e.done[i] = (uint8_t)o.done;
     e.reason[i] = (uint8_t)o.reason;
@@ -475,9 +510,10 @@ __global__ void __launch_bounds__(BLOCK) k_env_rollout(EnvDev e, int plies, int1
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= e.n) return;
     Pos s = e.st.load(i);
-    DevHist h = e.hist(i);
-    u32 d = e.draw[i];
-    int a = e.act[i];
+    u32 g0 = e.hgen[i], d = e.draw[i], ua = e.act[i];
+    pin(s); pin(g0); pin(d); pin(ua);
+    DevHist h = e.hist(i, g0);
+    int a = (int)ua;
     uint64_t steps = 0, rsum = 0;
     u32 e_mate = 0, e_rep = 0, e_cap = 0, e_nomove = 0, e_err = 0;
     for (int p = 0; p < plies; p++) {
@@ -519,6 +555,7 @@ __global__ void __launch_bounds__(BLOCK) k_env_rollout(EnvDev e, int plies, int1
         a = pick(s, g, ms, scr, e.seed, i, d);
     }
     e.st.store(i, s);
+    h.flush(g0);
     e.draw[i] = d;
     e.act[i] = (uint16_t)a;
     e.nsteps[i] += (u32)steps;
@@ -769,7 +806,7 @@ struct gc_env {
     uint64_t seed = 0;
     hipStream_t stream = nullptr;
     EnvDev d{};
-    u64* bb = nullptr; u32* meta = nullptr; u64* init = nullptr;
+    u64* bb = nullptr; u32* meta = nullptr;
     int8_t* mbox = nullptr; uint8_t* m8 = nullptr; uint8_t* mask = nullptr;
     uint16_t* list = nullptr; int list_cap = 0; int32_t* counts = nullptr; u64* lmask = nullptr;
     uint64_t* stats = nullptr;
@@ -778,7 +815,7 @@ struct gc_env {
 };
 
 static void env_free(gc_env* e) {
-    void* ps[] = {e->bb, e->meta, e->init, e->d.htab, e->d.hboard, e->d.hcnt, e->d.hgen, e->d.draw, e->d.act,
+    void* ps[] = {e->bb, e->meta, e->d.htab, e->d.hgen, e->d.draw, e->d.act,
                   e->d.reward, e->d.done, e->d.reason, e->d.nsteps, e->mbox, e->m8, e->mask, e->list, e->counts,
                   e->lmask, e->stats};
     for (void* p : ps) if (p) (void)hipFree(p);
@@ -806,9 +843,8 @@ extern "C" int gc_env_create(int device, int n_boards, uint64_t seed, const int8
     hipError_t he = hipSetDevice(device);
     if (he == hipSuccess) he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
     if (he != hipSuccess) { env_free(e); delete e; return fail(std::string("stream: ") + hipGetErrorString(he)); }
-    if (dalloc(&e->bb, (size_t)NBB * n) || dalloc(&e->meta, n) || dalloc(&e->init, NBB) ||
-        dalloc(&e->d.htab, (size_t)HTAB * n) || dalloc(&e->d.hboard, (size_t)HIST_CAP * NBB * n) ||
-        dalloc(&e->d.hcnt, (size_t)HIST_CAP * n) || dalloc(&e->d.hgen, n) ||
+    if (dalloc(&e->bb, (size_t)NBB * n) || dalloc(&e->meta, n) ||
+        dalloc(&e->d.htab, (size_t)HTAB * 8 * n) || dalloc(&e->d.hgen, n) ||
         dalloc(&e->d.draw, n) || dalloc(&e->d.act, n) || dalloc(&e->d.reward, n) || dalloc(&e->d.done, n) ||
         dalloc(&e->d.reason, n) || dalloc(&e->d.nsteps, n) || dalloc(&e->mbox, (size_t)64 * n) ||
         dalloc(&e->m8, (size_t)8 * n) || dalloc(&e->mask, n) || dalloc(&e->counts, n) || dalloc(&e->stats, (size_t)8 * n)) {
@@ -819,9 +855,10 @@ extern "C" int gc_env_create(int device, int n_boards, uint64_t seed, const int8
     // initial board bitboards (pure data conversion of the caller's input; no engine work)
     Pos ip = from_mailbox(ib, 0);
     u64 ibb[NBB] = {ip.k, ip.q, ip.r, ip.b, ip.n, ip.p, ip.w};
-    he = hipMemcpyAsync(e->init, ibb, sizeof(ibb), hipMemcpyHostToDevice, e->stream);
+    for (int j = 0; j < NBB; j++) e->d.init[j] = ibb[j];
+    he = hipSuccess;
     if (he == hipSuccess) he = hipMemsetAsync(e->d.draw, 0, (size_t)4 * n, e->stream);
-    if (he == hipSuccess) he = hipMemsetAsync(e->d.htab, 0, (size_t)8 * HTAB * n, e->stream);
+    if (he == hipSuccess) he = hipMemsetAsync(e->d.htab, 0, (size_t)64 * HTAB * n, e->stream);
     if (he == hipSuccess) he = hipMemsetAsync(e->d.hgen, 0, (size_t)4 * n, e->stream);
     if (he == hipSuccess) he = hipMemsetAsync(e->d.nsteps, 0, (size_t)4 * n, e->stream);
     if (he == hipSuccess) he = hipMemsetAsync(e->d.reward, 0, (size_t)4 * n, e->stream);
@@ -831,7 +868,6 @@ extern "C" int gc_env_create(int device, int n_boards, uint64_t seed, const int8
     for (auto& v : e->ev) if (he == hipSuccess) he = hipEventCreate(&v);
     if (he != hipSuccess) { env_free(e); delete e; return fail(std::string("env init: ") + hipGetErrorString(he)); }
     e->d.st = SoA{e->bb, e->meta, n};
-    e->d.init = e->init;
     e->d.seed = seed;
     e->d.n = n;
     k_env_reset<<<grid_for(n), BLOCK, 0, e->stream>>>(e->d, nullptr, 1);
@@ -1048,10 +1084,29 @@ extern "C" int gc_env_window_sum(gc_env* e, uint64_t* sum) {
     return 0;
 }
 
+#ifdef GC_STAMPS
+extern "C" int gc_debug_stamps(gc_env* e, int n_plies, uint64_t* out /* (n/64)*8 */) {
+    unsigned long long* d = nullptr;
+    size_t cnt = (size_t)((e->n + 63) / 64) * 8;
+    if (dalloc(&d, cnt)) return -1;
+    HIPCHK(hipMemsetAsync(d, 0, cnt * 8, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_out), &d, sizeof(d)));
+    for (int p = 0; p < n_plies; p++) k_env_step<true><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(out, d, cnt * 8, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    unsigned long long* z = nullptr;
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_out), &z, sizeof(z)));
+    (void)hipFree(d);
+    return 0;
+}
+#endif
+
 // bytes of device memory held by the env (for reports)
 extern "C" uint64_t gc_env_device_bytes(gc_env* e) {
     if (!e) return 0;
     uint64_t n = (uint64_t)e->n;
-    return n * (NBB * 8 + 4) + n * HTAB * 8 + n * HIST_CAP * (1 + NBB * 8) + n * (4 + 4 + 2 + 4 + 1 + 1 + 4) +
+    return n * (NBB * 8 + 4) + n * HTAB * 64 + n * (4 + 4 + 2 + 4 + 1 + 1 + 4) +
            n * (64 + 8 + 1 + 4 + 64);
 }

@@ -124,23 +124,17 @@ extern "C" uint64_t host_perft(const int8_t* b, const uint8_t* m, int depth) {
 }
 
 // ---- env rollout on the host with the same driver as k_env_rollout ----------------------
-struct HostHist {  // same contract as the device DevHist (gc_env.h rep_count)
-    std::vector<u64> tabv;
-    std::vector<Pos> boards;
-    std::vector<int> cnts;
-    u32 g = 1;
-    HostHist() : tabv(HTAB, 0), boards(HIST_CAP), cnts(HIST_CAP, 0) {}
+struct HostHist {  // same contract as the device DevHist (gc_env.h rep_prefetch/rep_commit)
+    std::vector<RepEntry> tabv;
+    u32 g = 0;
+    HostHist() : tabv(HTAB) {
+        for (auto& e : tabv) e = RepEntry{0, 0, 0, 0, 0, 0, 0, 0};
+    }
     u32 gen() const { return g; }
     void bump_gen() { g++; }
-    u64 tab(int p) const { return tabv[p]; }
-    void set_tab(int p, u64 v) { tabv[p] = v; }
-    bool same(int i, const Pos& s) const {
-        const Pos& h = boards[i];
-        return h.k == s.k && h.q == s.q && h.r == s.r && h.b == s.b && h.n == s.n && h.p == s.p && h.w == s.w;
-    }
-    void put(int i, const Pos& s) { boards[i] = s; }
-    int cnt(int i) const { return cnts[i]; }
-    void set_cnt(int i, int c) { cnts[i] = c; }
+    RepEntry load(int p) const { return tabv[p]; }
+    void store_hdr(int p, u64 h) { tabv[p].hdr = h; }
+    void store(int p, const RepEntry& e) { tabv[p] = e; }
 };
 
 struct HostScratch {

@@ -21,9 +21,9 @@ for s in ${STEPS:-smoke pytest bench prof}; do
     pytest) step pytest 1200 python -m pytest tests -x -q -m gpu ;;
     bench)  step bench 600 python bench.py ${BENCH_ARGS:-} ;;
     prof)   step prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 100 --warmup 20 ;;
-    pmcf)   step pmcf 600 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 20 --warmup 20 --fused-plies 0 ;;
-    pmcw)   step pmcw 600 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 20 --warmup 20 --fused-plies 0 ;;
-    pmcv)   step pmcv 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES -d $OUT/pmc_valu -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 20 --warmup 20 --fused-plies 0 ;;
+    pmcf)   step pmcf 600 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 20 --warmup 400 --fused-plies 0 ;;
+    pmcw)   step pmcw 600 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 20 --warmup 400 --fused-plies 0 ;;
+    pmcv)   step pmcv 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU -d $OUT/pmc_valu -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 20 --warmup 400 --fused-plies 0 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
