@@ -33,6 +33,7 @@ __device__ __forceinline__ void gc_stamp(int k) {
 #endif
 #include "gc_core.h"
 #include "gc_env.h"
+#include "gc_perft.h"
 #include "../../include/gymchess.h"
 
 using namespace gc;
@@ -226,102 +227,39 @@ __global__ void k_update_state(SoA st) {
 }
 
 // ----------------------------------------------------------------------------- perft
-// perft(s, d) = sum over get_all_possible_moves of perft(next_state, d-1), perft(s,1) = #moves
-// (SURVEY §3.4).  Per-lane iterative DFS; bulk count at depth 1.
+// Leaves: one lane = one subtree of depth <= 3 (gc_perft.h).  Interior levels: expand every
+// node of a level into its children (count, exclusive scan, write), level by level, until
+// the subtrees are small enough and numerous enough to fill the chip; then sum back up.
 #define PERFT_MAXD 8
-struct Frame {
-    Pos s;
-    Gen g;
-    u64 pcs;   // own pieces not yet expanded
-    u64 tg;    // remaining targets of the current piece
-    int sq;    // current piece square
-    u32 cast;  // remaining castle bits
+struct LdsScratch2 {  // second scratch region (perft's second interior level)
+    u64* base;
+    __device__ void put(int j, u64 v) { base[j * BLOCK] = v; }
+    __device__ u64 get(int j) const { return base[j * BLOCK]; }
 };
 
-__device__ Pos child_of(const Pos& s, bool white, int action) {
-    Pos c = s;
-    int rw;
-    bool irrev;
-    apply_move(c, white, action, &rw, &irrev);
-    // each engine call re-reads the dict: State::new forces rights by king presence
-    c.meta = (c.meta & ~(u32)M_RIGHTS) | eff_rights(c);
-    return c;
-}
-
-__device__ uint64_t perft_lane(const Pos& root, int depth) {
-    if (depth <= 0) return 1;
-    Frame st[PERFT_MAXD];
-    uint64_t nodes = 0;
-    int top = 0;
-    st[0].s = root;
-    gen_init(st[0].s, st[0].g);
-    NoScratch ns;
-    MoveSet ms;
-    if (depth == 1) {
-        gen_moves(st[0].s, st[0].g, ms, ns);
-        return (uint64_t)ms.total;
-    }
-    st[0].pcs = st[0].g.own;
-    st[0].tg = 0;
-    st[0].sq = -1;
-    st[0].cast = st[0].g.castles;
-    while (top >= 0) {
-        Frame& f = st[top];
-        int action = -1;
-        if (f.tg) {
-            int t = ctz(f.tg);
-            f.tg &= f.tg - 1;
-            action = f.sq * 64 + t;
-        } else if (f.pcs) {
-            f.sq = ctz(f.pcs);
-            f.pcs &= f.pcs - 1;
-            f.tg = legal_targets(f.s, f.g, f.sq, type_at(f.s, f.sq));
-            continue;
-        } else if (f.cast) {
-            int c = ctz((u64)f.cast);
-            f.cast &= f.cast - 1;
-            action = c == 0 ? (f.g.white ? A_QSW : A_QSB) : (f.g.white ? A_KSW : A_KSB);
-        } else {
-            top--;
-            continue;
-        }
-        Pos c = child_of(f.s, f.g.white, action);
-        int remaining = depth - 1 - top;  // depth of the child subtree
-        if (remaining == 1) {
-            Gen g;
-            gen_init(c, g);
-            gen_moves(c, g, ms, ns);
-            nodes += (uint64_t)ms.total;
-        } else {
-            Frame& nf = st[top + 1];
-            nf.s = c;
-            gen_init(nf.s, nf.g);
-            nf.pcs = nf.g.own;
-            nf.tg = 0;
-            nf.sq = -1;
-            nf.cast = nf.g.castles;
-            top++;
-        }
-    }
-    return nodes;
-}
-
-__global__ void k_perft(SoA in, int depth, uint64_t* __restrict__ nodes) {
+__global__ void __launch_bounds__(BLOCK) k_perft_small(SoA in, int depth, uint64_t* __restrict__ nodes) {
+    __shared__ u64 lds_a[SCRATCH_SLOTS * BLOCK];
+    __shared__ u64 lds_b[SCRATCH_SLOTS * BLOCK];
+    LdsScratch sa{lds_a + threadIdx.x};
+    LdsScratch2 sb{lds_b + threadIdx.x};
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= in.n) return;
-    nodes[i] = perft_lane(in.load(i), depth);
+    nodes[i] = perft_small(in.load(i), depth, sa, sb);
 }
 
-// split: children of every root, written at offs[i] .. offs[i]+cnt[i] (offs = exclusive scan)
+// children of every node, written at offs[i] .. offs[i]+cnt[i] (offs = exclusive scan)
 __global__ void k_count_children(SoA in, int32_t* __restrict__ cnt) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= in.n) return;
     Pos s = in.load(i);
     Gen g;
+    MoveSet ms;
+    NoScratch none;
     gen_init(s, g);
-    cnt[i] = count_legal(s, g);
+    gen_moves(s, g, ms, none);
+    cnt[i] = ms.total;
 }
-__global__ void k_expand(SoA in, const int32_t* __restrict__ offs, SoA out, int32_t* __restrict__ parent) {
+__global__ void k_expand(SoA in, const int32_t* __restrict__ offs, SoA out) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= in.n) return;
     Pos s = in.load(i);
@@ -336,25 +274,19 @@ __global__ void k_expand(SoA in, const int32_t* __restrict__ offs, SoA out, int3
         while (tg) {
             int t = ctz(tg);
             tg &= tg - 1;
-            out.store(o, child_of(s, g.white, sq * 64 + t));
-            parent[o++] = i;
+            out.store(o++, child_of(s, g.white, sq * 64 + t));
         }
     }
-    if (g.castles & 1) { out.store(o, child_of(s, g.white, g.white ? A_QSW : A_QSB)); parent[o++] = i; }
-    if (g.castles & 2) { out.store(o, child_of(s, g.white, g.white ? A_KSW : A_KSB)); parent[o++] = i; }
+    if (g.castles & 1) out.store(o++, child_of(s, g.white, g.white ? A_QSW : A_QSB));
+    if (g.castles & 2) out.store(o++, child_of(s, g.white, g.white ? A_KSW : A_KSB));
 }
-// per-task perft + deterministic per-root sum (tasks of one root are contiguous)
-__global__ void k_perft_tasks(SoA tasks, int depth, uint64_t* __restrict__ nodes) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= tasks.n) return;
-    nodes[i] = perft_lane(tasks.load(i), depth);
-}
-__global__ void k_sum_tasks(const int32_t* __restrict__ offs, const int32_t* __restrict__ cnt,
-                            const uint64_t* __restrict__ tnodes, int n, uint64_t* __restrict__ out) {
+// parent value = sum of its children's values (children of one parent are contiguous)
+__global__ void k_sum_children(const int32_t* __restrict__ offs, const int32_t* __restrict__ cnt,
+                               const uint64_t* __restrict__ child, int n, uint64_t* __restrict__ out) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     uint64_t s = 0;
-    for (int k = 0; k < cnt[i]; k++) s += tnodes[offs[i] + k];
+    for (int k = 0; k < cnt[i]; k++) s += child[offs[i] + k];
     out[i] = s;
 }
 
@@ -750,53 +682,85 @@ extern "C" int gc_engine_update_state(gc_engine* e, int n, const int8_t* boards,
     return 0;
 }
 
-// perft over n roots.  split_depth > 0 expands every root into its children first (one
-// lane per child subtree) so that few roots still fill the chip.
+// perft over n roots (side to move = meta[0]).  Levels are expanded on the device while
+// more than 3 plies remain, or while there are too few subtrees to fill the chip.
+static int perft_device(hipStream_t st, SoA roots, int depth, uint64_t* d_out) {
+    struct Level {
+        u64* bb = nullptr; u32* meta = nullptr; int32_t* cnt = nullptr; int32_t* offs = nullptr;
+        uint64_t* val = nullptr; int n = 0;
+    };
+    std::vector<Level> lv(1);
+    lv[0].bb = roots.bb; lv[0].meta = roots.meta; lv[0].n = roots.n;
+    int rem = depth;
+    int rc = 0;
+    std::string err;
+    auto cleanup = [&]() {
+        for (size_t l = 0; l < lv.size(); l++) {
+            if (l > 0) { (void)hipFree(lv[l].bb); (void)hipFree(lv[l].meta); }
+            (void)hipFree(lv[l].cnt); (void)hipFree(lv[l].offs);
+            if (l > 0) (void)hipFree(lv[l].val);
+        }
+    };
+    while (rem > 3 || (rem >= 2 && lv.back().n < 131072)) {
+        Level& cur = lv.back();
+        if (dalloc(&cur.cnt, cur.n) || dalloc(&cur.offs, cur.n)) { cleanup(); return -1; }
+        SoA cs{cur.bb, cur.meta, cur.n};
+        k_count_children<<<grid_for(cur.n), BLOCK, 0, st>>>(cs, cur.cnt);
+        size_t tmp_bytes = 0;
+        void* tmp = nullptr;
+        hipError_t he = hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, cur.cnt, cur.offs, cur.n, st);
+        if (he == hipSuccess && dalloc((char**)&tmp, tmp_bytes) == 0)
+            he = hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, cur.cnt, cur.offs, cur.n, st);
+        int32_t lo = 0, lc = 0;
+        if (he == hipSuccess) he = hipMemcpyAsync(&lo, cur.offs + cur.n - 1, 4, hipMemcpyDeviceToHost, st);
+        if (he == hipSuccess) he = hipMemcpyAsync(&lc, cur.cnt + cur.n - 1, 4, hipMemcpyDeviceToHost, st);
+        if (he == hipSuccess) he = hipStreamSynchronize(st);
+        (void)hipFree(tmp);
+        if (he != hipSuccess) { cleanup(); return fail(std::string("perft scan: ") + hipGetErrorString(he)); }
+        int64_t total = (int64_t)lo + lc;
+        if (total > (int64_t)1 << 29) { cleanup(); return fail("perft: level too large (split roots into batches)"); }
+        Level nx;
+        nx.n = (int)total;
+        if (dalloc(&nx.bb, (size_t)NBB * (total ? total : 1)) || dalloc(&nx.meta, total ? total : 1)) {
+            cleanup();
+            return -1;
+        }
+        SoA ns{nx.bb, nx.meta, nx.n};
+        k_expand<<<grid_for(cur.n), BLOCK, 0, st>>>(cs, cur.offs, ns);
+        lv.push_back(nx);
+        rem--;
+        if (total == 0) break;
+    }
+    Level& leaf = lv.back();
+    if (lv.size() > 1 && dalloc(&leaf.val, leaf.n ? leaf.n : 1)) { cleanup(); return -1; }
+    uint64_t* leaf_out = lv.size() > 1 ? leaf.val : d_out;
+    if (leaf.n > 0) {
+        SoA ls{leaf.bb, leaf.meta, leaf.n};
+        k_perft_small<<<grid_for(leaf.n), BLOCK, 0, st>>>(ls, rem, leaf_out);
+    }
+    for (int l = (int)lv.size() - 2; l >= 0; l--) {
+        uint64_t* dst = l == 0 ? d_out : lv[l].val;
+        if (l > 0 && dalloc(&lv[l].val, lv[l].n)) { cleanup(); return -1; }
+        dst = l == 0 ? d_out : lv[l].val;
+        k_sum_children<<<grid_for(lv[l].n), BLOCK, 0, st>>>(lv[l].offs, lv[l].cnt, lv[l + 1].val, lv[l].n, dst);
+    }
+    hipError_t he = hipGetLastError();
+    if (he == hipSuccess) he = hipStreamSynchronize(st);
+    if (he != hipSuccess) { err = std::string("perft kernels: ") + hipGetErrorString(he); rc = -1; }
+    cleanup();
+    if (rc) return fail(err);
+    return 0;
+}
+
 extern "C" int gc_engine_perft(gc_engine* e, int n, const int8_t* boards, const uint8_t* meta, int depth,
                                uint64_t* nodes) {
     if (!e || !nodes) return fail("null argument");
     if (depth < 0 || depth > PERFT_MAXD) return fail("depth must be in [0, 8]");
     if (engine_reserve(e, n, 1)) return -1;
     if (engine_upload(e, n, boards, meta, nullptr)) return -1;
-    SoA roots{e->bb, e->meta, n};
-    if (depth <= 2) {
-        k_perft<<<grid_for(n), BLOCK, 0, e->stream>>>(roots, depth, e->u64o);
-        HIPCHK(hipGetLastError());
-        HIPCHK(hipMemcpyAsync(nodes, e->u64o, (size_t)8 * n, hipMemcpyDeviceToHost, e->stream));
-        HIPCHK(hipStreamSynchronize(e->stream));
-        return 0;
-    }
-    // split at depth 1: tasks = children of every root
-    int32_t *cnt = e->i32a, *offs = e->i32b;
-    k_count_children<<<grid_for(n), BLOCK, 0, e->stream>>>(roots, cnt);
-    HIPCHK(hipGetLastError());
-    size_t tmp_bytes = 0;
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, cnt, offs, n, e->stream));
-    void* tmp = nullptr;
-    if (dalloc((char**)&tmp, tmp_bytes)) return -1;
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, cnt, offs, n, e->stream));
-    int32_t last_off = 0, last_cnt = 0;
-    HIPCHK(hipMemcpyAsync(&last_off, offs + n - 1, 4, hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(hipMemcpyAsync(&last_cnt, cnt + n - 1, 4, hipMemcpyDeviceToHost, e->stream));
+    if (perft_device(e->stream, SoA{e->bb, e->meta, n}, depth, e->u64o)) return -1;
+    HIPCHK(hipMemcpyAsync(nodes, e->u64o, (size_t)8 * n, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
-    (void)hipFree(tmp);
-    int nt = last_off + last_cnt;
-    if (nt == 0) {
-        for (int i = 0; i < n; i++) nodes[i] = 0;
-        return 0;
-    }
-    u64* tbb = nullptr; u32* tmeta = nullptr; int32_t* parent = nullptr; uint64_t* tnodes = nullptr;
-    if (dalloc(&tbb, (size_t)NBB * nt) || dalloc(&tmeta, nt) || dalloc(&parent, nt) || dalloc(&tnodes, nt)) return -1;
-    SoA tasks{tbb, tmeta, nt};
-    k_expand<<<grid_for(n), BLOCK, 0, e->stream>>>(roots, offs, tasks, parent);
-    k_perft_tasks<<<grid_for(nt), BLOCK, 0, e->stream>>>(tasks, depth - 1, tnodes);
-    k_sum_tasks<<<grid_for(n), BLOCK, 0, e->stream>>>(offs, cnt, tnodes, n, e->u64o);
-    hipError_t le = hipGetLastError();
-    hipError_t ce = hipMemcpyAsync(nodes, e->u64o, (size_t)8 * n, hipMemcpyDeviceToHost, e->stream);
-    hipError_t se = hipStreamSynchronize(e->stream);
-    (void)hipFree(tbb); (void)hipFree(tmeta); (void)hipFree(parent); (void)hipFree(tnodes);
-    if (le != hipSuccess || ce != hipSuccess || se != hipSuccess)
-        return fail(std::string("perft kernels failed: ") + hipGetErrorString(le != hipSuccess ? le : (ce != hipSuccess ? ce : se)));
     return 0;
 }
 

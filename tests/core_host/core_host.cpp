@@ -250,3 +250,22 @@ extern "C" int host_env_moves(void* p, uint16_t* out, int cap) {
     export_state(e->s, b, m);
     return host_list(b, m, -1, 0, out, cap);
 }
+
+// perft via the device algorithm (gc_perft.h): levels > 3 expanded recursively here
+#include "../../gym-chess_amd/csrc/gc_perft.h"
+static uint64_t perft_split(const Pos& s, int d) {
+    if (d <= 3) {
+        HostScratch a, b;
+        return perft_small(s, d, a, b);
+    }
+    Gen g;
+    gen_init(s, g);
+    uint64_t tot = 0;
+    int n = count_legal(s, g);
+    for (int k = 0; k < n; k++) tot += perft_split(child_of(s, g.white, select_legal(s, g, k)), d - 1);
+    return tot;
+}
+extern "C" uint64_t host_perft_small(const int8_t* b, const uint8_t* m, int depth) {
+    Pos s = import_state(b, m, -1);
+    return perft_split(s, depth);
+}

@@ -30,6 +30,8 @@ def lib():
         L.host_side_attacks.argtypes = [P, ctypes.c_int]
         L.host_perft.restype = ctypes.c_uint64
         L.host_perft.argtypes = [P, P, ctypes.c_int]
+        L.host_perft_small.restype = ctypes.c_uint64
+        L.host_perft_small.argtypes = [P, P, ctypes.c_int]
         L.host_list.argtypes = [P, P, ctypes.c_int, ctypes.c_int, P, ctypes.c_int]
         L.host_count.argtypes = [P, P, ctypes.c_int]
         L.host_count2.argtypes = [P, P, ctypes.c_int]
@@ -110,6 +112,11 @@ def update_state(board, meta):
 def perft(board, meta, depth):
     b, m = _bm(board, meta)
     return int(lib().host_perft(_p(b), _p(m), int(depth)))
+
+
+def perft_small(board, meta, depth):
+    b, m = _bm(board, meta)
+    return int(lib().host_perft_small(_p(b), _p(m), int(depth)))
 
 
 def rollout_trace(seed, board_id, plies, init):

@@ -110,7 +110,14 @@ def test_fuzz_perft(oracle):
     boards, metas = random_positions(40, 77)
     for i in range(len(boards)):
         for d in (1, 2, 3):
-            assert H.perft(boards[i], metas[i], d) == oracle.perft(boards[i], metas[i], d), (i, d)
+            ref = oracle.perft(boards[i], metas[i], d)
+            assert H.perft(boards[i], metas[i], d) == ref, (i, d)
+            assert H.perft_small(boards[i], metas[i], d) == ref, (i, d)
+
+
+def test_perft_small_startpos(oracle):
+    b, m = oracle.DEFAULT_BOARD, oracle.make_meta()
+    assert [H.perft_small(b, m, d) for d in range(0, 5)] == [1, 20, 400, 8982, 200915]
 
 
 def test_rollout_trajectories(oracle):
