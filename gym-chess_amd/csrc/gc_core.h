@@ -468,8 +468,9 @@ GC_HD int select_legal(const Pos& s, const Gen& g, int k) {
 // type serialises every type's code on every iteration.  Here each loop handles ONE piece
 // type (lanes differ only in trip count) and pawns are done set-wise.  The targets of every
 // other piece are parked in a per-lane scratch slot (LDS on the device) under the piece's
-// ordinal among the side's pieces -- its position in the reference's row-major scan
-// (lib.rs:510-511) -- so the ordered pick reads them back instead of regenerating them.
+// ordinal among the side's pieces (its position in the row-major scan, lib.rs:510-511),
+// and every piece's move count is recorded bit-sliced in 5 bitboards (cnt[b] bit sq = bit b
+// of the count of the piece on sq), so a pick by rank needs no per-piece loop.
 static constexpr int SCRATCH_SLOTS = 16;
 static constexpr u64 ROW1 = 0xFFull << 8;   // black pawns' start row (lib.rs:947)
 static constexpr u64 ROW6 = 0xFFull << 48;  // white pawns' start row (lib.rs:946)
@@ -477,11 +478,13 @@ static constexpr u64 ROW6 = 0xFFull << 48;  // white pawns' start row (lib.rs:94
 struct MoveSet {
     u64 fastp;            // own pawns handled set-wise (the unpinned ones)
     u64 o1, o2, ol, orr;  // fast pawns with: single push, double push, capture c+1, capture c-1
+    u64 cnt[5];           // bit-sliced per-square move counts (< 32) of all own pieces
     int total;            // legal move count including castles
     bool big;             // more own pieces than scratch slots: per-square fallback
 };
 
-struct NoScratch {  // count-only callers (perft leaves)
+struct NoScratch {  // count-only callers (perft leaves): no parking, no count planes
+    static constexpr bool kPark = false;
     GC_HDM void put(int, u64) {}
     GC_HDM u64 get(int) const { return 0; }
 };
@@ -489,8 +492,22 @@ struct NoScratch {  // count-only callers (perft leaves)
 GC_HD int ordinal(u64 own, int sq) { return popc(own & (bit(sq) - 1)); }
 
 template <class S>
+GC_HD void park(MoveSet& ms, S& scr, u64 own, int sq, u64 tg, int& total) {
+    int c = popc(tg);
+    total += c;
+    if (S::kPark) {
+        scr.put(ordinal(own, sq), tg);
+        u64 m = bit(sq);
+#pragma unroll
+        for (int b = 0; b < 5; b++) ms.cnt[b] |= ((c >> b) & 1) ? m : 0ull;
+    }
+}
+
+template <class S>
 GC_HD void gen_moves(const Pos& s, const Gen& g, MoveSet& ms, S& scr) {
     ms.fastp = ms.o1 = ms.o2 = ms.ol = ms.orr = 0;
+#pragma unroll
+    for (int b = 0; b < 5; b++) ms.cnt[b] = 0;
     ms.big = popc(g.own) > SCRATCH_SLOTS;
     if (ms.big) {
         ms.total = count_legal(s, g);
@@ -513,21 +530,24 @@ GC_HD void gen_moves(const Pos& s, const Gen& g, MoveSet& ms, S& scr) {
     }
     ms.fastp = fp;
     total += popc(ms.o1) + popc(ms.o2) + popc(ms.ol) + popc(ms.orr);
+    if (S::kPark) {  // per-pawn counts o1+o2+ol+orr (0..4) as a bit-sliced sum
+        u64 s1 = ms.o1 ^ ms.o2, c1 = ms.o1 & ms.o2, s2 = ms.ol ^ ms.orr, c2 = ms.ol & ms.orr;
+        u64 b0 = s1 ^ s2, k0 = s1 & s2;
+        ms.cnt[0] = b0;
+        ms.cnt[1] = c1 ^ c2 ^ k0;
+        ms.cnt[2] = (c1 & c2) | (k0 & (c1 ^ c2));
+    }
     u64 pp = P & g.pinned;  // pinned pawns: rare, per piece
     while (pp) {
         int sq = ctz(pp);
         pp &= pp - 1;
-        u64 tg = legal_targets(s, g, sq, PAWN);
-        scr.put(ordinal(own, sq), tg);
-        total += popc(tg);
+        park(ms, scr, own, sq, legal_targets(s, g, sq, PAWN), total);
     }
     u64 x = s.n & own;  // a pinned knight never has a move on its pin segment
     while (x) {
         int sq = ctz(x);
         x &= x - 1;
-        u64 tg = ((g.pinned >> sq) & 1) ? 0 : knight_set(bit(sq)) & notown_cm;
-        scr.put(ordinal(own, sq), tg);
-        total += popc(tg);
+        park(ms, scr, own, sq, ((g.pinned >> sq) & 1) ? 0 : knight_set(bit(sq)) & notown_cm, total);
     }
     x = s.b & own;
     while (x) {
@@ -535,8 +555,7 @@ GC_HD void gen_moves(const Pos& s, const Gen& g, MoveSet& ms, S& scr) {
         x &= x - 1;
         u64 tg = bishop_att(sq, g.occ) & notown_cm;
         if ((g.pinned >> sq) & 1) tg &= g.pinrays & line_through(g.ks, sq);
-        scr.put(ordinal(own, sq), tg);
-        total += popc(tg);
+        park(ms, scr, own, sq, tg, total);
     }
     x = s.r & own;
     while (x) {
@@ -544,8 +563,7 @@ GC_HD void gen_moves(const Pos& s, const Gen& g, MoveSet& ms, S& scr) {
         x &= x - 1;
         u64 tg = rook_att(sq, g.occ) & notown_cm;
         if ((g.pinned >> sq) & 1) tg &= g.pinrays & line_through(g.ks, sq);
-        scr.put(ordinal(own, sq), tg);
-        total += popc(tg);
+        park(ms, scr, own, sq, tg, total);
     }
     x = s.q & own;
     while (x) {
@@ -553,18 +571,75 @@ GC_HD void gen_moves(const Pos& s, const Gen& g, MoveSet& ms, S& scr) {
         x &= x - 1;
         u64 tg = (rook_att(sq, g.occ) | bishop_att(sq, g.occ)) & notown_cm;
         if ((g.pinned >> sq) & 1) tg &= g.pinrays & line_through(g.ks, sq);
-        scr.put(ordinal(own, sq), tg);
-        total += popc(tg);
+        park(ms, scr, own, sq, tg, total);
     }
     x = s.k & own;  // every own king; filtered by the pre-move enemy map only (lib.rs:613-619)
     while (x) {
         int sq = ctz(x);
         x &= x - 1;
-        u64 tg = king_set(bit(sq)) & ~own & ~g.enemy_att;
-        scr.put(ordinal(own, sq), tg);
-        total += popc(tg);
+        park(ms, scr, own, sq, king_set(bit(sq)) & ~own & ~g.enemy_att, total);
     }
     ms.total = total;
+}
+
+// ---- pick by rank in ACTION-ID order (the random self-play policy) ----------------------
+// The driver draws k uniformly in [0, #legal); k maps to the k-th legal action in ascending
+// action id (from*64+to, castles 4096.. last) -- the order of the legal-action mask, i.e.
+// how a policy over the 4101-action space samples.  Any fixed bijection gives the same
+// uniform policy; this one needs no per-piece loop: a 6-step binary search over the
+// bit-sliced prefix counts finds the from-square, a 6-step popcount search the target.
+GC_HD int prefix_count(const u64* cnt, u64 below) {
+    return popc(cnt[0] & below) + 2 * popc(cnt[1] & below) + 4 * popc(cnt[2] & below) +
+           8 * popc(cnt[3] & below) + 16 * popc(cnt[4] & below);
+}
+GC_HD int kth_set_bit(u64 x, int k) {  // 0-based, ascending; x has > k set bits
+    int base = 0;
+    u32 lo = (u32)x, c = (u32)__builtin_popcount(lo);
+    u32 v = lo;
+    if ((u32)k >= c) { k -= (int)c; v = (u32)(x >> 32); base = 32; }
+#pragma unroll
+    for (int w = 16; w; w >>= 1) {
+        u32 m = (1u << w) - 1;
+        int cc = __builtin_popcount(v & m);
+        if (k >= cc) { k -= cc; v >>= w; base += w; }
+    }
+    return base;
+}
+GC_HD u64 fast_pawn_targets(const MoveSet& ms, int sq, bool white) {
+    u64 t = 0;
+    if ((ms.o1 >> sq) & 1) t |= bit(white ? sq - 8 : sq + 8);
+    if ((ms.o2 >> sq) & 1) t |= bit(white ? sq - 16 : sq + 16);
+    if ((ms.ol >> sq) & 1) t |= bit(white ? sq - 7 : sq + 9);
+    if ((ms.orr >> sq) & 1) t |= bit(white ? sq - 9 : sq + 7);
+    return t;
+}
+template <class S>
+GC_HD int select_action(const Pos& s, const Gen& g, const MoveSet& ms, const S& scr, int k) {
+    int normal = ms.total - popc(g.castles);
+    if (k >= normal) {  // castles: KS (4096 / 4098) sorts before QS (4097 / 4099)
+        k -= normal;
+        if (g.castles & 2) { if (k == 0) return g.white ? A_KSW : A_KSB; k--; }
+        return g.white ? A_QSW : A_QSB;
+    }
+    if (ms.big) {  // per-square fallback (> SCRATCH_SLOTS own pieces)
+        u64 pcs = g.own;
+        while (pcs) {
+            int sq = ctz(pcs);
+            pcs &= pcs - 1;
+            u64 tg = legal_targets(s, g, sq, type_at(s, sq));
+            int c = popc(tg);
+            if (k < c) return sq * 64 + kth_set_bit(tg, k);
+            k -= c;
+        }
+        return A_NONE;
+    }
+    int lo = 0;  // largest square whose prefix count (squares below it) is <= k
+#pragma unroll
+    for (int step = 32; step; step >>= 1)
+        if (prefix_count(ms.cnt, bit(lo + step) - 1) <= k) lo += step;
+    k -= prefix_count(ms.cnt, bit(lo) - 1);
+    u64 tg = ((ms.fastp >> lo) & 1) ? fast_pawn_targets(ms, lo, g.white) : scr.get(ordinal(g.own, lo));
+    return lo * 64 + kth_set_bit(tg, k);
 }
 
 // k-th legal action (0 <= k < ms.total) in reference order, from gen_moves' results

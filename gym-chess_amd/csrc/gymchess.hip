@@ -111,6 +111,7 @@ struct DevHist {
 // per-lane move-target scratch in LDS: slot j of lane t at lds[j*BLOCK + t] (each wave's
 // ds_read_b64/ds_write_b64 touches 512 contiguous bytes: conflict-free)
 struct LdsScratch {
+    static constexpr bool kPark = true;
     u64* base;
     __device__ void put(int j, u64 v) { base[j * BLOCK] = v; }
     __device__ u64 get(int j) const { return base[j * BLOCK]; }
@@ -231,17 +232,12 @@ __global__ void k_update_state(SoA st) {
 // node of a level into its children (count, exclusive scan, write), level by level, until
 // the subtrees are small enough and numerous enough to fill the chip; then sum back up.
 #define PERFT_MAXD 8
-struct LdsScratch2 {  // second scratch region (perft's second interior level)
-    u64* base;
-    __device__ void put(int j, u64 v) { base[j * BLOCK] = v; }
-    __device__ u64 get(int j) const { return base[j * BLOCK]; }
-};
 
 __global__ void __launch_bounds__(BLOCK) k_perft_small(SoA in, int depth, uint64_t* __restrict__ nodes) {
     __shared__ u64 lds_a[SCRATCH_SLOTS * BLOCK];
     __shared__ u64 lds_b[SCRATCH_SLOTS * BLOCK];
     LdsScratch sa{lds_a + threadIdx.x};
-    LdsScratch2 sb{lds_b + threadIdx.x};
+    LdsScratch sb{lds_b + threadIdx.x};
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= in.n) return;
     nodes[i] = perft_small(in.load(i), depth, sa, sb);
@@ -304,6 +300,18 @@ struct EnvDev {
     u64 init[NBB];   // 7 bitboards of the initial board (kernel argument: scalar loads)
     uint64_t seed;
     int n;
+    // Every reset lands on the same position: its state, move set and parked targets are
+    // computed once at env creation (k_init_cache) and passed here by value.
+    struct InitCache {
+        Pos pos;
+        u64 own, fastp, o1, o2, ol, orr;
+        u64 cnt[5];
+        u64 slots[SCRATCH_SLOTS];
+        int total;
+        u32 castles;
+        int white;
+        int usable;  // 0: the start position needs the per-square fallback (> 16 pieces)
+    } ic;
     __device__ DevHist hist(int i, u32 g) const { return DevHist{htab, hgen, g, i}; }
 };
 
@@ -323,17 +331,56 @@ __device__ Pos init_pos(const u64* init) {
 }
 
 // reset (chess_v2.py:183-206); the generation bump empties the repetition window
-__device__ void reset_board(Pos& s, DevHist& h, const u64* init) {
-    s = init_pos(init);
+__device__ void reset_board(const EnvDev& e, Pos& s, DevHist& h) {
+    s = e.ic.pos;
     h.bump_gen();
 }
 
-// policy: uniform choice among the reference-ordered legal list (test_benchmark.py:22-27)
+// move set of the current position: cached for a freshly reset board, else generated
+__device__ void moves_after_reset(const EnvDev& e, const Pos& s, Gen& g, MoveSet& ms, LdsScratch& scr) {
+    if (!e.ic.usable) {
+        gen_init(s, g);
+        gen_moves(s, g, ms, scr);
+        return;
+    }
+    g.white = e.ic.white;
+    g.own = e.ic.own;
+    g.castles = e.ic.castles;
+    ms.fastp = e.ic.fastp; ms.o1 = e.ic.o1; ms.o2 = e.ic.o2; ms.ol = e.ic.ol; ms.orr = e.ic.orr;
+#pragma unroll
+    for (int b = 0; b < 5; b++) ms.cnt[b] = e.ic.cnt[b];
+    ms.total = e.ic.total;
+    ms.big = false;
+#pragma unroll
+    for (int j = 0; j < SCRATCH_SLOTS; j++) scr.put(j, e.ic.slots[j]);
+}
+
+__global__ void __launch_bounds__(BLOCK) k_init_cache(EnvDev e, EnvDev::InitCache* out) {
+    LDS_SCRATCH_DECL;
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    EnvDev::InitCache c = {};
+    c.pos = init_pos(e.init);
+    Gen g;
+    MoveSet ms;
+    gen_init(c.pos, g);
+    gen_moves(c.pos, g, ms, scr);
+    c.own = g.own; c.fastp = ms.fastp; c.o1 = ms.o1; c.o2 = ms.o2; c.ol = ms.ol; c.orr = ms.orr;
+    for (int b = 0; b < 5; b++) c.cnt[b] = ms.cnt[b];
+    for (int j = 0; j < SCRATCH_SLOTS; j++) c.slots[j] = ms.big ? 0 : scr.get(j);
+    c.total = ms.total;
+    c.castles = g.castles;
+    c.white = g.white;
+    c.usable = !ms.big;
+    *out = c;
+}
+
+// policy: uniform choice among the legal actions (test_benchmark.py:22-27); rank k maps to
+// the k-th legal action in action-id order (gc_core.h select_action)
 __device__ uint16_t pick(const Pos& s, const Gen& g, const MoveSet& ms, const LdsScratch& scr, uint64_t seed,
                          int i, u32& draw) {
     if (ms.total == 0) return (uint16_t)A_NONE;
     u32 k = policy_index(seed, (u32)i, draw++, (u32)ms.total);
-    return (uint16_t)select_move(s, g, ms, scr, (int)k);
+    return (uint16_t)select_action(s, g, ms, scr, (int)k);
 }
 
 __global__ void __launch_bounds__(BLOCK) k_env_reset(EnvDev e, const uint8_t* __restrict__ mask, int select) {
@@ -344,14 +391,13 @@ __global__ void __launch_bounds__(BLOCK) k_env_reset(EnvDev e, const uint8_t* __
     u32 g0 = e.hgen[i];
     DevHist h = e.hist(i, g0);
     Pos s;
-    reset_board(s, h, e.init);
+    reset_board(e, s, h);
     h.flush(g0);
     e.st.store(i, s);
     if (select) {
         Gen g;
         MoveSet ms;
-        gen_init(s, g);
-        gen_moves(s, g, ms, scr);
+        moves_after_reset(e, s, g, ms, scr);
         u32 d = e.draw[i];
         e.act[i] = pick(s, g, ms, scr, e.seed, i, d);
         e.draw[i] = d;
@@ -395,7 +441,7 @@ __global__ void __launch_bounds__(BLOCK) k_env_step(EnvDev e) {
     MoveSet ms;
     bool have = false;
     if (POLICY && a == A_NONE) {
-        reset_board(s, h, e.init);
+        reset_board(e, s, h);
         o.reason = R_NO_MOVES;
     } else {
         if (POLICY) {
@@ -408,15 +454,12 @@ __global__ void __launch_bounds__(BLOCK) k_env_step(EnvDev e) {
         have = o.moved;
         nst += 1;
         if (POLICY && o.done) {
-            reset_board(s, h, e.init);
+            reset_board(e, s, h);
             have = false;
         }
     }
     if (POLICY) {
-        if (!have) {
-            gen_init(s, g);
-            gen_moves(s, g, ms, scr);
-        }
+        if (!have) moves_after_reset(e, s, g, ms, scr);
         GC_STAMP(6);
         e.act[i] = pick(s, g, ms, scr, e.seed, i, d);
         e.draw[i] = d;
@@ -434,7 +477,8 @@ __global__ void __launch_bounds__(BLOCK) k_env_step(EnvDev e) {
     e.reason[i] = (uint8_t)o.reason;
 }
 
-// Fused K-ply random self-play: state in registers for the whole launch.  Optional per-ply
+// Fused K-ply random self-play: state in registers for the whole launch.  Per-ply outputs
+// (reward / done / reason) are written every ply, like the one-ply kernel; optional per-ply
 // trace [ply][N] (tests).  stats per board: [steps, reward_sum(two's complement), ends[0..5]]
 __global__ void __launch_bounds__(BLOCK) k_env_rollout(EnvDev e, int plies, int16_t* tr_action, int16_t* tr_reward,
                                                        uint8_t* tr_done, uint8_t* tr_reason, uint64_t* stats) {
@@ -448,14 +492,15 @@ __global__ void __launch_bounds__(BLOCK) k_env_rollout(EnvDev e, int plies, int1
     int a = (int)ua;
     uint64_t steps = 0, rsum = 0;
     u32 e_mate = 0, e_rep = 0, e_cap = 0, e_nomove = 0, e_err = 0;
+    StepOut o = {0, 0, R_NONE, 0};
     for (int p = 0; p < plies; p++) {
-        StepOut o = {0, 0, R_NONE, 0};
+        o = {0, 0, R_NONE, 0};
         Gen g;
         MoveSet ms;
         bool have = false;
         int played = a;
         if (a == A_NONE) {
-            reset_board(s, h, e.init);
+            reset_board(e, s, h);
             o.reason = R_NO_MOVES;
             e_nomove++;
             played = -1;
@@ -469,14 +514,11 @@ __global__ void __launch_bounds__(BLOCK) k_env_rollout(EnvDev e, int plies, int1
                 e_rep += o.reason == R_REPETITION;
                 e_cap += o.reason == R_MOVE_CAP;
                 e_err += o.reason == R_BOTH_CHECKED;
-                reset_board(s, h, e.init);
+                reset_board(e, s, h);
                 have = false;
             }
         }
-        if (!have) {
-            gen_init(s, g);
-            gen_moves(s, g, ms, scr);
-        }
+        if (!have) moves_after_reset(e, s, g, ms, scr);
         if (tr_action) {
             size_t t = (size_t)p * e.n + i;
             tr_action[t] = (int16_t)played;
@@ -484,6 +526,9 @@ __global__ void __launch_bounds__(BLOCK) k_env_rollout(EnvDev e, int plies, int1
             tr_done[t] = (uint8_t)o.done;
             tr_reason[t] = (uint8_t)o.reason;
         }
+        e.reward[i] = o.reward;  // the env.step() outputs of this ply
+        e.done[i] = (uint8_t)o.done;
+        e.reason[i] = (uint8_t)o.reason;
         a = pick(s, g, ms, scr, e.seed, i, d);
     }
     e.st.store(i, s);
@@ -492,10 +537,10 @@ __global__ void __launch_bounds__(BLOCK) k_env_rollout(EnvDev e, int plies, int1
     e.act[i] = (uint16_t)a;
     e.nsteps[i] += (u32)steps;
     if (stats) {
-        uint64_t* o = stats + 8 * (size_t)i;
-        o[0] += steps; o[1] += rsum;
-        o[2 + R_MATE] += e_mate; o[2 + R_REPETITION] += e_rep; o[2 + R_MOVE_CAP] += e_cap;
-        o[2 + R_NO_MOVES] += e_nomove; o[2 + R_BOTH_CHECKED] += e_err;
+        uint64_t* so = stats + 8 * (size_t)i;
+        so[0] += steps; so[1] += rsum;
+        so[2 + R_MATE] += e_mate; so[2 + R_REPETITION] += e_rep; so[2 + R_MOVE_CAP] += e_cap;
+        so[2 + R_NO_MOVES] += e_nomove; so[2 + R_BOTH_CHECKED] += e_err;
     }
 }
 
@@ -834,6 +879,16 @@ extern "C" int gc_env_create(int device, int n_boards, uint64_t seed, const int8
     e->d.st = SoA{e->bb, e->meta, n};
     e->d.seed = seed;
     e->d.n = n;
+    {  // the start position's move set, shared by every reset (EnvDev::ic)
+        EnvDev::InitCache* dic = nullptr;
+        if (dalloc(&dic, 1)) { std::string m = g_err; env_free(e); delete e; return fail(m); }
+        k_init_cache<<<1, BLOCK, 0, e->stream>>>(e->d, dic);
+        he = hipGetLastError();
+        if (he == hipSuccess) he = hipMemcpyAsync(&e->d.ic, dic, sizeof(EnvDev::InitCache), hipMemcpyDeviceToHost, e->stream);
+        if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
+        (void)hipFree(dic);
+        if (he != hipSuccess) { env_free(e); delete e; return fail(std::string("init cache: ") + hipGetErrorString(he)); }
+    }
     k_env_reset<<<grid_for(n), BLOCK, 0, e->stream>>>(e->d, nullptr, 1);
     he = hipGetLastError();
     if (he == hipSuccess) he = hipStreamSynchronize(e->stream);

@@ -519,6 +519,20 @@ uint32_t oracle_policy_index(uint64_t seed, uint32_t board, uint32_t draw, uint3
     return (uint32_t)(((uint64_t)o[0] * n) >> 32);
 }
 
+/* The random policy is uniform over the legal list; rank k maps to the k-th legal action in
+ * ascending action id (the order of a legal-action mask; the device pick uses the same
+ * bijection).  Any fixed bijection gives the same uniform policy. */
+static int kth_in_action_order(const uint16_t *moves, int n, int k) {
+    uint16_t tmp[MAXMOVES];
+    for (int i = 0; i < n; i++) {  /* insertion sort: lists are short */
+        uint16_t v = moves[i];
+        int j = i;
+        while (j > 0 && tmp[j - 1] > v) { tmp[j] = tmp[j - 1]; j--; }
+        tmp[j] = v;
+    }
+    return tmp[k];
+}
+
 /* Random self-play rollout of one board (the test_benchmark.py driver shape, auto-reset):
  * at each ply: if no legal moves -> episode ends (driver `break`), reset, no step counted;
  * else action = moves[policy_index(...)], step; if done -> reset.
@@ -543,7 +557,7 @@ static void rollout_board(const int8_t *init, uint64_t seed, uint32_t board, int
             o_env_reset(&e);
         } else {
             uint32_t k = oracle_policy_index(seed, board, draw++, (uint32_t)e.nmoves);
-            action = e.moves[k];
+            action = kth_in_action_order(e.moves, e.nmoves, (int)k);
             int rc = o_env_step(&e, action, &rw, &dn, &reason);
             st->steps++;
             st->reward_sum += (uint64_t)(int64_t)rw;

@@ -138,6 +138,7 @@ struct HostHist {  // same contract as the device DevHist (gc_env.h rep_prefetch
 };
 
 struct HostScratch {
+    static constexpr bool kPark = true;
     u64 v[SCRATCH_SLOTS];
     void put(int j, u64 x) { v[j] = x; }
     u64 get(int j) const { return v[j]; }
@@ -161,6 +162,15 @@ extern "C" int host_select2(const int8_t* b, const uint8_t* m, int white, int k)
     gen_moves(s, g, ms, scr);
     return select_move(s, g, ms, scr, k);
 }
+extern "C" int host_select_action(const int8_t* b, const uint8_t* m, int white, int k) {
+    Pos s = import_state(b, m, white);
+    Gen g;
+    gen_init(s, g);
+    MoveSet ms;
+    HostScratch scr;
+    gen_moves(s, g, ms, scr);
+    return select_action(s, g, ms, scr, k);
+}
 
 static void host_reset(Pos& s, HostHist& h, const Pos& ip) {
     s = env_reset_pos(ip);
@@ -180,7 +190,7 @@ extern "C" void host_rollout_trace(const int8_t* init, uint64_t seed, uint32_t b
     MoveSet ms;
     gen_init(s, g);
     gen_moves(s, g, ms, scr);
-    int a = ms.total ? select_move(s, g, ms, scr, (int)policy_index(seed, board, draw++, (u32)ms.total)) : A_NONE;
+    int a = ms.total ? select_action(s, g, ms, scr, (int)policy_index(seed, board, draw++, (u32)ms.total)) : A_NONE;
     uint64_t steps = 0, rsum = 0, ends[6] = {0, 0, 0, 0, 0, 0};
     for (int p = 0; p < plies; p++) {
         StepOut o = {0, 0, R_NONE, 0};
@@ -210,7 +220,7 @@ extern "C" void host_rollout_trace(const int8_t* init, uint64_t seed, uint32_t b
         tr_reward[p] = (int16_t)o.reward;
         tr_done[p] = (uint8_t)o.done;
         tr_reason[p] = (uint8_t)o.reason;
-        a = ms.total ? select_move(s, g, ms, scr, (int)policy_index(seed, board, draw++, (u32)ms.total)) : A_NONE;
+        a = ms.total ? select_action(s, g, ms, scr, (int)policy_index(seed, board, draw++, (u32)ms.total)) : A_NONE;
     }
     export_state(s, final_board, final_meta);
     stats8[0] = steps; stats8[1] = rsum;

@@ -36,6 +36,7 @@ def lib():
         L.host_count.argtypes = [P, P, ctypes.c_int]
         L.host_count2.argtypes = [P, P, ctypes.c_int]
         L.host_select2.argtypes = [P, P, ctypes.c_int, ctypes.c_int]
+        L.host_select_action.argtypes = [P, P, ctypes.c_int, ctypes.c_int]
         L.host_select.argtypes = [P, P, ctypes.c_int, ctypes.c_int]
         L.host_action_legal.argtypes = [P, P, ctypes.c_int, ctypes.c_int]
         L.host_next_state.argtypes = [P, P, ctypes.c_int, ctypes.c_int, P, P, P]
@@ -80,6 +81,11 @@ def count2(board, meta, white):
 def select2(board, meta, white, k):
     b, m = _bm(board, meta)
     return lib().host_select2(_p(b), _p(m), int(white), int(k))
+
+
+def select_action(board, meta, white, k):
+    b, m = _bm(board, meta)
+    return lib().host_select_action(_p(b), _p(m), int(white), int(k))
 
 
 def select(board, meta, white, k):

@@ -85,9 +85,11 @@ def test_fuzz_positions(oracle, seed):
             assert H.get_list(b, m, white) == ref, (i, white)
             assert H.count(b, m, white) == len(ref)
             assert H.count2(b, m, white) == len(ref)
+            srt = sorted(ref)
             for k in range(len(ref)):
                 assert H.select(b, m, white, k) == ref[k]
                 assert H.select2(b, m, white, k) == ref[k]
+                assert H.select_action(b, m, white, k) == srt[k]  # the policy's action-id order
             legal = set(ref)
             for a in list(legal)[:5] + [int(x) for x in rng.randint(0, 4101, size=5)]:
                 assert H.action_legal(b, m, white, a) == (a in legal)
