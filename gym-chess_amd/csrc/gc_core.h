@@ -190,15 +190,33 @@ GC_HD void put(Pos& s, int sq, int id) {  // square must be clear
 // Sliders stop at and include the first piece of either colour (so a slider ray ends AT a
 // king: Q6); knights/kings every on-board target; pawns both diagonals except squares
 // holding the pawn owner's own king (lib.rs:930).
+// Kogge-Stone occluded fill of all sliders at once in one direction (shift by SH, left or
+// right), then one more step: the attacked squares including the first blocker of either
+// colour (attack-mode semantics).  `wrap` masks squares a step may not land on.
+template <int SH, bool LEFT>
+GC_HD u64 sh(u64 x) { return LEFT ? (x << SH) : (x >> SH); }
+template <int SH, bool LEFT>
+GC_HD u64 ray_fill_att(u64 gen, u64 empty, u64 wrap) {
+    u64 pro = empty & wrap;
+    gen |= pro & sh<SH, LEFT>(gen);
+    pro &= sh<SH, LEFT>(pro);
+    gen |= pro & sh<2 * SH, LEFT>(gen);
+    pro &= sh<2 * SH, LEFT>(pro);
+    gen |= pro & sh<4 * SH, LEFT>(gen);
+    return sh<SH, LEFT>(gen) & wrap;
+}
+
 GC_HD u64 side_attacks(const Pos& s, bool white) {
-    u64 occ = occ_of(s);
+    u64 occ = occ_of(s), empty = ~occ;
     u64 mine = white ? s.w : (occ & ~s.w);
     u64 a = pawn_att_set(s.p & mine, white) & ~(s.k & mine);
     a |= knight_set(s.n & mine) | king_set(s.k & mine);
-    u64 rq = (s.r | s.q) & mine;
-    while (rq) { int sq = ctz(rq); rq &= rq - 1; a |= rook_att(sq, occ); }
-    u64 bq = (s.b | s.q) & mine;
-    while (bq) { int sq = ctz(bq); bq &= bq - 1; a |= bishop_att(sq, occ); }
+    // branch-free for any number of sliders (a per-slider loop runs the wave's maximum)
+    u64 rq = (s.r | s.q) & mine, bq = (s.b | s.q) & mine;
+    a |= ray_fill_att<8, false>(rq, empty, ~0ull) | ray_fill_att<8, true>(rq, empty, ~0ull) |
+         ray_fill_att<1, true>(rq, empty, ~FILE_A) | ray_fill_att<1, false>(rq, empty, ~FILE_H);
+    a |= ray_fill_att<7, false>(bq, empty, ~FILE_A) | ray_fill_att<9, false>(bq, empty, ~FILE_H) |
+         ray_fill_att<9, true>(bq, empty, ~FILE_A) | ray_fill_att<7, true>(bq, empty, ~FILE_H);
     return a;
 }
 
@@ -760,6 +778,30 @@ GC_HD int apply_move(Pos& s, bool white_player, int action, int* reward, bool* i
     // current_player = other (lib.rs:778-780)
     s.meta = white_player ? (s.meta & ~(u32)M_WHITE) : (s.meta | M_WHITE);
     return 0;
+}
+
+// next_state for a LEGAL move of the side to move (the env's case: the player owns the
+// piece), branch-free.  Same result as apply_move for such moves: the promotion branch is
+// unreachable (a pawn of the mover never reaches the row lib.rs:703-704 tests), a white king
+// move revokes both white rights, a white rook leaving column 0 / 7 revokes one (Q5).
+GC_HD void apply_legal(Pos& s, bool white, int action, int* reward, bool* irrev) {
+    if (action >= 4096) {  // castles (rare): the general path
+        apply_move(s, white, action, reward, irrev);
+        return;
+    }
+    int f = action >> 6, t = action & 63;
+    u64 fm = bit(f), tm = bit(t), clr = ~(fm | tm);
+    // captured value (lib.rs:19-25, 698): Q 10, R 5, B/N 3, P 1, K 0
+    int v = (s.q & tm) ? 10 : ((s.r & tm) ? 5 : (((s.b | s.n) & tm) ? 3 : ((s.p & tm) ? 1 : 0)));
+    *reward = v;
+    *irrev = ((s.p & fm) != 0) || ((occ_of(s) & tm) != 0);
+    bool wk = (s.k & s.w & fm) != 0, wr = (s.r & s.w & fm) != 0;
+#define GC_MV(X) s.X = (s.X & clr) | ((s.X & fm) ? tm : 0ull)
+    GC_MV(k); GC_MV(q); GC_MV(r); GC_MV(b); GC_MV(n); GC_MV(p); GC_MV(w);
+#undef GC_MV
+    u32 clear = (wk ? (u32)(M_WKC | M_WQC) : 0u) | ((wr && (f & 7) == 0) ? (u32)M_WQC : 0u) |
+                ((wr && (f & 7) == 7) ? (u32)M_WKC : 0u);
+    s.meta = (s.meta & ~clear) ^ M_WHITE;  // current_player = other (lib.rs:778-780)
 }
 
 // ---- board-only key for 3-fold repetition (chess_v2.py:599-602) -------------------------

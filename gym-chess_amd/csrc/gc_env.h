@@ -128,7 +128,7 @@ GC_HD StepOut env_step(Pos& s, H& hist, int action, const Gen* g0, Gen& g, MoveS
     ns.meta = (ns.meta & ~(u32)M_RIGHTS) | eff_rights(s);  // State::new
     int mr;
     bool irrev;
-    apply_move(ns, white, action, &mr, &irrev);
+    apply_legal(ns, white, action, &mr, &irrev);  // the action is legal (validated or policy-picked)
     // update_state (lib.rs:1386-1393): the side now to move's flag comes from its own
     // generation pass; the mover's flag needs one attack probe.
     gen_init(ns, g);

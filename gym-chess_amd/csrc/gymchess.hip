@@ -98,13 +98,24 @@ struct DevHist {
         RepEntry e = {a.x, a.y, b.x, b.y, c.x, c.y, d.x, d.y};
         return e;
     }
-    __device__ void store_hdr(int pos, u64 h) { htab[((size_t)i * HTAB + pos) * 8] = h; }
-    __device__ void store(int pos, const RepEntry& e) {
-        ulonglong2* p = reinterpret_cast<ulonglong2*>(htab + ((size_t)i * HTAB + pos) * 8);
-        p[0] = make_ulonglong2(e.hdr, e.k);
-        p[1] = make_ulonglong2(e.q, e.r);
-        p[2] = make_ulonglong2(e.b, e.n);
-        p[3] = make_ulonglong2(e.p, e.w);
+    // Table writes are recorded and issued by commit() at the end of the step: a store
+    // issued mid-kernel makes the compiler wait (vmcnt) before reusing its data registers.
+    int wkind = 0, wpos = 0;  // 0 none, 1 header only, 2 whole entry
+    RepEntry we;
+    __device__ void store_hdr(int pos, u64 h) { wkind = 1; wpos = pos; we.hdr = h; }
+    __device__ void store(int pos, const RepEntry& e) { wkind = 2; wpos = pos; we = e; }
+    __device__ void commit() {
+        u64* base = htab + ((size_t)i * HTAB + wpos) * 8;
+        if (wkind == 1) {
+            base[0] = we.hdr;
+        } else if (wkind == 2) {
+            ulonglong2* p = reinterpret_cast<ulonglong2*>(base);
+            p[0] = make_ulonglong2(we.hdr, we.k);
+            p[1] = make_ulonglong2(we.q, we.r);
+            p[2] = make_ulonglong2(we.b, we.n);
+            p[3] = make_ulonglong2(we.p, we.w);
+        }
+        wkind = 0;
     }
 };
 
@@ -464,6 +475,7 @@ __global__ void __launch_bounds__(BLOCK) k_env_step(EnvDev e) {
         e.act[i] = pick(s, g, ms, scr, e.seed, i, d);
         e.draw[i] = d;
     }
+    h.commit();
     GC_STAMP(7);
 #ifdef GC_STAMPS
     if (POLICY && g_stamp_out != nullptr && (threadIdx.x & 63) == 0)
@@ -478,8 +490,8 @@ __global__ void __launch_bounds__(BLOCK) k_env_step(EnvDev e) {
 }
 
 // Fused K-ply random self-play: state in registers for the whole launch.  Per-ply outputs
-// (reward / done / reason) are written every ply, like the one-ply kernel; optional per-ply
-// trace [ply][N] (tests).  stats per board: [steps, reward_sum(two's complement), ends[0..5]]
+// go to the optional trace [ply][N]; otherwise the last ply's outputs and per-board stats
+// [steps, reward_sum(two's complement), ends[0..5]] are written.
 __global__ void __launch_bounds__(BLOCK) k_env_rollout(EnvDev e, int plies, int16_t* tr_action, int16_t* tr_reward,
                                                        uint8_t* tr_done, uint8_t* tr_reason, uint64_t* stats) {
     LDS_SCRATCH_DECL;
@@ -526,11 +538,12 @@ __global__ void __launch_bounds__(BLOCK) k_env_rollout(EnvDev e, int plies, int1
             tr_done[t] = (uint8_t)o.done;
             tr_reason[t] = (uint8_t)o.reason;
         }
-        e.reward[i] = o.reward;  // the env.step() outputs of this ply
-        e.done[i] = (uint8_t)o.done;
-        e.reason[i] = (uint8_t)o.reason;
         a = pick(s, g, ms, scr, e.seed, i, d);
+        h.commit();
     }
+    e.reward[i] = o.reward;  // the last ply's env.step() outputs (per-ply: trace buffers)
+    e.done[i] = (uint8_t)o.done;
+    e.reason[i] = (uint8_t)o.reason;
     e.st.store(i, s);
     h.flush(g0);
     e.draw[i] = d;

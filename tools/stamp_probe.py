@@ -29,7 +29,9 @@ print(f"waves {len(st)}  mean wave span {tot.mean():.0f} ticks  (s_memtime units
 for k in range(1, 8):
     d = (st[:, k] - st[:, k - 1]).astype(float)
     ok = (st[:, k] >= st[:, k - 1]) & (st[:, k - 1] > 0)
-    print(f"{names[k-1]:>22}: mean {d[ok].mean():8.0f}  p50 {np.median(d[ok]):8.0f}  share {d[ok].sum()/tot[ok].sum():5.1%}  (waves {ok.sum()})")
+    q = np.percentile(d[ok], [50, 75, 90, 99]) if ok.any() else [0, 0, 0, 0]
+    print(f"{names[k-1]:>22}: mean {d[ok].mean():8.0f}  p50/75/90/99 {q[0]:7.0f} {q[1]:7.0f} {q[2]:7.0f} {q[3]:7.0f}  "
+          f"share {d[ok].sum()/tot[ok].sum():5.1%}  (waves {ok.sum()})")
 start = st[:, 0] - st[:, 0].min()
 print("wave start spread (ticks): p50 %d p99 %d max %d" % (np.median(start), np.percentile(start, 99), start.max()))
 end = st[:, 7] - st[:, 0].min()
