@@ -1,0 +1,119 @@
+"""Single-board ChessEnv (gym_chess_amd.single, chess_v2.py:132-602 restated) against the
+reference ChessEnvV2's own recorded traces (tests/golden/v2_env_traces.json.gz, written by
+make_golden.py from the reference env): opponent "none" and "random" (numpy's global
+generator, so the seeded driver below replays the reference's games move for move),
+invalid actions, 3-fold, kingless play.  CPU: on the oracle engine; GPU: on the HIP engine.
+"""
+import numpy as np
+import pytest
+
+from conftest import load_golden
+
+
+def _replay(make_env, t):
+    from gym_chess_amd import codec as C
+
+    ib = None if t.get("initial_board") is None else C.text_to_board(t["initial_board"]).reshape(8, 8)
+    kw = dict(log=False)
+    if ib is not None:
+        kw["initial_board"] = ib
+    if t.get("scripted"):
+        env = make_env(opponent="none", **kw)
+        for a, s in zip(t["actions"], t["steps"]):
+            _check(env, env.step(int(a)), s)
+        return len(t["steps"])
+    np.random.seed(t["seed"])  # the same generator calls as make_golden.trace_env
+    env = make_env(opponent=t["opponent"], **kw)
+    rng = np.random.RandomState(t["seed"] + 7)
+    steps = t["steps"]
+    j, i, every = 0, 0, t["invalid_every"]
+    while j < len(steps):
+        moves = env.possible_moves
+        if not moves:
+            assert steps[j]["kind"] == "reset"
+            env.reset()
+            j += 1
+            i += 1
+            continue
+        if every and i % every == every - 1:
+            action = int(rng.randint(0, 4100))
+        else:
+            action = env.move_to_action(moves[np.random.choice(np.arange(len(moves)))])
+        s = steps[j]
+        assert s.get("action") == action, (j, s, action)
+        try:
+            out = env.step(action)
+        except SystemError:
+            assert s["kind"] == "error"
+            env.reset()
+            j += 1
+            i += 1
+            continue
+        _check(env, out, s)
+        j += 1
+        i += 1
+        if out[2]:
+            assert steps[j]["kind"] == "reset"
+            env.reset()
+            j += 1
+    return j
+
+
+def _check(env, out, s):
+    from gym_chess_amd import codec as C
+
+    state, reward, done, info = out
+    assert s["kind"] == "step"
+    assert reward == s["reward"] and bool(done) == s["done"], s
+    assert C.board_to_text(np.asarray(state["board"]).reshape(64)) == s["board"]
+    assert info["move_count"] == s["move_count"] and len(env.possible_moves) == s["n_moves"]
+    if "meta" in s:
+        got = [int(env.current_player == "WHITE"), int(state["white_king_castle_is_possible"]),
+               int(state["white_queen_castle_is_possible"]), int(state["black_king_castle_is_possible"]),
+               int(state["black_queen_castle_is_possible"]), int(bool(state["white_king_is_checked"])),
+               int(bool(state["black_king_is_checked"]))]
+        assert got == s["meta"], s
+
+
+def test_single_env_traces_on_oracle_engine():
+    from gym_chess_amd.single import ChessEnv
+    from oracle_engine import OracleChessEngine
+
+    eng = OracleChessEngine()
+    n = 0
+    for t in load_golden("v2_env_traces.json.gz"):
+        n += _replay(lambda **kw: ChessEnv(engine=eng, **kw), t)
+    assert n > 3000
+
+
+def test_single_env_black_player_and_errors():
+    from gym_chess_amd import codec as C
+    from gym_chess_amd.single import ChessEnv
+    from oracle_engine import OracleChessEngine
+
+    np.random.seed(5)
+    env = ChessEnv(player_color=C.BLACK, opponent="random", log=False, engine=OracleChessEngine())
+    assert env.current_player == C.BLACK and env.move_count == 1
+    assert sum(1 for row in env.board for v in row if v > 0) == 16
+    acts = env.possible_actions
+    assert len(acts) == 20
+    with pytest.raises(AssertionError):
+        env.step(4101)
+    _, r, d, _ = env.step(0)  # a8a8: not legal -> -10, state unchanged
+    assert r == -10 and not d and env.move_count == 1
+    env2 = ChessEnv(opponent="none", log=False, engine=OracleChessEngine())
+    assert env2.render(mode="string").count("\n") == 11
+    with pytest.raises(ValueError):
+        ChessEnv(opponent="bogus", log=False, engine=OracleChessEngine())
+
+
+@pytest.mark.gpu
+def test_single_env_traces_on_gpu_engine():
+    from gym_chess_amd.engine import ChessEngine
+    from gym_chess_amd.single import ChessEnv
+
+    eng = ChessEngine(0)
+    n = 0
+    for t in load_golden("v2_env_traces.json.gz"):
+        n += _replay(lambda **kw: ChessEnv(engine=eng, **kw), t)
+    assert n > 3000
