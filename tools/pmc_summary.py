@@ -1,0 +1,59 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 PMC passes (tools/gpu_run.sh steps pmcf / pmcw / pmcv) for one kernel.
+
+HBM traffic per launch, corrected as MI355X_MICROARCH.md §HBM prescribes for gfx950:
+FETCH_SIZE (KiB) counts half the bytes of wide streaming reads -> x2; WRITE_SIZE (KiB) as is.
+Writes <out>/pmc_traffic_latest.json (read by bench.py for roofline.traffic) and prints a table.
+
+  python tools/pmc_summary.py gpurun_out profiles/r01_v7 [--kernel 'void k_env_step<true>'] [--last 20]
+"""
+import argparse
+import collections
+import csv
+import json
+import os
+
+
+def per_dispatch(path, kernel):
+    d = collections.defaultdict(dict)
+    for r in csv.DictReader(open(path)):
+        if r["Kernel_Name"].startswith(kernel):
+            d[int(r["Dispatch_Id"])][r["Counter_Name"]] = float(r["Counter_Value"])
+    return [d[k] for k in sorted(d)]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("src")
+    ap.add_argument("dst")
+    ap.add_argument("--kernel", default="void k_env_step<true>")
+    ap.add_argument("--last", type=int, default=20)
+    ap.add_argument("--boards", type=int, default=65536)
+    ap.add_argument("--alg-bytes-per-board", type=int, default=282)
+    a = ap.parse_args()
+    mean = lambda rows, k: sum(r[k] for r in rows) / len(rows)  # noqa: E731
+    f = per_dispatch(os.path.join(a.src, "pmc_fetch/run_counter_collection.csv"), a.kernel)[-a.last:]
+    w = per_dispatch(os.path.join(a.src, "pmc_write/run_counter_collection.csv"), a.kernel)[-a.last:]
+    fetch = mean(f, "FETCH_SIZE") * 1024 * 2
+    write = mean(w, "WRITE_SIZE") * 1024
+    out = {"kernel": a.kernel, "launches_averaged": len(f), "boards": a.boards,
+           "fetch_bytes_corrected": fetch, "fetch_size_kib_raw": mean(f, "FETCH_SIZE"), "write_bytes": write,
+           "bytes_per_launch": fetch + write, "bytes_per_board": (fetch + write) / a.boards,
+           "alg_bytes_per_launch": a.alg_bytes_per_board * a.boards,
+           "note": "FETCH_SIZE x2 (gfx950 correction for wide streaming reads; 8-B/lane loads uncalibrated)"}
+    vp = os.path.join(a.src, "pmc_valu/run_counter_collection.csv")
+    if os.path.exists(vp):
+        v = per_dispatch(vp, a.kernel)[-a.last:]
+        waves = mean(v, "SQ_WAVES")
+        sq = {k: mean(v, k) / waves for k in v[0] if k != "SQ_WAVES"}
+        out["per_wave"] = sq
+        out["per_wave"]["note"] = "SQ_*_CYCLES / WAIT / ACTIVE in units of 4 cycles (quad-cycles)"
+    os.makedirs(a.dst, exist_ok=True)
+    for p in (os.path.join(a.dst, "pmc_traffic.json"), os.path.join(os.path.dirname(a.dst.rstrip("/")),
+                                                                       "pmc_traffic_latest.json")):
+        json.dump(out, open(p, "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
