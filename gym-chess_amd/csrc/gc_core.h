@@ -49,7 +49,8 @@ enum : u32 {
 
 // ---- step reasons (per-ply info code) -------------------------------------------
 enum { R_NONE = 0, R_MATE = 1, R_REPETITION = 2, R_MOVE_CAP = 3, R_NO_MOVES = 4, R_BOTH_CHECKED = 5,
-       R_INVALID = 6, R_DONE_ALREADY = 7 };
+       R_INVALID = 6, R_DONE_ALREADY = 7, R_MATED = 8, R_OPP_NO_MOVE = 9,
+       R_WINDOW_FULL = 10 };
 
 struct Pos {
     u64 k, q, r, b, n, p, w;  // by type (both colours) + white occupancy

@@ -26,7 +26,11 @@
 
 namespace gc {
 
-static constexpr int HIST_CAP = 300;
+// Window capacity.  With opponent "none" (and a WHITE agent) the move cap bounds a window to
+// ~301 boards; a BLACK agent's move_count never advances (chess_v2.py:291-292), so its
+// window is unbounded in the reference: a window that would exceed HIST_CAP ends the episode
+// with R_WINDOW_FULL (the oracle does the same), keeping the table at load <= 0.75.
+static constexpr int HIST_CAP = 768;
 static constexpr int HTAB_BITS = 10;
 static constexpr int HTAB = 1 << HTAB_BITS;
 static constexpr int MOVES_MAX = 149;  // chess_v2.py:141
@@ -75,7 +79,8 @@ GC_HD void rep_prefetch(H& h, const Pos& s, RepProbe& pr) {
     pr.e0 = h.load((int)(pr.key & (HTAB - 1)));
 }
 
-// Returns how many times the board has been the pre-move board so far, this one included.
+// Returns how many times the board has been the pre-move board so far, this one included;
+// 0 if it is new and the window is full (HIST_CAP).
 template <class H>
 GC_HD int rep_commit(H& h, const Pos& s, const RepProbe& pr, u32& hl, bool irrev) {
     u32 gen = h.gen();
@@ -98,17 +103,56 @@ GC_HD int rep_commit(H& h, const Pos& s, const RepProbe& pr, u32& hl, bool irrev
         return c ? c : 1;
     }
     if (c) return c;
-    if (hl < HIST_CAP) {
-        RepEntry ne = {(u64)gen | ((u64)tag << 32) | (1ull << 56), s.k, s.q, s.r, s.b, s.n, s.p, s.w};
-        h.store((int)pos, ne);
-        hl++;
-    }
+    if (hl >= HIST_CAP) return 0;
+    RepEntry ne = {(u64)gen | ((u64)tag << 32) | (1ull << 56), s.k, s.q, s.r, s.b, s.n, s.p, s.w};
+    h.store((int)pos, ne);
+    hl++;
     return 1;
 }
 
-// One step().  On return with o.moved, `g`/`ms`/`scr` describe the new position (side now
-// to move) so the caller can pick the next action without regenerating.  `g0` must be
-// gen_init(s) when VALIDATE (external actions); the on-device policy is trusted.
+// One player_move (chess_v2.py:393-420) of the legal `action` of the side to move, with the
+// engine's update_state and the next side's move list: on return 0, `s` is the new position
+// (check flags, window length, M_DONE if the PRE-move board reached 3 occurrences) and
+// `g`/`ms`/`scr` describe the side now to move; *mr = capture value, *rep = 3-fold verdict,
+// *nchk = the side now to move is in check.  Returns 1 (state unchanged) when both kings
+// end up in check (lib.rs:1442-1446), 2 (move applied, M_DONE) when the window is full.
+// Never touches move_count.
+template <class H, class S>
+GC_HD int env_ply(Pos& s, H& hist, int action, Gen& g, MoveSet& ms, S& scr, int* mr, bool* rep, bool* nchk) {
+    RepProbe pr;
+    rep_prefetch(hist, s, pr);  // in flight during the move generation below
+    GC_STAMP(2);
+    bool white = s.meta & M_WHITE;
+    Pos ns = s;
+    ns.meta = (ns.meta & ~(u32)M_RIGHTS) | eff_rights(s);  // State::new
+    bool irrev;
+    apply_legal(ns, white, action, mr, &irrev);  // the action is legal (validated or policy-picked)
+    // update_state (lib.rs:1386-1393): the side now to move's flag comes from its own
+    // generation pass; the mover's flag needs one attack probe.
+    gen_init(ns, g);
+    bool opp_chk = g.in_check;
+    int mk = tracked_king(ns, white);
+    bool my_chk = mk >= 0 && sq_attacked(ns, mk, !white);
+    GC_STAMP(3);
+    if (opp_chk && my_chk) return 1;
+    gen_moves(ns, g, ms, scr);  // the next side's possible moves (chess_v2.py:268 / 278)
+    GC_STAMP(4);
+    u32 chk = white ? ((my_chk ? M_WCHK : 0u) | (opp_chk ? M_BCHK : 0u))
+                    : ((opp_chk ? M_WCHK : 0u) | (my_chk ? M_BCHK : 0u));
+    u32 hl = hl_of(s.meta);
+    int c = rep_commit(hist, s, pr, hl, irrev);
+    *rep = c >= 3;  // chess_v2.py:404-407
+    GC_STAMP(5);
+    ns.meta = with_hl((ns.meta & ~(u32)(M_WCHK | M_BCHK | M_DONE)) | chk | ((*rep || c == 0) ? M_DONE : 0u), hl);
+    *nchk = opp_chk;
+    s = ns;
+    return c == 0 ? 2 : 0;
+}
+
+// One step() (chess_v2.py:219-294, opponent="none").  On return with o.moved, `g`/`ms`/`scr`
+// describe the new position (side now to move) so the caller can pick the next action
+// without regenerating.  `g0` must be gen_init(s) when VALIDATE (external actions); the
+// on-device policy is trusted.
 template <bool VALIDATE, class H, class S>
 GC_HD StepOut env_step(Pos& s, H& hist, int action, const Gen* g0, Gen& g, MoveSet& ms, S& scr) {
     StepOut o = {0, 0, R_NONE, 0};
@@ -120,48 +164,113 @@ GC_HD StepOut env_step(Pos& s, H& hist, int action, const Gen* g0, Gen& g, MoveS
     }
     if (s.meta & M_DONE) { o.done = 1; o.reason = R_DONE_ALREADY; return o; }       // 245-251
     if (mc_of(s.meta) > MOVES_MAX) { o.done = 1; o.reason = R_MOVE_CAP; return o; }  // 252-258
-    RepProbe pr;
-    rep_prefetch(hist, s, pr);  // in flight during the move generation below
-    GC_STAMP(2);
     bool white = s.meta & M_WHITE;
-    Pos ns = s;
-    ns.meta = (ns.meta & ~(u32)M_RIGHTS) | eff_rights(s);  // State::new
     int mr;
-    bool irrev;
-    apply_legal(ns, white, action, &mr, &irrev);  // the action is legal (validated or policy-picked)
-    // update_state (lib.rs:1386-1393): the side now to move's flag comes from its own
-    // generation pass; the mover's flag needs one attack probe.
-    gen_init(ns, g);
-    bool opp_chk = g.in_check;
-    int mk = tracked_king(ns, white);
-    bool my_chk = mk >= 0 && sq_attacked(ns, mk, !white);
-    GC_STAMP(3);
-    if (opp_chk && my_chk) {  // lib.rs:1442-1446
+    bool rep, opp_chk;
+    int rc = env_ply(s, hist, action, g, ms, scr, &mr, &rep, &opp_chk);
+    if (rc == 1) {
         o.reason = R_BOTH_CHECKED;
         o.done = 1;
         return o;
     }
-    // the opponent's possible moves (chess_v2.py:268)
-    gen_moves(ns, g, ms, scr);
-    GC_STAMP(4);
-    u32 chk = white ? ((my_chk ? M_WCHK : 0u) | (opp_chk ? M_BCHK : 0u))
-                    : ((opp_chk ? M_WCHK : 0u) | (my_chk ? M_BCHK : 0u));
-    u32 hl = hl_of(s.meta);
-    bool rep = rep_commit(hist, s, pr, hl, irrev) >= 3;  // chess_v2.py:404-407
-    GC_STAMP(5);
-    ns.meta = with_hl((ns.meta & ~(u32)(M_WCHK | M_BCHK | M_DONE)) | chk | (rep ? M_DONE : 0u), hl);
     o.reward = -10 + mr;  // INVALID_ACTION_REWARD + move reward (Q9)
     o.moved = 1;
     if (rep) { o.done = 1; o.reason = R_REPETITION; }
+    if (rc == 2) { o.done = 1; o.reason = R_WINDOW_FULL; }
     if (ms.total == 0 && opp_chk) {  // 270-272
-        ns.meta |= M_DONE;
+        s.meta |= M_DONE;
         o.done = 1;
         o.reward += 100;
         o.reason = R_MATE;
     }
-    if (!o.done && !white) ns.meta += (1u << M_MC_SHIFT);  // 291-292
-    s = ns;
+    if (!o.done && !white) s.meta += (1u << M_MC_SHIFT);  // 291-292
     return o;
+}
+
+// The random opponent's pick (make_random_policy, chess_v2.py:116-127, on the device policy
+// stream): rank drawn uniformly over the legal list, k-th legal action in action-id order.
+struct PolicyCtx {
+    u64 seed;
+    u32 board;
+    u32 draw;
+};
+
+// step() with the random opponent (chess_v2.py:219-294 with opponent_policy set): the
+// agent's ply, WIN (+100) if the opponent is mated, else the opponent's reply (its capture
+// value is subtracted), LOSS (-100) if the agent is then mated; move_count advances only
+// when WHITE is to move after the step (so never for a BLACK agent, as in the reference).
+// An opponent with no legal reply and no check ends the env (R_OPP_NO_MOVE; the reference's
+// policy returns "resign", which maps to no action and raises).
+template <bool VALIDATE, class H, class S>
+GC_HD StepOut env_step_vs(Pos& s, H& hist, int action, const Gen* g0, Gen& g, MoveSet& ms, S& scr, PolicyCtx& pc) {
+    StepOut o = {0, 0, R_NONE, 0};
+    if (VALIDATE && !action_legal(s, *g0, action)) {
+        o.reward = -10;
+        o.done = (s.meta & M_DONE) ? 1 : 0;
+        o.reason = R_INVALID;
+        return o;
+    }
+    if (s.meta & M_DONE) { o.done = 1; o.reason = R_DONE_ALREADY; return o; }
+    if (mc_of(s.meta) > MOVES_MAX) { o.done = 1; o.reason = R_MOVE_CAP; return o; }
+    int mr;
+    bool rep, chk;
+    int rc = env_ply(s, hist, action, g, ms, scr, &mr, &rep, &chk);
+    if (rc == 1) {
+        o.reason = R_BOTH_CHECKED;
+        o.done = 1;
+        return o;
+    }
+    o.reward = -10 + mr;
+    o.moved = 1;
+    if (rep) { o.done = 1; o.reason = R_REPETITION; }
+    if (rc == 2) { o.done = 1; o.reason = R_WINDOW_FULL; }
+    if (ms.total == 0 && chk) {  // 270-272
+        s.meta |= M_DONE;
+        o.done = 1;
+        o.reward += 100;
+        o.reason = R_MATE;
+    }
+    if (o.done) return o;
+    if (ms.total == 0) {  // 120-122: "resign" -> no action
+        s.meta |= M_DONE;
+        o.done = 1;
+        o.reason = R_OPP_NO_MOVE;
+        return o;
+    }
+    hist.commit();  // the agent ply's table write lands before the reply probes the table
+    int k = (int)policy_index(pc.seed, pc.board, pc.draw++, (u32)ms.total);
+    int oa = select_action(s, g, ms, scr, k);
+    rc = env_ply(s, hist, oa, g, ms, scr, &mr, &rep, &chk);
+    if (rc == 1) {
+        o.reason = R_BOTH_CHECKED;
+        o.done = 1;
+        return o;
+    }
+    o.reward -= mr;  // 283
+    if (rep) { o.done = 1; o.reason = R_REPETITION; }
+    if (rc == 2) { o.done = 1; o.reason = R_WINDOW_FULL; }
+    if (ms.total == 0 && chk) {  // 285-288
+        s.meta |= M_DONE;
+        o.done = 1;
+        o.reward -= 100;
+        o.reason = R_MATED;
+    }
+    if (s.meta & M_WHITE) s.meta += (1u << M_MC_SHIFT);  // 291-292
+    return o;
+}
+
+// reset() for a BLACK agent (chess_v2.py:208-216): from the reset position (WHITE to move,
+// `g`/`ms`/`scr` its move set) the opponent opens; its 3-fold verdict is discarded and
+// move_count becomes 1.  With no opening move the env is left done (R_OPP_NO_MOVE).
+template <class H, class S>
+GC_HD void env_open_vs(Pos& s, H& hist, Gen& g, MoveSet& ms, S& scr, PolicyCtx& pc) {
+    if (ms.total == 0) { s.meta |= M_DONE; return; }
+    int k = (int)policy_index(pc.seed, pc.board, pc.draw++, (u32)ms.total);
+    int oa = select_action(s, g, ms, scr, k);
+    int mr;
+    bool rep, chk;
+    if (env_ply(s, hist, oa, g, ms, scr, &mr, &rep, &chk) == 1) { s.meta |= M_DONE; return; }
+    s.meta = (s.meta & ~(u32)M_DONE) + (1u << M_MC_SHIFT);
 }
 
 }  // namespace gc

@@ -311,6 +311,8 @@ struct EnvDev {
     u64 init[NBB];   // 7 bitboards of the initial board (kernel argument: scalar loads)
     uint64_t seed;
     int n;
+    int opp;          // 0: opponent "none"; 1: the random opponent replies inside step()
+    int agent_black;  // player_color BLACK (needs opp): the opponent opens at every reset
     // Every reset lands on the same position: its state, move set and parked targets are
     // computed once at env creation (k_init_cache) and passed here by value.
     struct InitCache {
@@ -394,6 +396,15 @@ __device__ uint16_t pick(const Pos& s, const Gen& g, const MoveSet& ms, const Ld
     return (uint16_t)select_action(s, g, ms, scr, (int)k);
 }
 
+// after a reset: the move set of the side to move; a BLACK agent's opponent opens first
+template <bool OPP>
+__device__ void after_reset(const EnvDev& e, Pos& s, DevHist& h, Gen& g, MoveSet& ms, LdsScratch& scr,
+                            PolicyCtx& pc) {
+    moves_after_reset(e, s, g, ms, scr);
+    if (OPP && e.agent_black) env_open_vs(s, h, g, ms, scr, pc);
+}
+
+template <bool OPP>
 __global__ void __launch_bounds__(BLOCK) k_env_reset(EnvDev e, const uint8_t* __restrict__ mask, int select) {
     LDS_SCRATCH_DECL;
     int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -403,16 +414,17 @@ __global__ void __launch_bounds__(BLOCK) k_env_reset(EnvDev e, const uint8_t* __
     DevHist h = e.hist(i, g0);
     Pos s;
     reset_board(e, s, h);
-    h.flush(g0);
-    e.st.store(i, s);
-    if (select) {
+    PolicyCtx pc = {e.seed, (u32)i, e.draw[i]};
+    if ((OPP && e.agent_black) || select) {
         Gen g;
         MoveSet ms;
-        moves_after_reset(e, s, g, ms, scr);
-        u32 d = e.draw[i];
-        e.act[i] = pick(s, g, ms, scr, e.seed, i, d);
-        e.draw[i] = d;
+        after_reset<OPP>(e, s, h, g, ms, scr, pc);
+        if (select) e.act[i] = pick(s, g, ms, scr, e.seed, i, pc.draw);
+        h.commit();
+        e.draw[i] = pc.draw;
     }
+    h.flush(g0);
+    e.st.store(i, s);
 }
 
 // set_states ingest for the env: import + empty window
@@ -435,17 +447,18 @@ __global__ void k_env_import(const int8_t* __restrict__ boards, const uint8_t* _
 #ifdef GC_STAMPS
 __device__ unsigned long long* g_stamp_out;
 #endif
-template <bool POLICY>
+template <bool POLICY, bool OPP>
 __global__ void __launch_bounds__(BLOCK) k_env_step(EnvDev e) {
     LDS_SCRATCH_DECL;
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= e.n) return;
     GC_STAMP(0);
     Pos s = e.st.load(i);
-    u32 g0 = e.hgen[i], d = POLICY ? e.draw[i] : 0u, nst = e.nsteps[i], ua = e.act[i];
+    u32 g0 = e.hgen[i], d = (POLICY || OPP) ? e.draw[i] : 0u, nst = e.nsteps[i], ua = e.act[i];
     pin(s); pin(g0); pin(d); pin(nst); pin(ua);
     GC_STAMP(1);
     DevHist h = e.hist(i, g0);
+    PolicyCtx pc = {e.seed, (u32)i, d};
     int a = (int)ua;
     StepOut o = {0, 0, R_NONE, 0};
     Gen g;
@@ -456,11 +469,11 @@ __global__ void __launch_bounds__(BLOCK) k_env_step(EnvDev e) {
         o.reason = R_NO_MOVES;
     } else {
         if (POLICY) {
-            o = env_step<false>(s, h, a, nullptr, g, ms, scr);
+            o = OPP ? env_step_vs<false>(s, h, a, nullptr, g, ms, scr, pc) : env_step<false>(s, h, a, nullptr, g, ms, scr);
         } else {
             Gen g0;
             gen_init(s, g0);
-            o = env_step<true>(s, h, a, &g0, g, ms, scr);
+            o = OPP ? env_step_vs<true>(s, h, a, &g0, g, ms, scr, pc) : env_step<true>(s, h, a, &g0, g, ms, scr);
         }
         have = o.moved;
         nst += 1;
@@ -470,11 +483,11 @@ __global__ void __launch_bounds__(BLOCK) k_env_step(EnvDev e) {
         }
     }
     if (POLICY) {
-        if (!have) moves_after_reset(e, s, g, ms, scr);
+        if (!have) after_reset<OPP>(e, s, h, g, ms, scr, pc);
         GC_STAMP(6);
-        e.act[i] = pick(s, g, ms, scr, e.seed, i, d);
-        e.draw[i] = d;
+        e.act[i] = pick(s, g, ms, scr, e.seed, i, pc.draw);
     }
+    if (POLICY || OPP) e.draw[i] = pc.draw;
     h.commit();
     GC_STAMP(7);
 #ifdef GC_STAMPS
@@ -492,6 +505,7 @@ __global__ void __launch_bounds__(BLOCK) k_env_step(EnvDev e) {
 // Fused K-ply random self-play: state in registers for the whole launch.  Per-ply outputs
 // go to the optional trace [ply][N]; otherwise the last ply's outputs and per-board stats
 // [steps, reward_sum(two's complement), ends[0..5]] are written.
+template <bool OPP>
 __global__ void __launch_bounds__(BLOCK) k_env_rollout(EnvDev e, int plies, int16_t* tr_action, int16_t* tr_reward,
                                                        uint8_t* tr_done, uint8_t* tr_reason, uint64_t* stats) {
     LDS_SCRATCH_DECL;
@@ -501,6 +515,7 @@ __global__ void __launch_bounds__(BLOCK) k_env_rollout(EnvDev e, int plies, int1
     u32 g0 = e.hgen[i], d = e.draw[i], ua = e.act[i];
     pin(s); pin(g0); pin(d); pin(ua);
     DevHist h = e.hist(i, g0);
+    PolicyCtx pc = {e.seed, (u32)i, d};
     int a = (int)ua;
     uint64_t steps = 0, rsum = 0;
     u32 e_mate = 0, e_rep = 0, e_cap = 0, e_nomove = 0, e_err = 0;
@@ -517,20 +532,21 @@ __global__ void __launch_bounds__(BLOCK) k_env_rollout(EnvDev e, int plies, int1
             e_nomove++;
             played = -1;
         } else {
-            o = env_step<false>(s, h, a, nullptr, g, ms, scr);
+            o = OPP ? env_step_vs<false>(s, h, a, nullptr, g, ms, scr, pc) : env_step<false>(s, h, a, nullptr, g, ms, scr);
             have = o.moved;
             steps++;
             rsum += (uint64_t)(int64_t)o.reward;
             if (o.done) {
-                e_mate += o.reason == R_MATE;
+                e_mate += o.reason == R_MATE || o.reason == R_MATED;
                 e_rep += o.reason == R_REPETITION;
                 e_cap += o.reason == R_MOVE_CAP;
-                e_err += o.reason == R_BOTH_CHECKED;
+                e_err += o.reason == R_BOTH_CHECKED || o.reason == R_WINDOW_FULL;
+                e_nomove += o.reason == R_OPP_NO_MOVE;
                 reset_board(e, s, h);
                 have = false;
             }
         }
-        if (!have) moves_after_reset(e, s, g, ms, scr);
+        if (!have) after_reset<OPP>(e, s, h, g, ms, scr, pc);
         if (tr_action) {
             size_t t = (size_t)p * e.n + i;
             tr_action[t] = (int16_t)played;
@@ -538,7 +554,7 @@ __global__ void __launch_bounds__(BLOCK) k_env_rollout(EnvDev e, int plies, int1
             tr_done[t] = (uint8_t)o.done;
             tr_reason[t] = (uint8_t)o.reason;
         }
-        a = pick(s, g, ms, scr, e.seed, i, d);
+        a = pick(s, g, ms, scr, e.seed, i, pc.draw);
         h.commit();
     }
     e.reward[i] = o.reward;  // the last ply's env.step() outputs (per-ply: trace buffers)
@@ -546,7 +562,7 @@ __global__ void __launch_bounds__(BLOCK) k_env_rollout(EnvDev e, int plies, int1
     e.reason[i] = (uint8_t)o.reason;
     e.st.store(i, s);
     h.flush(g0);
-    e.draw[i] = d;
+    e.draw[i] = pc.draw;
     e.act[i] = (uint16_t)a;
     e.nsteps[i] += (u32)steps;
     if (stats) {
@@ -845,6 +861,18 @@ static void env_free(gc_env* e) {
     if (e->stream) (void)hipStreamDestroy(e->stream);
 }
 
+// kernel dispatch on the env's opponent mode (a kernel-argument-uniform choice made once per
+// launch on the host, so the opponent="none" kernels carry no opponent code)
+static void launch_reset(gc_env* e, const uint8_t* mask, int select) {
+    if (e->d.opp) k_env_reset<true><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d, mask, select);
+    else k_env_reset<false><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d, mask, select);
+}
+template <bool POLICY>
+static void launch_step(gc_env* e) {
+    if (e->d.opp) k_env_step<POLICY, true><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d);
+    else k_env_step<POLICY, false><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d);
+}
+
 extern "C" int gc_env_create(int device, int n_boards, uint64_t seed, const int8_t* initial_board, gc_env** out) {
     if (!out) return fail("null out pointer");
     if (n_boards <= 0) return fail("n_boards must be > 0");
@@ -892,6 +920,8 @@ extern "C" int gc_env_create(int device, int n_boards, uint64_t seed, const int8
     e->d.st = SoA{e->bb, e->meta, n};
     e->d.seed = seed;
     e->d.n = n;
+    e->d.opp = 0;
+    e->d.agent_black = 0;
     {  // the start position's move set, shared by every reset (EnvDev::ic)
         EnvDev::InitCache* dic = nullptr;
         if (dalloc(&dic, 1)) { std::string m = g_err; env_free(e); delete e; return fail(m); }
@@ -902,12 +932,31 @@ extern "C" int gc_env_create(int device, int n_boards, uint64_t seed, const int8
         (void)hipFree(dic);
         if (he != hipSuccess) { env_free(e); delete e; return fail(std::string("init cache: ") + hipGetErrorString(he)); }
     }
-    k_env_reset<<<grid_for(n), BLOCK, 0, e->stream>>>(e->d, nullptr, 1);
+    launch_reset(e, nullptr, 1);
     he = hipGetLastError();
     if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
     if (he != hipSuccess) { env_free(e); delete e; return fail(std::string("reset: ") + hipGetErrorString(he)); }
     e->policy_ready = true;
     *out = e;
+    return 0;
+}
+
+// opponent mode (chess_v2.py:133-181): opponent 0 "none", 1 "random" (the device policy
+// answers inside every step); agent_white 0 = player_color BLACK (requires an opponent: the
+// reference's reset calls the opponent policy to open).  Resets every board.
+extern "C" int gc_env_set_opponent(gc_env* e, int opponent, int agent_white) {
+    if (!e) return fail("null env");
+    if (opponent != 0 && opponent != 1) return fail("opponent must be 0 (none) or 1 (random)");
+    if (!agent_white && !opponent) return fail("player_color BLACK needs an opponent (chess_v2.py:208-212)");
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    e->d.opp = opponent;
+    e->d.agent_black = agent_white ? 0 : 1;
+    HIPCHK(hipMemsetAsync(e->d.draw, 0, (size_t)4 * e->n, e->stream));  // fresh policy streams
+    launch_reset(e, nullptr, 1);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(e->stream));
+    e->policy_ready = true;
     return 0;
 }
 
@@ -926,7 +975,7 @@ extern "C" int gc_env_reset(gc_env* e, const uint8_t* mask) {
     if (!e) return fail("null env");
     HIPCHK(hipSetDevice(e->device));
     if (mask) HIPCHK(hipMemcpyAsync(e->mask, mask, e->n, hipMemcpyHostToDevice, e->stream));
-    k_env_reset<<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d, mask ? e->mask : nullptr, 1);
+    launch_reset(e, mask ? e->mask : nullptr, 1);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(e->stream));
     e->policy_ready = true;
@@ -939,7 +988,7 @@ extern "C" int gc_env_step(gc_env* e, const uint16_t* actions, int32_t* reward, 
         if (actions[i] > A_RESIGN) return fail("action out of range [0, 4100] at index " + std::to_string(i));
     HIPCHK(hipSetDevice(e->device));
     HIPCHK(hipMemcpyAsync(e->d.act, actions, (size_t)2 * e->n, hipMemcpyHostToDevice, e->stream));
-    k_env_step<false><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d);
+    launch_step<false>(e);
     HIPCHK(hipGetLastError());
     e->policy_ready = false;
     if (reward) HIPCHK(hipMemcpyAsync(reward, e->d.reward, (size_t)4 * e->n, hipMemcpyDeviceToHost, e->stream));
@@ -956,7 +1005,7 @@ extern "C" int gc_env_step_random(gc_env* e, int n_plies) {
     if (!e->policy_ready) return fail("policy actions stale: call gc_env_reset or gc_env_select_random first");
     HIPCHK(hipSetDevice(e->device));
     for (int p = 0; p < n_plies; p++) {
-        k_env_step<true><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d);
+        launch_step<true>(e);
         HIPCHK(hipGetLastError());
     }
     return 0;
@@ -983,7 +1032,8 @@ extern "C" int gc_env_rollout(gc_env* e, int n_plies, int16_t* tr_action, int16_
     size_t cnt = (size_t)n_plies * e->n;
     if (trace && (dalloc(&da, cnt) || dalloc(&dr, cnt) || dalloc(&dd, cnt) || dalloc(&dq, cnt))) return -1;
     HIPCHK(hipMemsetAsync(e->stats, 0, (size_t)64 * e->n, e->stream));
-    k_env_rollout<<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d, n_plies, da, dr, dd, dq, e->stats);
+    if (e->d.opp) k_env_rollout<true><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d, n_plies, da, dr, dd, dq, e->stats);
+    else k_env_rollout<false><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d, n_plies, da, dr, dd, dq, e->stats);
     hipError_t le = hipGetLastError();
     if (le != hipSuccess) return fail(std::string("rollout launch: ") + hipGetErrorString(le));
     if (trace) {
@@ -1124,7 +1174,7 @@ extern "C" int gc_debug_stamps(gc_env* e, int n_plies, uint64_t* out /* (n/64)*8
     HIPCHK(hipMemsetAsync(d, 0, cnt * 8, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
     HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_out), &d, sizeof(d)));
-    for (int p = 0; p < n_plies; p++) k_env_step<true><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d);
+    for (int p = 0; p < n_plies; p++) k_env_step<true, false><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(out, d, cnt * 8, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));

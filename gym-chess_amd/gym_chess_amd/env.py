@@ -1,4 +1,8 @@
-"""Batched ChessEnvV2 on one GPU (chess_v2.py:132-602 semantics, opponent="none").
+"""Batched ChessEnvV2 on one GPU (chess_v2.py:132-602 semantics).
+
+opponent="none" (each step() is one ply, the caller plays both sides) or "random" (the
+device policy replies inside step(), chess_v2.py:275-292); player_color=BLACK makes the
+opponent open at every reset (chess_v2.py:208-216).
 
 `BatchedChessEnv(num_boards)` keeps N boards resident in HBM (bitboard SoA) and exposes
 the reference env surface vectorised over boards:
@@ -18,11 +22,11 @@ from . import _lib
 from . import codec as C
 
 REASONS = {0: "none", 1: "mate", 2: "repetition", 3: "move_cap", 4: "no_moves", 5: "both_kings_checked",
-           6: "invalid_action", 7: "already_done"}
+           6: "invalid_action", 7: "already_done", 8: "mated_by_opponent", 9: "opponent_no_move"}
 
 
 class BatchedChessEnv:
-    def __init__(self, num_boards, device=0, seed=0, initial_board=None):
+    def __init__(self, num_boards, device=0, seed=0, initial_board=None, opponent="none", player_color=C.WHITE):
         self._L = _lib.load()
         self.num_boards = int(num_boards)
         self.device = int(device)
@@ -34,6 +38,13 @@ class BatchedChessEnv:
         _lib.check(self._L.gc_env_create(self.device, self.num_boards, ctypes.c_uint64(self.seed),
                                          _lib.ptr(ib) if ib is not None else None, ctypes.byref(h)))
         self._h = h
+        if opponent not in ("none", "random"):
+            raise ValueError(f"Unrecognized opponent policy {opponent} (batched env: 'none' or 'random'; "
+                             "drive both sides yourself for a custom opponent)")
+        self.opponent = opponent
+        self.player_color = player_color
+        if opponent != "none" or player_color != C.WHITE:
+            _lib.check(self._L.gc_env_set_opponent(self._h, int(opponent == "random"), int(player_color == C.WHITE)))
 
     def close(self):
         if getattr(self, "_h", None):

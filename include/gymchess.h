@@ -72,11 +72,20 @@ typedef struct gc_env gc_env;
 int gc_env_create(int device, int n_boards, uint64_t seed, const int8_t* initial_board, gc_env** out);
 int gc_env_destroy(gc_env* e);
 int gc_env_num_boards(gc_env* e);
+/* Opponent mode (replaces ChessEnvV2(player_color, opponent), chess_v2.py:133-181):
+ * opponent 0 = "none", 1 = "random" -- the device policy replies inside every step()
+ * (chess_v2.py:275-292: -opp_reward, -100 when the agent is then mated); agent_white 0 =
+ * player_color BLACK (the opponent opens at every reset, chess_v2.py:208-216; requires
+ * opponent 1).  Resets every board.  A callable opponent = opponent 0 with the caller
+ * stepping both sides. */
+int gc_env_set_opponent(gc_env* e, int opponent, int agent_white);
 /* reset() (chess_v2.py:183-217) of the boards with mask[i] != 0 (mask NULL = all) */
 int gc_env_reset(gc_env* e, const uint8_t* mask);
 /* step(action) (chess_v2.py:219-294) for every board; host buffers of n entries.
  * reason[i]: 0 none, 1 mate (+100), 2 3-fold repetition, 3 move cap, 5 both kings checked
- * (reference raises; state unchanged), 6 invalid action (-10), 7 step after done. */
+ * (reference raises; state unchanged), 6 invalid action (-10), 7 step after done,
+ * 8 agent mated by the opponent's reply (-100), 9 the opponent has no legal reply (the
+ * reference's random policy returns "resign", which maps to no action and raises). */
 int gc_env_step(gc_env* e, const uint16_t* actions, int32_t* reward, uint8_t* done, uint8_t* reason);
 /* Device-resident random self-play (the test_benchmark.py driver): n_plies one-ply kernel
  * launches; each ply = one env.step() with a uniform Philox pick over the legal list, a

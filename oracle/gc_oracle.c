@@ -409,7 +409,7 @@ uint64_t oracle_perft(const int8_t *board, const uint8_t *meta, int depth) {
 }
 
 /* ====================================================================== */
-/* Env layer: chess_v2.py ChessEnvV2 with opponent="none"                 */
+/* Env layer: chess_v2.py ChessEnvV2, opponent "none" or the on-device random opponent     */
 /* ====================================================================== */
 typedef struct {
     OState st;               /* board, rights, checks; st.player = current_player */
@@ -422,9 +422,23 @@ typedef struct {
     int nsaved, capsaved;
     uint16_t moves[MAXMOVES];
     int nmoves;
+    /* opponent (chess_v2.py:167-181): 0 none, 1 random = the Philox policy below, drawing
+     * from the same per-board stream (seed, board, draw++) as the self-play driver */
+    int opp, agent_black;
+    uint64_t seed;
+    uint32_t board, draw;
+    /* distinct pre-move boards of reversible moves since the last pawn move / capture: the
+     * device's window length.  A BLACK agent's move_count never advances (291-292), so its
+     * games have no move cap; a window that would pass WINDOW_CAP ends the episode (reason
+     * 10) on the device and here alike. */
+    int win;
 } OEnv;
+#define WINDOW_CAP 768
 
-static void env_clear_saved(OEnv *e) { e->nsaved = 0; }
+uint32_t oracle_policy_index(uint64_t seed, uint32_t board, uint32_t draw, uint32_t n);
+static int kth_in_action_order(const uint16_t *moves, int n, int k);
+
+static void env_clear_saved(OEnv *e) { e->nsaved = 0; e->win = 0; }
 
 static int env_saved_inc(OEnv *e, const int8_t *b) {
     for (int i = 0; i < e->nsaved; i++)
@@ -439,7 +453,49 @@ static int env_saved_inc(OEnv *e, const int8_t *b) {
     return e->cnt[e->nsaved++];
 }
 
-/* chess_v2.py:183-217 (player_color=WHITE) */
+/* state as the engine sees it on each FFI call (convert_py_state -> State::new) */
+static void env_engine_state(const OEnv *e, OState *s) {
+    o_state_new(s, e->st.b, e->st.player, e->st.wkc, e->st.wqc, e->st.bkc, e->st.bqc);
+}
+
+/* the random opponent's pick: uniform rank over the legal list, k-th in action-id order */
+static int env_policy_pick(OEnv *e) {
+    uint32_t k = oracle_policy_index(e->seed, e->board, e->draw++, (uint32_t)e->nmoves);
+    return kth_in_action_order(e->moves, e->nmoves, (int)k);
+}
+
+/* player_move (chess_v2.py:393-412) + the state setter + switch_player + the next
+ * get_possible_moves: returns 1 on the both-kings-checked error (env unchanged), else 0
+ * with *mr = capture value and *rep = the 3-fold verdict on the PRE-move board, or 2 (move
+ * applied) when the window passes WINDOW_CAP. */
+static int env_player_move(OEnv *e, int action, int *mr, int *rep) {
+    OState s, ns;
+    env_engine_state(e, &s);
+    int me = e->st.player;
+    int irrev = action < 4096 && (type_of(e->st.b[action >> 6]) == PAWN || e->st.b[action & 63] != 0);
+    o_next_state(&s, me, action, &ns, mr);                                               /* 419 */
+    o_update_state(&ns);
+    if (ns.wchk && ns.bchk) return 1;                                                    /* lib.rs:1442 */
+    int c = env_saved_inc(e, e->st.b);
+    *rep = c >= 3;                                                                       /* 404-407 */
+    int full = 0;
+    if (irrev) e->win = 0;
+    else if (c == 1) { if (e->win >= WINDOW_CAP) full = 1; else e->win++; }
+    /* state setter (315-323): board, rights, checks; current_player is NOT taken from the dict */
+    memcpy(e->st.b, ns.b, 64);
+    e->st.wkc = ns.wkc; e->st.wqc = ns.wqc; e->st.bkc = ns.bkc; e->st.bqc = ns.bqc;
+    e->st.wchk = ns.wchk; e->st.bchk = ns.bchk;
+    e->st.player = (int8_t)(-me);                                                        /* switch_player */
+    OState s2;
+    env_engine_state(e, &s2);
+    e->nmoves = o_get_possible_moves(&s2, e->st.player, 0, e->moves, MAXMOVES);
+    return full ? 2 : 0;
+}
+
+/* chess_v2.py:183-217.  With player_color=BLACK the opponent opens as WHITE (208-216):
+ * its move counts for 3-fold, its `done` is discarded, move_count becomes 1.  An opening
+ * position without a legal move makes the reference's policy return "resign" and crash;
+ * here that marks the env done (reason 9 is reported by the next step). */
 void o_env_reset(OEnv *e) {
     OState s;
     o_state_new(&s, e->init, WHITE, 1, 1, 1, 1);
@@ -449,49 +505,53 @@ void o_env_reset(OEnv *e) {
     e->move_count = 0;
     env_clear_saved(e);
     e->nmoves = o_get_possible_moves(&e->st, WHITE, 0, e->moves, MAXMOVES);
+    if (e->opp && e->agent_black) {
+        if (e->nmoves == 0) { e->done = 1; return; }
+        int mr, rep;
+        if (env_player_move(e, env_policy_pick(e), &mr, &rep) == 1) { e->done = 1; return; }
+        e->move_count = 1;
+    }
 }
 
-/* state as the engine sees it on each FFI call (convert_py_state -> State::new) */
-static void env_engine_state(const OEnv *e, OState *s) {
-    o_state_new(s, e->st.b, e->st.player, e->st.wkc, e->st.wqc, e->st.bkc, e->st.bqc);
-}
-
-/* chess_v2.py:219-294 with opponent_policy=None.
- * Returns status: 0 ok, 1 both-kings-checked error (env unchanged; the reference raises SystemError).
- * reward / done out.  terminal reason out (0 none, 1 mate, 2 3-fold, 3 move cap, 6 invalid action). */
+/* chess_v2.py:219-294.
+ * Returns status: 0 ok, 1 both-kings-checked error (the reference raises SystemError).
+ * reward / done out.  Reason: 0 none, 1 opponent mated (+100), 2 3-fold, 3 move cap,
+ * 6 invalid action, 7 already done, 8 agent mated by the opponent's reply (-100),
+ * 9 the opponent has no legal reply and no check (the reference's policy returns "resign",
+ * which maps to no action: the reference raises; here the env ends), 10 window full. */
 int o_env_step(OEnv *e, int action, int *reward, int *done, int *reason) {
     *reason = 0;
     int valid = 0;
     for (int k = 0; k < e->nmoves; k++) if (e->moves[k] == action) { valid = 1; break; }
     if (!valid) { *reward = -10; *done = e->done; *reason = 6; return 0; }           /* 240-242 */
-    if (e->done) { *reward = 0; *done = 1; return 0; }                                 /* 245-251 */
+    if (e->done) { *reward = 0; *done = 1; *reason = 7; return 0; }                  /* 245-251 */
     if (e->move_count > 149) { *reward = 0; *done = 1; *reason = 3; return 0; }       /* 252-258 */
     int rw = -10;                                                                       /* 261 (Q9) */
-    OState s, ns;
-    env_engine_state(e, &s);
-    int mr;
-    int me = e->st.player;
-    o_next_state(&s, me, action, &ns, &mr);                                             /* 419 */
-    o_update_state(&ns);
-    if (ns.wchk && ns.bchk) { *reward = 0; *done = 0; return 1; }                      /* lib.rs:1442 */
-    int rep = env_saved_inc(e, e->st.b) >= 3;                                           /* 404-407 (pre-move board) */
-    /* state setter (315-323): board, rights, checks; current_player is NOT taken from the dict */
-    memcpy(e->st.b, ns.b, 64);
-    e->st.wkc = ns.wkc; e->st.wqc = ns.wqc; e->st.bkc = ns.bkc; e->st.bqc = ns.bqc;
-    e->st.wchk = ns.wchk; e->st.bchk = ns.bchk;
-    e->done = rep;
+    int mr, rep;
+    int pm = env_player_move(e, action, &mr, &rep);
+    if (pm == 1) { *reward = 0; *done = 0; return 1; }
+    e->done = rep || pm == 2;
     if (rep) *reason = 2;
+    if (pm == 2) *reason = 10;
     rw += mr;
-    e->st.player = (int8_t)(-me);                                                       /* switch_player */
-    OState s2;
-    env_engine_state(e, &s2);
-    e->nmoves = o_get_possible_moves(&s2, e->st.player, 0, e->moves, MAXMOVES);         /* 268 */
     int opp_chk = e->st.player == WHITE ? e->st.wchk : e->st.bchk;
     if (e->nmoves == 0 && opp_chk) { e->done = 1; rw += 100; *reason = 1; }              /* 270-272 */
     if (e->done) { *reward = rw; *done = 1; return 0; }
+    if (e->opp) {                                                                        /* 275-288 */
+        if (e->nmoves == 0) { e->done = 1; *reward = rw; *done = 1; *reason = 9; return 0; }
+        int omr, orep;
+        pm = env_player_move(e, env_policy_pick(e), &omr, &orep);
+        if (pm == 1) { *reward = rw; *done = 1; return 1; }
+        e->done = orep || pm == 2;
+        if (orep) *reason = 2;
+        if (pm == 2) *reason = 10;
+        rw -= omr;
+        int my_chk = e->st.player == WHITE ? e->st.wchk : e->st.bchk;
+        if (e->nmoves == 0 && my_chk) { e->done = 1; rw -= 100; *reason = 8; }
+    }
     if (e->st.player == WHITE) e->move_count++;                                         /* 291-292 */
     *reward = rw;
-    *done = 0;
+    *done = e->done;
     return 0;
 }
 
@@ -540,14 +600,16 @@ static int kth_in_action_order(const uint16_t *moves, int n, int k) {
  * Counters: steps taken; episodes by reason [0 none,1 mate,2 rep,3 cap,4 stalemate,5 error]. */
 typedef struct { uint64_t steps, reward_sum, ends[6]; } OStats; /* ends[0] unused */
 
-static void rollout_board(const int8_t *init, uint64_t seed, uint32_t board, int plies,
+static int stats_slot(int reason) { return reason == 8 ? 1 : (reason == 9 ? 4 : (reason == 10 ? 5 : reason)); }
+
+static void rollout_board(const int8_t *init, uint64_t seed, uint32_t board, int plies, int opp, int agent_black,
                           int16_t *tr_action, int16_t *tr_reward, uint8_t *tr_done, uint8_t *tr_reason,
                           int8_t *final_board, uint8_t *final_meta, uint32_t *final_draw, OStats *st) {
     OEnv e;
     memset(&e, 0, sizeof(e));
     memcpy(e.init, init, 64);
+    e.opp = opp; e.agent_black = agent_black; e.seed = seed; e.board = board; e.draw = 0;
     o_env_reset(&e);
-    uint32_t draw = 0;
     for (int p = 0; p < plies; p++) {
         int action = -1, rw = 0, dn = 0, reason = 0;
         if (e.nmoves == 0) {
@@ -556,13 +618,12 @@ static void rollout_board(const int8_t *init, uint64_t seed, uint32_t board, int
             st->ends[4]++;
             o_env_reset(&e);
         } else {
-            uint32_t k = oracle_policy_index(seed, board, draw++, (uint32_t)e.nmoves);
-            action = kth_in_action_order(e.moves, e.nmoves, (int)k);
+            action = env_policy_pick(&e);
             int rc = o_env_step(&e, action, &rw, &dn, &reason);
             st->steps++;
             st->reward_sum += (uint64_t)(int64_t)rw;
             if (rc == 1) { reason = 5; dn = 1; }
-            if (dn) { st->ends[reason]++; o_env_reset(&e); }
+            if (dn) { st->ends[stats_slot(reason)]++; o_env_reset(&e); }
         }
         if (tr_action) {
             tr_action[p] = (int16_t)action; tr_reward[p] = (int16_t)rw;
@@ -575,7 +636,7 @@ static void rollout_board(const int8_t *init, uint64_t seed, uint32_t board, int
         final_meta[1] = e.st.wkc; final_meta[2] = e.st.wqc; final_meta[3] = e.st.bkc; final_meta[4] = e.st.bqc;
         final_meta[5] = e.st.wchk; final_meta[6] = e.st.bchk; final_meta[7] = (uint8_t)e.move_count;
     }
-    if (final_draw) *final_draw = draw;
+    if (final_draw) *final_draw = e.draw;
     free(e.saved);
     free(e.cnt);
 }
@@ -587,26 +648,27 @@ void oracle_rollout_trace(const int8_t *init, uint64_t seed, uint32_t board, int
     OStats st;
     memset(&st, 0, sizeof(st));
     uint32_t draw;
-    rollout_board(init, seed, board, plies, tr_action, tr_reward, tr_done, tr_reason, final_board, final_meta, &draw, &st);
+    rollout_board(init, seed, board, plies, 0, 0, tr_action, tr_reward, tr_done, tr_reason, final_board, final_meta, &draw, &st);
     if (stats8) { stats8[0] = st.steps; stats8[1] = st.reward_sum; for (int i = 0; i < 6; i++) stats8[2 + i] = st.ends[i]; }
 }
 
 /* Multi-threaded batch rollout = CPU baseline (boards sharded across pthreads). */
-typedef struct { const int8_t *init; uint64_t seed; uint32_t b0, b1; int plies; OStats st; } Job;
+typedef struct { const int8_t *init; uint64_t seed; uint32_t b0, b1; int plies, opp, agent_black; OStats st; } Job;
 static void *job_run(void *arg) {
     Job *j = (Job *)arg;
     memset(&j->st, 0, sizeof(j->st));
     for (uint32_t b = j->b0; b < j->b1; b++)
-        rollout_board(j->init, j->seed, b, j->plies, NULL, NULL, NULL, NULL, NULL, NULL, NULL, &j->st);
+        rollout_board(j->init, j->seed, b, j->plies, j->opp, j->agent_black, NULL, NULL, NULL, NULL, NULL, NULL, NULL, &j->st);
     return NULL;
 }
-void oracle_rollout_batch(const int8_t *init, uint64_t seed, uint32_t b_begin, uint32_t n_boards, int plies,
-                          int threads, uint64_t *stats8) {
+void oracle_rollout_batch2(const int8_t *init, uint64_t seed, uint32_t b_begin, uint32_t n_boards, int plies,
+                           int opp, int agent_white, int threads, uint64_t *stats8) {
+    int agent_black = !agent_white;
     if (threads < 1) threads = 1;
     Job *jobs = (Job *)calloc((size_t)threads, sizeof(Job));
     pthread_t *th = (pthread_t *)calloc((size_t)threads, sizeof(pthread_t));
     for (int t = 0; t < threads; t++) {
-        jobs[t].init = init; jobs[t].seed = seed; jobs[t].plies = plies;
+        jobs[t].init = init; jobs[t].seed = seed; jobs[t].plies = plies; jobs[t].opp = opp; jobs[t].agent_black = agent_black;
         jobs[t].b0 = b_begin + (uint32_t)((uint64_t)n_boards * t / threads);
         jobs[t].b1 = b_begin + (uint32_t)((uint64_t)n_boards * (t + 1) / threads);
         pthread_create(&th[t], NULL, job_run, &jobs[t]);
@@ -619,6 +681,23 @@ void oracle_rollout_batch(const int8_t *init, uint64_t seed, uint32_t b_begin, u
     }
     free(jobs);
     free(th);
+}
+
+void oracle_rollout_batch(const int8_t *init, uint64_t seed, uint32_t b_begin, uint32_t n_boards, int plies,
+                          int threads, uint64_t *stats8) {
+    oracle_rollout_batch2(init, seed, b_begin, n_boards, plies, 0, 1, threads, stats8);
+}
+
+/* Trajectory with an opponent mode (0 none, 1 random) and agent colour. */
+void oracle_rollout_trace2(const int8_t *init, uint64_t seed, uint32_t board, int plies, int opp, int agent_white,
+                           int16_t *tr_action, int16_t *tr_reward, uint8_t *tr_done, uint8_t *tr_reason,
+                           int8_t *final_board, uint8_t *final_meta, uint64_t *stats8) {
+    OStats st;
+    memset(&st, 0, sizeof(st));
+    uint32_t draw;
+    rollout_board(init, seed, board, plies, opp, !agent_white, tr_action, tr_reward, tr_done, tr_reason, final_board,
+                  final_meta, &draw, &st);
+    if (stats8) { stats8[0] = st.steps; stats8[1] = st.reward_sum; for (int i = 0; i < 6; i++) stats8[2 + i] = st.ends[i]; }
 }
 
 /* Multi-threaded perft over many roots (CPU baseline for perft configs). */
@@ -644,12 +723,17 @@ void oracle_perft_batch(const int8_t *boards, const uint8_t *metas, uint32_t n, 
 }
 
 /* Env handle API for step-by-step trace tests (Python drives actions). */
-void *oracle_env_new(const int8_t *init) {
+void *oracle_env_new2(const int8_t *init, int opp, int agent_white, uint64_t seed, uint32_t board) {
     OEnv *e = (OEnv *)calloc(1, sizeof(OEnv));
     memcpy(e->init, init, 64);
+    e->opp = opp; e->agent_black = !agent_white; e->seed = seed; e->board = board;
     o_env_reset(e);
     return e;
 }
+void *oracle_env_new(const int8_t *init) { return oracle_env_new2(init, 0, 1, 0, 0); }
+uint32_t oracle_env_draw(void *h) { return ((OEnv *)h)->draw; }
+/* the self-play driver's pick for the side to move (same stream as the opponent's); -1 if none */
+int oracle_env_pick(void *h) { OEnv *e = (OEnv *)h; return e->nmoves ? env_policy_pick(e) : -1; }
 void oracle_env_free(void *h) { OEnv *e = (OEnv *)h; free(e->saved); free(e->cnt); free(e); }
 void oracle_env_reset(void *h) { o_env_reset((OEnv *)h); }
 int oracle_env_step(void *h, int action, int *reward, int *done, int *reason) { return o_env_step((OEnv *)h, action, reward, done, reason); }

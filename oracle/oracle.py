@@ -69,6 +69,16 @@ def lib():
         L.oracle_perft_batch.restype = None
         L.oracle_env_new.argtypes = [P]
         L.oracle_env_new.restype = P
+        L.oracle_env_new2.argtypes = [P, i32, i32, u64, u32]
+        L.oracle_env_new2.restype = P
+        L.oracle_env_pick.argtypes = [P]
+        L.oracle_env_pick.restype = i32
+        L.oracle_env_draw.argtypes = [P]
+        L.oracle_env_draw.restype = u32
+        L.oracle_rollout_trace2.argtypes = [P, u64, u32, i32, i32, i32, P, P, P, P, P, P, P]
+        L.oracle_rollout_trace2.restype = None
+        L.oracle_rollout_batch2.argtypes = [P, u64, u32, u32, i32, i32, i32, i32, P]
+        L.oracle_rollout_batch2.restype = None
         L.oracle_env_free.argtypes = [P]
         L.oracle_env_reset.argtypes = [P]
         L.oracle_env_step.argtypes = [P, i32, P, P, P]
@@ -146,8 +156,9 @@ def policy_index(seed, board, draw, n):
     return int(lib().oracle_policy_index(seed, board, draw, n))
 
 
-def rollout_trace(seed, board_id, plies, init=DEFAULT_BOARD):
-    """Single-board random self-play (test_benchmark.py driver shape, auto-reset).
+def rollout_trace(seed, board_id, plies, init=DEFAULT_BOARD, opponent=0, agent_white=True):
+    """Single-board random self-play (test_benchmark.py driver shape, auto-reset); with
+    opponent=1 the env answers every step with the random opponent (chess_v2.py:275-288).
     Returns dict of per-ply arrays + final state + stats."""
     init = np.ascontiguousarray(init, dtype=np.int8).reshape(64)
     a = np.zeros(plies, dtype=np.int16)
@@ -157,23 +168,34 @@ def rollout_trace(seed, board_id, plies, init=DEFAULT_BOARD):
     fb = np.zeros(64, dtype=np.int8)
     fm = np.zeros(8, dtype=np.uint8)
     st = np.zeros(8, dtype=np.uint64)
-    lib().oracle_rollout_trace(_p(init), seed, board_id, plies, _p(a), _p(r), _p(d), _p(why), _p(fb), _p(fm), _p(st))
+    lib().oracle_rollout_trace2(_p(init), seed, board_id, plies, int(opponent), int(bool(agent_white)), _p(a), _p(r),
+                                _p(d), _p(why), _p(fb), _p(fm), _p(st))
     return dict(action=a, reward=r, done=d, reason=why, final_board=fb, final_meta=fm, stats=st)
 
 
-def rollout_batch(seed, b_begin, n_boards, plies, threads=1, init=DEFAULT_BOARD):
+def rollout_batch(seed, b_begin, n_boards, plies, threads=1, init=DEFAULT_BOARD, opponent=0, agent_white=True):
     init = np.ascontiguousarray(init, dtype=np.int8).reshape(64)
     st = np.zeros(8, dtype=np.uint64)
-    lib().oracle_rollout_batch(_p(init), seed, b_begin, n_boards, plies, threads, _p(st))
+    lib().oracle_rollout_batch2(_p(init), seed, b_begin, n_boards, plies, int(opponent), int(bool(agent_white)), threads,
+                                _p(st))
     return st
 
 
 class OracleEnv:
-    """Step-by-step chess_v2.ChessEnvV2(opponent="none") restatement."""
+    """Step-by-step chess_v2.ChessEnvV2 restatement: opponent 0 = "none", 1 = the random
+    opponent drawing from the Philox stream (seed, board, draw++)."""
 
-    def __init__(self, init=DEFAULT_BOARD):
+    def __init__(self, init=DEFAULT_BOARD, opponent=0, agent_white=True, seed=0, board=0):
         self._init = np.ascontiguousarray(init, dtype=np.int8).reshape(64)
-        self.h = lib().oracle_env_new(_p(self._init))
+        self.h = lib().oracle_env_new2(_p(self._init), int(opponent), int(bool(agent_white)), int(seed), int(board))
+
+    def pick(self):
+        """the random policy's action for the side to move (advances the Philox counter)"""
+        return int(lib().oracle_env_pick(self.h))
+
+    @property
+    def draw(self):
+        return int(lib().oracle_env_draw(self.h))
 
     def __del__(self):
         if getattr(self, "h", None):

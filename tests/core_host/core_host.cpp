@@ -135,6 +135,7 @@ struct HostHist {  // same contract as the device DevHist (gc_env.h rep_prefetch
     RepEntry load(int p) const { return tabv[p]; }
     void store_hdr(int p, u64 h) { tabv[p].hdr = h; }
     void store(int p, const RepEntry& e) { tabv[p] = e; }
+    void commit() {}  // host stores are immediate
 };
 
 struct HostScratch {
@@ -177,76 +178,109 @@ static void host_reset(Pos& s, HostHist& h, const Pos& ip) {
     h.bump_gen();
 }
 
-extern "C" void host_rollout_trace(const int8_t* init, uint64_t seed, uint32_t board, int plies, int16_t* tr_action,
-                                   int16_t* tr_reward, uint8_t* tr_done, uint8_t* tr_reason, int8_t* final_board,
-                                   uint8_t* final_meta, uint64_t* stats8) {
-    Pos ip = from_mailbox(init, 0);
-    Pos s;
+// the self-play driver of k_env_step<true, OPP> / k_env_rollout<OPP> on the host
+struct HostEnv {
+    Pos init, s;
     HostHist h;
     HostScratch scr;
-    host_reset(s, h, ip);
-    u32 draw = 0;
     Gen g;
     MoveSet ms;
-    gen_init(s, g);
-    gen_moves(s, g, ms, scr);
-    int a = ms.total ? select_action(s, g, ms, scr, (int)policy_index(seed, board, draw++, (u32)ms.total)) : A_NONE;
+    int opp = 0, agent_black = 0;
+    PolicyCtx pc = {0, 0, 0};
+    void regen() {
+        gen_init(s, g);
+        gen_moves(s, g, ms, scr);
+    }
+    void reset() {
+        host_reset(s, h, init);
+        regen();
+        if (opp && agent_black) env_open_vs(s, h, g, ms, scr, pc);
+    }
+    int pick() {
+        return ms.total ? select_action(s, g, ms, scr, (int)policy_index(pc.seed, pc.board, pc.draw++, (u32)ms.total))
+                        : A_NONE;
+    }
+};
+
+extern "C" void host_rollout_trace2(const int8_t* init, uint64_t seed, uint32_t board, int plies, int opp,
+                                    int agent_white, int16_t* tr_action, int16_t* tr_reward, uint8_t* tr_done,
+                                    uint8_t* tr_reason, int8_t* final_board, uint8_t* final_meta, uint64_t* stats8) {
+    HostEnv e;
+    e.init = from_mailbox(init, 0);
+    e.opp = opp;
+    e.agent_black = !agent_white;
+    e.pc = PolicyCtx{seed, board, 0};
+    e.reset();
+    int a = e.pick();
     uint64_t steps = 0, rsum = 0, ends[6] = {0, 0, 0, 0, 0, 0};
     for (int p = 0; p < plies; p++) {
         StepOut o = {0, 0, R_NONE, 0};
         bool have = false;
         int played = a;
         if (a == A_NONE) {
-            host_reset(s, h, ip);
+            e.reset();
+            have = true;
             o.reason = R_NO_MOVES;
             ends[R_NO_MOVES]++;
             played = -1;
         } else {
-            o = env_step<false>(s, h, a, nullptr, g, ms, scr);
+            o = opp ? env_step_vs<false>(e.s, e.h, a, nullptr, e.g, e.ms, e.scr, e.pc)
+                    : env_step<false>(e.s, e.h, a, nullptr, e.g, e.ms, e.scr);
             have = o.moved;
             steps++;
             rsum += (uint64_t)(int64_t)o.reward;
             if (o.done) {
-                ends[o.reason < 6 ? o.reason : 0]++;
-                host_reset(s, h, ip);
-                have = false;
+                int slot = o.reason == R_MATED ? 1
+                           : (o.reason == R_OPP_NO_MOVE ? 4 : (o.reason == R_WINDOW_FULL ? 5 : o.reason));
+                ends[slot < 6 ? slot : 0]++;
+                e.reset();
+                have = true;
             }
         }
-        if (!have) {
-            gen_init(s, g);
-            gen_moves(s, g, ms, scr);
-        }
+        if (!have) e.regen();
         tr_action[p] = (int16_t)played;
         tr_reward[p] = (int16_t)o.reward;
         tr_done[p] = (uint8_t)o.done;
         tr_reason[p] = (uint8_t)o.reason;
-        a = ms.total ? select_action(s, g, ms, scr, (int)policy_index(seed, board, draw++, (u32)ms.total)) : A_NONE;
+        a = e.pick();
     }
-    export_state(s, final_board, final_meta);
+    export_state(e.s, final_board, final_meta);
     stats8[0] = steps; stats8[1] = rsum;
     for (int k = 0; k < 6; k++) stats8[2 + k] = ends[k];
 }
+extern "C" void host_rollout_trace(const int8_t* init, uint64_t seed, uint32_t board, int plies, int16_t* tr_action,
+                                   int16_t* tr_reward, uint8_t* tr_done, uint8_t* tr_reason, int8_t* final_board,
+                                   uint8_t* final_meta, uint64_t* stats8) {
+    host_rollout_trace2(init, seed, board, plies, 0, 1, tr_action, tr_reward, tr_done, tr_reason, final_board,
+                        final_meta, stats8);
+}
 
 // external-action env for step-by-step replay of the reference env traces
-struct HostEnv {
-    Pos init, s;
-    HostHist h;
-    HostScratch scr;
-};
-extern "C" void* host_env_new(const int8_t* init) {
+extern "C" void* host_env_new2(const int8_t* init, int opp, int agent_white, uint64_t seed, uint32_t board) {
     HostEnv* e = new HostEnv();
     e->init = from_mailbox(init, 0);
-    host_reset(e->s, e->h, e->init);
+    e->opp = opp;
+    e->agent_black = !agent_white;
+    e->pc = PolicyCtx{seed, board, 0};
+    e->reset();
     return e;
 }
+extern "C" void* host_env_new(const int8_t* init) { return host_env_new2(init, 0, 1, 0, 0); }
 extern "C" void host_env_free(void* p) { delete (HostEnv*)p; }
-extern "C" void host_env_reset(void* p) { HostEnv* e = (HostEnv*)p; host_reset(e->s, e->h, e->init); }
+extern "C" void host_env_reset(void* p) { ((HostEnv*)p)->reset(); }
+extern "C" int host_env_pick(void* p) {
+    HostEnv* e = (HostEnv*)p;
+    e->regen();
+    int a = e->pick();
+    return a == A_NONE ? -1 : a;
+}
+extern "C" uint32_t host_env_draw(void* p) { return ((HostEnv*)p)->pc.draw; }
 extern "C" int host_env_step(void* p, int action, int* reward, int* done, int* reason) {
     HostEnv* e = (HostEnv*)p;
-    Gen g0, g;
-    MoveSet ms;
+    Gen g0;
     gen_init(e->s, g0);
-    StepOut o = env_step<true>(e->s, e->h, action, &g0, g, ms, e->scr);
+    StepOut o = e->opp ? env_step_vs<true>(e->s, e->h, action, &g0, e->g, e->ms, e->scr, e->pc)
+                       : env_step<true>(e->s, e->h, action, &g0, e->g, e->ms, e->scr);
     *reward = o.reward;
     *done = o.done;
     *reason = o.reason;

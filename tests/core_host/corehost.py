@@ -44,6 +44,14 @@ def lib():
         L.host_rollout_trace.argtypes = [P, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, P, P, P, P, P, P, P]
         L.host_env_new.restype = P
         L.host_env_new.argtypes = [P]
+        L.host_env_new2.restype = P
+        L.host_env_new2.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint32]
+        L.host_env_pick.argtypes = [P]
+        L.host_env_pick.restype = ctypes.c_int
+        L.host_env_draw.argtypes = [P]
+        L.host_env_draw.restype = ctypes.c_uint32
+        L.host_rollout_trace2.argtypes = [P, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_int, P, P, P, P, P, P, P]
         L.host_env_free.argtypes = [P]
         L.host_env_reset.argtypes = [P]
         L.host_env_step.argtypes = [P, ctypes.c_int, P, P, P]
@@ -125,7 +133,7 @@ def perft_small(board, meta, depth):
     return int(lib().host_perft_small(_p(b), _p(m), int(depth)))
 
 
-def rollout_trace(seed, board_id, plies, init):
+def rollout_trace(seed, board_id, plies, init, opponent=0, agent_white=True):
     init = np.ascontiguousarray(init, dtype=np.int8).reshape(64)
     a = np.zeros(plies, dtype=np.int16)
     r = np.zeros(plies, dtype=np.int16)
@@ -134,14 +142,22 @@ def rollout_trace(seed, board_id, plies, init):
     fb = np.zeros(64, dtype=np.int8)
     fm = np.zeros(8, dtype=np.uint8)
     st = np.zeros(8, dtype=np.uint64)
-    lib().host_rollout_trace(_p(init), seed, board_id, plies, _p(a), _p(r), _p(d), _p(q), _p(fb), _p(fm), _p(st))
+    lib().host_rollout_trace2(_p(init), seed, board_id, plies, int(opponent), int(bool(agent_white)), _p(a), _p(r),
+                              _p(d), _p(q), _p(fb), _p(fm), _p(st))
     return dict(action=a, reward=r, done=d, reason=q, final_board=fb, final_meta=fm, stats=st)
 
 
 class HostEnv:
-    def __init__(self, init):
+    def __init__(self, init, opponent=0, agent_white=True, seed=0, board=0):
         self._init = np.ascontiguousarray(init, dtype=np.int8).reshape(64)
-        self.h = lib().host_env_new(_p(self._init))
+        self.h = lib().host_env_new2(_p(self._init), int(opponent), int(bool(agent_white)), int(seed), int(board))
+
+    def pick(self):
+        return int(lib().host_env_pick(self.h))
+
+    @property
+    def draw(self):
+        return int(lib().host_env_draw(self.h))
 
     def __del__(self):
         if getattr(self, "h", None):

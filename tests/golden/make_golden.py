@@ -484,6 +484,83 @@ def gen_env_traces(v2):
     return traces
 
 
+def trace_opp(v2, seed, board, n_steps, color, initial_board=None):
+    """ChessEnvV2 with a CALLABLE opponent (chess_v2.py:176-177, 211-212, 276-288) that plays
+    the device policy: rank k = policy_index(seed, board, draw++) over the legal list, k-th
+    in action-id order.  The driving agent draws from the same counter, so the device env
+    in opponent="random" mode must reproduce these traces exactly."""
+    draw = [0]
+
+    def pick(env, moves):
+        acts = sorted(env.move_to_action(m) for m in moves)
+        k = O.policy_index(seed, board, draw[0], len(acts))
+        draw[0] += 1
+        return acts[k]
+
+    def opponent(env):
+        if not env.possible_moves:
+            return "resign"  # make_random_policy's answer (chess_v2.py:120-122)
+        return C.action_to_move(pick(env, env.possible_moves))
+
+    kw = dict(player_color=color, opponent=opponent, log=False)
+    if initial_board is not None:
+        kw["initial_board"] = initial_board
+    env = v2.ChessEnvV2(**kw)
+    steps = []
+    for _ in range(n_steps):
+        moves = env.possible_moves
+        if not moves:
+            env.reset()
+            steps.append(dict(kind="reset", draw=draw[0]))
+            continue
+        action = pick(env, moves)
+        try:
+            state, reward, done, info = env.step(action)
+        except SystemError:
+            steps.append(dict(kind="error", action=int(action)))
+            env.reset()
+            steps.append(dict(kind="reset", draw=draw[0]))
+            continue
+        except TypeError:  # the opponent had no move: "resign" maps to no action
+            steps.append(dict(kind="opp_no_move", action=int(action)))
+            env.reset()
+            steps.append(dict(kind="reset", draw=draw[0]))
+            continue
+        steps.append(dict(kind="step", action=int(action), reward=float(reward), done=bool(done),
+                          board=C.board_to_text(np.asarray(state["board"]).reshape(64)),
+                          meta=[int(env.current_player == "WHITE"),
+                                int(state["white_king_castle_is_possible"]),
+                                int(state["white_queen_castle_is_possible"]),
+                                int(state["black_king_castle_is_possible"]),
+                                int(state["black_queen_castle_is_possible"]),
+                                int(bool(state["white_king_is_checked"])),
+                                int(bool(state["black_king_is_checked"]))],
+                          move_count=int(info["move_count"]), n_moves=len(env.possible_moves), draw=draw[0]))
+        if done:
+            env.reset()
+            steps.append(dict(kind="reset", draw=draw[0]))
+    return dict(seed=seed, board=board, color=color,
+                initial_board=None if initial_board is None else C.board_to_text(np.asarray(initial_board).reshape(64)),
+                steps=steps)
+
+
+def gen_opp_traces(v2):
+    out = []
+    for b in range(6):
+        out.append(trace_opp(v2, 0x0ABC, b, 400, "WHITE" if b % 2 == 0 else "BLACK"))
+    # sparse board: mates, kingless play and stalemated opponents come quickly
+    ib = np.zeros((8, 8), dtype=np.int8)
+    ib[7, 4] = 1
+    ib[7, 0] = 3
+    ib[6, 3] = 2
+    ib[0, 4] = -1
+    ib[1, 4] = -6
+    ib[0, 7] = -3
+    for b in range(6, 10):
+        out.append(trace_opp(v2, 0x0ABC, b, 300, "WHITE" if b % 2 == 0 else "BLACK", initial_board=ib))
+    return out
+
+
 def dump(name, obj, gz=False):
     path = os.path.join(HERE, name)
     data = json.dumps(obj, separators=(",", ":")).encode()
@@ -500,14 +577,19 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--deep", action="store_true", help="also v1 perft(5) (~4 min on 8 cores)")
     ap.add_argument("--games", type=int, default=10)
+    ap.add_argument("--only", choices=["opp"], help="regenerate one fixture only")
     args = ap.parse_args()
     v1, v2 = load_reference()
+    if args.only == "opp":
+        dump("v2_opp_traces.json.gz", gen_opp_traces(v2), gz=True)
+        return
     dump("perft_startpos.json", gen_perft_startpos(v1, args.deep))
     games, mid = gen_v1_games(v1, args.games, 320)
     dump("v1_games.json.gz", games, gz=True)
     dump("v1_perft_midgame.json", gen_v1_perft_midgame(v1, mid[:12], 3))
     dump("v2_known_answers.json", gen_v2_known_answers())
     dump("v2_env_traces.json.gz", gen_env_traces(v2), gz=True)
+    dump("v2_opp_traces.json.gz", gen_opp_traces(v2), gz=True)
 
 
 if __name__ == "__main__":
