@@ -428,13 +428,16 @@ __global__ void __launch_bounds__(BLOCK) k_env_reset(EnvDev e, const uint8_t* __
 }
 
 // set_states ingest for the env: import + empty window
-__global__ void k_env_import(const int8_t* __restrict__ boards, const uint8_t* __restrict__ meta8, EnvDev e) {
+// checks != 0: the check flags come from update_state (lib.rs:1386-1393) instead of meta8
+__global__ void k_env_import(const int8_t* __restrict__ boards, const uint8_t* __restrict__ meta8, EnvDev e,
+                             int checks) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= e.n) return;
     const uint8_t* m = meta8 + 8 * (size_t)i;
     u32 meta = (m[0] ? M_WHITE : 0u) | (m[1] ? M_WKC : 0u) | (m[2] ? M_WQC : 0u) | (m[3] ? M_BKC : 0u) |
                (m[4] ? M_BQC : 0u) | (m[5] ? M_WCHK : 0u) | (m[6] ? M_BCHK : 0u) | ((u32)m[7] << M_MC_SHIFT);
     Pos s = from_mailbox(boards + 64 * (size_t)i, meta);
+    if (checks) s.meta = (s.meta & ~(u32)(M_WCHK | M_BCHK)) | check_flags(s);
     e.st.store(i, s);
     e.hgen[i] += 1;  // empty the repetition window
 }
@@ -1086,7 +1089,125 @@ extern "C" int gc_env_set_states(gc_env* e, const int8_t* boards, const uint8_t*
     HIPCHK(hipSetDevice(e->device));
     HIPCHK(hipMemcpyAsync(e->mbox, boards, (size_t)64 * e->n, hipMemcpyHostToDevice, e->stream));
     HIPCHK(hipMemcpyAsync(e->m8, meta, (size_t)8 * e->n, hipMemcpyHostToDevice, e->stream));
-    k_env_import<<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->mbox, e->m8, e->d);
+    k_env_import<<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->mbox, e->m8, e->d, 0);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(e->stream));
+    e->policy_ready = false;
+    return 0;
+}
+
+// ----------------------------------------------------------------------------- FEN
+// Forsyth-Edwards ingest/export for the reference's state: piece
+// placement rank 8 first (= board row 0, lib.rs:41-50), side to move, castling -> the four
+// *_castle_is_possible flags; en passant and the half-move clock do not exist under the
+// reference's rules and are ignored; the full-move number n maps to move_count = n - 1
+// (chess_v2.py:291-292 counts completed full moves).  Host code, no GPU needed.
+static const char* FEN_PIECES = ".KQRBNP";
+
+extern "C" int gc_fen_to_state(const char* fen, int8_t* board, uint8_t* meta) {
+    if (!fen || !board || !meta) return fail("null argument");
+    int8_t b[64] = {0};
+    const char* p = fen;
+    while (*p == ' ') p++;
+    int row = 0, col = 0;
+    for (; *p && *p != ' '; p++) {
+        char c = *p;
+        if (c == '/') {
+            if (col != 8 || row >= 7) return fail(std::string("FEN: bad rank at '") + fen + "'");
+            row++;
+            col = 0;
+        } else if (c >= '1' && c <= '8') {
+            col += c - '0';
+            if (col > 8) return fail(std::string("FEN: rank overflow in '") + fen + "'");
+        } else {
+            const char* q = strchr(FEN_PIECES + 1, c >= 'a' ? c - 32 : c);
+            if (!q || c == '.' || col >= 8) return fail(std::string("FEN: bad piece '") + c + "' in '" + fen + "'");
+            int id = (int)(q - FEN_PIECES);
+            b[row * 8 + col++] = (int8_t)(c >= 'a' ? -id : id);
+        }
+    }
+    if (row != 7 || col != 8) return fail(std::string("FEN: placement must have 8 full ranks: '") + fen + "'");
+    uint8_t m[8] = {1, 0, 0, 0, 0, 0, 0, 0};
+    while (*p == ' ') p++;
+    if (*p) {
+        if (*p == 'b') m[0] = 0;
+        else if (*p != 'w') return fail(std::string("FEN: side to move must be w or b: '") + fen + "'");
+        p++;
+        while (*p == ' ') p++;
+        for (; *p && *p != ' '; p++) {
+            switch (*p) {
+                case 'K': m[1] = 1; break;
+                case 'Q': m[2] = 1; break;
+                case 'k': m[3] = 1; break;
+                case 'q': m[4] = 1; break;
+                case '-': break;
+                default: return fail(std::string("FEN: bad castling field in '") + fen + "'");
+            }
+        }
+        // en passant, half-move clock: ignored; full-move number -> move_count
+        int field = 0;
+        long full = 1;
+        while (*p) {
+            while (*p == ' ') p++;
+            if (!*p) break;
+            const char* st = p;
+            while (*p && *p != ' ') p++;
+            if (++field == 3) {
+                char* end = nullptr;
+                full = strtol(st, &end, 10);
+                if (end != p || full < 1) return fail(std::string("FEN: bad full-move number in '") + fen + "'");
+            }
+        }
+        long mc = full - 1;
+        m[7] = (uint8_t)(mc > 255 ? 255 : mc);
+    }
+    memcpy(board, b, 64);
+    memcpy(meta, m, 8);
+    return 0;
+}
+
+extern "C" int gc_state_to_fen(const int8_t* board, const uint8_t* meta, char* out, int cap) {
+    if (!board || !meta || !out) return fail("null argument");
+    if (check_boards(1, board)) return -1;
+    std::string f;
+    for (int r = 0; r < 8; r++) {
+        int gap = 0;
+        for (int c = 0; c < 8; c++) {
+            int v = board[r * 8 + c];
+            if (!v) { gap++; continue; }
+            if (gap) { f += (char)('0' + gap); gap = 0; }
+            char ch = FEN_PIECES[v < 0 ? -v : v];
+            f += v < 0 ? (char)(ch + 32) : ch;
+        }
+        if (gap) f += (char)('0' + gap);
+        if (r < 7) f += '/';
+    }
+    f += meta[0] ? " w " : " b ";
+    std::string cs;
+    if (meta[1]) cs += 'K';
+    if (meta[2]) cs += 'Q';
+    if (meta[3]) cs += 'k';
+    if (meta[4]) cs += 'q';
+    f += cs.empty() ? "-" : cs;
+    f += " - 0 " + std::to_string((int)meta[7] + 1);
+    if ((int)f.size() + 1 > cap) return fail("FEN output buffer too small");
+    memcpy(out, f.c_str(), f.size() + 1);
+    return 0;
+}
+
+// FEN ingest for the whole env: boards[i] := fens[i], check flags from update_state,
+// repetition windows cleared (like gc_env_set_states)
+extern "C" int gc_env_set_fens(gc_env* e, const char* const* fens) {
+    if (!e || !fens) return fail("null argument");
+    std::vector<int8_t> b((size_t)64 * e->n);
+    std::vector<uint8_t> m((size_t)8 * e->n);
+    for (int i = 0; i < e->n; i++)
+        if (gc_fen_to_state(fens[i], b.data() + 64 * (size_t)i, m.data() + 8 * (size_t)i))
+            return fail("board " + std::to_string(i) + ": " + g_err);
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipMemcpyAsync(e->mbox, b.data(), b.size(), hipMemcpyHostToDevice, e->stream));
+    HIPCHK(hipMemcpyAsync(e->m8, m.data(), m.size(), hipMemcpyHostToDevice, e->stream));
+    k_env_import<<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->mbox, e->m8, e->d, 1);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(e->stream));
     e->policy_ready = false;

@@ -28,6 +28,9 @@ SIGNATURES = {
     "gc_env_create": (_I, [_I, _I, _U64, _P, _P]),
     "gc_env_destroy": (_I, [_P]),
     "gc_env_set_opponent": (_I, [_P, _I, _I]),
+    "gc_env_set_fens": (_I, [_P, _P]),
+    "gc_fen_to_state": (_I, [ctypes.c_char_p, _P, _P]),
+    "gc_state_to_fen": (_I, [_P, _P, _P, _I]),
     "gc_env_num_boards": (_I, [_P]),
     "gc_env_reset": (_I, [_P, _P]),
     "gc_env_step": (_I, [_P, _P, _P, _P, _P]),

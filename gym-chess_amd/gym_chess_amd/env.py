@@ -121,6 +121,36 @@ class BatchedChessEnv:
         m = np.ascontiguousarray(meta, dtype=np.uint8).reshape(self.num_boards, 8)
         _lib.check(self._L.gc_env_set_states(self._h, _lib.ptr(b), _lib.ptr(m)))
 
+    def set_fens(self, fens):
+        """boards[i] := fens[i] (gym_chess_amd.fen mapping); check flags from update_state;
+        repetition windows cleared.  Call select_random() before step_random()."""
+        if len(fens) != self.num_boards:
+            raise ValueError(f"need {self.num_boards} FEN strings, got {len(fens)}")
+        arr = (ctypes.c_char_p * self.num_boards)(*[f.encode() for f in fens])
+        _lib.check(self._L.gc_env_set_fens(self._h, ctypes.cast(arr, ctypes.c_void_p)))
+
+    def fens(self):
+        from .fen import arrays_to_fen
+
+        b, m = self.boards()
+        return [arrays_to_fen(b[i], m[i]) for i in range(self.num_boards)]
+
+    def observation(self):
+        """int8[N, 8, 8] boards (the reference's observation, chess_v2.py:153-158)."""
+        return self.boards()[0].reshape(self.num_boards, 8, 8)
+
+    def info(self):
+        """the reference's info dict (chess_v2.py:337-353), batched as arrays."""
+        b, m = self.boards()
+        return dict(move_count=m[:, 7].astype(np.int32), current_player_is_white=m[:, 0].astype(bool),
+                    white_king_castle_is_possible=m[:, 1].astype(bool),
+                    white_queen_castle_is_possible=m[:, 2].astype(bool),
+                    black_king_castle_is_possible=m[:, 3].astype(bool),
+                    black_queen_castle_is_possible=m[:, 4].astype(bool),
+                    white_king_is_checked=m[:, 5].astype(bool), black_king_is_checked=m[:, 6].astype(bool),
+                    white_king_on_the_board=(b == C.KING_ID).any(axis=1),
+                    black_king_on_the_board=(b == -C.KING_ID).any(axis=1))
+
     # ------------------------------------------------------------------ device-resident driver
     def select_random(self):
         _lib.check(self._L.gc_env_select_random(self._h))

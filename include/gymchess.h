@@ -107,6 +107,15 @@ int gc_env_legal_moves(gc_env* e, uint16_t* moves, int cap, int32_t* counts);
 /* legal action mask per board: 64 words (from -> targets) + 1 word (bit c: action 4096+c) */
 int gc_env_legal_mask(gc_env* e, uint64_t* mask, int32_t* counts);
 int gc_env_synchronize(gc_env* e);
+/* FEN (host-side, no GPU): placement rank 8 first (board row 0), side to move, castling ->
+ * the four *_castle_is_possible flags (chess_v2.py:301-313); en passant and the half-move
+ * clock are ignored (not part of the reference's rules); full-move number n -> move_count
+ * n - 1 (meta8[7]).  A bare placement field means WHITE to move, no rights, move_count 0. */
+int gc_fen_to_state(const char* fen, int8_t* board, uint8_t* meta);
+int gc_state_to_fen(const int8_t* board, const uint8_t* meta, char* out, int cap);
+/* set every board from a FEN (n strings); check flags from update_state (lib.rs:1386-1393);
+ * repetition windows cleared */
+int gc_env_set_fens(gc_env* e, const char* const* fens);
 /* HIP events on the env's stream (8 slots) for in-process kernel timing */
 int gc_env_record_event(gc_env* e, int slot);
 int gc_env_elapsed_ms(gc_env* e, int a, int b, float* ms);
