@@ -48,8 +48,10 @@ def parse():
     ap.add_argument("--cpu-sample-boards", type=int, default=32768)
     ap.add_argument("--cpu-sample-plies", type=int, default=300)
     ap.add_argument("--fused-plies", type=int, default=200, help="also time the fused rollout kernel (0 = skip)")
-    ap.add_argument("--perft-roots", type=int, default=0, help="also time perft on mid-game roots (0 = skip)")
+    ap.add_argument("--perft-roots", type=int, default=65536, help="perft leg on mid-game FEN roots (0 = skip)")
     ap.add_argument("--perft-depth", type=int, default=5)
+    ap.add_argument("--cpu-perft-roots", type=int, default=256)
+    ap.add_argument("--cpu-perft-depth", type=int, default=4)
     return ap.parse_args()
 
 
@@ -75,24 +77,73 @@ def cpu_baseline(args):
     }
 
 
-def perft_leg(args, rep, device):
-    """configs[3]-shaped: mid-game roots from seeded random self-play, perft(depth)."""
-    from gym_chess_amd.engine import Engine
-    from gym_chess_amd.env import BatchedChessEnv
+def midgame_fens(n, seed, device):
+    """configs[3]: n mixed mid-game positions as FEN strings.  Board i is taken after
+    10 + (i*7919 mod 31) plies of seeded uniform-random self-play from the start position
+    (SURVEY.md §8d config 4), exported through the C-ABI's FEN codec."""
+    import numpy as np
 
-    src = BatchedChessEnv(args.perft_roots, device=device, seed=rep.board_seed(0x5EED + 4))
-    src.step_random(25)
-    b, m = src.boards()
+    from gym_chess_amd.env import BatchedChessEnv
+    from gym_chess_amd.fen import arrays_to_fen
+
+    src = BatchedChessEnv(n, device=device, seed=seed)
+    ply = 10 + (np.arange(n, dtype=np.int64) * 7919) % 31
+    b = np.zeros((n, 64), np.int8)
+    m = np.zeros((n, 8), np.uint8)
+    src.step_random(10)
+    for p in range(10, 41):
+        if p > 10:
+            src.step_random(1)
+        sel = ply == p
+        bb, mm = src.boards()
+        b[sel], m[sel] = bb[sel], mm[sel]
     src.close()
+    return [arrays_to_fen(b[i], m[i]) for i in range(n)]
+
+
+def perft_leg(args, rep, device):
+    """configs[3]: mid-game FEN roots, perft(depth) through the engine C-ABI
+    (gc_engine_perft: device level expansion + per-lane depth<=3 subtrees)."""
+    import numpy as np
+
+    from gym_chess_amd.engine import Engine
+    from gym_chess_amd.fen import fen_to_arrays
+
+    fens = midgame_fens(args.perft_roots, rep.board_seed(0x5EED + 4), device)
+    arr = [fen_to_arrays(f) for f in fens]
+    b = np.stack([a[0] for a in arr])
+    m = np.stack([a[1] for a in arr])
     eng = Engine(device)
+    b, m = eng.update_state(b, m)  # FEN carries no check flags: update_state, as chess_v2.py:204 does
+    eng.perft(b[:256], m[:256], 2)  # load the perft kernels outside the timed region
     rep.barrier()
     t0 = time.perf_counter()
     nodes = eng.perft(b, m, args.perft_depth)
     dt = time.perf_counter() - t0
+    eng.close()
     tot = rep.sum(float(nodes.sum()))
     dtm = rep.max(dt)
-    return {"value": tot / dtm, "unit": "perft_nodes/s", "roots_per_gpu": args.perft_roots, "depth": args.perft_depth,
-            "nodes": tot, "seconds": dtm}
+    castle = int((m[:, 1:5] != 0).any(axis=1).sum())
+    prom = int(((b[:, 8:16] == 6) | (b[:, 48:56] == -6)).any(axis=1).sum())
+    check = int((m[:, 5:7] != 0).any(axis=1).sum())
+    out = {"value": tot / dtm, "unit": "perft_nodes/s", "roots_per_gpu": args.perft_roots, "depth": args.perft_depth,
+           "nodes": tot, "seconds": dtm,
+           "roots_with": {"castle_right": castle, "pawn_on_7th": prom, "side_in_check": check}}
+    if rep.rank == 0 and not args.no_cpu_baseline and args.cpu_perft_roots > 0:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O
+
+        k, d = args.cpu_perft_roots, args.cpu_perft_depth
+        threads = max(1, min(16, os.cpu_count() or 1))
+        t0 = time.perf_counter()
+        cn = O.perft_batch(b[:k], m[:k], d, threads=threads)
+        cdt = time.perf_counter() - t0
+        if d == args.perft_depth:
+            assert (cn == nodes[:k]).all(), "oracle perft disagrees with the device"
+        out["cpu_baseline"] = {"value": float(cn.sum()) / cdt, "unit": "perft_nodes/s", "cores": threads,
+                               "kind": "port", "sample": f"first {k} roots x perft({d}) ({int(cn.sum())} nodes, "
+                               f"{cdt:.1f} s) with the C oracle"}
+    return out
 
 
 def main():
@@ -138,6 +189,7 @@ def main():
 
     extra = {}
     if args.fused_plies > 0:
+        env.rollout(1)  # load the rollout kernel: a first launch would time code-object loading
         env.synchronize()
         rep.barrier()
         f0 = time.perf_counter()

@@ -18,7 +18,7 @@ step() {
 for s in ${STEPS:-smoke pytest bench prof}; do
   case $s in
     smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    pytest) step pytest 1200 python -m pytest tests -x -q -m gpu ;;
+    pytest) step pytest 1200 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread ;;
     bench)  step bench 600 python bench.py ${BENCH_ARGS:-} ;;
     prof)   step prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 100 --warmup 20 ;;
     pmcf)   step pmcf 600 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 20 --warmup 400 --fused-plies 0 ;;
