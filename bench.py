@@ -5,7 +5,7 @@ Workload (BASELINE.json configs[2], the config the metric is quoted on): 65 536 
 GPU, random-policy self-play to terminal with auto-reset -- the reference's benchmark
 driver (/root/reference/gym_chess/test/v2/test_benchmark.py:9-43) vectorised.  One "step"
 = one env.step() on every board = one launch of the one-ply step kernel
-k_env_step<true>: the policy's action through the full chess_v2.py step bookkeeping
+k_env_step2 (two waves per 64 boards): the policy's action through the full chess_v2.py step bookkeeping
 (next_state, update_state, 3-fold on the pre-move board, move cap, mate bonus), the
 opponent's legal move list, the Philox pick of the next action, reset of finished boards.
 State, repetition windows and outputs stay in HBM; nothing crosses PCIe in the timed region.
@@ -27,7 +27,7 @@ sys.path.insert(0, os.path.join(ROOT, "gym-chess_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip-level parameters (8.0 TB/s spec)
 
-# algorithmic bytes per board per step of k_env_step<true>:
+# algorithmic bytes per board per step of k_env_step2:
 #   state 7x8 B bitboards + 4 B meta, read + write                     120
 #   action read + next-action write (u16)                                4
 #   Philox draw counter, step counter, window generation: read + write  24
@@ -175,7 +175,7 @@ def main():
     steps_all = rep.sum(s1 - s0)
     value = steps_all / dt_max
 
-    # roofline of the dominant kernel (k_env_step<true>), per launch, HIP events on its stream
+    # roofline of the dominant kernel (k_env_step2, the paired one-ply step), per launch, HIP events on its stream
     bytes_per_launch = n * ALG_BYTES_PER_BOARD
     avg_launch_s = kern_ms / 1e3 / args.steps
     achieved = bytes_per_launch / avg_launch_s / 1e9
@@ -229,7 +229,7 @@ def main():
                        "parallelism": f"replicas{rep.world_size}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_env_step<true>", "avg_launch_us": avg_launch_s * 1e6,
+                         "kernel": "k_env_step2", "avg_launch_us": avg_launch_s * 1e6,
                          "alg_bytes_per_board": ALG_BYTES_PER_BOARD, "mean_window": 0.5 * (w0 + w1) / n},
             "cpu_baseline": cpu,
             **extra,

@@ -284,7 +284,10 @@ struct Gen {
 // push jumps blockers (Q1) and can land beyond its pinner or beyond its own king.  King
 // moves are filtered by the pre-move enemy map instead (lib.rs:613-619, 1125-1128), which
 // keeps the Q6 retreat-along-the-ray quirk.
-GC_HD void gen_init(const Pos& s, Gen& g) {
+// The context is built in three parts so that a pair of waves can share it (gymchess.hip,
+// k_env_step2): gen_base (side, occupancy, tracked king), gen_pins (checkers, check mask,
+// pins) and gen_enemy (enemy attack map, castles) -- the last two are independent.
+GC_HD void gen_base(const Pos& s, Gen& g) {
     bool white = s.meta & M_WHITE;
     g.white = white;
     g.occ = occ_of(s);
@@ -297,8 +300,12 @@ GC_HD void gen_init(const Pos& s, Gen& g) {
     g.enemy_att = 0;
     g.castles = 0;
     g.in_check = false;
+}
+
+GC_HD void gen_pins(const Pos& s, Gen& g) {
     if (g.ks < 0) return;  // "King not present": no filter, no castling, no king moves
     int ks = g.ks;
+    bool white = g.white;
     u64 kb = bit(ks);
     u64 opp = g.opp;
     u64 rq = (s.r | s.q) & opp, bq = (s.b | s.q) & opp;
@@ -319,6 +326,11 @@ GC_HD void gen_init(const Pos& s, Gen& g) {
             g.pinrays |= between(ks, sq) | bit(sq);
         }
     }
+}
+
+GC_HD void gen_enemy(const Pos& s, Gen& g) {
+    if (g.ks < 0) return;
+    bool white = g.white;
     g.enemy_att = side_attacks(s, !white);
     // castling (lib.rs:578-610 gate = OR of the colour's rights + king on board;
     // geometry lib.rs:966-1056 tests the POSITIVE ids for black too: Q4)
@@ -333,6 +345,12 @@ GC_HD void gen_init(const Pos& s, Gen& g) {
         if (kpos && (wr & bit(base)) && !(occ & qs_empty) && !(A & qs_safe)) g.castles |= 1;
         if (kpos && (wr & bit(base + 7)) && !(occ & ks_empty) && !(A & ks_safe)) g.castles |= 2;
     }
+}
+
+GC_HD void gen_init(const Pos& s, Gen& g) {
+    gen_base(s, g);
+    gen_pins(s, g);
+    gen_enemy(s, g);
 }
 
 // pseudo targets (non-attack mode) of the own piece on `sq` of type `t`, before legality
@@ -522,18 +540,20 @@ GC_HD void park(MoveSet& ms, S& scr, u64 own, int sq, u64 tg, int& total) {
     }
 }
 
-template <class S>
-GC_HD void gen_moves(const Pos& s, const Gen& g, MoveSet& ms, S& scr) {
+GC_HD void moveset_clear(MoveSet& ms) {
     ms.fastp = ms.o1 = ms.o2 = ms.ol = ms.orr = 0;
 #pragma unroll
     for (int b = 0; b < 5; b++) ms.cnt[b] = 0;
-    ms.big = popc(g.own) > SCRATCH_SLOTS;
-    if (ms.big) {
-        ms.total = count_legal(s, g);
-        return;
-    }
+    ms.total = 0;
+    ms.big = false;
+}
+
+// Part A of the generation: pawns (set-wise), knights, kings.  `ms` cleared; ORs
+// into ms.cnt; returns the number of moves found.
+template <class S>
+GC_HD int gen_moves_a(const Pos& s, const Gen& g, MoveSet& ms, S& scr) {
     const u64 own = g.own, cm = g.checkmask, notown_cm = ~own & cm;
-    int total = popc(g.castles);
+    int total = 0;
     // pawns, set-wise (lib.rs:935-958; Q1: the double push tests only the destination)
     u64 P = s.p & own, fp = P & ~g.pinned, empty = ~g.occ;
     if (g.white) {
@@ -552,9 +572,9 @@ GC_HD void gen_moves(const Pos& s, const Gen& g, MoveSet& ms, S& scr) {
     if (S::kPark) {  // per-pawn counts o1+o2+ol+orr (0..4) as a bit-sliced sum
         u64 s1 = ms.o1 ^ ms.o2, c1 = ms.o1 & ms.o2, s2 = ms.ol ^ ms.orr, c2 = ms.ol & ms.orr;
         u64 b0 = s1 ^ s2, k0 = s1 & s2;
-        ms.cnt[0] = b0;
-        ms.cnt[1] = c1 ^ c2 ^ k0;
-        ms.cnt[2] = (c1 & c2) | (k0 & (c1 ^ c2));
+        ms.cnt[0] |= b0;
+        ms.cnt[1] |= c1 ^ c2 ^ k0;
+        ms.cnt[2] |= (c1 & c2) | (k0 & (c1 ^ c2));
     }
     u64 pp = P & g.pinned;  // pinned pawns: rare, per piece
     while (pp) {
@@ -568,7 +588,21 @@ GC_HD void gen_moves(const Pos& s, const Gen& g, MoveSet& ms, S& scr) {
         x &= x - 1;
         park(ms, scr, own, sq, ((g.pinned >> sq) & 1) ? 0 : knight_set(bit(sq)) & notown_cm, total);
     }
-    x = s.b & own;
+    x = s.k & own;  // every own king; filtered by the pre-move enemy map only (lib.rs:613-619)
+    while (x) {
+        int sq = ctz(x);
+        x &= x - 1;
+        park(ms, scr, own, sq, king_set(bit(sq)) & ~own & ~g.enemy_att, total);
+    }
+    return total;
+}
+
+// Part B: the sliders (bishops, rooks, queens).  ORs into ms.cnt; returns the number of moves found.
+template <class S>
+GC_HD int gen_moves_b(const Pos& s, const Gen& g, MoveSet& ms, S& scr) {
+    const u64 own = g.own, notown_cm = ~own & g.checkmask;
+    int total = 0;
+    u64 x = s.b & own;
     while (x) {
         int sq = ctz(x);
         x &= x - 1;
@@ -592,12 +626,20 @@ GC_HD void gen_moves(const Pos& s, const Gen& g, MoveSet& ms, S& scr) {
         if ((g.pinned >> sq) & 1) tg &= g.pinrays & line_through(g.ks, sq);
         park(ms, scr, own, sq, tg, total);
     }
-    x = s.k & own;  // every own king; filtered by the pre-move enemy map only (lib.rs:613-619)
-    while (x) {
-        int sq = ctz(x);
-        x &= x - 1;
-        park(ms, scr, own, sq, king_set(bit(sq)) & ~own & ~g.enemy_att, total);
+    return total;
+}
+
+template <class S>
+GC_HD void gen_moves(const Pos& s, const Gen& g, MoveSet& ms, S& scr) {
+    moveset_clear(ms);
+    ms.big = popc(g.own) > SCRATCH_SLOTS;
+    if (ms.big) {
+        ms.total = count_legal(s, g);
+        return;
     }
+    int total = popc(g.castles);
+    total += gen_moves_a(s, g, ms, scr);
+    total += gen_moves_b(s, g, ms, scr);
     ms.total = total;
 }
 
@@ -833,7 +875,7 @@ GC_HD void to_mailbox(const Pos& s, int8_t* b) {
 }
 
 // ---- Philox4x32-10 random policy (same stream as the test oracle's policy draw) -----------
-GC_HD u32 policy_index(u64 seed, u32 board, u32 draw, u32 n) {
+GC_HD u32 philox_x0(u64 seed, u32 board, u32 draw) {
     u32 k0 = (u32)seed, k1 = (u32)(seed >> 32);
     u32 x0 = board, x1 = draw, x2 = 0x5EEDu, x3 = 0u;
     for (int i = 0; i < 10; i++) {
@@ -847,7 +889,10 @@ GC_HD u32 policy_index(u64 seed, u32 board, u32 draw, u32 n) {
         k0 += 0x9E3779B9u;
         k1 += 0xBB67AE85u;
     }
-    return (u32)(((u64)x0 * n) >> 32);
+    return x0;
 }
+// uniform rank in [0, n) from the first Philox output word (multiply-shift)
+GC_HD u32 scale_rank(u32 x0, u32 n) { return (u32)(((u64)x0 * n) >> 32); }
+GC_HD u32 policy_index(u64 seed, u32 board, u32 draw, u32 n) { return scale_rank(philox_x0(seed, board, draw), n); }
 
 }  // namespace gc

@@ -14,6 +14,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -503,6 +504,229 @@ __global__ void __launch_bounds__(BLOCK) k_env_step(EnvDev e) {
     e.reward[i] = o.reward;
     e.done[i] = (uint8_t)o.done;
     e.reason[i] = (uint8_t)o.reason;
+}
+
+// ----------------------------------------------------------------------------- paired step
+// k_env_step2: the bench path (policy-driven self-play, opponent "none") with TWO waves per
+// 64 boards.  A lone wave issues a VALU instruction at most every 4 cycles while a SIMD-32
+// takes 2 per wave64 instruction (MI355X_MICROARCH.md, 'vector-instruction ISSUE cost'), so
+// one wave per SIMD -- 65 536 boards on 256 CUs -- leaves half the issue slots empty and
+// every memory/LDS wait exposed.  Here lane l of wave 0 and lane l of wave 1 share board l
+// and split its ply into two independent instruction streams (wave-uniform roles, no
+// divergence), exchanging through LDS at two barriers:
+//
+//   phase 1   W0: gen_pins (checkers, check mask, pins)
+//             W1: window probe of the pre-move board, gen_enemy (enemy map, castles), the
+//                 mover's own check flag
+//   ---- barrier: W0 gets enemy map / castles / mover-check, W1 gets check mask / pins
+//   phase 2   W0: Philox word of the next draw, pawns, knights, kings (gen_moves_a)
+//             W1: bishops, rooks, queens (gen_moves_b), then the 3-fold commit (the probe
+//                 has landed by now)
+//   ---- barrier: partial count planes / totals / 3-fold count exchanged
+//   phase 3   both: the step's outcome (reward, done, reason, move count, reset) --
+//             identical arithmetic on identical data; W0: the policy pick (k-th legal
+//             action in action-id order); W1: state, window and output stores.
+//
+// Results are bit-identical to k_env_step<true, false> (same gc_core/gc_env functions,
+// same order of decisions; tests/test_gpu_parity.py compares both with the oracle).
+#define PAIR_BOARDS 64
+struct PairLds {
+    u64 slots[SCRATCH_SLOTS][PAIR_BOARDS];  // parked targets (both waves write, W0 reads)
+    u64 pin3[3][PAIR_BOARDS];               // W0 -> W1: checkmask, pinned, pinrays
+    u64 enemy[PAIR_BOARDS];                 // W1 -> W0: enemy attack map
+    u32 f0[PAIR_BOARDS];                    // W0 -> W1: in_check
+    u32 f1[PAIR_BOARDS];                    // W1 -> W0: castles | my_chk << 2
+    u64 planes[2][5][PAIR_BOARDS];          // partial bit-sliced counts per wave
+    u32 part[2][PAIR_BOARDS];               // partial move totals per wave
+    u32 rep[PAIR_BOARDS];                   // W1 -> W0: 3-fold count c | window length << 8
+};
+struct PairScratch {
+    static constexpr bool kPark = true;
+    u64* base;
+    __device__ void put(int j, u64 v) { base[j * PAIR_BOARDS] = v; }
+    __device__ u64 get(int j) const { return base[j * PAIR_BOARDS]; }
+};
+// LDS writes of this wave complete, then the workgroup barrier.  Deliberately NOT
+// __syncthreads(): its fence would also drain vmcnt, i.e. wait for W1's window probe that
+// is meant to stay in flight through phase 1.
+__device__ __forceinline__ void pair_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+__global__ void __launch_bounds__(2 * PAIR_BOARDS) k_env_step2(EnvDev e) {
+    __shared__ PairLds L;
+    const int role = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // wave-uniform
+    const int l = threadIdx.x & (PAIR_BOARDS - 1);
+    const int i = blockIdx.x * PAIR_BOARDS + l;
+    const bool live = i < e.n;
+    const int ii = live ? i : e.n - 1;  // dead lanes read a valid board, store nothing
+    PairScratch scr{&L.slots[0][l]};
+    GC_STAMP(0);
+
+    // ---- phase 0: entry loads (one round trip), the action's preconditions, the move
+    Pos s = e.st.load(ii);
+    u32 ua = e.act[ii];
+    u32 g0 = 0, nst = 0, d = 0;
+    if (role) { g0 = e.hgen[ii]; nst = e.nsteps[ii]; } else { d = e.draw[ii]; }
+    pin(s); pin(ua); pin(g0); pin(nst); pin(d);
+    GC_STAMP(1);
+    const int a = (int)ua;
+    const bool none = a == A_NONE;                           // empty list: driver reset
+    const bool done0 = (s.meta & M_DONE) != 0;               // chess_v2.py:245-251
+    const bool cap = mc_of(s.meta) > MOVES_MAX;              // 252-258
+    const bool mv = live && !none && !done0 && !cap;         // env_ply runs
+    const bool white = (s.meta & M_WHITE) != 0;
+    Pos ns = s;
+    ns.meta = (ns.meta & ~(u32)M_RIGHTS) | eff_rights(s);    // State::new
+    int mr = 0;
+    bool irrev = false;
+    if (mv) apply_legal(ns, white, a, &mr, &irrev);
+    Gen g;
+    gen_base(ns, g);
+    DevHist h = e.hist(ii, g0);
+    RepProbe pr;
+    bool my_chk = false;
+    u32 x0 = 0;
+
+    // ---- phase 1
+    if (role == 0) {
+        gen_pins(ns, g);
+        L.pin3[0][l] = g.checkmask;
+        L.pin3[1][l] = g.pinned;
+        L.pin3[2][l] = g.pinrays;
+        L.f0[l] = g.in_check ? 1u : 0u;
+    } else {
+        if (mv) rep_prefetch(h, s, pr);  // pre-move board (Q8); lands during phases 1-2
+        gen_enemy(ns, g);
+        int mk = tracked_king(ns, white);
+        my_chk = mk >= 0 && sq_attacked(ns, mk, !white);
+        L.enemy[l] = g.enemy_att;
+        L.f1[l] = g.castles | (my_chk ? 4u : 0u);
+    }
+    GC_STAMP(2);
+    pair_barrier();
+    GC_STAMP(3);
+
+    // ---- phase 2
+    if (role == 0) {
+        g.enemy_att = L.enemy[l];
+        u32 f1 = L.f1[l];
+        g.castles = f1 & 3u;
+        my_chk = (f1 & 4u) != 0;
+    } else {
+        g.checkmask = L.pin3[0][l];
+        g.pinned = L.pin3[1][l];
+        g.pinrays = L.pin3[2][l];
+        g.in_check = L.f0[l] != 0;
+    }
+    const bool opp_chk = g.in_check;
+    const bool both = opp_chk && my_chk;                      // lib.rs:1442-1446
+    const bool gen = mv && !both;
+    MoveSet ms;
+    moveset_clear(ms);
+    ms.big = popc(g.own) > SCRATCH_SLOTS;
+    int part = 0;
+    int c = 0;
+    u32 hl = hl_of(s.meta);
+    if (role == 0) {
+        x0 = philox_x0(e.seed, (u32)i, d);  // the next draw (independent of the position)
+        if (gen) part = ms.big ? count_legal(ns, g) - popc(g.castles) : gen_moves_a(ns, g, ms, scr);
+    } else {
+        if (gen && !ms.big) part = gen_moves_b(ns, g, ms, scr);
+        if (gen) {
+            // the probe's data is first touched here (an opaque use after the generation:
+            // otherwise the compiler hoists the entry compare up to the load and waits there)
+            pin(pr.e0.hdr); pin(pr.e0.k); pin(pr.e0.q); pin(pr.e0.r);
+            pin(pr.e0.b); pin(pr.e0.n); pin(pr.e0.p); pin(pr.e0.w);
+            c = rep_commit(h, s, pr, hl, irrev);  // table write deferred to h.commit()
+        }
+        L.rep[l] = (u32)c | (hl << 8);
+    }
+#pragma unroll
+    for (int b = 0; b < 5; b++) L.planes[role][b][l] = ms.cnt[b];
+    L.part[role][l] = (u32)part;
+    GC_STAMP(4);
+    pair_barrier();
+    GC_STAMP(5);
+
+    // ---- phase 3: outcome (both waves), then pick (W0) / stores (W1)
+#pragma unroll
+    for (int b = 0; b < 5; b++) ms.cnt[b] |= L.planes[role ^ 1][b][l];
+    ms.total = part + (int)L.part[role ^ 1][l] + popc(g.castles);
+    if (role == 0) {
+        u32 rp = L.rep[l];
+        c = (int)(rp & 0xFFu);
+        hl = rp >> 8;
+    }
+    StepOut o = {0, 0, R_NONE, 0};
+    bool have = false;
+    if (none) {
+        o.reason = R_NO_MOVES;
+    } else {
+        nst += 1;
+        if (done0) { o.done = 1; o.reason = R_DONE_ALREADY; }
+        else if (cap) { o.done = 1; o.reason = R_MOVE_CAP; }
+        else if (both) { o.done = 1; o.reason = R_BOTH_CHECKED; }
+        else {
+            u32 chk = white ? ((my_chk ? M_WCHK : 0u) | (opp_chk ? M_BCHK : 0u))
+                            : ((opp_chk ? M_WCHK : 0u) | (my_chk ? M_BCHK : 0u));
+            bool rep = c >= 3;  // chess_v2.py:404-407
+            ns.meta = with_hl((ns.meta & ~(u32)(M_WCHK | M_BCHK | M_DONE)) | chk | ((rep || c == 0) ? M_DONE : 0u), hl);
+            s = ns;
+            o.reward = -10 + mr;
+            o.moved = 1;
+            if (rep) { o.done = 1; o.reason = R_REPETITION; }
+            if (c == 0) { o.done = 1; o.reason = R_WINDOW_FULL; }
+            if (ms.total == 0 && opp_chk) {  // 270-272
+                s.meta |= M_DONE;
+                o.done = 1;
+                o.reward += 100;
+                o.reason = R_MATE;
+            }
+            if (!o.done && !white) s.meta += (1u << M_MC_SHIFT);  // 291-292
+            have = true;
+        }
+        if (o.done) have = false;
+    }
+    if (!have) reset_board(e, s, h);  // also the no-move driver reset
+    if (role == 0) {
+        if (!have) {
+            if (e.ic.usable) {
+                g.white = e.ic.white; g.own = e.ic.own; g.castles = e.ic.castles;
+                ms.fastp = e.ic.fastp; ms.o1 = e.ic.o1; ms.o2 = e.ic.o2; ms.ol = e.ic.ol; ms.orr = e.ic.orr;
+#pragma unroll
+                for (int b = 0; b < 5; b++) ms.cnt[b] = e.ic.cnt[b];
+                ms.total = e.ic.total;
+                ms.big = false;
+#pragma unroll
+                for (int j = 0; j < SCRATCH_SLOTS; j++) scr.put(j, e.ic.slots[j]);
+            } else {
+                gen_init(s, g);
+                gen_moves(s, g, ms, scr);
+            }
+        }
+        uint16_t act = (uint16_t)A_NONE;
+        if (ms.total > 0) act = (uint16_t)select_action(s, g, ms, scr, (int)scale_rank(x0, (u32)ms.total));
+        GC_STAMP(6);
+        if (live) {
+            e.act[i] = act;
+            e.draw[i] = d + (ms.total > 0 ? 1u : 0u);
+        }
+    } else {
+        GC_STAMP(6);
+        if (live) {
+            h.commit();
+            e.st.store(i, s);
+            h.flush(g0);
+            e.nsteps[i] = nst;
+            e.reward[i] = o.reward;
+            e.done[i] = (uint8_t)o.done;
+            e.reason[i] = (uint8_t)o.reason;
+        }
+    }
+    GC_STAMP(7);
+#ifdef GC_STAMPS
+    if (g_stamp_out != nullptr && l == 0)
+        for (int q = 0; q < 8; q++) g_stamp_out[((size_t)blockIdx.x * 2 + role) * 8 + q] = gc_stamp_lds[role][q];
+#endif
 }
 
 // Fused K-ply random self-play: state in registers for the whole launch.  Per-ply outputs
@@ -1007,8 +1231,12 @@ extern "C" int gc_env_step_random(gc_env* e, int n_plies) {
     if (!e) return fail("null env");
     if (!e->policy_ready) return fail("policy actions stale: call gc_env_reset or gc_env_select_random first");
     HIPCHK(hipSetDevice(e->device));
+    static const bool one_wave = getenv("GC_STEP1") != nullptr;  // A/B switch to k_env_step<true, false>
     for (int p = 0; p < n_plies; p++) {
-        launch_step<true>(e);
+        if (!e->d.opp && !one_wave)
+            k_env_step2<<<(e->n + PAIR_BOARDS - 1) / PAIR_BOARDS, 2 * PAIR_BOARDS, 0, e->stream>>>(e->d);
+        else
+            launch_step<true>(e);
         HIPCHK(hipGetLastError());
     }
     return 0;
@@ -1290,12 +1518,15 @@ extern "C" int gc_env_window_sum(gc_env* e, uint64_t* sum) {
 #ifdef GC_STAMPS
 extern "C" int gc_debug_stamps(gc_env* e, int n_plies, uint64_t* out /* (n/64)*8 */) {
     unsigned long long* d = nullptr;
-    size_t cnt = (size_t)((e->n + 63) / 64) * 8;
+    size_t cnt = (size_t)((e->n + 63) / 64) * 16;  // per wave: 8 stamps (the paired kernel has 2 waves / 64 boards)
     if (dalloc(&d, cnt)) return -1;
     HIPCHK(hipMemsetAsync(d, 0, cnt * 8, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
     HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_out), &d, sizeof(d)));
-    for (int p = 0; p < n_plies; p++) k_env_step<true, false><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d);
+    for (int p = 0; p < n_plies; p++) {
+        if (getenv("GC_STEP1")) k_env_step<true, false><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d);
+        else k_env_step2<<<(e->n + PAIR_BOARDS - 1) / PAIR_BOARDS, 2 * PAIR_BOARDS, 0, e->stream>>>(e->d);
+    }
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(out, d, cnt * 8, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));

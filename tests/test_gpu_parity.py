@@ -260,6 +260,29 @@ def test_step_random_matches_fused_rollout():
     assert (oa["next_action"] == ob["next_action"]).all() and (oa["nsteps"] == ob["nsteps"]).all()
 
 
+def test_step_random_per_ply_vs_oracle(oracle):
+    """The bench kernel (k_env_step2, two waves per 64 boards) ply by ply: reward / done /
+    reason of every ply and the next policy action, bit-exact vs the oracle driver.  200
+    boards: the last workgroup is partial (dead lanes must reach the barriers)."""
+    from gym_chess_amd.env import BatchedChessEnv
+
+    n, plies, seed = 200, 320, 777
+    env = BatchedChessEnv(n, device=0, seed=seed)
+    refs = [oracle.rollout_trace(seed, i, plies + 1) for i in range(n)]
+    ra = np.stack([r["action"] for r in refs], axis=1)
+    rr = np.stack([r["reward"] for r in refs], axis=1)
+    rd = np.stack([r["done"] for r in refs], axis=1)
+    rq = np.stack([r["reason"] for r in refs], axis=1)
+    for p in range(plies):
+        env.step_random(1)
+        o = env.outputs()
+        nxt = np.where(ra[p + 1] < 0, 0xFFFF, ra[p + 1]).astype(np.uint16)
+        assert (o["reward"] == rr[p]).all(), (p, np.nonzero(o["reward"] != rr[p])[0][:4])
+        assert (o["done"] == rd[p]).all(), p
+        assert (o["reason"] == rq[p]).all(), p  # incl. R_NO_MOVES (4) on a no-move reset ply
+        assert (o["next_action"] == nxt).all(), (p, np.nonzero(o["next_action"] != nxt)[0][:4])
+
+
 def test_step_random_vs_oracle_final_state(oracle):
     from gym_chess_amd.env import BatchedChessEnv
 
