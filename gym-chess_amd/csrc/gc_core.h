@@ -226,13 +226,12 @@ GC_HD bool sq_attacked(const Pos& s, int sq, bool by_white) {
     u64 occ = occ_of(s);
     u64 them = by_white ? s.w : (occ & ~s.w);
     u64 m = bit(sq);
-    // pawn attack squares exclude squares holding the pawn owner's own king
-    if (!(s.k & them & m) && (pawn_att_set(m, !by_white) & s.p & them)) return true;
-    if (knight_set(m) & s.n & them) return true;
-    if (king_set(m) & s.k & them) return true;
-    if (rook_att(sq, occ) & (s.r | s.q) & them) return true;
-    if (bishop_att(sq, occ) & (s.b | s.q) & them) return true;
-    return false;
+    // pawn attack squares exclude squares holding the pawn owner's own king.  Branch-free:
+    // lanes of a wave hold different boards, so early exits only add branch overhead.
+    u64 pawns = (s.k & them & m) ? 0ull : (pawn_att_set(m, !by_white) & s.p & them);
+    u64 att = pawns | (knight_set(m) & s.n & them) | (king_set(m) & s.k & them) |
+              (rook_att(sq, occ) & (s.r | s.q) & them) | (bishop_att(sq, occ) & (s.b | s.q) & them);
+    return att != 0;
 }
 
 // tracked king square of a colour, or -1 (lib.rs:641-653: the `break` leaves only the
@@ -240,9 +239,10 @@ GC_HD bool sq_attacked(const Pos& s, int sq, bool by_white) {
 GC_HD int tracked_king(const Pos& s, bool white) {
     u64 occ = occ_of(s);
     u64 kk = s.k & (white ? s.w : (occ & ~s.w));
-    if (!kk) return -1;
-    int row = msb(kk) >> 3;
-    return ctz(kk & (0xFFull << (8 * row)));
+    u64 kz = kk ? kk : 1ull;  // branch-free: the result is discarded when there is no king
+    int row = msb(kz) >> 3;
+    int sq = ctz(kz & (0xFFull << (8 * row)));
+    return kk ? sq : -1;
 }
 
 // castle rights as the engine sees them on every call: State::new forces a colour's
@@ -312,19 +312,18 @@ GC_HD void gen_pins(const Pos& s, Gen& g) {
     u64 checkers = (pawn_att_set(kb, white) & s.p & opp) | (knight_set(kb) & s.n & opp) |
                    (king_set(kb) & s.k & opp) | (rook_att(ks, g.occ) & rq) | (bishop_att(ks, g.occ) & bq);
     g.in_check = checkers != 0;
-    if (checkers) {
-        if (checkers & (checkers - 1)) g.checkmask = 0;
-        else g.checkmask = checkers | between(ks, ctz(checkers));
-    }
+    // one checker: capture it or block (checkers | between); two: king moves only; none: all
+    u64 single = checkers | between(ks, ctz(checkers ? checkers : 1ull));
+    g.checkmask = !checkers ? ~0ull : ((checkers & (checkers - 1)) ? 0ull : single);
     u64 snipers = (rook_att(ks, opp) & rq) | (bishop_att(ks, opp) & bq);
     while (snipers) {
         int sq = ctz(snipers);
         snipers &= snipers - 1;
-        u64 bw = between(ks, sq) & g.occ;
-        if (bw && !(bw & (bw - 1)) && (bw & g.own)) {
-            g.pinned |= bw;
-            g.pinrays |= between(ks, sq) | bit(sq);
-        }
+        u64 seg = between(ks, sq);
+        u64 bw = seg & g.occ;
+        bool pin = bw && !(bw & (bw - 1)) && (bw & g.own);
+        g.pinned |= pin ? bw : 0ull;
+        g.pinrays |= pin ? (seg | bit(sq)) : 0ull;
     }
 }
 
@@ -336,15 +335,14 @@ GC_HD void gen_enemy(const Pos& s, Gen& g) {
     // geometry lib.rs:966-1056 tests the POSITIVE ids for black too: Q4)
     u32 er = eff_rights(s);
     bool gate = white ? (er & (M_WKC | M_WQC)) : (er & (M_BKC | M_BQC));
-    if (gate) {
-        u64 wr = s.r & s.w, wk = s.k & s.w, A = g.enemy_att, occ = g.occ;
-        int base = white ? 56 : 0;
-        u64 qs_empty = 7ull << (base + 1), ks_empty = 3ull << (base + 5);
-        u64 qs_safe = 7ull << (base + 2), ks_safe = 7ull << (base + 4);
-        bool kpos = wk & bit(base + 4);
-        if (kpos && (wr & bit(base)) && !(occ & qs_empty) && !(A & qs_safe)) g.castles |= 1;
-        if (kpos && (wr & bit(base + 7)) && !(occ & ks_empty) && !(A & ks_safe)) g.castles |= 2;
-    }
+    u64 wr = s.r & s.w, wk = s.k & s.w, A = g.enemy_att, occ = g.occ;
+    int base = white ? 56 : 0;
+    u64 qs_empty = 7ull << (base + 1), ks_empty = 3ull << (base + 5);
+    u64 qs_safe = 7ull << (base + 2), ks_safe = 7ull << (base + 4);
+    bool kpos = gate && (wk & bit(base + 4));
+    bool qs = kpos && (wr & bit(base)) && !(occ & qs_empty) && !(A & qs_safe);
+    bool kside = kpos && (wr & bit(base + 7)) && !(occ & ks_empty) && !(A & ks_safe);
+    g.castles = (qs ? 1u : 0u) | (kside ? 2u : 0u);
 }
 
 GC_HD void gen_init(const Pos& s, Gen& g) {
@@ -667,12 +665,13 @@ GC_HD int kth_set_bit(u64 x, int k) {  // 0-based, ascending; x has > k set bits
     return base;
 }
 GC_HD u64 fast_pawn_targets(const MoveSet& ms, int sq, bool white) {
-    u64 t = 0;
-    if ((ms.o1 >> sq) & 1) t |= bit(white ? sq - 8 : sq + 8);
-    if ((ms.o2 >> sq) & 1) t |= bit(white ? sq - 16 : sq + 16);
-    if ((ms.ol >> sq) & 1) t |= bit(white ? sq - 7 : sq + 9);
-    if ((ms.orr >> sq) & 1) t |= bit(white ? sq - 9 : sq + 7);
-    return t;
+    // origin-indexed move sets shifted onto the target squares, then isolated at sq's targets
+    u64 m = bit(sq);
+    u64 t1 = white ? ((ms.o1 & m) >> 8) : ((ms.o1 & m) << 8);
+    u64 t2 = white ? ((ms.o2 & m) >> 16) : ((ms.o2 & m) << 16);
+    u64 tl = white ? ((ms.ol & m) >> 7) : ((ms.ol & m) << 9);
+    u64 tr = white ? ((ms.orr & m) >> 9) : ((ms.orr & m) << 7);
+    return t1 | t2 | tl | tr;
 }
 template <class S>
 GC_HD int select_action(const Pos& s, const Gen& g, const MoveSet& ms, const S& scr, int k) {
@@ -699,7 +698,8 @@ GC_HD int select_action(const Pos& s, const Gen& g, const MoveSet& ms, const S& 
     for (int step = 32; step; step >>= 1)
         if (prefix_count(ms.cnt, bit(lo + step) - 1) <= k) lo += step;
     k -= prefix_count(ms.cnt, bit(lo) - 1);
-    u64 tg = ((ms.fastp >> lo) & 1) ? fast_pawn_targets(ms, lo, g.white) : scr.get(ordinal(g.own, lo));
+    u64 parked = scr.get(ordinal(g.own, lo));  // both candidates, then a select (no branch)
+    u64 tg = ((ms.fastp >> lo) & 1) ? fast_pawn_targets(ms, lo, g.white) : parked;
     return lo * 64 + kth_set_bit(tg, k);
 }
 
@@ -835,7 +835,9 @@ GC_HD void apply_legal(Pos& s, bool white, int action, int* reward, bool* irrev)
     int f = action >> 6, t = action & 63;
     u64 fm = bit(f), tm = bit(t), clr = ~(fm | tm);
     // captured value (lib.rs:19-25, 698): Q 10, R 5, B/N 3, P 1, K 0
-    int v = (s.q & tm) ? 10 : ((s.r & tm) ? 5 : (((s.b | s.n) & tm) ? 3 : ((s.p & tm) ? 1 : 0)));
+    // the target holds at most one piece: a sum of bit tests, no branch chain
+    int v = 10 * (int)((s.q >> t) & 1) + 5 * (int)((s.r >> t) & 1) + 3 * (int)(((s.b | s.n) >> t) & 1) +
+            (int)((s.p >> t) & 1);
     *reward = v;
     *irrev = ((s.p & fm) != 0) || ((occ_of(s) & tm) != 0);
     bool wk = (s.k & s.w & fm) != 0, wr = (s.r & s.w & fm) != 0;

@@ -35,6 +35,7 @@ __device__ __forceinline__ void gc_stamp(int k) {
 #include "gc_core.h"
 #include "gc_env.h"
 #include "gc_perft.h"
+#include "gc_fide.h"
 #include "../../include/gymchess.h"
 
 using namespace gc;
@@ -814,6 +815,8 @@ __global__ void __launch_bounds__(BLOCK) k_select(EnvDev e) {
     e.draw[i] = d;
 }
 
+#include "gc_fide_kernels.h"
+
 // ----------------------------------------------------------------------------- host side
 static inline int grid_for(int n) { return (n + BLOCK - 1) / BLOCK; }
 
@@ -834,6 +837,7 @@ struct gc_engine {
     int8_t* mbox = nullptr; uint8_t* m8 = nullptr; uint8_t* side = nullptr;
     uint16_t* acts = nullptr; int32_t* i32a = nullptr; int32_t* i32b = nullptr;
     uint16_t* list = nullptr; uint64_t* u64o = nullptr;
+    int rules = 0;  // 0 reference (lib.rs), 1 FIDE (gc_fide.h)
 };
 
 static void engine_free_bufs(gc_engine* e) {
@@ -873,8 +877,22 @@ static int engine_upload(gc_engine* e, int n, const int8_t* boards, const uint8_
     HIPCHK(hipMemcpyAsync(e->m8, meta, (size_t)8 * n, hipMemcpyHostToDevice, e->stream));
     if (side) HIPCHK(hipMemcpyAsync(e->side, side, n, hipMemcpyHostToDevice, e->stream));
     SoA st{e->bb, e->meta, n};
-    k_import<<<grid_for(n), BLOCK, 0, e->stream>>>(e->mbox, e->m8, side ? e->side : nullptr, st);
+    if (e->rules) k_fimport<<<grid_for(n), BLOCK, 0, e->stream>>>(e->mbox, e->m8, side ? e->side : nullptr, st);
+    else k_import<<<grid_for(n), BLOCK, 0, e->stream>>>(e->mbox, e->m8, side ? e->side : nullptr, st);
     HIPCHK(hipGetLastError());
+    return 0;
+}
+
+static void engine_export(gc_engine* e, SoA st) {
+    if (e->rules) k_fexport<<<grid_for(st.n), BLOCK, 0, e->stream>>>(st, e->mbox, e->m8);
+    else k_export<<<grid_for(st.n), BLOCK, 0, e->stream>>>(st, e->mbox, e->m8);
+}
+
+// rules 0: the reference's (default); 1: FIDE (gc_fide.h; meta8[7] = en-passant file + 1)
+extern "C" int gc_engine_set_rules(gc_engine* e, int rules) {
+    if (!e) return fail("null engine");
+    if (rules != 0 && rules != 1) return fail("rules must be 0 (reference) or 1 (fide)");
+    e->rules = rules;
     return 0;
 }
 
@@ -909,7 +927,8 @@ extern "C" int gc_engine_get_possible_moves(gc_engine* e, int n, const int8_t* b
     if (cap <= 0) return fail("cap must be > 0");
     if (engine_reserve(e, n, cap)) return -1;
     if (engine_upload(e, n, boards, meta, player_white)) return -1;
-    k_list<<<grid_for(n), BLOCK, 0, e->stream>>>(SoA{e->bb, e->meta, n}, attack ? 1 : 0, cap, e->list, e->i32a);
+    if (e->rules) k_flist<<<grid_for(n), BLOCK, 0, e->stream>>>(SoA{e->bb, e->meta, n}, attack ? 1 : 0, cap, e->list, e->i32a);
+    else k_list<<<grid_for(n), BLOCK, 0, e->stream>>>(SoA{e->bb, e->meta, n}, attack ? 1 : 0, cap, e->list, e->i32a);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(moves, e->list, (size_t)2 * cap * n, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipMemcpyAsync(counts, e->i32a, (size_t)4 * n, hipMemcpyDeviceToHost, e->stream));
@@ -925,7 +944,8 @@ extern "C" int gc_engine_get_castle_moves(gc_engine* e, int n, const int8_t* boa
     std::vector<u64> mask((size_t)65 * n);
     u64* dmask = nullptr;
     if (dalloc(&dmask, (size_t)65 * n)) return -1;
-    k_mask<<<grid_for(n), BLOCK, 0, e->stream>>>(SoA{e->bb, e->meta, n}, dmask, nullptr);
+    if (e->rules) k_fmask<<<grid_for(n), BLOCK, 0, e->stream>>>(SoA{e->bb, e->meta, n}, dmask, nullptr);
+    else k_mask<<<grid_for(n), BLOCK, 0, e->stream>>>(SoA{e->bb, e->meta, n}, dmask, nullptr);
     hipError_t le = hipGetLastError();
     hipError_t ce = hipMemcpyAsync(mask.data(), dmask, (size_t)8 * 65 * n, hipMemcpyDeviceToHost, e->stream);
     hipError_t se = hipStreamSynchronize(e->stream);
@@ -951,13 +971,16 @@ extern "C" int gc_engine_next_state(gc_engine* e, int n, const int8_t* boards, c
     for (int i = 0; i < n; i++)
         if (actions[i] > A_QSB) return fail("action out of range at index " + std::to_string(i));
     if (engine_reserve(e, n, 1)) return -1;
-    if (engine_upload(e, n, boards, meta, nullptr)) return -1;
+    // FIDE: the player argument is the side to move; reference: it only steers next_state's
+    // promotion colour and rights logic (lib.rs:679-784), the state keeps current_player
+    if (engine_upload(e, n, boards, meta, e->rules ? player_white : nullptr)) return -1;
     HIPCHK(hipMemcpyAsync(e->side, player_white, n, hipMemcpyHostToDevice, e->stream));
     HIPCHK(hipMemcpyAsync(e->acts, actions, (size_t)2 * n, hipMemcpyHostToDevice, e->stream));
     SoA in{e->bb, e->meta, n}, out{e->bb2, e->meta2, n};
-    k_next_state<<<grid_for(n), BLOCK, 0, e->stream>>>(in, e->side, e->acts, out, e->i32a, e->i32b);
+    if (e->rules) k_fnext_state<<<grid_for(n), BLOCK, 0, e->stream>>>(in, e->acts, out, e->i32a, e->i32b);
+    else k_next_state<<<grid_for(n), BLOCK, 0, e->stream>>>(in, e->side, e->acts, out, e->i32a, e->i32b);
     HIPCHK(hipGetLastError());
-    k_export<<<grid_for(n), BLOCK, 0, e->stream>>>(out, e->mbox, e->m8);
+    engine_export(e, out);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(out_boards, e->mbox, (size_t)64 * n, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipMemcpyAsync(out_meta, e->m8, (size_t)8 * n, hipMemcpyDeviceToHost, e->stream));
@@ -973,9 +996,10 @@ extern "C" int gc_engine_update_state(gc_engine* e, int n, const int8_t* boards,
     if (engine_reserve(e, n, 1)) return -1;
     if (engine_upload(e, n, boards, meta, nullptr)) return -1;
     SoA st{e->bb, e->meta, n};
-    k_update_state<<<grid_for(n), BLOCK, 0, e->stream>>>(st);
+    if (e->rules) k_fupdate_state<<<grid_for(n), BLOCK, 0, e->stream>>>(st);
+    else k_update_state<<<grid_for(n), BLOCK, 0, e->stream>>>(st);
     HIPCHK(hipGetLastError());
-    k_export<<<grid_for(n), BLOCK, 0, e->stream>>>(st, e->mbox, e->m8);
+    engine_export(e, st);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(out_boards, e->mbox, (size_t)64 * n, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipMemcpyAsync(out_meta, e->m8, (size_t)8 * n, hipMemcpyDeviceToHost, e->stream));
@@ -985,7 +1009,7 @@ extern "C" int gc_engine_update_state(gc_engine* e, int n, const int8_t* boards,
 
 // perft over n roots (side to move = meta[0]).  Levels are expanded on the device while
 // more than 3 plies remain, or while there are too few subtrees to fill the chip.
-static int perft_device(hipStream_t st, SoA roots, int depth, uint64_t* d_out) {
+static int perft_device(hipStream_t st, SoA roots, int depth, uint64_t* d_out, int fide) {
     struct Level {
         u64* bb = nullptr; u32* meta = nullptr; int32_t* cnt = nullptr; int32_t* offs = nullptr;
         uint64_t* val = nullptr; int n = 0;
@@ -1006,7 +1030,8 @@ static int perft_device(hipStream_t st, SoA roots, int depth, uint64_t* d_out) {
         Level& cur = lv.back();
         if (dalloc(&cur.cnt, cur.n) || dalloc(&cur.offs, cur.n)) { cleanup(); return -1; }
         SoA cs{cur.bb, cur.meta, cur.n};
-        k_count_children<<<grid_for(cur.n), BLOCK, 0, st>>>(cs, cur.cnt);
+        if (fide) k_fcount_children<<<grid_for(cur.n), BLOCK, 0, st>>>(cs, cur.cnt);
+        else k_count_children<<<grid_for(cur.n), BLOCK, 0, st>>>(cs, cur.cnt);
         size_t tmp_bytes = 0;
         void* tmp = nullptr;
         hipError_t he = hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, cur.cnt, cur.offs, cur.n, st);
@@ -1027,7 +1052,8 @@ static int perft_device(hipStream_t st, SoA roots, int depth, uint64_t* d_out) {
             return -1;
         }
         SoA ns{nx.bb, nx.meta, nx.n};
-        k_expand<<<grid_for(cur.n), BLOCK, 0, st>>>(cs, cur.offs, ns);
+        if (fide) k_fexpand<<<grid_for(cur.n), BLOCK, 0, st>>>(cs, cur.offs, ns);
+        else k_expand<<<grid_for(cur.n), BLOCK, 0, st>>>(cs, cur.offs, ns);
         lv.push_back(nx);
         rem--;
         if (total == 0) break;
@@ -1037,7 +1063,8 @@ static int perft_device(hipStream_t st, SoA roots, int depth, uint64_t* d_out) {
     uint64_t* leaf_out = lv.size() > 1 ? leaf.val : d_out;
     if (leaf.n > 0) {
         SoA ls{leaf.bb, leaf.meta, leaf.n};
-        k_perft_small<<<grid_for(leaf.n), BLOCK, 0, st>>>(ls, rem, leaf_out);
+        if (fide) k_fperft_small<<<grid_for(leaf.n), BLOCK, 0, st>>>(ls, rem, leaf_out);
+        else k_perft_small<<<grid_for(leaf.n), BLOCK, 0, st>>>(ls, rem, leaf_out);
     }
     for (int l = (int)lv.size() - 2; l >= 0; l--) {
         uint64_t* dst = l == 0 ? d_out : lv[l].val;
@@ -1059,7 +1086,7 @@ extern "C" int gc_engine_perft(gc_engine* e, int n, const int8_t* boards, const 
     if (depth < 0 || depth > PERFT_MAXD) return fail("depth must be in [0, 8]");
     if (engine_reserve(e, n, 1)) return -1;
     if (engine_upload(e, n, boards, meta, nullptr)) return -1;
-    if (perft_device(e->stream, SoA{e->bb, e->meta, n}, depth, e->u64o)) return -1;
+    if (perft_device(e->stream, SoA{e->bb, e->meta, n}, depth, e->u64o, e->rules)) return -1;
     HIPCHK(hipMemcpyAsync(nodes, e->u64o, (size_t)8 * n, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
     return 0;
@@ -1077,10 +1104,12 @@ struct gc_env {
     uint64_t* stats = nullptr;
     hipEvent_t ev[8] = {};
     bool policy_ready = false;  // act[] holds policy picks for the current states
+    int rules = 0;              // 0 reference, 1 FIDE (gc_fide.h)
+    int8_t* ep = nullptr;       // FIDE ingest: en-passant files
 };
 
 static void env_free(gc_env* e) {
-    void* ps[] = {e->bb, e->meta, e->d.htab, e->d.hgen, e->d.draw, e->d.act,
+    void* ps[] = {e->ep, e->bb, e->meta, e->d.htab, e->d.hgen, e->d.draw, e->d.act,
                   e->d.reward, e->d.done, e->d.reason, e->d.nsteps, e->mbox, e->m8, e->mask, e->list, e->counts,
                   e->lmask, e->stats};
     for (void* p : ps) if (p) (void)hipFree(p);
@@ -1091,12 +1120,14 @@ static void env_free(gc_env* e) {
 // kernel dispatch on the env's opponent mode (a kernel-argument-uniform choice made once per
 // launch on the host, so the opponent="none" kernels carry no opponent code)
 static void launch_reset(gc_env* e, const uint8_t* mask, int select) {
-    if (e->d.opp) k_env_reset<true><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d, mask, select);
+    if (e->rules) k_fenv_reset<<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d, mask, select);
+    else if (e->d.opp) k_env_reset<true><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d, mask, select);
     else k_env_reset<false><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d, mask, select);
 }
 template <bool POLICY>
 static void launch_step(gc_env* e) {
-    if (e->d.opp) k_env_step<POLICY, true><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d);
+    if (e->rules) k_fenv_step<POLICY><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d);
+    else if (e->d.opp) k_env_step<POLICY, true><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d);
     else k_env_step<POLICY, false><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d);
 }
 
@@ -1175,11 +1206,29 @@ extern "C" int gc_env_set_opponent(gc_env* e, int opponent, int agent_white) {
     if (!e) return fail("null env");
     if (opponent != 0 && opponent != 1) return fail("opponent must be 0 (none) or 1 (random)");
     if (!agent_white && !opponent) return fail("player_color BLACK needs an opponent (chess_v2.py:208-212)");
+    if (opponent && e->rules) return fail("the FIDE rules mode supports opponent \"none\" only");
     HIPCHK(hipSetDevice(e->device));
     HIPCHK(hipStreamSynchronize(e->stream));
     e->d.opp = opponent;
     e->d.agent_black = agent_white ? 0 : 1;
     HIPCHK(hipMemsetAsync(e->d.draw, 0, (size_t)4 * e->n, e->stream));  // fresh policy streams
+    launch_reset(e, nullptr, 1);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(e->stream));
+    e->policy_ready = true;
+    return 0;
+}
+
+// rules 0: the reference's (default); 1: FIDE (gc_fide.h; opponent "none" only).  Resets
+// every board and restarts the policy streams.
+extern "C" int gc_env_set_rules(gc_env* e, int rules) {
+    if (!e) return fail("null env");
+    if (rules != 0 && rules != 1) return fail("rules must be 0 (reference) or 1 (fide)");
+    if (rules && e->d.opp) return fail("the FIDE rules mode supports opponent \"none\" only");
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    e->rules = rules;
+    HIPCHK(hipMemsetAsync(e->d.draw, 0, (size_t)4 * e->n, e->stream));
     launch_reset(e, nullptr, 1);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(e->stream));
@@ -1233,7 +1282,7 @@ extern "C" int gc_env_step_random(gc_env* e, int n_plies) {
     HIPCHK(hipSetDevice(e->device));
     static const bool one_wave = getenv("GC_STEP1") != nullptr;  // A/B switch to k_env_step<true, false>
     for (int p = 0; p < n_plies; p++) {
-        if (!e->d.opp && !one_wave)
+        if (!e->d.opp && !e->rules && !one_wave)
             k_env_step2<<<(e->n + PAIR_BOARDS - 1) / PAIR_BOARDS, 2 * PAIR_BOARDS, 0, e->stream>>>(e->d);
         else
             launch_step<true>(e);
@@ -1245,7 +1294,8 @@ extern "C" int gc_env_step_random(gc_env* e, int n_plies) {
 extern "C" int gc_env_select_random(gc_env* e) {
     if (!e) return fail("null env");
     HIPCHK(hipSetDevice(e->device));
-    k_select<<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d);
+    if (e->rules) k_fenv_select<<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d);
+    else k_select<<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d);
     HIPCHK(hipGetLastError());
     e->policy_ready = true;
     return 0;
@@ -1255,6 +1305,7 @@ extern "C" int gc_env_rollout(gc_env* e, int n_plies, int16_t* tr_action, int16_
                               uint8_t* tr_reason, uint64_t* stats8) {
     if (!e) return fail("null env");
     if (n_plies < 0) return fail("n_plies must be >= 0");
+    if (e->rules) return fail("fused rollout: reference rules only (use gc_env_step_random under FIDE rules)");
     if (!e->policy_ready) return fail("policy actions stale: call gc_env_reset or gc_env_select_random first");
     HIPCHK(hipSetDevice(e->device));
     bool trace = tr_action || tr_reward || tr_done || tr_reason;
@@ -1317,7 +1368,8 @@ extern "C" int gc_env_set_states(gc_env* e, const int8_t* boards, const uint8_t*
     HIPCHK(hipSetDevice(e->device));
     HIPCHK(hipMemcpyAsync(e->mbox, boards, (size_t)64 * e->n, hipMemcpyHostToDevice, e->stream));
     HIPCHK(hipMemcpyAsync(e->m8, meta, (size_t)8 * e->n, hipMemcpyHostToDevice, e->stream));
-    k_env_import<<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->mbox, e->m8, e->d, 0);
+    if (e->rules) k_fenv_import<<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->mbox, e->m8, nullptr, e->d);
+    else k_env_import<<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->mbox, e->m8, e->d, 0);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(e->stream));
     e->policy_ready = false;
@@ -1333,6 +1385,12 @@ extern "C" int gc_env_set_states(gc_env* e, const int8_t* boards, const uint8_t*
 static const char* FEN_PIECES = ".KQRBNP";
 
 extern "C" int gc_fen_to_state(const char* fen, int8_t* board, uint8_t* meta) {
+    return gc_fen_to_state_rules(fen, board, meta, 0);
+}
+
+// rules 1 (FIDE): the en-passant field is parsed (it must be on the rank the side to move
+// captures onto) and meta8[7] = its file + 1 (0 = "-"), the engine's FIDE convention
+extern "C" int gc_fen_to_state_rules(const char* fen, int8_t* board, uint8_t* meta, int rules) {
     if (!fen || !board || !meta) return fail("null argument");
     int8_t b[64] = {0};
     const char* p = fen;
@@ -1372,22 +1430,31 @@ extern "C" int gc_fen_to_state(const char* fen, int8_t* board, uint8_t* meta) {
                 default: return fail(std::string("FEN: bad castling field in '") + fen + "'");
             }
         }
-        // en passant, half-move clock: ignored; full-move number -> move_count
+        // reference rules: en passant and half-move clock ignored, full-move number ->
+        // move_count; FIDE: en passant -> meta8[7]
         int field = 0;
         long full = 1;
+        int epf = -1;
         while (*p) {
             while (*p == ' ') p++;
             if (!*p) break;
             const char* st = p;
             while (*p && *p != ' ') p++;
-            if (++field == 3) {
+            ++field;
+            if (field == 1 && rules && !(p - st == 1 && *st == '-')) {
+                int want = m[0] ? '6' : '3';
+                if (p - st != 2 || st[0] < 'a' || st[0] > 'h' || st[1] != want)
+                    return fail(std::string("FEN: bad en-passant field in '") + fen + "'");
+                epf = st[0] - 'a';
+            }
+            if (field == 3) {
                 char* end = nullptr;
                 full = strtol(st, &end, 10);
                 if (end != p || full < 1) return fail(std::string("FEN: bad full-move number in '") + fen + "'");
             }
         }
         long mc = full - 1;
-        m[7] = (uint8_t)(mc > 255 ? 255 : mc);
+        m[7] = rules ? (uint8_t)(epf + 1) : (uint8_t)(mc > 255 ? 255 : mc);
     }
     memcpy(board, b, 64);
     memcpy(meta, m, 8);
@@ -1395,6 +1462,10 @@ extern "C" int gc_fen_to_state(const char* fen, int8_t* board, uint8_t* meta) {
 }
 
 extern "C" int gc_state_to_fen(const int8_t* board, const uint8_t* meta, char* out, int cap) {
+    return gc_state_to_fen_rules(board, meta, out, cap, 0);
+}
+
+extern "C" int gc_state_to_fen_rules(const int8_t* board, const uint8_t* meta, char* out, int cap, int rules) {
     if (!board || !meta || !out) return fail("null argument");
     if (check_boards(1, board)) return -1;
     std::string f;
@@ -1417,7 +1488,14 @@ extern "C" int gc_state_to_fen(const int8_t* board, const uint8_t* meta, char* o
     if (meta[3]) cs += 'k';
     if (meta[4]) cs += 'q';
     f += cs.empty() ? "-" : cs;
-    f += " - 0 " + std::to_string((int)meta[7] + 1);
+    if (rules) {
+        f += " ";
+        if (meta[7]) { f += (char)('a' + ((meta[7] - 1) & 7)); f += meta[0] ? '6' : '3'; }
+        else f += "-";
+        f += " 0 1";
+    } else {
+        f += " - 0 " + std::to_string((int)meta[7] + 1);
+    }
     if ((int)f.size() + 1 > cap) return fail("FEN output buffer too small");
     memcpy(out, f.c_str(), f.size() + 1);
     return 0;
@@ -1427,15 +1505,27 @@ extern "C" int gc_state_to_fen(const int8_t* board, const uint8_t* meta, char* o
 // repetition windows cleared (like gc_env_set_states)
 extern "C" int gc_env_set_fens(gc_env* e, const char* const* fens) {
     if (!e || !fens) return fail("null argument");
-    std::vector<int8_t> b((size_t)64 * e->n);
+    std::vector<int8_t> b((size_t)64 * e->n), ep(e->n, -1);
     std::vector<uint8_t> m((size_t)8 * e->n);
-    for (int i = 0; i < e->n; i++)
-        if (gc_fen_to_state(fens[i], b.data() + 64 * (size_t)i, m.data() + 8 * (size_t)i))
+    for (int i = 0; i < e->n; i++) {
+        uint8_t* mi = m.data() + 8 * (size_t)i;
+        if (gc_fen_to_state_rules(fens[i], b.data() + 64 * (size_t)i, mi, e->rules))
             return fail("board " + std::to_string(i) + ": " + g_err);
+        if (e->rules) {  // meta8[7] carried the en-passant file: the env keeps move_count 0
+            ep[i] = (int8_t)(mi[7] ? mi[7] - 1 : -1);
+            mi[7] = 0;
+        }
+    }
     HIPCHK(hipSetDevice(e->device));
     HIPCHK(hipMemcpyAsync(e->mbox, b.data(), b.size(), hipMemcpyHostToDevice, e->stream));
     HIPCHK(hipMemcpyAsync(e->m8, m.data(), m.size(), hipMemcpyHostToDevice, e->stream));
-    k_env_import<<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->mbox, e->m8, e->d, 1);
+    if (e->rules) {
+        if (!e->ep && dalloc(&e->ep, e->n)) return -1;
+        HIPCHK(hipMemcpyAsync(e->ep, ep.data(), e->n, hipMemcpyHostToDevice, e->stream));
+        k_fenv_import<<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->mbox, e->m8, e->ep, e->d);
+    } else {
+        k_env_import<<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->mbox, e->m8, e->d, 1);
+    }
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(e->stream));
     e->policy_ready = false;
@@ -1453,7 +1543,8 @@ extern "C" int gc_env_legal_moves(gc_env* e, uint16_t* moves, int cap, int32_t* 
         if (dalloc(&e->list, (size_t)cap * e->n)) return -1;
         e->list_cap = cap;
     }
-    k_list<<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d.st, 0, cap, e->list, e->counts);
+    if (e->rules) k_flist<<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d.st, 0, cap, e->list, e->counts);
+    else k_list<<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d.st, 0, cap, e->list, e->counts);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(moves, e->list, (size_t)2 * cap * e->n, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipMemcpyAsync(counts, e->counts, (size_t)4 * e->n, hipMemcpyDeviceToHost, e->stream));
@@ -1465,7 +1556,8 @@ extern "C" int gc_env_legal_mask(gc_env* e, uint64_t* mask, int32_t* counts) {
     if (!e || !mask) return fail("null argument");
     HIPCHK(hipSetDevice(e->device));
     if (!e->lmask && dalloc(&e->lmask, (size_t)65 * e->n)) return -1;
-    k_mask<<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d.st, e->lmask, e->counts);
+    if (e->rules) k_fmask<<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d.st, e->lmask, e->counts);
+    else k_mask<<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d.st, e->lmask, e->counts);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(mask, e->lmask, (size_t)8 * 65 * e->n, hipMemcpyDeviceToHost, e->stream));
     if (counts) HIPCHK(hipMemcpyAsync(counts, e->counts, (size_t)4 * e->n, hipMemcpyDeviceToHost, e->stream));

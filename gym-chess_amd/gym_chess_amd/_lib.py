@@ -25,12 +25,16 @@ SIGNATURES = {
     "gc_engine_next_state": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
     "gc_engine_update_state": (_I, [_P, _I, _P, _P, _P, _P]),
     "gc_engine_perft": (_I, [_P, _I, _P, _P, _I, _P]),
+    "gc_engine_set_rules": (_I, [_P, _I]),
     "gc_env_create": (_I, [_I, _I, _U64, _P, _P]),
     "gc_env_destroy": (_I, [_P]),
     "gc_env_set_opponent": (_I, [_P, _I, _I]),
     "gc_env_set_fens": (_I, [_P, _P]),
     "gc_fen_to_state": (_I, [ctypes.c_char_p, _P, _P]),
     "gc_state_to_fen": (_I, [_P, _P, _P, _I]),
+    "gc_fen_to_state_rules": (_I, [ctypes.c_char_p, _P, _P, _I]),
+    "gc_state_to_fen_rules": (_I, [_P, _P, _P, _I, _I]),
+    "gc_env_set_rules": (_I, [_P, _I]),
     "gc_env_num_boards": (_I, [_P]),
     "gc_env_reset": (_I, [_P, _P]),
     "gc_env_step": (_I, [_P, _P, _P, _P, _P]),
@@ -72,6 +76,16 @@ def load(path=LIB_PATH):
         fn.argtypes = args
     _lib = lib
     return lib
+
+
+RULES = {"reference": 0, "fide": 1}
+
+
+def rules_id(rules):
+    """'reference' (default: lib.rs's rules) or 'fide' (gc_fide.h) -> the C-ABI's rules code."""
+    if rules not in RULES:
+        raise ValueError(f"rules must be one of {sorted(RULES)}, got {rules!r}")
+    return RULES[rules]
 
 
 def check(rc):

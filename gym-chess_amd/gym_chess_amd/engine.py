@@ -19,14 +19,21 @@ MAX_LIST = 320  # > the largest legal move list of any position reachable by the
 
 
 class Engine:
-    """Batched stateless engine on one device.  States are (boards int8[n,64], meta uint8[n,8])."""
+    """Batched stateless engine on one device.  States are (boards int8[n,64], meta uint8[n,8]).
 
-    def __init__(self, device=0):
+    rules="fide" (not the reference's rules): en passant, promotion,
+    per-side castling, no king captures; meta[7] is then the en-passant file + 1 (0 = none),
+    lists are in ascending action id with castles last, perft counts the four promotions."""
+
+    def __init__(self, device=0, rules="reference"):
         self._L = _lib.load()
+        rid = _lib.rules_id(rules)
         h = ctypes.c_void_p()
         _lib.check(self._L.gc_engine_create(int(device), ctypes.byref(h)))
         self._h = h
         self.device = device
+        self.rules = rules
+        _lib.check(self._L.gc_engine_set_rules(self._h, rid))
 
     def close(self):
         if getattr(self, "_h", None):

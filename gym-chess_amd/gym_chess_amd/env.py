@@ -13,6 +13,9 @@ the reference env surface vectorised over boards:
 
 plus the device-resident random self-play driver of test_benchmark.py
 (`step_random`, `rollout`) used by bench.py.
+
+rules="fide" plays FIDE chess (gym-chess_amd/csrc/gc_fide.h) with the
+reference env's rewards and bookkeeping; an action promotes to a queen.
 """
 import ctypes
 
@@ -26,7 +29,8 @@ REASONS = {0: "none", 1: "mate", 2: "repetition", 3: "move_cap", 4: "no_moves", 
 
 
 class BatchedChessEnv:
-    def __init__(self, num_boards, device=0, seed=0, initial_board=None, opponent="none", player_color=C.WHITE):
+    def __init__(self, num_boards, device=0, seed=0, initial_board=None, opponent="none", player_color=C.WHITE,
+                 rules="reference"):
         self._L = _lib.load()
         self.num_boards = int(num_boards)
         self.device = int(device)
@@ -45,6 +49,9 @@ class BatchedChessEnv:
         self.player_color = player_color
         if opponent != "none" or player_color != C.WHITE:
             _lib.check(self._L.gc_env_set_opponent(self._h, int(opponent == "random"), int(player_color == C.WHITE)))
+        self.rules = rules
+        if _lib.rules_id(rules):  # FIDE (gc_fide.h): opponent "none", no fused rollout
+            _lib.check(self._L.gc_env_set_rules(self._h, _lib.rules_id(rules)))
 
     def close(self):
         if getattr(self, "_h", None):

@@ -62,6 +62,13 @@ int gc_engine_update_state(gc_engine* e, int n, const int8_t* boards, const uint
  * to move is meta[0]. depth in [0, 8]. */
 int gc_engine_perft(gc_engine* e, int n, const int8_t* boards, const uint8_t* meta, int depth,
                     uint64_t* nodes);
+/* Rules of every later call on this engine (not in the reference):
+ * 0 = the reference's (default, lib.rs), 1 = FIDE (gym-chess_amd/csrc/gc_fide.h: en passant,
+ * promotion, per-side castling through unattacked squares, no king captures).  Under FIDE
+ * rules meta[7] is the en-passant FILE + 1 (0 = none) on input and output; move lists hold
+ * each promotion once (as a queen promotion) in ascending action id, castles last; perft
+ * counts the four promotion pieces. */
+int gc_engine_set_rules(gc_engine* e, int rules);
 
 /* ---------------------------------------------------------------------------------
  * Batched env: N independent ChessEnvV2(opponent="none") boards resident on one device
@@ -113,6 +120,12 @@ int gc_env_synchronize(gc_env* e);
  * n - 1 (meta8[7]).  A bare placement field means WHITE to move, no rights, move_count 0. */
 int gc_fen_to_state(const char* fen, int8_t* board, uint8_t* meta);
 int gc_state_to_fen(const int8_t* board, const uint8_t* meta, char* out, int cap);
+/* rules 1 (FIDE): meta[7] = en-passant file + 1 (parsed / written) instead of move_count */
+int gc_fen_to_state_rules(const char* fen, int8_t* board, uint8_t* meta, int rules);
+int gc_state_to_fen_rules(const int8_t* board, const uint8_t* meta, char* out, int cap, int rules);
+/* Rules of the env (see gc_engine_set_rules); FIDE needs opponent "none" and has no fused
+ * rollout.  Resets every board. */
+int gc_env_set_rules(gc_env* e, int rules);
 /* set every board from a FEN (n strings); check flags from update_state (lib.rs:1386-1393);
  * repetition windows cleared */
 int gc_env_set_fens(gc_env* e, const char* const* fens);

@@ -313,3 +313,120 @@ extern "C" uint64_t host_perft_small(const int8_t* b, const uint8_t* m, int dept
     Pos s = import_state(b, m, -1);
     return perft_split(s, depth);
 }
+
+// ---- FIDE rules mode (gc_fide.h), engine convention meta8[7] = en-passant file + 1 --------
+#include "../../gym-chess_amd/csrc/gc_fide.h"
+
+static Pos fide_import(const int8_t* b, const uint8_t* m) {
+    u32 meta = (m[0] ? M_WHITE : 0u) | (m[1] ? M_WKC : 0u) | (m[2] ? M_WQC : 0u) | (m[3] ? M_BKC : 0u) |
+               (m[4] ? M_BQC : 0u);
+    meta = fide::with_ep(meta, m[7] ? (m[7] - 1) & 7 : -1);
+    return from_mailbox(b, meta);
+}
+
+static uint64_t fide_perft_rec(const Pos& s, int depth) {
+    if (depth <= 3) return fide::fperft_small(s, depth);
+    fide::FGen f;
+    fide::fgen(s, f);
+    uint64_t n = 0;
+    int rw;
+    bool irr;
+    u64 pcs = f.g.own;
+    while (pcs) {
+        int sq = ctz(pcs);
+        pcs &= pcs - 1;
+        int t = type_at(s, sq);
+        u64 tg = fide::ftargets(s, f, sq, t);
+        while (tg) {
+            int to = ctz(tg);
+            tg &= tg - 1;
+            int np = (t == PAWN && (bit(to) & fide::promo_row(f.g.white))) ? 4 : 1;
+            for (int pc = 0; pc < np; pc++) {
+                Pos c = s;
+                fide::fapply(c, sq * 64 + to, np == 4 ? QUEEN + pc : 0, &rw, &irr);
+                n += fide_perft_rec(c, depth - 1);
+            }
+        }
+    }
+    for (int cb = 0; cb < 2; cb++) {
+        if (!(f.g.castles & (1u << cb))) continue;
+        Pos c = s;
+        fide::fapply(c, cb ? (f.g.white ? A_KSW : A_KSB) : (f.g.white ? A_QSW : A_QSB), 0, &rw, &irr);
+        n += fide_perft_rec(c, depth - 1);
+    }
+    return n;
+}
+
+extern "C" uint64_t host_fide_perft(const int8_t* b, const uint8_t* m, int depth) {
+    return fide_perft_rec(fide_import(b, m), depth);
+}
+
+extern "C" int host_fide_list(const int8_t* b, const uint8_t* m, uint16_t* out, int cap) {
+    Pos s = fide_import(b, m);
+    fide::FGen f;
+    fide::fgen(s, f);
+    int n = 0;
+    u64 pcs = f.g.own;
+    while (pcs) {
+        int sq = ctz(pcs);
+        pcs &= pcs - 1;
+        u64 tg = fide::ftargets(s, f, sq, type_at(s, sq));
+        while (tg) {
+            int to = ctz(tg);
+            tg &= tg - 1;
+            if (n < cap) out[n] = (uint16_t)(sq * 64 + to);
+            n++;
+        }
+    }
+    if (f.g.castles & 1) { if (n < cap) out[n] = f.g.white ? A_QSW : A_QSB; n++; }
+    if (f.g.castles & 2) { if (n < cap) out[n] = f.g.white ? A_KSW : A_KSB; n++; }
+    return n;
+}
+
+// FIDE env trajectory (random self-play driver, as k_fenv_step<true>): per-ply action,
+// reward, done, reason
+extern "C" void host_fide_rollout(const int8_t* init, uint64_t seed, uint32_t board, int plies, int16_t* tr_action,
+                                  int16_t* tr_reward, uint8_t* tr_done, uint8_t* tr_reason) {
+    Pos ip = from_mailbox(init, 0);
+    auto reset = [&]() {
+        Pos s = ip;
+        s.meta = M_WHITE | M_RIGHTS;
+        s.meta |= fide::fcheck_flags(s);
+        return s;
+    };
+    HostHist h;
+    h.bump_gen();  // zeroed entries are of generation 0: dead
+    Pos s = reset();
+    u32 draw = 0;
+    auto pick = [&](const Pos& p) {
+        fide::FGen f;
+        fide::fgen(p, f);
+        int n = fide::fcount(p, f, false);
+        if (n == 0) return (int)A_NONE;
+        u32 k = policy_index(seed, board, draw++, (u32)n);
+        return fide::fselect(p, f, (int)k);
+    };
+    int a = pick(s);
+    for (int p = 0; p < plies; p++) {
+        StepOut o = {0, 0, R_NONE, 0};
+        int played = a;
+        if (a == A_NONE) {
+            s = reset();
+            h.bump_gen();
+            o.reason = R_NO_MOVES;
+            played = -1;
+        } else {
+            fide::FGen f;
+            o = fide::fenv_step<false>(s, h, a, f);
+            if (o.done) {
+                s = reset();
+                h.bump_gen();
+            }
+        }
+        a = pick(s);
+        tr_action[p] = (int16_t)played;
+        tr_reward[p] = (int16_t)o.reward;
+        tr_done[p] = (uint8_t)o.done;
+        tr_reason[p] = (uint8_t)o.reason;
+    }
+}

@@ -16,10 +16,10 @@ def lib():
     global _L
     if _L is None:
         src = os.path.join(_HERE, "core_host.cpp")
-        hdr = [os.path.join(_HERE, "..", "..", "gym-chess_amd", "csrc", h) for h in ("gc_core.h", "gc_env.h")]
+        hdr = [os.path.join(_HERE, "..", "..", "gym-chess_amd", "csrc", h) for h in ("gc_core.h", "gc_env.h", "gc_fide.h")]
         if not os.path.exists(_SO) or os.path.getmtime(_SO) < max(os.path.getmtime(p) for p in [src] + hdr):
             os.makedirs(os.path.dirname(_SO), exist_ok=True)
-            subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-o", _SO, src], check=True)
+            subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wno-unknown-pragmas", "-o", _SO, src], check=True)
         L = ctypes.CDLL(_SO)
         L.host_between.restype = ctypes.c_uint64
         L.host_rook_att.restype = ctypes.c_uint64
@@ -57,6 +57,10 @@ def lib():
         L.host_env_step.argtypes = [P, ctypes.c_int, P, P, P]
         L.host_env_state.argtypes = [P, P, P]
         L.host_env_moves.argtypes = [P, P, ctypes.c_int]
+        L.host_fide_perft.restype = ctypes.c_uint64
+        L.host_fide_perft.argtypes = [P, P, ctypes.c_int]
+        L.host_fide_list.argtypes = [P, P, P, ctypes.c_int]
+        L.host_fide_rollout.argtypes = [P, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, P, P, P, P]
         _L = L
     return _L
 
@@ -181,3 +185,26 @@ class HostEnv:
         out = np.zeros(1024, dtype=np.uint16)
         n = lib().host_env_moves(self.h, _p(out), 1024)
         return [int(x) for x in out[:n]]
+
+
+# ---- FIDE rules mode (gc_fide.h); meta[7] = en-passant file + 1 ---------------------------
+def fide_perft(board, meta, depth):
+    b, m = _bm(board, meta)
+    return int(lib().host_fide_perft(_p(b), _p(m), int(depth)))
+
+
+def fide_list(board, meta):
+    b, m = _bm(board, meta)
+    out = np.zeros(1024, dtype=np.uint16)
+    n = lib().host_fide_list(_p(b), _p(m), _p(out), 1024)
+    return [int(x) for x in out[:n]]
+
+
+def fide_rollout(seed, board_id, plies, init):
+    init = np.ascontiguousarray(init, dtype=np.int8).reshape(64)
+    a = np.zeros(plies, dtype=np.int16)
+    r = np.zeros(plies, dtype=np.int16)
+    d = np.zeros(plies, dtype=np.uint8)
+    q = np.zeros(plies, dtype=np.uint8)
+    lib().host_fide_rollout(_p(init), seed, board_id, plies, _p(a), _p(r), _p(d), _p(q))
+    return dict(action=a, reward=r, done=d, reason=q)

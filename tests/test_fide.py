@@ -1,0 +1,201 @@
+"""Optional FIDE rules mode -- OUTSIDE the reference-parity contract.
+
+The reference plays its own rules (gc_core.h); for rules="fide" there is no reference
+implementation, so the pin is the published perft totals: the standard positions of the
+chessprogramming.org "Perft Results" page (start position, Kiwipete, positions 3-6) and
+the en-passant / castling / promotion / stalemate edge positions in wide use for testing
+move generators.  CPU tests run the host build of gc_fide.h (tests/core_host); GPU tests
+run the same positions through the C-ABI (device level expansion + per-lane subtrees),
+plus the FIDE env against the host build of the same step function.
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "core_host"))
+import corehost as H  # noqa: E402  (test infrastructure: host build of gc_fide.h)
+
+# (FEN, {depth: published node count})
+STANDARD = [
+    ("rnbqkbnr/pppppppp/8/8/8/8/PPPPPPPP/RNBQKBNR w KQkq - 0 1",
+     {1: 20, 2: 400, 3: 8902, 4: 197281, 5: 4865609, 6: 119060324}),
+    ("r3k2r/p1ppqpb1/bn2pnp1/3PN3/1p2P3/2N2Q1p/PPPBBPPP/R3K2R w KQkq - 0 1",
+     {1: 48, 2: 2039, 3: 97862, 4: 4085603, 5: 193690690}),
+    ("8/2p5/3p4/KP5r/1R3p1k/8/4P1P1/8 w - - 0 1", {1: 14, 2: 191, 3: 2812, 4: 43238, 5: 674624, 6: 11030083}),
+    ("r3k2r/Pppp1ppp/1b3nbN/nP6/BBP1P3/q4N2/Pp1P2PP/R2Q1RK1 w kq - 0 1",
+     {1: 6, 2: 264, 3: 9467, 4: 422333, 5: 15833292}),
+    ("r2q1rk1/pP1p2pp/Q4n2/bbp1p3/Np6/1B3NBn/pPPP1PPP/R3K2R b KQ - 0 1", {1: 6, 2: 264, 3: 9467, 4: 422333}),
+    ("rnbq1k1r/pp1Pbppp/2p5/8/2B5/8/PPP1NnPP/RNBQK2R w KQ - 1 8", {1: 44, 2: 1486, 3: 62379, 4: 2103487, 5: 89941194}),
+    ("r4rk1/1pp1qppp/p1np1n2/2b1p1B1/2B1P1b1/P1NP1N2/1PP1QPPP/R4RK1 w - - 0 10",
+     {1: 46, 2: 2079, 3: 89890, 4: 3894594, 5: 164075551}),
+]
+EDGE = [  # (FEN, depth, nodes, what it exercises)
+    ("3k4/3p4/8/K1P4r/8/8/8/8 b - - 0 1", 6, 1134888, "illegal en passant (pin along the rank)"),
+    ("8/8/4k3/8/2p5/8/B2P2K1/8 w - - 0 1", 6, 1015133, "illegal en passant (diagonal pin)"),
+    ("8/8/1k6/2b5/2pP4/8/5K2/8 b - d3 0 1", 6, 1440467, "en passant capture gives check"),
+    ("5k2/8/8/8/8/8/8/4K2R w K - 0 1", 6, 661072, "short castling gives check"),
+    ("3k4/8/8/8/8/8/8/R3K3 w Q - 0 1", 6, 803711, "long castling gives check"),
+    ("r3k2r/1b4bq/8/8/8/8/7B/R3K2R w KQkq - 0 1", 4, 1274206, "castling rights"),
+    ("r3k2r/8/3Q4/8/8/5q2/8/R3K2R b KQkq - 0 1", 4, 1720476, "castling prevented"),
+    ("2K2r2/4P3/8/8/8/8/8/3k4 w - - 0 1", 6, 3821001, "promote out of check"),
+    ("8/8/1P2K3/8/2n5/1q6/8/5k2 b - - 0 1", 5, 1004658, "discovered check"),
+    ("4k3/1P6/8/8/8/8/K7/8 w - - 0 1", 6, 217342, "promote to give check"),
+    ("8/P1k5/K7/8/8/8/8/8 w - - 0 1", 6, 92683, "under-promote to give check"),
+    ("K1k5/8/P7/8/8/8/8/8 w - - 0 1", 6, 2217, "self stalemate"),
+    ("8/k1P5/8/1K6/8/8/8/8 w - - 0 1", 7, 567584, "stalemate and checkmate"),
+    ("8/8/2k5/5q2/5n2/8/5K2/8 b - - 0 1", 4, 23527, "stalemate and checkmate"),
+]
+CPU_NODE_LIMIT = 5_000_000  # the host build counts ~1e8 nodes/s; keep the CPU suite quick
+
+
+def fide_arrays(fen):
+    from gym_chess_amd.fen import fen_to_arrays
+
+    return fen_to_arrays(fen, rules="fide")
+
+
+def cases(limit=None):
+    out = []
+    for fen, dn in STANDARD:
+        for d, n in dn.items():
+            out.append((fen, d, n))
+    out += [(f, d, n) for f, d, n, _ in EDGE]
+    return [c for c in out if limit is None or c[2] <= limit]
+
+
+# ------------------------------------------------------------------ CPU (host build)
+@pytest.mark.parametrize("fen,depth,nodes", cases(CPU_NODE_LIMIT))
+def test_fide_perft_host(fen, depth, nodes):
+    b, m = fide_arrays(fen)
+    assert H.fide_perft(b, m, depth) == nodes
+
+
+def test_fide_fen_en_passant_field():
+    from gym_chess_amd import _lib
+    from gym_chess_amd.fen import arrays_to_fen, fen_to_arrays
+
+    b, m = fen_to_arrays("8/8/1k6/2b5/2pP4/8/5K2/8 b - d3 0 1", rules="fide")
+    assert m[0] == 0 and m[7] == 4  # file d + 1
+    assert arrays_to_fen(b, m, rules="fide") == "8/8/1k6/2b5/2pP4/8/5K2/8 b - d3 0 1"
+    b, m = fen_to_arrays("8/8/1k6/2b5/2pP4/8/5K2/8 b - d3 0 1")  # reference rules: ignored
+    assert m[7] == 0
+    for bad in ("8/8/8/8/8/8/8/8 w - d3 0 1", "8/8/8/8/8/8/8/8 b - d6 0 1", "8/8/8/8/8/8/8/8 w - z6 0 1"):
+        with pytest.raises(_lib.GymChessError):
+            fen_to_arrays(bad, rules="fide")
+    with pytest.raises(ValueError):
+        fen_to_arrays("8/8/8/8/8/8/8/8 w - - 0 1", rules="chess960")
+
+
+def test_fide_host_lists_are_legal_sets():
+    """Start position: 20 moves in ascending action id; Kiwipete has both castles listed
+    last (queen side, then king side) and no en passant without a target."""
+    b, m = fide_arrays(STANDARD[0][0])
+    lst = H.fide_list(b, m)
+    assert len(lst) == 20 and lst == sorted(lst)
+    b, m = fide_arrays(STANDARD[1][0])
+    lst = H.fide_list(b, m)
+    assert len(lst) == 48 and lst[-2:] == [4097, 4096]
+
+
+def test_fide_host_rollout_sane():
+    """Random self-play under FIDE rules on the host build: every reason is a normal one
+    (no invalid or both-kings-checked steps), mates happen, rewards are -10 + capture
+    (+10 promotion) (+100 mate)."""
+    from gym_chess_amd import codec as C
+
+    init = np.array(C.DEFAULT_BOARD, dtype=np.int8).reshape(64)
+    reasons = np.zeros(16, dtype=np.int64)
+    for bd in range(24):
+        tr = H.fide_rollout(0xF1DE, bd, 600, init)
+        reasons += np.bincount(tr["reason"], minlength=16)
+        played = tr["action"] >= 0
+        assert ((tr["reward"][played] >= -10) & (tr["reward"][played] <= 120)).all()
+    assert reasons[5] == 0 and reasons[6] == 0  # R_BOTH_CHECKED, R_INVALID never happen
+    assert reasons[1] > 0 and reasons[3] > 0  # some mates, some move caps
+
+
+# ------------------------------------------------------------------ GPU (C-ABI)
+@pytest.mark.gpu
+def test_fide_perft_gpu():
+    from gym_chess_amd.engine import Engine
+
+    eng = Engine(0, rules="fide")
+    by_depth = {}
+    for fen, d, n in cases(250_000_000):
+        by_depth.setdefault(d, []).append((fen, n))
+    for d, lst in sorted(by_depth.items()):
+        arr = [fide_arrays(f) for f, _ in lst]
+        b = np.stack([a[0] for a in arr])
+        m = np.stack([a[1] for a in arr])
+        got = eng.perft(b, m, d)
+        exp = np.array([n for _, n in lst], dtype=np.uint64)
+        assert (got == exp).all(), [(lst[k][0], d, int(got[k]), int(exp[k])) for k in np.nonzero(got != exp)[0]]
+
+
+@pytest.mark.gpu
+def test_fide_engine_lists_and_next_state_vs_host():
+    """Random walks from the standard positions: device move lists == the host build's at
+    every step (en passant carried in meta[7]), next_state applied on the device."""
+    from gym_chess_amd.engine import Engine
+
+    eng = Engine(0, rules="fide")
+    rng = np.random.RandomState(7)
+    for fen, _ in STANDARD:
+        b, m = fide_arrays(fen)
+        for ply in range(60):
+            moves, cnt = eng.possible_moves(b[None], m[None], bool(m[0]))
+            dev = [int(x) for x in moves[0, : cnt[0]]]
+            assert dev == H.fide_list(b, m), (fen, ply)
+            if not dev:
+                break
+            a = dev[rng.randint(len(dev))]
+            nb, nm, rw, st = eng.next_state(b[None], m[None], bool(m[0]), np.array([a], dtype=np.uint16))
+            assert int(st[0]) == 0
+            b, m = nb[0], nm[0]
+
+
+@pytest.mark.gpu
+def test_fide_env_step_random_vs_host():
+    """The FIDE env's device driver (k_fenv_step<true>) ply by ply == the host build of
+    fide::fenv_step with the same Philox policy stream."""
+    from gym_chess_amd import codec as C
+    from gym_chess_amd.env import BatchedChessEnv
+
+    n, plies, seed = 96, 400, 0xF1DE
+    env = BatchedChessEnv(n, device=0, seed=seed, rules="fide")
+    init = np.array(C.DEFAULT_BOARD, dtype=np.int8).reshape(64)
+    refs = [H.fide_rollout(seed, i, plies + 1, init) for i in range(n)]
+    ra = np.stack([r["action"] for r in refs], axis=1)
+    for p in range(plies):
+        env.step_random(1)
+        o = env.outputs()
+        assert (o["reward"] == np.stack([r["reward"][p] for r in refs])).all(), p
+        assert (o["done"] == np.stack([r["done"][p] for r in refs])).all(), p
+        assert (o["reason"] == np.stack([r["reason"][p] for r in refs])).all(), p
+        nxt = np.where(ra[p + 1] < 0, 0xFFFF, ra[p + 1]).astype(np.uint16)
+        assert (o["next_action"] == nxt).all(), p
+
+
+@pytest.mark.gpu
+def test_fide_env_external_steps_and_fens():
+    from gym_chess_amd.env import BatchedChessEnv
+
+    fens = [STANDARD[0][0], "8/8/1k6/2b5/2pP4/8/5K2/8 b - d3 0 1", STANDARD[1][0], "4k3/1P6/8/8/8/8/K7/8 w - - 0 1"]
+    env = BatchedChessEnv(4, device=0, seed=1, rules="fide")
+    env.set_fens(fens)
+    acts = env.possible_actions()
+    assert len(acts[0]) == 20 and len(acts[2]) == 48
+    assert 34 * 64 + 43 in acts[1]  # c4xd3 en passant (c4 = 34, d3 = 43)
+    assert 9 * 64 + 1 in acts[3]  # b7-b8 promotes (to a queen)
+    a = np.array([acts[0][0], 34 * 64 + 43, 4096, 9 * 64 + 1], dtype=np.uint16)
+    rw, dn, why = env.step(a)
+    b, m = env.boards()
+    assert b[1][35] == 0 and b[1][43] == -6 and rw[1] == -10 + 1  # the d4 pawn is gone
+    assert b[2][62] == 1 and b[2][61] == 3 and b[2][60] == 0 and b[2][63] == 0  # O-O
+    assert b[3][1] == 2 and rw[3] == -10 + 10  # promotion to a queen, +10
+    rw, dn, why = env.step(np.array([4100] * 4, dtype=np.uint16))
+    assert (rw == -10).all() and (why == 6).all()  # RESIGN is never a legal action
+    with pytest.raises(Exception):
+        env.rollout(10)  # no fused rollout under FIDE rules
