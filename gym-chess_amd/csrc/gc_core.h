@@ -66,6 +66,9 @@ GC_HD int popc(u64 x) { return __builtin_popcountll(x); }
 GC_HD int ctz(u64 x) { return __builtin_ctzll(x); }
 GC_HD int msb(u64 x) { return 63 - __builtin_clzll(x); }
 GC_HD u64 bit(int s) { return 1ull << s; }
+// squares below s (s < 64): shift-only, so no 64-bit subtract (a VCC carry chain, and on
+// gfx950 a wait state before the carry is consumed)
+GC_HD u64 below(int s) { return ~(~0ull << s); }
 
 GC_HD u64 rbit(u64 x) {
 #if defined(__clang__)
@@ -92,21 +95,33 @@ GC_HD u64 anti_mask(int sq) {  // row + col = s
     return s >= 7 ? ANTI << (8 * (s - 7)) : ANTI >> (8 * (7 - s));
 }
 
-// hyperbola quintessence on one line (mask includes the slider square)
-GC_HD u64 line_att(u64 occ, u64 mask, u64 s) {
-    u64 m = mask ^ s;
+// hyperbola quintessence on one line (mask includes the slider square).  The subtractions
+// o - s and rbit(o) - rbit(s) are written as additions of -s = ~0 << sq and
+// -rbit(s) = ~0 << (63 - sq): a 64-bit add is one instruction on gfx950 (v_lshl_add_u64),
+// a 64-bit subtract is a carry pair through VCC plus a hazard wait state.
+struct LineNeg {
+    u64 s, neg, negr;
+};
+GC_HD LineNeg line_neg(int sq) { return LineNeg{bit(sq), ~0ull << sq, ~0ull << (63 - sq)}; }
+GC_HD u64 line_att(u64 occ, u64 mask, const LineNeg& n) {
+    u64 m = mask ^ n.s;
     u64 o = occ & m;
-    u64 fwd = o - s;
-    u64 rev = rbit(o) - rbit(s);
+    u64 fwd = o + n.neg;
+    u64 rev = rbit(o) + n.negr;
     return (fwd ^ rbit(rev)) & m;
 }
 GC_HD u64 rook_att(int sq, u64 occ) {
-    u64 s = bit(sq);
-    return line_att(occ, file_mask(sq), s) | line_att(occ, row_mask(sq), s);
+    LineNeg n = line_neg(sq);
+    return line_att(occ, file_mask(sq), n) | line_att(occ, row_mask(sq), n);
 }
 GC_HD u64 bishop_att(int sq, u64 occ) {
-    u64 s = bit(sq);
-    return line_att(occ, diag_mask(sq), s) | line_att(occ, anti_mask(sq), s);
+    LineNeg n = line_neg(sq);
+    return line_att(occ, diag_mask(sq), n) | line_att(occ, anti_mask(sq), n);
+}
+GC_HD u64 queen_att(int sq, u64 occ) {
+    LineNeg n = line_neg(sq);
+    return line_att(occ, file_mask(sq), n) | line_att(occ, row_mask(sq), n) | line_att(occ, diag_mask(sq), n) |
+           line_att(occ, anti_mask(sq), n);
 }
 
 // leapers (set-wise; wrap masks per direction)
@@ -318,7 +333,7 @@ GC_HD void gen_pins(const Pos& s, Gen& g) {
     u64 snipers = (rook_att(ks, opp) & rq) | (bishop_att(ks, opp) & bq);
     while (snipers) {
         int sq = ctz(snipers);
-        snipers &= snipers - 1;
+        snipers ^= bit(sq);
         u64 seg = between(ks, sq);
         u64 bw = seg & g.occ;
         bool pin = bw && !(bw & (bw - 1)) && (bw & g.own);
@@ -355,7 +370,7 @@ GC_HD void gen_init(const Pos& s, Gen& g) {
 GC_HD u64 pseudo_targets(const Pos& s, const Gen& g, int sq, int t) {
     u64 notown = ~g.own;
     switch (t) {
-        case QUEEN: return (rook_att(sq, g.occ) | bishop_att(sq, g.occ)) & notown;
+        case QUEEN: return queen_att(sq, g.occ) & notown;
         case ROOK: return rook_att(sq, g.occ) & notown;
         case BISHOP: return bishop_att(sq, g.occ) & notown;
         case KNIGHT: return knight_set(bit(sq)) & notown;
@@ -418,7 +433,7 @@ GC_HD int kth_bit_asc(u64 x, int k) {
 }
 GC_HD int ray_pick(u64 tg, int sq, u64 fm, u64 rm, u64 dm, u64 am, bool rook, bool bish, int& k) {
     // outward from sq: rays toward lower indices are walked high->low ("desc")
-    u64 below = bit(sq) - 1, above = ~below & ~bit(sq);
+    u64 below = gc::below(sq), above = ~below & ~bit(sq);
 #define GC_RAY(G, DESC)                                                      \
     {                                                                        \
         u64 gg = (G);                                                        \
@@ -475,7 +490,7 @@ GC_HD int count_legal(const Pos& s, const Gen& g) {
     u64 pcs = g.own;
     while (pcs) {
         int sq = ctz(pcs);
-        pcs &= pcs - 1;
+        pcs ^= bit(sq);
         n += popc(legal_targets(s, g, sq, type_at(s, sq)));
     }
     return n + popc(g.castles);
@@ -486,7 +501,7 @@ GC_HD int select_legal(const Pos& s, const Gen& g, int k) {
     u64 pcs = g.own;
     while (pcs) {
         int sq = ctz(pcs);
-        pcs &= pcs - 1;
+        pcs ^= bit(sq);
         int t = type_at(s, sq);
         u64 tg = legal_targets(s, g, sq, t);
         int c = popc(tg);
@@ -524,7 +539,7 @@ struct NoScratch {  // count-only callers (perft leaves): no parking, no count p
     GC_HDM u64 get(int) const { return 0; }
 };
 
-GC_HD int ordinal(u64 own, int sq) { return popc(own & (bit(sq) - 1)); }
+GC_HD int ordinal(u64 own, int sq) { return popc(own & below(sq)); }
 
 template <class S>
 GC_HD void park(MoveSet& ms, S& scr, u64 own, int sq, u64 tg, int& total) {
@@ -532,9 +547,8 @@ GC_HD void park(MoveSet& ms, S& scr, u64 own, int sq, u64 tg, int& total) {
     total += c;
     if (S::kPark) {
         scr.put(ordinal(own, sq), tg);
-        u64 m = bit(sq);
 #pragma unroll
-        for (int b = 0; b < 5; b++) ms.cnt[b] |= ((c >> b) & 1) ? m : 0ull;
+        for (int b = 0; b < 5; b++) ms.cnt[b] |= (u64)((c >> b) & 1) << sq;  // no VCC select
     }
 }
 
@@ -577,19 +591,19 @@ GC_HD int gen_moves_a(const Pos& s, const Gen& g, MoveSet& ms, S& scr) {
     u64 pp = P & g.pinned;  // pinned pawns: rare, per piece
     while (pp) {
         int sq = ctz(pp);
-        pp &= pp - 1;
+        pp ^= bit(sq);
         park(ms, scr, own, sq, legal_targets(s, g, sq, PAWN), total);
     }
     u64 x = s.n & own;  // a pinned knight never has a move on its pin segment
     while (x) {
         int sq = ctz(x);
-        x &= x - 1;
+        x ^= bit(sq);
         park(ms, scr, own, sq, ((g.pinned >> sq) & 1) ? 0 : knight_set(bit(sq)) & notown_cm, total);
     }
     x = s.k & own;  // every own king; filtered by the pre-move enemy map only (lib.rs:613-619)
     while (x) {
         int sq = ctz(x);
-        x &= x - 1;
+        x ^= bit(sq);
         park(ms, scr, own, sq, king_set(bit(sq)) & ~own & ~g.enemy_att, total);
     }
     return total;
@@ -603,7 +617,7 @@ GC_HD int gen_moves_b(const Pos& s, const Gen& g, MoveSet& ms, S& scr) {
     u64 x = s.b & own;
     while (x) {
         int sq = ctz(x);
-        x &= x - 1;
+        x ^= bit(sq);
         u64 tg = bishop_att(sq, g.occ) & notown_cm;
         if ((g.pinned >> sq) & 1) tg &= g.pinrays & line_through(g.ks, sq);
         park(ms, scr, own, sq, tg, total);
@@ -611,7 +625,7 @@ GC_HD int gen_moves_b(const Pos& s, const Gen& g, MoveSet& ms, S& scr) {
     x = s.r & own;
     while (x) {
         int sq = ctz(x);
-        x &= x - 1;
+        x ^= bit(sq);
         u64 tg = rook_att(sq, g.occ) & notown_cm;
         if ((g.pinned >> sq) & 1) tg &= g.pinrays & line_through(g.ks, sq);
         park(ms, scr, own, sq, tg, total);
@@ -619,8 +633,8 @@ GC_HD int gen_moves_b(const Pos& s, const Gen& g, MoveSet& ms, S& scr) {
     x = s.q & own;
     while (x) {
         int sq = ctz(x);
-        x &= x - 1;
-        u64 tg = (rook_att(sq, g.occ) | bishop_att(sq, g.occ)) & notown_cm;
+        x ^= bit(sq);
+        u64 tg = queen_att(sq, g.occ) & notown_cm;
         if ((g.pinned >> sq) & 1) tg &= g.pinrays & line_through(g.ks, sq);
         park(ms, scr, own, sq, tg, total);
     }
@@ -685,7 +699,7 @@ GC_HD int select_action(const Pos& s, const Gen& g, const MoveSet& ms, const S& 
         u64 pcs = g.own;
         while (pcs) {
             int sq = ctz(pcs);
-            pcs &= pcs - 1;
+            pcs ^= bit(sq);
             u64 tg = legal_targets(s, g, sq, type_at(s, sq));
             int c = popc(tg);
             if (k < c) return sq * 64 + kth_set_bit(tg, k);
@@ -696,8 +710,8 @@ GC_HD int select_action(const Pos& s, const Gen& g, const MoveSet& ms, const S& 
     int lo = 0;  // largest square whose prefix count (squares below it) is <= k
 #pragma unroll
     for (int step = 32; step; step >>= 1)
-        if (prefix_count(ms.cnt, bit(lo + step) - 1) <= k) lo += step;
-    k -= prefix_count(ms.cnt, bit(lo) - 1);
+        if (prefix_count(ms.cnt, below(lo + step)) <= k) lo += step;
+    k -= prefix_count(ms.cnt, below(lo));
     u64 parked = scr.get(ordinal(g.own, lo));  // both candidates, then a select (no branch)
     u64 tg = ((ms.fastp >> lo) & 1) ? fast_pawn_targets(ms, lo, g.white) : parked;
     return lo * 64 + kth_set_bit(tg, k);

@@ -85,17 +85,23 @@ struct SoA {
 };
 
 // repetition window of board i (gc_env.h rep_prefetch / rep_commit): HTAB 64-byte entries
-// per board at htab[(i*HTAB + pos)*8 ..], one cache line each (4 x 16-B loads); generation [N]
+// per board (entry() below), one cache line each (4 x 16-B loads); generation [N]
 struct DevHist {
     u64* htab;
     u32* hgen;
     u32 g;
     int i;
+    // Wave-blocked layout: entry pos of board i at ((i/64)*HTAB + pos)*64 + i%64, i.e. the 64
+    // boards of a wave share one 4 MiB block and a wave's 64 probes land on 64 random 4 KiB
+    // rows of it.  Board-major tables (64 KiB per board) put a wave's probes 64 KiB apart, on
+    // the same HBM channels: tools/lat_probe.hip measures 9.6 vs 5.5 us per launch for one
+    // random 64-B read + write per board at 65 536 boards.
+    __device__ size_t entry(int pos) const { return ((size_t)(i >> 6) * HTAB + pos) * 64 + (i & 63); }
     __device__ u32 gen() const { return g; }
     __device__ void bump_gen() { g++; }                // written back by flush()
     __device__ void flush(u32 g0) const { if (g != g0) hgen[i] = g; }
     __device__ RepEntry load(int pos) const {
-        const ulonglong2* p = reinterpret_cast<const ulonglong2*>(htab + ((size_t)i * HTAB + pos) * 8);
+        const ulonglong2* p = reinterpret_cast<const ulonglong2*>(htab + entry(pos) * 8);
         ulonglong2 a = p[0], b = p[1], c = p[2], d = p[3];
         RepEntry e = {a.x, a.y, b.x, b.y, c.x, c.y, d.x, d.y};
         return e;
@@ -107,7 +113,7 @@ struct DevHist {
     __device__ void store_hdr(int pos, u64 h) { wkind = 1; wpos = pos; we.hdr = h; }
     __device__ void store(int pos, const RepEntry& e) { wkind = 2; wpos = pos; we = e; }
     __device__ void commit() {
-        u64* base = htab + ((size_t)i * HTAB + wpos) * 8;
+        u64* base = htab + entry(wpos) * 8;
         if (wkind == 1) {
             base[0] = we.hdr;
         } else if (wkind == 2) {
@@ -302,7 +308,7 @@ __global__ void k_sum_children(const int32_t* __restrict__ offs, const int32_t* 
 // ----------------------------------------------------------------------------- env kernels
 struct EnvDev {
     SoA st;
-    u64* htab;       // [N][HTAB][8] repetition tables (gc_env.h)
+    u64* htab;       // [N/64][HTAB][64][8] repetition tables (gc_env.h; DevHist::entry)
     u32* hgen;
     u32* draw;       // policy draws per board (Philox counter)
     uint16_t* act;   // next action per board (A_NONE = no legal move)
@@ -315,6 +321,9 @@ struct EnvDev {
     int n;
     int opp;          // 0: opponent "none"; 1: the random opponent replies inside step()
     int agent_black;  // player_color BLACK (needs opp): the opponent opens at every reset
+    const uint16_t* reset_acts;  // the start position's legal actions in action-id order
+                                 // (RESET_ACTS_MAX; valid when ic.table): a reset board's pick
+                                 // is one table read
     // Every reset lands on the same position: its state, move set and parked targets are
     // computed once at env creation (k_init_cache) and passed here by value.
     struct InitCache {
@@ -326,6 +335,7 @@ struct EnvDev {
         u32 castles;
         int white;
         int usable;  // 0: the start position needs the per-square fallback (> 16 pieces)
+        int table;   // reset_acts holds all `total` actions
     } ic;
     __device__ DevHist hist(int i, u32 g) const { return DevHist{htab, hgen, g, i}; }
 };
@@ -370,7 +380,8 @@ __device__ void moves_after_reset(const EnvDev& e, const Pos& s, Gen& g, MoveSet
     for (int j = 0; j < SCRATCH_SLOTS; j++) scr.put(j, e.ic.slots[j]);
 }
 
-__global__ void __launch_bounds__(BLOCK) k_init_cache(EnvDev e, EnvDev::InitCache* out) {
+#define RESET_ACTS_MAX 128
+__global__ void __launch_bounds__(BLOCK) k_init_cache(EnvDev e, EnvDev::InitCache* out, uint16_t* acts) {
     LDS_SCRATCH_DECL;
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     EnvDev::InitCache c = {};
@@ -386,6 +397,8 @@ __global__ void __launch_bounds__(BLOCK) k_init_cache(EnvDev e, EnvDev::InitCach
     c.castles = g.castles;
     c.white = g.white;
     c.usable = !ms.big;
+    c.table = c.usable && ms.total > 0 && ms.total <= RESET_ACTS_MAX;
+    for (int k = 0; c.table && k < ms.total; k++) acts[k] = (uint16_t)select_action(c.pos, g, ms, scr, k);
     *out = c;
 }
 
@@ -552,21 +565,36 @@ struct PairScratch {
 // is meant to stay in flight through phase 1.
 __device__ __forceinline__ void pair_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-__global__ void __launch_bounds__(2 * PAIR_BOARDS) k_env_step2(EnvDev e) {
+__global__ void __launch_bounds__(2 * PAIR_BOARDS) k_env_step2(EnvDev e, int blk0) {
     __shared__ PairLds L;
     const int role = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // wave-uniform
     const int l = threadIdx.x & (PAIR_BOARDS - 1);
-    const int i = blockIdx.x * PAIR_BOARDS + l;
+    const int blk = blockIdx.x + blk0;  // board block (a launch may cover a sub-range)
+    const int i = blk * PAIR_BOARDS + l;
     const bool live = i < e.n;
     const int ii = live ? i : e.n - 1;  // dead lanes read a valid board, store nothing
     PairScratch scr{&L.slots[0][l]};
     GC_STAMP(0);
 
-    // ---- phase 0: entry loads (one round trip), the action's preconditions, the move
-    Pos s = e.st.load(ii);
-    u32 ua = e.act[ii];
-    u32 g0 = 0, nst = 0, d = 0;
-    if (role) { g0 = e.hgen[ii]; nst = e.nsteps[ii]; } else { d = e.draw[ii]; }
+    // ---- phase 0: entry loads (one round trip), the action's preconditions, the move.
+    // Every kernel-argument pointer of the entry loads is fetched in ONE scalar batch (an
+    // opaque SGPR use here): left to the compiler, each pointer's s_load sinks to its first
+    // use and its wait splits the vector loads into dependent rounds.  Both waves load every
+    // input (no role branch: a branch that loads into a register on one side and zeroes it on
+    // the other makes the compiler drain every outstanding load before the zeroing).
+    const u64* bbp = e.st.bb;
+    const u32* mp = e.st.meta;
+    const uint16_t* ap = e.act;
+    const u32* hp = e.hgen;
+    const u32* np = e.nsteps;
+    const u32* dp = e.draw;
+    const int nn = e.st.n;
+    asm volatile("" ::"s"(bbp), "s"(mp), "s"(ap), "s"(hp), "s"(np), "s"(dp), "s"(nn));
+    Pos s;
+    s.k = bbp[ii]; s.q = bbp[(size_t)nn + ii]; s.r = bbp[2 * (size_t)nn + ii]; s.b = bbp[3 * (size_t)nn + ii];
+    s.n = bbp[4 * (size_t)nn + ii]; s.p = bbp[5 * (size_t)nn + ii]; s.w = bbp[6 * (size_t)nn + ii];
+    s.meta = mp[ii];
+    u32 ua = ap[ii], g0 = hp[ii], nst = np[ii], d = dp[ii];
     pin(s); pin(ua); pin(g0); pin(nst); pin(d);
     GC_STAMP(1);
     const int a = (int)ua;
@@ -588,7 +616,12 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS) k_env_step2(EnvDev e) {
     u32 x0 = 0;
 
     // ---- phase 1
+    uint16_t ra = (uint16_t)A_NONE;
     if (role == 0) {
+        x0 = philox_x0(e.seed, (u32)i, d);  // the next draw (independent of the position)
+        // a board that resets this step picks from the start position's table: issue that
+        // read now, it lands long before phase 3
+        if (e.ic.table) ra = e.reset_acts[scale_rank(x0, (u32)e.ic.total)];
         gen_pins(ns, g);
         L.pin3[0][l] = g.checkmask;
         L.pin3[1][l] = g.pinned;
@@ -628,7 +661,6 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS) k_env_step2(EnvDev e) {
     int c = 0;
     u32 hl = hl_of(s.meta);
     if (role == 0) {
-        x0 = philox_x0(e.seed, (u32)i, d);  // the next draw (independent of the position)
         if (gen) part = ms.big ? count_legal(ns, g) - popc(g.castles) : gen_moves_a(ns, g, ms, scr);
     } else {
         if (gen && !ms.big) part = gen_moves_b(ns, g, ms, scr);
@@ -687,31 +719,39 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS) k_env_step2(EnvDev e) {
         }
         if (o.done) have = false;
     }
-    if (!have) reset_board(e, s, h);  // also the no-move driver reset
     if (role == 0) {
-        if (!have) {
-            if (e.ic.usable) {
-                g.white = e.ic.white; g.own = e.ic.own; g.castles = e.ic.castles;
-                ms.fastp = e.ic.fastp; ms.o1 = e.ic.o1; ms.o2 = e.ic.o2; ms.ol = e.ic.ol; ms.orr = e.ic.orr;
-#pragma unroll
-                for (int b = 0; b < 5; b++) ms.cnt[b] = e.ic.cnt[b];
-                ms.total = e.ic.total;
-                ms.big = false;
-#pragma unroll
-                for (int j = 0; j < SCRATCH_SLOTS; j++) scr.put(j, e.ic.slots[j]);
-            } else {
-                gen_init(s, g);
-                gen_moves(s, g, ms, scr);
-            }
-        }
         uint16_t act = (uint16_t)A_NONE;
-        if (ms.total > 0) act = (uint16_t)select_action(s, g, ms, scr, (int)scale_rank(x0, (u32)ms.total));
+        int tot = ms.total;
+        if (!have && e.ic.table) {  // reset (also the no-move driver reset): the table
+            act = ra;
+            tot = e.ic.total;
+        } else {
+            if (!have) {
+                s = e.ic.pos;
+                if (e.ic.usable) {
+                    g.white = e.ic.white; g.own = e.ic.own; g.castles = e.ic.castles;
+                    ms.fastp = e.ic.fastp; ms.o1 = e.ic.o1; ms.o2 = e.ic.o2; ms.ol = e.ic.ol; ms.orr = e.ic.orr;
+#pragma unroll
+                    for (int b = 0; b < 5; b++) ms.cnt[b] = e.ic.cnt[b];
+                    ms.total = e.ic.total;
+                    ms.big = false;
+#pragma unroll
+                    for (int j = 0; j < SCRATCH_SLOTS; j++) scr.put(j, e.ic.slots[j]);
+                } else {
+                    gen_init(s, g);
+                    gen_moves(s, g, ms, scr);
+                }
+            }
+            tot = ms.total;
+            if (tot > 0) act = (uint16_t)select_action(s, g, ms, scr, (int)scale_rank(x0, (u32)tot));
+        }
         GC_STAMP(6);
         if (live) {
             e.act[i] = act;
-            e.draw[i] = d + (ms.total > 0 ? 1u : 0u);
+            e.draw[i] = d + (tot > 0 ? 1u : 0u);
         }
     } else {
+        if (!have) reset_board(e, s, h);  // also the no-move driver reset
         GC_STAMP(6);
         if (live) {
             h.commit();
@@ -726,7 +766,7 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS) k_env_step2(EnvDev e) {
     GC_STAMP(7);
 #ifdef GC_STAMPS
     if (g_stamp_out != nullptr && l == 0)
-        for (int q = 0; q < 8; q++) g_stamp_out[((size_t)blockIdx.x * 2 + role) * 8 + q] = gc_stamp_lds[role][q];
+        for (int q = 0; q < 8; q++) g_stamp_out[((size_t)blk * 2 + role) * 8 + q] = gc_stamp_lds[role][q];
 #endif
 }
 
@@ -1106,10 +1146,11 @@ struct gc_env {
     bool policy_ready = false;  // act[] holds policy picks for the current states
     int rules = 0;              // 0 reference, 1 FIDE (gc_fide.h)
     int8_t* ep = nullptr;       // FIDE ingest: en-passant files
+    uint16_t* reset_acts = nullptr;
 };
 
 static void env_free(gc_env* e) {
-    void* ps[] = {e->ep, e->bb, e->meta, e->d.htab, e->d.hgen, e->d.draw, e->d.act,
+    void* ps[] = {e->reset_acts, e->ep, e->bb, e->meta, e->d.htab, e->d.hgen, e->d.draw, e->d.act,
                   e->d.reward, e->d.done, e->d.reason, e->d.nsteps, e->mbox, e->m8, e->mask, e->list, e->counts,
                   e->lmask, e->stats};
     for (void* p : ps) if (p) (void)hipFree(p);
@@ -1148,11 +1189,12 @@ extern "C" int gc_env_create(int device, int n_boards, uint64_t seed, const int8
     e->n = n_boards;
     e->seed = seed;
     int n = n_boards;
+    size_t nb64 = ((size_t)n + 63) / 64 * 64;  // the window tables come in blocks of 64 boards
     hipError_t he = hipSetDevice(device);
     if (he == hipSuccess) he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
     if (he != hipSuccess) { env_free(e); delete e; return fail(std::string("stream: ") + hipGetErrorString(he)); }
     if (dalloc(&e->bb, (size_t)NBB * n) || dalloc(&e->meta, n) ||
-        dalloc(&e->d.htab, (size_t)HTAB * 8 * n) || dalloc(&e->d.hgen, n) ||
+        dalloc(&e->d.htab, (size_t)HTAB * 8 * nb64) || dalloc(&e->d.hgen, n) ||
         dalloc(&e->d.draw, n) || dalloc(&e->d.act, n) || dalloc(&e->d.reward, n) || dalloc(&e->d.done, n) ||
         dalloc(&e->d.reason, n) || dalloc(&e->d.nsteps, n) || dalloc(&e->mbox, (size_t)64 * n) ||
         dalloc(&e->m8, (size_t)8 * n) || dalloc(&e->mask, n) || dalloc(&e->counts, n) || dalloc(&e->stats, (size_t)8 * n)) {
@@ -1166,7 +1208,7 @@ extern "C" int gc_env_create(int device, int n_boards, uint64_t seed, const int8
     for (int j = 0; j < NBB; j++) e->d.init[j] = ibb[j];
     he = hipSuccess;
     if (he == hipSuccess) he = hipMemsetAsync(e->d.draw, 0, (size_t)4 * n, e->stream);
-    if (he == hipSuccess) he = hipMemsetAsync(e->d.htab, 0, (size_t)64 * HTAB * n, e->stream);
+    if (he == hipSuccess) he = hipMemsetAsync(e->d.htab, 0, (size_t)64 * HTAB * nb64, e->stream);
     if (he == hipSuccess) he = hipMemsetAsync(e->d.hgen, 0, (size_t)4 * n, e->stream);
     if (he == hipSuccess) he = hipMemsetAsync(e->d.nsteps, 0, (size_t)4 * n, e->stream);
     if (he == hipSuccess) he = hipMemsetAsync(e->d.reward, 0, (size_t)4 * n, e->stream);
@@ -1182,8 +1224,13 @@ extern "C" int gc_env_create(int device, int n_boards, uint64_t seed, const int8
     e->d.agent_black = 0;
     {  // the start position's move set, shared by every reset (EnvDev::ic)
         EnvDev::InitCache* dic = nullptr;
-        if (dalloc(&dic, 1)) { std::string m = g_err; env_free(e); delete e; return fail(m); }
-        k_init_cache<<<1, BLOCK, 0, e->stream>>>(e->d, dic);
+        uint16_t* dacts = nullptr;
+        if (dalloc(&dic, 1) || dalloc(&dacts, RESET_ACTS_MAX)) {
+            std::string m = g_err; (void)hipFree(dic); env_free(e); delete e; return fail(m);
+        }
+        e->reset_acts = dacts;
+        e->d.reset_acts = dacts;
+        k_init_cache<<<1, BLOCK, 0, e->stream>>>(e->d, dic, dacts);
         he = hipGetLastError();
         if (he == hipSuccess) he = hipMemcpyAsync(&e->d.ic, dic, sizeof(EnvDev::InitCache), hipMemcpyDeviceToHost, e->stream);
         if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
@@ -1281,9 +1328,10 @@ extern "C" int gc_env_step_random(gc_env* e, int n_plies) {
     if (!e->policy_ready) return fail("policy actions stale: call gc_env_reset or gc_env_select_random first");
     HIPCHK(hipSetDevice(e->device));
     static const bool one_wave = getenv("GC_STEP1") != nullptr;  // A/B switch to k_env_step<true, false>
+    const int nblk = (e->n + PAIR_BOARDS - 1) / PAIR_BOARDS;
     for (int p = 0; p < n_plies; p++) {
         if (!e->d.opp && !e->rules && !one_wave)
-            k_env_step2<<<(e->n + PAIR_BOARDS - 1) / PAIR_BOARDS, 2 * PAIR_BOARDS, 0, e->stream>>>(e->d);
+            k_env_step2<<<nblk, 2 * PAIR_BOARDS, 0, e->stream>>>(e->d, 0);
         else
             launch_step<true>(e);
         HIPCHK(hipGetLastError());
@@ -1617,7 +1665,7 @@ extern "C" int gc_debug_stamps(gc_env* e, int n_plies, uint64_t* out /* (n/64)*8
     HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_out), &d, sizeof(d)));
     for (int p = 0; p < n_plies; p++) {
         if (getenv("GC_STEP1")) k_env_step<true, false><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d);
-        else k_env_step2<<<(e->n + PAIR_BOARDS - 1) / PAIR_BOARDS, 2 * PAIR_BOARDS, 0, e->stream>>>(e->d);
+        else k_env_step2<<<(e->n + PAIR_BOARDS - 1) / PAIR_BOARDS, 2 * PAIR_BOARDS, 0, e->stream>>>(e->d, 0);
     }
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(out, d, cnt * 8, hipMemcpyDeviceToHost, e->stream));

@@ -5,4 +5,4 @@ timeout -k 10 120 python bench.py --perft-roots 0 --no-cpu-baseline --fused-plie
 python -c "
 import json
 d=json.loads(open('gpurun_out/b2.log').read().strip().splitlines()[-1]); print(d['value'], d['roofline']['avg_launch_us'])"
-timeout -k 10 60 python tools/stamp_fine.py
+timeout -k 10 60 python tools/stamp_probe2.py
