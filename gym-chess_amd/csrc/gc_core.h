@@ -707,11 +707,15 @@ GC_HD int select_action(const Pos& s, const Gen& g, const MoveSet& ms, const S& 
         }
         return A_NONE;
     }
-    int lo = 0;  // largest square whose prefix count (squares below it) is <= k
+    int lo = 0, pre = 0;  // largest square whose prefix count (squares below it) is <= k
 #pragma unroll
-    for (int step = 32; step; step >>= 1)
-        if (prefix_count(ms.cnt, below(lo + step)) <= k) lo += step;
-    k -= prefix_count(ms.cnt, below(lo));
+    for (int step = 32; step; step >>= 1) {
+        int p = prefix_count(ms.cnt, below(lo + step));
+        bool take = p <= k;
+        lo = take ? lo + step : lo;
+        pre = take ? p : pre;  // the prefix at lo rides along: no seventh count
+    }
+    k -= pre;
     u64 parked = scr.get(ordinal(g.own, lo));  // both candidates, then a select (no branch)
     u64 tg = ((ms.fastp >> lo) & 1) ? fast_pawn_targets(ms, lo, g.white) : parked;
     return lo * 64 + kth_set_bit(tg, k);

@@ -340,6 +340,22 @@ struct EnvDev {
     __device__ DevHist hist(int i, u32 g) const { return DevHist{htab, hgen, g, i}; }
 };
 
+// The env's per-board fields live in ONE allocation (the "slab"), at offsets that are a
+// function of n only, so a kernel needs a single base pointer for all of them:
+//   [0, 56n) bitboards K Q R B N P W (SoA) | meta u32 | hgen u32 | draw u32 | nsteps u32 |
+//   reward i32 | act u16 | done u8 | reason u8            = 80 B per board
+struct Slab {
+    static constexpr size_t BYTES_PER_BOARD = 80;
+    __host__ __device__ static size_t meta(size_t n) { return 56 * n; }
+    __host__ __device__ static size_t hgen(size_t n) { return 60 * n; }
+    __host__ __device__ static size_t draw(size_t n) { return 64 * n; }
+    __host__ __device__ static size_t nsteps(size_t n) { return 68 * n; }
+    __host__ __device__ static size_t reward(size_t n) { return 72 * n; }
+    __host__ __device__ static size_t act(size_t n) { return 76 * n; }
+    __host__ __device__ static size_t done(size_t n) { return 78 * n; }
+    __host__ __device__ static size_t reason(size_t n) { return 79 * n; }
+};
+
 // Keep a loaded value in a VGPR from here on.  The per-board inputs are all loaded at kernel
 // entry and pinned, so they cost ONE round trip; otherwise the compiler sinks each load to
 // its first use, and because vmcnt retires in order, the wait for such a late load also
@@ -553,6 +569,7 @@ struct PairLds {
     u64 planes[2][5][PAIR_BOARDS];          // partial bit-sliced counts per wave
     u32 part[2][PAIR_BOARDS];               // partial move totals per wave
     u32 rep[PAIR_BOARDS];                   // W1 -> W0: 3-fold count c | window length << 8
+    u32 act[PAIR_BOARDS];                   // W0 -> W1: the next action (fused rollout)
 };
 struct PairScratch {
     static constexpr bool kPark = true;
@@ -565,39 +582,26 @@ struct PairScratch {
 // is meant to stay in flight through phase 1.
 __device__ __forceinline__ void pair_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-__global__ void __launch_bounds__(2 * PAIR_BOARDS) k_env_step2(EnvDev e, int blk0) {
-    __shared__ PairLds L;
-    const int role = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // wave-uniform
-    const int l = threadIdx.x & (PAIR_BOARDS - 1);
-    const int blk = blockIdx.x + blk0;  // board block (a launch may cover a sub-range)
-    const int i = blk * PAIR_BOARDS + l;
-    const bool live = i < e.n;
-    const int ii = live ? i : e.n - 1;  // dead lanes read a valid board, store nothing
-    PairScratch scr{&L.slots[0][l]};
-    GC_STAMP(0);
+// Per-launch constants of the paired kernels (SGPRs).
+struct PairCtx {
+    uint64_t seed;
+    u64* htab;
+    u32* hgen;
+    const uint16_t* racts;  // the start position's actions (reset picks), valid when rtable
+    bool rtable;
+    u32 rtotal;
+};
 
-    // ---- phase 0: entry loads (one round trip), the action's preconditions, the move.
-    // Every kernel-argument pointer of the entry loads is fetched in ONE scalar batch (an
-    // opaque SGPR use here): left to the compiler, each pointer's s_load sinks to its first
-    // use and its wait splits the vector loads into dependent rounds.  Both waves load every
-    // input (no role branch: a branch that loads into a register on one side and zeroes it on
-    // the other makes the compiler drain every outstanding load before the zeroing).
-    const u64* bbp = e.st.bb;
-    const u32* mp = e.st.meta;
-    const uint16_t* ap = e.act;
-    const u32* hp = e.hgen;
-    const u32* np = e.nsteps;
-    const u32* dp = e.draw;
-    const int nn = e.st.n;
-    asm volatile("" ::"s"(bbp), "s"(mp), "s"(ap), "s"(hp), "s"(np), "s"(dp), "s"(nn));
-    Pos s;
-    s.k = bbp[ii]; s.q = bbp[(size_t)nn + ii]; s.r = bbp[2 * (size_t)nn + ii]; s.b = bbp[3 * (size_t)nn + ii];
-    s.n = bbp[4 * (size_t)nn + ii]; s.p = bbp[5 * (size_t)nn + ii]; s.w = bbp[6 * (size_t)nn + ii];
-    s.meta = mp[ii];
-    u32 ua = ap[ii], g0 = hp[ii], nst = np[ii], d = dp[ii];
-    pin(s); pin(ua); pin(g0); pin(nst); pin(d);
-    GC_STAMP(1);
-    const int a = (int)ua;
+// One ply of the paired driver for board i (lane l of this role's wave).  In/out: the state
+// s, the action a (picked for s by the previous ply or by the reset), the draw counter d
+// (W0), the window h (W1; its table write is left deferred in h), the step counter nst.
+// Returns the ply's env.step() outputs; on return both waves hold the same s, and with
+// SHARE_ACT the same next action a (W0 picks it; it crosses to W1 through LDS).
+template <bool SHARE_ACT>
+__device__ __forceinline__ StepOut pair_ply(PairLds& L, const EnvDev& e, const PairCtx& C, int role, int l, int i,
+                                            bool live, const Pos& rp, Pos& s, int& a, u32& d, DevHist& h,
+                                            u32& nst) {
+    PairScratch scr{&L.slots[0][l]};
     const bool none = a == A_NONE;                           // empty list: driver reset
     const bool done0 = (s.meta & M_DONE) != 0;               // chess_v2.py:245-251
     const bool cap = mc_of(s.meta) > MOVES_MAX;              // 252-258
@@ -610,7 +614,6 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS) k_env_step2(EnvDev e, int blk
     if (mv) apply_legal(ns, white, a, &mr, &irrev);
     Gen g;
     gen_base(ns, g);
-    DevHist h = e.hist(ii, g0);
     RepProbe pr;
     bool my_chk = false;
     u32 x0 = 0;
@@ -618,10 +621,10 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS) k_env_step2(EnvDev e, int blk
     // ---- phase 1
     uint16_t ra = (uint16_t)A_NONE;
     if (role == 0) {
-        x0 = philox_x0(e.seed, (u32)i, d);  // the next draw (independent of the position)
-        // a board that resets this step picks from the start position's table: issue that
+        x0 = philox_x0(C.seed, (u32)i, d);  // the next draw (independent of the position)
+        // a board that resets this ply picks from the start position's table: issue that
         // read now, it lands long before phase 3
-        if (e.ic.table) ra = e.reset_acts[scale_rank(x0, (u32)e.ic.total)];
+        if (C.rtable) ra = C.racts[scale_rank(x0, C.rtotal)];
         gen_pins(ns, g);
         L.pin3[0][l] = g.checkmask;
         L.pin3[1][l] = g.pinned;
@@ -680,14 +683,14 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS) k_env_step2(EnvDev e, int blk
     pair_barrier();
     GC_STAMP(5);
 
-    // ---- phase 3: outcome (both waves), then pick (W0) / stores (W1)
+    // ---- phase 3: outcome (both waves), then the pick (W0)
 #pragma unroll
     for (int b = 0; b < 5; b++) ms.cnt[b] |= L.planes[role ^ 1][b][l];
     ms.total = part + (int)L.part[role ^ 1][l] + popc(g.castles);
     if (role == 0) {
-        u32 rp = L.rep[l];
-        c = (int)(rp & 0xFFu);
-        hl = rp >> 8;
+        u32 rpk = L.rep[l];
+        c = (int)(rpk & 0xFFu);
+        hl = rpk >> 8;
     }
     StepOut o = {0, 0, R_NONE, 0};
     bool have = false;
@@ -719,15 +722,18 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS) k_env_step2(EnvDev e, int blk
         }
         if (o.done) have = false;
     }
+    if (!have) {  // reset (chess_v2.py:183-206), also the no-move driver reset
+        s = rp;
+        h.bump_gen();
+    }
     if (role == 0) {
         uint16_t act = (uint16_t)A_NONE;
         int tot = ms.total;
-        if (!have && e.ic.table) {  // reset (also the no-move driver reset): the table
+        if (!have && C.rtable) {  // the start position's table
             act = ra;
-            tot = e.ic.total;
+            tot = (int)C.rtotal;
         } else {
             if (!have) {
-                s = e.ic.pos;
                 if (e.ic.usable) {
                     g.white = e.ic.white; g.own = e.ic.own; g.castles = e.ic.castles;
                     ms.fastp = e.ic.fastp; ms.o1 = e.ic.o1; ms.o2 = e.ic.o2; ms.ol = e.ic.ol; ms.orr = e.ic.orr;
@@ -745,22 +751,103 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS) k_env_step2(EnvDev e, int blk
             tot = ms.total;
             if (tot > 0) act = (uint16_t)select_action(s, g, ms, scr, (int)scale_rank(x0, (u32)tot));
         }
-        GC_STAMP(6);
-        if (live) {
-            e.act[i] = act;
-            e.draw[i] = d + (tot > 0 ? 1u : 0u);
-        }
-    } else {
-        if (!have) reset_board(e, s, h);  // also the no-move driver reset
-        GC_STAMP(6);
-        if (live) {
+        a = act;
+        d += tot > 0 ? 1u : 0u;
+        if (SHARE_ACT) L.act[l] = act;
+    }
+    if (SHARE_ACT) {  // the next action to W1; LDS free for the next ply
+        pair_barrier();
+        if (role) a = (int)L.act[l];
+    }
+    return o;
+}
+
+// entry loads of the paired kernels (both waves load every input: a role branch that loads
+// into a register on one side and zeroes it on the other makes the compiler drain every
+// outstanding load before the zeroing)
+struct PairIO {
+    u64* bb; u32* meta; u32* hgen; u32* draw; u32* nsteps; int32_t* reward; uint16_t* act; uint8_t* done;
+    uint8_t* reason; int n;
+    __device__ PairIO(uint8_t* slab, int nn)
+        : bb(reinterpret_cast<u64*>(slab)), meta(reinterpret_cast<u32*>(slab + Slab::meta(nn))),
+          hgen(reinterpret_cast<u32*>(slab + Slab::hgen(nn))), draw(reinterpret_cast<u32*>(slab + Slab::draw(nn))),
+          nsteps(reinterpret_cast<u32*>(slab + Slab::nsteps(nn))),
+          reward(reinterpret_cast<int32_t*>(slab + Slab::reward(nn))),
+          act(reinterpret_cast<uint16_t*>(slab + Slab::act(nn))), done(slab + Slab::done(nn)),
+          reason(slab + Slab::reason(nn)), n(nn) {}
+    __device__ Pos load(int i) const {
+        size_t N = (size_t)n;
+        Pos s;
+        s.k = bb[i]; s.q = bb[N + i]; s.r = bb[2 * N + i]; s.b = bb[3 * N + i];
+        s.n = bb[4 * N + i]; s.p = bb[5 * N + i]; s.w = bb[6 * N + i];
+        s.meta = meta[i];
+        return s;
+    }
+    __device__ void store(int i, const Pos& s) const {
+        size_t N = (size_t)n;
+        bb[i] = s.k; bb[N + i] = s.q; bb[2 * N + i] = s.r; bb[3 * N + i] = s.b;
+        bb[4 * N + i] = s.n; bb[5 * N + i] = s.p; bb[6 * N + i] = s.w;
+        meta[i] = s.meta;
+    }
+};
+
+// The store pointers, re-derived at the end of the kernel from an opaque copy of n: left to
+// CSE, the entry pointers (18 SGPRs) would stay live through the whole ply and push the
+// compiler into SGPR spills.
+__device__ __forceinline__ PairIO store_io(uint8_t* slab, int nn) {
+    asm volatile("" : "+s"(nn));
+    return PairIO(slab, nn);
+}
+
+// Everything the step needs on its common path leads the argument list (11 dwords: the slab
+// base, n, the block offset, the seed, the window tables, the reset table and its size) so
+// that kernarg preloading (hipcc -mllvm -amdgpu-kernarg-preload-count=16) hands it over in
+// SGPRs at wave launch: a kernel-argument s_load costs a scalar-memory round trip at every
+// launch (the scalar cache starts cold), paid wherever the compiler sinks it.
+#define PAIR_PROLOGUE                                                                                       \
+    __shared__ PairLds L;                                                                                   \
+    const int role = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); /* wave-uniform */           \
+    const int l = threadIdx.x & (PAIR_BOARDS - 1);                                                          \
+    const int blk = blockIdx.x + blk0; /* board block (a launch may cover a sub-range) */                   \
+    const int i = blk * PAIR_BOARDS + l;                                                                    \
+    const bool live = i < nn;                                                                               \
+    const int ii = live ? i : nn - 1; /* dead lanes read a valid board, store nothing */                    \
+    const PairIO in_io(slab, nn);                                                                           \
+    const PairCtx C = {seed, htab, in_io.hgen, racts, (rinfo >> 16) != 0, rinfo & 0xFFFFu};                 \
+    GC_STAMP(0);                                                                                            \
+    Pos s = in_io.load(ii);                                                                                 \
+    u32 ua = in_io.act[ii], g0 = in_io.hgen[ii], nst = in_io.nsteps[ii], d = in_io.draw[ii];                \
+    /* the reset position (15 dwords, not preloaded): its s_load is waited for only after the */           \
+    /* board loads above have issued (an asm use is a scheduling barrier for memory operations: */         \
+    /* placed first, the kernarg round trip -- ~2k cycles, the scalar cache is cold at every launch -- */  \
+    /* delayed every global load); the opaque use keeps the compiler from re-loading it at the reset */    \
+    Pos rp = e.ic.pos;                                                                                      \
+    asm volatile("" : "+v"(rp.k), "+v"(rp.q), "+v"(rp.r), "+v"(rp.b), "+v"(rp.n), "+v"(rp.p), "+v"(rp.w),  \
+                 "+v"(rp.meta)); /* VGPRs: SGPRs are the scarce file here */                                  \
+    pin(s); pin(ua); pin(g0); pin(nst); pin(d);                                                             \
+    GC_STAMP(1);                                                                                            \
+    int a = (int)ua;                                                                                        \
+    DevHist h = DevHist{htab, in_io.hgen, g0, ii};
+
+__global__ void __launch_bounds__(2 * PAIR_BOARDS)
+    k_env_step2(uint8_t* __restrict__ slab, int nn, int blk0, uint64_t seed, u64* __restrict__ htab,
+                const uint16_t* __restrict__ racts, u32 rinfo /* ic.table << 16 | ic.total */, EnvDev e) {
+    PAIR_PROLOGUE
+    StepOut o = pair_ply<false>(L, e, C, role, l, i, live, rp, s, a, d, h, nst);
+    GC_STAMP(6);
+    const PairIO io = store_io(slab, nn);
+    if (live) {
+        if (role == 0) {
+            io.act[i] = (uint16_t)a;
+            io.draw[i] = d;
+        } else {
             h.commit();
-            e.st.store(i, s);
+            io.store(i, s);
             h.flush(g0);
-            e.nsteps[i] = nst;
-            e.reward[i] = o.reward;
-            e.done[i] = (uint8_t)o.done;
-            e.reason[i] = (uint8_t)o.reason;
+            io.nsteps[i] = nst;
+            io.reward[i] = o.reward;
+            io.done[i] = (uint8_t)o.done;
+            io.reason[i] = (uint8_t)o.reason;
         }
     }
     GC_STAMP(7);
@@ -768,6 +855,55 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS) k_env_step2(EnvDev e, int blk
     if (g_stamp_out != nullptr && l == 0)
         for (int q = 0; q < 8; q++) g_stamp_out[((size_t)blk * 2 + role) * 8 + q] = gc_stamp_lds[role][q];
 #endif
+}
+
+// Fused K-ply random self-play on the paired step: the state stays in registers; the last
+// ply's outputs and per-board stats (as k_env_rollout) are written at the end.
+__global__ void __launch_bounds__(2 * PAIR_BOARDS)
+    k_env_rollout2(uint8_t* __restrict__ slab, int nn, int blk0, uint64_t seed, u64* __restrict__ htab,
+                   const uint16_t* __restrict__ racts, u32 rinfo, int plies, uint64_t* __restrict__ stats, EnvDev e) {
+    PAIR_PROLOGUE
+    uint64_t steps = 0, rsum = 0;
+    u32 e_mate = 0, e_rep = 0, e_cap = 0, e_nomove = 0, e_err = 0;
+    StepOut o = {0, 0, R_NONE, 0};
+    for (int p = 0; p < plies; p++) {
+        int played = a;
+        o = pair_ply<true>(L, e, C, role, l, i, live, rp, s, a, d, h, nst);
+        if (played == A_NONE) {
+            e_nomove++;
+        } else {
+            steps++;
+            rsum += (uint64_t)(int64_t)o.reward;
+            if (o.done) {
+                e_mate += o.reason == R_MATE || o.reason == R_MATED;
+                e_rep += o.reason == R_REPETITION;
+                e_cap += o.reason == R_MOVE_CAP;
+                e_err += o.reason == R_BOTH_CHECKED || o.reason == R_WINDOW_FULL;
+                e_nomove += o.reason == R_OPP_NO_MOVE;
+            }
+        }
+        if (role) h.commit();  // this ply's window write lands before the next ply's probe
+    }
+    const PairIO io = store_io(slab, nn);
+    if (live) {
+        if (role == 0) {
+            io.act[i] = (uint16_t)a;
+            io.draw[i] = d;
+        } else {
+            io.store(i, s);
+            h.flush(g0);
+            io.nsteps[i] = nst;
+            io.reward[i] = o.reward;
+            io.done[i] = (uint8_t)o.done;
+            io.reason[i] = (uint8_t)o.reason;
+            if (stats) {
+                uint64_t* so = stats + 8 * (size_t)i;
+                so[0] += steps; so[1] += rsum;
+                so[2 + R_MATE] += e_mate; so[2 + R_REPETITION] += e_rep; so[2 + R_MOVE_CAP] += e_cap;
+                so[2 + R_NO_MOVES] += e_nomove; so[2 + R_BOTH_CHECKED] += e_err;
+            }
+        }
+    }
 }
 
 // Fused K-ply random self-play: state in registers for the whole launch.  Per-ply outputs
@@ -838,6 +974,21 @@ __global__ void __launch_bounds__(BLOCK) k_env_rollout(EnvDev e, int plies, int1
         so[0] += steps; so[1] += rsum;
         so[2 + R_MATE] += e_mate; so[2 + R_REPETITION] += e_rep; so[2 + R_MOVE_CAP] += e_cap;
         so[2 + R_NO_MOVES] += e_nomove; so[2 + R_BOTH_CHECKED] += e_err;
+    }
+}
+
+// Column sums of the per-board rollout stats [n][8] into out[8] (zeroed by the caller): a
+// wave-level butterfly per column, one atomic per column per wave.  Copying the 64 B/board
+// table to the host and summing there cost more than the rollout itself at 65 536 boards.
+__global__ void __launch_bounds__(BLOCK) k_sum_stats(const uint64_t* __restrict__ stats, int n,
+                                                     unsigned long long* __restrict__ out) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        unsigned long long v = i < n ? stats[8 * (size_t)i + k] : 0ull;
+#pragma unroll
+        for (int off = 32; off; off >>= 1) v += __shfl_xor(v, off, 64);
+        if ((threadIdx.x & 63) == 0 && v) atomicAdd(out + k, v);
     }
 }
 
@@ -1147,14 +1298,17 @@ struct gc_env {
     int rules = 0;              // 0 reference, 1 FIDE (gc_fide.h)
     int8_t* ep = nullptr;       // FIDE ingest: en-passant files
     uint16_t* reset_acts = nullptr;
+    uint8_t* slab = nullptr;  // per-board fields (Slab): bb, meta, hgen, draw, nsteps, reward, act, done, reason
+    hipGraphExec_t graph_exec = nullptr;  // GC_GRAPH: a captured chunk of step launches
+    int graph_chunk = 0;
 };
 
 static void env_free(gc_env* e) {
-    void* ps[] = {e->reset_acts, e->ep, e->bb, e->meta, e->d.htab, e->d.hgen, e->d.draw, e->d.act,
-                  e->d.reward, e->d.done, e->d.reason, e->d.nsteps, e->mbox, e->m8, e->mask, e->list, e->counts,
+    void* ps[] = {e->reset_acts, e->ep, e->slab, e->d.htab, e->mbox, e->m8, e->mask, e->list, e->counts,
                   e->lmask, e->stats};
     for (void* p : ps) if (p) (void)hipFree(p);
     for (auto& v : e->ev) if (v) (void)hipEventDestroy(v);
+    if (e->graph_exec) (void)hipGraphExecDestroy(e->graph_exec);
     if (e->stream) (void)hipStreamDestroy(e->stream);
 }
 
@@ -1170,6 +1324,13 @@ static void launch_step(gc_env* e) {
     if (e->rules) k_fenv_step<POLICY><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d);
     else if (e->d.opp) k_env_step<POLICY, true><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d);
     else k_env_step<POLICY, false><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d);
+}
+
+static void launch_step2(gc_env* e, hipStream_t st) {
+    const EnvDev& d = e->d;
+    u32 rinfo = (d.ic.table ? 1u << 16 : 0u) | (u32)(d.ic.total & 0xFFFF);
+    k_env_step2<<<(e->n + PAIR_BOARDS - 1) / PAIR_BOARDS, 2 * PAIR_BOARDS, 0, st>>>(
+        e->slab, d.n, 0, d.seed, d.htab, d.reset_acts, rinfo, d);
 }
 
 extern "C" int gc_env_create(int device, int n_boards, uint64_t seed, const int8_t* initial_board, gc_env** out) {
@@ -1193,14 +1354,25 @@ extern "C" int gc_env_create(int device, int n_boards, uint64_t seed, const int8
     hipError_t he = hipSetDevice(device);
     if (he == hipSuccess) he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
     if (he != hipSuccess) { env_free(e); delete e; return fail(std::string("stream: ") + hipGetErrorString(he)); }
-    if (dalloc(&e->bb, (size_t)NBB * n) || dalloc(&e->meta, n) ||
-        dalloc(&e->d.htab, (size_t)HTAB * 8 * nb64) || dalloc(&e->d.hgen, n) ||
-        dalloc(&e->d.draw, n) || dalloc(&e->d.act, n) || dalloc(&e->d.reward, n) || dalloc(&e->d.done, n) ||
-        dalloc(&e->d.reason, n) || dalloc(&e->d.nsteps, n) || dalloc(&e->mbox, (size_t)64 * n) ||
-        dalloc(&e->m8, (size_t)8 * n) || dalloc(&e->mask, n) || dalloc(&e->counts, n) || dalloc(&e->stats, (size_t)8 * n)) {
+    if (dalloc(&e->slab, Slab::BYTES_PER_BOARD * (size_t)n) ||
+        dalloc(&e->d.htab, (size_t)HTAB * 8 * nb64) || dalloc(&e->mbox, (size_t)64 * n) ||
+        dalloc(&e->m8, (size_t)8 * n) || dalloc(&e->mask, n) || dalloc(&e->counts, n) || dalloc(&e->stats, (size_t)8 * n + 8) /* [n][8] + the 8 sums */) {
         std::string m = g_err;
         env_free(e); delete e;
         return fail(m);
+    }
+    {
+        uint8_t* sl = e->slab;
+        size_t nz = (size_t)n;
+        e->bb = reinterpret_cast<u64*>(sl);
+        e->meta = reinterpret_cast<u32*>(sl + Slab::meta(nz));
+        e->d.hgen = reinterpret_cast<u32*>(sl + Slab::hgen(nz));
+        e->d.draw = reinterpret_cast<u32*>(sl + Slab::draw(nz));
+        e->d.nsteps = reinterpret_cast<u32*>(sl + Slab::nsteps(nz));
+        e->d.reward = reinterpret_cast<int32_t*>(sl + Slab::reward(nz));
+        e->d.act = reinterpret_cast<uint16_t*>(sl + Slab::act(nz));
+        e->d.done = sl + Slab::done(nz);
+        e->d.reason = sl + Slab::reason(nz);
     }
     // initial board bitboards (pure data conversion of the caller's input; no engine work)
     Pos ip = from_mailbox(ib, 0);
@@ -1328,10 +1500,27 @@ extern "C" int gc_env_step_random(gc_env* e, int n_plies) {
     if (!e->policy_ready) return fail("policy actions stale: call gc_env_reset or gc_env_select_random first");
     HIPCHK(hipSetDevice(e->device));
     static const bool one_wave = getenv("GC_STEP1") != nullptr;  // A/B switch to k_env_step<true, false>
-    const int nblk = (e->n + PAIR_BOARDS - 1) / PAIR_BOARDS;
-    for (int p = 0; p < n_plies; p++) {
-        if (!e->d.opp && !e->rules && !one_wave)
-            k_env_step2<<<nblk, 2 * PAIR_BOARDS, 0, e->stream>>>(e->d, 0);
+    static const int graph_chunk = getenv("GC_GRAPH") ? atoi(getenv("GC_GRAPH")) : 0;
+    const bool pair = !e->d.opp && !e->rules && !one_wave;
+    int p = 0;
+    if (pair && graph_chunk > 0) {
+        if (!e->graph_exec || e->graph_chunk != graph_chunk) {  // captured once per env
+            if (e->graph_exec) (void)hipGraphExecDestroy(e->graph_exec);
+            e->graph_exec = nullptr;
+            hipGraph_t g = nullptr;
+            HIPCHK(hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
+            for (int k = 0; k < graph_chunk; k++) launch_step2(e, e->stream);
+            HIPCHK(hipStreamEndCapture(e->stream, &g));
+            hipError_t ge = hipGraphInstantiate(&e->graph_exec, g, nullptr, nullptr, 0);
+            (void)hipGraphDestroy(g);
+            if (ge != hipSuccess) return fail(std::string("graph instantiate: ") + hipGetErrorString(ge));
+            e->graph_chunk = graph_chunk;
+        }
+        for (; p + graph_chunk <= n_plies; p += graph_chunk) HIPCHK(hipGraphLaunch(e->graph_exec, e->stream));
+    }
+    for (; p < n_plies; p++) {
+        if (pair)
+            launch_step2(e, e->stream);
         else
             launch_step<true>(e);
         HIPCHK(hipGetLastError());
@@ -1362,8 +1551,17 @@ extern "C" int gc_env_rollout(gc_env* e, int n_plies, int16_t* tr_action, int16_
     size_t cnt = (size_t)n_plies * e->n;
     if (trace && (dalloc(&da, cnt) || dalloc(&dr, cnt) || dalloc(&dd, cnt) || dalloc(&dq, cnt))) return -1;
     HIPCHK(hipMemsetAsync(e->stats, 0, (size_t)64 * e->n, e->stream));
-    if (e->d.opp) k_env_rollout<true><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d, n_plies, da, dr, dd, dq, e->stats);
-    else k_env_rollout<false><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d, n_plies, da, dr, dd, dq, e->stats);
+    static const bool one_wave = getenv("GC_STEP1") != nullptr;
+    if (e->d.opp) {
+        k_env_rollout<true><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d, n_plies, da, dr, dd, dq, e->stats);
+    } else if (!trace && !one_wave) {  // the paired kernel (per-ply traces: the one-wave kernel)
+        const EnvDev& d = e->d;
+        u32 rinfo = (d.ic.table ? 1u << 16 : 0u) | (u32)(d.ic.total & 0xFFFF);
+        k_env_rollout2<<<(e->n + PAIR_BOARDS - 1) / PAIR_BOARDS, 2 * PAIR_BOARDS, 0, e->stream>>>(
+            e->slab, d.n, 0, d.seed, d.htab, d.reset_acts, rinfo, n_plies, e->stats, d);
+    } else {
+        k_env_rollout<false><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d, n_plies, da, dr, dd, dq, e->stats);
+    }
     hipError_t le = hipGetLastError();
     if (le != hipSuccess) return fail(std::string("rollout launch: ") + hipGetErrorString(le));
     if (trace) {
@@ -1375,12 +1573,12 @@ extern "C" int gc_env_rollout(gc_env* e, int n_plies, int16_t* tr_action, int16_
         (void)hipFree(da); (void)hipFree(dr); (void)hipFree(dd); (void)hipFree(dq);
     }
     if (stats8) {
-        std::vector<uint64_t> st((size_t)8 * e->n);
-        HIPCHK(hipMemcpyAsync(st.data(), e->stats, st.size() * 8, hipMemcpyDeviceToHost, e->stream));
+        uint64_t* sums = e->stats + (size_t)8 * e->n;
+        HIPCHK(hipMemsetAsync(sums, 0, 64, e->stream));
+        k_sum_stats<<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->stats, e->n, reinterpret_cast<unsigned long long*>(sums));
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(stats8, sums, 64, hipMemcpyDeviceToHost, e->stream));
         HIPCHK(hipStreamSynchronize(e->stream));
-        for (int k = 0; k < 8; k++) stats8[k] = 0;
-        for (int i = 0; i < e->n; i++)
-            for (int k = 0; k < 8; k++) stats8[k] += st[(size_t)8 * i + k];
     }
     return 0;
 }
@@ -1665,7 +1863,7 @@ extern "C" int gc_debug_stamps(gc_env* e, int n_plies, uint64_t* out /* (n/64)*8
     HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_out), &d, sizeof(d)));
     for (int p = 0; p < n_plies; p++) {
         if (getenv("GC_STEP1")) k_env_step<true, false><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d);
-        else k_env_step2<<<(e->n + PAIR_BOARDS - 1) / PAIR_BOARDS, 2 * PAIR_BOARDS, 0, e->stream>>>(e->d, 0);
+        else launch_step2(e, e->stream);
     }
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(out, d, cnt * 8, hipMemcpyDeviceToHost, e->stream));

@@ -283,6 +283,23 @@ def test_step_random_per_ply_vs_oracle(oracle):
         assert (o["next_action"] == nxt).all(), (p, np.nonzero(o["next_action"] != nxt)[0][:4])
 
 
+def test_fused_rollout_stats_and_states_vs_oracle(oracle):
+    """The paired fused-rollout kernel (k_env_rollout2, no trace): per-board final states and
+    the aggregate episode stats of 200 boards x 500 plies == the oracle driver's."""
+    from gym_chess_amd.env import BatchedChessEnv
+
+    n, plies, seed = 200, 500, 31337
+    env = BatchedChessEnv(n, device=0, seed=seed)
+    st, _ = env.rollout(plies)
+    b, m = env.boards()
+    ref = np.zeros(8, dtype=np.uint64)
+    for i in range(n):
+        r = oracle.rollout_trace(seed, i, plies)
+        ref += r["stats"]
+        assert (b[i] == r["final_board"]).all() and list(m[i]) == list(r["final_meta"]), i
+    assert (st == ref).all(), (st, ref)
+
+
 def test_step_random_vs_oracle_final_state(oracle):
     from gym_chess_amd.env import BatchedChessEnv
 
