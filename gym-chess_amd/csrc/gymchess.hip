@@ -588,6 +588,7 @@ struct PairCtx {
     u64* htab;
     u32* hgen;
     const uint16_t* racts;  // the start position's actions (reset picks), valid when rtable
+    const EnvDev::InitCache* icd;  // the start position's move set (device memory)
     bool rtable;
     u32 rtotal;
 };
@@ -598,7 +599,7 @@ struct PairCtx {
 // Returns the ply's env.step() outputs; on return both waves hold the same s, and with
 // SHARE_ACT the same next action a (W0 picks it; it crosses to W1 through LDS).
 template <bool SHARE_ACT>
-__device__ __forceinline__ StepOut pair_ply(PairLds& L, const EnvDev& e, const PairCtx& C, int role, int l, int i,
+__device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, int role, int l, int i,
                                             bool live, const Pos& rp, Pos& s, int& a, u32& d, DevHist& h,
                                             u32& nst) {
     PairScratch scr{&L.slots[0][l]};
@@ -734,15 +735,16 @@ __device__ __forceinline__ StepOut pair_ply(PairLds& L, const EnvDev& e, const P
             tot = (int)C.rtotal;
         } else {
             if (!have) {
-                if (e.ic.usable) {
-                    g.white = e.ic.white; g.own = e.ic.own; g.castles = e.ic.castles;
-                    ms.fastp = e.ic.fastp; ms.o1 = e.ic.o1; ms.o2 = e.ic.o2; ms.ol = e.ic.ol; ms.orr = e.ic.orr;
+                const EnvDev::InitCache& ic = *C.icd;
+                if (ic.usable) {
+                    g.white = ic.white; g.own = ic.own; g.castles = ic.castles;
+                    ms.fastp = ic.fastp; ms.o1 = ic.o1; ms.o2 = ic.o2; ms.ol = ic.ol; ms.orr = ic.orr;
 #pragma unroll
-                    for (int b = 0; b < 5; b++) ms.cnt[b] = e.ic.cnt[b];
-                    ms.total = e.ic.total;
+                    for (int b = 0; b < 5; b++) ms.cnt[b] = ic.cnt[b];
+                    ms.total = ic.total;
                     ms.big = false;
 #pragma unroll
-                    for (int j = 0; j < SCRATCH_SLOTS; j++) scr.put(j, e.ic.slots[j]);
+                    for (int j = 0; j < SCRATCH_SLOTS; j++) scr.put(j, ic.slots[j]);
                 } else {
                     gen_init(s, g);
                     gen_moves(s, g, ms, scr);
@@ -799,11 +801,12 @@ __device__ __forceinline__ PairIO store_io(uint8_t* slab, int nn) {
     return PairIO(slab, nn);
 }
 
-// Everything the step needs on its common path leads the argument list (11 dwords: the slab
-// base, n, the block offset, the seed, the window tables, the reset table and its size) so
-// that kernarg preloading (hipcc -mllvm -amdgpu-kernarg-preload-count=16) hands it over in
-// SGPRs at wave launch: a kernel-argument s_load costs a scalar-memory round trip at every
-// launch (the scalar cache starts cold), paid wherever the compiler sinks it.
+// The paired kernels take no EnvDev: every argument fits the 16 preloaded dwords
+// (hipcc -mllvm -amdgpu-kernarg-preload-count=16; step: 13, rollout: 16), which arrive in
+// SGPRs at wave launch.  A kernel-argument s_load is a round trip to the kernarg buffer at
+// every launch -- measured ~2-3k cycles, paid wherever the compiler sinks it, and with SGPRs
+// scarce it sank it next to a spill that forced the wait in phase 1.  The reset position and
+// move set come from a device-memory copy (icd) instead.
 #define PAIR_PROLOGUE                                                                                       \
     __shared__ PairLds L;                                                                                   \
     const int role = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); /* wave-uniform */           \
@@ -813,15 +816,14 @@ __device__ __forceinline__ PairIO store_io(uint8_t* slab, int nn) {
     const bool live = i < nn;                                                                               \
     const int ii = live ? i : nn - 1; /* dead lanes read a valid board, store nothing */                    \
     const PairIO in_io(slab, nn);                                                                           \
-    const PairCtx C = {seed, htab, in_io.hgen, racts, (rinfo >> 16) != 0, rinfo & 0xFFFFu};                 \
+    const PairCtx C = {seed, htab, in_io.hgen, racts, icd, (rinfo >> 16) != 0, rinfo & 0xFFFFu};                 \
     GC_STAMP(0);                                                                                            \
     Pos s = in_io.load(ii);                                                                                 \
     u32 ua = in_io.act[ii], g0 = in_io.hgen[ii], nst = in_io.nsteps[ii], d = in_io.draw[ii];                \
-    /* the reset position (15 dwords, not preloaded): its s_load is waited for only after the */           \
-    /* board loads above have issued (an asm use is a scheduling barrier for memory operations: */         \
-    /* placed first, the kernarg round trip -- ~2k cycles, the scalar cache is cold at every launch -- */  \
-    /* delayed every global load); the opaque use keeps the compiler from re-loading it at the reset */    \
-    Pos rp = e.ic.pos;                                                                                      \
+    /* the reset position (HBM, scalar loads): waited for only after the board loads above have */         \
+    /* issued (an asm use is a scheduling barrier for memory operations: placed first, its round */        \
+    /* trip delayed every global load); the opaque use keeps it from being re-loaded at the reset */       \
+    Pos rp = icd->pos;                                                                                      \
     asm volatile("" : "+v"(rp.k), "+v"(rp.q), "+v"(rp.r), "+v"(rp.b), "+v"(rp.n), "+v"(rp.p), "+v"(rp.w),  \
                  "+v"(rp.meta)); /* VGPRs: SGPRs are the scarce file here */                                  \
     pin(s); pin(ua); pin(g0); pin(nst); pin(d);                                                             \
@@ -831,9 +833,10 @@ __device__ __forceinline__ PairIO store_io(uint8_t* slab, int nn) {
 
 __global__ void __launch_bounds__(2 * PAIR_BOARDS)
     k_env_step2(uint8_t* __restrict__ slab, int nn, int blk0, uint64_t seed, u64* __restrict__ htab,
-                const uint16_t* __restrict__ racts, u32 rinfo /* ic.table << 16 | ic.total */, EnvDev e) {
+                const uint16_t* __restrict__ racts, const EnvDev::InitCache* __restrict__ icd,
+                u32 rinfo /* ic.table << 16 | ic.total */) {
     PAIR_PROLOGUE
-    StepOut o = pair_ply<false>(L, e, C, role, l, i, live, rp, s, a, d, h, nst);
+    StepOut o = pair_ply<false>(L, C, role, l, i, live, rp, s, a, d, h, nst);
     GC_STAMP(6);
     const PairIO io = store_io(slab, nn);
     if (live) {
@@ -861,14 +864,15 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS)
 // ply's outputs and per-board stats (as k_env_rollout) are written at the end.
 __global__ void __launch_bounds__(2 * PAIR_BOARDS)
     k_env_rollout2(uint8_t* __restrict__ slab, int nn, int blk0, uint64_t seed, u64* __restrict__ htab,
-                   const uint16_t* __restrict__ racts, u32 rinfo, int plies, uint64_t* __restrict__ stats, EnvDev e) {
+                   const uint16_t* __restrict__ racts, const EnvDev::InitCache* __restrict__ icd, u32 rinfo, int plies,
+                   uint64_t* __restrict__ stats) {
     PAIR_PROLOGUE
     uint64_t steps = 0, rsum = 0;
     u32 e_mate = 0, e_rep = 0, e_cap = 0, e_nomove = 0, e_err = 0;
     StepOut o = {0, 0, R_NONE, 0};
     for (int p = 0; p < plies; p++) {
         int played = a;
-        o = pair_ply<true>(L, e, C, role, l, i, live, rp, s, a, d, h, nst);
+        o = pair_ply<true>(L, C, role, l, i, live, rp, s, a, d, h, nst);
         if (played == A_NONE) {
             e_nomove++;
         } else {
@@ -1298,13 +1302,14 @@ struct gc_env {
     int rules = 0;              // 0 reference, 1 FIDE (gc_fide.h)
     int8_t* ep = nullptr;       // FIDE ingest: en-passant files
     uint16_t* reset_acts = nullptr;
+    EnvDev::InitCache* icd = nullptr;  // device copy of d.ic (the paired kernels read it from HBM)
     uint8_t* slab = nullptr;  // per-board fields (Slab): bb, meta, hgen, draw, nsteps, reward, act, done, reason
     hipGraphExec_t graph_exec = nullptr;  // GC_GRAPH: a captured chunk of step launches
     int graph_chunk = 0;
 };
 
 static void env_free(gc_env* e) {
-    void* ps[] = {e->reset_acts, e->ep, e->slab, e->d.htab, e->mbox, e->m8, e->mask, e->list, e->counts,
+    void* ps[] = {e->reset_acts, e->icd, e->ep, e->slab, e->d.htab, e->mbox, e->m8, e->mask, e->list, e->counts,
                   e->lmask, e->stats};
     for (void* p : ps) if (p) (void)hipFree(p);
     for (auto& v : e->ev) if (v) (void)hipEventDestroy(v);
@@ -1330,7 +1335,7 @@ static void launch_step2(gc_env* e, hipStream_t st) {
     const EnvDev& d = e->d;
     u32 rinfo = (d.ic.table ? 1u << 16 : 0u) | (u32)(d.ic.total & 0xFFFF);
     k_env_step2<<<(e->n + PAIR_BOARDS - 1) / PAIR_BOARDS, 2 * PAIR_BOARDS, 0, st>>>(
-        e->slab, d.n, 0, d.seed, d.htab, d.reset_acts, rinfo, d);
+        e->slab, d.n, 0, d.seed, d.htab, d.reset_acts, e->icd, rinfo);
 }
 
 extern "C" int gc_env_create(int device, int n_boards, uint64_t seed, const int8_t* initial_board, gc_env** out) {
@@ -1402,11 +1407,11 @@ extern "C" int gc_env_create(int device, int n_boards, uint64_t seed, const int8
         }
         e->reset_acts = dacts;
         e->d.reset_acts = dacts;
+        e->icd = dic;
         k_init_cache<<<1, BLOCK, 0, e->stream>>>(e->d, dic, dacts);
         he = hipGetLastError();
         if (he == hipSuccess) he = hipMemcpyAsync(&e->d.ic, dic, sizeof(EnvDev::InitCache), hipMemcpyDeviceToHost, e->stream);
         if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
-        (void)hipFree(dic);
         if (he != hipSuccess) { env_free(e); delete e; return fail(std::string("init cache: ") + hipGetErrorString(he)); }
     }
     launch_reset(e, nullptr, 1);
@@ -1558,7 +1563,7 @@ extern "C" int gc_env_rollout(gc_env* e, int n_plies, int16_t* tr_action, int16_
         const EnvDev& d = e->d;
         u32 rinfo = (d.ic.table ? 1u << 16 : 0u) | (u32)(d.ic.total & 0xFFFF);
         k_env_rollout2<<<(e->n + PAIR_BOARDS - 1) / PAIR_BOARDS, 2 * PAIR_BOARDS, 0, e->stream>>>(
-            e->slab, d.n, 0, d.seed, d.htab, d.reset_acts, rinfo, n_plies, e->stats, d);
+            e->slab, d.n, 0, d.seed, d.htab, d.reset_acts, e->icd, rinfo, n_plies, e->stats);
     } else {
         k_env_rollout<false><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d, n_plies, da, dr, dd, dq, e->stats);
     }
