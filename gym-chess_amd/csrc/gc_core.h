@@ -317,29 +317,48 @@ GC_HD void gen_base(const Pos& s, Gen& g) {
     g.in_check = false;
 }
 
+// Checkers, check mask and pins set-wise, one line through the king at a time (no loop over
+// pinners, no `between`): a1 = the line's attack set from the king (up to and including the
+// first blocker each way), a2 = the same with the own first blockers removed (the x-ray).
+// Per direction (squares above / below the king): a slider of the line's kind at the end of
+// a1 checks, and a1 on that side is "checker | between"; one at the end of a2 but not in a1
+// pins the own blocker, and a2 on that side is the pin segment king..pinner (pinner included).
+// Same sets as the reference's per-move filter (see above): a pinner is the first enemy piece
+// on its ray with exactly one (own) piece between.
+GC_HD void pin_line(u64 mask, const LineNeg& ln, u64 occ, u64 own, u64 sliders, u64 hi, u64 lo, u64& checkers,
+                    u64& block, u64& pinned, u64& pinrays) {
+    u64 a1 = line_att(occ, mask, ln);
+    u64 a2 = line_att(occ ^ (a1 & own), mask, ln);
+    u64 chk = a1 & sliders;
+    u64 pn = a2 & ~a1 & sliders;
+    checkers |= chk;
+    u64 a1u = a1 & hi, a1d = a1 & lo, a2u = a2 & hi, a2d = a2 & lo;
+    block |= ((a1u & chk) ? a1u : 0ull) | ((a1d & chk) ? a1d : 0ull);
+    bool pu = (a2u & pn) != 0, pd = (a2d & pn) != 0;
+    pinned |= ((pu ? a1u : 0ull) | (pd ? a1d : 0ull)) & own;
+    pinrays |= (pu ? a2u : 0ull) | (pd ? a2d : 0ull);
+}
+
 GC_HD void gen_pins(const Pos& s, Gen& g) {
     if (g.ks < 0) return;  // "King not present": no filter, no castling, no king moves
     int ks = g.ks;
     bool white = g.white;
     u64 kb = bit(ks);
-    u64 opp = g.opp;
+    u64 opp = g.opp, occ = g.occ, own = g.own;
     u64 rq = (s.r | s.q) & opp, bq = (s.b | s.q) & opp;
-    u64 checkers = (pawn_att_set(kb, white) & s.p & opp) | (knight_set(kb) & s.n & opp) |
-                   (king_set(kb) & s.k & opp) | (rook_att(ks, g.occ) & rq) | (bishop_att(ks, g.occ) & bq);
+    u64 checkers = (pawn_att_set(kb, white) & s.p & opp) | (knight_set(kb) & s.n & opp) | (king_set(kb) & s.k & opp);
+    u64 block = 0, pinned = 0, pinrays = 0;
+    u64 lo = below(ks), hi = ~(lo | kb);
+    LineNeg ln = line_neg(ks);
+    pin_line(file_mask(ks), ln, occ, own, rq, hi, lo, checkers, block, pinned, pinrays);
+    pin_line(row_mask(ks), ln, occ, own, rq, hi, lo, checkers, block, pinned, pinrays);
+    pin_line(diag_mask(ks), ln, occ, own, bq, hi, lo, checkers, block, pinned, pinrays);
+    pin_line(anti_mask(ks), ln, occ, own, bq, hi, lo, checkers, block, pinned, pinrays);
     g.in_check = checkers != 0;
     // one checker: capture it or block (checkers | between); two: king moves only; none: all
-    u64 single = checkers | between(ks, ctz(checkers ? checkers : 1ull));
-    g.checkmask = !checkers ? ~0ull : ((checkers & (checkers - 1)) ? 0ull : single);
-    u64 snipers = (rook_att(ks, opp) & rq) | (bishop_att(ks, opp) & bq);
-    while (snipers) {
-        int sq = ctz(snipers);
-        snipers ^= bit(sq);
-        u64 seg = between(ks, sq);
-        u64 bw = seg & g.occ;
-        bool pin = bw && !(bw & (bw - 1)) && (bw & g.own);
-        g.pinned |= pin ? bw : 0ull;
-        g.pinrays |= pin ? (seg | bit(sq)) : 0ull;
-    }
+    g.checkmask = !checkers ? ~0ull : ((checkers & (checkers - 1)) ? 0ull : (checkers | block));
+    g.pinned = pinned;
+    g.pinrays = pinrays;
 }
 
 GC_HD void gen_enemy(const Pos& s, Gen& g) {

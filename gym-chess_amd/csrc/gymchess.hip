@@ -26,7 +26,11 @@ __shared__ unsigned long long gc_stamp_lds[4][8];
 __device__ __forceinline__ void gc_stamp(int k) {
     __builtin_amdgcn_sched_barrier(0);
     unsigned long long t;
+#ifdef GC_STAMPS_REAL  // the 100 MHz constant clock, comparable across CUs (launch ramp / tail)
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+#else
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+#endif
     __builtin_amdgcn_sched_barrier(0);
     if ((threadIdx.x & 63) == 0) gc_stamp_lds[threadIdx.x >> 6][k] = t;
 }
@@ -560,6 +564,9 @@ __global__ void __launch_bounds__(BLOCK) k_env_step(EnvDev e) {
 // Results are bit-identical to k_env_step<true, false> (same gc_core/gc_env functions,
 // same order of decisions; tests/test_gpu_parity.py compares both with the oracle).
 #define PAIR_BOARDS 64
+#ifndef PAIRS_WG
+#define PAIRS_WG 1  // board pairs (64 boards, two waves) per workgroup
+#endif
 struct PairLds {
     u64 slots[SCRATCH_SLOTS][PAIR_BOARDS];  // parked targets (both waves write, W0 reads)
     u64 pin3[3][PAIR_BOARDS];               // W0 -> W1: checkmask, pinned, pinrays
@@ -570,6 +577,13 @@ struct PairLds {
     u32 part[2][PAIR_BOARDS];               // partial move totals per wave
     u32 rep[PAIR_BOARDS];                   // W1 -> W0: 3-fold count c | window length << 8
     u32 act[PAIR_BOARDS];                   // W0 -> W1: the next action (fused rollout)
+    u32 draw[PAIR_BOARDS];                  // W0 -> W1: the next draw counter (fused rollout)
+    u64 ns[NBB][PAIR_BOARDS];               // W0 -> W1: the post-move board (phase 0)
+    u32 nmeta[PAIR_BOARDS];
+    int32_t mr[PAIR_BOARDS];                //           its capture reward
+    u32 irrev[PAIR_BOARDS];                 //           irreversible move (3-fold window reset)
+    u32 x0[PAIR_BOARDS];                    // W1 -> W0: the Philox word of the next draw
+    u32 ra[PAIR_BOARDS];                    // W1 -> W0: the start-position table pick
 };
 struct PairScratch {
     static constexpr bool kPark = true;
@@ -582,6 +596,11 @@ struct PairScratch {
 // is meant to stay in flight through phase 1.
 __device__ __forceinline__ void pair_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+#ifdef GC_WPE  // diagnostic builds: register budget of the paired kernels
+#define PAIR_ATTR __attribute__((amdgpu_waves_per_eu(GC_WPE)))
+#else
+#define PAIR_ATTR
+#endif
 // Per-launch constants of the paired kernels (SGPRs).
 struct PairCtx {
     uint64_t seed;
@@ -608,31 +627,51 @@ __device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, int ro
     const bool cap = mc_of(s.meta) > MOVES_MAX;              // 252-258
     const bool mv = live && !none && !done0 && !cap;         // env_ply runs
     const bool white = (s.meta & M_WHITE) != 0;
-    Pos ns = s;
-    ns.meta = (ns.meta & ~(u32)M_RIGHTS) | eff_rights(s);    // State::new
     int mr = 0;
     bool irrev = false;
-    if (mv) apply_legal(ns, white, a, &mr, &irrev);
-    Gen g;
-    gen_base(ns, g);
+    Pos ns;
     RepProbe pr;
     bool my_chk = false;
     u32 x0 = 0;
+    uint16_t ra = (uint16_t)A_NONE;
+
+    // ---- phase 0: W0 applies the action (once per board, not once per wave); W1 issues the
+    // window probe of the pre-move board (Q8), draws the next Philox word and, for a board
+    // that resets this ply, reads its pick from the start position's table (lands long
+    // before phase 3)
+    if (role == 0) {
+        ns = s;
+        ns.meta = (ns.meta & ~(u32)M_RIGHTS) | eff_rights(s);  // State::new
+        if (mv) apply_legal(ns, white, a, &mr, &irrev);
+        L.ns[0][l] = ns.k; L.ns[1][l] = ns.q; L.ns[2][l] = ns.r; L.ns[3][l] = ns.b;
+        L.ns[4][l] = ns.n; L.ns[5][l] = ns.p; L.ns[6][l] = ns.w;
+        L.nmeta[l] = ns.meta;
+        L.mr[l] = mr;
+        L.irrev[l] = irrev ? 1u : 0u;
+    } else {
+        if (mv) rep_prefetch(h, s, pr);
+        x0 = philox_x0(C.seed, (u32)i, d);  // the next draw (independent of the position)
+        if (C.rtable) ra = C.racts[scale_rank(x0, C.rtotal)];
+        L.x0[l] = x0;
+    }
+    pair_barrier();
 
     // ---- phase 1
-    uint16_t ra = (uint16_t)A_NONE;
+    Gen g;
     if (role == 0) {
-        x0 = philox_x0(C.seed, (u32)i, d);  // the next draw (independent of the position)
-        // a board that resets this ply picks from the start position's table: issue that
-        // read now, it lands long before phase 3
-        if (C.rtable) ra = C.racts[scale_rank(x0, C.rtotal)];
+        gen_base(ns, g);
         gen_pins(ns, g);
         L.pin3[0][l] = g.checkmask;
         L.pin3[1][l] = g.pinned;
         L.pin3[2][l] = g.pinrays;
         L.f0[l] = g.in_check ? 1u : 0u;
     } else {
-        if (mv) rep_prefetch(h, s, pr);  // pre-move board (Q8); lands during phases 1-2
+        ns.k = L.ns[0][l]; ns.q = L.ns[1][l]; ns.r = L.ns[2][l]; ns.b = L.ns[3][l];
+        ns.n = L.ns[4][l]; ns.p = L.ns[5][l]; ns.w = L.ns[6][l];
+        ns.meta = L.nmeta[l];
+        mr = L.mr[l];
+        irrev = L.irrev[l] != 0;
+        gen_base(ns, g);
         gen_enemy(ns, g);
         int mk = tracked_king(ns, white);
         my_chk = mk >= 0 && sq_attacked(ns, mk, !white);
@@ -676,6 +715,7 @@ __device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, int ro
             c = rep_commit(h, s, pr, hl, irrev);  // table write deferred to h.commit()
         }
         L.rep[l] = (u32)c | (hl << 8);
+        L.ra[l] = ra;  // landed by now (issued in phase 0)
     }
 #pragma unroll
     for (int b = 0; b < 5; b++) L.planes[role][b][l] = ms.cnt[b];
@@ -692,6 +732,8 @@ __device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, int ro
         u32 rpk = L.rep[l];
         c = (int)(rpk & 0xFFu);
         hl = rpk >> 8;
+        x0 = L.x0[l];
+        ra = (uint16_t)L.ra[l];
     }
     StepOut o = {0, 0, R_NONE, 0};
     bool have = false;
@@ -755,11 +797,17 @@ __device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, int ro
         }
         a = act;
         d += tot > 0 ? 1u : 0u;
-        if (SHARE_ACT) L.act[l] = act;
+        if (SHARE_ACT) {
+            L.act[l] = act;
+            L.draw[l] = d;
+        }
     }
-    if (SHARE_ACT) {  // the next action to W1; LDS free for the next ply
+    if (SHARE_ACT) {  // the next action and draw counter to W1; LDS free for the next ply
         pair_barrier();
-        if (role) a = (int)L.act[l];
+        if (role) {
+            a = (int)L.act[l];
+            d = L.draw[l];
+        }
     }
     return o;
 }
@@ -808,10 +856,12 @@ __device__ __forceinline__ PairIO store_io(uint8_t* slab, int nn) {
 // scarce it sank it next to a spill that forced the wait in phase 1.  The reset position and
 // move set come from a device-memory copy (icd) instead.
 #define PAIR_PROLOGUE                                                                                       \
-    __shared__ PairLds L;                                                                                   \
-    const int role = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); /* wave-uniform */           \
+    __shared__ PairLds Ls[PAIRS_WG];                                                                        \
+    const int pw = PAIRS_WG > 1 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 7)) : 0;              \
+    PairLds& L = Ls[pw];                                                                                    \
+    const int role = __builtin_amdgcn_readfirstlane((int)((threadIdx.x >> 6) & 1)); /* wave-uniform */     \
     const int l = threadIdx.x & (PAIR_BOARDS - 1);                                                          \
-    const int blk = blockIdx.x + blk0; /* board block (a launch may cover a sub-range) */                   \
+    const int blk = blockIdx.x * PAIRS_WG + pw + blk0; /* board block (a launch may cover a sub-range) */   \
     const int i = blk * PAIR_BOARDS + l;                                                                    \
     const bool live = i < nn;                                                                               \
     const int ii = live ? i : nn - 1; /* dead lanes read a valid board, store nothing */                    \
@@ -831,7 +881,7 @@ __device__ __forceinline__ PairIO store_io(uint8_t* slab, int nn) {
     int a = (int)ua;                                                                                        \
     DevHist h = DevHist{htab, in_io.hgen, g0, ii};
 
-__global__ void __launch_bounds__(2 * PAIR_BOARDS)
+__global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
     k_env_step2(uint8_t* __restrict__ slab, int nn, int blk0, uint64_t seed, u64* __restrict__ htab,
                 const uint16_t* __restrict__ racts, const EnvDev::InitCache* __restrict__ icd,
                 u32 rinfo /* ic.table << 16 | ic.total */) {
@@ -856,13 +906,13 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS)
     GC_STAMP(7);
 #ifdef GC_STAMPS
     if (g_stamp_out != nullptr && l == 0)
-        for (int q = 0; q < 8; q++) g_stamp_out[((size_t)blk * 2 + role) * 8 + q] = gc_stamp_lds[role][q];
+        for (int q = 0; q < 8; q++) g_stamp_out[((size_t)blk * 2 + role) * 8 + q] = gc_stamp_lds[threadIdx.x >> 6][q];
 #endif
 }
 
 // Fused K-ply random self-play on the paired step: the state stays in registers; the last
 // ply's outputs and per-board stats (as k_env_rollout) are written at the end.
-__global__ void __launch_bounds__(2 * PAIR_BOARDS)
+__global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
     k_env_rollout2(uint8_t* __restrict__ slab, int nn, int blk0, uint64_t seed, u64* __restrict__ htab,
                    const uint16_t* __restrict__ racts, const EnvDev::InitCache* __restrict__ icd, u32 rinfo, int plies,
                    uint64_t* __restrict__ stats) {
@@ -1334,7 +1384,7 @@ static void launch_step(gc_env* e) {
 static void launch_step2(gc_env* e, hipStream_t st) {
     const EnvDev& d = e->d;
     u32 rinfo = (d.ic.table ? 1u << 16 : 0u) | (u32)(d.ic.total & 0xFFFF);
-    k_env_step2<<<(e->n + PAIR_BOARDS - 1) / PAIR_BOARDS, 2 * PAIR_BOARDS, 0, st>>>(
+    k_env_step2<<<(e->n + PAIR_BOARDS * PAIRS_WG - 1) / (PAIR_BOARDS * PAIRS_WG), 2 * PAIR_BOARDS * PAIRS_WG, 0, st>>>(
         e->slab, d.n, 0, d.seed, d.htab, d.reset_acts, e->icd, rinfo);
 }
 
@@ -1562,7 +1612,8 @@ extern "C" int gc_env_rollout(gc_env* e, int n_plies, int16_t* tr_action, int16_
     } else if (!trace && !one_wave) {  // the paired kernel (per-ply traces: the one-wave kernel)
         const EnvDev& d = e->d;
         u32 rinfo = (d.ic.table ? 1u << 16 : 0u) | (u32)(d.ic.total & 0xFFFF);
-        k_env_rollout2<<<(e->n + PAIR_BOARDS - 1) / PAIR_BOARDS, 2 * PAIR_BOARDS, 0, e->stream>>>(
+        k_env_rollout2<<<(e->n + PAIR_BOARDS * PAIRS_WG - 1) / (PAIR_BOARDS * PAIRS_WG), 2 * PAIR_BOARDS * PAIRS_WG, 0,
+                         e->stream>>>(
             e->slab, d.n, 0, d.seed, d.htab, d.reset_acts, e->icd, rinfo, n_plies, e->stats);
     } else {
         k_env_rollout<false><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d, n_plies, da, dr, dd, dq, e->stats);
