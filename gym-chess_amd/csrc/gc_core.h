@@ -579,8 +579,9 @@ GC_HD void moveset_clear(MoveSet& ms) {
     ms.big = false;
 }
 
-// Part A of the generation: pawns (set-wise), knights, kings.  `ms` cleared; ORs
-// into ms.cnt; returns the number of moves found.
+// Part A of the generation: pawns (set-wise), knights, kings, queens.  `ms` cleared; ORs
+// into ms.cnt; returns the number of moves found.  (The split A | B balances the two waves
+// of the paired step kernel: queens cost a bishop plus a rook.)
 template <class S>
 GC_HD int gen_moves_a(const Pos& s, const Gen& g, MoveSet& ms, S& scr) {
     const u64 own = g.own, cm = g.checkmask, notown_cm = ~own & cm;
@@ -625,10 +626,18 @@ GC_HD int gen_moves_a(const Pos& s, const Gen& g, MoveSet& ms, S& scr) {
         x ^= bit(sq);
         park(ms, scr, own, sq, king_set(bit(sq)) & ~own & ~g.enemy_att, total);
     }
+    x = s.q & own;
+    while (x) {
+        int sq = ctz(x);
+        x ^= bit(sq);
+        u64 tg = queen_att(sq, g.occ) & notown_cm;
+        if ((g.pinned >> sq) & 1) tg &= g.pinrays & line_through(g.ks, sq);
+        park(ms, scr, own, sq, tg, total);
+    }
     return total;
 }
 
-// Part B: the sliders (bishops, rooks, queens).  ORs into ms.cnt; returns the number of moves found.
+// Part B: bishops and rooks.  ORs into ms.cnt; returns the number of moves found.
 template <class S>
 GC_HD int gen_moves_b(const Pos& s, const Gen& g, MoveSet& ms, S& scr) {
     const u64 own = g.own, notown_cm = ~own & g.checkmask;
@@ -646,14 +655,6 @@ GC_HD int gen_moves_b(const Pos& s, const Gen& g, MoveSet& ms, S& scr) {
         int sq = ctz(x);
         x ^= bit(sq);
         u64 tg = rook_att(sq, g.occ) & notown_cm;
-        if ((g.pinned >> sq) & 1) tg &= g.pinrays & line_through(g.ks, sq);
-        park(ms, scr, own, sq, tg, total);
-    }
-    x = s.q & own;
-    while (x) {
-        int sq = ctz(x);
-        x ^= bit(sq);
-        u64 tg = queen_att(sq, g.occ) & notown_cm;
         if ((g.pinned >> sq) & 1) tg &= g.pinrays & line_through(g.ks, sq);
         park(ms, scr, own, sq, tg, total);
     }

@@ -28,6 +28,14 @@ __device__ __forceinline__ void gc_stamp(int k) {
     unsigned long long t;
 #ifdef GC_STAMPS_REAL  // the 100 MHz constant clock, comparable across CUs (launch ramp / tail)
     asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    if (k == 0) {  // placement of the wave in bits 44+ of its first stamp: cu | sh | se | simd | xcc
+        unsigned hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)\n\ts_getreg_b32 %1, hwreg(HW_REG_XCC_ID)"
+                     : "=s"(hw), "=s"(xcc));
+        unsigned long long where = ((hw >> 8) & 0xF) | (((hw >> 12) & 1) << 4) | (((hw >> 13) & 3) << 5) |
+                                   (((hw >> 4) & 3) << 7) | ((unsigned long long)(xcc & 0xF) << 9);
+        t = (t & ((1ull << 44) - 1)) | (where << 44);
+    }
 #else
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
 #endif
