@@ -283,6 +283,43 @@ def test_step_random_per_ply_vs_oracle(oracle):
         assert (o["next_action"] == nxt).all(), (p, np.nonzero(o["next_action"] != nxt)[0][:4])
 
 
+def _weird_initial_boards():
+    """Initial boards the reference accepts but chess never has (several / no kings, pawns on
+    the back rank, > 16 own pieces), for the bench kernel's reset and fallback paths."""
+    from oracle import DEFAULT_BOARD
+
+    boards, _ = random_positions(10, 4711)
+    crowd = DEFAULT_BOARD.copy()  # 20 white pieces: the per-square fallback, no reset cache
+    crowd[[33, 35, 37, 39]] = 2
+    return list(boards) + [crowd]
+
+
+@pytest.mark.parametrize("k", range(11))
+def test_step_random_weird_initial_boards_vs_oracle(oracle, k):
+    """k_env_step2 ply by ply from (and resetting to) a weird initial board: outputs, next
+    action and final states vs the oracle driver with the same initial board.  70 boards:
+    a partial second workgroup."""
+    from gym_chess_amd.env import BatchedChessEnv
+
+    ib = _weird_initial_boards()[k]
+    n, plies, seed = 70, 90, 1000 + k
+    env = BatchedChessEnv(n, device=0, seed=seed, initial_board=ib)
+    refs = [oracle.rollout_trace(seed, i, plies + 1, init=ib) for i in range(n)]
+    ra = np.stack([r["action"] for r in refs], axis=1)
+    for p in range(plies):
+        env.step_random(1)
+        o = env.outputs()
+        nxt = np.where(ra[p + 1] < 0, 0xFFFF, ra[p + 1]).astype(np.uint16)
+        for key, name in (("reward", "reward"), ("done", "done"), ("reason", "reason")):
+            want = np.stack([r[name][p] for r in refs])
+            assert (o[key] == want).all(), (k, p, key, np.nonzero(o[key] != want)[0][:4])
+        assert (o["next_action"] == nxt).all(), (k, p, np.nonzero(o["next_action"] != nxt)[0][:4])
+    b, m = env.boards()
+    fin = [oracle.rollout_trace(seed, i, plies, init=ib) for i in range(n)]
+    for i in range(n):
+        assert (b[i] == fin[i]["final_board"]).all() and list(m[i]) == list(fin[i]["final_meta"]), (k, i)
+
+
 def test_fused_rollout_stats_and_states_vs_oracle(oracle):
     """The paired fused-rollout kernel (k_env_rollout2, no trace): per-board final states and
     the aggregate episode stats of 200 boards x 500 plies == the oracle driver's."""
