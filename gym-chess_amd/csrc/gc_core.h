@@ -260,6 +260,41 @@ GC_HD int tracked_king(const Pos& s, bool white) {
     return kk ? sq : -1;
 }
 
+// The mover's check flag after a LEGAL `action` of the side `white` (update_state,
+// lib.rs:1386-1393, for the side that just moved): s = the position before, ns = after.
+//  * a non-king move: false.  The reference admits it only if king_is_checked(next_state)
+//    is false (move_leaves_king_checked, lib.rs:612-624) -- the very flag computed here.
+//  * a king move (the only own king): its target was outside the pre-move enemy map
+//    (lib.rs:613-619), and vacating f / occupying t changes no leaper's attacks, so t is
+//    attacked afterwards only (a) along the line through t and f by an enemy slider that had
+//    the king on f in check (the Q6 retreat along the checking ray), or (b) by an enemy pawn,
+//    when t held the enemy king: pawns skip squares holding their own king (lib.rs:930).
+//  * castles and several own kings (tracked king may change): the full attack probe.
+GC_HD bool mover_checked(const Pos& s, const Pos& ns, bool white, int action) {
+    u64 occ0 = occ_of(s);
+    u64 mine0 = white ? s.w : (occ0 & ~s.w);
+    u64 kings = s.k & mine0;
+    int f = (action >> 6) & 63, t = action & 63;
+    bool kmove = action < 4096 && ((kings >> f) & 1);
+    if (action >= 4096 || (kmove && (kings & (kings - 1)))) {  // rare: the general probe
+        int mk = tracked_king(ns, white);
+        return mk >= 0 && sq_attacked(ns, mk, !white);
+    }
+    if (!kmove) return false;
+    u64 occn = occ_of(ns);
+    u64 them = white ? (occn & ~ns.w) : ns.w;
+    int dc = (t & 7) - (f & 7), dr = (t >> 3) - (f >> 3);
+    bool orth = dc == 0 || dr == 0;
+    u64 line = dc == 0 ? file_mask(f) : dr == 0 ? row_mask(f) : dr == dc ? diag_mask(f) : anti_mask(f);
+    u64 sl = (orth ? (ns.r | ns.q) : (ns.b | ns.q)) & them;
+    u64 att = line_att(occn, line, line_neg(f));
+    u64 away = t > f ? below(f) : ~(below(f) | bit(f));  // beyond f, away from t
+    u64 tb = bit(t);
+    bool xray = (att & away & sl) != 0;
+    bool pawn = (s.k & tb & ~mine0) && (pawn_att_set(tb, white) & ns.p & them);
+    return xray || pawn;
+}
+
 // castle rights as the engine sees them on every call: State::new forces a colour's
 // rights false when it has no king (lib.rs:315-322)
 GC_HD u32 eff_rights(const Pos& s) {

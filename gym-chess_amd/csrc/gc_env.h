@@ -128,11 +128,10 @@ GC_HD int env_ply(Pos& s, H& hist, int action, Gen& g, MoveSet& ms, S& scr, int*
     bool irrev;
     apply_legal(ns, white, action, mr, &irrev);  // the action is legal (validated or policy-picked)
     // update_state (lib.rs:1386-1393): the side now to move's flag comes from its own
-    // generation pass; the mover's flag needs one attack probe.
+    // generation pass; the mover's flag follows from the move's legality (mover_checked).
     gen_init(ns, g);
     bool opp_chk = g.in_check;
-    int mk = tracked_king(ns, white);
-    bool my_chk = mk >= 0 && sq_attacked(ns, mk, !white);
+    bool my_chk = mover_checked(s, ns, white, action);
     GC_STAMP(3);
     if (opp_chk && my_chk) return 1;
     gen_moves(ns, g, ms, scr);  // the next side's possible moves (chess_v2.py:268 / 278)

@@ -681,8 +681,7 @@ __device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, int ro
         irrev = L.irrev[l] != 0;
         gen_base(ns, g);
         gen_enemy(ns, g);
-        int mk = tracked_king(ns, white);
-        my_chk = mk >= 0 && sq_attacked(ns, mk, !white);
+        my_chk = mv && mover_checked(s, ns, white, a);
         L.enemy[l] = g.enemy_att;
         L.f1[l] = g.castles | (my_chk ? 4u : 0u);
     }

@@ -91,6 +91,20 @@ extern "C" void host_update_state(const int8_t* b, const uint8_t* m, int8_t* ob,
     export_state(s, ob, om);
 }
 
+// mover_checked (the step's shortcut for the mover's check flag) next to the full probe it
+// replaces, for a legal `action` of the side to move: bit 0 = shortcut, bit 1 = full probe
+extern "C" int host_mover_checked(const int8_t* b, const uint8_t* m, int action) {
+    Pos s = import_state(b, m, -1);
+    bool white = (s.meta & M_WHITE) != 0;
+    Pos ns = s;
+    int r;
+    bool irrev;
+    apply_legal(ns, white, action, &r, &irrev);
+    int mk = tracked_king(ns, white);
+    bool full = mk >= 0 && sq_attacked(ns, mk, !white);
+    return (mover_checked(s, ns, white, action) ? 1 : 0) | (full ? 2 : 0);
+}
+
 extern "C" uint64_t host_between(int a, int b) { return between(a, b); }
 extern "C" uint64_t host_rook_att(int sq, uint64_t occ) { return rook_att(sq, occ); }
 extern "C" uint64_t host_bishop_att(int sq, uint64_t occ) { return bishop_att(sq, occ); }

@@ -40,6 +40,7 @@ def lib():
         L.host_select.argtypes = [P, P, ctypes.c_int, ctypes.c_int]
         L.host_action_legal.argtypes = [P, P, ctypes.c_int, ctypes.c_int]
         L.host_next_state.argtypes = [P, P, ctypes.c_int, ctypes.c_int, P, P, P]
+        L.host_mover_checked.argtypes = [P, P, ctypes.c_int]
         L.host_update_state.argtypes = [P, P, P, P]
         L.host_rollout_trace.argtypes = [P, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, P, P, P, P, P, P, P]
         L.host_env_new.restype = P
@@ -208,3 +209,10 @@ def fide_rollout(seed, board_id, plies, init):
     q = np.zeros(plies, dtype=np.uint8)
     lib().host_fide_rollout(_p(init), seed, board_id, plies, _p(a), _p(r), _p(d), _p(q))
     return dict(action=a, reward=r, done=d, reason=q)
+
+
+def mover_checked(board, meta, action):
+    """(shortcut, full probe) of the mover's check flag after a legal action (side to move = meta[0])"""
+    b, m = _bm(board, meta)
+    r = lib().host_mover_checked(_p(b), _p(m), int(action))
+    return bool(r & 1), bool(r & 2)

@@ -161,3 +161,23 @@ def test_env_traces(oracle):
             b, m = e.state()
             assert C.board_to_text(b) == s["board"] and m[7] == s["move_count"]
             assert len(e.moves()) == s["n_moves"]
+
+
+def test_mover_check_shortcut_every_legal_move():
+    """The step's mover check flag (mover_checked: false for non-king moves, x-ray along the
+    line through the king's squares or a captured enemy king's pawn-attacked square for king
+    moves, the full probe for castles / several kings) == the full attack probe, on every
+    legal move of weird random positions (several / no kings, castling geometry)."""
+    hits = {"king_move_checked": 0, "castle_or_multi": 0, "moves": 0}
+    for seed in (71, 72, 73):
+        boards, metas = random_positions(1500, seed)
+        for b, m in zip(boards, metas):
+            white = int(m[0])
+            for a in H.get_list(b, m, white):
+                short, full = H.mover_checked(b, m, a)
+                assert short == full, (seed, b.tolist(), m.tolist(), a)
+                hits["moves"] += 1
+                hits["king_move_checked"] += a < 4096 and full
+                hits["castle_or_multi"] += a >= 4096
+    # the interesting cases occur (Q6 retreats along a checking ray, castles)
+    assert hits["king_move_checked"] > 50 and hits["castle_or_multi"] > 50, hits
