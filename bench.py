@@ -179,13 +179,15 @@ def main():
     bytes_per_launch = n * ALG_BYTES_PER_BOARD
     avg_launch_s = kern_ms / 1e3 / args.steps
     achieved = bytes_per_launch / avg_launch_s / 1e9
-    traffic = None
+    traffic = valu = None
     tf = os.path.join(ROOT, "profiles", "pmc_traffic_latest.json")
     if os.path.exists(tf):
         try:
-            traffic = json.load(open(tf)).get("bytes_per_launch")
+            pmc = json.load(open(tf))
+            traffic = pmc.get("bytes_per_launch")
+            valu = pmc.get("valu")
         except Exception:
-            traffic = None
+            traffic = valu = None
 
     extra = {}
     if args.fused_plies > 0:
@@ -230,7 +232,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "k_env_step2", "avg_launch_us": avg_launch_s * 1e6,
-                         "alg_bytes_per_board": ALG_BYTES_PER_BOARD, "mean_window": 0.5 * (w0 + w1) / n},
+                         "alg_bytes_per_board": ALG_BYTES_PER_BOARD, "mean_window": 0.5 * (w0 + w1) / n,
+                         "valu": valu},
             "cpu_baseline": cpu,
             **extra,
         }

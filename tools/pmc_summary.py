@@ -48,6 +48,18 @@ def main():
         sq = {k: mean(v, k) / waves for k in v[0] if k != "SQ_WAVES"}
         out["per_wave"] = sq
         out["per_wave"]["note"] = "SQ_*_CYCLES / WAIT / ACTIVE in units of 4 cycles (quad-cycles)"
+    mp = os.path.join(a.src, "pmc_mix/run_counter_collection.csv")
+    if os.path.exists(mp):  # VALU utilisation (SURVEY 8d asks for it beside the HBM figure)
+        v = per_dispatch(mp, a.kernel)[-a.last:]
+        waves = mean(v, "SQ_WAVES")
+        simds_per_se = 1024 / 32  # MI355X: 256 CUs x 4 SIMDs over 8 XCDs x 4 SEs
+        out["valu"] = {
+            "insts_per_wave": mean(v, "SQ_INSTS_VALU") / waves,
+            "lane_utilisation": mean(v, "SQ_THREAD_CYCLES_VALU") / (mean(v, "SQ_ACTIVE_INST_VALU") * 64),
+            "busy_frac": mean(v, "SQ_ACTIVE_INST_VALU") * 4 / (mean(v, "SQ_BUSY_CYCLES") * simds_per_se),
+            "note": "busy_frac = SQ_ACTIVE_INST_VALU x 4 cycles / (SQ_BUSY_CYCLES x SIMDs per SE), whole launch "
+                    "incl. ramp and tail; lane_utilisation = active lanes per VALU instruction / 64",
+        }
     os.makedirs(a.dst, exist_ok=True)
     for p in (os.path.join(a.dst, "pmc_traffic.json"), os.path.join(os.path.dirname(a.dst.rstrip("/")),
                                                                        "pmc_traffic_latest.json")):
