@@ -129,7 +129,7 @@ def perft_leg(args, rep, device):
     out = {"value": tot / dtm, "unit": "perft_nodes/s", "roots_per_gpu": args.perft_roots, "depth": args.perft_depth,
            "nodes": tot, "seconds": dtm,
            "roots_with": {"castle_right": castle, "pawn_on_7th": prom, "side_in_check": check}}
-    if rep.rank == 0 and not args.no_cpu_baseline and args.cpu_perft_roots > 0:
+    if rep.rank == 0 and rep.world_size == 1 and not args.no_cpu_baseline and args.cpu_perft_roots > 0:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle as O
 
@@ -209,7 +209,7 @@ def main():
         extra["perft"] = perft_leg(args, rep, rep.local_rank)
 
     cpu = None
-    if rep.rank == 0 and not args.no_cpu_baseline:
+    if rep.rank == 0 and rep.world_size == 1 and not args.no_cpu_baseline:  # N=1 only (contract)
         cpu = cpu_baseline(args)
 
     if rep.rank == 0:
