@@ -274,6 +274,25 @@ __global__ void __launch_bounds__(BLOCK) k_perft_small(SoA in, int depth, uint64
     nodes[i] = perft_small(in.load(i), depth, sa, sb);
 }
 
+// The same over a permutation of the subtrees: perft_small's outer loop runs the subtree
+// root's move count, so lanes of one wave given roots of equal count (perm = roots sorted by
+// it) do not idle through the wave's longest list.  (PMC: 56 % lane utilisation unsorted.)
+__global__ void __launch_bounds__(BLOCK) k_perft_small_perm(SoA in, const int32_t* __restrict__ perm, int depth,
+                                                            uint64_t* __restrict__ nodes) {
+    __shared__ u64 lds_a[SCRATCH_SLOTS * BLOCK];
+    __shared__ u64 lds_b[SCRATCH_SLOTS * BLOCK];
+    LdsScratch sa{lds_a + threadIdx.x};
+    LdsScratch sb{lds_b + threadIdx.x};
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= in.n) return;
+    int j = perm[i];
+    nodes[j] = perft_small(in.load(j), depth, sa, sb);
+}
+__global__ void k_iota(int32_t* __restrict__ v, int n) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) v[i] = i;
+}
+
 // children of every node, written at offs[i] .. offs[i]+cnt[i] (offs = exclusive scan)
 __global__ void k_count_children(SoA in, int32_t* __restrict__ cnt) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1315,8 +1334,33 @@ static int perft_device(hipStream_t st, SoA roots, int depth, uint64_t* d_out, i
     uint64_t* leaf_out = lv.size() > 1 ? leaf.val : d_out;
     if (leaf.n > 0) {
         SoA ls{leaf.bb, leaf.meta, leaf.n};
-        if (fide) k_fperft_small<<<grid_for(leaf.n), BLOCK, 0, st>>>(ls, rem, leaf_out);
-        else k_perft_small<<<grid_for(leaf.n), BLOCK, 0, st>>>(ls, rem, leaf_out);
+        static const bool unsorted = getenv("GC_PERFT_UNSORTED") != nullptr;  // A/B switch
+        bool sorted = false;
+        if (!fide && rem >= 2 && leaf.n >= 65536 && !unsorted) {  // subtrees by root move count
+            int32_t *kc = nullptr, *ks = nullptr, *ix = nullptr, *is = nullptr;
+            void* tmp = nullptr;
+            size_t tb = 0;
+            hipError_t he = hipSuccess;
+            if (dalloc(&kc, leaf.n) || dalloc(&ks, leaf.n) || dalloc(&ix, leaf.n) || dalloc(&is, leaf.n)) he = hipErrorOutOfMemory;
+            if (he == hipSuccess) {
+                k_count_children<<<grid_for(leaf.n), BLOCK, 0, st>>>(ls, kc);
+                k_iota<<<grid_for(leaf.n), BLOCK, 0, st>>>(ix, leaf.n);
+                he = hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kc, ks, ix, is, leaf.n, 0, 10, st);
+            }
+            if (he == hipSuccess && dalloc((char**)&tmp, tb) == 0)
+                he = hipcub::DeviceRadixSort::SortPairs(tmp, tb, kc, ks, ix, is, leaf.n, 0, 10, st);
+            if (he == hipSuccess && tmp) {
+                k_perft_small_perm<<<grid_for(leaf.n), BLOCK, 0, st>>>(ls, is, rem, leaf_out);
+                sorted = true;
+                he = hipStreamSynchronize(st);  // before the temporaries are freed
+            }
+            (void)hipFree(tmp); (void)hipFree(kc); (void)hipFree(ks); (void)hipFree(ix); (void)hipFree(is);
+            if (he != hipSuccess) { cleanup(); return fail(std::string("perft sort: ") + hipGetErrorString(he)); }
+        }
+        if (!sorted) {
+            if (fide) k_fperft_small<<<grid_for(leaf.n), BLOCK, 0, st>>>(ls, rem, leaf_out);
+            else k_perft_small<<<grid_for(leaf.n), BLOCK, 0, st>>>(ls, rem, leaf_out);
+        }
     }
     for (int l = (int)lv.size() - 2; l >= 0; l--) {
         uint64_t* dst = l == 0 ? d_out : lv[l].val;

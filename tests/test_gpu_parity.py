@@ -153,6 +153,19 @@ def test_perft_random_positions(engine, oracle):
         assert (got == ref).all(), d
 
 
+def test_perft_sorted_subtrees_vs_oracle(engine, oracle):
+    """perft(4) of 256 mid-game roots: the leaf level (~2e5 depth-2 subtrees) runs in order of
+    the subtree roots' move counts (k_perft_small_perm); totals per root == the oracle's."""
+    from gym_chess_amd.env import BatchedChessEnv
+
+    env = BatchedChessEnv(256, device=0, seed=0x5EED + 4)
+    env.step_random(25)
+    b, m = env.boards()
+    got = engine.perft(b, m, 4)
+    ref = oracle.perft_batch(b, m, 4, threads=16)
+    assert (got == ref).all(), np.nonzero(got != ref)[0][:4]
+
+
 # ------------------------------------------------------------------ env
 def _replay_trace(env, oracle_env, steps):
     """Drive the batched env (1 board) with the recorded actions; compare to the golden."""
