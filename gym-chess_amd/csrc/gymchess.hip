@@ -326,6 +326,29 @@ __global__ void k_expand(SoA in, const int32_t* __restrict__ offs, SoA out) {
     if (g.castles & 1) out.store(o++, child_of(s, g.white, g.white ? A_QSW : A_QSB));
     if (g.castles & 2) out.store(o++, child_of(s, g.white, g.white ? A_KSW : A_KSB));
 }
+// k_expand over the parents a .. a+c-1 of `in` (offs indexed from a): one chunk of a level
+// too large to materialise whole
+__global__ void k_expand_range(SoA in, int a, int c, const int32_t* __restrict__ offs, SoA out) {
+    int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= c) return;
+    Pos s = in.load(a + t);
+    Gen g;
+    gen_init(s, g);
+    int o = offs[t];
+    u64 pcs = g.own;
+    while (pcs) {
+        int sq = ctz(pcs);
+        pcs &= pcs - 1;
+        u64 tg = legal_targets(s, g, sq, type_at(s, sq));
+        while (tg) {
+            int tt = ctz(tg);
+            tg &= tg - 1;
+            out.store(o++, child_of(s, g.white, sq * 64 + tt));
+        }
+    }
+    if (g.castles & 1) out.store(o++, child_of(s, g.white, g.white ? A_QSW : A_QSB));
+    if (g.castles & 2) out.store(o++, child_of(s, g.white, g.white ? A_KSW : A_KSB));
+}
 // parent value = sum of its children's values (children of one parent are contiguous)
 __global__ void k_sum_children(const int32_t* __restrict__ offs, const int32_t* __restrict__ cnt,
                                const uint64_t* __restrict__ child, int n, uint64_t* __restrict__ out) {
@@ -1278,6 +1301,71 @@ extern "C" int gc_engine_update_state(gc_engine* e, int n, const int8_t* boards,
     return 0;
 }
 
+// depth-3 subtrees as depth-2 ones: the level below `leaf` is materialised chunk by chunk
+// (it is ~30x larger) and its nodes run in order of their move counts, so the leaf kernel's
+// one remaining loop has (nearly) equal trip counts across a wave -- with depth-3 subtrees
+// the inner loop's trip count varied per lane (PMC: ~60 % lane utilisation).
+static int perft_split_leaves(hipStream_t st, SoA leaf, uint64_t* leaf_out) {
+    const int64_t cap = (int64_t)1 << 27;  // children per chunk (7.5 GiB of boards)
+    int chunk = 1 << 21;
+    int32_t *kc = nullptr, *offs = nullptr, *kc2 = nullptr, *ks = nullptr, *ix = nullptr, *is = nullptr;
+    u64* cb = nullptr;
+    u32* cm = nullptr;
+    uint64_t* cval = nullptr;
+    void* tmp = nullptr;
+    size_t tmp_bytes = 0;
+    int rc = 0;
+    std::string err;
+    auto done = [&]() {
+        void* ps[] = {kc, offs, kc2, ks, ix, is, cb, cm, cval, tmp};
+        for (void* q : ps) (void)hipFree(q);
+    };
+    if (dalloc(&kc, leaf.n) || dalloc(&offs, chunk) || dalloc(&kc2, cap) || dalloc(&ks, cap) || dalloc(&ix, cap) ||
+        dalloc(&is, cap) || dalloc(&cb, (size_t)NBB * cap) || dalloc(&cm, cap) || dalloc(&cval, cap)) {
+        done();
+        return -1;
+    }
+    {  // scratch for the largest scan and sort of a chunk
+        size_t b1 = 0, b2 = 0;
+        hipError_t he = hipcub::DeviceScan::ExclusiveSum(nullptr, b1, kc, offs, chunk, st);
+        if (he == hipSuccess) he = hipcub::DeviceRadixSort::SortPairs(nullptr, b2, kc2, ks, ix, is, (int)cap, 0, 10, st);
+        tmp_bytes = b1 > b2 ? b1 : b2;
+        if (he != hipSuccess) { done(); return fail(std::string("perft split: ") + hipGetErrorString(he)); }
+        if (dalloc((char**)&tmp, tmp_bytes)) { done(); return -1; }
+    }
+    k_count_children<<<grid_for(leaf.n), BLOCK, 0, st>>>(leaf, kc);
+    for (int a = 0; a < leaf.n && rc == 0;) {
+        int c = leaf.n - a < chunk ? leaf.n - a : chunk;
+        size_t tb = tmp_bytes;
+        hipError_t he = hipcub::DeviceScan::ExclusiveSum(tmp, tb, kc + a, offs, c, st);
+        int32_t lo = 0, lc = 0;
+        if (he == hipSuccess) he = hipMemcpyAsync(&lo, offs + c - 1, 4, hipMemcpyDeviceToHost, st);
+        if (he == hipSuccess) he = hipMemcpyAsync(&lc, kc + a + c - 1, 4, hipMemcpyDeviceToHost, st);
+        if (he == hipSuccess) he = hipStreamSynchronize(st);
+        if (he != hipSuccess) { err = std::string("perft split: ") + hipGetErrorString(he); rc = -1; break; }
+        int64_t total = (int64_t)lo + lc;
+        if (total > cap) { chunk /= 2; continue; }  // an unusually bushy chunk: halve and retry
+        if (total > 0) {
+            SoA ch{cb, cm, (int)total};
+            k_expand_range<<<grid_for(c), BLOCK, 0, st>>>(leaf, a, c, offs, ch);
+            k_count_children<<<grid_for((int)total), BLOCK, 0, st>>>(ch, kc2);
+            k_iota<<<grid_for((int)total), BLOCK, 0, st>>>(ix, (int)total);
+            tb = tmp_bytes;
+            he = hipcub::DeviceRadixSort::SortPairs(tmp, tb, kc2, ks, ix, is, (int)total, 0, 10, st);
+            if (he != hipSuccess) { err = std::string("perft split sort: ") + hipGetErrorString(he); rc = -1; break; }
+            k_perft_small_perm<<<grid_for((int)total), BLOCK, 0, st>>>(ch, is, 2, cval);
+        }
+        k_sum_children<<<grid_for(c), BLOCK, 0, st>>>(offs, kc + a, cval, c, leaf_out + a);
+        he = hipGetLastError();
+        if (he != hipSuccess) { err = std::string("perft split kernels: ") + hipGetErrorString(he); rc = -1; break; }
+        a += c;
+    }
+    hipError_t he = hipStreamSynchronize(st);  // before the buffers are freed
+    if (rc == 0 && he != hipSuccess) { err = std::string("perft split: ") + hipGetErrorString(he); rc = -1; }
+    done();
+    return rc ? fail(err) : 0;
+}
+
 // perft over n roots (side to move = meta[0]).  Levels are expanded on the device while
 // more than 3 plies remain, or while there are too few subtrees to fill the chip.
 static int perft_device(hipStream_t st, SoA roots, int depth, uint64_t* d_out, int fide) {
@@ -1336,7 +1424,12 @@ static int perft_device(hipStream_t st, SoA roots, int depth, uint64_t* d_out, i
         SoA ls{leaf.bb, leaf.meta, leaf.n};
         static const bool unsorted = getenv("GC_PERFT_UNSORTED") != nullptr;  // A/B switch
         bool sorted = false;
-        if (!fide && rem >= 2 && leaf.n >= 65536 && !unsorted) {  // subtrees by root move count
+        const char* sp = getenv("GC_PERFT_SPLIT");  // per call: tests compare both paths
+        if (!fide && rem == 3 && leaf.n >= 65536 && !unsorted && !(sp && sp[0] == '0')) {
+            if (perft_split_leaves(st, ls, leaf_out)) { cleanup(); return -1; }
+            sorted = true;
+        }
+        if (!sorted && !fide && rem >= 2 && leaf.n >= 65536 && !unsorted) {  // subtrees by root move count
             int32_t *kc = nullptr, *ks = nullptr, *ix = nullptr, *is = nullptr;
             void* tmp = nullptr;
             size_t tb = 0;

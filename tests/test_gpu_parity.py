@@ -166,6 +166,26 @@ def test_perft_sorted_subtrees_vs_oracle(engine, oracle):
     assert (got == ref).all(), np.nonzero(got != ref)[0][:4]
 
 
+def test_perft_split_leaves_matches_depth3_subtrees(engine):
+    """perft(5) of 200 mid-game roots: the leaf level split one more ply in chunks
+    (perft_split_leaves, depth-2 subtrees sorted by move count) == the depth-3 subtrees
+    (GC_PERFT_SPLIT=0), per root."""
+    import os
+
+    from gym_chess_amd.env import BatchedChessEnv
+
+    env = BatchedChessEnv(200, device=0, seed=0x5EED + 5)
+    env.step_random(21)
+    b, m = env.boards()
+    split = engine.perft(b, m, 5)
+    os.environ["GC_PERFT_SPLIT"] = "0"
+    try:
+        whole = engine.perft(b, m, 5)
+    finally:
+        del os.environ["GC_PERFT_SPLIT"]
+    assert (split == whole).all() and split.sum() > 200 * 10**6, np.nonzero(split != whole)[0][:4]
+
+
 # ------------------------------------------------------------------ env
 def _replay_trace(env, oracle_env, steps):
     """Drive the batched env (1 board) with the recorded actions; compare to the golden."""
