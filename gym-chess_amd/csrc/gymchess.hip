@@ -288,6 +288,19 @@ __global__ void __launch_bounds__(BLOCK) k_perft_small_perm(SoA in, const int32_
     int j = perm[i];
     nodes[j] = perft_small(in.load(j), depth, sa, sb);
 }
+#ifndef PERFT2_WPE
+#define PERFT2_WPE 4  // 128 VGPRs (a few spilled): 4 waves per SIMD beat 2 by ~9 %
+#endif
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(PERFT2_WPE)))
+k_perft2_perm(SoA in, const int32_t* __restrict__ perm,
+                                                       uint64_t* __restrict__ nodes) {
+    __shared__ u64 lds_a[SCRATCH_SLOTS * BLOCK];
+    LdsScratch sa{lds_a + threadIdx.x};
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= in.n) return;
+    int j = perm[i];
+    nodes[j] = perft2(in.load(j), sa);
+}
 __global__ void k_iota(int32_t* __restrict__ v, int n) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) v[i] = i;
@@ -1353,7 +1366,7 @@ static int perft_split_leaves(hipStream_t st, SoA leaf, uint64_t* leaf_out) {
             tb = tmp_bytes;
             he = hipcub::DeviceRadixSort::SortPairs(tmp, tb, kc2, ks, ix, is, (int)total, 0, 10, st);
             if (he != hipSuccess) { err = std::string("perft split sort: ") + hipGetErrorString(he); rc = -1; break; }
-            k_perft_small_perm<<<grid_for((int)total), BLOCK, 0, st>>>(ch, is, 2, cval);
+            k_perft2_perm<<<grid_for((int)total), BLOCK, 0, st>>>(ch, is, cval);
         }
         k_sum_children<<<grid_for(c), BLOCK, 0, st>>>(offs, kc + a, cval, c, leaf_out + a);
         he = hipGetLastError();
