@@ -17,7 +17,7 @@ GC_HD Pos child_of(const Pos& s, bool white, int action) {
     Pos c = s;
     int rw;
     bool irrev;
-    apply_move(c, white, action, &rw, &irrev);
+    apply_legal(c, white, action, &rw, &irrev);  // a generated (legal) move: the branch-free path
     c.meta = (c.meta & ~(u32)M_RIGHTS) | eff_rights(c);
     return c;
 }
