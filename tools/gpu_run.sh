@@ -20,7 +20,7 @@ for s in ${STEPS:-smoke pytest bench prof}; do
     smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     pytest) step pytest 1200 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread ;;
     bench)  step bench 600 python bench.py ${BENCH_ARGS:-} ;;
-    prof)   step prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 100 --warmup 20 --perft-roots 4096 ;;
+    prof)   step prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --no-cpu-baseline --perft-roots 4096 ;;  # bench defaults: the same launches bench.py times
     pmcf)   step pmcf 600 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 20 --warmup 400 --fused-plies 0 --perft-roots 0 ;;
     pmcw)   step pmcw 600 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 20 --warmup 400 --fused-plies 0 --perft-roots 0 ;;
     pmcv)   step pmcv 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU -d $OUT/pmc_valu -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 20 --warmup 400 --fused-plies 0 --perft-roots 0 ;;
