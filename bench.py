@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--cpu-sample-plies", type=int, default=300)
     ap.add_argument("--fused-plies", type=int, default=200, help="also time the fused rollout kernel (0 = skip)")
     ap.add_argument("--perft-roots", type=int, default=65536, help="perft leg on mid-game FEN roots (0 = skip)")
+    ap.add_argument("--variant-steps", type=int, default=300,
+                    help="also time step() with opponent='random' and with rules='fide' (SURVEY 8f rows 2, 4; 0 = skip)")
     ap.add_argument("--perft-depth", type=int, default=5)
     ap.add_argument("--cpu-perft-roots", type=int, default=256)
     ap.add_argument("--cpu-perft-depth", type=int, default=4)
@@ -146,6 +148,29 @@ def perft_leg(args, rep, device):
     return out
 
 
+def variant_legs(args, rep, n):
+    """step() throughput of the SURVEY 8f variants at the same batch: the in-kernel random
+    opponent (one step = the agent's ply + the opponent's reply, k_env_step<true, true>) and
+    FIDE rules (k_fenv_step).  Same timing discipline as the main line, fewer steps."""
+    from gym_chess_amd.env import BatchedChessEnv
+
+    out = {}
+    for name, kw in (("opponent_random", dict(opponent="random")), ("rules_fide", dict(rules="fide"))):
+        env = BatchedChessEnv(n, device=rep.local_rank, seed=rep.board_seed(args.seed + 7), **kw)
+        env.step_random(args.warmup)
+        env.synchronize()
+        s0 = int(env.outputs()["nsteps"].sum())
+        rep.barrier()
+        t0 = time.perf_counter()
+        env.step_random(args.variant_steps)
+        env.synchronize()
+        dt = rep.max(time.perf_counter() - t0)
+        s1 = int(env.outputs()["nsteps"].sum())
+        env.close()
+        out[name] = {"value": rep.sum(s1 - s0) / dt, "unit": "env_steps/s", "steps": args.variant_steps}
+    return out
+
+
 def main():
     args = parse()
     from gym_chess_amd.env import BatchedChessEnv
@@ -205,6 +230,8 @@ def main():
         extra["fused_rollout"] = {"value": fsteps / fdt, "unit": "env_steps/s", "plies_per_launch": args.fused_plies,
                                   "kernel_ms": env.elapsed_ms(2, 3)}
     env.close()
+    if args.variant_steps > 0:
+        extra["variants"] = variant_legs(args, rep, n)
     if args.perft_roots > 0:
         extra["perft"] = perft_leg(args, rep, rep.local_rank)
 

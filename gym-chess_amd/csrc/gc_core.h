@@ -614,25 +614,53 @@ GC_HD void moveset_clear(MoveSet& ms) {
     ms.big = false;
 }
 
+// Rules = FIDE (gc_fide.h) reuses this generator with F = true: no king captures, the double
+// step needs both squares empty, en passant for the pawns in ep_from (legality decided by
+// fide::fgen).  Promotions are generated once per target (perft multiplies, gc_fide.h).
+struct FideExtra {
+    u64 ep_from;  // own pawns with a legal en-passant capture onto ep
+    int ep;       // en-passant target square, or -1
+};
+GC_HD u64 fide_pawn_targets(const Pos& s, const Gen& g, int sq, const FideExtra& fx) {
+    u64 m = bit(sq), empty = ~g.occ, notown = ~g.own & ~(s.k & g.opp);
+    u64 one = g.white ? ((m >> 8) & empty) : ((m << 8) & empty);
+    u64 two = g.white ? (((one & (0xFFull << 40)) >> 8) & empty) : (((one & (0xFFull << 16)) << 8) & empty);
+    u64 tg = (one | two | (pawn_att_set(m, g.white) & g.opp)) & notown;
+    if (g.ks >= 0) {
+        tg &= g.checkmask;
+        if (g.pinned & m) tg &= g.pinrays & line_through(g.ks, sq);
+    }
+    if (fx.ep_from & m) tg |= bit(fx.ep);
+    return tg;
+}
+
 // Part A of the generation: pawns (set-wise), knights, kings, queens.  `ms` cleared; ORs
 // into ms.cnt; returns the number of moves found.  (The split A | B balances the two waves
 // of the paired step kernel: queens cost a bishop plus a rook.)
-template <class S>
-GC_HD int gen_moves_a(const Pos& s, const Gen& g, MoveSet& ms, S& scr) {
-    const u64 own = g.own, cm = g.checkmask, notown_cm = ~own & cm;
+template <class S, bool F = false>
+GC_HD int gen_moves_a(const Pos& s, const Gen& g, MoveSet& ms, S& scr, const FideExtra& fx = FideExtra{0, -1}) {
+    const u64 own = g.own, cm = g.checkmask, nocap = F ? ~(s.k & g.opp) : ~0ull;  // FIDE: no king captures
+    const u64 notown_cm = ~own & cm & nocap, opp = g.opp & nocap;
     int total = 0;
     // pawns, set-wise (lib.rs:935-958; Q1: the double push tests only the destination)
     u64 P = s.p & own, fp = P & ~g.pinned, empty = ~g.occ;
     if (g.white) {
         ms.o1 = ((fp >> 8) & empty & cm) << 8;
-        ms.o2 = (((fp & ROW6) >> 16) & empty & cm) << 16;
-        ms.ol = (((fp >> 7) & ~FILE_A) & g.opp & cm) << 7;
-        ms.orr = (((fp >> 9) & ~FILE_H) & g.opp & cm) << 9;
+        ms.o2 = F ? ((((((fp & ROW6) >> 8) & empty) >> 8) & empty & cm) << 16)
+                  : ((((fp & ROW6) >> 16) & empty & cm) << 16);
+        ms.ol = (((fp >> 7) & ~FILE_A) & opp & cm) << 7;
+        ms.orr = (((fp >> 9) & ~FILE_H) & opp & cm) << 9;
     } else {
         ms.o1 = ((fp << 8) & empty & cm) >> 8;
-        ms.o2 = (((fp & ROW1) << 16) & empty & cm) >> 16;
-        ms.ol = (((fp << 9) & ~FILE_A) & g.opp & cm) >> 9;
-        ms.orr = (((fp << 7) & ~FILE_H) & g.opp & cm) >> 7;
+        ms.o2 = F ? ((((((fp & ROW1) << 8) & empty) << 8) & empty & cm) >> 16)
+                  : ((((fp & ROW1) << 16) & empty & cm) >> 16);
+        ms.ol = (((fp << 9) & ~FILE_A) & opp & cm) >> 9;
+        ms.orr = (((fp << 7) & ~FILE_H) & opp & cm) >> 7;
+    }
+    if (F && fx.ep >= 0) {  // en passant (legal by construction: fide::fgen)
+        u64 epb = bit(fx.ep), ef = fx.ep_from & fp;
+        ms.ol |= ef & (g.white ? ((epb & ~FILE_A) << 7) : ((epb & ~FILE_A) >> 9));
+        ms.orr |= ef & (g.white ? ((epb & ~FILE_H) << 9) : ((epb & ~FILE_H) >> 7));
     }
     ms.fastp = fp;
     total += popc(ms.o1) + popc(ms.o2) + popc(ms.ol) + popc(ms.orr);
@@ -647,7 +675,7 @@ GC_HD int gen_moves_a(const Pos& s, const Gen& g, MoveSet& ms, S& scr) {
     while (pp) {
         int sq = ctz(pp);
         pp ^= bit(sq);
-        park(ms, scr, own, sq, legal_targets(s, g, sq, PAWN), total);
+        park(ms, scr, own, sq, F ? fide_pawn_targets(s, g, sq, fx) : legal_targets(s, g, sq, PAWN), total);
     }
     u64 x = s.n & own;  // a pinned knight never has a move on its pin segment
     while (x) {
@@ -659,7 +687,7 @@ GC_HD int gen_moves_a(const Pos& s, const Gen& g, MoveSet& ms, S& scr) {
     while (x) {
         int sq = ctz(x);
         x ^= bit(sq);
-        park(ms, scr, own, sq, king_set(bit(sq)) & ~own & ~g.enemy_att, total);
+        park(ms, scr, own, sq, king_set(bit(sq)) & ~own & ~g.enemy_att & nocap, total);
     }
     x = s.q & own;
     while (x) {
@@ -673,9 +701,9 @@ GC_HD int gen_moves_a(const Pos& s, const Gen& g, MoveSet& ms, S& scr) {
 }
 
 // Part B: bishops and rooks.  ORs into ms.cnt; returns the number of moves found.
-template <class S>
+template <class S, bool F = false>
 GC_HD int gen_moves_b(const Pos& s, const Gen& g, MoveSet& ms, S& scr) {
-    const u64 own = g.own, notown_cm = ~own & g.checkmask;
+    const u64 own = g.own, notown_cm = ~own & g.checkmask & (F ? ~(s.k & g.opp) : ~0ull);
     int total = 0;
     u64 x = s.b & own;
     while (x) {

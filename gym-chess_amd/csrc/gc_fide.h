@@ -122,8 +122,23 @@ GC_HD u64 ftargets(const Pos& s, const FGen& f, int sq, int t) {
 
 GC_HD u64 promo_row(bool white) { return white ? ROW0 : ROW7; }
 
-// number of legal moves, promotions counted once (env actions) or four times (perft)
-GC_HD int fcount(const Pos& s, const FGen& f, bool perft) {
+// The shared type-uniform generator (gc_core.h gen_moves_a/b with F = true: pawns set-wise,
+// one loop per piece type, targets parked per ordinal, bit-sliced count planes) for FIDE
+// positions with at most SCRATCH_SLOTS own pieces; the per-square walk below serves the rest.
+template <class S>
+GC_HD void fgen_moves(const Pos& s, const FGen& f, MoveSet& ms, S& scr) {
+    moveset_clear(ms);
+    FideExtra fx{f.ep_from, f.ep};
+    int total = popc(f.g.castles);
+    total += gen_moves_a<S, true>(s, f.g, ms, scr, fx);
+    total += gen_moves_b<S, true>(s, f.g, ms, scr);
+    ms.total = total;
+}
+GC_HD bool fuses_walk(const FGen& f) { return popc(f.g.own) > SCRATCH_SLOTS; }
+
+// number of legal moves, promotions counted once (env actions) or four times (perft):
+// per-square walk (> SCRATCH_SLOTS own pieces)
+GC_HD int fcount_walk(const Pos& s, const FGen& f, bool perft) {
     int n = popc(f.g.castles);
     u64 pcs = f.g.own;
     while (pcs) {
@@ -133,6 +148,27 @@ GC_HD int fcount(const Pos& s, const FGen& f, bool perft) {
         u64 tg = ftargets(s, f, sq, t);
         n += popc(tg);
         if (perft && t == PAWN) n += 3 * popc(tg & promo_row(f.g.white));
+    }
+    return n;
+}
+
+// the same count through the shared generator
+GC_HD int fcount(const Pos& s, const FGen& f, bool perft) {
+    if (fuses_walk(f)) return fcount_walk(s, f, perft);
+    MoveSet ms;
+    NoScratch none;
+    fgen_moves(s, f, ms, none);
+    int n = ms.total;
+    if (perft) {  // three more per promoting move (the origins on the last-but-one rank)
+        u64 pre = f.g.white ? (0xFFull << 8) : (0xFFull << 48);
+        n += 3 * (popc(ms.o1 & pre) + popc(ms.ol & pre) + popc(ms.orr & pre));  // per move, not per pawn
+        FideExtra fx{f.ep_from, f.ep};
+        u64 pp = s.p & f.g.own & f.g.pinned & pre;
+        while (pp) {
+            int sq = ctz(pp);
+            pp &= pp - 1;
+            n += 3 * popc(fide_pawn_targets(s, f.g, sq, fx) & promo_row(f.g.white));
+        }
     }
     return n;
 }
@@ -153,6 +189,22 @@ GC_HD int fselect(const Pos& s, const FGen& f, int k) {
     if (f.g.castles & 2) { if (k == 0) return w ? A_KSW : A_KSB; k--; }
     if (f.g.castles & 1) { if (k == 0) return w ? A_QSW : A_QSB; }
     return A_NONE;
+}
+
+// the random policy's pick for the side to move of s (fgen'd into f): draws k uniformly in
+// [0, #legal) from the Philox stream (board, draw++) and returns the k-th legal action in
+// action-id order -- through the count-plane search when the shared generator applies
+template <class S>
+GC_HD int fpick_action(const Pos& s, const FGen& f, S& scr, uint64_t seed, u32 board, u32& draw) {
+    if (fuses_walk(f)) {
+        int n = fcount_walk(s, f, false);
+        if (n == 0) return A_NONE;
+        return fselect(s, f, (int)policy_index(seed, board, draw++, (u32)n));
+    }
+    MoveSet ms;
+    fgen_moves(s, f, ms, scr);
+    if (ms.total == 0) return A_NONE;
+    return select_action(s, f.g, ms, scr, (int)policy_index(seed, board, draw++, (u32)ms.total));
 }
 
 GC_HD bool faction_legal(const Pos& s, const FGen& f, int action) {

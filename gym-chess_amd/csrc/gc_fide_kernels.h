@@ -160,11 +160,9 @@ __global__ void k_fperft_small(SoA in, int depth, uint64_t* __restrict__ nodes) 
 }
 
 // ---- env (opponent "none"): one lane = one board, per-square policy pick ------------------
-__device__ uint16_t fpick(const Pos& s, const gcf::FGen& f, uint64_t seed, int i, u32& draw) {
-    int n = gcf::fcount(s, f, false);
-    if (n == 0) return (uint16_t)A_NONE;
-    u32 k = policy_index(seed, (u32)i, draw++, (u32)n);
-    return (uint16_t)gcf::fselect(s, f, (int)k);
+template <class S>
+__device__ uint16_t fpick(const Pos& s, const gcf::FGen& f, S& scr, uint64_t seed, int i, u32& draw) {
+    return (uint16_t)gcf::fpick_action(s, f, scr, seed, (u32)i, draw);
 }
 
 __device__ Pos fide_reset_pos(const EnvDev& e) {
@@ -178,6 +176,7 @@ __device__ Pos fide_reset_pos(const EnvDev& e) {
 // driver (act[i] = this state's policy pick; A_NONE or done -> reset; pick the next action)
 template <bool POLICY>
 __global__ void __launch_bounds__(BLOCK) k_fenv_step(EnvDev e) {
+    LDS_SCRATCH_DECL;
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= e.n) return;
     Pos s = e.st.load(i);
@@ -203,7 +202,7 @@ __global__ void __launch_bounds__(BLOCK) k_fenv_step(EnvDev e) {
     }
     if (POLICY) {
         if (!have) gcf::fgen(s, f);
-        e.act[i] = fpick(s, f, e.seed, i, d);
+        e.act[i] = fpick(s, f, scr, e.seed, i, d);
         e.draw[i] = d;
     }
     h.commit();
@@ -216,6 +215,7 @@ __global__ void __launch_bounds__(BLOCK) k_fenv_step(EnvDev e) {
 }
 
 __global__ void __launch_bounds__(BLOCK) k_fenv_reset(EnvDev e, const uint8_t* __restrict__ mask, int select) {
+    LDS_SCRATCH_DECL;
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= e.n) return;
     if (mask && !mask[i]) return;
@@ -225,20 +225,21 @@ __global__ void __launch_bounds__(BLOCK) k_fenv_reset(EnvDev e, const uint8_t* _
         gcf::FGen f;
         gcf::fgen(s, f);
         u32 d = e.draw[i];
-        e.act[i] = fpick(s, f, e.seed, i, d);
+        e.act[i] = fpick(s, f, scr, e.seed, i, d);
         e.draw[i] = d;
     }
     e.st.store(i, s);
 }
 
 __global__ void __launch_bounds__(BLOCK) k_fenv_select(EnvDev e) {
+    LDS_SCRATCH_DECL;
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= e.n) return;
     Pos s = e.st.load(i);
     gcf::FGen f;
     gcf::fgen(s, f);
     u32 d = e.draw[i];
-    e.act[i] = fpick(s, f, e.seed, i, d);
+    e.act[i] = fpick(s, f, scr, e.seed, i, d);
     e.draw[i] = d;
 }
 

@@ -371,6 +371,50 @@ static uint64_t fide_perft_rec(const Pos& s, int depth) {
     return n;
 }
 
+// the shared generator (fcount) against the per-square walk (fcount_walk) at every node of a
+// FIDE perft tree; on the first difference the node is exported to (ob, om) and 1 returned
+static int fide_cmp_rec(const Pos& s, int depth, int8_t* ob, uint8_t* om, int* counts) {
+    fide::FGen f;
+    fide::fgen(s, f);
+    int a = fide::fcount(s, f, true), w = fide::fcount_walk(s, f, true);
+    if (a != w) {
+        to_mailbox(s, ob);
+        for (int k = 0; k < 8; k++) om[k] = 0;
+        om[0] = (s.meta & M_WHITE) != 0;
+        counts[0] = a;
+        counts[1] = w;
+        counts[2] = fide::ep_square(s.meta);
+        return 1;
+    }
+    if (depth <= 1) return 0;
+    int rw;
+    bool irr;
+    u64 pcs = f.g.own;
+    while (pcs) {
+        int sq = ctz(pcs);
+        pcs &= pcs - 1;
+        int t = type_at(s, sq);
+        u64 tg = fide::ftargets(s, f, sq, t);
+        while (tg) {
+            int to = ctz(tg);
+            tg &= tg - 1;
+            Pos c = s;
+            fide::fapply(c, sq * 64 + to, (t == PAWN && (bit(to) & fide::promo_row(f.g.white))) ? QUEEN : 0, &rw, &irr);
+            if (fide_cmp_rec(c, depth - 1, ob, om, counts)) return 1;
+        }
+    }
+    for (int cb = 0; cb < 2; cb++) {
+        if (!(f.g.castles & (1u << cb))) continue;
+        Pos c = s;
+        fide::fapply(c, cb ? (f.g.white ? A_KSW : A_KSB) : (f.g.white ? A_QSW : A_QSB), 0, &rw, &irr);
+        if (fide_cmp_rec(c, depth - 1, ob, om, counts)) return 1;
+    }
+    return 0;
+}
+extern "C" int host_fide_gen_check(const int8_t* b, const uint8_t* m, int depth, int8_t* ob, uint8_t* om, int* counts) {
+    return fide_cmp_rec(fide_import(b, m), depth, ob, om, counts);
+}
+
 extern "C" uint64_t host_fide_perft(const int8_t* b, const uint8_t* m, int depth) {
     return fide_perft_rec(fide_import(b, m), depth);
 }
@@ -412,13 +456,11 @@ extern "C" void host_fide_rollout(const int8_t* init, uint64_t seed, uint32_t bo
     h.bump_gen();  // zeroed entries are of generation 0: dead
     Pos s = reset();
     u32 draw = 0;
+    HostScratch scr;
     auto pick = [&](const Pos& p) {
         fide::FGen f;
         fide::fgen(p, f);
-        int n = fide::fcount(p, f, false);
-        if (n == 0) return (int)A_NONE;
-        u32 k = policy_index(seed, board, draw++, (u32)n);
-        return fide::fselect(p, f, (int)k);
+        return fide::fpick_action(p, f, scr, seed, board, draw);
     };
     int a = pick(s);
     for (int p = 0; p < plies; p++) {

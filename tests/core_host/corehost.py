@@ -60,6 +60,7 @@ def lib():
         L.host_env_moves.argtypes = [P, P, ctypes.c_int]
         L.host_fide_perft.restype = ctypes.c_uint64
         L.host_fide_perft.argtypes = [P, P, ctypes.c_int]
+        L.host_fide_gen_check.argtypes = [P, P, ctypes.c_int, P, P, P]
         L.host_fide_list.argtypes = [P, P, P, ctypes.c_int]
         L.host_fide_rollout.argtypes = [P, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, P, P, P, P]
         _L = L
@@ -216,3 +217,16 @@ def mover_checked(board, meta, action):
     b, m = _bm(board, meta)
     r = lib().host_mover_checked(_p(b), _p(m), int(action))
     return bool(r & 1), bool(r & 2)
+
+
+def fide_gen_check(board, meta, depth):
+    """None if the shared generator and the per-square walk agree at every node of the FIDE
+    perft tree to `depth`; else (board, white, shared count, walk count, ep square) of the first
+    node where they differ"""
+    b, m = _bm(board, meta)
+    ob = np.zeros(64, dtype=np.int8)
+    om = np.zeros(8, dtype=np.uint8)
+    c = np.zeros(3, dtype=np.int32)
+    if lib().host_fide_gen_check(_p(b), _p(m), int(depth), _p(ob), _p(om), _p(c)) == 0:
+        return None
+    return ob, int(om[0]), int(c[0]), int(c[1]), int(c[2])

@@ -72,6 +72,18 @@ def test_fide_perft_host(fen, depth, nodes):
     assert H.fide_perft(b, m, depth) == nodes
 
 
+@pytest.mark.parametrize("fen", [f for f, _ in STANDARD] + [f for f, *_ in EDGE])
+def test_fide_shared_generator_matches_walk(fen):
+    """The shared type-uniform generator (gc_core gen_moves_a/b, F = true: what the env pick
+    and the perft leaf counts use) == the per-square walk (ftargets) at every node of the
+    position's tree to depth 3, promotions x4 included."""
+    import numpy as np
+
+    b, m = fide_arrays(fen)
+    r = H.fide_gen_check(np.asarray(b).reshape(64), np.asarray(m).reshape(8), 3)
+    assert r is None, (fen, r[1:], r[0].reshape(8, 8).tolist())
+
+
 def test_fide_fen_en_passant_field():
     from gym_chess_amd import _lib
     from gym_chess_amd.fen import arrays_to_fen, fen_to_arrays
