@@ -4,15 +4,21 @@
 Workload (BASELINE.json configs[2], the config the metric is quoted on): 65 536 boards per
 GPU, random-policy self-play to terminal with auto-reset -- the reference's benchmark
 driver (/root/reference/gym_chess/test/v2/test_benchmark.py:9-43) vectorised.  One "step"
-= one env.step() on every board = one launch of the one-ply step kernel
-k_env_step2 (two waves per 64 boards): the policy's action through the full chess_v2.py step bookkeeping
+= one env.step() on every board = one launch of the one-ply step kernel k_env_step2 (two
+waves per 64 boards): the policy's action through the full chess_v2.py step bookkeeping
 (next_state, update_state, 3-fold on the pre-move board, move cap, mate bonus), the
 opponent's legal move list, the Philox pick of the next action, reset of finished boards.
 State, repetition windows and outputs stay in HBM; nothing crosses PCIe in the timed region.
 
+The batch is first settled into steady state (a fused rollout of --settle plies, then
+--warmup single-ply launches), so the timed launches see mid/late-game boards, resets and
+terminals in their steady-state proportions, whatever --warmup is.
+
   python bench.py [--gpus N --steps K --warmup W --boards B]
-  multi-GPU: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
-  (one process per GPU, boards sharded, no data-path collective: "scaling": "weak")
+      N replicas in ONE process: one host thread + one env handle per device (no torch)
+  python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+      one process per GPU; barrier / max / sum through a file group (gym_chess_amd.replicas)
+  (boards sharded, no data-path collective: "scaling": "weak")
 
 Prints ONE JSON line (rank 0).
 """
@@ -36,12 +42,18 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip-level parameters (8.0 TB/s spe
 #   3-fold window: 64-B entry write (reversible plies; counted always)   64
 ALG_BYTES_PER_BOARD = 120 + 4 + 24 + 6 + 64 + 64
 
+# the PMC profile the traffic / VALU figures come from (rocprofv3 passes, tools/pmc_*.sh);
+# counters cannot be read from inside this process
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic_latest.json")
+
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None, help="replicas (GPUs); default 1, or WORLD_SIZE under a launcher")
     ap.add_argument("--steps", type=int, default=1000)
-    ap.add_argument("--warmup", type=int, default=400)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--settle", type=int, default=1000,
+                    help="fused-rollout plies before --warmup: moves the batch from all-startpos into steady state")
     ap.add_argument("--boards", type=int, default=65536)
     ap.add_argument("--seed", type=int, default=0x5EED + 3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -52,8 +64,8 @@ def parse():
     ap.add_argument("--variant-steps", type=int, default=300,
                     help="also time step() with opponent='random' and with rules='fide' (SURVEY 8f rows 2, 4; 0 = skip)")
     ap.add_argument("--perft-depth", type=int, default=5)
-    ap.add_argument("--cpu-perft-roots", type=int, default=256)
-    ap.add_argument("--cpu-perft-depth", type=int, default=4)
+    ap.add_argument("--oracle-perft-roots", type=int, default=8,
+                    help="roots of the perft leg checked against the oracle at --perft-depth (also its CPU baseline)")
     return ap.parse_args()
 
 
@@ -103,71 +115,99 @@ def midgame_fens(n, seed, device):
     return [arrays_to_fen(b[i], m[i]) for i in range(n)]
 
 
-def perft_leg(args, rep, device):
-    """configs[3]: mid-game FEN roots, perft(depth) through the engine C-ABI
-    (gc_engine_perft: device level expansion + per-lane depth<=3 subtrees)."""
+def perft_leg(args, rep):
+    """configs[3]: mid-game FEN roots, perft(depth) through the engine C-ABI (device level
+    expansion, then the split leaf pass: depth-3 subtrees split to sorted depth-2 ones).  The
+    first --oracle-perft-roots roots of replica 0 are recomputed by the oracle at the same
+    depth and must match exactly; at N=1 that run is also the perft CPU baseline."""
     import numpy as np
 
-    from gym_chess_amd.engine import Engine
+    from gym_chess_amd.engine import Engine, perft_path_counts
     from gym_chess_amd.fen import fen_to_arrays
 
-    fens = midgame_fens(args.perft_roots, rep.board_seed(0x5EED + 4), device)
-    arr = [fen_to_arrays(f) for f in fens]
-    b = np.stack([a[0] for a in arr])
-    m = np.stack([a[1] for a in arr])
-    eng = Engine(device)
-    b, m = eng.update_state(b, m)  # FEN carries no check flags: update_state, as chess_v2.py:204 does
-    eng.perft(b[:256], m[:256], 2)  # load the perft kernels outside the timed region
-    rep.barrier()
-    t0 = time.perf_counter()
-    nodes = eng.perft(b, m, args.perft_depth)
-    dt = time.perf_counter() - t0
-    eng.close()
-    tot = rep.sum(float(nodes.sum()))
-    dtm = rep.max(dt)
+    def prep(rp):
+        fens = midgame_fens(args.perft_roots, rp.board_seed(0x5EED + 4), rp.device)
+        arr = [fen_to_arrays(f) for f in fens]
+        b = np.stack([a[0] for a in arr])
+        m = np.stack([a[1] for a in arr])
+        eng = Engine(rp.device)
+        b, m = eng.update_state(b, m)  # FEN carries no check flags: update_state, as chess_v2.py:204 does
+        eng.perft(b[:256], m[:256], 2)  # load the perft kernels outside the timed region
+        return eng, b, m
+
+    ctx = rep.run(prep)
+    paths0 = perft_path_counts()
+
+    def run(rp):
+        eng, b, m = ctx[rep.local.index(rp)]
+        t0 = time.perf_counter()
+        nodes = eng.perft(b, m, args.perft_depth)
+        return nodes, time.perf_counter() - t0
+
+    res, dtm = rep.timed(run)
+    paths1 = perft_path_counts()
+    for eng, _, _ in ctx:
+        eng.close()
+    tot = rep.sum(float(sum(float(r.sum()) for r in res)))
+    b, m = ctx[0][1], ctx[0][2]
     castle = int((m[:, 1:5] != 0).any(axis=1).sum())
     prom = int(((b[:, 8:16] == 6) | (b[:, 48:56] == -6)).any(axis=1).sum())
     check = int((m[:, 5:7] != 0).any(axis=1).sum())
     out = {"value": tot / dtm, "unit": "perft_nodes/s", "roots_per_gpu": args.perft_roots, "depth": args.perft_depth,
            "nodes": tot, "seconds": dtm,
+           "leaf_pass": {k: paths1[k] - paths0[k] for k in paths0},
            "roots_with": {"castle_right": castle, "pawn_on_7th": prom, "side_in_check": check}}
-    if rep.rank == 0 and rep.world_size == 1 and not args.no_cpu_baseline and args.cpu_perft_roots > 0:
+    k = min(args.oracle_perft_roots, args.perft_roots)
+    if rep.rank == 0 and k > 0:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle as O
 
-        k, d = args.cpu_perft_roots, args.cpu_perft_depth
         threads = max(1, min(16, os.cpu_count() or 1))
         t0 = time.perf_counter()
-        cn = O.perft_batch(b[:k], m[:k], d, threads=threads)
+        cn = O.perft_by_children(b[:k], m[:k], args.perft_depth, threads=threads)
         cdt = time.perf_counter() - t0
-        if d == args.perft_depth:
-            assert (cn == nodes[:k]).all(), "oracle perft disagrees with the device"
-        out["cpu_baseline"] = {"value": float(cn.sum()) / cdt, "unit": "perft_nodes/s", "cores": threads,
-                               "kind": "port", "sample": f"first {k} roots x perft({d}) ({int(cn.sum())} nodes, "
-                               f"{cdt:.1f} s) with the C oracle"}
+        mism = np.nonzero(cn != res[0][:k])[0]
+        assert len(mism) == 0, f"oracle perft({args.perft_depth}) disagrees with the device at roots {mism[:8]}"
+        out["oracle_checked_roots"] = int(k)
+        out["oracle_checked_nodes"] = int(cn.sum())
+        if rep.world_size == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = {"value": float(cn.sum()) / cdt, "unit": "perft_nodes/s", "cores": threads,
+                                   "kind": "port",
+                                   "sample": f"first {k} roots x perft({args.perft_depth}) ({int(cn.sum())} nodes, "
+                                   f"{cdt:.1f} s) with the C oracle (children handed out across threads)"}
     return out
 
 
 def variant_legs(args, rep, n):
     """step() throughput of the SURVEY 8f variants at the same batch: the in-kernel random
-    opponent (one step = the agent's ply + the opponent's reply, k_env_step<true, true>) and
-    FIDE rules (k_fenv_step).  Same timing discipline as the main line, fewer steps."""
+    opponent (one step = the agent's ply + the opponent's reply) and FIDE rules.  Same timing
+    discipline as the main line, fewer steps."""
     from gym_chess_amd.env import BatchedChessEnv
 
     out = {}
     for name, kw in (("opponent_random", dict(opponent="random")), ("rules_fide", dict(rules="fide"))):
-        env = BatchedChessEnv(n, device=rep.local_rank, seed=rep.board_seed(args.seed + 7), **kw)
-        env.step_random(args.warmup)
-        env.synchronize()
-        s0 = int(env.outputs()["nsteps"].sum())
-        rep.barrier()
-        t0 = time.perf_counter()
-        env.step_random(args.variant_steps)
-        env.synchronize()
-        dt = rep.max(time.perf_counter() - t0)
-        s1 = int(env.outputs()["nsteps"].sum())
-        env.close()
-        out[name] = {"value": rep.sum(s1 - s0) / dt, "unit": "env_steps/s", "steps": args.variant_steps}
+        def setup(rp):
+            env = BatchedChessEnv(n, device=rp.device, seed=rp.board_seed(args.seed + 7), **kw)
+            env.step_random(max(args.warmup, 200))
+            env.synchronize()
+            return env
+
+        envs = rep.run(setup)
+        s0 = [int(e.outputs()["nsteps"].sum()) for e in envs]
+
+        def run(rp):
+            env = envs[rep.local.index(rp)]
+            t0 = time.perf_counter()
+            env.step_random(args.variant_steps)
+            env.synchronize()
+            return None, time.perf_counter() - t0
+
+        _, dt = rep.timed(run)
+        s1 = [int(e.outputs()["nsteps"].sum()) for e in envs]
+        for e in envs:
+            e.close()
+        out[name] = {"value": rep.sum(sum(b - a for a, b in zip(s0, s1))) / dt, "unit": "env_steps/s",
+                     "steps": args.variant_steps}
     return out
 
 
@@ -176,64 +216,81 @@ def main():
     from gym_chess_amd.env import BatchedChessEnv
     from gym_chess_amd.replicas import Replicas
 
-    rep = Replicas().init()
+    devs = os.environ.get("GC_BENCH_DEVICES")  # replica -> device map (tests: several replicas on one GPU)
+    rep = Replicas(gpus=args.gpus, devices=[int(d) for d in devs.split(",")] if devs else None).init()
     n = args.boards
-    env = BatchedChessEnv(n, device=rep.local_rank, seed=rep.board_seed(args.seed))
-    # warmup: moves the batch from the all-startpos state into steady-state play
-    env.step_random(args.warmup)
-    env.synchronize()
-    s0 = int(env.outputs()["nsteps"].sum())
-    w0 = env.window_sum()
-    rep.barrier()
-    env.synchronize()
-    t0 = time.perf_counter()
-    env.record_event(0)
-    env.step_random(args.steps)
-    env.record_event(1)
-    env.synchronize()
-    t1 = time.perf_counter()
-    rep.barrier()
-    dt_max = rep.max(t1 - t0)
-    kern_ms = env.elapsed_ms(0, 1)
-    s1 = int(env.outputs()["nsteps"].sum())
-    w1 = env.window_sum()
-    steps_all = rep.sum(s1 - s0)
-    value = steps_all / dt_max
 
-    # roofline of the dominant kernel (k_env_step2, the paired one-ply step), per launch, HIP events on its stream
+    def setup(rp):
+        env = BatchedChessEnv(n, device=rp.device, seed=rp.board_seed(args.seed))
+        if args.settle > 0:  # into steady state: mid/late-game boards, resets, terminals
+            env.rollout(args.settle)
+        env.step_random(args.warmup)
+        env.synchronize()
+        return env, int(env.outputs()["nsteps"].sum()), env.window_sum()
+
+    ctx = rep.run(setup)
+    envs = [c[0] for c in ctx]
+
+    def step(rp):
+        env = envs[rep.local.index(rp)]
+        env.synchronize()
+        t0 = time.perf_counter()
+        env.record_event(0)
+        env.step_random(args.steps)
+        env.record_event(1)
+        env.synchronize()
+        return None, time.perf_counter() - t0
+
+    _, dt_max = rep.timed(step)
+    kern_ms = [e.elapsed_ms(0, 1) for e in envs]
+    s1 = [int(e.outputs()["nsteps"].sum()) for e in envs]
+    w1 = [e.window_sum() for e in envs]
+    steps_all = rep.sum(sum(b - c[1] for c, b in zip(ctx, s1)))
+    value = steps_all / dt_max
+    mean_window = sum(c[2] + w for c, w in zip(ctx, w1)) / (2.0 * n * len(envs))
+
+    # roofline of the dominant kernel (k_env_step2, the paired one-ply step), per launch, from
+    # HIP events on the stream it is launched on (mean over this process's replicas)
     bytes_per_launch = n * ALG_BYTES_PER_BOARD
-    avg_launch_s = kern_ms / 1e3 / args.steps
+    avg_launch_s = sum(kern_ms) / len(kern_ms) / 1e3 / args.steps
     achieved = bytes_per_launch / avg_launch_s / 1e9
-    traffic = valu = None
-    tf = os.path.join(ROOT, "profiles", "pmc_traffic_latest.json")
-    if os.path.exists(tf):
+    traffic = valu = pmc_src = None
+    if os.path.exists(PMC_FILE):
         try:
-            pmc = json.load(open(tf))
+            pmc = json.load(open(PMC_FILE))
             traffic = pmc.get("bytes_per_launch")
             valu = pmc.get("valu")
-        except Exception:
-            traffic = valu = None
+            pmc_src = {"file": os.path.relpath(PMC_FILE, ROOT), "profile": pmc.get("profile"),
+                       "mean_window": pmc.get("mean_window"), "boards": pmc.get("boards"),
+                       "note": "rocprofv3 PMC passes of the same bench command (not this process); "
+                               "traffic = FETCH_SIZE x2 + WRITE_SIZE per launch"}
+        except (OSError, ValueError):
+            traffic = valu = pmc_src = None
 
     extra = {}
     if args.fused_plies > 0:
-        env.rollout(1)  # load the rollout kernel: a first launch would time code-object loading
-        env.synchronize()
-        rep.barrier()
-        f0 = time.perf_counter()
-        env.record_event(2)
-        st, _ = env.rollout(args.fused_plies)
-        env.record_event(3)
-        env.synchronize()
-        f1 = time.perf_counter()
-        fsteps = rep.sum(float(st[0]))
-        fdt = rep.max(f1 - f0)
-        extra["fused_rollout"] = {"value": fsteps / fdt, "unit": "env_steps/s", "plies_per_launch": args.fused_plies,
-                                  "kernel_ms": env.elapsed_ms(2, 3)}
-    env.close()
+        for e in envs:
+            e.rollout(1)  # load the rollout kernel: a first launch would time code-object loading
+            e.synchronize()
+
+        def fused(rp):
+            env = envs[rep.local.index(rp)]
+            t0 = time.perf_counter()
+            env.record_event(2)
+            st, _ = env.rollout(args.fused_plies)
+            env.record_event(3)
+            env.synchronize()
+            return float(st[0]), time.perf_counter() - t0
+
+        fs, fdt = rep.timed(fused)
+        extra["fused_rollout"] = {"value": rep.sum(sum(fs)) / fdt, "unit": "env_steps/s",
+                                  "plies_per_launch": args.fused_plies, "kernel_ms": envs[0].elapsed_ms(2, 3)}
+    for e in envs:
+        e.close()
     if args.variant_steps > 0:
         extra["variants"] = variant_legs(args, rep, n)
     if args.perft_roots > 0:
-        extra["perft"] = perft_leg(args, rep, rep.local_rank)
+        extra["perft"] = perft_leg(args, rep)
 
     cpu = None
     if rep.rank == 0 and rep.world_size == 1 and not args.no_cpu_baseline:  # N=1 only (contract)
@@ -248,6 +305,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": dt_max * 1e3 / args.steps,
+            "timed_region_ms": dt_max * 1e3,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -255,12 +313,13 @@ def main():
             "data": "synthetic (DEFAULT_BOARD starts, Philox uniform policy)",
             "config": {"workload": "configs[2]: 65536 boards/GPU random-policy rollout to terminal, step() throughput",
                        "boards_per_gpu": n, "global_boards": n * rep.world_size,
-                       "parallelism": f"replicas{rep.world_size}"},
+                       "parallelism": f"replicas{rep.world_size}", "replica_mode": rep.mode,
+                       "settle_plies": args.settle},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "k_env_step2", "avg_launch_us": avg_launch_s * 1e6,
-                         "alg_bytes_per_board": ALG_BYTES_PER_BOARD, "mean_window": 0.5 * (w0 + w1) / n,
-                         "valu": valu},
+                         "alg_bytes_per_board": ALG_BYTES_PER_BOARD, "mean_window": mean_window,
+                         "valu": valu, "pmc_source": pmc_src},
             "cpu_baseline": cpu,
             **extra,
         }

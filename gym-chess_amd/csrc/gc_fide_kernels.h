@@ -112,7 +112,7 @@ __global__ void k_fupdate_state(SoA st) {
 }
 
 // perft levels: children counted with promotions x4, expanded in enumeration order
-__global__ void k_fcount_children(SoA in, int32_t* __restrict__ cnt) {
+__global__ void k_fcount_children(SoA in, int64_t* __restrict__ cnt) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= in.n) return;
     Pos s = in.load(i);
@@ -120,13 +120,14 @@ __global__ void k_fcount_children(SoA in, int32_t* __restrict__ cnt) {
     gcf::fgen(s, f);
     cnt[i] = gcf::fcount(s, f, true);
 }
-__global__ void k_fexpand(SoA in, const int32_t* __restrict__ offs, SoA out) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= in.n) return;
-    Pos s = in.load(i);
+// parents a .. a+c-1 of `in`, children at offs[t] (relative to the chunk's first child)
+__global__ void k_fexpand_range(SoA in, int a, int c, const int64_t* __restrict__ offs, SoA out) {
+    int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= c) return;
+    Pos s = in.load(a + t);
     gcf::FGen f;
     gcf::fgen(s, f);
-    int o = offs[i];
+    int o = (int)offs[t];
     u64 pcs = f.g.own;
     int rw;
     bool irr;

@@ -16,6 +16,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -306,8 +307,11 @@ __global__ void k_iota(int32_t* __restrict__ v, int n) {
     if (i < n) v[i] = i;
 }
 
-// children of every node, written at offs[i] .. offs[i]+cnt[i] (offs = exclusive scan)
-__global__ void k_count_children(SoA in, int32_t* __restrict__ cnt) {
+// children of every node, written at offs[i] .. offs[i]+cnt[i] (offs = exclusive scan).
+// T = int32_t for radix-sort keys, int64_t for level sizes (a level's child total can pass
+// 2^31: depth 6 over 65 536 mid-game roots has ~3e9 nodes at its fourth level).
+template <class T>
+__global__ void k_count_children(SoA in, T* __restrict__ cnt) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= in.n) return;
     Pos s = in.load(i);
@@ -316,38 +320,18 @@ __global__ void k_count_children(SoA in, int32_t* __restrict__ cnt) {
     NoScratch none;
     gen_init(s, g);
     gen_moves(s, g, ms, none);
-    cnt[i] = ms.total;
+    cnt[i] = (T)ms.total;
 }
-__global__ void k_expand(SoA in, const int32_t* __restrict__ offs, SoA out) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= in.n) return;
-    Pos s = in.load(i);
-    Gen g;
-    gen_init(s, g);
-    int o = offs[i];
-    u64 pcs = g.own;
-    while (pcs) {
-        int sq = ctz(pcs);
-        pcs &= pcs - 1;
-        u64 tg = legal_targets(s, g, sq, type_at(s, sq));
-        while (tg) {
-            int t = ctz(tg);
-            tg &= tg - 1;
-            out.store(o++, child_of(s, g.white, sq * 64 + t));
-        }
-    }
-    if (g.castles & 1) out.store(o++, child_of(s, g.white, g.white ? A_QSW : A_QSB));
-    if (g.castles & 2) out.store(o++, child_of(s, g.white, g.white ? A_KSW : A_KSB));
-}
-// k_expand over the parents a .. a+c-1 of `in` (offs indexed from a): one chunk of a level
-// too large to materialise whole
-__global__ void k_expand_range(SoA in, int a, int c, const int32_t* __restrict__ offs, SoA out) {
+// expand the parents a .. a+c-1 of `in` into `out` at offs[t] (offs indexed from a, relative
+// to the chunk's first child; a chunk holds < 2^31 children)
+template <class T>
+__global__ void k_expand_range(SoA in, int a, int c, const T* __restrict__ offs, SoA out) {
     int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= c) return;
     Pos s = in.load(a + t);
     Gen g;
     gen_init(s, g);
-    int o = offs[t];
+    int o = (int)offs[t];
     u64 pcs = g.own;
     while (pcs) {
         int sq = ctz(pcs);
@@ -363,12 +347,14 @@ __global__ void k_expand_range(SoA in, int a, int c, const int32_t* __restrict__
     if (g.castles & 2) out.store(o++, child_of(s, g.white, g.white ? A_KSW : A_KSB));
 }
 // parent value = sum of its children's values (children of one parent are contiguous)
-__global__ void k_sum_children(const int32_t* __restrict__ offs, const int32_t* __restrict__ cnt,
+template <class T>
+__global__ void k_sum_children(const T* __restrict__ offs, const T* __restrict__ cnt,
                                const uint64_t* __restrict__ child, int n, uint64_t* __restrict__ out) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     uint64_t s = 0;
-    for (int k = 0; k < cnt[i]; k++) s += child[offs[i] + k];
+    const T c = cnt[i], o = offs[i];
+    for (T k = 0; k < c; k++) s += child[o + k];
     out[i] = s;
 }
 
@@ -1346,7 +1332,7 @@ static int perft_split_leaves(hipStream_t st, SoA leaf, uint64_t* leaf_out) {
         if (he != hipSuccess) { done(); return fail(std::string("perft split: ") + hipGetErrorString(he)); }
         if (dalloc((char**)&tmp, tmp_bytes)) { done(); return -1; }
     }
-    k_count_children<<<grid_for(leaf.n), BLOCK, 0, st>>>(leaf, kc);
+    k_count_children<int32_t><<<grid_for(leaf.n), BLOCK, 0, st>>>(leaf, kc);
     for (int a = 0; a < leaf.n && rc == 0;) {
         int c = leaf.n - a < chunk ? leaf.n - a : chunk;
         size_t tb = tmp_bytes;
@@ -1360,15 +1346,15 @@ static int perft_split_leaves(hipStream_t st, SoA leaf, uint64_t* leaf_out) {
         if (total > cap) { chunk /= 2; continue; }  // an unusually bushy chunk: halve and retry
         if (total > 0) {
             SoA ch{cb, cm, (int)total};
-            k_expand_range<<<grid_for(c), BLOCK, 0, st>>>(leaf, a, c, offs, ch);
-            k_count_children<<<grid_for((int)total), BLOCK, 0, st>>>(ch, kc2);
+            k_expand_range<int32_t><<<grid_for(c), BLOCK, 0, st>>>(leaf, a, c, offs, ch);
+            k_count_children<int32_t><<<grid_for((int)total), BLOCK, 0, st>>>(ch, kc2);
             k_iota<<<grid_for((int)total), BLOCK, 0, st>>>(ix, (int)total);
             tb = tmp_bytes;
             he = hipcub::DeviceRadixSort::SortPairs(tmp, tb, kc2, ks, ix, is, (int)total, 0, 10, st);
             if (he != hipSuccess) { err = std::string("perft split sort: ") + hipGetErrorString(he); rc = -1; break; }
             k_perft2_perm<<<grid_for((int)total), BLOCK, 0, st>>>(ch, is, cval);
         }
-        k_sum_children<<<grid_for(c), BLOCK, 0, st>>>(offs, kc + a, cval, c, leaf_out + a);
+        k_sum_children<int32_t><<<grid_for(c), BLOCK, 0, st>>>(offs, kc + a, cval, c, leaf_out + a);
         he = hipGetLastError();
         if (he != hipSuccess) { err = std::string("perft split kernels: ") + hipGetErrorString(he); rc = -1; break; }
         a += c;
@@ -1379,106 +1365,136 @@ static int perft_split_leaves(hipStream_t st, SoA leaf, uint64_t* leaf_out) {
     return rc ? fail(err) : 0;
 }
 
-// perft over n roots (side to move = meta[0]).  Levels are expanded on the device while
-// more than 3 plies remain, or while there are too few subtrees to fill the chip.
-static int perft_device(hipStream_t st, SoA roots, int depth, uint64_t* d_out, int fide) {
-    struct Level {
-        u64* bb = nullptr; u32* meta = nullptr; int32_t* cnt = nullptr; int32_t* offs = nullptr;
-        uint64_t* val = nullptr; int n = 0;
-    };
-    std::vector<Level> lv(1);
-    lv[0].bb = roots.bb; lv[0].meta = roots.meta; lv[0].n = roots.n;
-    int rem = depth;
-    int rc = 0;
-    std::string err;
-    auto cleanup = [&]() {
-        for (size_t l = 0; l < lv.size(); l++) {
-            if (l > 0) { (void)hipFree(lv[l].bb); (void)hipFree(lv[l].meta); }
-            (void)hipFree(lv[l].cnt); (void)hipFree(lv[l].offs);
-            if (l > 0) (void)hipFree(lv[l].val);
-        }
-    };
-    while (rem > 3 || (rem >= 2 && lv.back().n < 131072)) {
-        Level& cur = lv.back();
-        if (dalloc(&cur.cnt, cur.n) || dalloc(&cur.offs, cur.n)) { cleanup(); return -1; }
-        SoA cs{cur.bb, cur.meta, cur.n};
-        if (fide) k_fcount_children<<<grid_for(cur.n), BLOCK, 0, st>>>(cs, cur.cnt);
-        else k_count_children<<<grid_for(cur.n), BLOCK, 0, st>>>(cs, cur.cnt);
-        size_t tmp_bytes = 0;
+// which leaf pass ran, per pass (gc_perft_path_counts): tests assert that a configuration
+// takes the path it is meant to pin
+static std::atomic<unsigned long long> g_perft_path[4];  // split, sorted, small, fide
+
+// Leaf level: perft(node, rem) of every node of `leaf` (rem <= 3, or few nodes) into out.
+static int perft_leaf(hipStream_t st, SoA ls, int rem, uint64_t* out, int fide) {
+    if (ls.n == 0) return 0;
+    static const bool unsorted = getenv("GC_PERFT_UNSORTED") != nullptr;  // A/B switch
+    const char* sp = getenv("GC_PERFT_SPLIT");  // per call: tests compare both paths
+    if (!fide && rem == 3 && ls.n >= 65536 && !unsorted && !(sp && sp[0] == '0')) {
+        g_perft_path[0]++;
+        return perft_split_leaves(st, ls, out);
+    }
+    if (!fide && rem >= 2 && ls.n >= 65536 && !unsorted) {  // subtrees by root move count
+        int32_t *kc = nullptr, *ks = nullptr, *ix = nullptr, *is = nullptr;
         void* tmp = nullptr;
-        hipError_t he = hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, cur.cnt, cur.offs, cur.n, st);
-        if (he == hipSuccess && dalloc((char**)&tmp, tmp_bytes) == 0)
-            he = hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, cur.cnt, cur.offs, cur.n, st);
-        int32_t lo = 0, lc = 0;
-        if (he == hipSuccess) he = hipMemcpyAsync(&lo, cur.offs + cur.n - 1, 4, hipMemcpyDeviceToHost, st);
-        if (he == hipSuccess) he = hipMemcpyAsync(&lc, cur.cnt + cur.n - 1, 4, hipMemcpyDeviceToHost, st);
+        size_t tb = 0;
+        hipError_t he = hipSuccess;
+        if (dalloc(&kc, ls.n) || dalloc(&ks, ls.n) || dalloc(&ix, ls.n) || dalloc(&is, ls.n)) he = hipErrorOutOfMemory;
+        if (he == hipSuccess) {
+            k_count_children<int32_t><<<grid_for(ls.n), BLOCK, 0, st>>>(ls, kc);
+            k_iota<<<grid_for(ls.n), BLOCK, 0, st>>>(ix, ls.n);
+            he = hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kc, ks, ix, is, ls.n, 0, 10, st);
+        }
+        if (he == hipSuccess && dalloc((char**)&tmp, tb) == 0)
+            he = hipcub::DeviceRadixSort::SortPairs(tmp, tb, kc, ks, ix, is, ls.n, 0, 10, st);
+        bool ok = he == hipSuccess && tmp;
+        if (ok) {
+            k_perft_small_perm<<<grid_for(ls.n), BLOCK, 0, st>>>(ls, is, rem, out);
+            he = hipStreamSynchronize(st);  // before the temporaries are freed
+        }
+        (void)hipFree(tmp); (void)hipFree(kc); (void)hipFree(ks); (void)hipFree(ix); (void)hipFree(is);
+        if (he != hipSuccess) return fail(std::string("perft sort: ") + hipGetErrorString(he));
+        if (ok) { g_perft_path[1]++; return 0; }
+    }
+    g_perft_path[fide ? 3 : 2]++;
+    if (fide) k_fperft_small<<<grid_for(ls.n), BLOCK, 0, st>>>(ls, rem, out);
+    else k_perft_small<<<grid_for(ls.n), BLOCK, 0, st>>>(ls, rem, out);
+    return 0;
+}
+
+// Children materialised per chunk of parents: <= PERFT_LEVEL_CAP nodes (60 B each plus
+// 24 B of counts / offsets / values, ~11 GiB at 2^27) so any depth fits HBM; the split-leaf
+// pass below holds its own <= 2^27-child chunk.  GC_PERFT_LEVEL_CAP (per call) lowers it so
+// tests drive the chunked path at small sizes.
+static const int64_t PERFT_LEVEL_CAP = (int64_t)1 << 27;
+
+// out[i] = perft(nodes[i], rem).  While more than 3 plies remain, or while there are too few
+// subtrees to fill the chip, the nodes are expanded into their children on the device
+// (count, exclusive scan in 64 bits, write) and the children recursed on, one chunk of
+// parents at a time when the level would not fit; the parents' values are the sums of their
+// children's.  Sizes are 64-bit throughout: a level's child total may pass 2^31.
+static int perft_nodes(hipStream_t st, SoA nodes, int rem, uint64_t* out, int fide) {
+    if (nodes.n == 0) return 0;
+    if (!(rem > 3 || (rem >= 2 && nodes.n < 131072))) return perft_leaf(st, nodes, rem, out, fide);
+    int64_t cap = PERFT_LEVEL_CAP;
+    if (const char* e = getenv("GC_PERFT_LEVEL_CAP")) cap = atoll(e) > 0 ? atoll(e) : cap;
+    const int n = nodes.n;
+    int64_t *cnt = nullptr, *offs = nullptr;
+    u64* cb = nullptr;
+    u32* cm = nullptr;
+    uint64_t* cval = nullptr;
+    void* tmp = nullptr;
+    size_t tmp_bytes = 0;
+    int64_t held = 0;  // children the buffers below can hold
+    std::string err;
+    auto release = [&]() {
+        (void)hipStreamSynchronize(st);  // nothing in flight may still use the buffers
+        void* ps[] = {cnt, offs, cb, cm, cval, tmp};
+        for (void* q : ps) (void)hipFree(q);
+        cb = nullptr; cm = nullptr; cval = nullptr;
+    };
+    if (dalloc(&cnt, n) || dalloc(&offs, n)) { release(); return -1; }
+    if (fide) k_fcount_children<<<grid_for(n), BLOCK, 0, st>>>(nodes, cnt);
+    else k_count_children<int64_t><<<grid_for(n), BLOCK, 0, st>>>(nodes, cnt);
+    hipError_t he = hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, cnt, offs, n, st);
+    if (he != hipSuccess || dalloc((char**)&tmp, tmp_bytes ? tmp_bytes : 1)) {
+        release();
+        return he != hipSuccess ? fail(std::string("perft scan: ") + hipGetErrorString(he)) : -1;
+    }
+    int chunk = n;
+    for (int a = 0; a < n;) {
+        const int c = n - a < chunk ? n - a : chunk;
+        size_t tb = tmp_bytes;
+        int64_t lo = 0, lc = 0;
+        he = hipcub::DeviceScan::ExclusiveSum(tmp, tb, cnt + a, offs, c, st);
+        if (he == hipSuccess) he = hipMemcpyAsync(&lo, offs + c - 1, 8, hipMemcpyDeviceToHost, st);
+        if (he == hipSuccess) he = hipMemcpyAsync(&lc, cnt + a + c - 1, 8, hipMemcpyDeviceToHost, st);
         if (he == hipSuccess) he = hipStreamSynchronize(st);
-        (void)hipFree(tmp);
-        if (he != hipSuccess) { cleanup(); return fail(std::string("perft scan: ") + hipGetErrorString(he)); }
-        int64_t total = (int64_t)lo + lc;
-        if (total > (int64_t)1 << 29) { cleanup(); return fail("perft: level too large (split roots into batches)"); }
-        Level nx;
-        nx.n = (int)total;
-        if (dalloc(&nx.bb, (size_t)NBB * (total ? total : 1)) || dalloc(&nx.meta, total ? total : 1)) {
-            cleanup();
-            return -1;
+        if (he != hipSuccess) { err = std::string("perft scan: ") + hipGetErrorString(he); break; }
+        const int64_t total = lo + lc;
+        if (total > cap && c > 1) { chunk = (c + 1) / 2; continue; }  // halve the chunk and rescan
+        if (total >= ((int64_t)1 << 31)) { err = "perft: one node has too many children"; break; }
+        if (total > held) {  // (re)allocate the child buffers for this chunk
+            (void)hipStreamSynchronize(st);
+            (void)hipFree(cb); (void)hipFree(cm); (void)hipFree(cval);
+            cb = nullptr; cm = nullptr; cval = nullptr;
+            held = 0;
+            if (dalloc(&cb, (size_t)NBB * total) || dalloc(&cm, total) || dalloc(&cval, total)) { err = g_err; break; }
+            held = total;
         }
-        SoA ns{nx.bb, nx.meta, nx.n};
-        if (fide) k_fexpand<<<grid_for(cur.n), BLOCK, 0, st>>>(cs, cur.offs, ns);
-        else k_expand<<<grid_for(cur.n), BLOCK, 0, st>>>(cs, cur.offs, ns);
-        lv.push_back(nx);
-        rem--;
-        if (total == 0) break;
+        if (total > 0) {
+            SoA ch{cb, cm, (int)total};
+            if (fide) k_fexpand_range<<<grid_for(c), BLOCK, 0, st>>>(nodes, a, c, offs, ch);
+            else k_expand_range<int64_t><<<grid_for(c), BLOCK, 0, st>>>(nodes, a, c, offs, ch);
+            he = hipGetLastError();
+            if (he != hipSuccess) { err = std::string("perft expand: ") + hipGetErrorString(he); break; }
+            if (perft_nodes(st, ch, rem - 1, cval, fide)) { err = g_err; break; }
+        }
+        k_sum_children<int64_t><<<grid_for(c), BLOCK, 0, st>>>(offs, cnt + a, cval, c, out + a);
+        he = hipGetLastError();
+        if (he != hipSuccess) { err = std::string("perft sum: ") + hipGetErrorString(he); break; }
+        a += c;
     }
-    Level& leaf = lv.back();
-    if (lv.size() > 1 && dalloc(&leaf.val, leaf.n ? leaf.n : 1)) { cleanup(); return -1; }
-    uint64_t* leaf_out = lv.size() > 1 ? leaf.val : d_out;
-    if (leaf.n > 0) {
-        SoA ls{leaf.bb, leaf.meta, leaf.n};
-        static const bool unsorted = getenv("GC_PERFT_UNSORTED") != nullptr;  // A/B switch
-        bool sorted = false;
-        const char* sp = getenv("GC_PERFT_SPLIT");  // per call: tests compare both paths
-        if (!fide && rem == 3 && leaf.n >= 65536 && !unsorted && !(sp && sp[0] == '0')) {
-            if (perft_split_leaves(st, ls, leaf_out)) { cleanup(); return -1; }
-            sorted = true;
-        }
-        if (!sorted && !fide && rem >= 2 && leaf.n >= 65536 && !unsorted) {  // subtrees by root move count
-            int32_t *kc = nullptr, *ks = nullptr, *ix = nullptr, *is = nullptr;
-            void* tmp = nullptr;
-            size_t tb = 0;
-            hipError_t he = hipSuccess;
-            if (dalloc(&kc, leaf.n) || dalloc(&ks, leaf.n) || dalloc(&ix, leaf.n) || dalloc(&is, leaf.n)) he = hipErrorOutOfMemory;
-            if (he == hipSuccess) {
-                k_count_children<<<grid_for(leaf.n), BLOCK, 0, st>>>(ls, kc);
-                k_iota<<<grid_for(leaf.n), BLOCK, 0, st>>>(ix, leaf.n);
-                he = hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kc, ks, ix, is, leaf.n, 0, 10, st);
-            }
-            if (he == hipSuccess && dalloc((char**)&tmp, tb) == 0)
-                he = hipcub::DeviceRadixSort::SortPairs(tmp, tb, kc, ks, ix, is, leaf.n, 0, 10, st);
-            if (he == hipSuccess && tmp) {
-                k_perft_small_perm<<<grid_for(leaf.n), BLOCK, 0, st>>>(ls, is, rem, leaf_out);
-                sorted = true;
-                he = hipStreamSynchronize(st);  // before the temporaries are freed
-            }
-            (void)hipFree(tmp); (void)hipFree(kc); (void)hipFree(ks); (void)hipFree(ix); (void)hipFree(is);
-            if (he != hipSuccess) { cleanup(); return fail(std::string("perft sort: ") + hipGetErrorString(he)); }
-        }
-        if (!sorted) {
-            if (fide) k_fperft_small<<<grid_for(leaf.n), BLOCK, 0, st>>>(ls, rem, leaf_out);
-            else k_perft_small<<<grid_for(leaf.n), BLOCK, 0, st>>>(ls, rem, leaf_out);
-        }
-    }
-    for (int l = (int)lv.size() - 2; l >= 0; l--) {
-        uint64_t* dst = l == 0 ? d_out : lv[l].val;
-        if (l > 0 && dalloc(&lv[l].val, lv[l].n)) { cleanup(); return -1; }
-        dst = l == 0 ? d_out : lv[l].val;
-        k_sum_children<<<grid_for(lv[l].n), BLOCK, 0, st>>>(lv[l].offs, lv[l].cnt, lv[l + 1].val, lv[l].n, dst);
-    }
+    release();
+    return err.empty() ? 0 : fail(err);
+}
+
+// perft over n roots (side to move = meta[0])
+static int perft_device(hipStream_t st, SoA roots, int depth, uint64_t* d_out, int fide) {
+    if (perft_nodes(st, roots, depth, d_out, fide)) return -1;
     hipError_t he = hipGetLastError();
     if (he == hipSuccess) he = hipStreamSynchronize(st);
-    if (he != hipSuccess) { err = std::string("perft kernels: ") + hipGetErrorString(he); rc = -1; }
-    cleanup();
-    if (rc) return fail(err);
+    if (he != hipSuccess) return fail(std::string("perft kernels: ") + hipGetErrorString(he));
+    return 0;
+}
+
+extern "C" int gc_perft_path_counts(uint64_t* out4) {
+    if (!out4) return fail("null argument");
+    for (int k = 0; k < 4; k++) out4[k] = g_perft_path[k].load();
     return 0;
 }
 

@@ -28,7 +28,7 @@ def __getattr__(name):  # lazy: importing the package must not require a GPU
         from . import engine
 
         return getattr(engine, name)
-    if name in ("BatchedChessEnv",):
+    if name in ("BatchedChessEnv", "MultiDeviceChessEnv"):
         from . import env
 
         return getattr(env, name)

@@ -110,6 +110,13 @@ class Engine:
         return out
 
 
+def perft_path_counts():
+    """Diagnostics: {pass: runs in this process} of the perft leaf passes (gc_perft_path_counts)."""
+    out = np.zeros(4, dtype=np.uint64)
+    _lib.check(_lib.load().gc_perft_path_counts(_lib.ptr(out)))
+    return dict(zip(("split", "sorted", "small", "fide"), (int(x) for x in out)))
+
+
 class ChessEngine:
     """Drop-in replacement for the reference's `gym_chess.ChessEngine` (lib.rs:1412-1512).
 

@@ -208,3 +208,67 @@ class BatchedChessEnv:
 
     def device_bytes(self):
         return int(self._L.gc_env_device_bytes(self._h))
+
+
+class MultiDeviceChessEnv:
+    """`device_ids` form of the batched env (SURVEY.md §5 Config, §8e): num_boards boards per
+    device, one BatchedChessEnv per device, global board g on device g // num_boards.  Device
+    calls run in one host thread per device (ctypes releases the GIL), no collective; the
+    policy stream of replica r is keyed seed + (r << 40) (gym_chess_amd.replicas)."""
+
+    def __init__(self, num_boards, device_ids=(0,), seed=0, **kw):
+        from .replicas import Replicas
+
+        self.rep = Replicas(gpus=len(device_ids), devices=device_ids)
+        self.num_boards = int(num_boards)
+        self.envs = self.rep.run(lambda rp: BatchedChessEnv(num_boards, device=rp.device, seed=rp.board_seed(seed), **kw))
+
+    @property
+    def total_boards(self):
+        return self.num_boards * len(self.envs)
+
+    def _each(self, fn):
+        return self.rep.run(lambda rp: fn(self.envs[rp.index]))
+
+    def _split(self, x):
+        x = np.asarray(x)
+        return [x[k * self.num_boards:(k + 1) * self.num_boards] for k in range(len(self.envs))]
+
+    def reset(self, mask=None):
+        parts = self._split(mask) if mask is not None else [None] * len(self.envs)
+        self.rep.run(lambda rp: self.envs[rp.index].reset(parts[rp.index]))
+
+    def step(self, actions):
+        parts = self._split(actions)
+        out = self.rep.run(lambda rp: self.envs[rp.index].step(parts[rp.index]))
+        return tuple(np.concatenate([o[k] for o in out]) for k in range(3))
+
+    def step_random(self, n_plies=1):
+        self._each(lambda e: e.step_random(n_plies))
+
+    def rollout(self, n_plies):
+        """fused random self-play on every device; stats8 summed over devices"""
+        st = self._each(lambda e: e.rollout(n_plies)[0])
+        return np.sum(st, axis=0, dtype=np.uint64)
+
+    def boards(self):
+        out = self._each(lambda e: e.boards())
+        return np.concatenate([o[0] for o in out]), np.concatenate([o[1] for o in out])
+
+    def outputs(self):
+        out = self._each(lambda e: e.outputs())
+        return {k: np.concatenate([o[k] for o in out]) for k in out[0]}
+
+    def synchronize(self):
+        self._each(lambda e: e.synchronize())
+
+    def close(self):
+        for e in getattr(self, "envs", []):
+            e.close()
+        self.envs = []
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

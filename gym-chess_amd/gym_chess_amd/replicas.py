@@ -1,60 +1,219 @@
-"""Multi-GPU = independent replicas (DESIGN.md §6).
+"""Multi-GPU = independent replicas (DESIGN.md §6; SURVEY.md §8e).
 
-Boards never interact, so N GPUs run N independent batches with no data-path collective.
-One process per GPU (torch.distributed.run sets RANK / LOCAL_RANK / WORLD_SIZE); gloo is
-used only for the barrier around the timed region and to combine scalar results (max of
-the per-rank times, sum of the per-rank step counts).
+Boards never interact, so N GPUs run N independent batches with no data-path collective;
+the only cross-GPU data are a few host-side scalars (steps, nodes, times).  Two ways to get
+N replicas, neither needing PyTorch:
+
+* threads (preferred; `bench.py --gpus N` run directly): ONE process, one host thread and
+  one gc_env / gc_engine handle per device.  ctypes releases the GIL for every C-ABI call,
+  and a whole timed region is a single call per replica (gc_env_step_random launches K
+  kernels), so the threads drive their devices concurrently.
+* processes (`python -m torch.distributed.run --nproc-per-node N bench.py --gpus N`, the
+  launcher the driver uses): one process per GPU, RANK / WORLD_SIZE / LOCAL_RANK from the
+  environment.  The barrier and the max / sum of per-rank scalars go through a file group
+  in the node's temp directory (all ranks share one node; keyed by the launcher's pid, so
+  concurrent launches never meet).  GC_REPLICA_BACKEND=gloo uses torch.distributed's gloo
+  instead (the only place torch is ever imported).
+
+Replica r (0 <= r < world_size) owns global boards [r*B, (r+1)*B) and draws its policy
+stream under the Philox key seed + (r << 40).
 """
+import json
 import os
+import tempfile
+import threading
+import time
 
-SEED_STRIDE_BITS = 40  # rank r draws its Philox stream under key seed + (r << 40)
+SEED_STRIDE_BITS = 40  # replica r draws its Philox stream under key seed + (r << 40)
+
+
+class Replica:
+    """One replica: its global index and the device it runs on."""
+
+    def __init__(self, index, device):
+        self.index = int(index)
+        self.device = int(device)
+
+    def board_seed(self, base_seed):
+        """Distinct policy stream per replica (same board index on two GPUs plays differently)."""
+        return (int(base_seed) + (self.index << SEED_STRIDE_BITS)) & 0xFFFFFFFFFFFFFFFF
+
+    def board_range(self, boards_per_replica):
+        """[begin, end) of this replica's boards in the global batch (weak scaling)."""
+        return self.index * boards_per_replica, (self.index + 1) * boards_per_replica
+
+
+def _remove_stale_groups():
+    """A group's files stay until its launcher is gone (a rank cannot know when the others
+    have read its last record); groups of launchers that no longer exist are removed here."""
+    import glob
+    import shutil
+
+    for d in glob.glob(os.path.join(tempfile.gettempdir(), "gymchess_replicas_*")):
+        try:
+            pid = int(os.path.basename(d).split("_")[2])
+            os.kill(pid, 0)
+        except (ValueError, IndexError):
+            continue
+        except ProcessLookupError:
+            shutil.rmtree(d, ignore_errors=True)
+        except PermissionError:
+            continue
+
+
+class _FileGroup:
+    """Barrier + all-gather of small JSON values among the ranks of one node, through one file
+    per rank.  A rank's file holds its latest round and the values of its last two rounds: a
+    rank can run at most one round ahead of the slowest (it cannot pass round k before every
+    rank has reached k), so a reader of round k finds it as `cur` or `prev`."""
+
+    def __init__(self, rank, world, key, timeout=900.0):
+        self.rank, self.world, self.timeout = rank, world, timeout
+        self.dir = os.path.join(tempfile.gettempdir(), f"gymchess_replicas_{key}")
+        _remove_stale_groups()
+        os.makedirs(self.dir, exist_ok=True)
+        self.round = 0
+        self.prev = None
+
+    def _path(self, r):
+        return os.path.join(self.dir, f"rank{r}.json")
+
+    def _read(self, r):
+        try:
+            with open(self._path(r)) as f:
+                return json.load(f)
+        except (FileNotFoundError, json.JSONDecodeError):
+            return None
+
+    def allgather(self, value):
+        k = self.round
+        self.round += 1
+        rec = {"round": k, "cur": value, "prev": self.prev}
+        self.prev = value
+        tmp = self._path(self.rank) + f".tmp{os.getpid()}"
+        with open(tmp, "w") as f:
+            json.dump(rec, f)
+        os.replace(tmp, self._path(self.rank))  # atomic: readers see the old or the new record
+        out = [None] * self.world
+        t0 = time.monotonic()
+        pending = set(range(self.world))
+        while pending:
+            for r in list(pending):
+                d = self._read(r)
+                if d is not None and d["round"] >= k:
+                    out[r] = d["cur"] if d["round"] == k else d["prev"]
+                    pending.discard(r)
+            if pending:
+                if time.monotonic() - t0 > self.timeout:
+                    raise TimeoutError(f"replica group: ranks {sorted(pending)} never reached round {k}")
+                time.sleep(0.0005)
+        return out
 
 
 class Replicas:
-    def __init__(self, world_size=None, rank=None, local_rank=None):
-        self.world_size = int(os.environ.get("WORLD_SIZE", "1")) if world_size is None else world_size
-        self.rank = int(os.environ.get("RANK", "0")) if rank is None else rank
-        self.local_rank = int(os.environ.get("LOCAL_RANK", str(self.rank))) if local_rank is None else local_rank
+    def __init__(self, gpus=None, world_size=None, rank=None, local_rank=None, devices=None):
+        if "WORLD_SIZE" in os.environ or world_size is not None:  # one process per GPU
+            self.mode = "processes"
+            self.world_size = int(os.environ.get("WORLD_SIZE", "1")) if world_size is None else int(world_size)
+            self.rank = int(os.environ.get("RANK", "0")) if rank is None else int(rank)
+            lr = os.environ.get("LOCAL_RANK", str(self.rank)) if local_rank is None else local_rank
+            self.local = [Replica(self.rank, int(lr))]
+            if gpus is not None and int(gpus) != self.world_size:
+                raise ValueError(f"--gpus {gpus} does not match the launcher's WORLD_SIZE={self.world_size}")
+        else:  # one process, one thread per device
+            self.mode = "threads"
+            self.world_size = 1 if gpus is None else int(gpus)
+            if self.world_size < 1:
+                raise ValueError("--gpus must be >= 1")
+            self.rank = 0
+            devs = list(range(self.world_size)) if devices is None else [int(d) for d in devices]
+            if len(devs) != self.world_size:
+                raise ValueError(f"{len(devs)} devices for {self.world_size} replicas")
+            # devices may repeat (several replicas on one GPU: the 1-GPU tests of this path)
+            self.local = [Replica(r, d) for r, d in enumerate(devs)]
+        self._group = None
         self._dist = None
 
     def init(self):
-        if self.world_size > 1:
-            import torch.distributed as dist
+        if self.mode == "processes" and self.world_size > 1:
+            if os.environ.get("GC_REPLICA_BACKEND", "file") == "gloo":
+                import torch.distributed as dist
 
-            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            if not dist.is_initialized():
-                dist.init_process_group("gloo", rank=self.rank, world_size=self.world_size)
-            self._dist = dist
+                os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+                if not dist.is_initialized():
+                    dist.init_process_group("gloo", rank=self.rank, world_size=self.world_size)
+                self._dist = dist
+            else:
+                key = os.environ.get("GC_REPLICA_KEY") or f"{os.getppid()}_{os.environ.get('MASTER_PORT', '0')}"
+                self._group = _FileGroup(self.rank, self.world_size, key)
         return self
 
-    def board_seed(self, base_seed):
-        """Distinct policy stream per rank (same board index on two GPUs plays differently)."""
-        return (int(base_seed) + (self.rank << SEED_STRIDE_BITS)) & 0xFFFFFFFFFFFFFFFF
+    # ------------------------------------------------------------------ local replicas
+    def run(self, fn):
+        """fn(replica) on every local replica, one thread each; results in replica order.
+        An exception in any thread is re-raised here."""
+        if len(self.local) == 1:
+            return [fn(self.local[0])]
+        res = [None] * len(self.local)
+        err = []
 
-    def global_board_range(self, boards_per_rank):
-        """[begin, end) of this rank's boards in the global batch (weak scaling)."""
-        return self.rank * boards_per_rank, (self.rank + 1) * boards_per_rank
+        def body(k, rp):
+            try:
+                res[k] = fn(rp)
+            except BaseException as ex:  # noqa: BLE001 -- re-raised in the caller
+                err.append(ex)
 
+        th = [threading.Thread(target=body, args=(k, rp)) for k, rp in enumerate(self.local)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        if err:
+            raise err[0]
+        return res
+
+    def timed(self, fn):
+        """Barrier, then fn(replica) on every local replica started together (a thread
+        barrier), each timing itself; returns (results, the max of the replicas' seconds over
+        the whole job).  fn must return (result, seconds)."""
+        gate = threading.Barrier(len(self.local))
+
+        def body(rp):
+            gate.wait()
+            return fn(rp)
+
+        self.barrier()
+        out = self.run(body)
+        return [r for r, _ in out], self.max(max(dt for _, dt in out))
+
+    # ------------------------------------------------------------------ across processes
     def barrier(self):
-        if self._dist is not None:
+        if self._group is not None:
+            self._group.allgather(None)
+        elif self._dist is not None:
             self._dist.barrier()
 
     def _reduce(self, x, op):
-        if self._dist is None:
-            return float(x)
-        import torch
+        if self._group is not None:
+            vals = self._group.allgather(float(x))
+            return max(vals) if op == "max" else sum(vals)
+        if self._dist is not None:
+            import torch
 
-        t = torch.tensor([float(x)], dtype=torch.float64)
-        self._dist.all_reduce(t, op=op)
-        return float(t.item())
+            t = torch.tensor([float(x)], dtype=torch.float64)
+            self._dist.all_reduce(t, op=self._dist.ReduceOp.MAX if op == "max" else self._dist.ReduceOp.SUM)
+            return float(t.item())
+        return float(x)
 
     def max(self, x):
-        return self._reduce(x, None if self._dist is None else self._dist.ReduceOp.MAX)
+        return self._reduce(x, "max")
 
     def sum(self, x):
-        return self._reduce(x, None if self._dist is None else self._dist.ReduceOp.SUM)
+        return self._reduce(x, "sum")
 
     def close(self):
+        if self._group is not None:
+            self._group.allgather(None)  # nobody leaves while another rank still reads
         if self._dist is not None and self._dist.is_initialized():
             self._dist.destroy_process_group()
         self._dist = None

@@ -59,9 +59,14 @@ int gc_engine_next_state(gc_engine* e, int n, const int8_t* boards, const uint8_
 int gc_engine_update_state(gc_engine* e, int n, const int8_t* boards, const uint8_t* meta,
                            int8_t* out_boards, uint8_t* out_meta);
 /* perft by composition of get_all_possible_moves and next_state; the side
- * to move is meta[0]. depth in [0, 8]. */
+ * to move is meta[0]. depth in [0, 8]; any n (levels too large for HBM are expanded one
+ * chunk of parents at a time, sizes are 64-bit). */
 int gc_engine_perft(gc_engine* e, int n, const int8_t* boards, const uint8_t* meta, int depth,
                     uint64_t* nodes);
+/* diagnostics: how many times each perft leaf pass ran in this process, out4 = {split
+ * (depth-3 subtrees split to depth-2, sorted), sorted (subtrees by move count), small
+ * (unsorted nested loops), fide} */
+int gc_perft_path_counts(uint64_t* out4);
 /* Rules of every later call on this engine (not in the reference):
  * 0 = the reference's (default, lib.rs), 1 = FIDE (gym-chess_amd/csrc/gc_fide.h: en passant,
  * promotion, per-side castling through unattacked squares, no king captures).  Under FIDE

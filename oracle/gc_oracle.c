@@ -23,6 +23,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <pthread.h>
+#include <stdatomic.h>
 
 #define EMPTY 0
 #define KING 1
@@ -700,21 +701,28 @@ void oracle_rollout_trace2(const int8_t *init, uint64_t seed, uint32_t board, in
     if (stats8) { stats8[0] = st.steps; stats8[1] = st.reward_sum; for (int i = 0; i < 6; i++) stats8[2 + i] = st.ends[i]; }
 }
 
-/* Multi-threaded perft over many roots (CPU baseline for perft configs). */
-typedef struct { const int8_t *boards; const uint8_t *metas; int depth; uint32_t b0, b1; uint64_t *out; } PJob;
+/* Multi-threaded perft over many roots (CPU baseline for perft configs).  Roots are handed
+ * out one at a time from a shared counter: subtree sizes vary by 10x between mid-game roots,
+ * so a static split leaves most threads idle behind the largest ones. */
+typedef struct { const int8_t *boards; const uint8_t *metas; int depth; uint32_t n; atomic_uint *next; uint64_t *out; } PJob;
 static void *pjob_run(void *arg) {
     PJob *j = (PJob *)arg;
-    for (uint32_t b = j->b0; b < j->b1; b++) j->out[b] = oracle_perft(j->boards + 64 * (size_t)b, j->metas + 8 * (size_t)b, j->depth);
+    for (;;) {
+        uint32_t b = atomic_fetch_add(j->next, 1u);
+        if (b >= j->n) break;
+        j->out[b] = oracle_perft(j->boards + 64 * (size_t)b, j->metas + 8 * (size_t)b, j->depth);
+    }
     return NULL;
 }
 void oracle_perft_batch(const int8_t *boards, const uint8_t *metas, uint32_t n, int depth, int threads, uint64_t *out) {
     if (threads < 1) threads = 1;
+    atomic_uint next;
+    atomic_init(&next, 0u);
     PJob *jobs = (PJob *)calloc((size_t)threads, sizeof(PJob));
     pthread_t *th = (pthread_t *)calloc((size_t)threads, sizeof(pthread_t));
     for (int t = 0; t < threads; t++) {
         jobs[t].boards = boards; jobs[t].metas = metas; jobs[t].depth = depth; jobs[t].out = out;
-        jobs[t].b0 = (uint32_t)((uint64_t)n * t / threads);
-        jobs[t].b1 = (uint32_t)((uint64_t)n * (t + 1) / threads);
+        jobs[t].n = n; jobs[t].next = &next;
         pthread_create(&th[t], NULL, pjob_run, &jobs[t]);
     }
     for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);

@@ -152,6 +152,27 @@ def perft_batch(boards, metas, depth, threads=1):
     return out
 
 
+def perft_by_children(boards, metas, depth, threads=1):
+    """perft(depth) per root as the sum of perft(depth - 1) over its children (the definition,
+    SURVEY.md §3.4), so the threads share the work of a few large roots evenly."""
+    b = np.ascontiguousarray(boards, dtype=np.int8).reshape(-1, 64)
+    m = np.ascontiguousarray(metas, dtype=np.uint8).reshape(-1, 8)
+    if depth <= 1:
+        return perft_batch(b, m, depth, threads)
+    kb, km, owner = [], [], []
+    for i in range(b.shape[0]):
+        for a in get_possible_moves(b[i], m[i], int(m[i, 0])):
+            _, nb, nm, _ = next_state(b[i], m[i], int(m[i, 0]), a)
+            kb.append(nb)
+            km.append(nm)
+            owner.append(i)
+    out = np.zeros(b.shape[0], dtype=np.uint64)
+    if kb:
+        sub = perft_batch(np.stack(kb), np.stack(km), depth - 1, threads)
+        np.add.at(out, np.array(owner), sub)
+    return out
+
+
 def policy_index(seed, board, draw, n):
     return int(lib().oracle_policy_index(seed, board, draw, n))
 

@@ -186,6 +186,88 @@ def test_perft_split_leaves_matches_depth3_subtrees(engine):
     assert (split == whole).all() and split.sum() > 200 * 10**6, np.nonzero(split != whole)[0][:4]
 
 
+def _midgame_roots(n, plies, seed):
+    from gym_chess_amd.env import BatchedChessEnv
+
+    env = BatchedChessEnv(n, device=0, seed=seed)
+    env.step_random(plies)
+    b, m = env.boards()
+    env.close()
+    return b, m
+
+
+def test_perft5_split_leaves_vs_oracle(engine, oracle):
+    """BASELINE configs[3] path: perft(5) of 200 mid-game roots.  200 roots -> 7e3 -> 2.4e5
+    nodes with 3 plies left (>= 131 072: no further expansion), so the leaf level takes the
+    split pass (depth-3 subtrees split one more ply in chunks, depth-2 subtrees sorted by move
+    count: perft_split_leaves) -- asserted through the path counters.  12 roots spread over
+    the batch are compared with the oracle at depth 5, per root."""
+    from gym_chess_amd.engine import perft_path_counts
+
+    b, m = _midgame_roots(200, 21, 0x5EED + 5)
+    c0 = perft_path_counts()
+    got = engine.perft(b, m, 5)
+    c1 = perft_path_counts()
+    assert c1["split"] == c0["split"] + 1 and c1["sorted"] == c0["sorted"] and c1["small"] == c0["small"]
+    pick = np.arange(0, 200, 25)  # 8 roots, ~3e8 nodes for the oracle
+    ref = oracle.perft_by_children(b[pick], m[pick], 5, threads=16)
+    assert (got[pick] == ref).all(), (pick, got[pick], ref)
+    assert got.sum() > 200 * 10**6
+
+
+def test_perft5_equals_sum_of_children_perft4(engine, oracle):
+    """All 200 roots of the split-pass test: perft(5)(root) == sum over the root's legal moves
+    (oracle list + oracle next_state) of perft(4)(child), the children run through the OTHER
+    leaf pass (GC_PERFT_SPLIT=0: depth-3 subtrees sorted by move count, k_perft_small_perm)."""
+    import os
+
+    b, m = _midgame_roots(200, 21, 0x5EED + 5)
+    p5 = engine.perft(b, m, 5)
+    kids_b, kids_m, owner = [], [], []
+    for i in range(len(b)):
+        for a in oracle.get_possible_moves(b[i], m[i], int(m[i, 0])):
+            rc, nb, nm, _ = oracle.next_state(b[i], m[i], int(m[i, 0]), a)
+            assert rc in (0, 1)
+            kids_b.append(nb)
+            kids_m.append(nm)
+            owner.append(i)
+    os.environ["GC_PERFT_SPLIT"] = "0"
+    try:
+        p4 = engine.perft(np.stack(kids_b), np.stack(kids_m), 4)
+    finally:
+        del os.environ["GC_PERFT_SPLIT"]
+    sums = np.bincount(np.array(owner), weights=p4.astype(np.float64), minlength=len(b))
+    assert (p5.astype(np.float64) == sums).all(), np.nonzero(p5.astype(np.float64) != sums)[0][:4]
+
+
+def test_perft_chunked_levels_match(engine, oracle):
+    """Levels too large to materialise are expanded one chunk of parents at a time (64-bit
+    sizes; ADVICE r01: int32 level sums wrapped).  A 1 000-node level cap forces chunking at
+    every expanded level; results == the unchunked run == the oracle."""
+    import os
+
+    b, m = _midgame_roots(48, 17, 0x5EED + 9)
+    whole = engine.perft(b, m, 4)
+    os.environ["GC_PERFT_LEVEL_CAP"] = "1000"
+    try:
+        chunked = engine.perft(b, m, 4)
+    finally:
+        del os.environ["GC_PERFT_LEVEL_CAP"]
+    assert (whole == chunked).all()
+    assert (whole == oracle.perft_batch(b, m, 4, threads=16)).all()
+
+
+def test_perft6_startpos_vs_oracle(engine, oracle):
+    """Depth 6 from the start position (four expanded levels, recursion through each): == the
+    oracle (sum of perft(5) over the 20 children) == 124 483 101 (reference rules; FIDE is
+    119 060 324 -- the difference is Q1, the double push over a blocker)."""
+    from oracle import DEFAULT_BOARD, make_meta
+
+    got = int(engine.perft(DEFAULT_BOARD[None], make_meta()[None], 6)[0])
+    ref = int(oracle.perft_by_children(DEFAULT_BOARD[None], make_meta()[None], 6, threads=16)[0])
+    assert got == ref == 124483101
+
+
 # ------------------------------------------------------------------ env
 def _replay_trace(env, oracle_env, steps):
     """Drive the batched env (1 board) with the recorded actions; compare to the golden."""

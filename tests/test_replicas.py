@@ -1,12 +1,20 @@
-"""Multi-process (world_size 2, gloo, CPU) coverage of the replica path used by bench.py:
-rank seeds, board ranges, barrier, max/sum of per-rank scalars, and that the per-rank
-work really is independent (each rank's CPU-oracle rollouts depend only on its own seed)."""
+"""Multi-replica coverage on the CPU (no GPU): the replica path bench.py uses.
+
+* processes (world_size 2, one process per rank as torch.distributed.run starts them): rank
+  seeds, board ranges, barrier, max / sum of per-rank scalars through the file group (the
+  default, no torch) and through gloo (GC_REPLICA_BACKEND=gloo); per-rank work is
+  independent (each rank's CPU-oracle rollouts depend only on its own seed).
+* threads (`bench.py --gpus N` without a launcher): N replicas in one process, one thread
+  each, results in replica order, exceptions propagated, the timed region's max.
+"""
+import multiprocessing as mp
 import os
 import socket
 import sys
+import time
 
 import numpy as np
-import torch.multiprocessing as mp
+import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -19,35 +27,49 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, out):
+def _worker(rank, world, port, backend, out):
     sys.path.insert(0, os.path.join(ROOT, "gym-chess_amd"))
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK=str(rank))
+                      LOCAL_RANK=str(rank), GC_REPLICA_BACKEND=backend, GC_REPLICA_KEY=f"test_{port}")
     from gym_chess_amd.replicas import Replicas
     import oracle as O
 
-    r = Replicas().init()
-    seed = r.board_seed(0x5EED)
-    b0, b1 = r.global_board_range(4)
+    r = Replicas(gpus=world).init()
+    (rp,) = r.local
+    seed = rp.board_seed(0x5EED)
+    b0, b1 = rp.board_range(4)
     st = O.rollout_batch(seed, 0, 4, 60, threads=1)  # this rank's shard, local board ids
     r.barrier()
-    out[rank] = dict(seed=seed, range=(b0, b1), steps=int(st[0]), tmax=r.max(float(rank + 1)),
-                     ssum=r.sum(float(st[0])))
+    res = dict(seed=seed, range=(b0, b1), steps=int(st[0]), tmax=r.max(float(rank + 1)), ssum=r.sum(float(st[0])),
+               device=rp.device, mode=r.mode)
+    # many rounds back to back: a fast rank may run one round ahead of a slow one
+    acc = [r.sum(float(k * (rank + 1))) for k in range(50)]
+    res["acc_ok"] = acc == [float(3 * k) for k in range(50)]
     r.close()
+    out.put((rank, res))
 
 
-def test_two_rank_replicas():
+@pytest.mark.parametrize("backend", ["file", "gloo"])
+def test_two_rank_replicas(backend):
     world = 2
     port = _free_port()
-    mgr = mp.Manager()
-    out = mgr.dict()
-    mp.spawn(_worker, args=(world, port, out), nprocs=world, join=True)
-    res = [out[r] for r in range(world)]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, backend, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    got = dict(q.get(timeout=300) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res = [got[r] for r in range(world)]
+    assert res[0]["mode"] == "processes" and [x["device"] for x in res] == [0, 1]
     assert res[0]["seed"] != res[1]["seed"]
     assert res[0]["range"] == (0, 4) and res[1]["range"] == (4, 8)
     assert res[0]["tmax"] == res[1]["tmax"] == 2.0
     assert res[0]["ssum"] == res[1]["ssum"] == res[0]["steps"] + res[1]["steps"]
+    assert res[0]["acc_ok"] and res[1]["acc_ok"]
     # independence: rank 1's shard equals what a lone process with rank 1's seed computes
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
@@ -55,12 +77,57 @@ def test_two_rank_replicas():
     assert int(O.rollout_batch(res[1]["seed"], 0, 4, 60, threads=1)[0]) == res[1]["steps"]
 
 
-def test_single_process_defaults():
+def test_gpus_mismatch_with_launcher(monkeypatch):
     sys.path.insert(0, os.path.join(ROOT, "gym-chess_amd"))
     from gym_chess_amd.replicas import Replicas
 
-    r = Replicas(world_size=1, rank=0, local_rank=0).init()
-    assert r.board_seed(7) == 7 and r.max(3.5) == 3.5 and r.sum(2.0) == 2.0
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    with pytest.raises(ValueError):
+        Replicas(gpus=8)
+
+
+def test_threaded_replicas(monkeypatch):
+    """--gpus 3 in one process: one thread per replica on devices 0..2, the oracle standing in
+    for each replica's device work; results in replica order == the same work done serially."""
+    sys.path.insert(0, os.path.join(ROOT, "gym-chess_amd"))
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        monkeypatch.delenv(k, raising=False)
+    from gym_chess_amd.replicas import Replicas
+    import oracle as O
+
+    r = Replicas(gpus=3).init()
+    assert r.mode == "threads" and r.world_size == 3 and [x.device for x in r.local] == [0, 1, 2]
+
+    def work(rp):
+        t0 = time.perf_counter()
+        st = O.rollout_batch(rp.board_seed(0x5EED), 0, 4, 60, threads=1)
+        return (rp.index, int(st[0])), time.perf_counter() - t0
+
+    res, dt = r.timed(work)
+    assert [x[0] for x in res] == [0, 1, 2] and dt > 0
+    serial = [int(O.rollout_batch(rp.board_seed(0x5EED), 0, 4, 60, threads=1)[0]) for rp in r.local]
+    assert [x[1] for x in res] == serial
+    assert r.sum(5.0) == 5.0 and r.max(2.0) == 2.0  # one process: nothing to reduce across
+
+    def boom(rp):
+        if rp.index == 1:
+            raise RuntimeError("replica 1 failed")
+        return rp.index
+
+    with pytest.raises(RuntimeError, match="replica 1"):
+        r.run(boom)
+    r.close()
+
+
+def test_single_process_defaults(monkeypatch):
+    sys.path.insert(0, os.path.join(ROOT, "gym-chess_amd"))
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        monkeypatch.delenv(k, raising=False)
+    from gym_chess_amd.replicas import Replica, Replicas
+
+    r = Replicas().init()
+    assert r.world_size == 1 and r.local[0].board_seed(7) == 7 and r.max(3.5) == 3.5 and r.sum(2.0) == 2.0
     r.barrier()
     r.close()
-    assert np.uint64(Replicas(world_size=8, rank=7).board_seed(1)) == np.uint64(1 + (7 << 40))
+    assert np.uint64(Replica(7, 0).board_seed(1)) == np.uint64(1 + (7 << 40))

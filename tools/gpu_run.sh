@@ -15,16 +15,24 @@ step() {
   tail -5 "$OUT/$name.log"
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP after $name rc=$rc"; exit $rc; fi
 }
+# PMC passes time the bench's own steady-state launches (bench defaults: --settle 1000
+# --warmup 50), 20 of them; one counter group per pass (rocprofv3 does not split passes)
+PMCB="python bench.py --no-cpu-baseline --steps 20 --fused-plies 0 --perft-roots 0 --variant-steps 0"
+# perft passes: the bench's perft leg (65 536 mid-game FEN roots, perft(5)) without the step legs
+PERFTB="python bench.py --no-cpu-baseline --steps 5 --warmup 5 --settle 0 --fused-plies 0 --variant-steps 0 --oracle-perft-roots 0"
 for s in ${STEPS:-smoke pytest bench prof}; do
   case $s in
     smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    pytest) step pytest 1200 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread ;;
+    pytest) step pytest 1100 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread ;;
     bench)  step bench 600 python bench.py ${BENCH_ARGS:-} ;;
-    prof)   step prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --no-cpu-baseline --perft-roots 4096 ;;  # bench defaults: the same launches bench.py times
-    pmcf)   step pmcf 600 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 20 --warmup 400 --fused-plies 0 --perft-roots 0 ;;
-    pmcw)   step pmcw 600 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 20 --warmup 400 --fused-plies 0 --perft-roots 0 ;;
-    pmcv)   step pmcv 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU -d $OUT/pmc_valu -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 20 --warmup 400 --fused-plies 0 --perft-roots 0 ;;
-    pmcm)   step pmcm 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VALU2 SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d $OUT/pmc_mix -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 20 --warmup 400 --fused-plies 0 --perft-roots 0 ;;
+    prof)   step prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --no-cpu-baseline --oracle-perft-roots 0 ;;  # bench defaults: the same launches bench.py times
+    pmcf)   step pmcf 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-format csv -- $PMCB ;;
+    pmcw)   step pmcw 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run --output-format csv -- $PMCB ;;
+    pmcv)   step pmcv 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU -d $OUT/pmc_valu -o run --output-format csv -- $PMCB ;;
+    pmcm)   step pmcm 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VALU2 SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d $OUT/pmc_mix -o run --output-format csv -- $PMCB ;;
+    pmcpf)  step pmcpf 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_perft_fetch -o run --output-format csv -- $PERFTB ;;
+    pmcpw)  step pmcpw 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_perft_write -o run --output-format csv -- $PERFTB ;;
+    pmcpm)  step pmcpm 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES -d $OUT/pmc_perft_mix -o run --output-format csv -- $PERFTB ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
