@@ -122,7 +122,7 @@ def perft_leg(args, rep):
     depth and must match exactly; at N=1 that run is also the perft CPU baseline."""
     import numpy as np
 
-    from gym_chess_amd.engine import Engine, perft_path_counts
+    from gym_chess_amd.engine import Engine, perft_leaf_stats, perft_path_counts
     from gym_chess_amd.fen import fen_to_arrays
 
     def prep(rp):
@@ -137,6 +137,7 @@ def perft_leg(args, rep):
 
     ctx = rep.run(prep)
     paths0 = perft_path_counts()
+    leaf0 = perft_leaf_stats()
 
     def run(rp):
         eng, b, m = ctx[rep.local.index(rp)]
@@ -146,6 +147,7 @@ def perft_leg(args, rep):
 
     res, dtm = rep.timed(run)
     paths1 = perft_path_counts()
+    leaf1 = perft_leaf_stats()
     for eng, _, _ in ctx:
         eng.close()
     tot = rep.sum(float(sum(float(r.sum()) for r in res)))
@@ -157,6 +159,25 @@ def perft_leg(args, rep):
            "nodes": tot, "seconds": dtm,
            "leaf_pass": {k: paths1[k] - paths0[k] for k in paths0},
            "roots_with": {"castle_right": castle, "pawn_on_7th": prom, "side_in_check": check}}
+    # the leaf kernel (k_perft2_perm: one lane = one depth-2 subtree, last ply bulk-counted):
+    # where the time goes.  It is VALU-bound -- 72 algorithmic HBM bytes per subtree (root
+    # state + index in, count out) against ~1e3 leaves -- so its roof is the VALU issue rate:
+    # busy_frac and lane use from the PMC profile (tools/gpu_run.sh pmcp*)
+    la, sub, kms = (b - a for a, b in zip(leaf0, leaf1))
+    if la:
+        roof = {"bound": "valu", "kernel": "k_perft2_perm", "launches": la, "subtrees": sub,
+                "kernel_ms": kms, "share_of_perft_time": kms / 1e3 / len(rep.local) / dtm,
+                "alg_bytes_per_subtree": 72, "hbm_achieved_gbs": 72.0 * sub / (kms / 1e3) / 1e9}
+        pf = os.path.join(ROOT, "profiles", "pmc_perft_latest.json")
+        if os.path.exists(pf):
+            try:
+                pm = json.load(open(pf))
+                roof["valu"] = pm.get("valu")
+                roof["traffic_bytes_per_subtree"] = pm.get("hbm_bytes_per_subtree")
+                roof["pmc_source"] = {"file": os.path.relpath(pf, ROOT), "profile": pm.get("profile")}
+            except (OSError, ValueError):
+                pass
+        out["roofline"] = roof
     k = min(args.oracle_perft_roots, args.perft_roots)
     if rep.rank == 0 and k > 0:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))

@@ -1304,9 +1304,17 @@ extern "C" int gc_engine_update_state(gc_engine* e, int n, const int8_t* boards,
 // (it is ~30x larger) and its nodes run in order of their move counts, so the leaf kernel's
 // one remaining loop has (nearly) equal trip counts across a wave -- with depth-3 subtrees
 // the inner loop's trip count varied per lane (PMC: ~60 % lane utilisation).
+// leaf-kernel time of the split pass (gc_perft_leaf_stats): HIP events around every
+// k_perft2_perm launch, on the stream it runs on; summed once the pass has synchronised
+static std::mutex g_leaf_mu;
+static uint64_t g_leaf_launches = 0, g_leaf_subtrees = 0;
+static double g_leaf_ms = 0.0;
+
 static int perft_split_leaves(hipStream_t st, SoA leaf, uint64_t* leaf_out) {
     const int64_t cap = (int64_t)1 << 27;  // children per chunk (7.5 GiB of boards)
     int chunk = 1 << 21;
+    std::vector<hipEvent_t> evs;  // pairs around the leaf launches
+    uint64_t subtrees = 0;
     int32_t *kc = nullptr, *offs = nullptr, *kc2 = nullptr, *ks = nullptr, *ix = nullptr, *is = nullptr;
     u64* cb = nullptr;
     u32* cm = nullptr;
@@ -1318,6 +1326,7 @@ static int perft_split_leaves(hipStream_t st, SoA leaf, uint64_t* leaf_out) {
     auto done = [&]() {
         void* ps[] = {kc, offs, kc2, ks, ix, is, cb, cm, cval, tmp};
         for (void* q : ps) (void)hipFree(q);
+        for (hipEvent_t ev : evs) (void)hipEventDestroy(ev);
     };
     if (dalloc(&kc, leaf.n) || dalloc(&offs, chunk) || dalloc(&kc2, cap) || dalloc(&ks, cap) || dalloc(&ix, cap) ||
         dalloc(&is, cap) || dalloc(&cb, (size_t)NBB * cap) || dalloc(&cm, cap) || dalloc(&cval, cap)) {
@@ -1352,7 +1361,13 @@ static int perft_split_leaves(hipStream_t st, SoA leaf, uint64_t* leaf_out) {
             tb = tmp_bytes;
             he = hipcub::DeviceRadixSort::SortPairs(tmp, tb, kc2, ks, ix, is, (int)total, 0, 10, st);
             if (he != hipSuccess) { err = std::string("perft split sort: ") + hipGetErrorString(he); rc = -1; break; }
+            hipEvent_t e0 = nullptr, e1 = nullptr;
+            if (hipEventCreate(&e0) == hipSuccess) evs.push_back(e0);
+            if (hipEventCreate(&e1) == hipSuccess) evs.push_back(e1);
+            if (e0 && e1) (void)hipEventRecord(e0, st);
             k_perft2_perm<<<grid_for((int)total), BLOCK, 0, st>>>(ch, is, cval);
+            if (e0 && e1) (void)hipEventRecord(e1, st);
+            subtrees += (uint64_t)total;
         }
         k_sum_children<int32_t><<<grid_for(c), BLOCK, 0, st>>>(offs, kc + a, cval, c, leaf_out + a);
         he = hipGetLastError();
@@ -1361,6 +1376,17 @@ static int perft_split_leaves(hipStream_t st, SoA leaf, uint64_t* leaf_out) {
     }
     hipError_t he = hipStreamSynchronize(st);  // before the buffers are freed
     if (rc == 0 && he != hipSuccess) { err = std::string("perft split: ") + hipGetErrorString(he); rc = -1; }
+    if (rc == 0) {
+        double ms = 0.0;
+        for (size_t k = 0; k + 1 < evs.size(); k += 2) {
+            float t = 0.f;
+            if (hipEventElapsedTime(&t, evs[k], evs[k + 1]) == hipSuccess) ms += t;
+        }
+        std::lock_guard<std::mutex> lk(g_leaf_mu);
+        g_leaf_launches += evs.size() / 2;
+        g_leaf_subtrees += subtrees;
+        g_leaf_ms += ms;
+    }
     done();
     return rc ? fail(err) : 0;
 }
@@ -1495,6 +1521,15 @@ static int perft_device(hipStream_t st, SoA roots, int depth, uint64_t* d_out, i
 extern "C" int gc_perft_path_counts(uint64_t* out4) {
     if (!out4) return fail("null argument");
     for (int k = 0; k < 4; k++) out4[k] = g_perft_path[k].load();
+    return 0;
+}
+
+extern "C" int gc_perft_leaf_stats(uint64_t* launches, uint64_t* subtrees, double* kernel_ms) {
+    if (!launches || !subtrees || !kernel_ms) return fail("null argument");
+    std::lock_guard<std::mutex> lk(g_leaf_mu);
+    *launches = g_leaf_launches;
+    *subtrees = g_leaf_subtrees;
+    *kernel_ms = g_leaf_ms;
     return 0;
 }
 
@@ -2103,6 +2138,226 @@ extern "C" int gc_debug_stamps(gc_env* e, int n_plies, uint64_t* out /* (n/64)*8
     return 0;
 }
 #endif
+
+// ----------------------------------------------------------------------------- checkpoint
+// Bit-exact save / restore of a whole env (SURVEY.md §5 "save/load = memcpy of state +
+// repetition history"; the reference keeps its history in ChessEnvV2.saved_boards,
+// chess_v2.py:192, 404-407, beside the state dict, 301-323).  Blob layout:
+//   CkptHeader | slab (Slab::BYTES_PER_BOARD * n: bitboards, meta, window generation, Philox
+//   draw counter, step counter, last outputs, next action) | the live window entries, board
+//   by board (hl_of(meta[i]) entries of 8 u64: header {tag | count << 56}, 7 bitboards).
+// Only live entries travel (<= ~301 per board, not the table): restoring re-inserts them
+// under a fresh generation, so a restored board answers every later probe exactly as before
+// (same boards, same counts; slot positions may differ, which no result depends on).
+struct CkptHeader {
+    char magic[8];  // "GCCKPT1"
+    uint32_t version, n, rules, opp, agent_black, policy_ready;
+    uint64_t seed;
+    uint64_t init[NBB];  // the env's initial board (resets land on it)
+    uint64_t entries;
+};
+static const char CKPT_MAGIC[8] = {'G', 'C', 'C', 'K', 'P', 'T', '1', 0};
+
+__global__ void k_hl_of(const u32* __restrict__ meta, int n, uint32_t* __restrict__ hl) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) hl[i] = hl_of(meta[i]);
+}
+
+// the live entries (generation == hgen[i]) of board i, in table order, at out[offs[i]..]
+__global__ void k_ckpt_pack(const u64* __restrict__ htab, const u32* __restrict__ hgen, const u32* __restrict__ meta,
+                            int n, const uint32_t* __restrict__ offs, u64* __restrict__ out, uint32_t* __restrict__ bad) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    DevHist h{const_cast<u64*>(htab), const_cast<u32*>(hgen), hgen[i], i};
+    const u32 g = h.gen(), hl = hl_of(meta[i]);
+    u32 k = 0;
+    u64* o = out + (size_t)offs[i] * 8;
+    for (int pos = 0; pos < HTAB; pos++) {
+        const u64* e = htab + h.entry(pos) * 8;
+        u64 hdr = e[0];
+        if ((u32)hdr != g) continue;
+        if (k < hl) {
+            u64* d = o + (size_t)k * 8;
+            d[0] = hdr & ~0xFFFFFFFFull;  // tag | count; the generation is re-issued on restore
+#pragma unroll
+            for (int j = 1; j < 8; j++) d[j] = e[j];
+        }
+        k++;
+    }
+    if (k != hl) atomicOr(bad, 1u);
+}
+
+// fresh generation per board: above both the live table's and the saved one, so no entry of
+// the live table can pass for a restored one
+__global__ void k_ckpt_gen(const u32* __restrict__ live_hgen, const u32* __restrict__ saved_hgen, int n,
+                           uint32_t* __restrict__ gnew) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) gnew[i] = (live_hgen[i] > saved_hgen[i] ? live_hgen[i] : saved_hgen[i]) + 1u;
+}
+
+// board i takes generation gnew[i] and its saved entries are inserted by the probe rule of
+// rep_commit (gc_env.h): home slot = key & (HTAB-1), linear probing
+__global__ void k_ckpt_unpack(u64* __restrict__ htab, u32* __restrict__ hgen, const u32* __restrict__ meta, int n,
+                              const uint32_t* __restrict__ gnew, const uint32_t* __restrict__ offs,
+                              const u64* __restrict__ in, uint32_t* __restrict__ bad) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const u32 g = gnew[i];
+    hgen[i] = g;
+    DevHist h{htab, hgen, g, i};
+    const u32 hl = hl_of(meta[i]);
+    for (u32 k = 0; k < hl; k++) {
+        const u64* e = in + ((size_t)offs[i] + k) * 8;
+        Pos b = {e[1], e[2], e[3], e[4], e[5], e[6], e[7], 0};
+        u32 key = board_key(b);
+        u32 pos = key & (HTAB - 1), tag = key >> HTAB_BITS;
+        int probe = 0;
+        while ((u32)htab[h.entry((int)pos) * 8] == g && probe < HTAB) { pos = (pos + 1) & (HTAB - 1); probe++; }
+        if (probe == HTAB) { atomicOr(bad, 2u); return; }
+        u64* d = htab + h.entry((int)pos) * 8;
+        d[0] = (u64)g | ((u64)tag << 32) | (e[0] & (0xFFull << 56));
+#pragma unroll
+        for (int j = 1; j < 8; j++) d[j] = e[j];
+    }
+}
+
+// exclusive scan of the window lengths of `meta` (the saved or live slab's) -> offs; returns
+// the total entry count
+static int ckpt_offsets(gc_env* e, const u32* meta, uint32_t* hl, uint32_t* offs, uint64_t* total) {
+    const int n = e->n;
+    k_hl_of<<<grid_for(n), BLOCK, 0, e->stream>>>(meta, n, hl);
+    size_t tb = 0;
+    void* tmp = nullptr;
+    hipError_t he = hipcub::DeviceScan::ExclusiveSum(nullptr, tb, hl, offs, n, e->stream);
+    if (he == hipSuccess && dalloc((char**)&tmp, tb ? tb : 1)) return -1;
+    if (he == hipSuccess) he = hipcub::DeviceScan::ExclusiveSum(tmp, tb, hl, offs, n, e->stream);
+    uint32_t lo = 0, lc = 0;
+    if (he == hipSuccess) he = hipMemcpyAsync(&lo, offs + n - 1, 4, hipMemcpyDeviceToHost, e->stream);
+    if (he == hipSuccess) he = hipMemcpyAsync(&lc, hl + n - 1, 4, hipMemcpyDeviceToHost, e->stream);
+    if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
+    (void)hipFree(tmp);
+    if (he != hipSuccess) return fail(std::string("checkpoint scan: ") + hipGetErrorString(he));
+    *total = (uint64_t)lo + lc;
+    return 0;
+}
+
+static size_t ckpt_bytes(int n, uint64_t entries) {
+    return sizeof(CkptHeader) + Slab::BYTES_PER_BOARD * (size_t)n + 64 * (size_t)entries;
+}
+
+extern "C" int gc_env_checkpoint_bytes(gc_env* e, uint64_t* bytes) {
+    if (!e || !bytes) return fail("null argument");
+    HIPCHK(hipSetDevice(e->device));
+    uint32_t *hl = nullptr, *offs = nullptr;
+    if (dalloc(&hl, e->n) || dalloc(&offs, e->n)) { (void)hipFree(hl); return -1; }
+    uint64_t total = 0;
+    int rc = ckpt_offsets(e, e->meta, hl, offs, &total);
+    (void)hipFree(hl); (void)hipFree(offs);
+    if (rc) return rc;
+    *bytes = ckpt_bytes(e->n, total);
+    return 0;
+}
+
+extern "C" int gc_env_save(gc_env* e, void* buf, uint64_t cap, uint64_t* written) {
+    if (!e || !buf) return fail("null argument");
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    const int n = e->n;
+    uint32_t *hl = nullptr, *offs = nullptr, *bad = nullptr;
+    u64* ents = nullptr;
+    auto release = [&]() { (void)hipFree(hl); (void)hipFree(offs); (void)hipFree(bad); (void)hipFree(ents); };
+    if (dalloc(&hl, n) || dalloc(&offs, n) || dalloc(&bad, 1)) { release(); return -1; }
+    uint64_t total = 0;
+    if (ckpt_offsets(e, e->meta, hl, offs, &total)) { release(); return -1; }
+    const size_t need = ckpt_bytes(n, total);
+    if (written) *written = need;
+    if (cap < need) { release(); return fail("checkpoint buffer too small: need " + std::to_string(need) + " bytes"); }
+    if (dalloc(&ents, 8 * (total ? total : 1))) { release(); return -1; }
+    CkptHeader hd = {};
+    memcpy(hd.magic, CKPT_MAGIC, 8);
+    hd.version = 1; hd.n = (uint32_t)n; hd.rules = (uint32_t)e->rules; hd.opp = (uint32_t)e->d.opp;
+    hd.agent_black = (uint32_t)e->d.agent_black; hd.policy_ready = e->policy_ready ? 1u : 0u;
+    hd.seed = e->seed;
+    for (int j = 0; j < NBB; j++) hd.init[j] = e->d.init[j];
+    hd.entries = total;
+    uint8_t* out = static_cast<uint8_t*>(buf);
+    memcpy(out, &hd, sizeof hd);
+    uint32_t flag = 0;
+    hipError_t he = hipMemsetAsync(bad, 0, 4, e->stream);
+    if (he == hipSuccess) {
+        k_ckpt_pack<<<grid_for(n), BLOCK, 0, e->stream>>>(e->d.htab, e->d.hgen, e->meta, n, offs, ents, bad);
+        he = hipGetLastError();
+    }
+    if (he == hipSuccess)
+        he = hipMemcpyAsync(out + sizeof hd, e->slab, Slab::BYTES_PER_BOARD * (size_t)n, hipMemcpyDeviceToHost, e->stream);
+    if (he == hipSuccess && total)
+        he = hipMemcpyAsync(out + sizeof hd + Slab::BYTES_PER_BOARD * (size_t)n, ents, 64 * total, hipMemcpyDeviceToHost,
+                            e->stream);
+    if (he == hipSuccess) he = hipMemcpyAsync(&flag, bad, 4, hipMemcpyDeviceToHost, e->stream);
+    if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
+    release();
+    if (he != hipSuccess) return fail(std::string("checkpoint save: ") + hipGetErrorString(he));
+    if (flag) return fail("checkpoint save: a repetition window does not match its recorded length");
+    return 0;
+}
+
+extern "C" int gc_env_load(gc_env* e, const void* buf, uint64_t size) {
+    if (!e || !buf) return fail("null argument");
+    if (size < sizeof(CkptHeader)) return fail("checkpoint: truncated header");
+    CkptHeader hd;
+    memcpy(&hd, buf, sizeof hd);
+    if (memcmp(hd.magic, CKPT_MAGIC, 8) != 0 || hd.version != 1) return fail("checkpoint: not a gc_env checkpoint (v1)");
+    if ((int)hd.n != e->n) return fail("checkpoint: it holds " + std::to_string(hd.n) + " boards, the env " + std::to_string(e->n));
+    if ((int)hd.rules != e->rules || (int)hd.opp != e->d.opp || (int)hd.agent_black != e->d.agent_black)
+        return fail("checkpoint: rules / opponent / player colour differ from the env's");
+    if (hd.seed != e->seed) return fail("checkpoint: the env's seed differs (the policy streams would not continue)");
+    for (int j = 0; j < NBB; j++)
+        if (hd.init[j] != e->d.init[j]) return fail("checkpoint: the env's initial board differs");
+    if (size != ckpt_bytes(e->n, hd.entries)) return fail("checkpoint: size does not match its header");
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    const int n = e->n;
+    const uint8_t* in = static_cast<const uint8_t*>(buf);
+    uint8_t* slab = nullptr;
+    u64* ents = nullptr;
+    uint32_t *hl = nullptr, *offs = nullptr, *gnew = nullptr, *bad = nullptr;
+    auto release = [&]() {
+        (void)hipFree(slab); (void)hipFree(ents); (void)hipFree(hl); (void)hipFree(offs); (void)hipFree(gnew);
+        (void)hipFree(bad);
+    };
+    if (dalloc(&slab, Slab::BYTES_PER_BOARD * (size_t)n) || dalloc(&ents, 8 * (hd.entries ? hd.entries : 1)) ||
+        dalloc(&hl, n) || dalloc(&offs, n) || dalloc(&gnew, n) || dalloc(&bad, 1)) {
+        release();
+        return -1;
+    }
+    hipError_t he = hipMemcpyAsync(slab, in + sizeof hd, Slab::BYTES_PER_BOARD * (size_t)n, hipMemcpyHostToDevice, e->stream);
+    if (he == hipSuccess && hd.entries)
+        he = hipMemcpyAsync(ents, in + sizeof hd + Slab::BYTES_PER_BOARD * (size_t)n, 64 * hd.entries,
+                            hipMemcpyHostToDevice, e->stream);
+    if (he != hipSuccess) { release(); return fail(std::string("checkpoint load: ") + hipGetErrorString(he)); }
+    uint64_t total = 0;
+    const u32* smeta = reinterpret_cast<const u32*>(slab + Slab::meta(n));
+    if (ckpt_offsets(e, smeta, hl, offs, &total)) { release(); return -1; }
+    if (total != hd.entries) { release(); return fail("checkpoint: window lengths do not match the entries it holds"); }
+    k_ckpt_gen<<<grid_for(n), BLOCK, 0, e->stream>>>(e->d.hgen, reinterpret_cast<const u32*>(slab + Slab::hgen(n)), n,
+                                                     gnew);
+    he = hipGetLastError();
+    if (he == hipSuccess)
+        he = hipMemcpyAsync(e->slab, slab, Slab::BYTES_PER_BOARD * (size_t)n, hipMemcpyDeviceToDevice, e->stream);
+    if (he == hipSuccess) he = hipMemsetAsync(bad, 0, 4, e->stream);
+    if (he == hipSuccess) {
+        k_ckpt_unpack<<<grid_for(n), BLOCK, 0, e->stream>>>(e->d.htab, e->d.hgen, e->meta, n, gnew, offs, ents, bad);
+        he = hipGetLastError();
+    }
+    uint32_t flag = 0;
+    if (he == hipSuccess) he = hipMemcpyAsync(&flag, bad, 4, hipMemcpyDeviceToHost, e->stream);
+    if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
+    release();
+    if (he != hipSuccess) return fail(std::string("checkpoint load: ") + hipGetErrorString(he));
+    if (flag) return fail("checkpoint load: a repetition window does not fit the table");
+    e->policy_ready = hd.policy_ready != 0;
+    return 0;
+}
 
 // bytes of device memory held by the env (for reports)
 extern "C" uint64_t gc_env_device_bytes(gc_env* e) {

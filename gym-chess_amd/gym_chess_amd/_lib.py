@@ -26,6 +26,7 @@ SIGNATURES = {
     "gc_engine_update_state": (_I, [_P, _I, _P, _P, _P, _P]),
     "gc_engine_perft": (_I, [_P, _I, _P, _P, _I, _P]),
     "gc_perft_path_counts": (_I, [_P]),
+    "gc_perft_leaf_stats": (_I, [_P, _P, _P]),
     "gc_engine_set_rules": (_I, [_P, _I]),
     "gc_env_create": (_I, [_I, _I, _U64, _P, _P]),
     "gc_env_destroy": (_I, [_P]),
@@ -52,6 +53,9 @@ SIGNATURES = {
     "gc_env_elapsed_ms": (_I, [_P, _I, _I, _P]),
     "gc_env_device_bytes": (_U64, [_P]),
     "gc_env_window_sum": (_I, [_P, _P]),
+    "gc_env_checkpoint_bytes": (_I, [_P, _P]),
+    "gc_env_save": (_I, [_P, _P, _U64, _P]),
+    "gc_env_load": (_I, [_P, _P, _U64]),
 }
 
 _lib = None

@@ -167,3 +167,10 @@ class ChessEngine:
             return C.player_to_white(player)
         except ValueError as ex:  # lib.rs:433-437
             raise SystemError(str(ex)) from None
+
+
+def perft_leaf_stats():
+    """Diagnostics: the split pass's leaf kernel in this process -> (launches, subtrees, kernel ms)."""
+    la, st, ms = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_double()
+    _lib.check(_lib.load().gc_perft_leaf_stats(ctypes.byref(la), ctypes.byref(st), ctypes.byref(ms)))
+    return int(la.value), int(st.value), float(ms.value)

@@ -209,6 +209,30 @@ class BatchedChessEnv:
     def device_bytes(self):
         return int(self._L.gc_env_device_bytes(self._h))
 
+    # ------------------------------------------------------------------ checkpoint / resume
+    def checkpoint(self):
+        """The whole env as bytes (gc_env_save): states, move counts, done flags, 3-fold
+        windows, policy streams, step counters.  load() on an env built with the same
+        arguments continues exactly as this one would."""
+        need = ctypes.c_uint64()
+        _lib.check(self._L.gc_env_checkpoint_bytes(self._h, ctypes.byref(need)))
+        buf = np.zeros(need.value, dtype=np.uint8)
+        wr = ctypes.c_uint64()
+        _lib.check(self._L.gc_env_save(self._h, _lib.ptr(buf), ctypes.c_uint64(buf.size), ctypes.byref(wr)))
+        return buf[: wr.value].tobytes()
+
+    def load(self, blob):
+        a = np.frombuffer(blob, dtype=np.uint8)
+        _lib.check(self._L.gc_env_load(self._h, _lib.ptr(a), ctypes.c_uint64(a.size)))
+
+    def save_to(self, path):
+        with open(path, "wb") as f:
+            f.write(self.checkpoint())
+
+    def load_from(self, path):
+        with open(path, "rb") as f:
+            self.load(f.read())
+
 
 class MultiDeviceChessEnv:
     """`device_ids` form of the batched env (SURVEY.md §5 Config, §8e): num_boards boards per

@@ -67,6 +67,9 @@ int gc_engine_perft(gc_engine* e, int n, const int8_t* boards, const uint8_t* me
  * (depth-3 subtrees split to depth-2, sorted), sorted (subtrees by move count), small
  * (unsorted nested loops), fide} */
 int gc_perft_path_counts(uint64_t* out4);
+/* diagnostics: the split pass's leaf kernel (k_perft2_perm, one lane = one depth-2 subtree)
+ * in this process -- launches, subtrees and summed kernel time (HIP events on its stream) */
+int gc_perft_leaf_stats(uint64_t* launches, uint64_t* subtrees, double* kernel_ms);
 /* Rules of every later call on this engine (not in the reference):
  * 0 = the reference's (default, lib.rs), 1 = FIDE (gym-chess_amd/csrc/gc_fide.h: en passant,
  * promotion, per-side castling through unattacked squares, no king captures).  Under FIDE
@@ -134,6 +137,17 @@ int gc_env_set_rules(gc_env* e, int rules);
 /* set every board from a FEN (n strings); check flags from update_state (lib.rs:1386-1393);
  * repetition windows cleared */
 int gc_env_set_fens(gc_env* e, const char* const* fens);
+/* Bit-exact checkpoint / resume of the whole env (replaces ChessEnvV2's state dict getter /
+ * setter, chess_v2.py:301-323, PLUS what it leaves out: the 3-fold history saved_boards
+ * (192, 404-407), move_count, done, the policy streams and step counters).  The blob is
+ * self-describing (header, per-board slab, the live repetition-window entries; ~80 B/board
+ * + 64 B per window entry).  gc_env_load needs an env of the same size, rules, opponent mode,
+ * player colour, seed and initial board; a loaded env continues exactly as the saved one
+ * would have.  gc_env_save: cap = buffer size, *written = the bytes needed (also on a
+ * too-small buffer). */
+int gc_env_checkpoint_bytes(gc_env* e, uint64_t* bytes);
+int gc_env_save(gc_env* e, void* buf, uint64_t cap, uint64_t* written);
+int gc_env_load(gc_env* e, const void* buf, uint64_t size);
 /* HIP events on the env's stream (8 slots) for in-process kernel timing */
 int gc_env_record_event(gc_env* e, int slot);
 int gc_env_elapsed_ms(gc_env* e, int a, int b, float* ms);

@@ -30,7 +30,11 @@ def main():
     ap.add_argument("--last", type=int, default=20)
     ap.add_argument("--boards", type=int, default=65536)
     ap.add_argument("--alg-bytes-per-board", type=int, default=282)
+    ap.add_argument("--perft", action="store_true",
+                    help="perft leaf kernel (k_perft2_perm) passes pmc_perft_{fetch,write,mix} -> pmc_perft.json")
     a = ap.parse_args()
+    if a.perft:
+        return perft_summary(a)
     mean = lambda rows, k: sum(r[k] for r in rows) / len(rows)  # noqa: E731
     f = per_dispatch(os.path.join(a.src, "pmc_fetch/run_counter_collection.csv"), a.kernel)[-a.last:]
     w = per_dispatch(os.path.join(a.src, "pmc_write/run_counter_collection.csv"), a.kernel)[-a.last:]
@@ -60,9 +64,54 @@ def main():
             "note": "busy_frac = SQ_ACTIVE_INST_VALU x 4 cycles / (SQ_BUSY_CYCLES x SIMDs per SE), whole launch "
                     "incl. ramp and tail; lane_utilisation = active lanes per VALU instruction / 64",
         }
+    bl = bench_line(os.path.join(a.src, "pmcf.log"))
+    if bl:  # the steady state the counters describe
+        out["mean_window"] = bl["roofline"]["mean_window"]
+        out["settle_plies"] = bl["config"].get("settle_plies")
+    out["profile"] = os.path.basename(a.dst.rstrip("/"))
     os.makedirs(a.dst, exist_ok=True)
     for p in (os.path.join(a.dst, "pmc_traffic.json"), os.path.join(os.path.dirname(a.dst.rstrip("/")),
                                                                        "pmc_traffic_latest.json")):
+        json.dump(out, open(p, "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+def bench_line(path):
+    try:
+        for ln in reversed(open(path).read().splitlines()):
+            if ln.startswith("{"):
+                return json.loads(ln)
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def perft_summary(a):
+    """k_perft2_perm (the split leaf pass: one lane = one depth-2 subtree, bulk-counted last
+    ply) over the bench's perft leg.  Per launch: HBM bytes (FETCH_SIZE x2 + WRITE_SIZE),
+    VALU instructions per wave, lane utilisation, VALU busy fraction.  Algorithmic bytes per
+    subtree: the root's 7 bitboards + meta (60) + its permutation index (4) read, its count
+    (8) written = 72 B; the leaves never touch memory."""
+    kern = "k_perft2_perm"
+    rows = lambda sub: per_dispatch(os.path.join(a.src, sub, "run_counter_collection.csv"), kern)  # noqa: E731
+    f, w, m = rows("pmc_perft_fetch"), rows("pmc_perft_write"), rows("pmc_perft_mix")
+    tot = lambda rs, k: sum(r[k] for r in rs)  # noqa: E731
+    waves = tot(m, "SQ_WAVES")
+    simds_per_se = 1024 / 32
+    out = {"kernel": kern, "launches": len(m),
+           "hbm_bytes_total": tot(f, "FETCH_SIZE") * 1024 * 2 + tot(w, "WRITE_SIZE") * 1024,
+           "subtrees_total": waves * 64,
+           "alg_bytes_per_subtree": 72,
+           "valu": {"insts_per_wave": tot(m, "SQ_INSTS_VALU") / waves,
+                    "lane_utilisation": tot(m, "SQ_THREAD_CYCLES_VALU") / (tot(m, "SQ_ACTIVE_INST_VALU") * 64),
+                    "busy_frac": tot(m, "SQ_ACTIVE_INST_VALU") * 4 / (tot(m, "SQ_BUSY_CYCLES") * simds_per_se),
+                    "lds_insts_per_wave": tot(m, "SQ_INSTS_LDS") / waves,
+                    "salu_insts_per_wave": tot(m, "SQ_INSTS_SALU") / waves},
+           "profile": os.path.basename(a.dst.rstrip("/"))}
+    out["hbm_bytes_per_subtree"] = out["hbm_bytes_total"] / max(out["subtrees_total"], 1)
+    os.makedirs(a.dst, exist_ok=True)
+    for p in (os.path.join(a.dst, "pmc_perft.json"), os.path.join(os.path.dirname(a.dst.rstrip("/")),
+                                                                   "pmc_perft_latest.json")):
         json.dump(out, open(p, "w"), indent=1)
     print(json.dumps(out, indent=1))
 
