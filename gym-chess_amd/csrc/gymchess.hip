@@ -2139,6 +2139,47 @@ extern "C" int gc_debug_stamps(gc_env* e, int n_plies, uint64_t* out /* (n/64)*8
 }
 #endif
 
+// en passant of the FIDE-rules env (gc_fide.h keeps it in meta bits 25..28; the env's
+// meta8[7] is move_count, so it travels beside the state arrays)
+__global__ void k_get_ep(SoA st, int8_t* __restrict__ files) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= st.n) return;
+    u32 m = st.meta[i];
+    files[i] = (m & gcf::M_EP) ? (int8_t)((m & gcf::M_EP_MASK) >> gcf::M_EP_SHIFT) : (int8_t)-1;
+}
+__global__ void k_set_ep(SoA st, const int8_t* __restrict__ files) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= st.n) return;
+    st.meta[i] = gcf::with_ep(st.meta[i], files[i] < 0 ? -1 : (int)files[i]);
+}
+
+extern "C" int gc_env_get_en_passant(gc_env* e, int8_t* files) {
+    if (!e || !files) return fail("null argument");
+    HIPCHK(hipSetDevice(e->device));
+    if (!e->ep && dalloc(&e->ep, e->n)) return -1;
+    k_get_ep<<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d.st, e->ep);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(files, e->ep, e->n, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return 0;
+}
+
+extern "C" int gc_env_set_en_passant(gc_env* e, const int8_t* files) {
+    if (!e || !files) return fail("null argument");
+    for (int i = 0; i < e->n; i++) {
+        if (files[i] > 7) return fail("en-passant file out of range at index " + std::to_string(i));
+        if (files[i] >= 0 && !e->rules) return fail("en passant exists only under rules=fide (Q3: the reference has none)");
+    }
+    HIPCHK(hipSetDevice(e->device));
+    if (!e->ep && dalloc(&e->ep, e->n)) return -1;
+    HIPCHK(hipMemcpyAsync(e->ep, files, e->n, hipMemcpyHostToDevice, e->stream));
+    k_set_ep<<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d.st, e->ep);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(e->stream));
+    e->policy_ready = false;
+    return 0;
+}
+
 // ----------------------------------------------------------------------------- checkpoint
 // Bit-exact save / restore of a whole env (SURVEY.md §5 "save/load = memcpy of state +
 // repetition history"; the reference keeps its history in ChessEnvV2.saved_boards,

@@ -54,6 +54,8 @@ SIGNATURES = {
     "gc_env_device_bytes": (_U64, [_P]),
     "gc_env_window_sum": (_I, [_P, _P]),
     "gc_env_checkpoint_bytes": (_I, [_P, _P]),
+    "gc_env_get_en_passant": (_I, [_P, _P]),
+    "gc_env_set_en_passant": (_I, [_P, _P]),
     "gc_env_save": (_I, [_P, _P, _U64, _P]),
     "gc_env_load": (_I, [_P, _P, _U64]),
 }

@@ -137,6 +137,10 @@ int gc_env_set_rules(gc_env* e, int rules);
 /* set every board from a FEN (n strings); check flags from update_state (lib.rs:1386-1393);
  * repetition windows cleared */
 int gc_env_set_fens(gc_env* e, const char* const* fens);
+/* Under rules=fide the env's en-passant file per board (-1 = none) travels beside
+ * get_states / set_states (meta8[7] is the env's move_count there).  set: FIDE only. */
+int gc_env_get_en_passant(gc_env* e, int8_t* files);
+int gc_env_set_en_passant(gc_env* e, const int8_t* files);
 /* Bit-exact checkpoint / resume of the whole env (replaces ChessEnvV2's state dict getter /
  * setter, chess_v2.py:301-323, PLUS what it leaves out: the 3-fold history saved_boards
  * (192, 404-407), move_count, done, the policy streams and step counters).  The blob is

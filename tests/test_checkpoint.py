@@ -75,7 +75,7 @@ def test_restored_env_continues_the_oracle_trajectory(oracle):
         want_q = np.array([r["reason"][cut + p] for r in refs])
         want_a = np.array([r["action"][cut + p + 1] for r in refs])
         assert (rw == want_r).all() and (why == want_q).all(), p
-        assert (nxt == np.where(want_a < 0, 0xFFFF, want_a)).all(), p
+        assert (nxt == np.where(want_a < 0, 0xFFFF, want_a).astype(np.uint16)).all(), p
 
 
 def test_knight_shuffle_repetition_survives_restore():

@@ -211,3 +211,30 @@ def test_fide_env_external_steps_and_fens():
     assert (rw == -10).all() and (why == 6).all()  # RESIGN is never a legal action
     with pytest.raises(Exception):
         env.rollout(10)  # no fused rollout under FIDE rules
+
+
+@pytest.mark.gpu
+def test_fide_env_state_round_trips_keep_en_passant():
+    """boards() -> set_states() and fens() -> set_fens() must keep a legal
+    en-passant capture (the env carries the file beside meta8, whose [7] is move_count)."""
+    from gym_chess_amd.env import BatchedChessEnv
+
+    fens = ["8/8/1k6/2b5/2pP4/8/5K2/8 b - d3 0 1", STANDARD[0][0]]
+    ep_cap = 34 * 64 + 43  # c4xd3
+    env = BatchedChessEnv(2, device=0, seed=1, rules="fide")
+    env.set_fens(fens)
+    assert list(env.en_passant()) == [3, -1]
+    out = env.fens()
+    assert out[0].split()[3] == "d3" and out[1].split()[3] == "-"
+    b, m = env.boards()
+    ep = env.en_passant()
+    other = BatchedChessEnv(2, device=0, seed=1, rules="fide")
+    other.set_states(b, m, en_passant=ep)
+    assert ep_cap in other.possible_actions()[0]
+    other.set_fens(out)
+    assert ep_cap in other.possible_actions()[0] and list(other.en_passant()) == [3, -1]
+    other.set_states(b, m)  # without the file: no en passant
+    assert ep_cap not in other.possible_actions()[0]
+    ref = BatchedChessEnv(2, device=0, seed=1)
+    with pytest.raises(Exception):
+        ref.set_states(b, m, en_passant=ep)  # the reference's rules have no en passant (Q3)
