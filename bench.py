@@ -63,6 +63,8 @@ def parse():
     ap.add_argument("--perft-roots", type=int, default=65536, help="perft leg on mid-game FEN roots (0 = skip)")
     ap.add_argument("--variant-steps", type=int, default=300,
                     help="also time step() with opponent='random' and with rules='fide' (SURVEY 8f rows 2, 4; 0 = skip)")
+    ap.add_argument("--api-steps", type=int, default=300,
+                    help="also time the API-shaped step on device buffers (mask + obs out; 0 = skip)")
     ap.add_argument("--perft-depth", type=int, default=5)
     ap.add_argument("--oracle-perft-roots", type=int, default=8,
                     help="roots of the perft leg checked against the oracle at --perft-depth (also its CPU baseline)")
@@ -199,6 +201,55 @@ def perft_leg(args, rep):
     return out
 
 
+# algorithmic bytes per board of one API-shaped step (k_env_step_api): state
+# 120 r/w, action 2, draw / step counter / window generation 24 r/w, window probe 64 + entry
+# write 64, outputs reward / done / reason to the caller and the env 12, the legal-action mask
+# 520 (65 words), observation 64, legal count 4, the pick 2 + the env's act 2
+ALG_BYTES_API = 120 + 2 + 24 + 128 + 12 + 520 + 64 + 4 + 4
+
+
+def api_step_leg(args, rep, n):
+    """The reference's call shape (chess_v2.py:219-294 + possible_actions 333-335) on device
+    buffers: per step an external action per board in (here: the previous step's random-policy
+    pick, so no host round trip), reward / done / reason, the int8 observation, the legal-action
+    mask and count out, auto-reset of finished boards.  One launch of k_env_step_api per step."""
+    from gym_chess_amd.env import BatchedChessEnv
+
+    def setup(rp):
+        env = BatchedChessEnv(n, device=rp.device, seed=rp.board_seed(args.seed + 11))
+        if args.settle > 0:
+            env.rollout(args.settle)
+        io = env.device_io()
+        for _ in range(max(args.warmup, 20)):
+            env.step_device(io, autoreset=True)
+        env.synchronize()
+        return env, io
+
+    ctx = rep.run(setup)
+
+    def run(rp):
+        env, io = ctx[rep.local.index(rp)]
+        t0 = time.perf_counter()
+        env.record_event(4)
+        for _ in range(args.api_steps):
+            env.step_device(io, autoreset=True)
+        env.record_event(5)
+        env.synchronize()
+        return None, time.perf_counter() - t0
+
+    _, dt = rep.timed(run)
+    kms = sum(env.elapsed_ms(4, 5) for env, _ in ctx) / len(ctx)
+    for env, io in ctx:
+        io.close()
+        env.close()
+    avg = kms / 1e3 / args.api_steps
+    ach = n * ALG_BYTES_API / avg / 1e9
+    return {"value": rep.world_size * n * args.api_steps / dt, "unit": "env_steps/s", "steps": args.api_steps,
+            "roofline": {"bound": "hbm", "kernel": "k_env_step_api", "achieved": ach, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "avg_launch_us": avg * 1e6,
+                         "alg_bytes_per_board": ALG_BYTES_API}}
+
+
 def variant_legs(args, rep, n):
     """step() throughput of the SURVEY 8f variants at the same batch: the in-kernel random
     opponent (one step = the agent's ply + the opponent's reply) and FIDE rules.  Same timing
@@ -308,6 +359,8 @@ def main():
                                   "plies_per_launch": args.fused_plies, "kernel_ms": envs[0].elapsed_ms(2, 3)}
     for e in envs:
         e.close()
+    if args.api_steps > 0:
+        extra["api_step"] = api_step_leg(args, rep, n)
     if args.variant_steps > 0:
         extra["variants"] = variant_legs(args, rep, n)
     if args.perft_roots > 0:

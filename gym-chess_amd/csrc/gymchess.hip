@@ -1094,6 +1094,107 @@ __global__ void __launch_bounds__(BLOCK) k_sum_stats(const uint64_t* __restrict_
     }
 }
 
+// ----------------------------------------------------------------------------- API step
+// The reference's step() call shape for a policy that lives on the GPU: an external action
+// per board in, and out everything ChessEnvV2.step() hands back (chess_v2.py:219-294) plus
+// the rebuilt possible_actions (333-335) -- reward, done, info reason, the observation
+// (int8 mailbox, 153-158), the legal-action mask and count -- written straight into the
+// caller's device buffers.  Optional: auto-reset of finished boards (a vector-env
+// convention; the reference resets on the caller's reset()) and the random policy's pick
+// over the new list (a ready-made next action; also becomes the env's act[]).
+
+// legal-action mask of the position gen_moves described: word f = targets of from-square f,
+// word 64 bit c = action 4096 + c (castles)
+template <class S>
+__device__ void write_mask(const Pos& s, const Gen& g, const MoveSet& ms, const S& scr, u64* __restrict__ o) {
+    for (int sq = 0; sq < 64; sq++) {
+        u64 w = 0;
+        if ((g.own >> sq) & 1) {
+            if (ms.big) w = legal_targets(s, g, sq, type_at(s, sq));
+            else if ((ms.fastp >> sq) & 1) w = fast_pawn_targets(ms, sq, g.white);
+            else w = scr.get(ordinal(g.own, sq));
+        }
+        o[sq] = w;
+    }
+    u64 c = 0;
+    if (g.castles & 1) c |= g.white ? (1ull << 1) : (1ull << 3);  // QS: 4097 / 4099
+    if (g.castles & 2) c |= g.white ? (1ull << 0) : (1ull << 2);  // KS: 4096 / 4098
+    o[64] = c;
+}
+
+// spread the 8 bits of b over the 8 bytes of a word (bit j -> byte j, value 0/1): byte j
+// keeps bit j of a broadcast copy, then "nonzero -> 1" per byte (no carries: bytes <= 255)
+__device__ __forceinline__ u64 bits_to_bytes(u32 b) {
+    u64 y = ((u64)(b & 0xFFu) * 0x0101010101010101ull) & 0x8040201008040201ull;
+    return ((y + 0x7F7F7F7F7F7F7F7Full) >> 7) & 0x0101010101010101ull;
+}
+// int8 mailbox of the position (lib.rs:41-50 ids), 8 words of 8 squares: ids summed per
+// byte from the type planes, black bytes negated in two's complement without carries
+__device__ void write_obs(const Pos& s, int8_t* __restrict__ out) {
+    u64* o = reinterpret_cast<u64*>(out);
+    const u64 occ = occ_of(s), blk = occ & ~s.w;
+#pragma unroll
+    for (int r = 0; r < 8; r++) {
+        const int sh = 8 * r;
+        u64 v = bits_to_bytes((u32)(s.k >> sh)) * KING + bits_to_bytes((u32)(s.q >> sh)) * QUEEN +
+                bits_to_bytes((u32)(s.r >> sh)) * ROOK + bits_to_bytes((u32)(s.b >> sh)) * BISHOP +
+                bits_to_bytes((u32)(s.n >> sh)) * KNIGHT + bits_to_bytes((u32)(s.p >> sh)) * PAWN;
+        u64 b = bits_to_bytes((u32)(blk >> sh));
+        o[r] = (v ^ (b * 0xFFull)) + b;  // -id = ~id + 1 per black byte (no byte overflows)
+    }
+}
+
+template <bool OPP>
+__global__ void __launch_bounds__(BLOCK) k_env_step_api(EnvDev e, const uint16_t* __restrict__ acts,
+                                                        int32_t* __restrict__ rw, uint8_t* __restrict__ dn,
+                                                        uint8_t* __restrict__ rs, u64* __restrict__ mask,
+                                                        int8_t* __restrict__ obs, int32_t* __restrict__ cnt,
+                                                        uint16_t* __restrict__ pick_out, int autoreset) {
+    LDS_SCRATCH_DECL;
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= e.n) return;
+    Pos s = e.st.load(i);
+    u32 g0 = e.hgen[i], d = e.draw[i], nst = e.nsteps[i];
+    int a = (int)acts[i];
+    pin(s); pin(g0); pin(d); pin(nst);
+    DevHist h = e.hist(i, g0);
+    PolicyCtx pc = {e.seed, (u32)i, d};
+    Gen gv, g;
+    MoveSet ms;
+    gen_init(s, gv);
+    StepOut o = OPP ? env_step_vs<true>(s, h, a, &gv, g, ms, scr, pc) : env_step<true>(s, h, a, &gv, g, ms, scr);
+    bool have = o.moved;
+    nst += 1;
+    if (autoreset && o.done) {
+        reset_board(e, s, h);
+        after_reset<OPP>(e, s, h, g, ms, scr, pc);
+        have = true;
+    }
+    if (!have) {  // state unchanged (invalid action, done, move cap, both kings checked)
+        gen_init(s, g);
+        gen_moves(s, g, ms, scr);
+    }
+    rw[i] = o.reward;
+    dn[i] = (uint8_t)o.done;
+    rs[i] = (uint8_t)o.reason;
+    if (cnt) cnt[i] = ms.total;
+    if (mask) write_mask(s, g, ms, scr, mask + 65 * (size_t)i);
+    if (obs) write_obs(s, obs + 64 * (size_t)i);
+    if (pick_out) {
+        uint16_t p = pick(s, g, ms, scr, e.seed, i, pc.draw);
+        pick_out[i] = p;
+        e.act[i] = p;
+    }
+    h.commit();
+    e.st.store(i, s);
+    h.flush(g0);
+    e.draw[i] = pc.draw;
+    e.nsteps[i] = nst;
+    e.reward[i] = o.reward;
+    e.done[i] = (uint8_t)o.done;
+    e.reason[i] = (uint8_t)o.reason;
+}
+
 __global__ void __launch_bounds__(BLOCK) k_select(EnvDev e) {
     LDS_SCRATCH_DECL;
     int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1752,6 +1853,56 @@ extern "C" int gc_env_step(gc_env* e, const uint16_t* actions, int32_t* reward, 
     if (reward) HIPCHK(hipMemcpyAsync(reward, e->d.reward, (size_t)4 * e->n, hipMemcpyDeviceToHost, e->stream));
     if (done) HIPCHK(hipMemcpyAsync(done, e->d.done, e->n, hipMemcpyDeviceToHost, e->stream));
     if (reason) HIPCHK(hipMemcpyAsync(reason, e->d.reason, e->n, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return 0;
+}
+
+// step() with device buffers (k_env_step_api): asynchronous on the env's stream
+// (gc_env_get_stream); every pointer is device memory of n entries (mask: n*65 words, obs:
+// n*64 bytes); mask / obs / count / pick may be NULL.
+extern "C" int gc_env_step_device(gc_env* e, const uint16_t* d_actions, int32_t* d_reward, uint8_t* d_done,
+                                  uint8_t* d_reason, uint64_t* d_mask, int8_t* d_obs, int32_t* d_count,
+                                  uint16_t* d_pick, int flags) {
+    if (!e || !d_actions || !d_reward || !d_done || !d_reason) return fail("null argument");
+    if (e->rules) return fail("gc_env_step_device: reference rules only (FIDE: gc_env_step)");
+    if (flags & ~1) return fail("flags: bit 0 = auto-reset");
+    HIPCHK(hipSetDevice(e->device));
+    const int ar = flags & 1;
+    if (e->d.opp)
+        k_env_step_api<true><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d, d_actions, d_reward, d_done, d_reason,
+                                                                      d_mask, d_obs, d_count, d_pick, ar);
+    else
+        k_env_step_api<false><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d, d_actions, d_reward, d_done, d_reason,
+                                                                       d_mask, d_obs, d_count, d_pick, ar);
+    HIPCHK(hipGetLastError());
+    e->policy_ready = d_pick != nullptr;
+    return 0;
+}
+
+extern "C" int gc_env_get_stream(gc_env* e, void** stream) {
+    if (!e || !stream) return fail("null argument");
+    *stream = (void*)e->stream;
+    return 0;
+}
+
+// device buffers for callers without their own allocator (tests, bench): hipMalloc /
+// hipFree on the env's device, and copies on its stream
+extern "C" int gc_device_alloc(int device, uint64_t bytes, void** ptr) {
+    if (!ptr) return fail("null argument");
+    HIPCHK(hipSetDevice(device));
+    HIPCHK(hipMalloc(ptr, bytes ? bytes : 1));
+    return 0;
+}
+extern "C" int gc_device_free(int device, void* ptr) {
+    HIPCHK(hipSetDevice(device));
+    HIPCHK(hipFree(ptr));
+    return 0;
+}
+extern "C" int gc_env_copy(gc_env* e, void* dst, const void* src, uint64_t bytes, int kind) {
+    if (!e || !dst || !src) return fail("null argument");
+    if (kind < 0 || kind > 3) return fail("kind: 0 h2h, 1 h2d, 2 d2h, 3 d2d");
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipMemcpyAsync(dst, src, bytes, (hipMemcpyKind)kind, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
     return 0;
 }

@@ -225,6 +225,29 @@ class BatchedChessEnv:
     def device_bytes(self):
         return int(self._L.gc_env_device_bytes(self._h))
 
+    # ------------------------------------------------------------------ device-buffer step
+    def device_io(self, mask=True, obs=True, count=True, pick=True, select=True):
+        """Device buffers for step_device (gc_device_alloc on this env's device); with pick and
+        select, the pick buffer starts as the random policy's actions for the current states."""
+        return DeviceIO(self, mask=mask, obs=obs, count=count, pick=pick, select=select)
+
+    def step_device(self, io, actions=None, autoreset=False):
+        """step() on device buffers (gc_env_step_device), asynchronous on the env's stream.
+        actions: a device pointer (int, e.g. a torch tensor's data_ptr()) to uint16[N];
+        None = io.pick, the random policy's pick of the previous call (or select_device())."""
+        a = io.ptr["pick"] if actions is None else int(actions)
+        if not a:
+            raise ValueError("no actions: pass a device pointer or allocate io with pick=True")
+        p = io.ptr
+        _lib.check(self._L.gc_env_step_device(self._h, a, p["reward"], p["done"], p["reason"], p.get("mask"),
+                                              p.get("obs"), p.get("count"), p.get("pick"), int(bool(autoreset))))
+
+    def stream(self):
+        """the env's hipStream_t (for callers ordering their own device work with it)"""
+        v = ctypes.c_void_p()
+        _lib.check(self._L.gc_env_get_stream(self._h, ctypes.byref(v)))
+        return v.value
+
     # ------------------------------------------------------------------ checkpoint / resume
     def checkpoint(self):
         """The whole env as bytes (gc_env_save): states, move counts, done flags, 3-fold
@@ -248,6 +271,60 @@ class BatchedChessEnv:
     def load_from(self, path):
         with open(path, "rb") as f:
             self.load(f.read())
+
+
+class DeviceIO:
+    """Device buffers of one env's step_device outputs: reward i32, done u8, reason u8 and
+    optionally mask u64[N][65], obs i8[N][64], count i32, pick u16 (the random policy's next
+    action, which step_device uses as the actions when given none).  fetch() copies them to
+    host arrays; upload_actions() fills the pick buffer from the host."""
+
+    _SPEC = {"reward": (np.int32, ()), "done": (np.uint8, ()), "reason": (np.uint8, ()),
+             "mask": (np.uint64, (65,)), "obs": (np.int8, (64,)), "count": (np.int32, ()), "pick": (np.uint16, ())}
+
+    def __init__(self, env, mask=True, obs=True, count=True, pick=True, select=True):
+        self.env = env
+        want = {"reward": True, "done": True, "reason": True, "mask": mask, "obs": obs, "count": count, "pick": pick}
+        self.ptr = {}
+        for k, on in want.items():
+            if not on:
+                continue
+            dt, sh = self._SPEC[k]
+            nb = env.num_boards * int(np.prod(sh, dtype=np.int64)) * np.dtype(dt).itemsize
+            v = ctypes.c_void_p()
+            _lib.check(env._L.gc_device_alloc(env.device, ctypes.c_uint64(nb), ctypes.byref(v)))
+            self.ptr[k] = v.value
+        if pick and select:  # the policy's picks for the current states
+            self.select()
+
+    def select(self):
+        """pick = the env's current random-policy actions (picked at creation, reset(),
+        step_random(), rollout(); after set_states / set_fens call env.select_random() first)"""
+        self.upload_actions(self.env.outputs()["next_action"])
+
+    def upload_actions(self, actions):
+        a = np.ascontiguousarray(actions, dtype=np.uint16).reshape(self.env.num_boards)
+        _lib.check(self.env._L.gc_env_copy(self.env._h, self.ptr["pick"], _lib.ptr(a), ctypes.c_uint64(a.nbytes), 1))
+
+    def fetch(self, *keys):
+        out = {}
+        for k in keys or self.ptr:
+            dt, sh = self._SPEC[k]
+            a = np.zeros((self.env.num_boards,) + sh, dtype=dt)
+            _lib.check(self.env._L.gc_env_copy(self.env._h, _lib.ptr(a), self.ptr[k], ctypes.c_uint64(a.nbytes), 2))
+            out[k] = a
+        return out
+
+    def close(self):
+        for v in self.ptr.values():
+            self.env._L.gc_device_free(self.env.device, ctypes.c_void_p(v))
+        self.ptr = {}
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class MultiDeviceChessEnv:

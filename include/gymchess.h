@@ -102,6 +102,24 @@ int gc_env_reset(gc_env* e, const uint8_t* mask);
  * 8 agent mated by the opponent's reply (-100), 9 the opponent has no legal reply (the
  * reference's random policy returns "resign", which maps to no action and raises). */
 int gc_env_step(gc_env* e, const uint16_t* actions, int32_t* reward, uint8_t* done, uint8_t* reason);
+/* step(action) with DEVICE buffers, for a policy that lives on the GPU (chess_v2.py:219-294
+ * + the rebuilt possible_actions, 333-335): d_actions[n] in (validated like 240-242); out
+ * d_reward[n], d_done[n], d_reason[n] (as gc_env_step), and optionally (NULL = skip)
+ * d_mask[n][65] (legal-action mask of the new position, gc_env_legal_mask's layout),
+ * d_obs[n][64] (int8 board, the observation of 153-158), d_count[n] (legal actions),
+ * d_pick[n] (the random policy's pick over the new list; also the env's next policy
+ * action).  flags bit 0: auto-reset finished boards (the mask / obs / pick then describe
+ * the new episode).  Asynchronous on the env's stream: order your own work with it through
+ * gc_env_get_stream (a hipStream_t) or gc_env_synchronize.  Reference rules only. */
+int gc_env_step_device(gc_env* e, const uint16_t* d_actions, int32_t* d_reward, uint8_t* d_done,
+                       uint8_t* d_reason, uint64_t* d_mask, int8_t* d_obs, int32_t* d_count,
+                       uint16_t* d_pick, int flags);
+int gc_env_get_stream(gc_env* e, void** stream);
+/* device memory helpers for callers without an allocator; kind 0 h2h 1 h2d 2 d2h 3 d2d
+ * (synchronous on the env's stream) */
+int gc_device_alloc(int device, uint64_t bytes, void** ptr);
+int gc_device_free(int device, void* ptr);
+int gc_env_copy(gc_env* e, void* dst, const void* src, uint64_t bytes, int kind);
 /* Device-resident random self-play (the test_benchmark.py driver): n_plies one-ply kernel
  * launches; each ply = one env.step() with a uniform Philox pick over the legal list, a
  * reset when done, a reset without a step when the list is empty (reason 4). */

@@ -1,0 +1,91 @@
+"""GPU: step() on device buffers (gc_env_step_device) -- the reference's call shape
+(chess_v2.py:219-294: external action in; reward, done, info, observation out; the rebuilt
+possible_actions, 333-335) for a policy on the GPU."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _mask_bits(raw):
+    n = raw.shape[0]
+    bits = np.unpackbits(raw[:, :64].view(np.uint8).reshape(n, 64, 8), axis=2, bitorder="little")
+    out = np.zeros((n, 4101), dtype=bool)
+    out[:, :4096] = bits.reshape(n, 4096).astype(bool)
+    for c in range(4):
+        out[:, 4096 + c] = (raw[:, 64] >> np.uint64(c)) & np.uint64(1) != 0
+    return out
+
+
+@pytest.mark.parametrize("opponent", ["none", "random"])
+def test_step_device_equals_host_step(oracle, opponent):
+    """Same external actions (legal and invalid) into two envs: device-buffer step == host
+    step, ply by ply: outputs, states, and the mask / obs / count describe the new states."""
+    from gym_chess_amd.env import BatchedChessEnv
+
+    n = 300
+    a = BatchedChessEnv(n, device=0, seed=17, opponent=opponent)
+    b = BatchedChessEnv(n, device=0, seed=17, opponent=opponent)
+    io = a.device_io(pick=False)
+    act_buf = a.device_io(mask=False, obs=False, count=False, pick=True, select=False)  # action upload slot
+    rng = np.random.RandomState(3)
+    for ply in range(120):
+        lists = b.possible_actions()
+        acts = np.array([l[rng.randint(len(l))] if l and rng.rand() > 0.05 else rng.randint(4101) for l in lists],
+                        dtype=np.uint16)
+        act_buf.upload_actions(acts)
+        a.step_device(io, actions=act_buf.ptr["pick"])
+        rw, dn, why = b.step(acts)
+        o = io.fetch()
+        assert (o["reward"] == rw).all() and (o["done"].astype(bool) == dn).all() and (o["reason"] == why).all(), ply
+        bb, bm = b.boards()
+        ab, am = a.boards()
+        assert (ab == bb).all() and (am == bm).all(), ply
+        assert (o["obs"] == bb).all(), ply
+        assert (_mask_bits(o["mask"]) == b.legal_mask()).all(), ply
+        assert (o["count"] == np.array([len(x) for x in b.possible_actions()])).all(), ply
+        if dn.any():
+            a.reset(dn.astype(np.uint8))
+            b.reset(dn.astype(np.uint8))
+
+
+def test_step_device_autoreset_pick_loop_vs_oracle(oracle):
+    """actions = the previous call's pick, auto-reset on: the random self-play driver, ply
+    by ply == the oracle's, on every board until it first meets a position with no legal
+    move (there the driver resets without a step, while step() reports an invalid action)."""
+    from gym_chess_amd.env import BatchedChessEnv
+
+    n, plies, seed = 256, 400, 2718
+    env = BatchedChessEnv(n, device=0, seed=seed)
+    io = env.device_io()
+    refs = [oracle.rollout_trace(seed, i, plies + 1) for i in range(n)]
+    live = np.ones(n, dtype=bool)
+    checked = 0
+    for p in range(plies):
+        env.step_device(io, autoreset=True)
+        o = io.fetch("reward", "done", "reason", "pick")
+        live &= np.array([r["reason"][p] != 4 and r["action"][p] >= 0 for r in refs])
+        rr = np.array([r["reward"][p] for r in refs])
+        rd = np.array([r["done"][p] for r in refs])
+        nx = np.array([r["action"][p + 1] for r in refs])
+        assert (o["reward"][live] == rr[live]).all() and (o["done"][live] == rd[live]).all(), p
+        ok = live & (nx >= 0)
+        assert (o["pick"][ok] == nx[ok]).all(), p
+        checked += int(live.sum())
+    assert checked > n * plies // 2
+
+
+def test_obs_of_weird_boards(oracle):
+    """The byte-plane observation writer on boards with every piece id in every square class."""
+    from conftest import random_positions
+    from gym_chess_amd.env import BatchedChessEnv
+
+    boards, metas = random_positions(128, 99)
+    env = BatchedChessEnv(128, device=0, seed=1)
+    env.set_states(boards, metas)
+    io = env.device_io(mask=False, count=False, pick=False)
+    act = env.device_io(mask=False, obs=False, count=False, pick=True, select=False)
+    act.upload_actions(np.full(128, 4100, dtype=np.uint16))  # RESIGN: invalid, state unchanged
+    env.step_device(io, actions=act.ptr["pick"])
+    o = io.fetch()
+    assert (o["reason"] == 6).all() and (o["obs"] == boards).all()
