@@ -65,6 +65,8 @@ def parse():
                     help="also time step() with opponent='random' and with rules='fide' (SURVEY 8f rows 2, 4; 0 = skip)")
     ap.add_argument("--api-steps", type=int, default=300,
                     help="also time the API-shaped step on device buffers (mask + obs out; 0 = skip)")
+    ap.add_argument("--single-episodes", type=int, default=10,
+                    help="configs[0]: the reference benchmark driver on the single-board env (0 = skip)")
     ap.add_argument("--perft-depth", type=int, default=5)
     ap.add_argument("--oracle-perft-roots", type=int, default=8,
                     help="roots of the perft leg checked against the oracle at --perft-depth (also its CPU baseline)")
@@ -250,6 +252,53 @@ def api_step_leg(args, rep, n):
                          "alg_bytes_per_board": ALG_BYTES_API}}
 
 
+def reference_driver(env, episodes, steps, seed):
+    """/root/reference/gym_chess/test/v2/test_benchmark.py:9-43, statement for statement:
+    random self-play over env.possible_moves with numpy's global generator."""
+    import numpy as np
+
+    np.random.seed(seed)
+    total = 0
+    t0 = time.perf_counter()
+    for _ in range(episodes):
+        env.reset()
+        for _ in range(steps):
+            total += 1
+            moves = env.possible_moves
+            if not moves:
+                break
+            move = moves[np.random.choice(np.arange(len(moves)))]
+            _, _, done, _ = env.step(env.move_to_action(move))
+            if done:
+                break
+    return total, time.perf_counter() - t0
+
+
+def single_env_leg(args, rep):
+    """configs[0] / the reference's own benchmark (test_benchmark.py: 10 episodes x <= 100
+    steps, published 312 us per step for the Rust v2 engine): the chess_v2.py-shaped
+    single-board env on this package's ChessEngine (one C-ABI call + GPU launch per engine
+    call).  CPU baseline: the same driver over the C oracle's ChessEngine on one core."""
+    from gym_chess_amd.single import ChessEnv
+
+    rp = rep.local[0]
+    env = ChessEnv(opponent="none", log=False, device=rp.device)
+    reference_driver(env, 1, 10, 1)  # load the engine kernels
+    steps, dt = reference_driver(env, args.single_episodes, 100, 0x5EED)
+    out = {"value": dt / steps * 1e6, "unit": "us/step", "higher_is_better": False, "steps": steps,
+           "episodes": args.single_episodes, "reference_published_us_per_step": 312.0}
+    if rep.rank == 0 and rep.world_size == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from oracle_engine import OracleChessEngine
+
+        cenv = ChessEnv(opponent="none", log=False, engine=OracleChessEngine())
+        cs, cdt = reference_driver(cenv, args.single_episodes, 100, 0x5EED)
+        out["cpu_baseline"] = {"value": cdt / cs * 1e6, "unit": "us/step", "cores": 1, "kind": "port",
+                               "sample": f"the same driver, {cs} steps over the C oracle's ChessEngine"}
+    return out
+
+
 def variant_legs(args, rep, n):
     """step() throughput of the SURVEY 8f variants at the same batch: the in-kernel random
     opponent (one step = the agent's ply + the opponent's reply) and FIDE rules.  Same timing
@@ -361,6 +410,8 @@ def main():
         e.close()
     if args.api_steps > 0:
         extra["api_step"] = api_step_leg(args, rep, n)
+    if args.single_episodes > 0:
+        extra["single_env"] = single_env_leg(args, rep)
     if args.variant_steps > 0:
         extra["variants"] = variant_legs(args, rep, n)
     if args.perft_roots > 0:
