@@ -222,18 +222,27 @@ GC_HD u64 ray_fill_att(u64 gen, u64 empty, u64 wrap) {
     return sh<SH, LEFT>(gen) & wrap;
 }
 
-GC_HD u64 side_attacks(const Pos& s, bool white) {
-    u64 occ = occ_of(s), empty = ~occ;
+// the map in three parts (the quad step kernel computes them on different waves)
+GC_HD u64 side_attacks_leapers(const Pos& s, bool white) {
+    u64 occ = occ_of(s);
     u64 mine = white ? s.w : (occ & ~s.w);
-    u64 a = pawn_att_set(s.p & mine, white) & ~(s.k & mine);
-    a |= knight_set(s.n & mine) | king_set(s.k & mine);
-    // branch-free for any number of sliders (a per-slider loop runs the wave's maximum)
-    u64 rq = (s.r | s.q) & mine, bq = (s.b | s.q) & mine;
-    a |= ray_fill_att<8, false>(rq, empty, ~0ull) | ray_fill_att<8, true>(rq, empty, ~0ull) |
-         ray_fill_att<1, true>(rq, empty, ~FILE_A) | ray_fill_att<1, false>(rq, empty, ~FILE_H);
-    a |= ray_fill_att<7, false>(bq, empty, ~FILE_A) | ray_fill_att<9, false>(bq, empty, ~FILE_H) |
-         ray_fill_att<9, true>(bq, empty, ~FILE_A) | ray_fill_att<7, true>(bq, empty, ~FILE_H);
-    return a;
+    return (pawn_att_set(s.p & mine, white) & ~(s.k & mine)) | knight_set(s.n & mine) | king_set(s.k & mine);
+}
+// branch-free for any number of sliders (a per-slider loop runs the wave's maximum)
+GC_HD u64 side_attacks_orth(const Pos& s, bool white) {
+    u64 occ = occ_of(s), empty = ~occ;
+    u64 rq = (s.r | s.q) & (white ? s.w : (occ & ~s.w));
+    return ray_fill_att<8, false>(rq, empty, ~0ull) | ray_fill_att<8, true>(rq, empty, ~0ull) |
+           ray_fill_att<1, true>(rq, empty, ~FILE_A) | ray_fill_att<1, false>(rq, empty, ~FILE_H);
+}
+GC_HD u64 side_attacks_diag(const Pos& s, bool white) {
+    u64 occ = occ_of(s), empty = ~occ;
+    u64 bq = (s.b | s.q) & (white ? s.w : (occ & ~s.w));
+    return ray_fill_att<7, false>(bq, empty, ~FILE_A) | ray_fill_att<9, false>(bq, empty, ~FILE_H) |
+           ray_fill_att<9, true>(bq, empty, ~FILE_A) | ray_fill_att<7, true>(bq, empty, ~FILE_H);
+}
+GC_HD u64 side_attacks(const Pos& s, bool white) {
+    return side_attacks_leapers(s, white) | side_attacks_orth(s, white) | side_attacks_diag(s, white);
 }
 
 // is square `sq` in `by_white`'s attack map? (the map membership test of lib.rs:661)
@@ -374,34 +383,51 @@ GC_HD void pin_line(u64 mask, const LineNeg& ln, u64 occ, u64 own, u64 sliders, 
     pinrays |= (pu ? a2u : 0ull) | (pd ? a2d : 0ull);
 }
 
-GC_HD void gen_pins(const Pos& s, Gen& g) {
-    if (g.ks < 0) return;  // "King not present": no filter, no castling, no king moves
+// Partial pin / check sets of some of the four lines through the king (LINES bit 0 file,
+// 1 rank, 2 diagonal, 3 anti-diagonal; LEAPERS: pawn / knight / king checkers), so that the
+// quad step kernel can spread them over two waves; gen_pins_finish merges.
+struct PinPart {
+    u64 checkers, block, pinned, pinrays;
+};
+template <int LINES, bool LEAPERS>
+GC_HD PinPart gen_pins_part(const Pos& s, const Gen& g) {
+    PinPart p = {0, 0, 0, 0};
+    if (g.ks < 0) return p;  // "King not present": no filter, no castling, no king moves
     int ks = g.ks;
-    bool white = g.white;
     u64 kb = bit(ks);
     u64 opp = g.opp, occ = g.occ, own = g.own;
-    u64 rq = (s.r | s.q) & opp, bq = (s.b | s.q) & opp;
-    u64 checkers = (pawn_att_set(kb, white) & s.p & opp) | (knight_set(kb) & s.n & opp) | (king_set(kb) & s.k & opp);
-    u64 block = 0, pinned = 0, pinrays = 0;
+    if (LEAPERS)
+        p.checkers = (pawn_att_set(kb, g.white) & s.p & opp) | (knight_set(kb) & s.n & opp) | (king_set(kb) & s.k & opp);
     u64 lo = below(ks), hi = ~(lo | kb);
     LineNeg ln = line_neg(ks);
-    pin_line(file_mask(ks), ln, occ, own, rq, hi, lo, checkers, block, pinned, pinrays);
-    pin_line(row_mask(ks), ln, occ, own, rq, hi, lo, checkers, block, pinned, pinrays);
-    pin_line(diag_mask(ks), ln, occ, own, bq, hi, lo, checkers, block, pinned, pinrays);
-    pin_line(anti_mask(ks), ln, occ, own, bq, hi, lo, checkers, block, pinned, pinrays);
+    if (LINES & 3) {
+        u64 rq = (s.r | s.q) & opp;
+        if (LINES & 1) pin_line(file_mask(ks), ln, occ, own, rq, hi, lo, p.checkers, p.block, p.pinned, p.pinrays);
+        if (LINES & 2) pin_line(row_mask(ks), ln, occ, own, rq, hi, lo, p.checkers, p.block, p.pinned, p.pinrays);
+    }
+    if (LINES & 12) {
+        u64 bq = (s.b | s.q) & opp;
+        if (LINES & 4) pin_line(diag_mask(ks), ln, occ, own, bq, hi, lo, p.checkers, p.block, p.pinned, p.pinrays);
+        if (LINES & 8) pin_line(anti_mask(ks), ln, occ, own, bq, hi, lo, p.checkers, p.block, p.pinned, p.pinrays);
+    }
+    return p;
+}
+GC_HD void gen_pins_finish(Gen& g, const PinPart& p) {
+    if (g.ks < 0) return;
+    u64 checkers = p.checkers, block = p.block;
     g.in_check = checkers != 0;
     // one checker: capture it or block (checkers | between); two: king moves only; none: all
     g.checkmask = !checkers ? ~0ull : ((checkers & (checkers - 1)) ? 0ull : (checkers | block));
-    g.pinned = pinned;
-    g.pinrays = pinrays;
+    g.pinned = p.pinned;
+    g.pinrays = p.pinrays;
 }
+GC_HD void gen_pins(const Pos& s, Gen& g) { gen_pins_finish(g, gen_pins_part<15, true>(s, g)); }
 
-GC_HD void gen_enemy(const Pos& s, Gen& g) {
+// castling (lib.rs:578-610 gate = OR of the colour's rights + king on board; geometry
+// lib.rs:966-1056 tests the POSITIVE ids for black too: Q4), given g.enemy_att
+GC_HD void gen_castles(const Pos& s, Gen& g) {
     if (g.ks < 0) return;
     bool white = g.white;
-    g.enemy_att = side_attacks(s, !white);
-    // castling (lib.rs:578-610 gate = OR of the colour's rights + king on board;
-    // geometry lib.rs:966-1056 tests the POSITIVE ids for black too: Q4)
     u32 er = eff_rights(s);
     bool gate = white ? (er & (M_WKC | M_WQC)) : (er & (M_BKC | M_BQC));
     u64 wr = s.r & s.w, wk = s.k & s.w, A = g.enemy_att, occ = g.occ;
@@ -412,6 +438,11 @@ GC_HD void gen_enemy(const Pos& s, Gen& g) {
     bool qs = kpos && (wr & bit(base)) && !(occ & qs_empty) && !(A & qs_safe);
     bool kside = kpos && (wr & bit(base + 7)) && !(occ & ks_empty) && !(A & ks_safe);
     g.castles = (qs ? 1u : 0u) | (kside ? 2u : 0u);
+}
+GC_HD void gen_enemy(const Pos& s, Gen& g) {
+    if (g.ks < 0) return;
+    g.enemy_att = side_attacks(s, !g.white);
+    gen_castles(s, g);
 }
 
 GC_HD void gen_init(const Pos& s, Gen& g) {
@@ -634,15 +665,15 @@ GC_HD u64 fide_pawn_targets(const Pos& s, const Gen& g, int sq, const FideExtra&
     return tg;
 }
 
-// Part A of the generation: pawns (set-wise), knights, kings, queens.  `ms` cleared; ORs
-// into ms.cnt; returns the number of moves found.  (The split A | B balances the two waves
-// of the paired step kernel: queens cost a bishop plus a rook.)
+// Generator parts, one piece type each (the paired / quad step kernels run them on
+// different waves).  Each ORs its pieces' counts into ms.cnt and returns its move count.
+// Pawns, set-wise (lib.rs:935-958; Q1: the double push tests only the destination); the
+// unpinned ones leave their four origin sets in ms (fastp, o1, o2, ol, orr).
 template <class S, bool F = false>
-GC_HD int gen_moves_a(const Pos& s, const Gen& g, MoveSet& ms, S& scr, const FideExtra& fx = FideExtra{0, -1}) {
+GC_HD int gen_pawns(const Pos& s, const Gen& g, MoveSet& ms, S& scr, const FideExtra& fx = FideExtra{0, -1}) {
     const u64 own = g.own, cm = g.checkmask, nocap = F ? ~(s.k & g.opp) : ~0ull;  // FIDE: no king captures
-    const u64 notown_cm = ~own & cm & nocap, opp = g.opp & nocap;
+    const u64 opp = g.opp & nocap;
     int total = 0;
-    // pawns, set-wise (lib.rs:935-958; Q1: the double push tests only the destination)
     u64 P = s.p & own, fp = P & ~g.pinned, empty = ~g.occ;
     if (g.white) {
         ms.o1 = ((fp >> 8) & empty & cm) << 8;
@@ -677,51 +708,61 @@ GC_HD int gen_moves_a(const Pos& s, const Gen& g, MoveSet& ms, S& scr, const Fid
         pp ^= bit(sq);
         park(ms, scr, own, sq, F ? fide_pawn_targets(s, g, sq, fx) : legal_targets(s, g, sq, PAWN), total);
     }
+    return total;
+}
+template <class S, bool F = false>
+GC_HD int gen_knights(const Pos& s, const Gen& g, MoveSet& ms, S& scr) {
+    const u64 own = g.own, notown_cm = ~own & g.checkmask & (F ? ~(s.k & g.opp) : ~0ull);
+    int total = 0;
     u64 x = s.n & own;  // a pinned knight never has a move on its pin segment
     while (x) {
         int sq = ctz(x);
         x ^= bit(sq);
         park(ms, scr, own, sq, ((g.pinned >> sq) & 1) ? 0 : knight_set(bit(sq)) & notown_cm, total);
     }
-    x = s.k & own;  // every own king; filtered by the pre-move enemy map only (lib.rs:613-619)
+    return total;
+}
+template <class S, bool F = false>
+GC_HD int gen_kings(const Pos& s, const Gen& g, MoveSet& ms, S& scr) {
+    const u64 own = g.own, nocap = F ? ~(s.k & g.opp) : ~0ull;
+    int total = 0;
+    u64 x = s.k & own;  // every own king; filtered by the pre-move enemy map only (lib.rs:613-619)
     while (x) {
         int sq = ctz(x);
         x ^= bit(sq);
         park(ms, scr, own, sq, king_set(bit(sq)) & ~own & ~g.enemy_att & nocap, total);
     }
-    x = s.q & own;
+    return total;
+}
+// sliders of one kind: T = QUEEN, ROOK or BISHOP
+template <int T, class S, bool F = false>
+GC_HD int gen_sliders(const Pos& s, const Gen& g, MoveSet& ms, S& scr) {
+    const u64 own = g.own, notown_cm = ~own & g.checkmask & (F ? ~(s.k & g.opp) : ~0ull);
+    int total = 0;
+    u64 x = (T == QUEEN ? s.q : T == ROOK ? s.r : s.b) & own;
     while (x) {
         int sq = ctz(x);
         x ^= bit(sq);
-        u64 tg = queen_att(sq, g.occ) & notown_cm;
+        u64 tg = (T == QUEEN ? queen_att(sq, g.occ) : T == ROOK ? rook_att(sq, g.occ) : bishop_att(sq, g.occ)) & notown_cm;
         if ((g.pinned >> sq) & 1) tg &= g.pinrays & line_through(g.ks, sq);
         park(ms, scr, own, sq, tg, total);
     }
     return total;
 }
 
+// Part A of the generation: pawns (set-wise), knights, kings, queens.  `ms` cleared; ORs
+// into ms.cnt; returns the number of moves found.  (The split A | B balances the two waves
+// of the paired step kernel: queens cost a bishop plus a rook.)
+template <class S, bool F = false>
+GC_HD int gen_moves_a(const Pos& s, const Gen& g, MoveSet& ms, S& scr, const FideExtra& fx = FideExtra{0, -1}) {
+    return gen_pawns<S, F>(s, g, ms, scr, fx) + gen_knights<S, F>(s, g, ms, scr) + gen_kings<S, F>(s, g, ms, scr) +
+           gen_sliders<QUEEN, S, F>(s, g, ms, scr);
+}
+
 // Part B: bishops and rooks.  ORs into ms.cnt; returns the number of moves found.
 template <class S, bool F = false>
 GC_HD int gen_moves_b(const Pos& s, const Gen& g, MoveSet& ms, S& scr) {
-    const u64 own = g.own, notown_cm = ~own & g.checkmask & (F ? ~(s.k & g.opp) : ~0ull);
-    int total = 0;
-    u64 x = s.b & own;
-    while (x) {
-        int sq = ctz(x);
-        x ^= bit(sq);
-        u64 tg = bishop_att(sq, g.occ) & notown_cm;
-        if ((g.pinned >> sq) & 1) tg &= g.pinrays & line_through(g.ks, sq);
-        park(ms, scr, own, sq, tg, total);
-    }
-    x = s.r & own;
-    while (x) {
-        int sq = ctz(x);
-        x ^= bit(sq);
-        u64 tg = rook_att(sq, g.occ) & notown_cm;
-        if ((g.pinned >> sq) & 1) tg &= g.pinrays & line_through(g.ks, sq);
-        park(ms, scr, own, sq, tg, total);
-    }
-    return total;
+    return gen_sliders<BISHOP, S, F>(s, g, ms, scr) + gen_sliders<ROOK, S, F>(s, g, ms, scr);
 }
 
 template <class S>

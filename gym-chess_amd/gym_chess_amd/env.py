@@ -178,6 +178,10 @@ class BatchedChessEnv:
     def select_random(self):
         _lib.check(self._L.gc_env_select_random(self._h))
 
+    def set_streams(self, k):
+        """step_random over k board ranges on k device streams (gc_env_set_streams)."""
+        _lib.check(self._L.gc_env_set_streams(self._h, int(k)))
+
     def step_random(self, n_plies=1):
         _lib.check(self._L.gc_env_step_random(self._h, int(n_plies)))
 
@@ -359,6 +363,10 @@ class MultiDeviceChessEnv:
         parts = self._split(actions)
         out = self.rep.run(lambda rp: self.envs[rp.index].step(parts[rp.index]))
         return tuple(np.concatenate([o[k] for o in out]) for k in range(3))
+
+    def set_streams(self, k):
+        """step_random over k board ranges on k device streams (gc_env_set_streams)."""
+        _lib.check(self._L.gc_env_set_streams(self._h, int(k)))
 
     def step_random(self, n_plies=1):
         self._each(lambda e: e.step_random(n_plies))

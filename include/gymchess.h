@@ -124,6 +124,10 @@ int gc_env_copy(gc_env* e, void* dst, const void* src, uint64_t bytes, int kind)
  * launches; each ply = one env.step() with a uniform Philox pick over the legal list, a
  * reset when done, a reset without a step when the list is empty (reason 4). */
 int gc_env_step_random(gc_env* e, int n_plies);
+/* gc_env_step_random over k board ranges on k streams of the device (k in [1, 8]; default
+ * from GC_STREAMS, else 2): a range's ply p+1 waits only for its own ply p, so the ranges'
+ * launches overlap each other's ramp and tail.  Results are independent of k. */
+int gc_env_set_streams(gc_env* e, int k);
 /* re-pick policy actions for the current states (after set_states / external steps) */
 int gc_env_select_random(gc_env* e);
 /* Same driver fused into ONE launch of n_plies plies (state kept in registers).  Optional
