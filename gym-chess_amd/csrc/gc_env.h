@@ -12,7 +12,7 @@
 // a monotone potential and no later board equals an earlier one.  The window therefore
 // holds the distinct boards since the last pawn move / capture (<= 300: the move cap,
 // chess_v2.py:141, 252) with their occurrence counts, in a per-board open-addressed table
-// of HTAB 64-byte entries {generation u32 | key tag u22 | count u8, 7 bitboards}: one
+// of HTAB 64-byte entries {generation u32 | key tag u23 | count u8, 7 bitboards}: one
 // entry = one cache line, so a single probe both finds and verifies a board.  An entry is
 // live only if its generation equals the board's current one, so clearing the window
 // (irreversible move, reset) is a single generation bump.  The count is exact (full-board
@@ -28,11 +28,20 @@ namespace gc {
 
 // Window capacity.  With opponent "none" (and a WHITE agent) the move cap bounds a window to
 // ~301 boards; a BLACK agent's move_count never advances (chess_v2.py:291-292), so its
-// window is unbounded in the reference: a window that would exceed HIST_CAP ends the episode
-// with R_WINDOW_FULL (the oracle does the same), keeping the table at load <= 0.75.
-static constexpr int HIST_CAP = 768;
-static constexpr int HTAB_BITS = 10;
+// window is unbounded in the reference: a window that would exceed hist_cap ends the episode
+// with R_WINDOW_FULL (the oracle does the same).
+// The table size is per env (H::bits()):
+//  * 2^9 = 512 entries (32 KiB per board, 2 GiB at 65 536 boards) when the move cap bounds
+//    the games (opponent "none", or a WHITE agent): windows of <= ~301 boards, load <= 0.59;
+//    a window may hold HIST_CAP = 384 boards (load 0.75);
+//  * 2^10 = 1024 entries for a BLACK agent, whose games have no move cap: a window may hold
+//    511 boards (the 9-bit window-length field of the meta word), load 0.5.
+static constexpr int HTAB_BITS = 9;                 // the move-capped envs (all paired kernels)
+static constexpr int HTAB_BITS_UNCAPPED = 10;       // BLACK agent
 static constexpr int HTAB = 1 << HTAB_BITS;
+static constexpr int HTAB_MAX = 1 << HTAB_BITS_UNCAPPED;
+GC_HD int hist_cap(int bits) { return bits > HTAB_BITS ? 511 : 384; }
+GC_HD u32 tag_mask(int bits) { return (1u << (32 - bits)) - 1; }  // key bits above the slot index
 static constexpr int MOVES_MAX = 149;  // chess_v2.py:141
 
 struct StepOut {
@@ -58,7 +67,7 @@ GC_HD Pos env_reset_pos(const Pos& init) {
 
 // one table entry
 struct RepEntry {
-    u64 hdr;  // gen (bits 0..31) | tag (32..53) | count (56..63)
+    u64 hdr;  // gen (bits 0..31) | tag (32.., 32 - bits wide) | count (56..63)
     u64 k, q, r, b, n, p, w;
 };
 GC_HD bool rep_same(const RepEntry& e, const Pos& s) {
@@ -66,7 +75,7 @@ GC_HD bool rep_same(const RepEntry& e, const Pos& s) {
 }
 
 // H (per-board table storage) provides:
-//   u32 gen(); void bump_gen(); RepEntry load(int pos); void store_hdr(int pos, u64);
+//   int bits(); u32 gen(); void bump_gen(); RepEntry load(int pos); void store_hdr(int pos, u64);
 //   void store(int pos, const RepEntry&)
 struct RepProbe {
     u32 key;
@@ -76,26 +85,28 @@ struct RepProbe {
 template <class H>
 GC_HD void rep_prefetch(H& h, const Pos& s, RepProbe& pr) {
     pr.key = board_key(s);
-    pr.e0 = h.load((int)(pr.key & (HTAB - 1)));
+    pr.e0 = h.load((int)(pr.key & ((1u << h.bits()) - 1)));
 }
 
 // Returns how many times the board has been the pre-move board so far, this one included;
-// 0 if it is new and the window is full (HIST_CAP).
+// 0 if it is new and the window is full (hist_cap).
 template <class H>
 GC_HD int rep_commit(H& h, const Pos& s, const RepProbe& pr, u32& hl, bool irrev) {
+    const int bits = h.bits();
+    const u32 size_mask = (1u << bits) - 1;
     u32 gen = h.gen();
-    u32 pos = pr.key & (HTAB - 1), tag = pr.key >> HTAB_BITS;
+    u32 pos = pr.key & size_mask, tag = pr.key >> bits;
     int c = 0;
     RepEntry e = pr.e0;
-    for (int probe = 0; probe < HTAB; probe++) {
+    for (int probe = 0; probe <= (int)size_mask; probe++) {
         if (probe) e = h.load((int)pos);
         if ((u32)e.hdr != gen) break;  // free for this generation
-        if ((u32)((e.hdr >> 32) & 0x3FFFFF) == tag && rep_same(e, s)) {
+        if ((u32)((e.hdr >> 32) & tag_mask(bits)) == tag && rep_same(e, s)) {
             c = (int)(e.hdr >> 56) + 1;
             h.store_hdr((int)pos, (e.hdr & ~(0xFFull << 56)) | ((u64)c << 56));
             break;
         }
-        pos = (pos + 1) & (HTAB - 1);
+        pos = (pos + 1) & size_mask;
     }
     if (irrev) {  // nothing before this move can recur: clear the window
         h.bump_gen();
@@ -103,7 +114,7 @@ GC_HD int rep_commit(H& h, const Pos& s, const RepProbe& pr, u32& hl, bool irrev
         return c ? c : 1;
     }
     if (c) return c;
-    if (hl >= HIST_CAP) return 0;
+    if ((int)hl >= hist_cap(bits)) return 0;
     RepEntry ne = {(u64)gen | ((u64)tag << 32) | (1ull << 56), s.k, s.q, s.r, s.b, s.n, s.p, s.w};
     h.store((int)pos, ne);
     hl++;

@@ -104,12 +104,14 @@ struct DevHist {
     u32* hgen;
     u32 g;
     int i;
+    int nb = HTAB_BITS;  // log2 entries per board (gc_env.h: 9, or 10 for a BLACK agent)
     // Wave-blocked layout: entry pos of board i at ((i/64)*HTAB + pos)*64 + i%64, i.e. the 64
     // boards of a wave share one 4 MiB block and a wave's 64 probes land on 64 random 4 KiB
     // rows of it.  Board-major tables (64 KiB per board) put a wave's probes 64 KiB apart, on
     // the same HBM channels: tools/lat_probe.hip measures 9.6 vs 5.5 us per launch for one
     // random 64-B read + write per board at 65 536 boards.
-    __device__ size_t entry(int pos) const { return ((size_t)(i >> 6) * HTAB + pos) * 64 + (i & 63); }
+    __device__ size_t entry(int pos) const { return ((((size_t)(i >> 6)) << nb) + pos) * 64 + (i & 63); }
+    __device__ int bits() const { return nb; }
     __device__ u32 gen() const { return g; }
     __device__ void bump_gen() { g++; }                // written back by flush()
     __device__ void flush(u32 g0) const { if (g != g0) hgen[i] = g; }
@@ -390,7 +392,8 @@ struct EnvDev {
         int usable;  // 0: the start position needs the per-square fallback (> 16 pieces)
         int table;   // reset_acts holds all `total` actions
     } ic;
-    __device__ DevHist hist(int i, u32 g) const { return DevHist{htab, hgen, g, i}; }
+    int hbits;        // log2 window-table entries per board (DevHist::nb)
+    __device__ DevHist hist(int i, u32 g) const { return DevHist{htab, hgen, g, i, hbits}; }
 };
 
 // The env's per-board fields live in ONE allocation (the "slab"), at offsets that are a
@@ -1777,6 +1780,7 @@ extern "C" int gc_env_create(int device, int n_boards, uint64_t seed, const int8
     e->d.n = n;
     e->d.opp = 0;
     e->d.agent_black = 0;
+    e->d.hbits = HTAB_BITS;
     {  // the start position's move set, shared by every reset (EnvDev::ic)
         EnvDev::InitCache* dic = nullptr;
         uint16_t* dacts = nullptr;
@@ -1816,6 +1820,17 @@ extern "C" int gc_env_set_opponent(gc_env* e, int opponent, int agent_white) {
     if (opponent && e->rules) return fail("the FIDE rules mode supports opponent \"none\" only");
     HIPCHK(hipSetDevice(e->device));
     HIPCHK(hipStreamSynchronize(e->stream));
+    const int bits = agent_white ? HTAB_BITS : HTAB_BITS_UNCAPPED;  // a BLACK agent's games have no move cap
+    if (bits != e->d.hbits) {
+        size_t nb64 = ((size_t)e->n + 63) / 64 * 64;
+        u64* t = nullptr;
+        if (dalloc(&t, ((size_t)8 << bits) * nb64)) return -1;
+        HIPCHK(hipMemsetAsync(t, 0, ((size_t)64 << bits) * nb64, e->stream));
+        (void)hipFree(e->d.htab);
+        e->d.htab = t;
+        e->d.hbits = bits;
+        if (e->graph_exec) { (void)hipGraphExecDestroy(e->graph_exec); e->graph_exec = nullptr; }
+    }
     e->d.opp = opponent;
     e->d.agent_black = agent_white ? 0 : 1;
     HIPCHK(hipMemsetAsync(e->d.draw, 0, (size_t)4 * e->n, e->stream));  // fresh policy streams
@@ -2428,14 +2443,15 @@ __global__ void k_hl_of(const u32* __restrict__ meta, int n, uint32_t* __restric
 
 // the live entries (generation == hgen[i]) of board i, in table order, at out[offs[i]..]
 __global__ void k_ckpt_pack(const u64* __restrict__ htab, const u32* __restrict__ hgen, const u32* __restrict__ meta,
-                            int n, const uint32_t* __restrict__ offs, u64* __restrict__ out, uint32_t* __restrict__ bad) {
+                            int n, int nb, const uint32_t* __restrict__ offs, u64* __restrict__ out,
+                            uint32_t* __restrict__ bad) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    DevHist h{const_cast<u64*>(htab), const_cast<u32*>(hgen), hgen[i], i};
+    DevHist h{const_cast<u64*>(htab), const_cast<u32*>(hgen), hgen[i], i, nb};
     const u32 g = h.gen(), hl = hl_of(meta[i]);
     u32 k = 0;
     u64* o = out + (size_t)offs[i] * 8;
-    for (int pos = 0; pos < HTAB; pos++) {
+    for (int pos = 0; pos < (1 << nb); pos++) {
         const u64* e = htab + h.entry(pos) * 8;
         u64 hdr = e[0];
         if ((u32)hdr != g) continue;
@@ -2461,22 +2477,23 @@ __global__ void k_ckpt_gen(const u32* __restrict__ live_hgen, const u32* __restr
 // board i takes generation gnew[i] and its saved entries are inserted by the probe rule of
 // rep_commit (gc_env.h): home slot = key & (HTAB-1), linear probing
 __global__ void k_ckpt_unpack(u64* __restrict__ htab, u32* __restrict__ hgen, const u32* __restrict__ meta, int n,
-                              const uint32_t* __restrict__ gnew, const uint32_t* __restrict__ offs,
+                              int nb, const uint32_t* __restrict__ gnew, const uint32_t* __restrict__ offs,
                               const u64* __restrict__ in, uint32_t* __restrict__ bad) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const u32 g = gnew[i];
     hgen[i] = g;
-    DevHist h{htab, hgen, g, i};
+    DevHist h{htab, hgen, g, i, nb};
     const u32 hl = hl_of(meta[i]);
+    const int size = 1 << nb;
     for (u32 k = 0; k < hl; k++) {
         const u64* e = in + ((size_t)offs[i] + k) * 8;
         Pos b = {e[1], e[2], e[3], e[4], e[5], e[6], e[7], 0};
         u32 key = board_key(b);
-        u32 pos = key & (HTAB - 1), tag = key >> HTAB_BITS;
+        u32 pos = key & (size - 1), tag = key >> nb;
         int probe = 0;
-        while ((u32)htab[h.entry((int)pos) * 8] == g && probe < HTAB) { pos = (pos + 1) & (HTAB - 1); probe++; }
-        if (probe == HTAB) { atomicOr(bad, 2u); return; }
+        while ((u32)htab[h.entry((int)pos) * 8] == g && probe < size) { pos = (pos + 1) & (size - 1); probe++; }
+        if (probe == size) { atomicOr(bad, 2u); return; }
         u64* d = htab + h.entry((int)pos) * 8;
         d[0] = (u64)g | ((u64)tag << 32) | (e[0] & (0xFFull << 56));
 #pragma unroll
@@ -2548,7 +2565,7 @@ extern "C" int gc_env_save(gc_env* e, void* buf, uint64_t cap, uint64_t* written
     uint32_t flag = 0;
     hipError_t he = hipMemsetAsync(bad, 0, 4, e->stream);
     if (he == hipSuccess) {
-        k_ckpt_pack<<<grid_for(n), BLOCK, 0, e->stream>>>(e->d.htab, e->d.hgen, e->meta, n, offs, ents, bad);
+        k_ckpt_pack<<<grid_for(n), BLOCK, 0, e->stream>>>(e->d.htab, e->d.hgen, e->meta, n, e->d.hbits, offs, ents, bad);
         he = hipGetLastError();
     }
     if (he == hipSuccess)
@@ -2609,7 +2626,8 @@ extern "C" int gc_env_load(gc_env* e, const void* buf, uint64_t size) {
         he = hipMemcpyAsync(e->slab, slab, Slab::BYTES_PER_BOARD * (size_t)n, hipMemcpyDeviceToDevice, e->stream);
     if (he == hipSuccess) he = hipMemsetAsync(bad, 0, 4, e->stream);
     if (he == hipSuccess) {
-        k_ckpt_unpack<<<grid_for(n), BLOCK, 0, e->stream>>>(e->d.htab, e->d.hgen, e->meta, n, gnew, offs, ents, bad);
+        k_ckpt_unpack<<<grid_for(n), BLOCK, 0, e->stream>>>(e->d.htab, e->d.hgen, e->meta, n, e->d.hbits, gnew, offs,
+                                                            ents, bad);
         he = hipGetLastError();
     }
     uint32_t flag = 0;
@@ -2626,6 +2644,6 @@ extern "C" int gc_env_load(gc_env* e, const void* buf, uint64_t size) {
 extern "C" uint64_t gc_env_device_bytes(gc_env* e) {
     if (!e) return 0;
     uint64_t n = (uint64_t)e->n;
-    return n * (NBB * 8 + 4) + n * HTAB * 64 + n * (4 + 4 + 2 + 4 + 1 + 1 + 4) +
+    return n * (NBB * 8 + 4) + n * ((uint64_t)64 << e->d.hbits) + n * (4 + 4 + 2 + 4 + 1 + 1 + 4) +
            n * (64 + 8 + 1 + 4 + 64);
 }

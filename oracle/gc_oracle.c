@@ -434,7 +434,8 @@ typedef struct {
      * 10) on the device and here alike. */
     int win;
 } OEnv;
-#define WINDOW_CAP 768
+/* = gc_env.h hist_cap(): 384 boards for the move-capped games, 511 for a BLACK agent's */
+#define WINDOW_CAP(e) ((e)->agent_black ? 511 : 384)
 
 uint32_t oracle_policy_index(uint64_t seed, uint32_t board, uint32_t draw, uint32_t n);
 static int kth_in_action_order(const uint16_t *moves, int n, int k);
@@ -481,7 +482,7 @@ static int env_player_move(OEnv *e, int action, int *mr, int *rep) {
     *rep = c >= 3;                                                                       /* 404-407 */
     int full = 0;
     if (irrev) e->win = 0;
-    else if (c == 1) { if (e->win >= WINDOW_CAP) full = 1; else e->win++; }
+    else if (c == 1) { if (e->win >= WINDOW_CAP(e)) full = 1; else e->win++; }
     /* state setter (315-323): board, rights, checks; current_player is NOT taken from the dict */
     memcpy(e->st.b, ns.b, 64);
     e->st.wkc = ns.wkc; e->st.wqc = ns.wqc; e->st.bkc = ns.bkc; e->st.bqc = ns.bqc;

@@ -141,9 +141,11 @@ extern "C" uint64_t host_perft(const int8_t* b, const uint8_t* m, int depth) {
 struct HostHist {  // same contract as the device DevHist (gc_env.h rep_prefetch/rep_commit)
     std::vector<RepEntry> tabv;
     u32 g = 0;
-    HostHist() : tabv(HTAB) {
+    int nbits = HTAB_BITS;
+    HostHist() : tabv(HTAB_MAX) {
         for (auto& e : tabv) e = RepEntry{0, 0, 0, 0, 0, 0, 0, 0};
     }
+    int bits() const { return nbits; }
     u32 gen() const { return g; }
     void bump_gen() { g++; }
     RepEntry load(int p) const { return tabv[p]; }
@@ -223,6 +225,7 @@ extern "C" void host_rollout_trace2(const int8_t* init, uint64_t seed, uint32_t 
     e.init = from_mailbox(init, 0);
     e.opp = opp;
     e.agent_black = !agent_white;
+    e.h.nbits = e.agent_black ? HTAB_BITS_UNCAPPED : HTAB_BITS;
     e.pc = PolicyCtx{seed, board, 0};
     e.reset();
     int a = e.pick();
@@ -275,6 +278,7 @@ extern "C" void* host_env_new2(const int8_t* init, int opp, int agent_white, uin
     e->init = from_mailbox(init, 0);
     e->opp = opp;
     e->agent_black = !agent_white;
+    e->h.nbits = e->agent_black ? HTAB_BITS_UNCAPPED : HTAB_BITS;
     e->pc = PolicyCtx{seed, board, 0};
     e->reset();
     return e;
