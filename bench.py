@@ -325,10 +325,23 @@ def variant_legs(args, rep, n):
 
         _, dt = rep.timed(run)
         s1 = [int(e.outputs()["nsteps"].sum()) for e in envs]
-        for e in envs:
-            e.close()
         out[name] = {"value": rep.sum(sum(b - a for a, b in zip(s0, s1))) / dt, "unit": "env_steps/s",
                      "steps": args.variant_steps}
+        if args.fused_plies > 0:  # the same variant's fused rollout (state in registers for the launch)
+            def fused(rp):
+                env = envs[rep.local.index(rp)]
+                env.rollout(1)
+                env.synchronize()
+                t0 = time.perf_counter()
+                st, _ = env.rollout(args.fused_plies)
+                env.synchronize()
+                return float(st[0]), time.perf_counter() - t0
+
+            fs, fdt = rep.timed(fused)
+            out[name]["fused_rollout"] = {"value": rep.sum(sum(fs)) / fdt, "unit": "env_steps/s",
+                                          "plies_per_launch": args.fused_plies}
+        for e in envs:
+            e.close()
     return out
 
 

@@ -173,6 +173,31 @@ __device__ Pos fide_reset_pos(const EnvDev& e) {
     return s;
 }
 
+// the FIDE reset position's move set for the paired kernels (as k_init_cache for the
+// reference rules): every reset lands on it
+__global__ void __launch_bounds__(BLOCK) k_finit_cache(EnvDev e, EnvDev::InitCache* out, uint16_t* acts) {
+    LDS_SCRATCH_DECL;
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    EnvDev::InitCache c = {};
+    c.pos = fide_reset_pos(e);
+    gcf::FGen f;
+    gcf::fgen(c.pos, f);
+    const bool walk = gcf::fuses_walk(f);
+    MoveSet ms;
+    moveset_clear(ms);
+    if (!walk) gcf::fgen_moves(c.pos, f, ms, scr);
+    c.own = f.g.own; c.fastp = ms.fastp; c.o1 = ms.o1; c.o2 = ms.o2; c.ol = ms.ol; c.orr = ms.orr;
+    for (int b = 0; b < 5; b++) c.cnt[b] = ms.cnt[b];
+    for (int j = 0; j < SCRATCH_SLOTS; j++) c.slots[j] = walk ? 0 : scr.get(j);
+    c.total = walk ? gcf::fcount_walk(c.pos, f, false) : ms.total;
+    c.castles = f.g.castles;
+    c.white = f.g.white;
+    c.usable = !walk;
+    c.table = c.usable && c.total > 0 && c.total <= RESET_ACTS_MAX;
+    for (int k = 0; c.table && k < c.total; k++) acts[k] = (uint16_t)select_action(c.pos, f.g, ms, scr, k);
+    *out = c;
+}
+
 // POLICY=false: external action e.act[i] (validated); POLICY=true: the random self-play
 // driver (act[i] = this state's policy pick; A_NONE or done -> reset; pick the next action)
 template <bool POLICY>

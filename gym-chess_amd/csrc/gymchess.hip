@@ -52,6 +52,7 @@ __device__ __forceinline__ void gc_stamp(int k) {
 #include "../../include/gymchess.h"
 
 using namespace gc;
+namespace gcf = gc::fide;
 
 #define NBB 7
 #define BLOCK 256
@@ -636,6 +637,7 @@ struct PairLds {
     u32 irrev[PAIR_BOARDS];                 //           irreversible move (3-fold window reset)
     u32 x0[PAIR_BOARDS];                    // W1 -> W0: the Philox word of the next draw
     u32 ra[PAIR_BOARDS];                    // W1 -> W0: the start-position table pick
+    u64 ep[PAIR_BOARDS];                    // W1 -> W0: own pawns with a legal en-passant capture (FIDE)
 };
 struct PairScratch {
     static constexpr bool kPark = true;
@@ -669,7 +671,10 @@ struct PairCtx {
 // (W0), the window h (W1; its table write is left deferred in h), the step counter nst.
 // Returns the ply's env.step() outputs; on return both waves hold the same s, and with
 // SHARE_ACT the same next action a (W0 picks it; it crosses to W1 through LDS).
-template <bool SHARE_ACT>
+// FIDE = rules "fide" (gc_fide.h): fapply, the enemy map without the own king, en passant,
+// FIDE castling (from W0, which alone holds the in-check flag), no king captures; a legal
+// move never leaves the mover in check, so there is no mover-check and no both-checked end.
+template <bool SHARE_ACT, bool FIDE = false>
 __device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, int role, int l, int i,
                                             bool live, const Pos& rp, Pos& s, int& a, u32& d, DevHist& h,
                                             u32& nst) {
@@ -693,8 +698,12 @@ __device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, int ro
     // before phase 3)
     if (role == 0) {
         ns = s;
-        ns.meta = (ns.meta & ~(u32)M_RIGHTS) | eff_rights(s);  // State::new
-        if (mv) apply_legal(ns, white, a, &mr, &irrev);
+        if constexpr (FIDE) {
+            if (mv) gcf::fapply(ns, a, 0, &mr, &irrev);
+        } else {
+            ns.meta = (ns.meta & ~(u32)M_RIGHTS) | eff_rights(s);  // State::new
+            if (mv) apply_legal(ns, white, a, &mr, &irrev);
+        }
         L.ns[0][l] = ns.k; L.ns[1][l] = ns.q; L.ns[2][l] = ns.r; L.ns[3][l] = ns.b;
         L.ns[4][l] = ns.n; L.ns[5][l] = ns.p; L.ns[6][l] = ns.w;
         L.nmeta[l] = ns.meta;
@@ -710,8 +719,14 @@ __device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, int ro
 
     // ---- phase 1
     Gen g;
+    u64 ep_from = 0;
+    int ep = -1;
     if (role == 0) {
         gen_base(ns, g);
+        if constexpr (FIDE) {  // FIDE positions hold one king per side: the first one (gcf::fgen)
+            u64 myk = ns.k & g.own;
+            g.ks = myk ? ctz(myk) : -1;
+        }
         gen_pins(ns, g);
         L.pin3[0][l] = g.checkmask;
         L.pin3[1][l] = g.pinned;
@@ -724,10 +739,35 @@ __device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, int ro
         mr = L.mr[l];
         irrev = L.irrev[l] != 0;
         gen_base(ns, g);
-        gen_enemy(ns, g);
-        my_chk = mv && mover_checked(s, ns, white, a);
-        L.enemy[l] = g.enemy_att;
-        L.f1[l] = g.castles | (my_chk ? 4u : 0u);
+        if constexpr (FIDE) {
+            u64 myk = ns.k & g.own;
+            g.ks = myk ? ctz(myk) : -1;
+            if (g.ks >= 0) {  // enemy map with the own king removed: no retreat along a checking ray
+                Pos t = ns;
+                t.k &= ~myk;
+                t.w &= ~myk;
+                g.enemy_att = side_attacks(t, !g.white);
+            }
+            int ept = gcf::ep_square(ns.meta);  // en passant: legal captures (gcf::fgen)
+            if (ept >= 0) {
+                int capsq = g.white ? ept + 8 : ept - 8;
+                u64 cand = pawn_att_set(bit(ept), !g.white) & ns.p & g.own;
+                bool ok = (ns.p & g.opp & bit(capsq)) && !(g.occ & bit(ept));
+                while (ok && cand) {
+                    int fr = ctz(cand);
+                    cand &= cand - 1;
+                    u64 occ2 = (g.occ ^ bit(fr) ^ bit(capsq)) | bit(ept);
+                    if (g.ks < 0 || !gcf::king_hit(ns, g.ks, g.white, occ2, g.opp & ~bit(capsq))) ep_from |= bit(fr);
+                }
+            }
+            L.enemy[l] = g.enemy_att;
+            L.ep[l] = ep_from;
+        } else {
+            gen_enemy(ns, g);
+            my_chk = mv && mover_checked(s, ns, white, a);
+            L.enemy[l] = g.enemy_att;
+            L.f1[l] = g.castles | (my_chk ? 4u : 0u);
+        }
     }
     GC_STAMP(2);
     pair_barrier();
@@ -736,17 +776,34 @@ __device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, int ro
     // ---- phase 2
     if (role == 0) {
         g.enemy_att = L.enemy[l];
-        u32 f1 = L.f1[l];
-        g.castles = f1 & 3u;
-        my_chk = (f1 & 4u) != 0;
+        if constexpr (FIDE) {
+            ep_from = L.ep[l];
+            if (g.ks >= 0) {  // FIDE castling: rights, king and rook home, path empty and unattacked
+                const u64 myk = ns.k & g.own;
+                const int base = g.white ? 56 : 0;
+                bool kok = (myk & bit(base + 4)) && !g.in_check;
+                u64 myr = ns.r & g.own, A = g.enemy_att, occ = g.occ;
+                bool ksr = (ns.meta & (g.white ? M_WKC : M_BKC)) != 0, qsr = (ns.meta & (g.white ? M_WQC : M_BQC)) != 0;
+                bool kside = kok && ksr && (myr & bit(base + 7)) && !(occ & (3ull << (base + 5))) && !(A & (3ull << (base + 5)));
+                bool qside = kok && qsr && (myr & bit(base)) && !(occ & (7ull << (base + 1))) && !(A & (3ull << (base + 2)));
+                g.castles = (qside ? 1u : 0u) | (kside ? 2u : 0u);
+            }
+        } else {
+            u32 f1 = L.f1[l];
+            g.castles = f1 & 3u;
+            my_chk = (f1 & 4u) != 0;
+        }
     } else {
         g.checkmask = L.pin3[0][l];
         g.pinned = L.pin3[1][l];
         g.pinrays = L.pin3[2][l];
         g.in_check = L.f0[l] != 0;
     }
+    if constexpr (FIDE) {
+        ep = ep_from ? gcf::ep_square(ns.meta) : -1;
+    }
     const bool opp_chk = g.in_check;
-    const bool both = opp_chk && my_chk;                      // lib.rs:1442-1446
+    const bool both = !FIDE && opp_chk && my_chk;             // lib.rs:1442-1446
     const bool gen = mv && !both;
     MoveSet ms;
     moveset_clear(ms);
@@ -755,9 +812,20 @@ __device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, int ro
     int c = 0;
     u32 hl = hl_of(s.meta);
     if (role == 0) {
-        if (gen) part = ms.big ? count_legal(ns, g) - popc(g.castles) : gen_moves_a(ns, g, ms, scr);
+        if constexpr (FIDE) {  // castles counted here (W1 does not know them)
+            if (gen) {
+                if (ms.big) {
+                    gcf::FGen f{g, ep_from, ep};
+                    part = gcf::fcount_walk(ns, f, false);
+                } else {
+                    part = gen_moves_a<PairScratch, true>(ns, g, ms, scr, FideExtra{ep_from, ep}) + popc(g.castles);
+                }
+            }
+        } else {
+            if (gen) part = ms.big ? count_legal(ns, g) - popc(g.castles) : gen_moves_a(ns, g, ms, scr);
+        }
     } else {
-        if (gen && !ms.big) part = gen_moves_b(ns, g, ms, scr);
+        if (gen && !ms.big) part = FIDE ? gen_moves_b<PairScratch, true>(ns, g, ms, scr) : gen_moves_b(ns, g, ms, scr);
         if (gen) {
             // the probe's data is first touched here (an opaque use after the generation:
             // otherwise the compiler hoists the entry compare up to the load and waits there)
@@ -778,7 +846,7 @@ __device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, int ro
     // ---- phase 3: outcome (both waves), then the pick (W0)
 #pragma unroll
     for (int b = 0; b < 5; b++) ms.cnt[b] |= L.planes[role ^ 1][b][l];
-    ms.total = part + (int)L.part[role ^ 1][l] + popc(g.castles);
+    ms.total = part + (int)L.part[role ^ 1][l] + (FIDE ? 0 : popc(g.castles));
     if (role == 0) {
         u32 rpk = L.rep[l];
         c = (int)(rpk & 0xFFu);
@@ -827,6 +895,8 @@ __device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, int ro
             act = ra;
             tot = (int)C.rtotal;
         } else {
+            bool walk = false;  // FIDE, > SCRATCH_SLOTS own pieces: the per-square walk
+            gcf::FGen f;
             if (!have) {
                 const EnvDev::InitCache& ic = *C.icd;
                 if (ic.usable) {
@@ -838,13 +908,27 @@ __device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, int ro
                     ms.big = false;
 #pragma unroll
                     for (int j = 0; j < SCRATCH_SLOTS; j++) scr.put(j, ic.slots[j]);
+                } else if constexpr (FIDE) {
+                    gcf::fgen(s, f);
+                    g = f.g;
+                    walk = gcf::fuses_walk(f);
+                    if (walk) ms.total = gcf::fcount_walk(s, f, false);
+                    else gcf::fgen_moves(s, f, ms, scr);
                 } else {
                     gen_init(s, g);
                     gen_moves(s, g, ms, scr);
                 }
+            } else if constexpr (FIDE) {
+                if (ms.big) {
+                    f = gcf::FGen{g, ep_from, ep};
+                    walk = true;
+                }
             }
             tot = ms.total;
-            if (tot > 0) act = (uint16_t)select_action(s, g, ms, scr, (int)scale_rank(x0, (u32)tot));
+            if (tot > 0) {
+                int k = (int)scale_rank(x0, (u32)tot);
+                act = (uint16_t)(walk ? gcf::fselect(s, f, k) : select_action(s, g, ms, scr, k));
+            }
         }
         a = act;
         d += tot > 0 ? 1u : 0u;
@@ -932,12 +1016,13 @@ __device__ __forceinline__ PairIO store_io(uint8_t* slab, int nn) {
     int a = (int)ua;                                                                                        \
     DevHist h = DevHist{htab, in_io.hgen, g0, ii};
 
+template <bool FIDE>
 __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
     k_env_step2(uint8_t* __restrict__ slab, int nn, int blk0, uint64_t seed, u64* __restrict__ htab,
                 const uint16_t* __restrict__ racts, const EnvDev::InitCache* __restrict__ icd,
                 u32 rinfo /* ic.table << 16 | ic.total */) {
     PAIR_PROLOGUE
-    StepOut o = pair_ply<false>(L, C, role, l, i, live, rp, s, a, d, h, nst);
+    StepOut o = pair_ply<false, FIDE>(L, C, role, l, i, live, rp, s, a, d, h, nst);
     GC_STAMP(6);
     const PairIO io = store_io(slab, nn);
     if (live) {
@@ -963,6 +1048,7 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
 
 // Fused K-ply random self-play on the paired step: the state stays in registers; the last
 // ply's outputs and per-board stats (as k_env_rollout) are written at the end.
+template <bool FIDE>
 __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
     k_env_rollout2(uint8_t* __restrict__ slab, int nn, int blk0, uint64_t seed, u64* __restrict__ htab,
                    const uint16_t* __restrict__ racts, const EnvDev::InitCache* __restrict__ icd, u32 rinfo, int plies,
@@ -973,7 +1059,7 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
     StepOut o = {0, 0, R_NONE, 0};
     for (int p = 0; p < plies; p++) {
         int played = a;
-        o = pair_ply<true>(L, C, role, l, i, live, rp, s, a, d, h, nst);
+        o = pair_ply<true, FIDE>(L, C, role, l, i, live, rp, s, a, d, h, nst);
         if (played == A_NONE) {
             e_nomove++;
         } else {
@@ -1669,6 +1755,9 @@ struct gc_env {
     int8_t* ep = nullptr;       // FIDE ingest: en-passant files
     uint16_t* reset_acts = nullptr;
     EnvDev::InitCache* icd = nullptr;  // device copy of d.ic (the paired kernels read it from HBM)
+    EnvDev::InitCache* icd_f = nullptr;  // the same for the FIDE reset position (gc_env_set_rules)
+    uint16_t* racts_f = nullptr;
+    EnvDev::InitCache ic_f = {};
     uint8_t* slab = nullptr;  // per-board fields (Slab): bb, meta, hgen, draw, nsteps, reward, act, done, reason
     hipGraphExec_t graph_exec = nullptr;  // GC_GRAPH: a captured chunk of step launches
     int graph_chunk = 0;
@@ -1682,8 +1771,8 @@ struct gc_env {
 };
 
 static void env_free(gc_env* e) {
-    void* ps[] = {e->reset_acts, e->icd, e->ep, e->slab, e->d.htab, e->mbox, e->m8, e->mask, e->list, e->counts,
-                  e->lmask, e->stats};
+    void* ps[] = {e->reset_acts, e->icd, e->icd_f, e->racts_f, e->ep, e->slab, e->d.htab, e->mbox, e->m8, e->mask,
+                  e->list, e->counts, e->lmask, e->stats};
     for (void* p : ps) if (p) (void)hipFree(p);
     for (auto& v : e->ev) if (v) (void)hipEventDestroy(v);
     for (int j = 0; j < GC_MAX_SUBSTREAMS; j++) {
@@ -1709,14 +1798,30 @@ static void launch_step(gc_env* e) {
     else k_env_step<POLICY, false><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d);
 }
 
+// the reset position's cache of the env's rules (reference or FIDE) for the paired kernels
+struct ResetInfo {
+    const EnvDev::InitCache* icd;
+    const uint16_t* racts;
+    u32 rinfo;  // table << 16 | total
+};
+static ResetInfo reset_info(const gc_env* e) {
+    const EnvDev::InitCache& ic = e->rules ? e->ic_f : e->d.ic;
+    return ResetInfo{e->rules ? e->icd_f : e->icd, e->rules ? e->racts_f : e->d.reset_acts,
+                     (ic.table ? 1u << 16 : 0u) | (u32)(ic.total & 0xFFFF)};
+}
+
 // one ply of the paired step kernel over the board blocks [b0, b0 + nb) (64 boards each)
 static void launch_step2(gc_env* e, hipStream_t st, int b0 = 0, int nb = -1) {
     const EnvDev& d = e->d;
-    u32 rinfo = (d.ic.table ? 1u << 16 : 0u) | (u32)(d.ic.total & 0xFFFF);
+    const ResetInfo r = reset_info(e);
     const int per_wg = PAIR_BOARDS * PAIRS_WG;
     if (nb < 0) nb = (e->n + PAIR_BOARDS - 1) / PAIR_BOARDS;
-    k_env_step2<<<(nb + PAIRS_WG - 1) / PAIRS_WG, 2 * per_wg, 0, st>>>(e->slab, d.n, b0, d.seed, d.htab, d.reset_acts,
-                                                                     e->icd, rinfo);
+    if (e->rules)
+        k_env_step2<true><<<(nb + PAIRS_WG - 1) / PAIRS_WG, 2 * per_wg, 0, st>>>(e->slab, d.n, b0, d.seed, d.htab,
+                                                                               r.racts, r.icd, r.rinfo);
+    else
+        k_env_step2<false><<<(nb + PAIRS_WG - 1) / PAIRS_WG, 2 * per_wg, 0, st>>>(e->slab, d.n, b0, d.seed, d.htab,
+                                                                                r.racts, r.icd, r.rinfo);
 }
 
 extern "C" int gc_env_create(int device, int n_boards, uint64_t seed, const int8_t* initial_board, gc_env** out) {
@@ -1849,6 +1954,14 @@ extern "C" int gc_env_set_rules(gc_env* e, int rules) {
     if (rules && e->d.opp) return fail("the FIDE rules mode supports opponent \"none\" only");
     HIPCHK(hipSetDevice(e->device));
     HIPCHK(hipStreamSynchronize(e->stream));
+    if (rules && !e->icd_f) {  // the FIDE reset position's move set (paired kernels)
+        if (dalloc(&e->icd_f, 1) || dalloc(&e->racts_f, RESET_ACTS_MAX)) return -1;
+        k_finit_cache<<<1, BLOCK, 0, e->stream>>>(e->d, e->icd_f, e->racts_f);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(&e->ic_f, e->icd_f, sizeof(EnvDev::InitCache), hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream));
+    }
+    if (e->graph_exec && rules != e->rules) { (void)hipGraphExecDestroy(e->graph_exec); e->graph_exec = nullptr; }
     e->rules = rules;
     HIPCHK(hipMemsetAsync(e->d.draw, 0, (size_t)4 * e->n, e->stream));
     launch_reset(e, nullptr, 1);
@@ -1980,7 +2093,7 @@ extern "C" int gc_env_step_random(gc_env* e, int n_plies) {
     HIPCHK(hipSetDevice(e->device));
     static const bool one_wave = getenv("GC_STEP1") != nullptr;  // A/B switch to k_env_step<true, false>
     static const int graph_chunk = getenv("GC_GRAPH") ? atoi(getenv("GC_GRAPH")) : 0;
-    const bool pair = !e->d.opp && !e->rules && !one_wave;
+    const bool pair = !e->d.opp && !one_wave;  // reference or FIDE rules, opponent "none": the paired kernel
     int p = 0;
     if (pair && graph_chunk > 0) {
         if (!e->graph_exec || e->graph_chunk != graph_chunk) {  // captured once per env
@@ -2042,10 +2155,10 @@ extern "C" int gc_env_rollout(gc_env* e, int n_plies, int16_t* tr_action, int16_
                               uint8_t* tr_reason, uint64_t* stats8) {
     if (!e) return fail("null env");
     if (n_plies < 0) return fail("n_plies must be >= 0");
-    if (e->rules) return fail("fused rollout: reference rules only (use gc_env_step_random under FIDE rules)");
     if (!e->policy_ready) return fail("policy actions stale: call gc_env_reset or gc_env_select_random first");
     HIPCHK(hipSetDevice(e->device));
     bool trace = tr_action || tr_reward || tr_done || tr_reason;
+    if (e->rules && trace) return fail("fused rollout under FIDE rules: no per-ply traces (use gc_env_step_random)");
     int16_t *da = nullptr, *dr = nullptr;
     uint8_t *dd = nullptr, *dq = nullptr;
     size_t cnt = (size_t)n_plies * e->n;
@@ -2054,12 +2167,16 @@ extern "C" int gc_env_rollout(gc_env* e, int n_plies, int16_t* tr_action, int16_
     static const bool one_wave = getenv("GC_STEP1") != nullptr;
     if (e->d.opp) {
         k_env_rollout<true><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d, n_plies, da, dr, dd, dq, e->stats);
-    } else if (!trace && !one_wave) {  // the paired kernel (per-ply traces: the one-wave kernel)
+    } else if (!trace && (!one_wave || e->rules)) {  // the paired kernel (per-ply traces: the one-wave kernel)
         const EnvDev& d = e->d;
-        u32 rinfo = (d.ic.table ? 1u << 16 : 0u) | (u32)(d.ic.total & 0xFFFF);
-        k_env_rollout2<<<(e->n + PAIR_BOARDS * PAIRS_WG - 1) / (PAIR_BOARDS * PAIRS_WG), 2 * PAIR_BOARDS * PAIRS_WG, 0,
-                         e->stream>>>(
-            e->slab, d.n, 0, d.seed, d.htab, d.reset_acts, e->icd, rinfo, n_plies, e->stats);
+        const ResetInfo r = reset_info(e);
+        const int grid = (e->n + PAIR_BOARDS * PAIRS_WG - 1) / (PAIR_BOARDS * PAIRS_WG), bs = 2 * PAIR_BOARDS * PAIRS_WG;
+        if (e->rules)
+            k_env_rollout2<true><<<grid, bs, 0, e->stream>>>(e->slab, d.n, 0, d.seed, d.htab, r.racts, r.icd, r.rinfo,
+                                                             n_plies, e->stats);
+        else
+            k_env_rollout2<false><<<grid, bs, 0, e->stream>>>(e->slab, d.n, 0, d.seed, d.htab, r.racts, r.icd, r.rinfo,
+                                                              n_plies, e->stats);
     } else {
         k_env_rollout<false><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d, n_plies, da, dr, dd, dq, e->stats);
     }

@@ -153,8 +153,8 @@ int gc_state_to_fen(const int8_t* board, const uint8_t* meta, char* out, int cap
 /* rules 1 (FIDE): meta[7] = en-passant file + 1 (parsed / written) instead of move_count */
 int gc_fen_to_state_rules(const char* fen, int8_t* board, uint8_t* meta, int rules);
 int gc_state_to_fen_rules(const int8_t* board, const uint8_t* meta, char* out, int cap, int rules);
-/* Rules of the env (see gc_engine_set_rules); FIDE needs opponent "none" and has no fused
- * rollout.  Resets every board. */
+/* Rules of the env (see gc_engine_set_rules); FIDE needs opponent "none" (its fused rollout
+ * keeps no per-ply traces).  Resets every board. */
 int gc_env_set_rules(gc_env* e, int rules);
 /* set every board from a FEN (n strings); check flags from update_state (lib.rs:1386-1393);
  * repetition windows cleared */

@@ -170,12 +170,12 @@ def test_fide_engine_lists_and_next_state_vs_host():
 
 @pytest.mark.gpu
 def test_fide_env_step_random_vs_host():
-    """The FIDE env's device driver (k_fenv_step<true>) ply by ply == the host build of
-    fide::fenv_step with the same Philox policy stream."""
+    """The FIDE env's device driver (the paired kernel k_env_step2<FIDE>) ply by ply == the
+    host build of fide::fenv_step with the same Philox policy stream."""
     from gym_chess_amd import codec as C
     from gym_chess_amd.env import BatchedChessEnv
 
-    n, plies, seed = 96, 400, 0xF1DE
+    n, plies, seed = 256, 700, 0xF1DE
     env = BatchedChessEnv(n, device=0, seed=seed, rules="fide")
     init = np.array(C.DEFAULT_BOARD, dtype=np.int8).reshape(64)
     refs = [H.fide_rollout(seed, i, plies + 1, init) for i in range(n)]
@@ -188,6 +188,26 @@ def test_fide_env_step_random_vs_host():
         assert (o["reason"] == np.stack([r["reason"][p] for r in refs])).all(), p
         nxt = np.where(ra[p + 1] < 0, 0xFFFF, ra[p + 1]).astype(np.uint16)
         assert (o["next_action"] == nxt).all(), p
+
+
+@pytest.mark.gpu
+def test_fide_fused_rollout_matches_step_random():
+    """The FIDE paired kernels: the fused rollout (k_env_rollout2<FIDE>) == K launches of the
+    one-ply step (k_env_step2<FIDE>), states / outputs / next actions, on 200 boards (a
+    partial last workgroup) over 600 plies (resets, mates, repetitions, promotions)."""
+    from gym_chess_amd.env import BatchedChessEnv
+
+    n, plies = 200, 600
+    a = BatchedChessEnv(n, device=0, seed=77, rules="fide")
+    b = BatchedChessEnv(n, device=0, seed=77, rules="fide")
+    a.step_random(plies)
+    b.rollout(plies)
+    ba, ma = a.boards()
+    bb, mb = b.boards()
+    assert (ba == bb).all() and (ma == mb).all() and (a.en_passant() == b.en_passant()).all()
+    oa, ob = a.outputs(), b.outputs()
+    for k in ("next_action", "nsteps", "reward", "done", "reason"):
+        assert (oa[k] == ob[k]).all(), k
 
 
 @pytest.mark.gpu
@@ -210,7 +230,7 @@ def test_fide_env_external_steps_and_fens():
     rw, dn, why = env.step(np.array([4100] * 4, dtype=np.uint16))
     assert (rw == -10).all() and (why == 6).all()  # RESIGN is never a legal action
     with pytest.raises(Exception):
-        env.rollout(10)  # no fused rollout under FIDE rules
+        env.rollout(10, trace=True)  # the FIDE fused rollout keeps no per-ply traces
 
 
 @pytest.mark.gpu
