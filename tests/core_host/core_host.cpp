@@ -105,6 +105,16 @@ extern "C" int host_mover_checked(const int8_t* b, const uint8_t* m, int action)
     return (mover_checked(s, ns, white, action) ? 1 : 0) | (full ? 2 : 0);
 }
 
+// the two forms of the pin / check sets (gc_core.h gen_pins_aligned, gen_pins_part) agree
+extern "C" int host_pins_agree(const int8_t* b, const uint8_t* m, int white) {
+    Pos s = import_state(b, m, white);
+    Gen g, h;
+    gen_base(s, g);
+    h = g;
+    gen_pins_finish(g, gen_pins_aligned(s, g));  // the block sets differ by the checker square itself,
+    gen_pins_finish(h, gen_pins_part<15, true>(s, h));  // the check masks (checkers | block) do not
+    return g.in_check == h.in_check && g.checkmask == h.checkmask && g.pinned == h.pinned && g.pinrays == h.pinrays;
+}
 extern "C" uint64_t host_between(int a, int b) { return between(a, b); }
 extern "C" uint64_t host_rook_att(int sq, uint64_t occ) { return rook_att(sq, occ); }
 extern "C" uint64_t host_bishop_att(int sq, uint64_t occ) { return bishop_att(sq, occ); }

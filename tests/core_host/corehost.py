@@ -22,6 +22,7 @@ def lib():
             subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wno-unknown-pragmas", "-o", _SO, src], check=True)
         L = ctypes.CDLL(_SO)
         L.host_between.restype = ctypes.c_uint64
+        L.host_pins_agree.argtypes = [P, P, ctypes.c_int]
         L.host_rook_att.restype = ctypes.c_uint64
         L.host_rook_att.argtypes = [ctypes.c_int, ctypes.c_uint64]
         L.host_bishop_att.restype = ctypes.c_uint64

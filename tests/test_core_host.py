@@ -181,3 +181,17 @@ def test_mover_check_shortcut_every_legal_move():
                 hits["castle_or_multi"] += a >= 4096
     # the interesting cases occur (Q6 retreats along a checking ray, castles)
     assert hits["king_move_checked"] > 50 and hits["castle_or_multi"] > 50, hits
+
+
+@pytest.mark.parametrize("seed", [51, 52, 53])
+def test_pin_forms_agree(seed):
+    """gen_pins_aligned (the aligned-slider loop the kernels run) == gen_pins_part (the
+    four-line x-ray form) on fuzz positions, both sides to move: in check, check mask,
+    pinned, pin rays."""
+    from conftest import random_positions
+
+    boards, metas = random_positions(3000, seed)
+    L = H.lib()
+    for i in range(len(boards)):
+        for white in (0, 1):
+            assert L.host_pins_agree(boards[i].ctypes.data, metas[i].ctypes.data, white) == 1, (i, white)
