@@ -600,15 +600,20 @@ __global__ void __launch_bounds__(BLOCK) k_env_step(EnvDev e) {
 // one wave per SIMD -- 65 536 boards on 256 CUs -- leaves half the issue slots empty and
 // every memory/LDS wait exposed.  Here lane l of wave 0 and lane l of wave 1 share board l
 // and split its ply into two independent instruction streams (wave-uniform roles, no
-// divergence), exchanging through LDS at two barriers:
+// divergence), exchanging through LDS at barriers:
 //
-//   phase 1   W0: gen_pins (checkers, check mask, pins)
-//             W1: window probe of the pre-move board, gen_enemy (enemy map, castles), the
-//                 mover's own check flag
-//   ---- barrier: W0 gets enemy map / castles / mover-check, W1 gets check mask / pins
-//   phase 2   W0: Philox word of the next draw, pawns, knights, kings (gen_moves_a)
-//             W1: bishops, rooks, queens (gen_moves_b), then the 3-fold commit (the probe
-//                 has landed by now)
+//   phase 0   W0: applies the action (post-move board to LDS)
+//             W1: issues the 3-fold window probe of the pre-move board, the Philox word of the
+//                 next draw, the read of a reset board's pick from the start-position table
+//                 (a serial multiply chain, hidden behind W0's move)
+//   ---- barrier
+//   phase 1   W0: checkers, check mask, pins (from the aligned enemy sliders), the enemy's
+//                 diagonal slider attacks
+//             W1: the enemy's leaper and orthogonal slider attacks, the mover's own check flag
+//   ---- barrier: W0 gets the rest of the enemy map and the mover-check, W1 the check mask /
+//                 pins
+//   phase 2   W0: castles, pawns, knights, kings, queens (gen_moves_a)
+//             W1: bishops, rooks (gen_moves_b), then the 3-fold commit (the probe has landed)
 //   ---- barrier: partial count planes / totals / 3-fold count exchanged
 //   phase 3   both: the step's outcome (reward, done, reason, move count, reset) --
 //             identical arithmetic on identical data; W0: the policy pick (k-th legal
@@ -618,14 +623,14 @@ __global__ void __launch_bounds__(BLOCK) k_env_step(EnvDev e) {
 // same order of decisions; tests/test_gpu_parity.py compares both with the oracle).
 #define PAIR_BOARDS 64
 #ifndef PAIRS_WG
-#define PAIRS_WG 1  // board pairs (64 boards, two waves) per workgroup
+#define PAIRS_WG 2  // board pairs (64 boards, two waves) per workgroup: 1 -> 9.8 us per ply, 2 -> 9.3, 4 -> 10.6
 #endif
 struct PairLds {
     u64 slots[SCRATCH_SLOTS][PAIR_BOARDS];  // parked targets (both waves write, W0 reads)
     u64 pin3[3][PAIR_BOARDS];               // W0 -> W1: checkmask, pinned, pinrays
-    u64 enemy[PAIR_BOARDS];                 // W1 -> W0: enemy attack map
+    u64 enemy[PAIR_BOARDS];                 // W1 -> W0: enemy leaper + orthogonal attacks
     u32 f0[PAIR_BOARDS];                    // W0 -> W1: in_check
-    u32 f1[PAIR_BOARDS];                    // W1 -> W0: castles | my_chk << 2
+    u32 f1[PAIR_BOARDS];                    // W1 -> W0: my_chk
     u64 planes[2][5][PAIR_BOARDS];          // partial bit-sliced counts per wave
     u32 part[2][PAIR_BOARDS];               // partial move totals per wave
     u32 rep[PAIR_BOARDS];                   // W1 -> W0: 3-fold count c | window length << 8
@@ -717,10 +722,12 @@ __device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, int ro
     }
     pair_barrier();
 
-    // ---- phase 1
+    // ---- phase 1: W0 pins / checkers and the enemy's diagonal slider attacks; W1 the enemy's
+    // leaper and orthogonal slider attacks and the mover's own check flag (FIDE: en passant)
     Gen g;
     u64 ep_from = 0;
     int ep = -1;
+    u64 enemy_diag = 0;
     if (role == 0) {
         gen_base(ns, g);
         if constexpr (FIDE) {  // FIDE positions hold one king per side: the first one (gcf::fgen)
@@ -732,6 +739,16 @@ __device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, int ro
         L.pin3[1][l] = g.pinned;
         L.pin3[2][l] = g.pinrays;
         L.f0[l] = g.in_check ? 1u : 0u;
+        if (g.ks >= 0) {
+            if constexpr (FIDE) {  // without the own king: no retreat along a checking ray
+                Pos t = ns;
+                t.k &= ~(ns.k & g.own);
+                t.w &= ~(ns.k & g.own);
+                enemy_diag = side_attacks_diag(t, !g.white);
+            } else {
+                enemy_diag = side_attacks_diag(ns, !g.white);
+            }
+        }
     } else {
         ns.k = L.ns[0][l]; ns.q = L.ns[1][l]; ns.r = L.ns[2][l]; ns.b = L.ns[3][l];
         ns.n = L.ns[4][l]; ns.p = L.ns[5][l]; ns.w = L.ns[6][l];
@@ -746,7 +763,7 @@ __device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, int ro
                 Pos t = ns;
                 t.k &= ~myk;
                 t.w &= ~myk;
-                g.enemy_att = side_attacks(t, !g.white);
+                g.enemy_att = side_attacks_leapers(t, !g.white) | side_attacks_orth(t, !g.white);
             }
             int ept = gcf::ep_square(ns.meta);  // en passant: legal captures (gcf::fgen)
             if (ept >= 0) {
@@ -763,10 +780,10 @@ __device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, int ro
             L.enemy[l] = g.enemy_att;
             L.ep[l] = ep_from;
         } else {
-            gen_enemy(ns, g);
+            if (g.ks >= 0) g.enemy_att = side_attacks_leapers(ns, !g.white) | side_attacks_orth(ns, !g.white);
             my_chk = mv && mover_checked(s, ns, white, a);
             L.enemy[l] = g.enemy_att;
-            L.f1[l] = g.castles | (my_chk ? 4u : 0u);
+            L.f1[l] = my_chk ? 1u : 0u;
         }
     }
     GC_STAMP(2);
@@ -775,7 +792,7 @@ __device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, int ro
 
     // ---- phase 2
     if (role == 0) {
-        g.enemy_att = L.enemy[l];
+        g.enemy_att = L.enemy[l] | enemy_diag;
         if constexpr (FIDE) {
             ep_from = L.ep[l];
             if (g.ks >= 0) {  // FIDE castling: rights, king and rook home, path empty and unattacked
@@ -789,9 +806,8 @@ __device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, int ro
                 g.castles = (qside ? 1u : 0u) | (kside ? 2u : 0u);
             }
         } else {
-            u32 f1 = L.f1[l];
-            g.castles = f1 & 3u;
-            my_chk = (f1 & 4u) != 0;
+            gen_castles(ns, g);  // lib.rs:578-610 with the whole enemy map
+            my_chk = L.f1[l] != 0;
         }
     } else {
         g.checkmask = L.pin3[0][l];
@@ -821,8 +837,8 @@ __device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, int ro
                     part = gen_moves_a<PairScratch, true>(ns, g, ms, scr, FideExtra{ep_from, ep}) + popc(g.castles);
                 }
             }
-        } else {
-            if (gen) part = ms.big ? count_legal(ns, g) - popc(g.castles) : gen_moves_a(ns, g, ms, scr);
+        } else {  // castles counted here (W1 does not know them)
+            if (gen) part = ms.big ? count_legal(ns, g) : gen_moves_a(ns, g, ms, scr) + popc(g.castles);
         }
     } else {
         if (gen && !ms.big) part = FIDE ? gen_moves_b<PairScratch, true>(ns, g, ms, scr) : gen_moves_b(ns, g, ms, scr);
@@ -846,7 +862,7 @@ __device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, int ro
     // ---- phase 3: outcome (both waves), then the pick (W0)
 #pragma unroll
     for (int b = 0; b < 5; b++) ms.cnt[b] |= L.planes[role ^ 1][b][l];
-    ms.total = part + (int)L.part[role ^ 1][l] + (FIDE ? 0 : popc(g.castles));
+    ms.total = part + (int)L.part[role ^ 1][l];  // W0's part holds the castles
     if (role == 0) {
         u32 rpk = L.rep[l];
         c = (int)(rpk & 0xFFu);
@@ -2069,7 +2085,9 @@ static int issue_plies(gc_env* e, int n) {
     }
     const int blocks = (e->n + PAIR_BOARDS - 1) / PAIR_BOARDS;
     const int k = e->n_sub < blocks ? e->n_sub : blocks;
-    const int per = (blocks + k - 1) / k;
+    // a range is a whole number of workgroups (PAIRS_WG blocks each), so no workgroup reaches
+    // into the next range; only the last range is partial, and beyond it every lane is dead
+    const int per = ((blocks + k - 1) / k + PAIRS_WG - 1) / PAIRS_WG * PAIRS_WG;
     HIPCHK(hipEventRecord(e->fork_ev, e->stream));
     for (int j = 0; j < k; j++) HIPCHK(hipStreamWaitEvent(e->sub[j], e->fork_ev, 0));
     for (int p = 0; p < n; p++)

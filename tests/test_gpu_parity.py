@@ -495,3 +495,23 @@ def test_chess_engine_compat_dict_api(oracle):
     with pytest.raises(KeyError):
         eng.get_possible_moves({"board": C.DEFAULT_BOARD}, "WHITE")
     assert eng.get_castle_moves(st, "WHITE") == []
+
+
+@pytest.mark.parametrize("n", [70, 200, 1000])
+def test_step_random_board_range_streams_agree(n):
+    """gc_env_step_random over 1, 2 and 3 board-range streams (ranges are whole workgroups of
+    PAIRS_WG blocks; the last one partial): identical states and outputs."""
+    from gym_chess_amd.env import BatchedChessEnv
+
+    res = []
+    for k in (1, 2, 3):
+        env = BatchedChessEnv(n, device=0, seed=4040)
+        env.set_streams(k)
+        env.step_random(333)
+        b, m = env.boards()
+        res.append((b, m, env.outputs()))
+        env.close()
+    for b, m, o in res[1:]:
+        assert (b == res[0][0]).all() and (m == res[0][1]).all()
+        for key in o:
+            assert (o[key] == res[0][2][key]).all(), key

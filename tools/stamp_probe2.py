@@ -9,7 +9,7 @@ import sys
 
 import numpy as np
 
-L = ctypes.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "_build_stamps.so"))
+L = ctypes.CDLL(os.environ.get("STAMP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "_build_stamps.so"))
 P = ctypes.c_void_p
 L.gc_env_create.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint64, P, P]
 L.gc_env_step_random.argtypes = [P, ctypes.c_int]
