@@ -1208,23 +1208,28 @@ __global__ void __launch_bounds__(BLOCK) k_sum_stats(const uint64_t* __restrict_
 // convention; the reference resets on the caller's reset()) and the random policy's pick
 // over the new list (a ready-made next action; also becomes the env's act[]).
 
-// legal-action mask of the position gen_moves described: word f = targets of from-square f,
-// word 64 bit c = action 4096 + c (castles)
+// legal-action mask of the position gen_moves described, WORD-MAJOR: o[f * n] = targets of
+// from-square f of this board (o = mask + board), o[64 * n] bit c = action 4096 + c (castles).
+// Word-major so that each of the 65 stores of a wave writes 512 contiguous bytes: every word
+// is first zeroed (coalesced), then the own pieces' words are written (at most 16 of them;
+// the parked slot of the j-th own piece is slot j, fast pawns from their origin sets).
 template <class S>
-__device__ void write_mask(const Pos& s, const Gen& g, const MoveSet& ms, const S& scr, u64* __restrict__ o) {
-    for (int sq = 0; sq < 64; sq++) {
-        u64 w = 0;
-        if ((g.own >> sq) & 1) {
-            if (ms.big) w = legal_targets(s, g, sq, type_at(s, sq));
-            else if ((ms.fastp >> sq) & 1) w = fast_pawn_targets(ms, sq, g.white);
-            else w = scr.get(ordinal(g.own, sq));
-        }
-        o[sq] = w;
-    }
+__device__ void write_mask(const Pos& s, const Gen& g, const MoveSet& ms, const S& scr, u64* __restrict__ o,
+                           size_t n) {
     u64 c = 0;
     if (g.castles & 1) c |= g.white ? (1ull << 1) : (1ull << 3);  // QS: 4097 / 4099
     if (g.castles & 2) c |= g.white ? (1ull << 0) : (1ull << 2);  // KS: 4096 / 4098
-    o[64] = c;
+#pragma unroll 8
+    for (int sq = 0; sq < 64; sq++) o[sq * n] = 0;
+    o[64 * n] = c;
+    u64 pcs = g.own;
+    for (int j = 0; pcs; j++) {
+        int sq = ctz(pcs);
+        pcs &= pcs - 1;
+        u64 w = ms.big ? legal_targets(s, g, sq, type_at(s, sq))
+                       : (((ms.fastp >> sq) & 1) ? fast_pawn_targets(ms, sq, g.white) : scr.get(j));
+        if (w) o[sq * n] = w;
+    }
 }
 
 // spread the 8 bits of b over the 8 bytes of a word (bit j -> byte j, value 0/1): byte j
@@ -1283,7 +1288,7 @@ __global__ void __launch_bounds__(BLOCK) k_env_step_api(EnvDev e, const uint16_t
     dn[i] = (uint8_t)o.done;
     rs[i] = (uint8_t)o.reason;
     if (cnt) cnt[i] = ms.total;
-    if (mask) write_mask(s, g, ms, scr, mask + 65 * (size_t)i);
+    if (mask) write_mask(s, g, ms, scr, mask + i, (size_t)e.n);
     if (obs) write_obs(s, obs + 64 * (size_t)i);
     if (pick_out) {
         uint16_t p = pick(s, g, ms, scr, e.seed, i, pc.draw);

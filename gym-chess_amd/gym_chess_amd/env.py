@@ -279,7 +279,7 @@ class BatchedChessEnv:
 
 class DeviceIO:
     """Device buffers of one env's step_device outputs: reward i32, done u8, reason u8 and
-    optionally mask u64[N][65], obs i8[N][64], count i32, pick u16 (the random policy's next
+    optionally mask u64[65][N] (word-major), obs i8[N][64], count i32, pick u16 (the random policy's next
     action, which step_device uses as the actions when given none).  fetch() copies them to
     host arrays; upload_actions() fills the pick buffer from the host."""
 
@@ -311,12 +311,14 @@ class DeviceIO:
         _lib.check(self.env._L.gc_env_copy(self.env._h, self.ptr["pick"], _lib.ptr(a), ctypes.c_uint64(a.nbytes), 1))
 
     def fetch(self, *keys):
+        """host copies; the mask comes back as [N][65] (the device buffer is word-major [65][N])"""
         out = {}
         for k in keys or self.ptr:
             dt, sh = self._SPEC[k]
-            a = np.zeros((self.env.num_boards,) + sh, dtype=dt)
+            shape = (65, self.env.num_boards) if k == "mask" else (self.env.num_boards,) + sh
+            a = np.zeros(shape, dtype=dt)
             _lib.check(self.env._L.gc_env_copy(self.env._h, _lib.ptr(a), self.ptr[k], ctypes.c_uint64(a.nbytes), 2))
-            out[k] = a
+            out[k] = np.ascontiguousarray(a.T) if k == "mask" else a
         return out
 
     def close(self):

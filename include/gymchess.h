@@ -105,7 +105,10 @@ int gc_env_step(gc_env* e, const uint16_t* actions, int32_t* reward, uint8_t* do
 /* step(action) with DEVICE buffers, for a policy that lives on the GPU (chess_v2.py:219-294
  * + the rebuilt possible_actions, 333-335): d_actions[n] in (validated like 240-242); out
  * d_reward[n], d_done[n], d_reason[n] (as gc_env_step), and optionally (NULL = skip)
- * d_mask[n][65] (legal-action mask of the new position, gc_env_legal_mask's layout),
+ * d_mask[65][n] (legal-action mask of the new position, WORD-MAJOR: word f of board i at
+ * d_mask[f * n + i] = targets of from-square f, word 64 bit c = action 4096 + c -- each of
+ * the kernel's mask stores then writes 512 contiguous bytes; gc_env_legal_mask's host layout
+ * is the transpose),
  * d_obs[n][64] (int8 board, the observation of 153-158), d_count[n] (legal actions),
  * d_pick[n] (the random policy's pick over the new list; also the env's next policy
  * action).  flags bit 0: auto-reset finished boards (the mask / obs / pick then describe
