@@ -17,7 +17,7 @@ import os
 def per_dispatch(path, kernel):
     d = collections.defaultdict(dict)
     for r in csv.DictReader(open(path)):
-        if r["Kernel_Name"].startswith(kernel):
+        if kernel in r["Kernel_Name"]:
             d[int(r["Dispatch_Id"])][r["Counter_Name"]] = float(r["Counter_Value"])
     return [d[k] for k in sorted(d)]
 
@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--last", type=int, default=20)
     ap.add_argument("--boards", type=int, default=65536)
     ap.add_argument("--alg-bytes-per-board", type=int, default=282)
+    ap.add_argument("--dispatches-per-ply", type=int, default=1,
+                    help="dispatches of the kernel per ply (bench.py's board-range streams, GC_STREAMS)")
     ap.add_argument("--perft", action="store_true",
                     help="perft leaf kernel (k_perft2_perm) passes pmc_perft_{fetch,write,mix} -> pmc_perft.json")
     a = ap.parse_args()
@@ -38,13 +40,15 @@ def main():
     mean = lambda rows, k: sum(r[k] for r in rows) / len(rows)  # noqa: E731
     f = per_dispatch(os.path.join(a.src, "pmc_fetch/run_counter_collection.csv"), a.kernel)[-a.last:]
     w = per_dispatch(os.path.join(a.src, "pmc_write/run_counter_collection.csv"), a.kernel)[-a.last:]
-    fetch = mean(f, "FETCH_SIZE") * 1024 * 2
-    write = mean(w, "WRITE_SIZE") * 1024
-    out = {"kernel": a.kernel, "launches_averaged": len(f), "boards": a.boards,
-           "fetch_bytes_corrected": fetch, "fetch_size_kib_raw": mean(f, "FETCH_SIZE"), "write_bytes": write,
+    k = a.dispatches_per_ply
+    fetch = mean(f, "FETCH_SIZE") * 1024 * 2 * k
+    write = mean(w, "WRITE_SIZE") * 1024 * k
+    out = {"kernel": a.kernel, "launches_averaged": len(f), "boards": a.boards, "dispatches_per_ply": k,
+           "fetch_bytes_corrected": fetch, "fetch_size_kib_raw": mean(f, "FETCH_SIZE") * k, "write_bytes": write,
            "bytes_per_launch": fetch + write, "bytes_per_board": (fetch + write) / a.boards,
            "alg_bytes_per_launch": a.alg_bytes_per_board * a.boards,
-           "note": "FETCH_SIZE x2 (gfx950 correction for wide streaming reads; 8-B/lane loads uncalibrated)"}
+           "note": "per ply (all boards; the sum of its dispatches); FETCH_SIZE x2 (gfx950 correction for wide "
+                   "streaming reads; 8-B/lane loads uncalibrated)"}
     vp = os.path.join(a.src, "pmc_valu/run_counter_collection.csv")
     if os.path.exists(vp):
         v = per_dispatch(vp, a.kernel)[-a.last:]
@@ -70,8 +74,7 @@ def main():
         out["settle_plies"] = bl["config"].get("settle_plies")
     out["profile"] = os.path.basename(a.dst.rstrip("/"))
     os.makedirs(a.dst, exist_ok=True)
-    for p in (os.path.join(a.dst, "pmc_traffic.json"), os.path.join(os.path.dirname(a.dst.rstrip("/")),
-                                                                       "pmc_traffic_latest.json")):
+    for p in (os.path.join(a.dst, "pmc_traffic.json"),):
         json.dump(out, open(p, "w"), indent=1)
     print(json.dumps(out, indent=1))
 
@@ -110,8 +113,7 @@ def perft_summary(a):
            "profile": os.path.basename(a.dst.rstrip("/"))}
     out["hbm_bytes_per_subtree"] = out["hbm_bytes_total"] / max(out["subtrees_total"], 1)
     os.makedirs(a.dst, exist_ok=True)
-    for p in (os.path.join(a.dst, "pmc_perft.json"), os.path.join(os.path.dirname(a.dst.rstrip("/")),
-                                                                   "pmc_perft_latest.json")):
+    for p in (os.path.join(a.dst, "pmc_perft.json"),):
         json.dump(out, open(p, "w"), indent=1)
     print(json.dumps(out, indent=1))
 
