@@ -19,6 +19,7 @@
 #include <atomic>
 #include <mutex>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #ifdef GC_STAMPS
@@ -392,6 +393,7 @@ struct EnvDev {
         int white;
         int usable;  // 0: the start position needs the per-square fallback (> 16 pieces)
         int table;   // reset_acts holds all `total` actions
+        int open_safe;  // no opening move leaves both kings in check (paired BLACK-agent kernel)
     } ic;
     int hbits;        // log2 window-table entries per board (DevHist::nb)
     __device__ DevHist hist(int i, u32 g) const { return DevHist{htab, hgen, g, i, hbits}; }
@@ -471,7 +473,21 @@ __global__ void __launch_bounds__(BLOCK) k_init_cache(EnvDev e, EnvDev::InitCach
     c.white = g.white;
     c.usable = !ms.big;
     c.table = c.usable && ms.total > 0 && ms.total <= RESET_ACTS_MAX;
-    for (int k = 0; c.table && k < ms.total; k++) acts[k] = (uint16_t)select_action(c.pos, g, ms, scr, k);
+    c.open_safe = 1;
+    for (int k = 0; c.table && k < ms.total; k++) {
+        const int a = select_action(c.pos, g, ms, scr, k);
+        acts[k] = (uint16_t)a;
+        // env_ply's both-checked end (lib.rs:1442-1446) after this opening: the one-wave
+        // kernels handle it (env_open_vs), the paired one does not
+        Pos ns = c.pos;
+        ns.meta = (ns.meta & ~(u32)M_RIGHTS) | eff_rights(c.pos);
+        int mr;
+        bool irrev;
+        apply_legal(ns, c.white != 0, a, &mr, &irrev);
+        Gen g2;
+        gen_init(ns, g2);
+        if (g2.in_check && mover_checked(c.pos, ns, c.white != 0, a)) c.open_safe = 0;
+    }
     *out = c;
 }
 
@@ -671,36 +687,49 @@ struct PairCtx {
     u32 rtotal;
 };
 
-// One ply of the paired driver for board i (lane l of this role's wave).  In/out: the state
-// s, the action a (picked for s by the previous ply or by the reset), the draw counter d
-// (W0), the window h (W1; its table write is left deferred in h), the step counter nst.
-// Returns the ply's env.step() outputs; on return both waves hold the same s, and with
-// SHARE_ACT the same next action a (W0 picks it; it crosses to W1 through LDS).
+// One half-ply of the paired driver for board i (lane l of this role's wave): the move `a`
+// of the side to move in s (applied when mv) and everything env_ply (gc_env.h) derives from
+// it -- the post-move board, the next side's generation (count planes of both waves merged,
+// W0's parked targets in LDS), check flags, the 3-fold commit of the pre-move board (W1; its
+// table write left deferred in h).  Phases 0-2 and the exchange that opens phase 3:
+// w1_issue() runs on W1 in phase 0 behind the probe, w1_late() on W1 at the end of phase 2.
+// With ACT_LDS, W1 reads the action from act_lds[l] after phase 0 (W0 picked it: the
+// opponent's reply).
 // FIDE = rules "fide" (gc_fide.h): fapply, the enemy map without the own king, en passant,
 // FIDE castling (from W0, which alone holds the in-check flag), no king captures; a legal
 // move never leaves the mover in check, so there is no mover-check and no both-checked end.
-template <bool SHARE_ACT, bool FIDE = false>
-__device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, int role, int l, int i,
-                                            bool live, const Pos& rp, Pos& s, int& a, u32& d, DevHist& h,
-                                            u32& nst) {
+struct PairHalf {
+    Pos ns;         // the post-move board (check flags / window length / done not yet set)
+    Gen g;          // the next side's generation (W0 complete; W1: in_check, check mask, pins)
+    MoveSet ms;     // merged count planes and total (castles included)
+    int mr;         // capture reward of the move
+    bool irrev;     // irreversible move (3-fold window reset)
+    bool my_chk;    // the mover is in check after its move (lib.rs:1386-1393)
+    bool opp_chk;   // the side now to move is in check
+    bool both;      // both checked (lib.rs:1442-1446): the move is void
+    int c;          // 3-fold count of the pre-move board (0: window full)
+    u32 hl;         // window length after the commit
+    u64 ep_from;    // FIDE: own pawns with a legal en-passant capture
+    int ep;
+};
+struct PairNoop {
+    __device__ void operator()() const {}
+};
+
+template <bool FIDE, bool ACT_LDS, class W1Issue, class W1Late>
+__device__ __forceinline__ void pair_half(PairLds& L, int role, int l, bool mv, const Pos& s, int a,
+                                          const u32* act_lds, DevHist& h, PairHalf& H, W1Issue&& w1_issue,
+                                          W1Late&& w1_late) {
     PairScratch scr{&L.slots[0][l]};
-    const bool none = a == A_NONE;                           // empty list: driver reset
-    const bool done0 = (s.meta & M_DONE) != 0;               // chess_v2.py:245-251
-    const bool cap = mc_of(s.meta) > MOVES_MAX;              // 252-258
-    const bool mv = live && !none && !done0 && !cap;         // env_ply runs
     const bool white = (s.meta & M_WHITE) != 0;
     int mr = 0;
     bool irrev = false;
     Pos ns;
     RepProbe pr;
     bool my_chk = false;
-    u32 x0 = 0;
-    uint16_t ra = (uint16_t)A_NONE;
 
     // ---- phase 0: W0 applies the action (once per board, not once per wave); W1 issues the
-    // window probe of the pre-move board (Q8), draws the next Philox word and, for a board
-    // that resets this ply, reads its pick from the start position's table (lands long
-    // before phase 3)
+    // window probe of the pre-move board (Q8) and the caller's independent work
     if (role == 0) {
         ns = s;
         if constexpr (FIDE) {
@@ -716,15 +745,13 @@ __device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, int ro
         L.irrev[l] = irrev ? 1u : 0u;
     } else {
         if (mv) rep_prefetch(h, s, pr);
-        x0 = philox_x0(C.seed, (u32)i, d);  // the next draw (independent of the position)
-        if (C.rtable) ra = C.racts[scale_rank(x0, C.rtotal)];
-        L.x0[l] = x0;
+        w1_issue();
     }
     pair_barrier();
 
     // ---- phase 1: W0 pins / checkers and the enemy's diagonal slider attacks; W1 the enemy's
     // leaper and orthogonal slider attacks and the mover's own check flag (FIDE: en passant)
-    Gen g;
+    Gen& g = H.g;
     u64 ep_from = 0;
     int ep = -1;
     u64 enemy_diag = 0;
@@ -750,6 +777,7 @@ __device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, int ro
             }
         }
     } else {
+        if constexpr (ACT_LDS) a = (int)act_lds[l];
         ns.k = L.ns[0][l]; ns.q = L.ns[1][l]; ns.r = L.ns[2][l]; ns.b = L.ns[3][l];
         ns.n = L.ns[4][l]; ns.p = L.ns[5][l]; ns.w = L.ns[6][l];
         ns.meta = L.nmeta[l];
@@ -821,7 +849,7 @@ __device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, int ro
     const bool opp_chk = g.in_check;
     const bool both = !FIDE && opp_chk && my_chk;             // lib.rs:1442-1446
     const bool gen = mv && !both;
-    MoveSet ms;
+    MoveSet& ms = H.ms;
     moveset_clear(ms);
     ms.big = popc(g.own) > SCRATCH_SLOTS;
     int part = 0;
@@ -850,7 +878,7 @@ __device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, int ro
             c = rep_commit(h, s, pr, hl, irrev);  // table write deferred to h.commit()
         }
         L.rep[l] = (u32)c | (hl << 8);
-        L.ra[l] = ra;  // landed by now (issued in phase 0)
+        w1_late();
     }
 #pragma unroll
     for (int b = 0; b < 5; b++) L.planes[role][b][l] = ms.cnt[b];
@@ -859,7 +887,7 @@ __device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, int ro
     pair_barrier();
     GC_STAMP(5);
 
-    // ---- phase 3: outcome (both waves), then the pick (W0)
+    // ---- phase 3 opens: both waves merge the count planes, W0 takes the 3-fold verdict
 #pragma unroll
     for (int b = 0; b < 5; b++) ms.cnt[b] |= L.planes[role ^ 1][b][l];
     ms.total = part + (int)L.part[role ^ 1][l];  // W0's part holds the castles
@@ -867,9 +895,64 @@ __device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, int ro
         u32 rpk = L.rep[l];
         c = (int)(rpk & 0xFFu);
         hl = rpk >> 8;
+    }
+    H.ns = ns;
+    H.mr = mr;
+    H.irrev = irrev;
+    H.my_chk = my_chk;
+    H.opp_chk = opp_chk;
+    H.both = both;
+    H.c = c;
+    H.hl = hl;
+    H.ep_from = ep_from;
+    H.ep = ep;
+}
+
+// env_ply's epilogue (gc_env.h): the post-move board with the check flags of both sides, the
+// window length and M_DONE when the pre-move board reached 3 occurrences or the window is full
+__device__ __forceinline__ Pos pair_settle(const PairHalf& H, bool white) {
+    u32 chk = white ? ((H.my_chk ? M_WCHK : 0u) | (H.opp_chk ? M_BCHK : 0u))
+                    : ((H.opp_chk ? M_WCHK : 0u) | (H.my_chk ? M_BCHK : 0u));
+    Pos ns = H.ns;
+    ns.meta = with_hl((ns.meta & ~(u32)(M_WCHK | M_BCHK | M_DONE)) | chk | ((H.c >= 3 || H.c == 0) ? M_DONE : 0u), H.hl);
+    return ns;
+}
+
+// One ply of the paired driver (opponent "none").  In/out: the state s, the action a (picked
+// for s by the previous ply or by the reset), the draw counter d (W0), the window h (W1; its
+// table write is left deferred in h), the step counter nst.  Returns the ply's env.step()
+// outputs; on return both waves hold the same s, and with SHARE_ACT the same next action a
+// (W0 picks it; it crosses to W1 through LDS).
+template <bool SHARE_ACT, bool FIDE = false>
+__device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, int role, int l, int i,
+                                            bool live, const Pos& rp, Pos& s, int& a, u32& d, DevHist& h,
+                                            u32& nst) {
+    PairScratch scr{&L.slots[0][l]};
+    const bool none = a == A_NONE;                           // empty list: driver reset
+    const bool done0 = (s.meta & M_DONE) != 0;               // chess_v2.py:245-251
+    const bool cap = mc_of(s.meta) > MOVES_MAX;              // 252-258
+    const bool mv = live && !none && !done0 && !cap;         // env_ply runs
+    const bool white = (s.meta & M_WHITE) != 0;
+    u32 x0 = 0;
+    uint16_t ra = (uint16_t)A_NONE;
+    PairHalf H;
+    // W1, phase 0: the Philox word of the next draw and, for a board that resets this ply,
+    // its pick from the start position's table (a serial multiply chain and a load, hidden
+    // behind W0's move; the table read lands long before phase 3)
+    pair_half<FIDE, false>(
+        L, role, l, mv, s, a, nullptr, h, H,
+        [&] {
+            x0 = philox_x0(C.seed, (u32)i, d);  // the next draw (independent of the position)
+            if (C.rtable) ra = C.racts[scale_rank(x0, C.rtotal)];
+            L.x0[l] = x0;
+        },
+        [&] { L.ra[l] = ra; });
+    if (role == 0) {
         x0 = L.x0[l];
         ra = (uint16_t)L.ra[l];
     }
+    Gen& g = H.g;
+    MoveSet& ms = H.ms;
     StepOut o = {0, 0, R_NONE, 0};
     bool have = false;
     if (none) {
@@ -878,18 +961,14 @@ __device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, int ro
         nst += 1;
         if (done0) { o.done = 1; o.reason = R_DONE_ALREADY; }
         else if (cap) { o.done = 1; o.reason = R_MOVE_CAP; }
-        else if (both) { o.done = 1; o.reason = R_BOTH_CHECKED; }
+        else if (H.both) { o.done = 1; o.reason = R_BOTH_CHECKED; }
         else {
-            u32 chk = white ? ((my_chk ? M_WCHK : 0u) | (opp_chk ? M_BCHK : 0u))
-                            : ((opp_chk ? M_WCHK : 0u) | (my_chk ? M_BCHK : 0u));
-            bool rep = c >= 3;  // chess_v2.py:404-407
-            ns.meta = with_hl((ns.meta & ~(u32)(M_WCHK | M_BCHK | M_DONE)) | chk | ((rep || c == 0) ? M_DONE : 0u), hl);
-            s = ns;
-            o.reward = -10 + mr;
+            s = pair_settle(H, white);
+            o.reward = -10 + H.mr;
             o.moved = 1;
-            if (rep) { o.done = 1; o.reason = R_REPETITION; }
-            if (c == 0) { o.done = 1; o.reason = R_WINDOW_FULL; }
-            if (ms.total == 0 && opp_chk) {  // 270-272
+            if (H.c >= 3) { o.done = 1; o.reason = R_REPETITION; }  // chess_v2.py:404-407
+            if (H.c == 0) { o.done = 1; o.reason = R_WINDOW_FULL; }
+            if (ms.total == 0 && H.opp_chk) {  // 270-272
                 s.meta |= M_DONE;
                 o.done = 1;
                 o.reward += 100;
@@ -936,7 +1015,7 @@ __device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, int ro
                 }
             } else if constexpr (FIDE) {
                 if (ms.big) {
-                    f = gcf::FGen{g, ep_from, ep};
+                    f = gcf::FGen{g, H.ep_from, H.ep};
                     walk = true;
                 }
             }
@@ -954,6 +1033,177 @@ __device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, int ro
         }
     }
     if (SHARE_ACT) {  // the next action and draw counter to W1; LDS free for the next ply
+        pair_barrier();
+        if (role) {
+            a = (int)L.act[l];
+            d = L.draw[l];
+        }
+    }
+    return o;
+}
+
+// ----------------------------------------------------------------------------- paired step, opponent "random"
+// One step() with the random opponent (chess_v2.py:219-294 with opponent_policy set; gc_env.h
+// env_step_vs / env_open_vs; the one-wave k_env_step<true, true>) on the paired driver: the
+// agent's half-ply, the opponent's reply, and -- for a BLACK agent whose env resets -- the
+// opponent's opening, each one pair_half.  The draws of one step come from the same Philox
+// stream in the same order as the one-wave kernel: reply (d), [opening], the agent's next
+// pick; W1 computes the words of d, d+1 (, d+2) and the start-position-table picks of d and
+// d+1 in phase 0 of the agent's half-ply, before it knows which it needs.
+// Used when the start position has a pick table and (BLACK) no opening of it can leave
+// both kings in check (InitCache::open_safe); otherwise the one-wave kernel runs.
+struct PairLdsVs : PairLds {
+    u32 x1[PAIR_BOARDS];  // W1 -> W0: the Philox words of draws d+1, d+2
+    u32 x2[PAIR_BOARDS];
+    u32 oa[PAIR_BOARDS];  // W0 -> W1: the opponent's reply (read in its phase 1)
+    u32 vote[2];          // per wave: some board of it resets (BLACK: the opening half-ply runs)
+};
+
+template <bool BLACK, bool SHARE_ACT>
+__device__ __forceinline__ StepOut pair_step_vs(PairLdsVs* Ls, PairLdsVs& L, const PairCtx& C, int role, int l,
+                                                int i, bool live, const Pos& rp, Pos& s, int& a, u32& d, DevHist& h,
+                                                u32& nst) {
+    PairScratch scr{&L.slots[0][l]};
+    const bool none = a == A_NONE;                           // empty list: driver reset
+    const bool done0 = (s.meta & M_DONE) != 0;               // chess_v2.py:245-251
+    const bool cap = mc_of(s.meta) > MOVES_MAX;              // 252-258
+    const bool mv = live && !none && !done0 && !cap;         // the agent's ply runs
+    const bool white = (s.meta & M_WHITE) != 0;              // the agent's colour
+    u32 x0 = 0, x1 = 0, x2 = 0, ra = 0;
+    PairHalf H;
+    // ---- the agent's half-ply
+    pair_half<false, false>(
+        L, role, l, mv, s, a, nullptr, h, H,
+        [&] {
+            x0 = philox_x0(C.seed, (u32)i, d);
+            x1 = philox_x0(C.seed, (u32)i, d + 1);
+            if (BLACK) x2 = philox_x0(C.seed, (u32)i, d + 2);
+            ra = (u32)C.racts[scale_rank(x0, C.rtotal)] | ((u32)C.racts[scale_rank(x1, C.rtotal)] << 16);
+            L.x0[l] = x0;
+            L.x1[l] = x1;
+            if (BLACK) L.x2[l] = x2;
+        },
+        [&] { L.ra[l] = ra; });
+    if (role == 0) {
+        x0 = L.x0[l];
+        x1 = L.x1[l];
+        if (BLACK) x2 = L.x2[l];
+    }
+    ra = L.ra[l];  // W1 wrote it before the barrier that closed phase 2
+    StepOut o = {0, 0, R_NONE, 0};
+    bool cont = false;  // the opponent replies
+    if (none) {
+        o.reason = R_NO_MOVES;
+    } else {
+        nst += 1;
+        if (done0) { o.done = 1; o.reason = R_DONE_ALREADY; }
+        else if (cap) { o.done = 1; o.reason = R_MOVE_CAP; }
+        else if (H.both) { o.done = 1; o.reason = R_BOTH_CHECKED; }
+        else {
+            s = pair_settle(H, white);
+            o.reward = -10 + H.mr;
+            o.moved = 1;
+            if (H.c >= 3) { o.done = 1; o.reason = R_REPETITION; }
+            if (H.c == 0) { o.done = 1; o.reason = R_WINDOW_FULL; }
+            if (H.ms.total == 0 && H.opp_chk) {  // 270-272
+                s.meta |= M_DONE;
+                o.done = 1;
+                o.reward += 100;
+                o.reason = R_MATE;
+            }
+            if (!o.done && H.ms.total == 0) {  // 120-122: the opponent "resigns"
+                s.meta |= M_DONE;
+                o.done = 1;
+                o.reason = R_OPP_NO_MOVE;
+            }
+            cont = !o.done;
+        }
+    }
+    int nd = cont ? 1 : 0;  // draws taken so far this step
+    // ---- the opponent's reply: W0 picks it from the agent ply's generation (draw d)
+    int oa = A_NONE;  // W1 reads W0's pick in the reply's phase 1
+    if (role == 0) {
+        if (cont) oa = select_action(s, H.g, H.ms, scr, (int)scale_rank(x0, (u32)H.ms.total));
+        L.oa[l] = (u32)oa;
+    } else if (live) {
+        h.commit();  // the agent ply's window write lands before the reply probes the table
+    }
+    const Pos s1 = s;
+    pair_half<false, true>(L, role, l, cont, s1, oa, L.oa, h, H, PairNoop{}, PairNoop{});
+    if (cont) {
+        if (H.both) {
+            o.reason = R_BOTH_CHECKED;
+            o.done = 1;
+        } else {
+            s = pair_settle(H, !white);
+            o.reward -= H.mr;  // 283
+            if (H.c >= 3) { o.done = 1; o.reason = R_REPETITION; }
+            if (H.c == 0) { o.done = 1; o.reason = R_WINDOW_FULL; }
+            if (H.ms.total == 0 && H.opp_chk) {  // 285-288
+                s.meta |= M_DONE;
+                o.done = 1;
+                o.reward -= 100;
+                o.reason = R_MATED;
+            }
+            if (s.meta & M_WHITE) s.meta += (1u << M_MC_SHIFT);  // 291-292
+        }
+    }
+    const bool have = o.moved && !o.done;
+    if (!have) {  // reset (chess_v2.py:183-206), also the no-move driver reset
+        s = rp;
+        h.bump_gen();
+    }
+    // ---- the agent's next action (W0): from the reply's generation, or the start position's table
+    uint16_t act = (uint16_t)A_NONE;
+    int tot = 0;
+    if (role == 0) {
+        if (have) {
+            tot = H.ms.total;
+            if (tot > 0) act = (uint16_t)select_action(s, H.g, H.ms, scr, (int)scale_rank(x1, (u32)tot));
+        } else if (!BLACK) {
+            tot = (int)C.rtotal;
+            act = (uint16_t)(nd ? ra >> 16 : ra & 0xFFFFu);
+        }
+    }
+    if constexpr (BLACK) {
+        // ---- the opponent's opening after a reset (env_open_vs), when some board of the
+        // workgroup needs it: its pick from the table (draw d + nd), one half-ply, its 3-fold
+        // verdict discarded, move_count 1; then the agent's pick from its generation
+        const bool open = live && !have;
+        const unsigned long long vote = __ballot(open);
+        if (l == 0) L.vote[role] = vote != 0 ? 1u : 0u;
+        if (role) {
+            if (live) h.commit();
+        }
+        pair_barrier();
+        bool any = false;
+#pragma unroll
+        for (int q = 0; q < PAIRS_WG; q++) any = any || Ls[q].vote[0] != 0 || Ls[q].vote[1] != 0;
+        if (any) {
+            const int oa = (int)(nd ? ra >> 16 : ra & 0xFFFFu);
+            const Pos s0 = s;
+            pair_half<false, false>(L, role, l, open, s0, oa, nullptr, h, H, PairNoop{}, PairNoop{});
+            if (open) {
+                s = pair_settle(H, true);
+                s.meta = (s.meta & ~(u32)M_DONE) + (1u << M_MC_SHIFT);
+                nd += 1;
+                if (role == 0) {
+                    tot = H.ms.total;
+                    act = (uint16_t)A_NONE;
+                    if (tot > 0) act = (uint16_t)select_action(s, H.g, H.ms, scr, (int)scale_rank(nd == 1 ? x1 : x2, (u32)tot));
+                }
+            }
+        }
+    }
+    if (role == 0) {
+        a = act;
+        d += (u32)nd + (tot > 0 ? 1u : 0u);
+        if (SHARE_ACT) {
+            L.act[l] = act;
+            L.draw[l] = d;
+        }
+    }
+    if (SHARE_ACT) {  // the next action and draw counter to W1; LDS free for the next step
         pair_barrier();
         if (role) {
             a = (int)L.act[l];
@@ -1007,9 +1257,10 @@ __device__ __forceinline__ PairIO store_io(uint8_t* slab, int nn) {
 // scarce it sank it next to a spill that forced the wait in phase 1.  The reset position and
 // move set come from a device-memory copy (icd) instead.
 #define PAIR_PROLOGUE                                                                                       \
-    __shared__ PairLds Ls[PAIRS_WG];                                                                        \
+    using LdsT = typename std::conditional<OPP != 0, PairLdsVs, PairLds>::type;                             \
+    __shared__ LdsT Ls[PAIRS_WG];                                                                           \
     const int pw = PAIRS_WG > 1 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 7)) : 0;              \
-    PairLds& L = Ls[pw];                                                                                    \
+    LdsT& L = Ls[pw];                                                                                       \
     const int role = __builtin_amdgcn_readfirstlane((int)((threadIdx.x >> 6) & 1)); /* wave-uniform */     \
     const int l = threadIdx.x & (PAIR_BOARDS - 1);                                                          \
     const int blk = blockIdx.x * PAIRS_WG + pw + blk0; /* board block (a launch may cover a sub-range) */   \
@@ -1030,15 +1281,24 @@ __device__ __forceinline__ PairIO store_io(uint8_t* slab, int nn) {
     pin(s); pin(ua); pin(g0); pin(nst); pin(d);                                                             \
     GC_STAMP(1);                                                                                            \
     int a = (int)ua;                                                                                        \
-    DevHist h = DevHist{htab, in_io.hgen, g0, ii};
+    DevHist h = DevHist{htab, in_io.hgen, g0, ii, OPP == 2 ? HTAB_BITS_UNCAPPED : HTAB_BITS};
 
-template <bool FIDE>
+// One step of the paired driver: opponent "none" (OPP 0: pair_ply) or the random opponent
+// with a WHITE (1) or BLACK (2) agent (pair_step_vs).
+template <int OPP, bool SHARE_ACT, bool FIDE, class LdsT>
+__device__ __forceinline__ StepOut pair_step(LdsT* Ls, LdsT& L, const PairCtx& C, int role, int l, int i, bool live,
+                                             const Pos& rp, Pos& s, int& a, u32& d, DevHist& h, u32& nst) {
+    if constexpr (OPP == 0) return pair_ply<SHARE_ACT, FIDE>(L, C, role, l, i, live, rp, s, a, d, h, nst);
+    else return pair_step_vs<OPP == 2, SHARE_ACT>(Ls, L, C, role, l, i, live, rp, s, a, d, h, nst);
+}
+
+template <bool FIDE, int OPP = 0>
 __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
     k_env_step2(uint8_t* __restrict__ slab, int nn, int blk0, uint64_t seed, u64* __restrict__ htab,
                 const uint16_t* __restrict__ racts, const EnvDev::InitCache* __restrict__ icd,
                 u32 rinfo /* ic.table << 16 | ic.total */) {
     PAIR_PROLOGUE
-    StepOut o = pair_ply<false, FIDE>(L, C, role, l, i, live, rp, s, a, d, h, nst);
+    StepOut o = pair_step<OPP, false, FIDE>(Ls, L, C, role, l, i, live, rp, s, a, d, h, nst);
     GC_STAMP(6);
     const PairIO io = store_io(slab, nn);
     if (live) {
@@ -1064,7 +1324,7 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
 
 // Fused K-ply random self-play on the paired step: the state stays in registers; the last
 // ply's outputs and per-board stats (as k_env_rollout) are written at the end.
-template <bool FIDE>
+template <bool FIDE, int OPP = 0>
 __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
     k_env_rollout2(uint8_t* __restrict__ slab, int nn, int blk0, uint64_t seed, u64* __restrict__ htab,
                    const uint16_t* __restrict__ racts, const EnvDev::InitCache* __restrict__ icd, u32 rinfo, int plies,
@@ -1075,7 +1335,7 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
     StepOut o = {0, 0, R_NONE, 0};
     for (int p = 0; p < plies; p++) {
         int played = a;
-        o = pair_ply<true, FIDE>(L, C, role, l, i, live, rp, s, a, d, h, nst);
+        o = pair_step<OPP, true, FIDE>(Ls, L, C, role, l, i, live, rp, s, a, d, h, nst);
         if (played == A_NONE) {
             e_nomove++;
         } else {
@@ -1831,18 +2091,30 @@ static ResetInfo reset_info(const gc_env* e) {
                      (ic.table ? 1u << 16 : 0u) | (u32)(ic.total & 0xFFFF)};
 }
 
-// one ply of the paired step kernel over the board blocks [b0, b0 + nb) (64 boards each)
+// The paired kernels serve opponent "none" (both rules) and the random opponent when the
+// start position's picks come from its table and, for a BLACK agent, no opening can end in
+// both kings checked (pair_step_vs); otherwise the one-wave kernels run.
+static bool pair_ok(const gc_env* e) {
+    if (!e->d.opp) return true;
+    const EnvDev::InitCache& ic = e->d.ic;
+    return ic.usable && ic.table && (!e->d.agent_black || ic.open_safe);
+}
+static int pair_opp(const gc_env* e) { return e->d.opp ? (e->d.agent_black ? 2 : 1) : 0; }
+
+// one ply (opponent: one two-ply step) of the paired step kernel over the board blocks
+// [b0, b0 + nb) (64 boards each)
 static void launch_step2(gc_env* e, hipStream_t st, int b0 = 0, int nb = -1) {
     const EnvDev& d = e->d;
     const ResetInfo r = reset_info(e);
     const int per_wg = PAIR_BOARDS * PAIRS_WG;
     if (nb < 0) nb = (e->n + PAIR_BOARDS - 1) / PAIR_BOARDS;
-    if (e->rules)
-        k_env_step2<true><<<(nb + PAIRS_WG - 1) / PAIRS_WG, 2 * per_wg, 0, st>>>(e->slab, d.n, b0, d.seed, d.htab,
-                                                                               r.racts, r.icd, r.rinfo);
-    else
-        k_env_step2<false><<<(nb + PAIRS_WG - 1) / PAIRS_WG, 2 * per_wg, 0, st>>>(e->slab, d.n, b0, d.seed, d.htab,
-                                                                                r.racts, r.icd, r.rinfo);
+    const dim3 grid((nb + PAIRS_WG - 1) / PAIRS_WG), block(2 * per_wg);
+    switch (e->rules ? 3 : pair_opp(e)) {
+        case 3: k_env_step2<true><<<grid, block, 0, st>>>(e->slab, d.n, b0, d.seed, d.htab, r.racts, r.icd, r.rinfo); break;
+        case 0: k_env_step2<false><<<grid, block, 0, st>>>(e->slab, d.n, b0, d.seed, d.htab, r.racts, r.icd, r.rinfo); break;
+        case 1: k_env_step2<false, 1><<<grid, block, 0, st>>>(e->slab, d.n, b0, d.seed, d.htab, r.racts, r.icd, r.rinfo); break;
+        default: k_env_step2<false, 2><<<grid, block, 0, st>>>(e->slab, d.n, b0, d.seed, d.htab, r.racts, r.icd, r.rinfo); break;
+    }
 }
 
 extern "C" int gc_env_create(int device, int n_boards, uint64_t seed, const int8_t* initial_board, gc_env** out) {
@@ -2116,7 +2388,7 @@ extern "C" int gc_env_step_random(gc_env* e, int n_plies) {
     HIPCHK(hipSetDevice(e->device));
     static const bool one_wave = getenv("GC_STEP1") != nullptr;  // A/B switch to k_env_step<true, false>
     static const int graph_chunk = getenv("GC_GRAPH") ? atoi(getenv("GC_GRAPH")) : 0;
-    const bool pair = !e->d.opp && !one_wave;  // reference or FIDE rules, opponent "none": the paired kernel
+    const bool pair = pair_ok(e) && !one_wave;  // the paired kernel (pair_ok: all but rare opponent setups)
     int p = 0;
     if (pair && graph_chunk > 0) {
         if (!e->graph_exec || e->graph_chunk != graph_chunk) {  // captured once per env
@@ -2164,6 +2436,12 @@ extern "C" int gc_env_set_streams(gc_env* e, int k) {
     return 0;
 }
 
+extern "C" int gc_env_paired(gc_env* e) {
+    if (!e) return fail("null env");
+    static const bool one_wave = getenv("GC_STEP1") != nullptr;
+    return pair_ok(e) && !one_wave ? 1 : 0;
+}
+
 extern "C" int gc_env_select_random(gc_env* e) {
     if (!e) return fail("null env");
     HIPCHK(hipSetDevice(e->device));
@@ -2188,18 +2466,18 @@ extern "C" int gc_env_rollout(gc_env* e, int n_plies, int16_t* tr_action, int16_
     if (trace && (dalloc(&da, cnt) || dalloc(&dr, cnt) || dalloc(&dd, cnt) || dalloc(&dq, cnt))) return -1;
     HIPCHK(hipMemsetAsync(e->stats, 0, (size_t)64 * e->n, e->stream));
     static const bool one_wave = getenv("GC_STEP1") != nullptr;
-    if (e->d.opp) {
-        k_env_rollout<true><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d, n_plies, da, dr, dd, dq, e->stats);
-    } else if (!trace && (!one_wave || e->rules)) {  // the paired kernel (per-ply traces: the one-wave kernel)
+    if (!trace && pair_ok(e) && (!one_wave || e->rules)) {  // the paired kernel (per-ply traces: the one-wave kernel)
         const EnvDev& d = e->d;
         const ResetInfo r = reset_info(e);
         const int grid = (e->n + PAIR_BOARDS * PAIRS_WG - 1) / (PAIR_BOARDS * PAIRS_WG), bs = 2 * PAIR_BOARDS * PAIRS_WG;
-        if (e->rules)
-            k_env_rollout2<true><<<grid, bs, 0, e->stream>>>(e->slab, d.n, 0, d.seed, d.htab, r.racts, r.icd, r.rinfo,
-                                                             n_plies, e->stats);
-        else
-            k_env_rollout2<false><<<grid, bs, 0, e->stream>>>(e->slab, d.n, 0, d.seed, d.htab, r.racts, r.icd, r.rinfo,
-                                                              n_plies, e->stats);
+        switch (e->rules ? 3 : pair_opp(e)) {
+            case 3: k_env_rollout2<true><<<grid, bs, 0, e->stream>>>(e->slab, d.n, 0, d.seed, d.htab, r.racts, r.icd, r.rinfo, n_plies, e->stats); break;
+            case 0: k_env_rollout2<false><<<grid, bs, 0, e->stream>>>(e->slab, d.n, 0, d.seed, d.htab, r.racts, r.icd, r.rinfo, n_plies, e->stats); break;
+            case 1: k_env_rollout2<false, 1><<<grid, bs, 0, e->stream>>>(e->slab, d.n, 0, d.seed, d.htab, r.racts, r.icd, r.rinfo, n_plies, e->stats); break;
+            default: k_env_rollout2<false, 2><<<grid, bs, 0, e->stream>>>(e->slab, d.n, 0, d.seed, d.htab, r.racts, r.icd, r.rinfo, n_plies, e->stats); break;
+        }
+    } else if (e->d.opp) {
+        k_env_rollout<true><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d, n_plies, da, dr, dd, dq, e->stats);
     } else {
         k_env_rollout<false><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d, n_plies, da, dr, dd, dq, e->stats);
     }

@@ -182,6 +182,13 @@ class BatchedChessEnv:
         """step_random over k board ranges on k device streams (gc_env_set_streams)."""
         _lib.check(self._L.gc_env_set_streams(self._h, int(k)))
 
+    def paired(self):
+        """True when step_random / rollout run the paired two-wave kernels (gc_env_paired)."""
+        r = self._L.gc_env_paired(self._h)
+        if r < 0:
+            _lib.check(r)
+        return bool(r)
+
     def step_random(self, n_plies=1):
         _lib.check(self._L.gc_env_step_random(self._h, int(n_plies)))
 

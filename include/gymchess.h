@@ -131,6 +131,11 @@ int gc_env_step_random(gc_env* e, int n_plies);
  * from GC_STREAMS, else 2): a range's ply p+1 waits only for its own ply p, so the ranges'
  * launches overlap each other's ramp and tail.  Results are independent of k. */
 int gc_env_set_streams(gc_env* e, int k);
+/* 1 when gc_env_step_random / gc_env_rollout (without traces) run the paired two-wave
+ * kernels for this env's rules and opponent mode, 0 when the one-wave kernels run (the
+ * random opponent from a start position without a pick table, or whose opening can leave
+ * both kings checked), -1 on error.  Results are the same either way. */
+int gc_env_paired(gc_env* e);
 /* re-pick policy actions for the current states (after set_states / external steps) */
 int gc_env_select_random(gc_env* e);
 /* Same driver fused into ONE launch of n_plies plies (state kept in registers).  Optional

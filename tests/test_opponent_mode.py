@@ -204,6 +204,48 @@ def test_gpu_opponent_rollouts_vs_oracle(oracle, color):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("color", ["WHITE", "BLACK"])
+@pytest.mark.parametrize("streams,sparse", [(1, False), (2, False), (2, True)])
+def test_gpu_opponent_paired_step_vs_oracle(oracle, color, streams, sparse):
+    """The paired opponent kernels (k_env_step2<false, 1|2>: agent ply, reply, BLACK opening,
+    one pair_half each) ply by ply against the oracle's trace: every step's reward / done /
+    reason and next action, the final boards; then the fused paired rollout's stats.  200
+    boards: the last workgroup is partly dead lanes."""
+    from gym_chess_amd.env import BatchedChessEnv
+
+    n, plies, seed = 200, 500, 0x7A7A
+    init = oracle.DEFAULT_BOARD
+    if sparse:  # 6 pieces: short games, many resets and BLACK openings
+        init = np.zeros(64, dtype=np.int8)
+        init[[60, 56, 51, 4, 12, 7]] = [1, 3, 2, -1, -6, -3]
+    kw = dict(opponent=1, agent_white=color == "WHITE", init=init)
+    refs = [oracle.rollout_trace(seed, i, plies + 1, **kw) for i in range(n)]
+    exp = {k: np.stack([r[k] for r in refs], axis=1) for k in ("action", "reward", "done", "reason")}
+    ib = init if sparse else None
+    env = BatchedChessEnv(n, device=0, seed=seed, initial_board=ib, opponent="random", player_color=color)
+    assert env.paired()
+    env.set_streams(streams)
+    for p in range(plies):
+        assert (env.outputs()["next_action"].astype(np.int64) == (exp["action"][p].astype(np.int64) & 0xFFFF)).all(), p
+        env.step_random(1)
+        out = env.outputs()
+        for k in ("reward", "done", "reason"):
+            assert (out[k].astype(np.int64) == exp[k][p].astype(np.int64)).all(), (p, k)
+    env.close()
+
+    fused = BatchedChessEnv(n, device=0, seed=seed, initial_board=ib, opponent="random", player_color=color)
+    st, _ = fused.rollout(plies)
+    b, m = fused.boards()
+    tot = np.zeros(8, dtype=np.uint64)
+    for i in range(n):
+        ref = oracle.rollout_trace(seed, i, plies, **kw)
+        assert (b[i] == ref["final_board"]).all() and (m[i] == ref["final_meta"]).all(), i
+        tot += ref["stats"]
+    assert (st == tot).all()
+    fused.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("color", ["WHITE", "BLACK"])
 def test_gpu_opponent_external_actions_vs_oracle_env(oracle, color):
     """step(actions) with the opponent replying on the device, against OracleEnv(opponent=1);
     every 7th action is random (mostly invalid: -10, state unchanged)."""

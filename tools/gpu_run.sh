@@ -40,7 +40,7 @@ done
 if [ -n "${PROFILE_TAG:-}" ]; then
   mkdir -p $OUT/summary/$PROFILE_TAG
   [ -f $OUT/prof/run_kernel_stats.csv ] && cp $OUT/prof/run_kernel_stats.csv $OUT/summary/$PROFILE_TAG/kernel_stats.csv
-  [ -d $OUT/pmc_fetch ] && python tools/pmc_summary.py $OUT $OUT/summary/$PROFILE_TAG --kernel "k_env_step2<false>" --dispatches-per-ply ${GC_STREAMS:-2} > /dev/null
+  [ -d $OUT/pmc_fetch ] && python tools/pmc_summary.py $OUT $OUT/summary/$PROFILE_TAG --kernel "k_env_step2<false, 0>" --dispatches-per-ply ${GC_STREAMS:-2} > /dev/null
   [ -d $OUT/pmc_perft_fetch ] && python tools/pmc_summary.py $OUT $OUT/summary/$PROFILE_TAG --perft > /dev/null
   for f in bench pmcf; do [ -f $OUT/$f.log ] && grep '^{' $OUT/$f.log | tail -1 > $OUT/summary/$PROFILE_TAG/$f.json; done
   rm -rf $OUT/prof $OUT/pmc_*
