@@ -812,6 +812,59 @@ GC_HD void gen_moves(const Pos& s, const Gen& g, MoveSet& ms, S& scr) {
     ms.total = total;
 }
 
+// ---- counting only (perft leaves, level expansion) ---------------------------------------
+// gen_moves' total without parking anything, branch-free over the unpinned pieces: sliders
+// of each kind set-wise, one Kogge-Stone fill per direction -- in one direction the rays of
+// two own sliders never overlap (the rear one's ray ends on the front one), so the popcount
+// of the union counts every (slider, target) pair once; knights per jump direction for the
+// same reason (within one jump direction, knight -> target is one-to-one).  Pinned pieces
+// (rare) and the kings one at a time, as gen_moves.  Any number of pieces (no slots).
+template <int SH, bool LEFT>
+GC_HD int ray_count(u64 gen, u64 empty, u64 wrap, u64 tmask) {
+    return popc(ray_fill_att<SH, LEFT>(gen, empty, wrap) & tmask);
+}
+GC_HD int count_moves(const Pos& s, const Gen& g) {
+    const u64 own = g.own, cm = g.checkmask, tm = ~own & cm, empty = ~g.occ, opp = g.opp;
+    const u64 fr = own & ~g.pinned;
+    int total = popc(g.castles);
+    // pawns (lib.rs:935-958; Q1: the double push tests only the destination)
+    const u64 fp = s.p & fr;
+    if (g.white) {
+        total += popc((fp >> 8) & empty & cm) + popc(((fp & ROW6) >> 16) & empty & cm) +
+                 popc(((fp >> 7) & ~FILE_A) & opp & cm) + popc(((fp >> 9) & ~FILE_H) & opp & cm);
+    } else {
+        total += popc((fp << 8) & empty & cm) + popc(((fp & ROW1) << 16) & empty & cm) +
+                 popc(((fp << 9) & ~FILE_A) & opp & cm) + popc(((fp << 7) & ~FILE_H) & opp & cm);
+    }
+    // knights (a pinned knight never has a move on its pin segment)
+    const u64 N = s.n & fr;
+    const u64 l1 = (N >> 1) & ~FILE_H, r1 = (N << 1) & ~FILE_A;
+    const u64 l2 = (N >> 2) & ~(FILE_H | (FILE_H >> 1)), r2 = (N << 2) & ~(FILE_A | (FILE_A << 1));
+    total += popc((l1 << 16) & tm) + popc((r1 << 16) & tm) + popc((l1 >> 16) & tm) + popc((r1 >> 16) & tm) +
+             popc((l2 << 8) & tm) + popc((r2 << 8) & tm) + popc((l2 >> 8) & tm) + popc((r2 >> 8) & tm);
+    // unpinned sliders
+    const u64 RQ = (s.r | s.q) & fr, BQ = (s.b | s.q) & fr;
+    total += ray_count<8, false>(RQ, empty, ~0ull, tm) + ray_count<8, true>(RQ, empty, ~0ull, tm) +
+             ray_count<1, true>(RQ, empty, ~FILE_A, tm) + ray_count<1, false>(RQ, empty, ~FILE_H, tm);
+    total += ray_count<7, false>(BQ, empty, ~FILE_A, tm) + ray_count<9, false>(BQ, empty, ~FILE_H, tm) +
+             ray_count<9, true>(BQ, empty, ~FILE_A, tm) + ray_count<7, true>(BQ, empty, ~FILE_H, tm);
+    // kings: filtered by the pre-move enemy map only (lib.rs:613-619)
+    u64 K = s.k & own;
+    while (K) {
+        int sq = ctz(K);
+        K &= K - 1;
+        total += popc(king_set(bit(sq)) & ~own & ~g.enemy_att);
+    }
+    // pinned pawns and sliders
+    u64 pp = own & g.pinned & ~s.n & ~s.k;
+    while (pp) {
+        int sq = ctz(pp);
+        pp &= pp - 1;
+        total += popc(legal_targets(s, g, sq, type_at(s, sq)));
+    }
+    return total;
+}
+
 // ---- pick by rank in ACTION-ID order (the random self-play policy) ----------------------
 // The driver draws k uniformly in [0, #legal); k maps to the k-th legal action in ascending
 // action id (from*64+to, castles 4096.. last) -- the order of the legal-action mask, i.e.

@@ -63,14 +63,10 @@ GC_HD int next_child(MoveWalk& w, const Pos& s, const Gen& g, const MoveSet& ms,
 template <class SA, class SB>
 GC_HD uint64_t perft_small(const Pos& root, int depth, SA& sa, SB& sb) {
     if (depth <= 0) return 1;
-    NoScratch none;
     Gen g0;
     MoveSet m0;
     gen_init(root, g0);
-    if (depth == 1) {
-        gen_moves(root, g0, m0, none);
-        return (uint64_t)m0.total;
-    }
+    if (depth == 1) return (uint64_t)count_moves(root, g0);
     gen_moves(root, g0, m0, sa);
     uint64_t nodes = 0;
     MoveWalk w0(g0);
@@ -80,8 +76,7 @@ GC_HD uint64_t perft_small(const Pos& root, int depth, SA& sa, SB& sb) {
         MoveSet m1;
         gen_init(c1, g1);
         if (depth == 2) {
-            gen_moves(c1, g1, m1, none);
-            nodes += (uint64_t)m1.total;
+            nodes += (uint64_t)count_moves(c1, g1);
             continue;
         }
         gen_moves(c1, g1, m1, sb);
@@ -89,10 +84,8 @@ GC_HD uint64_t perft_small(const Pos& root, int depth, SA& sa, SB& sb) {
         for (int k2 = 0; k2 < m1.total; k2++) {
             Pos c2 = child_of(c1, g1.white, next_child(w1, c1, g1, m1, sb, k2));
             Gen g2;
-            MoveSet m2;
             gen_init(c2, g2);
-            gen_moves(c2, g2, m2, none);
-            nodes += (uint64_t)m2.total;
+            nodes += (uint64_t)count_moves(c2, g2);
         }
     }
     return nodes;
@@ -102,7 +95,6 @@ GC_HD uint64_t perft_small(const Pos& root, int depth, SA& sa, SB& sb) {
 // split leaf level's kernel, small enough in registers for more waves per SIMD
 template <class SA>
 GC_HD uint64_t perft2(const Pos& root, SA& sa) {
-    NoScratch none;
     Gen g0;
     MoveSet m0;
     gen_init(root, g0);
@@ -112,10 +104,8 @@ GC_HD uint64_t perft2(const Pos& root, SA& sa) {
     for (int k1 = 0; k1 < m0.total; k1++) {
         Pos c1 = child_of(root, g0.white, next_child(w0, root, g0, m0, sa, k1));
         Gen g1;
-        MoveSet m1;
         gen_init(c1, g1);
-        gen_moves(c1, g1, m1, none);
-        nodes += (uint64_t)m1.total;
+        nodes += (uint64_t)count_moves(c1, g1);
     }
     return nodes;
 }

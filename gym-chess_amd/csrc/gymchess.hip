@@ -320,11 +320,8 @@ __global__ void k_count_children(SoA in, T* __restrict__ cnt) {
     if (i >= in.n) return;
     Pos s = in.load(i);
     Gen g;
-    MoveSet ms;
-    NoScratch none;
     gen_init(s, g);
-    gen_moves(s, g, ms, none);
-    cnt[i] = (T)ms.total;
+    cnt[i] = (T)count_moves(s, g);
 }
 // expand the parents a .. a+c-1 of `in` into `out` at offs[t] (offs indexed from a, relative
 // to the chunk's first child; a chunk holds < 2^31 children)

@@ -115,6 +115,18 @@ extern "C" int host_pins_agree(const int8_t* b, const uint8_t* m, int white) {
     gen_pins_finish(h, gen_pins_part<15, true>(s, h));  // the check masks (checkers | block) do not
     return g.in_check == h.in_check && g.checkmask == h.checkmask && g.pinned == h.pinned && g.pinrays == h.pinrays;
 }
+// count_moves (the perft leaves' set-wise count) == gen_moves' total == count_legal: returns
+// the count, or -1 - gen_moves' total when they differ
+extern "C" int host_count_moves_agree(const int8_t* b, const uint8_t* m, int white) {
+    Pos s = import_state(b, m, white);
+    Gen g;
+    gen_init(s, g);
+    MoveSet ms;
+    NoScratch none;
+    gen_moves(s, g, ms, none);
+    int c = count_moves(s, g);
+    return (c == ms.total && c == count_legal(s, g)) ? c : -1 - ms.total;
+}
 extern "C" uint64_t host_between(int a, int b) { return between(a, b); }
 extern "C" uint64_t host_rook_att(int sq, uint64_t occ) { return rook_att(sq, occ); }
 extern "C" uint64_t host_bishop_att(int sq, uint64_t occ) { return bishop_att(sq, occ); }

@@ -183,6 +183,23 @@ def test_mover_check_shortcut_every_legal_move():
     assert hits["king_move_checked"] > 50 and hits["castle_or_multi"] > 50, hits
 
 
+@pytest.mark.parametrize("seed", [11, 12])
+def test_count_moves_agrees(seed):
+    """count_moves (perft leaves: set-wise sliders / knights) == gen_moves' total ==
+    count_legal on fuzz positions (several / no kings, pins, checks), both sides to move."""
+    from conftest import random_positions
+
+    boards, metas = random_positions(3000, seed)
+    L = H.lib()
+    seen = 0
+    for i in range(len(boards)):
+        for white in (0, 1):
+            c = L.host_count_moves_agree(boards[i].ctypes.data, metas[i].ctypes.data, white)
+            assert c >= 0, (i, white, -1 - c)
+            seen += c
+    assert seen > 0
+
+
 @pytest.mark.parametrize("seed", [51, 52, 53])
 def test_pin_forms_agree(seed):
     """gen_pins_aligned (the aligned-slider loop the kernels run) == gen_pins_part (the
