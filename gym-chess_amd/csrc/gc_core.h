@@ -990,6 +990,27 @@ GC_HD bool action_legal(const Pos& s, const Gen& g, int action) {
     return (legal_targets(s, g, f, type_at(s, f)) >> t) & 1;
 }
 
+// action_legal(s, gen_init(s), action) without the whole enemy attack map: a non-king move
+// needs the check mask and pins only, a king move the attack test of its one target (the
+// map's bit there: sliders stop at the king still on its square, Q6), castles -- rare -- the
+// full context.
+GC_HD bool quick_legal(const Pos& s, int action) {
+    if (action < 0 || action > A_RESIGN) return false;
+    Gen g;
+    gen_base(s, g);
+    if (action >= 4096) {
+        gen_pins(s, g);
+        gen_enemy(s, g);
+        return action_legal(s, g, action);
+    }
+    const int f = action >> 6, t = action & 63;
+    if (!((g.own >> f) & 1)) return false;
+    const int ty = type_at(s, f);
+    if (ty == KING) return ((king_set(bit(f)) & ~g.own) >> t & 1) && !sq_attacked(s, t, !g.white);
+    gen_pins(s, g);
+    return (legal_targets(s, g, f, ty) >> t) & 1;
+}
+
 // ---- transition: next_state (lib.rs:679-784) ------------------------------------------
 // `white_player` is the caller's player argument (it selects promotion colour and which
 // rights are revoked), not necessarily the piece's colour.  Returns 0 ok, -1 if the from

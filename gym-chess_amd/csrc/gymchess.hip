@@ -465,6 +465,12 @@ __global__ void __launch_bounds__(BLOCK) k_init_cache(EnvDev e, EnvDev::InitCach
     c.own = g.own; c.fastp = ms.fastp; c.o1 = ms.o1; c.o2 = ms.o2; c.ol = ms.ol; c.orr = ms.orr;
     for (int b = 0; b < 5; b++) c.cnt[b] = ms.cnt[b];
     for (int j = 0; j < SCRATCH_SLOTS; j++) c.slots[j] = ms.big ? 0 : scr.get(j);
+    // fast pawns' targets in their slots too (select_action / write_mask read them from the
+    // origin sets; the paired API step's square-major mask reads every own piece's slot)
+    for (u64 fp = ms.big ? 0 : ms.fastp; fp; fp &= fp - 1) {
+        const int sq = ctz(fp);
+        c.slots[ordinal(g.own, sq)] = fast_pawn_targets(ms, sq, g.white);
+    }
     c.total = ms.total;
     c.castles = g.castles;
     c.white = g.white;
@@ -691,7 +697,8 @@ struct PairCtx {
 // table write left deferred in h).  Phases 0-2 and the exchange that opens phase 3:
 // w1_issue() runs on W1 in phase 0 behind the probe, w1_late() on W1 at the end of phase 2.
 // With ACT_LDS, W1 reads the action from act_lds[l] after phase 0 (W0 picked it: the
-// opponent's reply).
+// opponent's reply); with MV_LDS, whether it is played from mv_lds[l] (W0 validated it: the
+// API step).  regen: a board whose move is not played gets the moves of s itself.
 // FIDE = rules "fide" (gc_fide.h): fapply, the enemy map without the own king, en passant,
 // FIDE castling (from W0, which alone holds the in-check flag), no king captures; a legal
 // move never leaves the mover in check, so there is no mover-check and no both-checked end.
@@ -704,6 +711,7 @@ struct PairHalf {
     bool my_chk;    // the mover is in check after its move (lib.rs:1386-1393)
     bool opp_chk;   // the side now to move is in check
     bool both;      // both checked (lib.rs:1442-1446): the move is void
+    bool mv;        // the move was played (MV_LDS: as W0 decided)
     int c;          // 3-fold count of the pre-move board (0: window full)
     u32 hl;         // window length after the commit
     u64 ep_from;    // FIDE: own pawns with a legal en-passant capture
@@ -713,10 +721,10 @@ struct PairNoop {
     __device__ void operator()() const {}
 };
 
-template <bool FIDE, bool ACT_LDS, class W1Issue, class W1Late>
-__device__ __forceinline__ void pair_half(PairLds& L, int role, int l, bool mv, const Pos& s, int a,
-                                          const u32* act_lds, DevHist& h, PairHalf& H, W1Issue&& w1_issue,
-                                          W1Late&& w1_late) {
+template <bool FIDE, bool ACT_LDS, bool MV_LDS = false, class W1Issue, class W1Late>
+__device__ __forceinline__ void pair_half(PairLds& L, int role, int l, bool mv, bool regen, const Pos& s, int a,
+                                          const u32* act_lds, const u32* mv_lds, DevHist& h, PairHalf& H,
+                                          W1Issue&& w1_issue, W1Late&& w1_late) {
     PairScratch scr{&L.slots[0][l]};
     const bool white = (s.meta & M_WHITE) != 0;
     int mr = 0;
@@ -775,6 +783,7 @@ __device__ __forceinline__ void pair_half(PairLds& L, int role, int l, bool mv, 
         }
     } else {
         if constexpr (ACT_LDS) a = (int)act_lds[l];
+        if constexpr (MV_LDS) mv = mv_lds[l] != 0;
         ns.k = L.ns[0][l]; ns.q = L.ns[1][l]; ns.r = L.ns[2][l]; ns.b = L.ns[3][l];
         ns.n = L.ns[4][l]; ns.p = L.ns[5][l]; ns.w = L.ns[6][l];
         ns.meta = L.nmeta[l];
@@ -845,7 +854,7 @@ __device__ __forceinline__ void pair_half(PairLds& L, int role, int l, bool mv, 
     }
     const bool opp_chk = g.in_check;
     const bool both = !FIDE && opp_chk && my_chk;             // lib.rs:1442-1446
-    const bool gen = mv && !both;
+    const bool gen = (mv && !both) || (regen && !mv);
     MoveSet& ms = H.ms;
     moveset_clear(ms);
     ms.big = popc(g.own) > SCRATCH_SLOTS;
@@ -867,7 +876,7 @@ __device__ __forceinline__ void pair_half(PairLds& L, int role, int l, bool mv, 
         }
     } else {
         if (gen && !ms.big) part = FIDE ? gen_moves_b<PairScratch, true>(ns, g, ms, scr) : gen_moves_b(ns, g, ms, scr);
-        if (gen) {
+        if (mv && !both) {
             // the probe's data is first touched here (an opaque use after the generation:
             // otherwise the compiler hoists the entry compare up to the load and waits there)
             pin(pr.e0.hdr); pin(pr.e0.k); pin(pr.e0.q); pin(pr.e0.r);
@@ -899,6 +908,7 @@ __device__ __forceinline__ void pair_half(PairLds& L, int role, int l, bool mv, 
     H.my_chk = my_chk;
     H.opp_chk = opp_chk;
     H.both = both;
+    H.mv = mv;
     H.c = c;
     H.hl = hl;
     H.ep_from = ep_from;
@@ -937,7 +947,7 @@ __device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, int ro
     // its pick from the start position's table (a serial multiply chain and a load, hidden
     // behind W0's move; the table read lands long before phase 3)
     pair_half<FIDE, false>(
-        L, role, l, mv, s, a, nullptr, h, H,
+        L, role, l, mv, false, s, a, nullptr, nullptr, h, H,
         [&] {
             x0 = philox_x0(C.seed, (u32)i, d);  // the next draw (independent of the position)
             if (C.rtable) ra = C.racts[scale_rank(x0, C.rtotal)];
@@ -1070,7 +1080,7 @@ __device__ __forceinline__ StepOut pair_step_vs(PairLdsVs* Ls, PairLdsVs& L, con
     PairHalf H;
     // ---- the agent's half-ply
     pair_half<false, false>(
-        L, role, l, mv, s, a, nullptr, h, H,
+        L, role, l, mv, false, s, a, nullptr, nullptr, h, H,
         [&] {
             x0 = philox_x0(C.seed, (u32)i, d);
             x1 = philox_x0(C.seed, (u32)i, d + 1);
@@ -1126,7 +1136,7 @@ __device__ __forceinline__ StepOut pair_step_vs(PairLdsVs* Ls, PairLdsVs& L, con
         h.commit();  // the agent ply's window write lands before the reply probes the table
     }
     const Pos s1 = s;
-    pair_half<false, true>(L, role, l, cont, s1, oa, L.oa, h, H, PairNoop{}, PairNoop{});
+    pair_half<false, true>(L, role, l, cont, false, s1, oa, L.oa, nullptr, h, H, PairNoop{}, PairNoop{});
     if (cont) {
         if (H.both) {
             o.reason = R_BOTH_CHECKED;
@@ -1179,7 +1189,7 @@ __device__ __forceinline__ StepOut pair_step_vs(PairLdsVs* Ls, PairLdsVs& L, con
         if (any) {
             const int oa = (int)(nd ? ra >> 16 : ra & 0xFFFFu);
             const Pos s0 = s;
-            pair_half<false, false>(L, role, l, open, s0, oa, nullptr, h, H, PairNoop{}, PairNoop{});
+            pair_half<false, false>(L, role, l, open, false, s0, oa, nullptr, nullptr, h, H, PairNoop{}, PairNoop{});
             if (open) {
                 s = pair_settle(H, true);
                 s.meta = (s.meta & ~(u32)M_DONE) + (1u << M_MC_SHIFT);
@@ -1253,8 +1263,11 @@ __device__ __forceinline__ PairIO store_io(uint8_t* slab, int nn) {
 // every launch -- measured ~2-3k cycles, paid wherever the compiler sinks it, and with SGPRs
 // scarce it sank it next to a spill that forced the wait in phase 1.  The reset position and
 // move set come from a device-memory copy (icd) instead.
-#define PAIR_PROLOGUE                                                                                       \
-    using LdsT = typename std::conditional<OPP != 0, PairLdsVs, PairLds>::type;                             \
+#define PAIR_PROLOGUE PAIR_PROLOGUE_ACT(in_io.act, )
+// ACTS: the action source (the env's next action, or the caller's for the API step);
+// ENTRY: more entry loads, waited for with the reset position's
+#define PAIR_PROLOGUE_ACT(ACTS, ENTRY)                                                                      \
+    using LdsT = typename std::conditional<OPP != 0 || API, PairLdsVs, PairLds>::type;                      \
     __shared__ LdsT Ls[PAIRS_WG];                                                                           \
     const int pw = PAIRS_WG > 1 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 7)) : 0;              \
     LdsT& L = Ls[pw];                                                                                       \
@@ -1268,13 +1281,14 @@ __device__ __forceinline__ PairIO store_io(uint8_t* slab, int nn) {
     const PairCtx C = {seed, htab, in_io.hgen, racts, icd, (rinfo >> 16) != 0, rinfo & 0xFFFFu};                 \
     GC_STAMP(0);                                                                                            \
     Pos s = in_io.load(ii);                                                                                 \
-    u32 ua = in_io.act[ii], g0 = in_io.hgen[ii], nst = in_io.nsteps[ii], d = in_io.draw[ii];                \
+    u32 ua = ACTS[ii], g0 = in_io.hgen[ii], nst = in_io.nsteps[ii], d = in_io.draw[ii];                     \
     /* the reset position (HBM, scalar loads): waited for only after the board loads above have */         \
     /* issued (an asm use is a scheduling barrier for memory operations: placed first, its round */        \
     /* trip delayed every global load); the opaque use keeps it from being re-loaded at the reset */       \
     Pos rp = icd->pos;                                                                                      \
     asm volatile("" : "+v"(rp.k), "+v"(rp.q), "+v"(rp.r), "+v"(rp.b), "+v"(rp.n), "+v"(rp.p), "+v"(rp.w),  \
                  "+v"(rp.meta)); /* VGPRs: SGPRs are the scarce file here */                                  \
+    ENTRY                                                                                                   \
     pin(s); pin(ua); pin(g0); pin(nst); pin(d);                                                             \
     GC_STAMP(1);                                                                                            \
     int a = (int)ua;                                                                                        \
@@ -1294,6 +1308,7 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
     k_env_step2(uint8_t* __restrict__ slab, int nn, int blk0, uint64_t seed, u64* __restrict__ htab,
                 const uint16_t* __restrict__ racts, const EnvDev::InitCache* __restrict__ icd,
                 u32 rinfo /* ic.table << 16 | ic.total */) {
+    constexpr bool API = false;
     PAIR_PROLOGUE
     StepOut o = pair_step<OPP, false, FIDE>(Ls, L, C, role, l, i, live, rp, s, a, d, h, nst);
     GC_STAMP(6);
@@ -1326,6 +1341,7 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
     k_env_rollout2(uint8_t* __restrict__ slab, int nn, int blk0, uint64_t seed, u64* __restrict__ htab,
                    const uint16_t* __restrict__ racts, const EnvDev::InitCache* __restrict__ icd, u32 rinfo, int plies,
                    uint64_t* __restrict__ stats) {
+    constexpr bool API = false;
     PAIR_PROLOGUE
     uint64_t steps = 0, rsum = 0;
     u32 e_mate = 0, e_rep = 0, e_cap = 0, e_nomove = 0, e_err = 0;
@@ -1560,6 +1576,197 @@ __global__ void __launch_bounds__(BLOCK) k_env_step_api(EnvDev e, const uint16_t
     e.reward[i] = o.reward;
     e.done[i] = (uint8_t)o.done;
     e.reason[i] = (uint8_t)o.reason;
+}
+
+// ----------------------------------------------------------------------------- API step, paired
+// k_env_step_api (opponent "none") on the paired driver.  W0 validates the external action
+// on the pre-move board (quick_legal: a king move's target is attack-tested alone, no enemy
+// map; chess_v2.py:240) and applies it; one pair_half generates the next side's moves, or --
+// for a board whose state stays (invalid action, done, move cap) -- its own moves again
+// (regen).  Phase 3: both waves settle the outcome (env_step<VALIDATE = true>); W0 completes
+// the parked targets (fast pawns, or a reset board's cached set) and picks; each wave writes
+// half of the square-major mask; W1 the observation and outputs.  A board left with both
+// kings checked and no reset (weird positions only) regenerates alone, without slots.
+struct ApiOut {
+    int32_t* rw;
+    uint8_t* dn;
+    uint8_t* rs;
+    u64* mask;
+    int8_t* obs;
+    int32_t* cnt;
+    uint16_t* pick;
+};
+__device__ __forceinline__ void ic_moves(const EnvDev::InitCache& ic, Gen& g, MoveSet& ms) {
+    g.white = ic.white;
+    g.own = ic.own;
+    g.castles = ic.castles;
+    ms.fastp = ic.fastp; ms.o1 = ic.o1; ms.o2 = ic.o2; ms.ol = ic.ol; ms.orr = ic.orr;
+#pragma unroll
+    for (int b = 0; b < 5; b++) ms.cnt[b] = ic.cnt[b];
+    ms.total = ic.total;
+    ms.big = false;
+}
+
+// 16 argument dwords, no padding (all preloaded): the output pointers live in device memory
+// (outp, rewritten only when the caller's buffers change), auto-reset rides in rinfo bit 17
+__global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
+    k_env_step_api2(uint8_t* __restrict__ slab, uint64_t seed, u64* __restrict__ htab,
+                    const uint16_t* __restrict__ racts, const EnvDev::InitCache* __restrict__ icd,
+                    const uint16_t* __restrict__ acts, const ApiOut* __restrict__ outp, int nn,
+                    u32 rinfo /* autoreset << 17 | ic.table << 16 | ic.total */) {
+    constexpr int OPP = 0;
+    constexpr bool API = true;
+    constexpr int blk0 = 0;
+    const int autoreset = (rinfo >> 17) & 1;
+    rinfo &= 0x1FFFFu;
+    ApiOut out;
+    PAIR_PROLOGUE_ACT(acts, out = *outp; asm volatile("" : "+s"(out.rw), "+s"(out.dn), "+s"(out.rs), "+s"(out.mask),
+                                                                  "+s"(out.obs), "+s"(out.cnt), "+s"(out.pick));)
+    PairScratch scr{&L.slots[0][l]};
+    const bool done0 = (s.meta & M_DONE) != 0;              // chess_v2.py:245-251
+    const bool cap = mc_of(s.meta) > MOVES_MAX;             // 252-258
+    const bool white = (s.meta & M_WHITE) != 0;
+    const bool pre = live && !done0 && !cap;
+    bool valid = false;
+    if (role == 0) {  // chess_v2.py:240-242, on the pre-move board
+        valid = quick_legal(s, a);
+        L.act[l] = valid ? 1u : 0u;
+        L.draw[l] = (pre && valid) ? 1u : 0u;  // W1 reads it in phase 1 (MV_LDS)
+    }
+    u32 x0 = 0;
+    uint16_t ra = (uint16_t)A_NONE;
+    PairHalf H;
+    pair_half<false, false, true>(
+        L, role, l, role == 0 ? (pre && valid) : pre, live, s, a, nullptr, L.draw, h, H,
+        [&] {
+            x0 = philox_x0(C.seed, (u32)i, d);
+            if (C.rtable) ra = C.racts[scale_rank(x0, C.rtotal)];
+            L.x0[l] = x0;
+        },
+        [&] { L.ra[l] = ra; });
+    if (role) valid = L.act[l] != 0;
+    else {
+        x0 = L.x0[l];
+        ra = (uint16_t)L.ra[l];
+    }
+    StepOut o = {0, 0, R_NONE, 0};
+    if (!valid) {
+        o.reward = -10;
+        o.done = done0 ? 1 : 0;
+        o.reason = R_INVALID;
+    } else if (done0) {
+        o.done = 1;
+        o.reason = R_DONE_ALREADY;
+    } else if (cap) {
+        o.done = 1;
+        o.reason = R_MOVE_CAP;
+    } else if (H.both) {
+        o.done = 1;
+        o.reason = R_BOTH_CHECKED;
+    } else {
+        s = pair_settle(H, white);
+        o.reward = -10 + H.mr;  // INVALID_ACTION_REWARD + move reward (Q9)
+        o.moved = 1;
+        if (H.c >= 3) { o.done = 1; o.reason = R_REPETITION; }
+        if (H.c == 0) { o.done = 1; o.reason = R_WINDOW_FULL; }
+        if (H.ms.total == 0 && H.opp_chk) {  // 270-272
+            s.meta |= M_DONE;
+            o.done = 1;
+            o.reward += 100;
+            o.reason = R_MATE;
+        }
+        if (!o.done && !white) s.meta += (1u << M_MC_SHIFT);  // 291-292
+    }
+    nst += 1;
+    const bool reset = live && autoreset && o.done;
+    if (reset) {
+        s = rp;
+        h.bump_gen();
+    }
+    const bool alone = live && !reset && valid && !done0 && !cap && H.both;  // state kept, moves not generated
+    // W0: every own piece's targets into its slot -- the fast pawns' from their origin sets, a
+    // reset board's from the start position's cache -- so that the mask is written square-major
+    // by both waves, each word once (coalesced, no zero-then-patch); castles and the whole
+    // enemy map (king targets of > 16-piece boards) to W1
+    if (role == 0) {
+        if (reset) {
+#pragma unroll
+            for (int j = 0; j < SCRATCH_SLOTS; j++) scr.put(j, C.icd->slots[j]);
+        } else if (!H.ms.big) {
+            for (u64 fp = H.ms.fastp; fp; fp &= fp - 1) {
+                const int sq = ctz(fp);
+                scr.put(ordinal(H.g.own, sq), fast_pawn_targets(H.ms, sq, H.g.white));
+            }
+        }
+        L.nmeta[l] = H.g.castles;
+        L.enemy[l] = H.g.enemy_att;
+    }
+    pair_barrier();
+    Gen g = H.g;
+    MoveSet ms = H.ms;
+    if (role) {
+        g.castles = L.nmeta[l];
+        g.enemy_att = L.enemy[l];
+    }
+    if (reset) ic_moves(*C.icd, g, ms);
+    if (alone) {  // the big-board path: legal targets per piece, no slots
+        gen_init(s, g);
+        moveset_clear(ms);
+        ms.big = true;
+        ms.total = count_legal(s, g);
+    }
+    if (out.mask && live) {
+        u64* o = out.mask + i;
+        const size_t N = (size_t)nn;
+        if (!ms.big) {  // W1 squares 0..31, W0 32..63 and the castles word
+            const int s0 = role ? 0 : 32;
+            int j = popc(g.own & below(s0));
+#pragma unroll 8
+            for (int sq = s0; sq < s0 + 32; sq++) {
+                const bool b = (g.own >> sq) & 1;
+                const u64 v = scr.get(j & (SCRATCH_SLOTS - 1));
+                o[sq * N] = b ? v : 0ull;
+                j += b ? 1 : 0;
+            }
+            if (role == 0) {
+                u64 c = 0;
+                if (g.castles & 1) c |= g.white ? (1ull << 1) : (1ull << 3);  // QS: 4097 / 4099
+                if (g.castles & 2) c |= g.white ? (1ull << 0) : (1ull << 2);  // KS: 4096 / 4098
+                o[64 * N] = c;
+            }
+        } else if (role) {
+            write_mask(s, g, ms, scr, o, N);
+        }
+    }
+    const PairIO io = store_io(slab, nn);
+    if (role == 0) {
+        if (out.pick && live) {
+            uint16_t p = (uint16_t)A_NONE;
+            if (reset && C.rtable) {
+                p = ra;
+            } else if (ms.total > 0) {
+                int k = (int)scale_rank(x0, (u32)ms.total);
+                p = (uint16_t)select_action(s, g, ms, scr, k);
+            }
+            d += ms.total > 0 ? 1u : 0u;
+            out.pick[i] = p;
+            io.act[i] = p;
+            io.draw[i] = d;
+        }
+    } else if (live) {
+        if (out.obs) write_obs(s, out.obs + 64 * (size_t)i);
+        if (out.cnt) out.cnt[i] = ms.total;
+        out.rw[i] = o.reward;
+        out.dn[i] = (uint8_t)o.done;
+        out.rs[i] = (uint8_t)o.reason;
+        h.commit();
+        io.store(i, s);
+        h.flush(g0);
+        io.nsteps[i] = nst;
+        io.reward[i] = o.reward;
+        io.done[i] = (uint8_t)o.done;
+        io.reason[i] = (uint8_t)o.reason;
+    }
 }
 
 __global__ void __launch_bounds__(BLOCK) k_select(EnvDev e) {
@@ -2031,6 +2238,8 @@ struct gc_env {
     bool policy_ready = false;  // act[] holds policy picks for the current states
     int rules = 0;              // 0 reference, 1 FIDE (gc_fide.h)
     int8_t* ep = nullptr;       // FIDE ingest: en-passant files
+    ApiOut* api_out = nullptr;  // the paired API step's output pointers (device copy of api_host)
+    ApiOut api_host{};
     uint16_t* reset_acts = nullptr;
     EnvDev::InitCache* icd = nullptr;  // device copy of d.ic (the paired kernels read it from HBM)
     EnvDev::InitCache* icd_f = nullptr;  // the same for the FIDE reset position (gc_env_set_rules)
@@ -2049,7 +2258,7 @@ struct gc_env {
 };
 
 static void env_free(gc_env* e) {
-    void* ps[] = {e->reset_acts, e->icd, e->icd_f, e->racts_f, e->ep, e->slab, e->d.htab, e->mbox, e->m8, e->mask,
+    void* ps[] = {e->api_out, e->reset_acts, e->icd, e->icd_f, e->racts_f, e->ep, e->slab, e->d.htab, e->mbox, e->m8, e->mask,
                   e->list, e->counts, e->lmask, e->stats};
     for (void* p : ps) if (p) (void)hipFree(p);
     for (auto& v : e->ev) if (v) (void)hipEventDestroy(v);
@@ -2310,7 +2519,24 @@ extern "C" int gc_env_step_device(gc_env* e, const uint16_t* d_actions, int32_t*
     if (flags & ~1) return fail("flags: bit 0 = auto-reset");
     HIPCHK(hipSetDevice(e->device));
     const int ar = flags & 1;
-    if (e->d.opp)
+    static const bool one_wave = getenv("GC_STEP1") != nullptr;  // A/B switch to the one-wave kernel
+    if (!e->d.opp && e->d.ic.usable && e->d.ic.table && !one_wave) {
+        const EnvDev& d = e->d;
+        const ResetInfo r = reset_info(e);
+        const int nb = (e->n + PAIR_BOARDS - 1) / PAIR_BOARDS;
+        const ApiOut o = {d_reward, d_done, d_reason, d_mask, d_obs, d_count, d_pick};
+        if (!e->api_out) {
+            if (dalloc(&e->api_out, 1)) return -1;
+            e->api_host = {};
+        }
+        if (memcmp(&o, &e->api_host, sizeof o) != 0) {  // the caller's buffers changed
+            e->api_host = o;
+            HIPCHK(hipMemcpyAsync(e->api_out, &e->api_host, sizeof o, hipMemcpyHostToDevice, e->stream));
+            HIPCHK(hipStreamSynchronize(e->stream));  // api_host may change again before a lazy copy ran
+        }
+        k_env_step_api2<<<(nb + PAIRS_WG - 1) / PAIRS_WG, 2 * PAIR_BOARDS * PAIRS_WG, 0, e->stream>>>(
+            e->slab, d.seed, d.htab, r.racts, r.icd, d_actions, e->api_out, d.n, r.rinfo | ((u32)ar << 17));
+    } else if (e->d.opp)
         k_env_step_api<true><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d, d_actions, d_reward, d_done, d_reason,
                                                                       d_mask, d_obs, d_count, d_pick, ar);
     else

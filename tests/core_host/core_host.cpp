@@ -127,6 +127,20 @@ extern "C" int host_count_moves_agree(const int8_t* b, const uint8_t* m, int whi
     int c = count_moves(s, g);
     return (c == ms.total && c == count_legal(s, g)) ? c : -1 - ms.total;
 }
+// quick_legal (the paired API step's validation) == action_legal over gen_init, for every
+// action id: returns the number of legal actions, or -1 - the first action that differs
+extern "C" int host_quick_legal_agree(const int8_t* b, const uint8_t* m, int white) {
+    Pos s = import_state(b, m, white);
+    Gen g;
+    gen_init(s, g);
+    int n = 0;
+    for (int a = -1; a <= A_RESIGN + 1; a++) {
+        bool q = quick_legal(s, a), r = action_legal(s, g, a);
+        if (q != r) return -1 - a;
+        n += r;
+    }
+    return n;
+}
 extern "C" uint64_t host_between(int a, int b) { return between(a, b); }
 extern "C" uint64_t host_rook_att(int sq, uint64_t occ) { return rook_att(sq, occ); }
 extern "C" uint64_t host_bishop_att(int sq, uint64_t occ) { return bishop_att(sq, occ); }

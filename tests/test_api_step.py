@@ -89,3 +89,44 @@ def test_obs_of_weird_boards(oracle):
     env.step_device(io, actions=act.ptr["pick"])
     o = io.fetch()
     assert (o["reason"] == 6).all() and (o["obs"] == boards).all()
+
+
+@pytest.mark.parametrize("autoreset", [False, True])
+def test_step_device_weird_boards_equal_host_step(oracle, autoreset):
+    """Fuzz positions (several / no kings, pawns on back ranks, > 16 pieces, rights without
+    rooks): the device-buffer step (the paired kernel: quick_legal validation, regen of kept
+    states, the lone regeneration of a both-checked board) == the host step ply by ply, with
+    the mask / obs / count of every board; with auto-reset, the reset boards' too."""
+    from conftest import random_positions
+    from gym_chess_amd.env import BatchedChessEnv
+
+    n = 1000
+    boards, metas = random_positions(n, 4242)
+    a = BatchedChessEnv(n, device=0, seed=5)
+    b = BatchedChessEnv(n, device=0, seed=5)
+    assert a.paired()
+    a.set_states(boards, metas)
+    b.set_states(boards, metas)
+    io = a.device_io(pick=False)
+    act_buf = a.device_io(mask=False, obs=False, count=False, pick=True, select=False)
+    rng = np.random.RandomState(8)
+    reasons = set()
+    for ply in range(6):
+        lists = b.possible_actions()
+        acts = np.array([l[rng.randint(len(l))] if l and rng.rand() > 0.2 else rng.randint(4101) for l in lists],
+                        dtype=np.uint16)
+        act_buf.upload_actions(acts)
+        a.step_device(io, actions=act_buf.ptr["pick"], autoreset=autoreset)
+        rw, dn, why = b.step(acts)
+        if autoreset and dn.any():
+            b.reset(dn.astype(np.uint8))
+        reasons |= set(int(x) for x in why)
+        o = io.fetch()
+        assert (o["reward"] == rw).all() and (o["done"].astype(bool) == dn).all() and (o["reason"] == why).all(), ply
+        bb, bm = b.boards()
+        ab, am = a.boards()
+        assert (ab == bb).all() and (am == bm).all(), ply
+        assert (o["obs"] == bb).all(), ply
+        assert (_mask_bits(o["mask"]) == b.legal_mask()).all(), ply
+        assert (o["count"] == np.array([len(x) for x in b.possible_actions()])).all(), ply
+    assert {0, 6}.issubset(reasons), reasons

@@ -200,6 +200,24 @@ def test_count_moves_agrees(seed):
     assert seen > 0
 
 
+@pytest.mark.parametrize("seed", [13])
+def test_quick_legal_agrees(seed):
+    """quick_legal (the paired API step's validation: no enemy map, a king target's attack
+    test alone) == action_legal over gen_init for all 4 101 action ids (and -1, 4101) on fuzz
+    positions, both sides to move."""
+    from conftest import random_positions
+
+    boards, metas = random_positions(600, seed)
+    L = H.lib()
+    legal = 0
+    for i in range(len(boards)):
+        for white in (0, 1):
+            c = L.host_quick_legal_agree(boards[i].ctypes.data, metas[i].ctypes.data, white)
+            assert c >= 0, (i, white, -1 - c)
+            legal += c
+    assert legal > 1000
+
+
 @pytest.mark.parametrize("seed", [51, 52, 53])
 def test_pin_forms_agree(seed):
     """gen_pins_aligned (the aligned-slider loop the kernels run) == gen_pins_part (the
