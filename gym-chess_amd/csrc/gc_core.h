@@ -931,6 +931,49 @@ GC_HD int select_action(const Pos& s, const Gen& g, const MoveSet& ms, const S& 
     return lo * 64 + kth_set_bit(tg, k);
 }
 
+// The same pick with short dependency chains (the rank search sits on the paired step's
+// critical path): row totals of all 8 rows at once (per-byte popcounts of the 5 count planes,
+// weighted), their byte-wise prefix sums by one multiply, a 3-step search over the 8 bytes;
+// then the same over the 8 squares of the row (the planes' bits of that row spread to bytes).
+// Byte sums need < 256 moves: more (never in play) take the bisection above.
+GC_HD u64 byte_popc(u64 x) {
+    x = x - ((x >> 1) & 0x5555555555555555ull);
+    x = (x & 0x3333333333333333ull) + ((x >> 2) & 0x3333333333333333ull);
+    return (x + (x >> 4)) & 0x0F0F0F0F0F0F0F0Full;
+}
+GC_HD u64 spread8(u32 b) {  // bit j of b -> byte j (0 / 1)
+    u64 y = ((u64)(b & 0xFFu) * 0x0101010101010101ull) & 0x8040201008040201ull;
+    return ((y + 0x7F7F7F7F7F7F7F7Full) >> 7) & 0x0101010101010101ull;
+}
+// p: inclusive prefix sums in 8 bytes (non-decreasing, byte 7 > k): the first byte above k
+GC_HD int first_byte_above(u64 p, int k) {
+    int r = (int)((p >> 24) & 0xFF) <= k ? 4 : 0;
+    r += (int)((p >> (8 * r + 8)) & 0xFF) <= k ? 2 : 0;
+    r += (int)((p >> (8 * r)) & 0xFF) <= k ? 1 : 0;
+    return r;
+}
+template <class S>
+GC_HD int select_action_swar(const Pos& s, const Gen& g, const MoveSet& ms, const S& scr, int k) {
+    const int normal = ms.total - popc(g.castles);
+    if (k >= normal || ms.big || normal > 255) return select_action(s, g, ms, scr, k);
+    const u64 rows = byte_popc(ms.cnt[0]) + (byte_popc(ms.cnt[1]) << 1) + (byte_popc(ms.cnt[2]) << 2) +
+                     (byte_popc(ms.cnt[3]) << 3) + (byte_popc(ms.cnt[4]) << 4);
+    const u64 rpre = rows * 0x0101010101010101ull;
+    const int r = first_byte_above(rpre, k);
+    k -= r ? (int)((rpre >> (8 * r - 8)) & 0xFF) : 0;
+    const int sh = 8 * r;
+    const u64 sqs = spread8((u32)(ms.cnt[0] >> sh)) + (spread8((u32)(ms.cnt[1] >> sh)) << 1) +
+                    (spread8((u32)(ms.cnt[2] >> sh)) << 2) + (spread8((u32)(ms.cnt[3] >> sh)) << 3) +
+                    (spread8((u32)(ms.cnt[4] >> sh)) << 4);
+    const u64 spre = sqs * 0x0101010101010101ull;
+    const int f = first_byte_above(spre, k);
+    k -= f ? (int)((spre >> (8 * f - 8)) & 0xFF) : 0;
+    const int lo = sh + f;
+    u64 parked = scr.get(ordinal(g.own, lo));
+    u64 tg = ((ms.fastp >> lo) & 1) ? fast_pawn_targets(ms, lo, g.white) : parked;
+    return lo * 64 + kth_set_bit(tg, k);
+}
+
 // k-th legal action (0 <= k < ms.total) in reference order, from gen_moves' results
 template <class S>
 GC_HD int select_move(const Pos& s, const Gen& g, const MoveSet& ms, const S& scr, int k) {

@@ -231,6 +231,20 @@ static void host_reset(Pos& s, HostHist& h, const Pos& ip) {
 }
 
 // the self-play driver of k_env_step<true, OPP> / k_env_rollout<OPP> on the host
+// select_action_swar (the paired step's pick) == select_action for every rank: returns the
+// number of ranks checked, or -1 - the first rank that differs
+extern "C" int host_pick_agree(const int8_t* b, const uint8_t* m, int white) {
+    Pos s = import_state(b, m, white);
+    Gen g;
+    gen_init(s, g);
+    MoveSet ms;
+    HostScratch scr;
+    gen_moves(s, g, ms, scr);
+    for (int k = 0; k < ms.total; k++)
+        if (select_action_swar(s, g, ms, scr, k) != select_action(s, g, ms, scr, k)) return -1 - k;
+    return ms.total;
+}
+
 struct HostEnv {
     Pos init, s;
     HostHist h;

@@ -200,6 +200,23 @@ def test_count_moves_agrees(seed):
     assert seen > 0
 
 
+@pytest.mark.parametrize("seed", [14, 15])
+def test_swar_pick_agrees(seed):
+    """select_action_swar (byte-wise prefix sums of the count planes) == select_action (the
+    bisection) for every rank on fuzz positions, both sides to move."""
+    from conftest import random_positions
+
+    boards, metas = random_positions(3000, seed)
+    L = H.lib()
+    ranks = 0
+    for i in range(len(boards)):
+        for white in (0, 1):
+            c = L.host_pick_agree(boards[i].ctypes.data, metas[i].ctypes.data, white)
+            assert c >= 0, (i, white, -1 - c)
+            ranks += c
+    assert ranks > 10000
+
+
 @pytest.mark.parametrize("seed", [13])
 def test_quick_legal_agrees(seed):
     """quick_legal (the paired API step's validation: no enemy map, a king target's attack

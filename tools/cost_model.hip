@@ -55,3 +55,17 @@ extern "C" __global__ void c_select_action(const u64* p, u64* o) {
     ms.total = (int)p[611]; ms.big = false;
     o[threadIdx.x] = select_action(s, g, ms, sc, (int)(p[612 + threadIdx.x] & 31));
 }
+// perft leaf pieces: the count of a position given its context, the child's context, a child
+extern "C" __global__ void c_count_moves(const u64* p, u64* o) {
+    Pos s = ld(p); Gen g; gen_init(s, g); o[threadIdx.x] = (u64)count_moves(s, g);
+}
+extern "C" __global__ void c_gen_init(const u64* p, u64* o) {
+    Pos s = ld(p); Gen g; gen_init(s, g);
+    o[threadIdx.x] = g.checkmask ^ g.pinned ^ g.pinrays ^ g.enemy_att ^ g.castles ^ (u64)g.ks;
+}
+extern "C" __global__ void c_child_count(const u64* p, u64* o) {
+    Pos s = ld(p); int r; bool ir;
+    apply_legal(s, true, (int)(p[512 + threadIdx.x] & 4095), &r, &ir);
+    s.meta = (s.meta & ~(u32)M_RIGHTS) | eff_rights(s);
+    Gen g; gen_init(s, g); o[threadIdx.x] = (u64)count_moves(s, g);
+}
