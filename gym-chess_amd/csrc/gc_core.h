@@ -823,7 +823,8 @@ template <int SH, bool LEFT>
 GC_HD int ray_count(u64 gen, u64 empty, u64 wrap, u64 tmask) {
     return popc(ray_fill_att<SH, LEFT>(gen, empty, wrap) & tmask);
 }
-GC_HD int count_moves(const Pos& s, const Gen& g) {
+// pawns, knights, kings and pinned pieces (count_moves without the unpinned sliders)
+GC_HD int count_nonsliders(const Pos& s, const Gen& g) {
     const u64 own = g.own, cm = g.checkmask, tm = ~own & cm, empty = ~g.occ, opp = g.opp;
     const u64 fr = own & ~g.pinned;
     int total = popc(g.castles);
@@ -842,12 +843,6 @@ GC_HD int count_moves(const Pos& s, const Gen& g) {
     const u64 l2 = (N >> 2) & ~(FILE_H | (FILE_H >> 1)), r2 = (N << 2) & ~(FILE_A | (FILE_A << 1));
     total += popc((l1 << 16) & tm) + popc((r1 << 16) & tm) + popc((l1 >> 16) & tm) + popc((r1 >> 16) & tm) +
              popc((l2 << 8) & tm) + popc((r2 << 8) & tm) + popc((l2 >> 8) & tm) + popc((r2 >> 8) & tm);
-    // unpinned sliders
-    const u64 RQ = (s.r | s.q) & fr, BQ = (s.b | s.q) & fr;
-    total += ray_count<8, false>(RQ, empty, ~0ull, tm) + ray_count<8, true>(RQ, empty, ~0ull, tm) +
-             ray_count<1, true>(RQ, empty, ~FILE_A, tm) + ray_count<1, false>(RQ, empty, ~FILE_H, tm);
-    total += ray_count<7, false>(BQ, empty, ~FILE_A, tm) + ray_count<9, false>(BQ, empty, ~FILE_H, tm) +
-             ray_count<9, true>(BQ, empty, ~FILE_A, tm) + ray_count<7, true>(BQ, empty, ~FILE_H, tm);
     // kings: filtered by the pre-move enemy map only (lib.rs:613-619)
     u64 K = s.k & own;
     while (K) {
@@ -863,6 +858,61 @@ GC_HD int count_moves(const Pos& s, const Gen& g) {
         total += popc(legal_targets(s, g, sq, type_at(s, sq)));
     }
     return total;
+}
+GC_HD int count_moves(const Pos& s, const Gen& g) {
+    const u64 tm = ~g.own & g.checkmask, empty = ~g.occ, fr = g.own & ~g.pinned;
+    const u64 RQ = (s.r | s.q) & fr, BQ = (s.b | s.q) & fr;
+    return count_nonsliders(s, g) +
+           ray_count<8, false>(RQ, empty, ~0ull, tm) + ray_count<8, true>(RQ, empty, ~0ull, tm) +
+           ray_count<1, true>(RQ, empty, ~FILE_A, tm) + ray_count<1, false>(RQ, empty, ~FILE_H, tm) +
+           ray_count<7, false>(BQ, empty, ~FILE_A, tm) + ray_count<9, false>(BQ, empty, ~FILE_H, tm) +
+           ray_count<9, true>(BQ, empty, ~FILE_A, tm) + ray_count<7, true>(BQ, empty, ~FILE_H, tm);
+}
+
+// gen_init + count_moves of a position with the two Kogge-Stone passes fused: in each
+// direction the enemy sliders' fill (the attack map) and the own unpinned sliders' fill (the
+// count) share their propagator masks (the empty squares).  The perft leaves' child count.
+template <int SH, bool LEFT>
+GC_HD void ray_fill_pair(u64 ge, u64 go, u64 empty, u64 wrap, u64& ae, u64& ao) {
+    u64 pro = empty & wrap;
+    ge |= pro & sh<SH, LEFT>(ge);
+    go |= pro & sh<SH, LEFT>(go);
+    pro &= sh<SH, LEFT>(pro);
+    ge |= pro & sh<2 * SH, LEFT>(ge);
+    go |= pro & sh<2 * SH, LEFT>(go);
+    pro &= sh<2 * SH, LEFT>(pro);
+    ge |= pro & sh<4 * SH, LEFT>(ge);
+    go |= pro & sh<4 * SH, LEFT>(go);
+    ae = sh<SH, LEFT>(ge) & wrap;
+    ao = sh<SH, LEFT>(go) & wrap;
+}
+GC_HD int count_position(const Pos& s) {
+    Gen g;
+    gen_base(s, g);
+    gen_pins(s, g);
+    const u64 empty = ~g.occ, fr = g.own & ~g.pinned, tm = ~g.own & g.checkmask;
+    const u64 eRQ = (s.r | s.q) & g.opp, eBQ = (s.b | s.q) & g.opp;
+    const u64 oRQ = (s.r | s.q) & fr, oBQ = (s.b | s.q) & fr;
+    u64 att = 0, ae, ao;
+    int n = 0;
+#define GC_PAIR(SH, LEFT, GE, GO, WRAP)                  \
+    ray_fill_pair<SH, LEFT>(GE, GO, empty, WRAP, ae, ao); \
+    att |= ae;                                           \
+    n += popc(ao & tm);
+    GC_PAIR(8, false, eRQ, oRQ, ~0ull)
+    GC_PAIR(8, true, eRQ, oRQ, ~0ull)
+    GC_PAIR(1, true, eRQ, oRQ, ~FILE_A)
+    GC_PAIR(1, false, eRQ, oRQ, ~FILE_H)
+    GC_PAIR(7, false, eBQ, oBQ, ~FILE_A)
+    GC_PAIR(9, false, eBQ, oBQ, ~FILE_H)
+    GC_PAIR(9, true, eBQ, oBQ, ~FILE_A)
+    GC_PAIR(7, true, eBQ, oBQ, ~FILE_H)
+#undef GC_PAIR
+    if (g.ks >= 0) {  // gen_enemy (no king: no map, no castling)
+        g.enemy_att = att | side_attacks_leapers(s, !g.white);
+        gen_castles(s, g);
+    }
+    return n + count_nonsliders(s, g);
 }
 
 // ---- pick by rank in ACTION-ID order (the random self-play policy) ----------------------

@@ -72,20 +72,18 @@ GC_HD uint64_t perft_small(const Pos& root, int depth, SA& sa, SB& sb) {
     MoveWalk w0(g0);
     for (int k1 = 0; k1 < m0.total; k1++) {
         Pos c1 = child_of(root, g0.white, next_child(w0, root, g0, m0, sa, k1));
+        if (depth == 2) {
+            nodes += (uint64_t)count_position(c1);
+            continue;
+        }
         Gen g1;
         MoveSet m1;
         gen_init(c1, g1);
-        if (depth == 2) {
-            nodes += (uint64_t)count_moves(c1, g1);
-            continue;
-        }
         gen_moves(c1, g1, m1, sb);
         MoveWalk w1(g1);
         for (int k2 = 0; k2 < m1.total; k2++) {
             Pos c2 = child_of(c1, g1.white, next_child(w1, c1, g1, m1, sb, k2));
-            Gen g2;
-            gen_init(c2, g2);
-            nodes += (uint64_t)count_moves(c2, g2);
+            nodes += (uint64_t)count_position(c2);
         }
     }
     return nodes;
@@ -103,9 +101,13 @@ GC_HD uint64_t perft2(const Pos& root, SA& sa) {
     MoveWalk w0(g0);
     for (int k1 = 0; k1 < m0.total; k1++) {
         Pos c1 = child_of(root, g0.white, next_child(w0, root, g0, m0, sa, k1));
+#ifdef GC_PERFT_UNFUSED  // A/B: the map and the count in two passes
         Gen g1;
         gen_init(c1, g1);
         nodes += (uint64_t)count_moves(c1, g1);
+#else
+        nodes += (uint64_t)count_position(c1);
+#endif
     }
     return nodes;
 }

@@ -294,7 +294,7 @@ __global__ void __launch_bounds__(BLOCK) k_perft_small_perm(SoA in, const int32_
     nodes[j] = perft_small(in.load(j), depth, sa, sb);
 }
 #ifndef PERFT2_WPE
-#define PERFT2_WPE 4  // 128 VGPRs (a few spilled): 4 waves per SIMD beat 2 by ~9 %
+#define PERFT2_WPE 3  // 168 VGPRs: 3 waves per SIMD -- 1.12e12 nodes/s vs 1.06 at 4 (128 VGPRs, ~110 spilled) and 1.03 at 2
 #endif
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(PERFT2_WPE)))
 k_perft2_perm(SoA in, const int32_t* __restrict__ perm,

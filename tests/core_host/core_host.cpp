@@ -125,7 +125,7 @@ extern "C" int host_count_moves_agree(const int8_t* b, const uint8_t* m, int whi
     NoScratch none;
     gen_moves(s, g, ms, none);
     int c = count_moves(s, g);
-    return (c == ms.total && c == count_legal(s, g)) ? c : -1 - ms.total;
+    return (c == ms.total && c == count_legal(s, g) && c == count_position(s)) ? c : -1 - ms.total;
 }
 // quick_legal (the paired API step's validation) == action_legal over gen_init, for every
 // action id: returns the number of legal actions, or -1 - the first action that differs

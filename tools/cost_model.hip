@@ -69,3 +69,4 @@ extern "C" __global__ void c_child_count(const u64* p, u64* o) {
     s.meta = (s.meta & ~(u32)M_RIGHTS) | eff_rights(s);
     Gen g; gen_init(s, g); o[threadIdx.x] = (u64)count_moves(s, g);
 }
+extern "C" __global__ void c_count_position(const u64* p, u64* o) { Pos s = ld(p); o[threadIdx.x] = (u64)count_position(s); }
