@@ -1024,6 +1024,143 @@ GC_HD int select_action_swar(const Pos& s, const Gen& g, const MoveSet& ms, cons
     return lo * 64 + kth_set_bit(tg, k);
 }
 
+// ---- set-wise generation in move-set order (the random self-play policy) ------------------
+// Every legal move lies in exactly one of SW_SETS target bitboards, and the set fixes the way
+// back from a target to its origin:
+//   0-3   pawns: single push, double push (Q1), capture toward col+1, capture toward col-1
+//   4-11  the eight knight jumps
+//   12-15 rooks and queens, one bitboard per direction (row-1, row+1, col+1, col-1); 16-19
+//         bishops and queens (row-1 col+1, row-1 col-1, row+1 col+1, row+1 col-1).  Within one
+//         direction the rays of two sliders never overlap (the rear one's ray ends on the front
+//         one), so a target has one origin: the first piece behind it in that direction
+//   20-27 the eight king steps, filtered by the pre-move enemy map (lib.rs:613-619), for every
+//         own king (boards with several kings: Q7)
+// then the castles (queen side, king side).  A pinned piece joins only the sets of the
+// directions along its pin line: a pinned slider's ray there ends at its king and at the
+// pinner; a pinned pawn's targets are cut to its pin segment (a Q1 double push can jump the
+// pinner); a pinned knight never moves.  The same legal moves as gen_moves (host test on fuzz
+// positions); no per-piece loop, no parking, any number of pieces.  The policy's rank k is the
+// k-th move in this order: sets by index, targets ascending within a set.
+enum { SW_P1 = 0, SW_P2 = 1, SW_PL = 2, SW_PR = 3, SW_N = 4, SW_ORTH = 12, SW_DIAG = 16, SW_K = 20, SW_SETS = 28 };
+struct MoveSets {
+    u64 t[SW_SETS];
+};
+GC_HD int sw_popc(const u64* t, int lo, int hi) {
+    int n = 0;
+    for (int i = lo; i < hi; i++) n += popc(t[i]);
+    return n;
+}
+// a square on the tracked king's lines (0 when there is no king: then nothing is pinned)
+GC_HD int sw_ksq(const Gen& g) { return g.ks < 0 ? 0 : g.ks; }
+GC_HD void sw_pawns(const Pos& s, const Gen& g, u64* t) {
+    const u64 cm = g.checkmask, empty = ~g.occ, opp = g.opp, P = s.p & g.own, pr = g.pinrays;
+    const int kq = sw_ksq(g);
+    const u64 fp = P & ~g.pinned, pp = P & g.pinned;
+    const u64 pf = pp & file_mask(kq), pd = pp & diag_mask(kq), pa = pp & anti_mask(kq);
+    if (g.white) {  // lib.rs:935-958, p = +1: toward row 0
+        t[SW_P1] = ((fp >> 8) | ((pf >> 8) & pr)) & empty & cm;
+        t[SW_P2] = (((fp & ROW6) >> 16) | (((pf & ROW6) >> 16) & pr)) & empty & cm;
+        t[SW_PL] = (((fp >> 7) | ((pa >> 7) & pr)) & ~FILE_A) & opp & cm;  // row-1 col+1: anti-diagonal
+        t[SW_PR] = (((fp >> 9) | ((pd >> 9) & pr)) & ~FILE_H) & opp & cm;  // row-1 col-1: diagonal
+    } else {
+        t[SW_P1] = ((fp << 8) | ((pf << 8) & pr)) & empty & cm;
+        t[SW_P2] = (((fp & ROW1) << 16) | (((pf & ROW1) << 16) & pr)) & empty & cm;
+        t[SW_PL] = (((fp << 9) | ((pd << 9) & pr)) & ~FILE_A) & opp & cm;  // row+1 col+1: diagonal
+        t[SW_PR] = (((fp << 7) | ((pa << 7) & pr)) & ~FILE_H) & opp & cm;  // row+1 col-1: anti-diagonal
+    }
+}
+GC_HD void sw_knights(const Pos& s, const Gen& g, u64* t) {
+    const u64 N = s.n & g.own & ~g.pinned, tm = ~g.own & g.checkmask;
+    const u64 l1 = (N >> 1) & ~FILE_H, r1 = (N << 1) & ~FILE_A;
+    const u64 l2 = (N >> 2) & ~(FILE_H | (FILE_H >> 1)), r2 = (N << 2) & ~(FILE_A | (FILE_A << 1));
+    t[SW_N + 0] = (l1 << 16) & tm;  // target = origin + 15
+    t[SW_N + 1] = (r1 << 16) & tm;  // + 17
+    t[SW_N + 2] = (l1 >> 16) & tm;  // - 17
+    t[SW_N + 3] = (r1 >> 16) & tm;  // - 15
+    t[SW_N + 4] = (l2 << 8) & tm;   // + 6
+    t[SW_N + 5] = (r2 << 8) & tm;   // + 10
+    t[SW_N + 6] = (l2 >> 8) & tm;   // - 10
+    t[SW_N + 7] = (r2 >> 8) & tm;   // - 6
+}
+GC_HD void sw_orth(const Pos& s, const Gen& g, u64* t) {
+    const int kq = sw_ksq(g);
+    const u64 S = (s.r | s.q) & g.own, fr = S & ~g.pinned, pp = S & g.pinned;
+    const u64 empty = ~g.occ, tm = ~g.own & g.checkmask;
+    const u64 gf = fr | (pp & file_mask(kq)), gr = fr | (pp & row_mask(kq));
+    t[SW_ORTH + 0] = ray_fill_att<8, false>(gf, empty, ~0ull) & tm;
+    t[SW_ORTH + 1] = ray_fill_att<8, true>(gf, empty, ~0ull) & tm;
+    t[SW_ORTH + 2] = ray_fill_att<1, true>(gr, empty, ~FILE_A) & tm;
+    t[SW_ORTH + 3] = ray_fill_att<1, false>(gr, empty, ~FILE_H) & tm;
+}
+GC_HD void sw_diag(const Pos& s, const Gen& g, u64* t) {
+    const int kq = sw_ksq(g);
+    const u64 S = (s.b | s.q) & g.own, fr = S & ~g.pinned, pp = S & g.pinned;
+    const u64 empty = ~g.occ, tm = ~g.own & g.checkmask;
+    const u64 gd = fr | (pp & diag_mask(kq)), ga = fr | (pp & anti_mask(kq));
+    t[SW_DIAG + 0] = ray_fill_att<7, false>(ga, empty, ~FILE_A) & tm;
+    t[SW_DIAG + 1] = ray_fill_att<9, false>(gd, empty, ~FILE_H) & tm;
+    t[SW_DIAG + 2] = ray_fill_att<9, true>(gd, empty, ~FILE_A) & tm;
+    t[SW_DIAG + 3] = ray_fill_att<7, true>(ga, empty, ~FILE_H) & tm;
+}
+GC_HD void sw_kings(const Pos& s, const Gen& g, u64* t) {
+    const u64 K = s.k & g.own, ok = ~g.own & ~g.enemy_att;
+    t[SW_K + 0] = (K >> 8) & ok;              // target = origin - 8
+    t[SW_K + 1] = (K << 8) & ok;              // + 8
+    t[SW_K + 2] = ((K >> 1) & ~FILE_H) & ok;  // - 1
+    t[SW_K + 3] = ((K << 1) & ~FILE_A) & ok;  // + 1
+    t[SW_K + 4] = ((K >> 9) & ~FILE_H) & ok;  // - 9
+    t[SW_K + 5] = ((K >> 7) & ~FILE_A) & ok;  // - 7
+    t[SW_K + 6] = ((K << 7) & ~FILE_H) & ok;  // + 7
+    t[SW_K + 7] = ((K << 9) & ~FILE_A) & ok;  // + 9
+}
+// all sets of a position whose Gen is complete (gen_init); returns the move count
+GC_HD int sw_gen(const Pos& s, const Gen& g, u64* t) {
+    sw_pawns(s, g, t);
+    sw_knights(s, g, t);
+    sw_orth(s, g, t);
+    sw_diag(s, g, t);
+    sw_kings(s, g, t);
+    return sw_popc(t, 0, SW_SETS) + popc(g.castles);
+}
+// origin of target `to` of set j.  Leapers: origin = to + a signed byte of four packed words
+// (pawn offsets by colour); sliders: the first occupied square behind the target along the
+// set's direction (one line attack from the target), branch-free for every lane.
+GC_HD int sw_origin(const Gen& g, int j, int to) {
+    const u64 w0 = g.white ? pack8(8, 16, 7, 9, -15, -17, 17, 15) : pack8(-8, -16, -9, -7, -15, -17, 17, 15);
+    const u64 w1 = pack8(-6, -10, 10, 6, 0, 0, 0, 0), w2 = pack8(0, 0, 0, 0, 8, -8, 1, -1);
+    const u64 w3 = pack8(9, 7, -7, -9, 0, 0, 0, 0);
+    const int q = j >> 3;
+    const u64 w = q == 0 ? w0 : q == 1 ? w1 : q == 2 ? w2 : w3;
+    const int off = (int)(signed char)(w >> (8 * (j & 7)));
+    // sliders: direction d = j - SW_ORTH; d 1, 2, 6, 7 move toward higher squares
+    const int d = (j - SW_ORTH) & 7;
+    const bool up = ((0xC6u >> d) & 1) != 0;
+    const u64 line = d < 2 ? file_mask(to) : d < 4 ? row_mask(to) : (d == 5 || d == 6) ? diag_mask(to) : anti_mask(to);
+    const u64 att = line_att(g.occ, line, line_neg(to));
+    const u64 lo = att & below(to), hi = att & ~below(to);
+    const int sl = up ? (lo ? ctz(lo) : 0) : (hi ? msb(hi) : 0);  // the ray's far end: its first blocker
+    const bool slider = j >= SW_ORTH && j < SW_K;
+    return slider ? sl : to + off;
+}
+GC_HD int sw_select(const Gen& g, const u64* t, int k) {
+    int j = SW_SETS;
+    u64 tj = 0;
+#pragma unroll
+    for (int i = 0; i < SW_SETS; i++) {
+        const int c = popc(t[i]);
+        const bool hit = j == SW_SETS && k < c;
+        j = hit ? i : j;
+        tj = hit ? t[i] : tj;
+        k = j == SW_SETS ? k - c : k;
+    }
+    if (j == SW_SETS) {  // castles: k is the rank among them
+        if ((g.castles & 1) && k == 0) return g.white ? A_QSW : A_QSB;
+        return g.white ? A_KSW : A_KSB;
+    }
+    const int to = kth_set_bit(tj, k);
+    return sw_origin(g, j, to) * 64 + to;
+}
+
 // k-th legal action (0 <= k < ms.total) in reference order, from gen_moves' results
 template <class S>
 GC_HD int select_move(const Pos& s, const Gen& g, const MoveSet& ms, const S& scr, int k) {

@@ -205,6 +205,18 @@ struct PolicyCtx {
     u32 draw;
 };
 
+// The random self-play policy (opponent "none", reference rules): rank k drawn uniformly over
+// the legal moves, the k-th in move-set order (gc_core.h sw_gen / sw_select), generated here
+// set-wise from the position.  A_NONE (no draw taken) when there is no legal move.
+GC_HD int selfplay_pick(const Pos& s, PolicyCtx& pc) {
+    Gen g;
+    gen_init(s, g);
+    u64 t[SW_SETS];
+    const int n = sw_gen(s, g, t);
+    if (n == 0) return A_NONE;
+    return sw_select(g, t, (int)policy_index(pc.seed, pc.board, pc.draw++, (u32)n));
+}
+
 // step() with the random opponent (chess_v2.py:219-294 with opponent_policy set): the
 // agent's ply, WIN (+100) if the opponent is mated, else the opponent's reply (its capture
 // value is subtracted), LOSS (-100) if the agent is then mated; move_count advances only

@@ -477,6 +477,11 @@ __global__ void __launch_bounds__(BLOCK) k_init_cache(EnvDev e, EnvDev::InitCach
     c.usable = !ms.big;
     c.table = c.usable && ms.total > 0 && ms.total <= RESET_ACTS_MAX;
     c.open_safe = 1;
+    if (c.table) {  // the self-play policy's order (move sets), RESET_ACTS_MAX further on
+        u64 t[SW_SETS];
+        sw_gen(c.pos, g, t);
+        for (int k = 0; k < ms.total; k++) acts[RESET_ACTS_MAX + k] = (uint16_t)sw_select(g, t, k);
+    }
     for (int k = 0; c.table && k < ms.total; k++) {
         const int a = select_action(c.pos, g, ms, scr, k);
         acts[k] = (uint16_t)a;
@@ -525,8 +530,12 @@ __global__ void __launch_bounds__(BLOCK) k_env_reset(EnvDev e, const uint8_t* __
     if ((OPP && e.agent_black) || select) {
         Gen g;
         MoveSet ms;
-        after_reset<OPP>(e, s, h, g, ms, scr, pc);
-        if (select) e.act[i] = pick(s, g, ms, scr, e.seed, i, pc.draw);
+        if (OPP) {
+            after_reset<OPP>(e, s, h, g, ms, scr, pc);
+            if (select) e.act[i] = pick(s, g, ms, scr, e.seed, i, pc.draw);
+        } else {
+            e.act[i] = (uint16_t)selfplay_pick(s, pc);
+        }
         h.commit();
         e.draw[i] = pc.draw;
     }
@@ -593,9 +602,13 @@ __global__ void __launch_bounds__(BLOCK) k_env_step(EnvDev e) {
         }
     }
     if (POLICY) {
-        if (!have) after_reset<OPP>(e, s, h, g, ms, scr, pc);
-        GC_STAMP(6);
-        e.act[i] = pick(s, g, ms, scr, e.seed, i, pc.draw);
+        if (OPP) {
+            if (!have) after_reset<OPP>(e, s, h, g, ms, scr, pc);
+            GC_STAMP(6);
+            e.act[i] = pick(s, g, ms, scr, e.seed, i, pc.draw);
+        } else {
+            e.act[i] = (uint16_t)selfplay_pick(s, pc);
+        }
     }
     if (POLICY || OPP) e.draw[i] = pc.draw;
     h.commit();
@@ -716,12 +729,13 @@ struct PairHalf {
     u32 hl;         // window length after the commit
     u64 ep_from;    // FIDE: own pawns with a legal en-passant capture
     int ep;
+    u64 T[SW_SETS];  // SW: the next side's move sets (W0 holds all of them after phase 2)
 };
 struct PairNoop {
     __device__ void operator()() const {}
 };
 
-template <bool FIDE, bool ACT_LDS, bool MV_LDS = false, class W1Issue, class W1Late>
+template <bool FIDE, bool ACT_LDS, bool MV_LDS = false, bool SW = false, class W1Issue, class W1Late>
 __device__ __forceinline__ void pair_half(PairLds& L, int role, int l, bool mv, bool regen, const Pos& s, int a,
                                           const u32* act_lds, const u32* mv_lds, DevHist& h, PairHalf& H,
                                           W1Issue&& w1_issue, W1Late&& w1_late) {
@@ -875,11 +889,28 @@ __device__ __forceinline__ void pair_half(PairLds& L, int role, int l, bool mv, 
                     part = gen_moves_a<PairScratch, true>(ns, g, ms, scr, FideExtra{ep_from, ep}) + popc(g.castles);
                 }
             }
+        } else if constexpr (SW) {  // pawn, knight and king sets; castles counted here
+            if (gen) {
+                sw_pawns(ns, g, H.T);
+                sw_knights(ns, g, H.T);
+                sw_kings(ns, g, H.T);
+                part = sw_popc(H.T, 0, SW_ORTH) + sw_popc(H.T, SW_K, SW_SETS) + popc(g.castles);
+            }
         } else {  // castles counted here (W1 does not know them)
             if (gen) part = ms.big ? count_legal(ns, g) : gen_moves_a(ns, g, ms, scr) + popc(g.castles);
         }
     } else {
-        if (gen && !ms.big) part = FIDE ? gen_moves_b<PairScratch, true>(ns, g, ms, scr) : gen_moves_b(ns, g, ms, scr);
+        if constexpr (SW) {  // the slider direction sets, to W0 through the (unused) slot array
+            if (gen) {
+                sw_orth(ns, g, H.T);
+                sw_diag(ns, g, H.T);
+                part = sw_popc(H.T, SW_ORTH, SW_K);
+#pragma unroll
+                for (int j = 0; j < 8; j++) L.slots[j][l] = H.T[SW_ORTH + j];
+            }
+        } else if (gen && !ms.big) {
+            part = FIDE ? gen_moves_b<PairScratch, true>(ns, g, ms, scr) : gen_moves_b(ns, g, ms, scr);
+        }
         if (mv && !both) {
             // the probe's data is first touched here (an opaque use after the generation:
             // otherwise the compiler hoists the entry compare up to the load and waits there)
@@ -893,16 +924,26 @@ __device__ __forceinline__ void pair_half(PairLds& L, int role, int l, bool mv, 
         L.rep[l] = (u32)c | (hl << 8);
         w1_late();
     }
+    if constexpr (!SW) {
 #pragma unroll
-    for (int b = 0; b < 5; b++) L.planes[role][b][l] = ms.cnt[b];
+        for (int b = 0; b < 5; b++) L.planes[role][b][l] = ms.cnt[b];
+    }
     L.part[role][l] = (u32)part;
     GC_STAMP(4);
     pair_barrier();
     GC_STAMP(5);
 
-    // ---- phase 3 opens: both waves merge the count planes, W0 takes the 3-fold verdict
+    // ---- phase 3 opens: both waves merge the count planes (SW: W0 takes W1's slider sets), W0
+    // takes the 3-fold verdict
+    if constexpr (SW) {
+        if (role == 0) {
 #pragma unroll
-    for (int b = 0; b < 5; b++) ms.cnt[b] |= L.planes[role ^ 1][b][l];
+            for (int j = 0; j < 8; j++) H.T[SW_ORTH + j] = L.slots[j][l];
+        }
+    } else {
+#pragma unroll
+        for (int b = 0; b < 5; b++) ms.cnt[b] |= L.planes[role ^ 1][b][l];
+    }
     ms.total = part + (int)L.part[role ^ 1][l];  // W0's part holds the castles
     if (role == 0) {
         u32 rpk = L.rep[l];
@@ -941,6 +982,7 @@ template <bool SHARE_ACT, bool FIDE = false>
 __device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, int role, int l, int i,
                                             bool live, const Pos& rp, Pos& s, int& a, u32& d, DevHist& h,
                                             u32& nst) {
+    constexpr bool SW = !FIDE;  // reference rules: the self-play policy's move-set order (gc_core.h sw_*)
     PairScratch scr{&L.slots[0][l]};
     const bool none = a == A_NONE;                           // empty list: driver reset
     const bool done0 = (s.meta & M_DONE) != 0;               // chess_v2.py:245-251
@@ -953,7 +995,7 @@ __device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, int ro
     // W1, phase 0: the Philox word of the next draw and, for a board that resets this ply,
     // its pick from the start position's table (a serial multiply chain and a load, hidden
     // behind W0's move; the table read lands long before phase 3)
-    pair_half<FIDE, false>(
+    pair_half<FIDE, false, false, SW>(
         L, role, l, mv, false, s, a, nullptr, nullptr, h, H,
         [&] {
             x0 = philox_x0(C.seed, (u32)i, d);  // the next draw (independent of the position)
@@ -1012,7 +1054,10 @@ __device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, int ro
         } else {
             bool walk = false;  // FIDE, > SCRATCH_SLOTS own pieces: the per-square walk
             gcf::FGen f;
-            if (!have) {
+            if (!have && SW) {  // the start position without a table: generated
+                gen_init(s, g);
+                ms.total = sw_gen(s, g, H.T);
+            } else if (!have) {
                 const EnvDev::InitCache& ic = *C.icd;
                 if (ic.usable) {
                     g.white = ic.white; g.own = ic.own; g.castles = ic.castles;
@@ -1045,7 +1090,7 @@ __device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, int ro
 #ifdef GC_STAMP_PICK  // diagnostic: stamps 2 / 3 around the rank search (phase-1 stamps dropped)
                 GC_STAMP(2);
 #endif
-                act = (uint16_t)(walk ? gcf::fselect(s, f, k) : select_action_swar(s, g, ms, scr, k));
+                act = (uint16_t)(SW ? sw_select(g, H.T, k) : walk ? gcf::fselect(s, f, k) : select_action_swar(s, g, ms, scr, k));
 #ifdef GC_STAMP_PICK
                 asm volatile("" ::"v"(act));
                 GC_STAMP(3);
@@ -1452,7 +1497,7 @@ __global__ void __launch_bounds__(BLOCK) k_env_rollout(EnvDev e, int plies, int1
                 have = false;
             }
         }
-        if (!have) after_reset<OPP>(e, s, h, g, ms, scr, pc);
+        if (OPP && !have) after_reset<OPP>(e, s, h, g, ms, scr, pc);
         if (tr_action) {
             size_t t = (size_t)p * e.n + i;
             tr_action[t] = (int16_t)played;
@@ -1460,7 +1505,7 @@ __global__ void __launch_bounds__(BLOCK) k_env_rollout(EnvDev e, int plies, int1
             tr_done[t] = (uint8_t)o.done;
             tr_reason[t] = (uint8_t)o.reason;
         }
-        a = pick(s, g, ms, scr, e.seed, i, pc.draw);
+        a = OPP ? pick(s, g, ms, scr, e.seed, i, pc.draw) : selfplay_pick(s, pc);
         h.commit();
     }
     e.reward[i] = o.reward;  // the last ply's env.step() outputs (per-ply: trace buffers)
@@ -1796,13 +1841,17 @@ __global__ void __launch_bounds__(BLOCK) k_select(EnvDev e) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= e.n) return;
     Pos s = e.st.load(i);
-    Gen g;
-    MoveSet ms;
-    gen_init(s, g);
-    gen_moves(s, g, ms, scr);
-    u32 d = e.draw[i];
-    e.act[i] = pick(s, g, ms, scr, e.seed, i, d);
-    e.draw[i] = d;
+    PolicyCtx pc = {e.seed, (u32)i, e.draw[i]};
+    if (e.opp) {
+        Gen g;
+        MoveSet ms;
+        gen_init(s, g);
+        gen_moves(s, g, ms, scr);
+        e.act[i] = pick(s, g, ms, scr, e.seed, i, pc.draw);
+    } else {
+        e.act[i] = (uint16_t)selfplay_pick(s, pc);
+    }
+    e.draw[i] = pc.draw;
 }
 
 #include "gc_fide_kernels.h"
@@ -2322,6 +2371,10 @@ static ResetInfo reset_info(const gc_env* e) {
 // The paired kernels serve opponent "none" (both rules) and the random opponent when the
 // start position's picks come from its table and, for a BLACK agent, no opening can end in
 // both kings checked (pair_step_vs); otherwise the one-wave kernels run.
+// the reset picks of the self-play policy (reference rules): the move-set order table
+static const uint16_t* sw_table(const ResetInfo& r) {
+    return r.racts ? r.racts + RESET_ACTS_MAX : r.racts;
+}
 static bool pair_ok(const gc_env* e) {
     if (!e->d.opp) return true;
     const EnvDev::InitCache& ic = e->d.ic;
@@ -2339,7 +2392,7 @@ static void launch_step2(gc_env* e, hipStream_t st, int b0 = 0, int nb = -1) {
     const dim3 grid((nb + PAIRS_WG - 1) / PAIRS_WG), block(2 * per_wg);
     switch (e->rules ? 3 : pair_opp(e)) {
         case 3: k_env_step2<true><<<grid, block, 0, st>>>(e->slab, d.n, b0, d.seed, d.htab, r.racts, r.icd, r.rinfo); break;
-        case 0: k_env_step2<false><<<grid, block, 0, st>>>(e->slab, d.n, b0, d.seed, d.htab, r.racts, r.icd, r.rinfo); break;
+        case 0: k_env_step2<false><<<grid, block, 0, st>>>(e->slab, d.n, b0, d.seed, d.htab, sw_table(r), r.icd, r.rinfo); break;
         case 1: k_env_step2<false, 1><<<grid, block, 0, st>>>(e->slab, d.n, b0, d.seed, d.htab, r.racts, r.icd, r.rinfo); break;
         default: k_env_step2<false, 2><<<grid, block, 0, st>>>(e->slab, d.n, b0, d.seed, d.htab, r.racts, r.icd, r.rinfo); break;
     }
@@ -2410,7 +2463,7 @@ extern "C" int gc_env_create(int device, int n_boards, uint64_t seed, const int8
     {  // the start position's move set, shared by every reset (EnvDev::ic)
         EnvDev::InitCache* dic = nullptr;
         uint16_t* dacts = nullptr;
-        if (dalloc(&dic, 1) || dalloc(&dacts, RESET_ACTS_MAX)) {
+        if (dalloc(&dic, 1) || dalloc(&dacts, 2 * RESET_ACTS_MAX)) {
             std::string m = g_err; (void)hipFree(dic); env_free(e); delete e; return fail(m);
         }
         e->reset_acts = dacts;
@@ -2717,7 +2770,7 @@ extern "C" int gc_env_rollout(gc_env* e, int n_plies, int16_t* tr_action, int16_
         const int grid = (e->n + PAIR_BOARDS * PAIRS_WG - 1) / (PAIR_BOARDS * PAIRS_WG), bs = 2 * PAIR_BOARDS * PAIRS_WG;
         switch (e->rules ? 3 : pair_opp(e)) {
             case 3: k_env_rollout2<true><<<grid, bs, 0, e->stream>>>(e->slab, d.n, 0, d.seed, d.htab, r.racts, r.icd, r.rinfo, n_plies, e->stats); break;
-            case 0: k_env_rollout2<false><<<grid, bs, 0, e->stream>>>(e->slab, d.n, 0, d.seed, d.htab, r.racts, r.icd, r.rinfo, n_plies, e->stats); break;
+            case 0: k_env_rollout2<false><<<grid, bs, 0, e->stream>>>(e->slab, d.n, 0, d.seed, d.htab, sw_table(r), r.icd, r.rinfo, n_plies, e->stats); break;
             case 1: k_env_rollout2<false, 1><<<grid, bs, 0, e->stream>>>(e->slab, d.n, 0, d.seed, d.htab, r.racts, r.icd, r.rinfo, n_plies, e->stats); break;
             default: k_env_rollout2<false, 2><<<grid, bs, 0, e->stream>>>(e->slab, d.n, 0, d.seed, d.htab, r.racts, r.icd, r.rinfo, n_plies, e->stats); break;
         }

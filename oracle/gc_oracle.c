@@ -426,6 +426,7 @@ typedef struct {
     /* opponent (chess_v2.py:167-181): 0 none, 1 random = the Philox policy below, drawing
      * from the same per-board stream (seed, board, draw++) as the self-play driver */
     int opp, agent_black;
+    int set_order;  /* the policy's order: 1 move-set order (self-play), 0 action-id order */
     uint64_t seed;
     uint32_t board, draw;
     /* distinct pre-move boards of reversible moves since the last pawn move / capture: the
@@ -460,9 +461,13 @@ static void env_engine_state(const OEnv *e, OState *s) {
     o_state_new(s, e->st.b, e->st.player, e->st.wkc, e->st.wqc, e->st.bkc, e->st.bqc);
 }
 
-/* the random opponent's pick: uniform rank over the legal list, k-th in action-id order */
+static int kth_in_set_order(const int8_t *b, const uint16_t *moves, int n, int k);
+
+/* the random policy's pick: uniform rank over the legal list; the k-th legal action in
+ * action-id order for the opponent modes, in move-set order for self-play (opponent "none") */
 static int env_policy_pick(OEnv *e) {
     uint32_t k = oracle_policy_index(e->seed, e->board, e->draw++, (uint32_t)e->nmoves);
+    if (e->set_order) return kth_in_set_order(e->st.b, e->moves, e->nmoves, (int)k);
     return kth_in_action_order(e->moves, e->nmoves, (int)k);
 }
 
@@ -595,6 +600,45 @@ static int kth_in_action_order(const uint16_t *moves, int n, int k) {
     return tmp[k];
 }
 
+/* The self-play policy's order (the device's gc_core.h sw_gen / sw_select, restated from the
+ * move's geometry): a legal move belongs to one of 28 sets -- pawn single push, double push,
+ * capture toward col+1, toward col-1; the eight knight jumps; rooks / queens by direction
+ * (row-1, row+1, col+1, col-1); bishops / queens by direction (row-1 col+1, row-1 col-1,
+ * row+1 col+1, row+1 col-1); the eight king steps -- ordered by set, then by target square;
+ * castles last, queen side first.  Any fixed bijection gives the same uniform policy; this
+ * is the one the device enumerates without a per-piece loop. */
+static int sgn(int x) { return (x > 0) - (x < 0); }
+static int set_key(const int8_t *b, int a) {
+    static const int8_t kn[8][2] = {{2, -1}, {2, 1}, {-2, -1}, {-2, 1}, {1, -2}, {1, 2}, {-1, -2}, {-1, 2}};
+    static const int8_t kg[8][2] = {{-1, 0}, {1, 0}, {0, -1}, {0, 1}, {-1, -1}, {-1, 1}, {1, -1}, {1, 1}};
+    static const int8_t sl[8][2] = {{-1, 0}, {1, 0}, {0, 1}, {0, -1}, {-1, 1}, {-1, -1}, {1, 1}, {1, -1}};
+    if (a >= 4096) return 28 * 64 + ((a == 4097 || a == 4099) ? 0 : 1);  /* QS (4097 / 4099), KS */
+    int f = a >> 6, t = a & 63, dr = (t >> 3) - (f >> 3), dc = (t & 7) - (f & 7);
+    int ty = b[f] < 0 ? -b[f] : b[f], set = -1;
+    if (ty == PAWN) {
+        set = dc == 0 ? ((dr == 1 || dr == -1) ? 0 : 1) : (dc > 0 ? 2 : 3);
+    } else if (ty == KNIGHT) {
+        for (int i = 0; i < 8; i++) if (kn[i][0] == dr && kn[i][1] == dc) set = 4 + i;
+    } else if (ty == KING) {
+        for (int i = 0; i < 8; i++) if (kg[i][0] == dr && kg[i][1] == dc) set = 20 + i;
+    } else {  /* Q, R, B: the direction of the ray */
+        for (int i = 0; i < 8; i++) if (sl[i][0] == sgn(dr) && sl[i][1] == sgn(dc)) set = 12 + i;
+    }
+    return set * 64 + t;
+}
+static int kth_in_set_order(const int8_t *b, const uint16_t *moves, int n, int k) {
+    uint16_t tmp[MAXMOVES];
+    int key[MAXMOVES];
+    for (int i = 0; i < n; i++) {  /* insertion sort by key: lists are short */
+        uint16_t v = moves[i];
+        int kv = set_key(b, v), j = i;
+        while (j > 0 && key[j - 1] > kv) { tmp[j] = tmp[j - 1]; key[j] = key[j - 1]; j--; }
+        tmp[j] = v;
+        key[j] = kv;
+    }
+    return tmp[k];
+}
+
 /* Random self-play rollout of one board (the test_benchmark.py driver shape, auto-reset):
  * at each ply: if no legal moves -> episode ends (driver `break`), reset, no step counted;
  * else action = moves[policy_index(...)], step; if done -> reset.
@@ -605,12 +649,13 @@ typedef struct { uint64_t steps, reward_sum, ends[6]; } OStats; /* ends[0] unuse
 static int stats_slot(int reason) { return reason == 8 ? 1 : (reason == 9 ? 4 : (reason == 10 ? 5 : reason)); }
 
 static void rollout_board(const int8_t *init, uint64_t seed, uint32_t board, int plies, int opp, int agent_black,
-                          int16_t *tr_action, int16_t *tr_reward, uint8_t *tr_done, uint8_t *tr_reason,
+                          int order, int16_t *tr_action, int16_t *tr_reward, uint8_t *tr_done, uint8_t *tr_reason,
                           int8_t *final_board, uint8_t *final_meta, uint32_t *final_draw, OStats *st) {
     OEnv e;
     memset(&e, 0, sizeof(e));
     memcpy(e.init, init, 64);
     e.opp = opp; e.agent_black = agent_black; e.seed = seed; e.board = board; e.draw = 0;
+    e.set_order = order < 0 ? !opp : order;
     o_env_reset(&e);
     for (int p = 0; p < plies; p++) {
         int action = -1, rw = 0, dn = 0, reason = 0;
@@ -650,7 +695,7 @@ void oracle_rollout_trace(const int8_t *init, uint64_t seed, uint32_t board, int
     OStats st;
     memset(&st, 0, sizeof(st));
     uint32_t draw;
-    rollout_board(init, seed, board, plies, 0, 0, tr_action, tr_reward, tr_done, tr_reason, final_board, final_meta, &draw, &st);
+    rollout_board(init, seed, board, plies, 0, 0, -1, tr_action, tr_reward, tr_done, tr_reason, final_board, final_meta, &draw, &st);
     if (stats8) { stats8[0] = st.steps; stats8[1] = st.reward_sum; for (int i = 0; i < 6; i++) stats8[2 + i] = st.ends[i]; }
 }
 
@@ -660,7 +705,7 @@ static void *job_run(void *arg) {
     Job *j = (Job *)arg;
     memset(&j->st, 0, sizeof(j->st));
     for (uint32_t b = j->b0; b < j->b1; b++)
-        rollout_board(j->init, j->seed, b, j->plies, j->opp, j->agent_black, NULL, NULL, NULL, NULL, NULL, NULL, NULL, &j->st);
+        rollout_board(j->init, j->seed, b, j->plies, j->opp, j->agent_black, -1, NULL, NULL, NULL, NULL, NULL, NULL, NULL, &j->st);
     return NULL;
 }
 void oracle_rollout_batch2(const int8_t *init, uint64_t seed, uint32_t b_begin, uint32_t n_boards, int plies,
@@ -690,16 +735,24 @@ void oracle_rollout_batch(const int8_t *init, uint64_t seed, uint32_t b_begin, u
     oracle_rollout_batch2(init, seed, b_begin, n_boards, plies, 0, 1, threads, stats8);
 }
 
-/* Trajectory with an opponent mode (0 none, 1 random) and agent colour. */
-void oracle_rollout_trace2(const int8_t *init, uint64_t seed, uint32_t board, int plies, int opp, int agent_white,
-                           int16_t *tr_action, int16_t *tr_reward, uint8_t *tr_done, uint8_t *tr_reason,
+/* Trajectory with an opponent mode (0 none, 1 random) and agent colour; order -1: the mode's
+ * policy order, 0: action-id order (the API step's `pick` output), 1: move-set order. */
+void oracle_rollout_trace3(const int8_t *init, uint64_t seed, uint32_t board, int plies, int opp, int agent_white,
+                           int order, int16_t *tr_action, int16_t *tr_reward, uint8_t *tr_done, uint8_t *tr_reason,
                            int8_t *final_board, uint8_t *final_meta, uint64_t *stats8) {
     OStats st;
     memset(&st, 0, sizeof(st));
     uint32_t draw;
-    rollout_board(init, seed, board, plies, opp, !agent_white, tr_action, tr_reward, tr_done, tr_reason, final_board,
+    rollout_board(init, seed, board, plies, opp, !agent_white, order, tr_action, tr_reward, tr_done, tr_reason, final_board,
                   final_meta, &draw, &st);
     if (stats8) { stats8[0] = st.steps; stats8[1] = st.reward_sum; for (int i = 0; i < 6; i++) stats8[2 + i] = st.ends[i]; }
+}
+
+void oracle_rollout_trace2(const int8_t *init, uint64_t seed, uint32_t board, int plies, int opp, int agent_white,
+                           int16_t *tr_action, int16_t *tr_reward, uint8_t *tr_done, uint8_t *tr_reason,
+                           int8_t *final_board, uint8_t *final_meta, uint64_t *stats8) {
+    oracle_rollout_trace3(init, seed, board, plies, opp, agent_white, -1, tr_action, tr_reward, tr_done, tr_reason,
+                          final_board, final_meta, stats8);
 }
 
 /* Multi-threaded perft over many roots (CPU baseline for perft configs).  Roots are handed
@@ -736,6 +789,7 @@ void *oracle_env_new2(const int8_t *init, int opp, int agent_white, uint64_t see
     OEnv *e = (OEnv *)calloc(1, sizeof(OEnv));
     memcpy(e->init, init, 64);
     e->opp = opp; e->agent_black = !agent_white; e->seed = seed; e->board = board;
+    e->set_order = !opp;
     o_env_reset(e);
     return e;
 }

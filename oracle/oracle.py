@@ -77,6 +77,8 @@ def lib():
         L.oracle_env_draw.restype = u32
         L.oracle_rollout_trace2.argtypes = [P, u64, u32, i32, i32, i32, P, P, P, P, P, P, P]
         L.oracle_rollout_trace2.restype = None
+        L.oracle_rollout_trace3.argtypes = [P, u64, u32, i32, i32, i32, i32, P, P, P, P, P, P, P]
+        L.oracle_rollout_trace3.restype = None
         L.oracle_rollout_batch2.argtypes = [P, u64, u32, u32, i32, i32, i32, i32, P]
         L.oracle_rollout_batch2.restype = None
         L.oracle_env_free.argtypes = [P]
@@ -177,9 +179,12 @@ def policy_index(seed, board, draw, n):
     return int(lib().oracle_policy_index(seed, board, draw, n))
 
 
-def rollout_trace(seed, board_id, plies, init=DEFAULT_BOARD, opponent=0, agent_white=True):
+def rollout_trace(seed, board_id, plies, init=DEFAULT_BOARD, opponent=0, agent_white=True, order=None):
     """Single-board random self-play (test_benchmark.py driver shape, auto-reset); with
     opponent=1 the env answers every step with the random opponent (chess_v2.py:275-288).
+    The policy ranks the legal moves in move-set order for self-play and in action-id order
+    with an opponent; order="action" / "set" forces one (the API step's `pick` output is in
+    action-id order: the order of its legal-action mask).
     Returns dict of per-ply arrays + final state + stats."""
     init = np.ascontiguousarray(init, dtype=np.int8).reshape(64)
     a = np.zeros(plies, dtype=np.int16)
@@ -189,8 +194,9 @@ def rollout_trace(seed, board_id, plies, init=DEFAULT_BOARD, opponent=0, agent_w
     fb = np.zeros(64, dtype=np.int8)
     fm = np.zeros(8, dtype=np.uint8)
     st = np.zeros(8, dtype=np.uint64)
-    lib().oracle_rollout_trace2(_p(init), seed, board_id, plies, int(opponent), int(bool(agent_white)), _p(a), _p(r),
-                                _p(d), _p(why), _p(fb), _p(fm), _p(st))
+    o = {None: -1, "action": 0, "set": 1}[order]
+    lib().oracle_rollout_trace3(_p(init), seed, board_id, plies, int(opponent), int(bool(agent_white)), o, _p(a),
+                                _p(r), _p(d), _p(why), _p(fb), _p(fm), _p(st))
     return dict(action=a, reward=r, done=d, reason=why, final_board=fb, final_meta=fm, stats=st)
 
 

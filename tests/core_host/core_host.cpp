@@ -127,6 +127,24 @@ extern "C" int host_count_moves_agree(const int8_t* b, const uint8_t* m, int whi
     int c = count_moves(s, g);
     return (c == ms.total && c == count_legal(s, g) && c == count_position(s)) ? c : -1 - ms.total;
 }
+// set-wise generation (the self-play policy's move-set order): the count == gen_moves' total,
+// and sw_select over every rank yields each legal action exactly once.  Returns the count, or
+// -1 - the first rank whose action is wrong (or -1000 - total on a count mismatch)
+extern "C" int host_sw_agree(const int8_t* b, const uint8_t* m, int white) {
+    Pos s = import_state(b, m, white);
+    Gen g;
+    gen_init(s, g);
+    u64 t[SW_SETS];
+    const int n = sw_gen(s, g, t);
+    if (n != count_legal(s, g)) return -1000 - n;
+    std::vector<char> seen(4101, 0);
+    for (int k = 0; k < n; k++) {
+        const int a = sw_select(g, t, k);
+        if (a < 0 || a > A_RESIGN || seen[a] || !action_legal(s, g, a)) return -1 - k;
+        seen[a] = 1;
+    }
+    return n;
+}
 // quick_legal (the paired API step's validation) == action_legal over gen_init, for every
 // action id: returns the number of legal actions, or -1 - the first action that differs
 extern "C" int host_quick_legal_agree(const int8_t* b, const uint8_t* m, int white) {
@@ -262,7 +280,8 @@ struct HostEnv {
         regen();
         if (opp && agent_black) env_open_vs(s, h, g, ms, scr, pc);
     }
-    int pick() {
+    int pick() {  // self-play: the move-set order (selfplay_pick); the opponent modes: action-id order
+        if (!opp) return selfplay_pick(s, pc);
         return ms.total ? select_action(s, g, ms, scr, (int)policy_index(pc.seed, pc.board, pc.draw++, (u32)ms.total))
                         : A_NONE;
     }

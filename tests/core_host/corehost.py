@@ -26,6 +26,7 @@ def lib():
         L.host_count_moves_agree.argtypes = [P, P, ctypes.c_int]
         L.host_quick_legal_agree.argtypes = [P, P, ctypes.c_int]
         L.host_pick_agree.argtypes = [P, P, ctypes.c_int]
+        L.host_sw_agree.argtypes = [P, P, ctypes.c_int]
         L.host_rook_att.restype = ctypes.c_uint64
         L.host_rook_att.argtypes = [ctypes.c_int, ctypes.c_uint64]
         L.host_bishop_att.restype = ctypes.c_uint64

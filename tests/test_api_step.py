@@ -50,15 +50,19 @@ def test_step_device_equals_host_step(oracle, opponent):
 
 
 def test_step_device_autoreset_pick_loop_vs_oracle(oracle):
-    """actions = the previous call's pick, auto-reset on: the random self-play driver, ply
-    by ply == the oracle's, on every board until it first meets a position with no legal
-    move (there the driver resets without a step, while step() reports an invalid action)."""
+    """actions = the previous call's pick, auto-reset on: the random self-play driver with the
+    pick in the mask's (action-id) order, ply by ply == the oracle's, on every board until it
+    first meets a position with no legal move (there the driver resets without a step, while
+    step() reports an invalid action)."""
     from gym_chess_amd.env import BatchedChessEnv
 
     n, plies, seed = 256, 400, 2718
     env = BatchedChessEnv(n, device=0, seed=seed)
     io = env.device_io()
-    refs = [oracle.rollout_trace(seed, i, plies + 1) for i in range(n)]
+    refs = [oracle.rollout_trace(seed, i, plies + 1, order="action") for i in range(n)]
+    # the env's own first picks are the self-play policy's (move-set order): start the loop
+    # from the action-id-order ones
+    io.upload_actions(np.array([r["action"][0] for r in refs], dtype=np.uint16))
     live = np.ones(n, dtype=bool)
     checked = 0
     for p in range(plies):

@@ -200,6 +200,25 @@ def test_count_moves_agrees(seed):
     assert seen > 0
 
 
+@pytest.mark.parametrize("seed", [16, 17])
+def test_setwise_generation_agrees(seed):
+    """Set-wise generation (sw_gen: pawn / knight / king / slider-direction target sets, the
+    self-play policy's move-set order): its count == count_legal, and sw_select over every
+    rank yields each legal action exactly once, on fuzz positions (several / no kings, pins,
+    checks, > 16 pieces), both sides to move."""
+    from conftest import random_positions
+
+    boards, metas = random_positions(3000, seed)
+    L = H.lib()
+    seen = 0
+    for i in range(len(boards)):
+        for white in (0, 1):
+            c = L.host_sw_agree(boards[i].ctypes.data, metas[i].ctypes.data, white)
+            assert c >= 0, (i, white, c)
+            seen += c
+    assert seen > 0
+
+
 @pytest.mark.parametrize("seed", [14, 15])
 def test_swar_pick_agrees(seed):
     """select_action_swar (byte-wise prefix sums of the count planes) == select_action (the
