@@ -1123,8 +1123,8 @@ GC_HD int sw_gen(const Pos& s, const Gen& g, u64* t) {
     return sw_popc(t, 0, SW_SETS) + popc(g.castles);
 }
 // origin of target `to` of set j.  Leapers: origin = to + a signed byte of four packed words
-// (pawn offsets by colour); sliders: the first occupied square behind the target along the
-// set's direction (one line attack from the target), branch-free for every lane.
+// (pawn offsets by colour); sliders: the nearest occupied square behind the target on the
+// set's line (the squares between are empty: the ray came through them), branch-free.
 GC_HD int sw_origin(const Gen& g, int j, int to) {
     const u64 w0 = g.white ? pack8(8, 16, 7, 9, -15, -17, 17, 15) : pack8(-8, -16, -9, -7, -15, -17, 17, 15);
     const u64 w1 = pack8(-6, -10, 10, 6, 0, 0, 0, 0), w2 = pack8(0, 0, 0, 0, 8, -8, 1, -1);
@@ -1136,9 +1136,9 @@ GC_HD int sw_origin(const Gen& g, int j, int to) {
     const int d = (j - SW_ORTH) & 7;
     const bool up = ((0xC6u >> d) & 1) != 0;
     const u64 line = d < 2 ? file_mask(to) : d < 4 ? row_mask(to) : (d == 5 || d == 6) ? diag_mask(to) : anti_mask(to);
-    const u64 att = line_att(g.occ, line, line_neg(to));
-    const u64 lo = att & below(to), hi = att & ~below(to);
-    const int sl = up ? (lo ? ctz(lo) : 0) : (hi ? msb(hi) : 0);  // the ray's far end: its first blocker
+    const u64 x = g.occ & line;
+    const u64 lo = x & below(to), hi = x & (~below(to) ^ bit(to));
+    const int sl = up ? (lo ? msb(lo) : 0) : (hi ? ctz(hi) : 0);
     const bool slider = j >= SW_ORTH && j < SW_K;
     return slider ? sl : to + off;
 }
@@ -1159,6 +1159,44 @@ GC_HD int sw_select(const Gen& g, const u64* t, int k) {
     }
     const int to = kth_set_bit(tj, k);
     return sw_origin(g, j, to) * 64 + to;
+}
+
+// The same pick in two steps for the paired step kernel, whose sets sit in LDS: the sets'
+// counts packed one byte per set into four words (set i in byte i % 8 of word i / 8), their
+// prefix sums by three shift-adds per word, the set holding rank k by a word step and a byte
+// step (no scan over 28 sets); then the caller fetches that one set and sw_finish turns the
+// rank within it into the action.  Byte sums need < 256 moves (more: sw_select).
+GC_HD void sw_pack(const u64* t, int lo, int hi, u64* cw) {
+    for (int i = lo; i < hi; i++) cw[i >> 3] |= (u64)popc(t[i]) << (8 * (i & 7));
+}
+GC_HD u64 byte_prefix(u64 w) {  // inclusive prefix sums of the 8 bytes (no byte overflows)
+    w += w << 8;
+    w += w << 16;
+    return w + (w << 32);
+}
+// rank k (< the sets' total) -> set index j and the rank within set j, with short dependency
+// chains (it is the paired step's tail): the word from three independent compares against the
+// running word totals; the byte as 8 - the number of byte prefixes > k, counted by a borrow-free
+// compare of the bytes spread over 16-bit lanes.
+GC_HD int sw_locate(const u64* cw, int& k) {
+    const u64 p0 = byte_prefix(cw[0]), p1 = byte_prefix(cw[1]), p2 = byte_prefix(cw[2]), p3 = byte_prefix(cw[3]);
+    const int c1 = (int)(p0 >> 56), c2 = c1 + (int)(p1 >> 56), c3 = c2 + (int)(p2 >> 56);
+    const int w = (k >= c1) + (k >= c2) + (k >= c3);
+    const u64 p = w == 0 ? p0 : w == 1 ? p1 : w == 2 ? p2 : p3;
+    k -= w == 0 ? 0 : w == 1 ? c1 : w == 2 ? c2 : c3;
+    const u64 H = 0x8000800080008000ull, K = (u64)(k + 1) * 0x0001000100010001ull, M = 0x00FF00FF00FF00FFull;
+    const int above = popc((((p & M) | H) - K) & H) + popc(((((p >> 8) & M) | H) - K) & H);
+    const int b = 8 - above;  // bytes with prefix <= k: the set is the next one
+    k -= b ? (int)((p >> (8 * b - 8)) & 0xFF) : 0;
+    return 8 * w + b;
+}
+GC_HD int sw_finish(const Gen& g, int j, u64 tj, int k) {
+    const int to = kth_set_bit(tj, k);
+    return sw_origin(g, j, to) * 64 + to;
+}
+GC_HD int sw_castle(const Gen& g, int k) {  // k: the rank among the castles
+    if ((g.castles & 1) && k == 0) return g.white ? A_QSW : A_QSB;
+    return g.white ? A_KSW : A_KSB;
 }
 
 // k-th legal action (0 <= k < ms.total) in reference order, from gen_moves' results

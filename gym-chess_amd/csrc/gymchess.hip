@@ -658,12 +658,18 @@ __global__ void __launch_bounds__(BLOCK) k_env_step(EnvDev e) {
 #define PAIRS_WG 2  // board pairs (64 boards, two waves) per workgroup: 1 -> 9.8 us per ply, 2 -> 9.3, 4 -> 10.6
 #endif
 struct PairLds {
-    u64 slots[SCRATCH_SLOTS][PAIR_BOARDS];  // parked targets (both waves write, W0 reads)
+    union {
+        struct {
+            u64 slots[SCRATCH_SLOTS][PAIR_BOARDS];  // parked targets (both waves write, W0 reads)
+            u64 planes[2][5][PAIR_BOARDS];          // partial bit-sliced counts per wave
+        };
+        u64 sets[SW_SETS][PAIR_BOARDS];  // SW: the next side's move sets (both waves write, W0 reads one)
+    };
+    u64 swc[2][PAIR_BOARDS];                // SW, W1 -> W0: its sets' byte counts (words 1 and 2)
     u64 pin3[3][PAIR_BOARDS];               // W0 -> W1: checkmask, pinned, pinrays
     u64 enemy[PAIR_BOARDS];                 // W1 -> W0: enemy leaper + orthogonal attacks
     u32 f0[PAIR_BOARDS];                    // W0 -> W1: in_check
     u32 f1[PAIR_BOARDS];                    // W1 -> W0: my_chk
-    u64 planes[2][5][PAIR_BOARDS];          // partial bit-sliced counts per wave
     u32 part[2][PAIR_BOARDS];               // partial move totals per wave
     u32 rep[PAIR_BOARDS];                   // W1 -> W0: 3-fold count c | window length << 8
     u32 act[PAIR_BOARDS];                   // W0 -> W1: the next action (fused rollout)
@@ -729,7 +735,8 @@ struct PairHalf {
     u32 hl;         // window length after the commit
     u64 ep_from;    // FIDE: own pawns with a legal en-passant capture
     int ep;
-    u64 T[SW_SETS];  // SW: the next side's move sets (W0 holds all of them after phase 2)
+    u64 T[SW_SETS];  // SW: the next side's move sets (each wave its own; all in LDS after phase 2)
+    u64 cw[4];       // SW, W0: every set's count, one byte per set (gc_core.h sw_pack)
 };
 struct PairNoop {
     __device__ void operator()() const {}
@@ -890,24 +897,35 @@ __device__ __forceinline__ void pair_half(PairLds& L, int role, int l, bool mv, 
                 }
             }
         } else if constexpr (SW) {  // pawn, knight and king sets; castles counted here
+            H.cw[0] = H.cw[1] = H.cw[2] = H.cw[3] = 0;
             if (gen) {
                 sw_pawns(ns, g, H.T);
                 sw_knights(ns, g, H.T);
                 sw_kings(ns, g, H.T);
+                sw_pack(H.T, 0, SW_ORTH, H.cw);
+                sw_pack(H.T, SW_K, SW_SETS, H.cw);
                 part = sw_popc(H.T, 0, SW_ORTH) + sw_popc(H.T, SW_K, SW_SETS) + popc(g.castles);
+#pragma unroll
+                for (int j = 0; j < SW_ORTH; j++) L.sets[j][l] = H.T[j];
+#pragma unroll
+                for (int j = SW_K; j < SW_SETS; j++) L.sets[j][l] = H.T[j];
             }
         } else {  // castles counted here (W1 does not know them)
             if (gen) part = ms.big ? count_legal(ns, g) : gen_moves_a(ns, g, ms, scr) + popc(g.castles);
         }
     } else {
-        if constexpr (SW) {  // the slider direction sets, to W0 through the (unused) slot array
+        if constexpr (SW) {  // the slider direction sets and their byte counts, to W0 through LDS
+            u64 cw[4] = {0, 0, 0, 0};
             if (gen) {
                 sw_orth(ns, g, H.T);
                 sw_diag(ns, g, H.T);
+                sw_pack(H.T, SW_ORTH, SW_K, cw);
                 part = sw_popc(H.T, SW_ORTH, SW_K);
 #pragma unroll
-                for (int j = 0; j < 8; j++) L.slots[j][l] = H.T[SW_ORTH + j];
+                for (int j = SW_ORTH; j < SW_K; j++) L.sets[j][l] = H.T[j];
             }
+            L.swc[0][l] = cw[1];
+            L.swc[1][l] = cw[2];
         } else if (gen && !ms.big) {
             part = FIDE ? gen_moves_b<PairScratch, true>(ns, g, ms, scr) : gen_moves_b(ns, g, ms, scr);
         }
@@ -937,8 +955,8 @@ __device__ __forceinline__ void pair_half(PairLds& L, int role, int l, bool mv, 
     // takes the 3-fold verdict
     if constexpr (SW) {
         if (role == 0) {
-#pragma unroll
-            for (int j = 0; j < 8; j++) H.T[SW_ORTH + j] = L.slots[j][l];
+            H.cw[1] |= L.swc[0][l];
+            H.cw[2] |= L.swc[1][l];
         }
     } else {
 #pragma unroll
@@ -1054,9 +1072,11 @@ __device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, int ro
         } else {
             bool walk = false;  // FIDE, > SCRATCH_SLOTS own pieces: the per-square walk
             gcf::FGen f;
+            bool regs = false;  // SW: the sets in registers (generated here), else in LDS
             if (!have && SW) {  // the start position without a table: generated
                 gen_init(s, g);
                 ms.total = sw_gen(s, g, H.T);
+                regs = true;
             } else if (!have) {
                 const EnvDev::InitCache& ic = *C.icd;
                 if (ic.usable) {
@@ -1090,7 +1110,33 @@ __device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, int ro
 #ifdef GC_STAMP_PICK  // diagnostic: stamps 2 / 3 around the rank search (phase-1 stamps dropped)
                 GC_STAMP(2);
 #endif
-                act = (uint16_t)(SW ? sw_select(g, H.T, k) : walk ? gcf::fselect(s, f, k) : select_action_swar(s, g, ms, scr, k));
+                if constexpr (SW) {
+                    if (regs) {  // sets generated here: into LDS and counted like the others (rare)
+                        H.cw[0] = H.cw[1] = H.cw[2] = H.cw[3] = 0;
+                        sw_pack(H.T, 0, SW_SETS, H.cw);
+#pragma unroll
+                        for (int j = 0; j < SW_SETS; j++) L.sets[j][l] = H.T[j];
+                    }
+                    // the set holding rank k by the byte counts, then that one set from LDS; more
+                    // moves than byte sums hold (never in play) take a rolled scan over LDS
+                    const int normal = tot - popc(g.castles);
+                    int r = k, j;
+                    if (tot < 256) {
+                        j = sw_locate(H.cw, r);
+                    } else {
+#pragma unroll 1
+                        for (j = 0; j < SW_SETS - 1; j++) {
+                            const int c = popc(L.sets[j][l]);
+                            if (r < c) break;
+                            r -= c;
+                        }
+                    }
+                    j = j < SW_SETS ? j : SW_SETS - 1;  // a castle's rank runs past the sets
+                    const int ms_act = sw_finish(g, j, L.sets[j][l], r);
+                    act = (uint16_t)(k >= normal ? sw_castle(g, k - normal) : ms_act);
+                } else {
+                    act = (uint16_t)(walk ? gcf::fselect(s, f, k) : select_action_swar(s, g, ms, scr, k));
+                }
 #ifdef GC_STAMP_PICK
                 asm volatile("" ::"v"(act));
                 GC_STAMP(3);

@@ -138,10 +138,23 @@ extern "C" int host_sw_agree(const int8_t* b, const uint8_t* m, int white) {
     const int n = sw_gen(s, g, t);
     if (n != count_legal(s, g)) return -1000 - n;
     std::vector<char> seen(4101, 0);
+    u64 cw[4] = {0, 0, 0, 0};
+    sw_pack(t, 0, SW_SETS, cw);
+    const int normal = n - popc(g.castles);
     for (int k = 0; k < n; k++) {
         const int a = sw_select(g, t, k);
         if (a < 0 || a > A_RESIGN || seen[a] || !action_legal(s, g, a)) return -1 - k;
         seen[a] = 1;
+        if (n < 256) {  // the two-step form of the paired kernel
+            int r = k, b;
+            if (k < normal) {
+                const int j = sw_locate(cw, r);
+                b = sw_finish(g, j, t[j], r);
+            } else {
+                b = sw_castle(g, k - normal);
+            }
+            if (b != a) return -1 - k;
+        }
     }
     return n;
 }
