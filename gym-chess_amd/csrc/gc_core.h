@@ -812,6 +812,105 @@ GC_HD void gen_moves(const Pos& s, const Gen& g, MoveSet& ms, S& scr) {
     ms.total = total;
 }
 
+// ---- set-wise generation in move-set order (the random self-play policy) ------------------
+// Every legal move lies in exactly one of SW_SETS target bitboards, and the set fixes the way
+// back from a target to its origin:
+//   0-3   pawns: single push, double push (Q1), capture toward col+1, capture toward col-1
+//   4-11  the eight knight jumps
+//   12-15 rooks and queens, one bitboard per direction (row-1, row+1, col+1, col-1); 16-19
+//         bishops and queens (row-1 col+1, row-1 col-1, row+1 col+1, row+1 col-1).  Within one
+//         direction the rays of two sliders never overlap (the rear one's ray ends on the front
+//         one), so a target has one origin: the first piece behind it in that direction
+//   20-27 the eight king steps, filtered by the pre-move enemy map (lib.rs:613-619), for every
+//         own king (boards with several kings: Q7)
+// then the castles (queen side, king side).  A pinned piece joins only the sets of the
+// directions along its pin line: a pinned slider's ray there ends at its king and at the
+// pinner; a pinned pawn's targets are cut to its pin segment (a Q1 double push can jump the
+// pinner); a pinned knight never moves.  The same legal moves as gen_moves (host test on fuzz
+// positions); no per-piece loop, no parking, any number of pieces.  The policy's rank k is the
+// k-th move in this order: sets by index, targets ascending within a set.
+enum { SW_P1 = 0, SW_P2 = 1, SW_PL = 2, SW_PR = 3, SW_N = 4, SW_ORTH = 12, SW_DIAG = 16, SW_K = 20, SW_SETS = 28 };
+struct MoveSets {
+    u64 t[SW_SETS];
+};
+GC_HD int sw_popc(const u64* t, int lo, int hi) {
+    int n = 0;
+    for (int i = lo; i < hi; i++) n += popc(t[i]);
+    return n;
+}
+// a square on the tracked king's lines (0 when there is no king: then nothing is pinned)
+GC_HD int sw_ksq(const Gen& g) { return g.ks < 0 ? 0 : g.ks; }
+GC_HD void sw_pawns(const Pos& s, const Gen& g, u64* t) {
+    const u64 cm = g.checkmask, empty = ~g.occ, opp = g.opp, P = s.p & g.own, pr = g.pinrays;
+    const int kq = sw_ksq(g);
+    const u64 fp = P & ~g.pinned, pp = P & g.pinned;
+    const u64 pf = pp & file_mask(kq), pd = pp & diag_mask(kq), pa = pp & anti_mask(kq);
+    if (g.white) {  // lib.rs:935-958, p = +1: toward row 0
+        t[SW_P1] = ((fp >> 8) | ((pf >> 8) & pr)) & empty & cm;
+        t[SW_P2] = (((fp & ROW6) >> 16) | (((pf & ROW6) >> 16) & pr)) & empty & cm;
+        t[SW_PL] = (((fp >> 7) | ((pa >> 7) & pr)) & ~FILE_A) & opp & cm;  // row-1 col+1: anti-diagonal
+        t[SW_PR] = (((fp >> 9) | ((pd >> 9) & pr)) & ~FILE_H) & opp & cm;  // row-1 col-1: diagonal
+    } else {
+        t[SW_P1] = ((fp << 8) | ((pf << 8) & pr)) & empty & cm;
+        t[SW_P2] = (((fp & ROW1) << 16) | (((pf & ROW1) << 16) & pr)) & empty & cm;
+        t[SW_PL] = (((fp << 9) | ((pd << 9) & pr)) & ~FILE_A) & opp & cm;  // row+1 col+1: diagonal
+        t[SW_PR] = (((fp << 7) | ((pa << 7) & pr)) & ~FILE_H) & opp & cm;  // row+1 col-1: anti-diagonal
+    }
+}
+// xm: extra target mask (FIDE: enemy kings are never captured)
+GC_HD void sw_knights(const Pos& s, const Gen& g, u64* t, u64 xm = ~0ull) {
+    const u64 N = s.n & g.own & ~g.pinned, tm = ~g.own & g.checkmask & xm;
+    const u64 l1 = (N >> 1) & ~FILE_H, r1 = (N << 1) & ~FILE_A;
+    const u64 l2 = (N >> 2) & ~(FILE_H | (FILE_H >> 1)), r2 = (N << 2) & ~(FILE_A | (FILE_A << 1));
+    t[SW_N + 0] = (l1 << 16) & tm;  // target = origin + 15
+    t[SW_N + 1] = (r1 << 16) & tm;  // + 17
+    t[SW_N + 2] = (l1 >> 16) & tm;  // - 17
+    t[SW_N + 3] = (r1 >> 16) & tm;  // - 15
+    t[SW_N + 4] = (l2 << 8) & tm;   // + 6
+    t[SW_N + 5] = (r2 << 8) & tm;   // + 10
+    t[SW_N + 6] = (l2 >> 8) & tm;   // - 10
+    t[SW_N + 7] = (r2 >> 8) & tm;   // - 6
+}
+GC_HD void sw_orth(const Pos& s, const Gen& g, u64* t, u64 xm = ~0ull) {
+    const int kq = sw_ksq(g);
+    const u64 S = (s.r | s.q) & g.own, fr = S & ~g.pinned, pp = S & g.pinned;
+    const u64 empty = ~g.occ, tm = ~g.own & g.checkmask & xm;
+    const u64 gf = fr | (pp & file_mask(kq)), gr = fr | (pp & row_mask(kq));
+    t[SW_ORTH + 0] = ray_fill_att<8, false>(gf, empty, ~0ull) & tm;
+    t[SW_ORTH + 1] = ray_fill_att<8, true>(gf, empty, ~0ull) & tm;
+    t[SW_ORTH + 2] = ray_fill_att<1, true>(gr, empty, ~FILE_A) & tm;
+    t[SW_ORTH + 3] = ray_fill_att<1, false>(gr, empty, ~FILE_H) & tm;
+}
+GC_HD void sw_diag(const Pos& s, const Gen& g, u64* t, u64 xm = ~0ull) {
+    const int kq = sw_ksq(g);
+    const u64 S = (s.b | s.q) & g.own, fr = S & ~g.pinned, pp = S & g.pinned;
+    const u64 empty = ~g.occ, tm = ~g.own & g.checkmask & xm;
+    const u64 gd = fr | (pp & diag_mask(kq)), ga = fr | (pp & anti_mask(kq));
+    t[SW_DIAG + 0] = ray_fill_att<7, false>(ga, empty, ~FILE_A) & tm;
+    t[SW_DIAG + 1] = ray_fill_att<9, false>(gd, empty, ~FILE_H) & tm;
+    t[SW_DIAG + 2] = ray_fill_att<9, true>(gd, empty, ~FILE_A) & tm;
+    t[SW_DIAG + 3] = ray_fill_att<7, true>(ga, empty, ~FILE_H) & tm;
+}
+GC_HD void sw_kings(const Pos& s, const Gen& g, u64* t, u64 xm = ~0ull) {
+    const u64 K = s.k & g.own, ok = ~g.own & ~g.enemy_att & xm;
+    t[SW_K + 0] = (K >> 8) & ok;              // target = origin - 8
+    t[SW_K + 1] = (K << 8) & ok;              // + 8
+    t[SW_K + 2] = ((K >> 1) & ~FILE_H) & ok;  // - 1
+    t[SW_K + 3] = ((K << 1) & ~FILE_A) & ok;  // + 1
+    t[SW_K + 4] = ((K >> 9) & ~FILE_H) & ok;  // - 9
+    t[SW_K + 5] = ((K >> 7) & ~FILE_A) & ok;  // - 7
+    t[SW_K + 6] = ((K << 7) & ~FILE_H) & ok;  // + 7
+    t[SW_K + 7] = ((K << 9) & ~FILE_A) & ok;  // + 9
+}
+// all sets of a position whose Gen is complete (gen_init); returns the move count
+GC_HD int sw_gen(const Pos& s, const Gen& g, u64* t) {
+    sw_pawns(s, g, t);
+    sw_knights(s, g, t);
+    sw_orth(s, g, t);
+    sw_diag(s, g, t);
+    sw_kings(s, g, t);
+    return sw_popc(t, 0, SW_SETS) + popc(g.castles);
+}
 // ---- counting only (perft leaves, level expansion) ---------------------------------------
 // gen_moves' total without parking anything, branch-free over the unpinned pieces: sliders
 // of each kind set-wise, one Kogge-Stone fill per direction -- in one direction the rays of
@@ -823,50 +922,53 @@ template <int SH, bool LEFT>
 GC_HD int ray_count(u64 gen, u64 empty, u64 wrap, u64 tmask) {
     return popc(ray_fill_att<SH, LEFT>(gen, empty, wrap) & tmask);
 }
-// pawns, knights, kings and pinned pieces (count_moves without the unpinned sliders)
+// Pinned pieces need no loop either (the set-wise generation below, sw_*): a pinned slider
+// fills only along its pin line -- its ray there ends at its king and at the pinner -- and a
+// pinned pawn moves only along its pin line, cut to the pin segment (Q1); a pinned knight
+// never moves.  So each direction's fill starts from the unpinned sliders plus the pinned ones
+// on the king's line of that direction.
+struct SliderGens {
+    u64 f, r, d, a;  // generators of the file, rank, diagonal and anti-diagonal directions
+};
+GC_HD SliderGens slider_gens(const Pos& s, const Gen& g) {
+    const int kq = g.ks < 0 ? 0 : g.ks;  // no king: nothing is pinned
+    const u64 pin = g.pinned, oRQ = (s.r | s.q) & g.own, oBQ = (s.b | s.q) & g.own;
+    const u64 fRQ = oRQ & ~pin, fBQ = oBQ & ~pin, pRQ = oRQ & pin, pBQ = oBQ & pin;
+    return SliderGens{fRQ | (pRQ & file_mask(kq)), fRQ | (pRQ & row_mask(kq)), fBQ | (pBQ & diag_mask(kq)),
+                      fBQ | (pBQ & anti_mask(kq))};
+}
+// pawns (set-wise, pinned ones included), knights, kings (count_moves without the sliders)
 GC_HD int count_nonsliders(const Pos& s, const Gen& g) {
-    const u64 own = g.own, cm = g.checkmask, tm = ~own & cm, empty = ~g.occ, opp = g.opp;
-    const u64 fr = own & ~g.pinned;
+    const u64 own = g.own, tm = ~own & g.checkmask;
     int total = popc(g.castles);
-    // pawns (lib.rs:935-958; Q1: the double push tests only the destination)
-    const u64 fp = s.p & fr;
-    if (g.white) {
-        total += popc((fp >> 8) & empty & cm) + popc(((fp & ROW6) >> 16) & empty & cm) +
-                 popc(((fp >> 7) & ~FILE_A) & opp & cm) + popc(((fp >> 9) & ~FILE_H) & opp & cm);
-    } else {
-        total += popc((fp << 8) & empty & cm) + popc(((fp & ROW1) << 16) & empty & cm) +
-                 popc(((fp << 9) & ~FILE_A) & opp & cm) + popc(((fp << 7) & ~FILE_H) & opp & cm);
-    }
+    // pawns (lib.rs:935-958; Q1: the double push tests only the destination): sw_pawns' sets
+    u64 pt[4];
+    sw_pawns(s, g, pt);
+    total += popc(pt[0]) + popc(pt[1]) + popc(pt[2]) + popc(pt[3]);
     // knights (a pinned knight never has a move on its pin segment)
-    const u64 N = s.n & fr;
+    const u64 N = s.n & own & ~g.pinned;
     const u64 l1 = (N >> 1) & ~FILE_H, r1 = (N << 1) & ~FILE_A;
     const u64 l2 = (N >> 2) & ~(FILE_H | (FILE_H >> 1)), r2 = (N << 2) & ~(FILE_A | (FILE_A << 1));
     total += popc((l1 << 16) & tm) + popc((r1 << 16) & tm) + popc((l1 >> 16) & tm) + popc((r1 >> 16) & tm) +
              popc((l2 << 8) & tm) + popc((r2 << 8) & tm) + popc((l2 >> 8) & tm) + popc((r2 >> 8) & tm);
-    // kings: filtered by the pre-move enemy map only (lib.rs:613-619)
-    u64 K = s.k & own;
-    while (K) {
-        int sq = ctz(K);
-        K &= K - 1;
-        total += popc(king_set(bit(sq)) & ~own & ~g.enemy_att);
-    }
-    // pinned pawns and sliders
-    u64 pp = own & g.pinned & ~s.n & ~s.k;
-    while (pp) {
-        int sq = ctz(pp);
-        pp &= pp - 1;
-        total += popc(legal_targets(s, g, sq, type_at(s, sq)));
+    // kings: filtered by the pre-move enemy map only (lib.rs:613-619); several kings (Q7
+    // boards, rare) one at a time
+    const u64 K = s.k & own, ok = ~own & ~g.enemy_att;
+    if (K & (K - 1)) {
+        for (u64 x = K; x; x &= x - 1) total += popc(king_set(x & (0 - x)) & ok);
+    } else {
+        total += popc(king_set(K) & ok);
     }
     return total;
 }
 GC_HD int count_moves(const Pos& s, const Gen& g) {
-    const u64 tm = ~g.own & g.checkmask, empty = ~g.occ, fr = g.own & ~g.pinned;
-    const u64 RQ = (s.r | s.q) & fr, BQ = (s.b | s.q) & fr;
+    const u64 tm = ~g.own & g.checkmask, empty = ~g.occ;
+    const SliderGens G = slider_gens(s, g);
     return count_nonsliders(s, g) +
-           ray_count<8, false>(RQ, empty, ~0ull, tm) + ray_count<8, true>(RQ, empty, ~0ull, tm) +
-           ray_count<1, true>(RQ, empty, ~FILE_A, tm) + ray_count<1, false>(RQ, empty, ~FILE_H, tm) +
-           ray_count<7, false>(BQ, empty, ~FILE_A, tm) + ray_count<9, false>(BQ, empty, ~FILE_H, tm) +
-           ray_count<9, true>(BQ, empty, ~FILE_A, tm) + ray_count<7, true>(BQ, empty, ~FILE_H, tm);
+           ray_count<8, false>(G.f, empty, ~0ull, tm) + ray_count<8, true>(G.f, empty, ~0ull, tm) +
+           ray_count<1, true>(G.r, empty, ~FILE_A, tm) + ray_count<1, false>(G.r, empty, ~FILE_H, tm) +
+           ray_count<7, false>(G.a, empty, ~FILE_A, tm) + ray_count<9, false>(G.d, empty, ~FILE_H, tm) +
+           ray_count<9, true>(G.d, empty, ~FILE_A, tm) + ray_count<7, true>(G.a, empty, ~FILE_H, tm);
 }
 
 // gen_init + count_moves of a position with the two Kogge-Stone passes fused: in each
@@ -890,23 +992,23 @@ GC_HD int count_position(const Pos& s) {
     Gen g;
     gen_base(s, g);
     gen_pins(s, g);
-    const u64 empty = ~g.occ, fr = g.own & ~g.pinned, tm = ~g.own & g.checkmask;
+    const u64 empty = ~g.occ, tm = ~g.own & g.checkmask;
     const u64 eRQ = (s.r | s.q) & g.opp, eBQ = (s.b | s.q) & g.opp;
-    const u64 oRQ = (s.r | s.q) & fr, oBQ = (s.b | s.q) & fr;
+    const SliderGens G = slider_gens(s, g);
     u64 att = 0, ae, ao;
     int n = 0;
 #define GC_PAIR(SH, LEFT, GE, GO, WRAP)                  \
     ray_fill_pair<SH, LEFT>(GE, GO, empty, WRAP, ae, ao); \
     att |= ae;                                           \
     n += popc(ao & tm);
-    GC_PAIR(8, false, eRQ, oRQ, ~0ull)
-    GC_PAIR(8, true, eRQ, oRQ, ~0ull)
-    GC_PAIR(1, true, eRQ, oRQ, ~FILE_A)
-    GC_PAIR(1, false, eRQ, oRQ, ~FILE_H)
-    GC_PAIR(7, false, eBQ, oBQ, ~FILE_A)
-    GC_PAIR(9, false, eBQ, oBQ, ~FILE_H)
-    GC_PAIR(9, true, eBQ, oBQ, ~FILE_A)
-    GC_PAIR(7, true, eBQ, oBQ, ~FILE_H)
+    GC_PAIR(8, false, eRQ, G.f, ~0ull)
+    GC_PAIR(8, true, eRQ, G.f, ~0ull)
+    GC_PAIR(1, true, eRQ, G.r, ~FILE_A)
+    GC_PAIR(1, false, eRQ, G.r, ~FILE_H)
+    GC_PAIR(7, false, eBQ, G.a, ~FILE_A)
+    GC_PAIR(9, false, eBQ, G.d, ~FILE_H)
+    GC_PAIR(9, true, eBQ, G.d, ~FILE_A)
+    GC_PAIR(7, true, eBQ, G.a, ~FILE_H)
 #undef GC_PAIR
     if (g.ks >= 0) {  // gen_enemy (no king: no map, no castling)
         g.enemy_att = att | side_attacks_leapers(s, !g.white);
@@ -1024,104 +1126,6 @@ GC_HD int select_action_swar(const Pos& s, const Gen& g, const MoveSet& ms, cons
     return lo * 64 + kth_set_bit(tg, k);
 }
 
-// ---- set-wise generation in move-set order (the random self-play policy) ------------------
-// Every legal move lies in exactly one of SW_SETS target bitboards, and the set fixes the way
-// back from a target to its origin:
-//   0-3   pawns: single push, double push (Q1), capture toward col+1, capture toward col-1
-//   4-11  the eight knight jumps
-//   12-15 rooks and queens, one bitboard per direction (row-1, row+1, col+1, col-1); 16-19
-//         bishops and queens (row-1 col+1, row-1 col-1, row+1 col+1, row+1 col-1).  Within one
-//         direction the rays of two sliders never overlap (the rear one's ray ends on the front
-//         one), so a target has one origin: the first piece behind it in that direction
-//   20-27 the eight king steps, filtered by the pre-move enemy map (lib.rs:613-619), for every
-//         own king (boards with several kings: Q7)
-// then the castles (queen side, king side).  A pinned piece joins only the sets of the
-// directions along its pin line: a pinned slider's ray there ends at its king and at the
-// pinner; a pinned pawn's targets are cut to its pin segment (a Q1 double push can jump the
-// pinner); a pinned knight never moves.  The same legal moves as gen_moves (host test on fuzz
-// positions); no per-piece loop, no parking, any number of pieces.  The policy's rank k is the
-// k-th move in this order: sets by index, targets ascending within a set.
-enum { SW_P1 = 0, SW_P2 = 1, SW_PL = 2, SW_PR = 3, SW_N = 4, SW_ORTH = 12, SW_DIAG = 16, SW_K = 20, SW_SETS = 28 };
-struct MoveSets {
-    u64 t[SW_SETS];
-};
-GC_HD int sw_popc(const u64* t, int lo, int hi) {
-    int n = 0;
-    for (int i = lo; i < hi; i++) n += popc(t[i]);
-    return n;
-}
-// a square on the tracked king's lines (0 when there is no king: then nothing is pinned)
-GC_HD int sw_ksq(const Gen& g) { return g.ks < 0 ? 0 : g.ks; }
-GC_HD void sw_pawns(const Pos& s, const Gen& g, u64* t) {
-    const u64 cm = g.checkmask, empty = ~g.occ, opp = g.opp, P = s.p & g.own, pr = g.pinrays;
-    const int kq = sw_ksq(g);
-    const u64 fp = P & ~g.pinned, pp = P & g.pinned;
-    const u64 pf = pp & file_mask(kq), pd = pp & diag_mask(kq), pa = pp & anti_mask(kq);
-    if (g.white) {  // lib.rs:935-958, p = +1: toward row 0
-        t[SW_P1] = ((fp >> 8) | ((pf >> 8) & pr)) & empty & cm;
-        t[SW_P2] = (((fp & ROW6) >> 16) | (((pf & ROW6) >> 16) & pr)) & empty & cm;
-        t[SW_PL] = (((fp >> 7) | ((pa >> 7) & pr)) & ~FILE_A) & opp & cm;  // row-1 col+1: anti-diagonal
-        t[SW_PR] = (((fp >> 9) | ((pd >> 9) & pr)) & ~FILE_H) & opp & cm;  // row-1 col-1: diagonal
-    } else {
-        t[SW_P1] = ((fp << 8) | ((pf << 8) & pr)) & empty & cm;
-        t[SW_P2] = (((fp & ROW1) << 16) | (((pf & ROW1) << 16) & pr)) & empty & cm;
-        t[SW_PL] = (((fp << 9) | ((pd << 9) & pr)) & ~FILE_A) & opp & cm;  // row+1 col+1: diagonal
-        t[SW_PR] = (((fp << 7) | ((pa << 7) & pr)) & ~FILE_H) & opp & cm;  // row+1 col-1: anti-diagonal
-    }
-}
-GC_HD void sw_knights(const Pos& s, const Gen& g, u64* t) {
-    const u64 N = s.n & g.own & ~g.pinned, tm = ~g.own & g.checkmask;
-    const u64 l1 = (N >> 1) & ~FILE_H, r1 = (N << 1) & ~FILE_A;
-    const u64 l2 = (N >> 2) & ~(FILE_H | (FILE_H >> 1)), r2 = (N << 2) & ~(FILE_A | (FILE_A << 1));
-    t[SW_N + 0] = (l1 << 16) & tm;  // target = origin + 15
-    t[SW_N + 1] = (r1 << 16) & tm;  // + 17
-    t[SW_N + 2] = (l1 >> 16) & tm;  // - 17
-    t[SW_N + 3] = (r1 >> 16) & tm;  // - 15
-    t[SW_N + 4] = (l2 << 8) & tm;   // + 6
-    t[SW_N + 5] = (r2 << 8) & tm;   // + 10
-    t[SW_N + 6] = (l2 >> 8) & tm;   // - 10
-    t[SW_N + 7] = (r2 >> 8) & tm;   // - 6
-}
-GC_HD void sw_orth(const Pos& s, const Gen& g, u64* t) {
-    const int kq = sw_ksq(g);
-    const u64 S = (s.r | s.q) & g.own, fr = S & ~g.pinned, pp = S & g.pinned;
-    const u64 empty = ~g.occ, tm = ~g.own & g.checkmask;
-    const u64 gf = fr | (pp & file_mask(kq)), gr = fr | (pp & row_mask(kq));
-    t[SW_ORTH + 0] = ray_fill_att<8, false>(gf, empty, ~0ull) & tm;
-    t[SW_ORTH + 1] = ray_fill_att<8, true>(gf, empty, ~0ull) & tm;
-    t[SW_ORTH + 2] = ray_fill_att<1, true>(gr, empty, ~FILE_A) & tm;
-    t[SW_ORTH + 3] = ray_fill_att<1, false>(gr, empty, ~FILE_H) & tm;
-}
-GC_HD void sw_diag(const Pos& s, const Gen& g, u64* t) {
-    const int kq = sw_ksq(g);
-    const u64 S = (s.b | s.q) & g.own, fr = S & ~g.pinned, pp = S & g.pinned;
-    const u64 empty = ~g.occ, tm = ~g.own & g.checkmask;
-    const u64 gd = fr | (pp & diag_mask(kq)), ga = fr | (pp & anti_mask(kq));
-    t[SW_DIAG + 0] = ray_fill_att<7, false>(ga, empty, ~FILE_A) & tm;
-    t[SW_DIAG + 1] = ray_fill_att<9, false>(gd, empty, ~FILE_H) & tm;
-    t[SW_DIAG + 2] = ray_fill_att<9, true>(gd, empty, ~FILE_A) & tm;
-    t[SW_DIAG + 3] = ray_fill_att<7, true>(ga, empty, ~FILE_H) & tm;
-}
-GC_HD void sw_kings(const Pos& s, const Gen& g, u64* t) {
-    const u64 K = s.k & g.own, ok = ~g.own & ~g.enemy_att;
-    t[SW_K + 0] = (K >> 8) & ok;              // target = origin - 8
-    t[SW_K + 1] = (K << 8) & ok;              // + 8
-    t[SW_K + 2] = ((K >> 1) & ~FILE_H) & ok;  // - 1
-    t[SW_K + 3] = ((K << 1) & ~FILE_A) & ok;  // + 1
-    t[SW_K + 4] = ((K >> 9) & ~FILE_H) & ok;  // - 9
-    t[SW_K + 5] = ((K >> 7) & ~FILE_A) & ok;  // - 7
-    t[SW_K + 6] = ((K << 7) & ~FILE_H) & ok;  // + 7
-    t[SW_K + 7] = ((K << 9) & ~FILE_A) & ok;  // + 9
-}
-// all sets of a position whose Gen is complete (gen_init); returns the move count
-GC_HD int sw_gen(const Pos& s, const Gen& g, u64* t) {
-    sw_pawns(s, g, t);
-    sw_knights(s, g, t);
-    sw_orth(s, g, t);
-    sw_diag(s, g, t);
-    sw_kings(s, g, t);
-    return sw_popc(t, 0, SW_SETS) + popc(g.castles);
-}
 // origin of target `to` of set j.  Leapers: origin = to + a signed byte of four packed words
 // (pawn offsets by colour); sliders: the nearest occupied square behind the target on the
 // set's line (the squares between are empty: the ray came through them), branch-free.

@@ -191,20 +191,57 @@ GC_HD int fselect(const Pos& s, const FGen& f, int k) {
     return A_NONE;
 }
 
+// Set-wise generation under FIDE rules (gc_core.h sw_*, the self-play policy's move-set
+// order): the double step needs the square between empty, enemy kings are never targets, and
+// the legal en-passant captures (ep_from, legality from fgen) join the capture sets.
+GC_HD void fsw_pawns(const Pos& s, const FGen& f, u64* t) {
+    const Gen& g = f.g;
+    const u64 cm = g.checkmask, empty = ~g.occ, opp = g.opp & ~s.k, P = s.p & g.own, pr = g.pinrays;
+    const int kq = sw_ksq(g);
+    const u64 fp = P & ~g.pinned, pp = P & g.pinned;
+    const u64 pf = pp & file_mask(kq), pd = pp & diag_mask(kq), pa = pp & anti_mask(kq);
+    const u64 epb = f.ep >= 0 ? bit(f.ep) : 0ull, ef = f.ep_from;
+    if (g.white) {
+        const u64 mf = ((fp & ROW6) >> 8) & empty, mp = ((pf & ROW6) >> 8) & empty;
+        t[SW_P1] = ((fp >> 8) | ((pf >> 8) & pr)) & empty & cm;
+        t[SW_P2] = ((mf >> 8) | ((mp >> 8) & pr)) & empty & cm;
+        t[SW_PL] = ((((fp >> 7) | ((pa >> 7) & pr)) & ~FILE_A) & opp & cm) | (((ef >> 7) & ~FILE_A) & epb);
+        t[SW_PR] = ((((fp >> 9) | ((pd >> 9) & pr)) & ~FILE_H) & opp & cm) | (((ef >> 9) & ~FILE_H) & epb);
+    } else {
+        const u64 mf = ((fp & ROW1) << 8) & empty, mp = ((pf & ROW1) << 8) & empty;
+        t[SW_P1] = ((fp << 8) | ((pf << 8) & pr)) & empty & cm;
+        t[SW_P2] = ((mf << 8) | ((mp << 8) & pr)) & empty & cm;
+        t[SW_PL] = ((((fp << 9) | ((pd << 9) & pr)) & ~FILE_A) & opp & cm) | (((ef << 9) & ~FILE_A) & epb);
+        t[SW_PR] = ((((fp << 7) | ((pa << 7) & pr)) & ~FILE_H) & opp & cm) | (((ef << 7) & ~FILE_H) & epb);
+    }
+}
+// the sets of part A (pawns, knights, kings) and B (sliders), as the paired kernel splits them
+GC_HD void fsw_gen_a(const Pos& s, const FGen& f, u64* t) {
+    const u64 nk = ~(s.k & f.g.opp);
+    fsw_pawns(s, f, t);
+    sw_knights(s, f.g, t, nk);
+    sw_kings(s, f.g, t, nk);
+}
+GC_HD void fsw_gen_b(const Pos& s, const FGen& f, u64* t) {
+    const u64 nk = ~(s.k & f.g.opp);
+    sw_orth(s, f.g, t, nk);
+    sw_diag(s, f.g, t, nk);
+}
+GC_HD int fsw_gen(const Pos& s, const FGen& f, u64* t) {
+    fsw_gen_a(s, f, t);
+    fsw_gen_b(s, f, t);
+    return sw_popc(t, 0, SW_SETS) + popc(f.g.castles);
+}
+
 // the random policy's pick for the side to move of s (fgen'd into f): draws k uniformly in
 // [0, #legal) from the Philox stream (board, draw++) and returns the k-th legal action in
-// action-id order -- through the count-plane search when the shared generator applies
+// move-set order (as the reference-rules self-play)
 template <class S>
-GC_HD int fpick_action(const Pos& s, const FGen& f, S& scr, uint64_t seed, u32 board, u32& draw) {
-    if (fuses_walk(f)) {
-        int n = fcount_walk(s, f, false);
-        if (n == 0) return A_NONE;
-        return fselect(s, f, (int)policy_index(seed, board, draw++, (u32)n));
-    }
-    MoveSet ms;
-    fgen_moves(s, f, ms, scr);
-    if (ms.total == 0) return A_NONE;
-    return select_action(s, f.g, ms, scr, (int)policy_index(seed, board, draw++, (u32)ms.total));
+GC_HD int fpick_action(const Pos& s, const FGen& f, S&, uint64_t seed, u32 board, u32& draw) {
+    u64 t[SW_SETS];
+    const int n = fsw_gen(s, f, t);
+    if (n == 0) return A_NONE;
+    return sw_select(f.g, t, (int)policy_index(seed, board, draw++, (u32)n));
 }
 
 GC_HD bool faction_legal(const Pos& s, const FGen& f, int action) {

@@ -194,7 +194,11 @@ __global__ void __launch_bounds__(BLOCK) k_finit_cache(EnvDev e, EnvDev::InitCac
     c.white = f.g.white;
     c.usable = !walk;
     c.table = c.usable && c.total > 0 && c.total <= RESET_ACTS_MAX;
-    for (int k = 0; c.table && k < c.total; k++) acts[k] = (uint16_t)select_action(c.pos, f.g, ms, scr, k);
+    if (c.table) {  // the self-play policy's move-set order (gcf::fpick_action)
+        u64 t[SW_SETS];
+        gcf::fsw_gen(c.pos, f, t);
+        for (int k = 0; k < c.total; k++) acts[k] = (uint16_t)sw_select(f.g, t, k);
+    }
     *out = c;
 }
 

@@ -887,21 +887,16 @@ __device__ __forceinline__ void pair_half(PairLds& L, int role, int l, bool mv, 
     int c = 0;
     u32 hl = hl_of(s.meta);
     if (role == 0) {
-        if constexpr (FIDE) {  // castles counted here (W1 does not know them)
-            if (gen) {
-                if (ms.big) {
-                    gcf::FGen f{g, ep_from, ep};
-                    part = gcf::fcount_walk(ns, f, false);
-                } else {
-                    part = gen_moves_a<PairScratch, true>(ns, g, ms, scr, FideExtra{ep_from, ep}) + popc(g.castles);
-                }
-            }
-        } else if constexpr (SW) {  // pawn, knight and king sets; castles counted here
+        if constexpr (SW) {  // pawn, knight and king sets; castles counted here
             H.cw[0] = H.cw[1] = H.cw[2] = H.cw[3] = 0;
             if (gen) {
-                sw_pawns(ns, g, H.T);
-                sw_knights(ns, g, H.T);
-                sw_kings(ns, g, H.T);
+                if constexpr (FIDE) {
+                    gcf::fsw_gen_a(ns, gcf::FGen{g, ep_from, ep}, H.T);
+                } else {
+                    sw_pawns(ns, g, H.T);
+                    sw_knights(ns, g, H.T);
+                    sw_kings(ns, g, H.T);
+                }
                 sw_pack(H.T, 0, SW_ORTH, H.cw);
                 sw_pack(H.T, SW_K, SW_SETS, H.cw);
                 part = sw_popc(H.T, 0, SW_ORTH) + sw_popc(H.T, SW_K, SW_SETS) + popc(g.castles);
@@ -910,6 +905,15 @@ __device__ __forceinline__ void pair_half(PairLds& L, int role, int l, bool mv, 
 #pragma unroll
                 for (int j = SW_K; j < SW_SETS; j++) L.sets[j][l] = H.T[j];
             }
+        } else if constexpr (FIDE) {  // castles counted here (W1 does not know them)
+            if (gen) {
+                if (ms.big) {
+                    gcf::FGen f{g, ep_from, ep};
+                    part = gcf::fcount_walk(ns, f, false);
+                } else {
+                    part = gen_moves_a<PairScratch, true>(ns, g, ms, scr, FideExtra{ep_from, ep}) + popc(g.castles);
+                }
+            }
         } else {  // castles counted here (W1 does not know them)
             if (gen) part = ms.big ? count_legal(ns, g) : gen_moves_a(ns, g, ms, scr) + popc(g.castles);
         }
@@ -917,8 +921,12 @@ __device__ __forceinline__ void pair_half(PairLds& L, int role, int l, bool mv, 
         if constexpr (SW) {  // the slider direction sets and their byte counts, to W0 through LDS
             u64 cw[4] = {0, 0, 0, 0};
             if (gen) {
-                sw_orth(ns, g, H.T);
-                sw_diag(ns, g, H.T);
+                if constexpr (FIDE) {
+                    gcf::fsw_gen_b(ns, gcf::FGen{g, 0, -1}, H.T);
+                } else {
+                    sw_orth(ns, g, H.T);
+                    sw_diag(ns, g, H.T);
+                }
                 sw_pack(H.T, SW_ORTH, SW_K, cw);
                 part = sw_popc(H.T, SW_ORTH, SW_K);
 #pragma unroll
@@ -1000,7 +1008,7 @@ template <bool SHARE_ACT, bool FIDE = false>
 __device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, int role, int l, int i,
                                             bool live, const Pos& rp, Pos& s, int& a, u32& d, DevHist& h,
                                             u32& nst) {
-    constexpr bool SW = !FIDE;  // reference rules: the self-play policy's move-set order (gc_core.h sw_*)
+    constexpr bool SW = true;  // the self-play policy's move-set order (gc_core.h sw_*), both rule sets
     PairScratch scr{&L.slots[0][l]};
     const bool none = a == A_NONE;                           // empty list: driver reset
     const bool done0 = (s.meta & M_DONE) != 0;               // chess_v2.py:245-251
@@ -1074,8 +1082,15 @@ __device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, int ro
             gcf::FGen f;
             bool regs = false;  // SW: the sets in registers (generated here), else in LDS
             if (!have && SW) {  // the start position without a table: generated
-                gen_init(s, g);
-                ms.total = sw_gen(s, g, H.T);
+                if constexpr (FIDE) {
+                    gcf::FGen fr;
+                    gcf::fgen(s, fr);
+                    g = fr.g;
+                    ms.total = gcf::fsw_gen(s, fr, H.T);
+                } else {
+                    gen_init(s, g);
+                    ms.total = sw_gen(s, g, H.T);
+                }
                 regs = true;
             } else if (!have) {
                 const EnvDev::InitCache& ic = *C.icd;

@@ -125,10 +125,10 @@ int gc_device_free(int device, void* ptr);
 int gc_env_copy(gc_env* e, void* dst, const void* src, uint64_t bytes, int kind);
 /* Device-resident random self-play (the test_benchmark.py driver): n_plies one-ply kernel
  * launches; each ply = one env.step() with a uniform Philox pick over the legal list, a
- * reset when done, a reset without a step when the list is empty (reason 4).  The pick's
- * rank indexes the legal moves in move-set order under reference rules without an opponent
- * (gc_core.h sw_gen: pawn / knight / slider-direction / king-step target sets, then
- * castles), in action-id order otherwise (opponent modes, rules "fide"). */
+ * reset when done, a reset without a step when the list is empty (reason 4).  Without an
+ * opponent the pick's rank indexes the legal moves in move-set order (gc_core.h sw_gen:
+ * pawn / knight / slider-direction / king-step target sets, then castles; both rule sets),
+ * with the random opponent in action-id order. */
 int gc_env_step_random(gc_env* e, int n_plies);
 /* gc_env_step_random over k board ranges on k streams of the device (k in [1, 8]; default
  * from GC_STREAMS, else 2): a range's ply p+1 waits only for its own ply p, so the ranges'

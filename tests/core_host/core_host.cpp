@@ -463,6 +463,19 @@ static int fide_cmp_rec(const Pos& s, int depth, int8_t* ob, uint8_t* om, int* c
     fide::FGen f;
     fide::fgen(s, f);
     int a = fide::fcount(s, f, true), w = fide::fcount_walk(s, f, true);
+    {  // the set-wise generator (the FIDE self-play pick): same action count, every rank a
+       // distinct legal action
+        u64 t[SW_SETS];
+        const int n = fide::fsw_gen(s, f, t), na = fide::fcount_walk(s, f, false);
+        std::vector<char> seen(4101, 0);
+        bool ok = n == na;
+        for (int k = 0; ok && k < n; k++) {
+            const int act = sw_select(f.g, t, k);
+            ok = act >= 0 && act < 4101 && !seen[act] && fide::faction_legal(s, f, act);
+            if (ok) seen[act] = 1;
+        }
+        if (!ok) a = -1 - n;
+    }
     if (a != w) {
         to_mailbox(s, ob);
         for (int k = 0; k < 8; k++) om[k] = 0;
