@@ -841,13 +841,9 @@ __device__ __forceinline__ void pair_half(PairLds& L, int role, int l, bool mv, 
             L.f1[l] = my_chk ? 1u : 0u;
         }
     }
-#ifndef GC_STAMP_PICK
     GC_STAMP(2);
-#endif
     pair_barrier();
-#ifndef GC_STAMP_PICK
     GC_STAMP(3);
-#endif
 
     // ---- phase 2
     if (role == 0) {
@@ -999,6 +995,27 @@ __device__ __forceinline__ Pos pair_settle(const PairHalf& H, bool white) {
     return ns;
 }
 
+// The self-play pick from the move sets in LDS (pair_half with SW): the set holding rank k by
+// the byte counts (gc_core.h sw_locate), then that one set from LDS; more moves than byte sums
+// hold (never in play) take a rolled scan over LDS.  k < tot.
+__device__ __forceinline__ int sw_pick_lds(const PairLds& L, int l, const Gen& g, const u64* cw, int tot, int k) {
+    const int normal = tot - popc(g.castles);
+    int r = k, j;
+    if (tot < 256) {
+        j = sw_locate(cw, r);
+    } else {
+#pragma unroll 1
+        for (j = 0; j < SW_SETS - 1; j++) {
+            const int c = popc(L.sets[j][l]);
+            if (r < c) break;
+            r -= c;
+        }
+    }
+    j = j < SW_SETS ? j : SW_SETS - 1;  // a castle's rank runs past the sets
+    const int set_act = sw_finish(g, j, L.sets[j][l], r);
+    return k >= normal ? sw_castle(g, k - normal) : set_act;
+}
+
 // One ply of the paired driver (opponent "none").  In/out: the state s, the action a (picked
 // for s by the previous ply or by the reset), the draw counter d (W0), the window h (W1; its
 // table write is left deferred in h), the step counter nst.  Returns the ply's env.step()
@@ -1009,7 +1026,6 @@ __device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, int ro
                                             bool live, const Pos& rp, Pos& s, int& a, u32& d, DevHist& h,
                                             u32& nst) {
     constexpr bool SW = true;  // the self-play policy's move-set order (gc_core.h sw_*), both rule sets
-    PairScratch scr{&L.slots[0][l]};
     const bool none = a == A_NONE;                           // empty list: driver reset
     const bool done0 = (s.meta & M_DONE) != 0;               // chess_v2.py:245-251
     const bool cap = mc_of(s.meta) > MOVES_MAX;              // 252-258
@@ -1038,6 +1054,10 @@ __device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, int ro
 #endif
     Gen& g = H.g;
     MoveSet& ms = H.ms;
+    // W0: the next action from this ply's move sets, ahead of the outcome (its LDS read and rank
+    // arithmetic overlap the outcome's; used unless the board resets)
+    int set_act = A_NONE;
+    if (role == 0 && ms.total > 0) set_act = sw_pick_lds(L, l, g, H.cw, ms.total, (int)scale_rank(x0, (u32)ms.total));
     StepOut o = {0, 0, R_NONE, 0};
     bool have = false;
     if (none) {
@@ -1072,91 +1092,26 @@ __device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, int ro
     GC_STAMP(6);
 #endif
     if (role == 0) {
-        uint16_t act = (uint16_t)A_NONE;
+        uint16_t act = (uint16_t)set_act;
         int tot = ms.total;
         if (!have && C.rtable) {  // the start position's table
             act = ra;
             tot = (int)C.rtotal;
-        } else {
-            bool walk = false;  // FIDE, > SCRATCH_SLOTS own pieces: the per-square walk
-            gcf::FGen f;
-            bool regs = false;  // SW: the sets in registers (generated here), else in LDS
-            if (!have && SW) {  // the start position without a table: generated
-                if constexpr (FIDE) {
-                    gcf::FGen fr;
-                    gcf::fgen(s, fr);
-                    g = fr.g;
-                    ms.total = gcf::fsw_gen(s, fr, H.T);
-                } else {
-                    gen_init(s, g);
-                    ms.total = sw_gen(s, g, H.T);
-                }
-                regs = true;
-            } else if (!have) {
-                const EnvDev::InitCache& ic = *C.icd;
-                if (ic.usable) {
-                    g.white = ic.white; g.own = ic.own; g.castles = ic.castles;
-                    ms.fastp = ic.fastp; ms.o1 = ic.o1; ms.o2 = ic.o2; ms.ol = ic.ol; ms.orr = ic.orr;
-#pragma unroll
-                    for (int b = 0; b < 5; b++) ms.cnt[b] = ic.cnt[b];
-                    ms.total = ic.total;
-                    ms.big = false;
-#pragma unroll
-                    for (int j = 0; j < SCRATCH_SLOTS; j++) scr.put(j, ic.slots[j]);
-                } else if constexpr (FIDE) {
-                    gcf::fgen(s, f);
-                    g = f.g;
-                    walk = gcf::fuses_walk(f);
-                    if (walk) ms.total = gcf::fcount_walk(s, f, false);
-                    else gcf::fgen_moves(s, f, ms, scr);
-                } else {
-                    gen_init(s, g);
-                    gen_moves(s, g, ms, scr);
-                }
-            } else if constexpr (FIDE) {
-                if (ms.big) {
-                    f = gcf::FGen{g, H.ep_from, H.ep};
-                    walk = true;
-                }
+        } else if (!have) {  // the start position without a table (rare): generated, through LDS
+            if constexpr (FIDE) {
+                gcf::FGen fr;
+                gcf::fgen(s, fr);
+                g = fr.g;
+                tot = gcf::fsw_gen(s, fr, H.T);
+            } else {
+                gen_init(s, g);
+                tot = sw_gen(s, g, H.T);
             }
-            tot = ms.total;
-            if (tot > 0) {
-                int k = (int)scale_rank(x0, (u32)tot);
-#ifdef GC_STAMP_PICK  // diagnostic: stamps 2 / 3 around the rank search (phase-1 stamps dropped)
-                GC_STAMP(2);
-#endif
-                if constexpr (SW) {
-                    if (regs) {  // sets generated here: into LDS and counted like the others (rare)
-                        H.cw[0] = H.cw[1] = H.cw[2] = H.cw[3] = 0;
-                        sw_pack(H.T, 0, SW_SETS, H.cw);
+            H.cw[0] = H.cw[1] = H.cw[2] = H.cw[3] = 0;
+            sw_pack(H.T, 0, SW_SETS, H.cw);
 #pragma unroll
-                        for (int j = 0; j < SW_SETS; j++) L.sets[j][l] = H.T[j];
-                    }
-                    // the set holding rank k by the byte counts, then that one set from LDS; more
-                    // moves than byte sums hold (never in play) take a rolled scan over LDS
-                    const int normal = tot - popc(g.castles);
-                    int r = k, j;
-                    if (tot < 256) {
-                        j = sw_locate(H.cw, r);
-                    } else {
-#pragma unroll 1
-                        for (j = 0; j < SW_SETS - 1; j++) {
-                            const int c = popc(L.sets[j][l]);
-                            if (r < c) break;
-                            r -= c;
-                        }
-                    }
-                    j = j < SW_SETS ? j : SW_SETS - 1;  // a castle's rank runs past the sets
-                    const int ms_act = sw_finish(g, j, L.sets[j][l], r);
-                    act = (uint16_t)(k >= normal ? sw_castle(g, k - normal) : ms_act);
-                } else {
-                    act = (uint16_t)(walk ? gcf::fselect(s, f, k) : select_action_swar(s, g, ms, scr, k));
-                }
-#ifdef GC_STAMP_PICK
-                asm volatile("" ::"v"(act));
-                GC_STAMP(3);
-#endif
-            }
+            for (int j = 0; j < SW_SETS; j++) L.sets[j][l] = H.T[j];
+            act = (uint16_t)(tot > 0 ? sw_pick_lds(L, l, g, H.cw, tot, (int)scale_rank(x0, (u32)tot)) : A_NONE);
         }
         a = act;
         d += tot > 0 ? 1u : 0u;
