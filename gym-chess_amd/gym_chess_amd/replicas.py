@@ -116,8 +116,10 @@ class Replicas:
             self.mode = "processes"
             self.world_size = int(os.environ.get("WORLD_SIZE", "1")) if world_size is None else int(world_size)
             self.rank = int(os.environ.get("RANK", "0")) if rank is None else int(rank)
-            lr = os.environ.get("LOCAL_RANK", str(self.rank)) if local_rank is None else local_rank
-            self.local = [Replica(self.rank, int(lr))]
+            lr = int(os.environ.get("LOCAL_RANK", str(self.rank)) if local_rank is None else local_rank)
+            # devices maps local ranks to devices (default: the local rank; the 1-GPU tests put
+            # several ranks on device 0)
+            self.local = [Replica(self.rank, lr if devices is None else int(devices[lr]))]
             if gpus is not None and int(gpus) != self.world_size:
                 raise ValueError(f"--gpus {gpus} does not match the launcher's WORLD_SIZE={self.world_size}")
         else:  # one process, one thread per device

@@ -81,3 +81,34 @@ def test_bench_threaded_two_replicas_line():
     line = json.loads(out.stdout.strip().splitlines()[-1])
     assert line["n_gpus"] == 2 and line["config"]["global_boards"] == 2 * 8192
     assert line["config"]["replica_mode"] == "threads" and line["value"] > 0
+
+
+def test_bench_torchrun_two_ranks_line():
+    """The driver's multi-GPU launch shape, rehearsed on the one GPU: python -m
+    torch.distributed.run --nproc-per-node 2 bench.py --gpus 2 (GC_BENCH_DEVICES=0,0 puts both
+    ranks on device 0): one process per rank, the file-group barrier and max / sum, and ONE
+    JSON line from rank 0 with n_gpus 2, global_boards 2 x boards, replica_mode processes."""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    env = dict(os.environ, GC_BENCH_DEVICES="0,0")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                          "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(root, "bench.py"),
+                          "--gpus", "2", "--steps", "20", "--warmup", "5", "--settle", "300", "--boards", "8192",
+                          "--perft-roots", "0", "--variant-steps", "0", "--api-steps", "0", "--single-episodes", "0",
+                          "--no-cpu-baseline", "--fused-plies", "0"], capture_output=True, text=True, env=env,
+                         timeout=240, check=True)
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["config"]["global_boards"] == 2 * 8192
+    assert line["config"]["replica_mode"] == "processes" and line["value"] > 0
