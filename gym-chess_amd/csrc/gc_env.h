@@ -198,7 +198,8 @@ GC_HD StepOut env_step(Pos& s, H& hist, int action, const Gen* g0, Gen& g, MoveS
 }
 
 // The random opponent's pick (make_random_policy, chess_v2.py:116-127, on the device policy
-// stream): rank drawn uniformly over the legal list, k-th legal action in action-id order.
+// stream): rank drawn uniformly over the legal list, the k-th legal action in move-set order
+// (selfplay_pick below, the same policy as the self-play driver's).
 struct PolicyCtx {
     u64 seed;
     u32 board;
@@ -260,8 +261,7 @@ GC_HD StepOut env_step_vs(Pos& s, H& hist, int action, const Gen* g0, Gen& g, Mo
         return o;
     }
     hist.commit();  // the agent ply's table write lands before the reply probes the table
-    int k = (int)policy_index(pc.seed, pc.board, pc.draw++, (u32)ms.total);
-    int oa = select_action(s, g, ms, scr, k);
+    int oa = selfplay_pick(s, pc);  // ms.total > 0: one draw
     rc = env_ply(s, hist, oa, g, ms, scr, &mr, &rep, &chk);
     if (rc == 1) {
         o.reason = R_BOTH_CHECKED;
@@ -287,8 +287,7 @@ GC_HD StepOut env_step_vs(Pos& s, H& hist, int action, const Gen* g0, Gen& g, Mo
 template <class H, class S>
 GC_HD void env_open_vs(Pos& s, H& hist, Gen& g, MoveSet& ms, S& scr, PolicyCtx& pc) {
     if (ms.total == 0) { s.meta |= M_DONE; return; }
-    int k = (int)policy_index(pc.seed, pc.board, pc.draw++, (u32)ms.total);
-    int oa = select_action(s, g, ms, scr, k);
+    int oa = selfplay_pick(s, pc);  // one draw
     int mr;
     bool rep, chk;
     if (env_ply(s, hist, oa, g, ms, scr, &mr, &rep, &chk) == 1) { s.meta |= M_DONE; return; }

@@ -499,13 +499,21 @@ __global__ void __launch_bounds__(BLOCK) k_init_cache(EnvDev e, EnvDev::InitCach
     *out = c;
 }
 
-// policy: uniform choice among the legal actions (test_benchmark.py:22-27); rank k maps to
-// the k-th legal action in action-id order (gc_core.h select_action)
-__device__ uint16_t pick(const Pos& s, const Gen& g, const MoveSet& ms, const LdsScratch& scr, uint64_t seed,
-                         int i, u32& draw) {
+// the API step's `pick` output: uniform over the legal actions, the k-th in action-id order
+// (the order of its legal-action mask; gc_core.h select_action)
+__device__ uint16_t pick_mask_order(const Pos& s, const Gen& g, const MoveSet& ms, const LdsScratch& scr,
+                                    uint64_t seed, int i, u32& draw) {
     if (ms.total == 0) return (uint16_t)A_NONE;
     u32 k = policy_index(seed, (u32)i, draw++, (u32)ms.total);
     return (uint16_t)select_action(s, g, ms, scr, (int)k);
+}
+// the random policy (self-play and the opponent modes): uniform, the k-th legal action in
+// move-set order (gc_env.h selfplay_pick: regenerated set-wise from the position)
+__device__ uint16_t pick(const Pos& s, uint64_t seed, int i, u32& draw) {
+    PolicyCtx pc = {seed, (u32)i, draw};
+    const int a = selfplay_pick(s, pc);
+    draw = pc.draw;
+    return (uint16_t)a;
 }
 
 // after a reset: the move set of the side to move; a BLACK agent's opponent opens first
@@ -532,7 +540,7 @@ __global__ void __launch_bounds__(BLOCK) k_env_reset(EnvDev e, const uint8_t* __
         MoveSet ms;
         if (OPP) {
             after_reset<OPP>(e, s, h, g, ms, scr, pc);
-            if (select) e.act[i] = pick(s, g, ms, scr, e.seed, i, pc.draw);
+            if (select) e.act[i] = pick(s, e.seed, i, pc.draw);
         } else {
             e.act[i] = (uint16_t)selfplay_pick(s, pc);
         }
@@ -605,7 +613,7 @@ __global__ void __launch_bounds__(BLOCK) k_env_step(EnvDev e) {
         if (OPP) {
             if (!have) after_reset<OPP>(e, s, h, g, ms, scr, pc);
             GC_STAMP(6);
-            e.act[i] = pick(s, g, ms, scr, e.seed, i, pc.draw);
+            e.act[i] = pick(s, e.seed, i, pc.draw);
         } else {
             e.act[i] = (uint16_t)selfplay_pick(s, pc);
         }
@@ -1151,7 +1159,6 @@ template <bool BLACK, bool SHARE_ACT>
 __device__ __forceinline__ StepOut pair_step_vs(PairLdsVs* Ls, PairLdsVs& L, const PairCtx& C, int role, int l,
                                                 int i, bool live, const Pos& rp, Pos& s, int& a, u32& d, DevHist& h,
                                                 u32& nst) {
-    PairScratch scr{&L.slots[0][l]};
     const bool none = a == A_NONE;                           // empty list: driver reset
     const bool done0 = (s.meta & M_DONE) != 0;               // chess_v2.py:245-251
     const bool cap = mc_of(s.meta) > MOVES_MAX;              // 252-258
@@ -1159,8 +1166,8 @@ __device__ __forceinline__ StepOut pair_step_vs(PairLdsVs* Ls, PairLdsVs& L, con
     const bool white = (s.meta & M_WHITE) != 0;              // the agent's colour
     u32 x0 = 0, x1 = 0, x2 = 0, ra = 0;
     PairHalf H;
-    // ---- the agent's half-ply
-    pair_half<false, false>(
+    // ---- the agent's half-ply (every half-ply generates set-wise: the picks are in move-set order)
+    pair_half<false, false, false, true>(
         L, role, l, mv, false, s, a, nullptr, nullptr, h, H,
         [&] {
             x0 = philox_x0(C.seed, (u32)i, d);
@@ -1211,13 +1218,13 @@ __device__ __forceinline__ StepOut pair_step_vs(PairLdsVs* Ls, PairLdsVs& L, con
     // ---- the opponent's reply: W0 picks it from the agent ply's generation (draw d)
     int oa = A_NONE;  // W1 reads W0's pick in the reply's phase 1
     if (role == 0) {
-        if (cont) oa = select_action_swar(s, H.g, H.ms, scr, (int)scale_rank(x0, (u32)H.ms.total));
+        if (cont) oa = sw_pick_lds(L, l, H.g, H.cw, H.ms.total, (int)scale_rank(x0, (u32)H.ms.total));
         L.oa[l] = (u32)oa;
     } else if (live) {
         h.commit();  // the agent ply's window write lands before the reply probes the table
     }
     const Pos s1 = s;
-    pair_half<false, true>(L, role, l, cont, false, s1, oa, L.oa, nullptr, h, H, PairNoop{}, PairNoop{});
+    pair_half<false, true, false, true>(L, role, l, cont, false, s1, oa, L.oa, nullptr, h, H, PairNoop{}, PairNoop{});
     if (cont) {
         if (H.both) {
             o.reason = R_BOTH_CHECKED;
@@ -1247,7 +1254,7 @@ __device__ __forceinline__ StepOut pair_step_vs(PairLdsVs* Ls, PairLdsVs& L, con
     if (role == 0) {
         if (have) {
             tot = H.ms.total;
-            if (tot > 0) act = (uint16_t)select_action_swar(s, H.g, H.ms, scr, (int)scale_rank(x1, (u32)tot));
+            if (tot > 0) act = (uint16_t)sw_pick_lds(L, l, H.g, H.cw, tot, (int)scale_rank(x1, (u32)tot));
         } else if (!BLACK) {
             tot = (int)C.rtotal;
             act = (uint16_t)(nd ? ra >> 16 : ra & 0xFFFFu);
@@ -1270,7 +1277,8 @@ __device__ __forceinline__ StepOut pair_step_vs(PairLdsVs* Ls, PairLdsVs& L, con
         if (any) {
             const int oa = (int)(nd ? ra >> 16 : ra & 0xFFFFu);
             const Pos s0 = s;
-            pair_half<false, false>(L, role, l, open, false, s0, oa, nullptr, nullptr, h, H, PairNoop{}, PairNoop{});
+            pair_half<false, false, false, true>(L, role, l, open, false, s0, oa, nullptr, nullptr, h, H, PairNoop{},
+                                                 PairNoop{});
             if (open) {
                 s = pair_settle(H, true);
                 s.meta = (s.meta & ~(u32)M_DONE) + (1u << M_MC_SHIFT);
@@ -1278,7 +1286,8 @@ __device__ __forceinline__ StepOut pair_step_vs(PairLdsVs* Ls, PairLdsVs& L, con
                 if (role == 0) {
                     tot = H.ms.total;
                     act = (uint16_t)A_NONE;
-                    if (tot > 0) act = (uint16_t)select_action_swar(s, H.g, H.ms, scr, (int)scale_rank(nd == 1 ? x1 : x2, (u32)tot));
+                    if (tot > 0)
+                        act = (uint16_t)sw_pick_lds(L, l, H.g, H.cw, tot, (int)scale_rank(nd == 1 ? x1 : x2, (u32)tot));
                 }
             }
         }
@@ -1521,7 +1530,7 @@ __global__ void __launch_bounds__(BLOCK) k_env_rollout(EnvDev e, int plies, int1
             tr_done[t] = (uint8_t)o.done;
             tr_reason[t] = (uint8_t)o.reason;
         }
-        a = OPP ? pick(s, g, ms, scr, e.seed, i, pc.draw) : selfplay_pick(s, pc);
+        a = selfplay_pick(s, pc);
         h.commit();
     }
     e.reward[i] = o.reward;  // the last ply's env.step() outputs (per-ply: trace buffers)
@@ -1647,7 +1656,7 @@ __global__ void __launch_bounds__(BLOCK) k_env_step_api(EnvDev e, const uint16_t
     if (mask) write_mask(s, g, ms, scr, mask + i, (size_t)e.n);
     if (obs) write_obs(s, obs + 64 * (size_t)i);
     if (pick_out) {
-        uint16_t p = pick(s, g, ms, scr, e.seed, i, pc.draw);
+        uint16_t p = pick_mask_order(s, g, ms, scr, e.seed, i, pc.draw);
         pick_out[i] = p;
         e.act[i] = p;
     }
@@ -1853,20 +1862,11 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
 }
 
 __global__ void __launch_bounds__(BLOCK) k_select(EnvDev e) {
-    LDS_SCRATCH_DECL;
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= e.n) return;
     Pos s = e.st.load(i);
     PolicyCtx pc = {e.seed, (u32)i, e.draw[i]};
-    if (e.opp) {
-        Gen g;
-        MoveSet ms;
-        gen_init(s, g);
-        gen_moves(s, g, ms, scr);
-        e.act[i] = pick(s, g, ms, scr, e.seed, i, pc.draw);
-    } else {
-        e.act[i] = (uint16_t)selfplay_pick(s, pc);
-    }
+    e.act[i] = (uint16_t)selfplay_pick(s, pc);
     e.draw[i] = pc.draw;
 }
 
@@ -2409,8 +2409,8 @@ static void launch_step2(gc_env* e, hipStream_t st, int b0 = 0, int nb = -1) {
     switch (e->rules ? 3 : pair_opp(e)) {
         case 3: k_env_step2<true><<<grid, block, 0, st>>>(e->slab, d.n, b0, d.seed, d.htab, r.racts, r.icd, r.rinfo); break;
         case 0: k_env_step2<false><<<grid, block, 0, st>>>(e->slab, d.n, b0, d.seed, d.htab, sw_table(r), r.icd, r.rinfo); break;
-        case 1: k_env_step2<false, 1><<<grid, block, 0, st>>>(e->slab, d.n, b0, d.seed, d.htab, r.racts, r.icd, r.rinfo); break;
-        default: k_env_step2<false, 2><<<grid, block, 0, st>>>(e->slab, d.n, b0, d.seed, d.htab, r.racts, r.icd, r.rinfo); break;
+        case 1: k_env_step2<false, 1><<<grid, block, 0, st>>>(e->slab, d.n, b0, d.seed, d.htab, sw_table(r), r.icd, r.rinfo); break;
+        default: k_env_step2<false, 2><<<grid, block, 0, st>>>(e->slab, d.n, b0, d.seed, d.htab, sw_table(r), r.icd, r.rinfo); break;
     }
 }
 
@@ -2787,8 +2787,8 @@ extern "C" int gc_env_rollout(gc_env* e, int n_plies, int16_t* tr_action, int16_
         switch (e->rules ? 3 : pair_opp(e)) {
             case 3: k_env_rollout2<true><<<grid, bs, 0, e->stream>>>(e->slab, d.n, 0, d.seed, d.htab, r.racts, r.icd, r.rinfo, n_plies, e->stats); break;
             case 0: k_env_rollout2<false><<<grid, bs, 0, e->stream>>>(e->slab, d.n, 0, d.seed, d.htab, sw_table(r), r.icd, r.rinfo, n_plies, e->stats); break;
-            case 1: k_env_rollout2<false, 1><<<grid, bs, 0, e->stream>>>(e->slab, d.n, 0, d.seed, d.htab, r.racts, r.icd, r.rinfo, n_plies, e->stats); break;
-            default: k_env_rollout2<false, 2><<<grid, bs, 0, e->stream>>>(e->slab, d.n, 0, d.seed, d.htab, r.racts, r.icd, r.rinfo, n_plies, e->stats); break;
+            case 1: k_env_rollout2<false, 1><<<grid, bs, 0, e->stream>>>(e->slab, d.n, 0, d.seed, d.htab, sw_table(r), r.icd, r.rinfo, n_plies, e->stats); break;
+            default: k_env_rollout2<false, 2><<<grid, bs, 0, e->stream>>>(e->slab, d.n, 0, d.seed, d.htab, sw_table(r), r.icd, r.rinfo, n_plies, e->stats); break;
         }
     } else if (e->d.opp) {
         k_env_rollout<true><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d, n_plies, da, dr, dd, dq, e->stats);

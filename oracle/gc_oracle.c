@@ -426,7 +426,7 @@ typedef struct {
     /* opponent (chess_v2.py:167-181): 0 none, 1 random = the Philox policy below, drawing
      * from the same per-board stream (seed, board, draw++) as the self-play driver */
     int opp, agent_black;
-    int set_order;  /* the policy's order: 1 move-set order (self-play), 0 action-id order */
+    int set_order;  /* the policy's order: 1 move-set order, 0 action-id order (the API step's pick) */
     uint64_t seed;
     uint32_t board, draw;
     /* distinct pre-move boards of reversible moves since the last pawn move / capture: the
@@ -463,8 +463,8 @@ static void env_engine_state(const OEnv *e, OState *s) {
 
 static int kth_in_set_order(const int8_t *b, const uint16_t *moves, int n, int k);
 
-/* the random policy's pick: uniform rank over the legal list; the k-th legal action in
- * action-id order for the opponent modes, in move-set order for self-play (opponent "none") */
+/* the random policy's pick (self-play and the opponent): uniform rank over the legal list, the
+ * k-th legal action in move-set order (set_order 0: action-id order, the API step's `pick`) */
 static int env_policy_pick(OEnv *e) {
     uint32_t k = oracle_policy_index(e->seed, e->board, e->draw++, (uint32_t)e->nmoves);
     if (e->set_order) return kth_in_set_order(e->st.b, e->moves, e->nmoves, (int)k);
@@ -655,7 +655,7 @@ static void rollout_board(const int8_t *init, uint64_t seed, uint32_t board, int
     memset(&e, 0, sizeof(e));
     memcpy(e.init, init, 64);
     e.opp = opp; e.agent_black = agent_black; e.seed = seed; e.board = board; e.draw = 0;
-    e.set_order = order < 0 ? !opp : order;
+    e.set_order = order < 0 ? 1 : order;
     o_env_reset(&e);
     for (int p = 0; p < plies; p++) {
         int action = -1, rw = 0, dn = 0, reason = 0;
@@ -735,8 +735,8 @@ void oracle_rollout_batch(const int8_t *init, uint64_t seed, uint32_t b_begin, u
     oracle_rollout_batch2(init, seed, b_begin, n_boards, plies, 0, 1, threads, stats8);
 }
 
-/* Trajectory with an opponent mode (0 none, 1 random) and agent colour; order -1: the mode's
- * policy order, 0: action-id order (the API step's `pick` output), 1: move-set order. */
+/* Trajectory with an opponent mode (0 none, 1 random) and agent colour; order -1 or 1: the
+ * policy's move-set order, 0: action-id order (the API step's `pick` output). */
 void oracle_rollout_trace3(const int8_t *init, uint64_t seed, uint32_t board, int plies, int opp, int agent_white,
                            int order, int16_t *tr_action, int16_t *tr_reward, uint8_t *tr_done, uint8_t *tr_reason,
                            int8_t *final_board, uint8_t *final_meta, uint64_t *stats8) {
@@ -789,7 +789,7 @@ void *oracle_env_new2(const int8_t *init, int opp, int agent_white, uint64_t see
     OEnv *e = (OEnv *)calloc(1, sizeof(OEnv));
     memcpy(e->init, init, 64);
     e->opp = opp; e->agent_black = !agent_white; e->seed = seed; e->board = board;
-    e->set_order = !opp;
+    e->set_order = 1;
     o_env_reset(e);
     return e;
 }

@@ -182,9 +182,9 @@ def policy_index(seed, board, draw, n):
 def rollout_trace(seed, board_id, plies, init=DEFAULT_BOARD, opponent=0, agent_white=True, order=None):
     """Single-board random self-play (test_benchmark.py driver shape, auto-reset); with
     opponent=1 the env answers every step with the random opponent (chess_v2.py:275-288).
-    The policy ranks the legal moves in move-set order for self-play and in action-id order
-    with an opponent; order="action" / "set" forces one (the API step's `pick` output is in
-    action-id order: the order of its legal-action mask).
+    The policy (agent and opponent) ranks the legal moves in move-set order; order="action"
+    ranks them in action-id order instead (the API step's `pick` output: the order of its
+    legal-action mask).
     Returns dict of per-ply arrays + final state + stats."""
     init = np.ascontiguousarray(init, dtype=np.int8).reshape(64)
     a = np.zeros(plies, dtype=np.int16)

@@ -293,11 +293,7 @@ struct HostEnv {
         regen();
         if (opp && agent_black) env_open_vs(s, h, g, ms, scr, pc);
     }
-    int pick() {  // self-play: the move-set order (selfplay_pick); the opponent modes: action-id order
-        if (!opp) return selfplay_pick(s, pc);
-        return ms.total ? select_action(s, g, ms, scr, (int)policy_index(pc.seed, pc.board, pc.draw++, (u32)ms.total))
-                        : A_NONE;
-    }
+    int pick() { return selfplay_pick(s, pc); }  // the random policy: move-set order
 };
 
 extern "C" void host_rollout_trace2(const int8_t* init, uint64_t seed, uint32_t board, int plies, int opp,

@@ -484,15 +484,43 @@ def gen_env_traces(v2):
     return traces
 
 
+# the device policy's move-set order (gym-chess_amd/csrc/gc_core.h sw_gen / sw_select; the
+# oracle's set_key): pawn single / double push / capture toward col+1 / col-1, the eight knight
+# jumps, slider directions (orthogonal, then diagonal), the eight king steps; by target square
+# within a set; castles last, queen side first
+_KN = [(2, -1), (2, 1), (-2, -1), (-2, 1), (1, -2), (1, 2), (-1, -2), (-1, 2)]
+_KG = [(-1, 0), (1, 0), (0, -1), (0, 1), (-1, -1), (-1, 1), (1, -1), (1, 1)]
+_SL = [(-1, 0), (1, 0), (0, 1), (0, -1), (-1, 1), (-1, -1), (1, 1), (1, -1)]
+
+
+def set_key(board64, a):
+    if a >= 4096:
+        return 28 * 64 + (0 if a in (4097, 4099) else 1)
+    f, t = a >> 6, a & 63
+    dr, dc = (t >> 3) - (f >> 3), (t & 7) - (f & 7)
+    ty = abs(int(board64[f]))
+    sg = lambda x: (x > 0) - (x < 0)  # noqa: E731
+    if ty == 6:
+        st = (0 if abs(dr) == 1 else 1) if dc == 0 else (2 if dc > 0 else 3)
+    elif ty == 5:
+        st = 4 + _KN.index((dr, dc))
+    elif ty == 1:
+        st = 20 + _KG.index((dr, dc))
+    else:
+        st = 12 + _SL.index((sg(dr), sg(dc)))
+    return st * 64 + t
+
+
 def trace_opp(v2, seed, board, n_steps, color, initial_board=None):
     """ChessEnvV2 with a CALLABLE opponent (chess_v2.py:176-177, 211-212, 276-288) that plays
     the device policy: rank k = policy_index(seed, board, draw++) over the legal list, k-th
-    in action-id order.  The driving agent draws from the same counter, so the device env
-    in opponent="random" mode must reproduce these traces exactly."""
+    in move-set order (set_key).  The driving agent draws from the same counter, so the device
+    env in opponent="random" mode must reproduce these traces exactly."""
     draw = [0]
 
     def pick(env, moves):
-        acts = sorted(env.move_to_action(m) for m in moves)
+        b64 = np.asarray(env.state["board"]).reshape(64)
+        acts = sorted((env.move_to_action(m) for m in moves), key=lambda a: set_key(b64, a))
         k = O.policy_index(seed, board, draw[0], len(acts))
         draw[0] += 1
         return acts[k]
