@@ -110,8 +110,8 @@ int gc_env_step(gc_env* e, const uint16_t* actions, int32_t* reward, uint8_t* do
  * the kernel's mask stores then writes 512 contiguous bytes; gc_env_legal_mask's host layout
  * is the transpose),
  * d_obs[n][64] (int8 board, the observation of 153-158), d_count[n] (legal actions),
- * d_pick[n] (the random policy's pick over the new list; also the env's next policy
- * action).  flags bit 0: auto-reset finished boards (the mask / obs / pick then describe
+ * d_pick[n] (a uniform Philox pick over the new list, the k-th legal action in action-id
+ * order -- the mask's order; also the env's next policy action).  flags bit 0: auto-reset finished boards (the mask / obs / pick then describe
  * the new episode).  Asynchronous on the env's stream: order your own work with it through
  * gc_env_get_stream (a hipStream_t) or gc_env_synchronize.  Reference rules only. */
 int gc_env_step_device(gc_env* e, const uint16_t* d_actions, int32_t* d_reward, uint8_t* d_done,
@@ -125,10 +125,10 @@ int gc_device_free(int device, void* ptr);
 int gc_env_copy(gc_env* e, void* dst, const void* src, uint64_t bytes, int kind);
 /* Device-resident random self-play (the test_benchmark.py driver): n_plies one-ply kernel
  * launches; each ply = one env.step() with a uniform Philox pick over the legal list, a
- * reset when done, a reset without a step when the list is empty (reason 4).  Without an
- * opponent the pick's rank indexes the legal moves in move-set order (gc_core.h sw_gen:
- * pawn / knight / slider-direction / king-step target sets, then castles; both rule sets),
- * with the random opponent in action-id order. */
+ * reset when done, a reset without a step when the list is empty (reason 4).  The policy's
+ * rank (agent and random opponent, both rule sets) indexes the legal moves in move-set order
+ * (gc_core.h sw_gen: pawn / knight / slider-direction / king-step target sets, then castles);
+ * gc_env_step_device's `pick` output indexes them in action-id order (its mask's order). */
 int gc_env_step_random(gc_env* e, int n_plies);
 /* gc_env_step_random over k board ranges on k streams of the device (k in [1, 8]; default
  * from GC_STREAMS, else 2): a range's ply p+1 waits only for its own ply p, so the ranges'
