@@ -420,13 +420,31 @@ GC_HD PinPart gen_pins_part(const Pos& s, const Gen& g) {
 // of the line form above.)  The loop runs the wave's largest aligned count, which under
 // random play averages 0.17 per board and ~1.6 per 64-board wave (tools/pin_stats.py): an
 // iteration of ~25 VALU ops against the ~440 of the four-line form.
-GC_HD PinPart gen_pins_aligned(const Pos& s, const Gen& g) {
+// Everything the pins and the set-wise generation derive from the tracked king's square alone:
+// its four lines and its leaper neighbourhoods (where an enemy pawn / knight / king checks it
+// from).  A perft leaf counts ~35 children of one position whose side to move is the same in
+// all of them and whose king did not move (the move was the other side's), so it computes this
+// once per subtree root (perft2) instead of once per child.  ks < 0: no king (all zero but the
+// masks of square 0, which nothing then uses: nothing is pinned).
+struct KingLines {
+    int ks;
+    bool white;
+    u64 fm, rm, dm, am;  // file, rank, diagonal, anti-diagonal through the king
+    u64 pawn, knight, king;  // squares from which an enemy pawn / knight / king attacks it
+};
+GC_HD KingLines king_lines(int ks, bool white) {
+    const int kq = ks < 0 ? 0 : ks;
+    const u64 kb = ks < 0 ? 0ull : bit(ks);
+    return KingLines{ks, white, file_mask(kq), row_mask(kq), diag_mask(kq), anti_mask(kq),
+                     pawn_att_set(kb, white), knight_set(kb), king_set(kb)};
+}
+GC_HD PinPart gen_pins_aligned_kl(const Pos& s, const Gen& g, const KingLines& kl) {
     PinPart p = {0, 0, 0, 0};
     if (g.ks < 0) return p;  // "King not present": no filter, no castling, no king moves
     const int ks = g.ks;
-    const u64 kb = bit(ks), opp = g.opp, occ = g.occ, own = g.own;
-    p.checkers = (pawn_att_set(kb, g.white) & s.p & opp) | (knight_set(kb) & s.n & opp) | (king_set(kb) & s.k & opp);
-    const u64 fm = file_mask(ks), rm = row_mask(ks), dm = diag_mask(ks), am = anti_mask(ks);
+    const u64 opp = g.opp, occ = g.occ, own = g.own;
+    p.checkers = (kl.pawn & s.p & opp) | (kl.knight & s.n & opp) | (kl.king & s.k & opp);
+    const u64 fm = kl.fm, rm = kl.rm, dm = kl.dm, am = kl.am;
     u64 cand = ((s.r | s.q) & opp & (fm | rm)) | ((s.b | s.q) & opp & (dm | am));
     while (cand) {
         const int x = ctz(cand);
@@ -445,6 +463,7 @@ GC_HD PinPart gen_pins_aligned(const Pos& s, const Gen& g) {
     }
     return p;
 }
+GC_HD PinPart gen_pins_aligned(const Pos& s, const Gen& g) { return gen_pins_aligned_kl(s, g, king_lines(g.ks, g.white)); }
 GC_HD void gen_pins_finish(Gen& g, const PinPart& p) {
     if (g.ks < 0) return;
     u64 checkers = p.checkers, block = p.block;
@@ -840,11 +859,10 @@ GC_HD int sw_popc(const u64* t, int lo, int hi) {
 }
 // a square on the tracked king's lines (0 when there is no king: then nothing is pinned)
 GC_HD int sw_ksq(const Gen& g) { return g.ks < 0 ? 0 : g.ks; }
-GC_HD void sw_pawns(const Pos& s, const Gen& g, u64* t) {
+GC_HD void sw_pawns_kl(const Pos& s, const Gen& g, const KingLines& kl, u64* t) {
     const u64 cm = g.checkmask, empty = ~g.occ, opp = g.opp, P = s.p & g.own, pr = g.pinrays;
-    const int kq = sw_ksq(g);
     const u64 fp = P & ~g.pinned, pp = P & g.pinned;
-    const u64 pf = pp & file_mask(kq), pd = pp & diag_mask(kq), pa = pp & anti_mask(kq);
+    const u64 pf = pp & kl.fm, pd = pp & kl.dm, pa = pp & kl.am;
     if (g.white) {  // lib.rs:935-958, p = +1: toward row 0
         t[SW_P1] = ((fp >> 8) | ((pf >> 8) & pr)) & empty & cm;
         t[SW_P2] = (((fp & ROW6) >> 16) | (((pf & ROW6) >> 16) & pr)) & empty & cm;
@@ -857,6 +875,7 @@ GC_HD void sw_pawns(const Pos& s, const Gen& g, u64* t) {
         t[SW_PR] = (((fp << 7) | ((pa << 7) & pr)) & ~FILE_H) & opp & cm;  // row+1 col-1: anti-diagonal
     }
 }
+GC_HD void sw_pawns(const Pos& s, const Gen& g, u64* t) { sw_pawns_kl(s, g, king_lines(g.ks, g.white), t); }
 // xm: extra target mask (FIDE: enemy kings are never captured)
 GC_HD void sw_knights(const Pos& s, const Gen& g, u64* t, u64 xm = ~0ull) {
     const u64 N = s.n & g.own & ~g.pinned, tm = ~g.own & g.checkmask & xm;
@@ -930,20 +949,19 @@ GC_HD int ray_count(u64 gen, u64 empty, u64 wrap, u64 tmask) {
 struct SliderGens {
     u64 f, r, d, a;  // generators of the file, rank, diagonal and anti-diagonal directions
 };
-GC_HD SliderGens slider_gens(const Pos& s, const Gen& g) {
-    const int kq = g.ks < 0 ? 0 : g.ks;  // no king: nothing is pinned
+GC_HD SliderGens slider_gens_kl(const Pos& s, const Gen& g, const KingLines& kl) {
     const u64 pin = g.pinned, oRQ = (s.r | s.q) & g.own, oBQ = (s.b | s.q) & g.own;
     const u64 fRQ = oRQ & ~pin, fBQ = oBQ & ~pin, pRQ = oRQ & pin, pBQ = oBQ & pin;
-    return SliderGens{fRQ | (pRQ & file_mask(kq)), fRQ | (pRQ & row_mask(kq)), fBQ | (pBQ & diag_mask(kq)),
-                      fBQ | (pBQ & anti_mask(kq))};
+    return SliderGens{fRQ | (pRQ & kl.fm), fRQ | (pRQ & kl.rm), fBQ | (pBQ & kl.dm), fBQ | (pBQ & kl.am)};
 }
+GC_HD SliderGens slider_gens(const Pos& s, const Gen& g) { return slider_gens_kl(s, g, king_lines(g.ks, g.white)); }
 // pawns (set-wise, pinned ones included), knights, kings (count_moves without the sliders)
-GC_HD int count_nonsliders(const Pos& s, const Gen& g) {
+GC_HD int count_nonsliders_kl(const Pos& s, const Gen& g, const KingLines& kl) {
     const u64 own = g.own, tm = ~own & g.checkmask;
     int total = popc(g.castles);
     // pawns (lib.rs:935-958; Q1: the double push tests only the destination): sw_pawns' sets
     u64 pt[4];
-    sw_pawns(s, g, pt);
+    sw_pawns_kl(s, g, kl, pt);
     total += popc(pt[0]) + popc(pt[1]) + popc(pt[2]) + popc(pt[3]);
     // knights (a pinned knight never has a move on its pin segment)
     const u64 N = s.n & own & ~g.pinned;
@@ -961,6 +979,7 @@ GC_HD int count_nonsliders(const Pos& s, const Gen& g) {
     }
     return total;
 }
+GC_HD int count_nonsliders(const Pos& s, const Gen& g) { return count_nonsliders_kl(s, g, king_lines(g.ks, g.white)); }
 GC_HD int count_moves(const Pos& s, const Gen& g) {
     const u64 tm = ~g.own & g.checkmask, empty = ~g.occ;
     const SliderGens G = slider_gens(s, g);
@@ -988,13 +1007,17 @@ GC_HD void ray_fill_pair(u64 ge, u64 go, u64 empty, u64 wrap, u64& ae, u64& ao) 
     ae = sh<SH, LEFT>(ge) & wrap;
     ao = sh<SH, LEFT>(go) & wrap;
 }
-GC_HD int count_position(const Pos& s) {
+// kh: the king lines of the side to move if its tracked king sits on kh.ks (perft: computed
+// once per subtree root); otherwise (a king captured, Q7) they are recomputed here
+GC_HD int count_position_kl(const Pos& s, const KingLines& kh) {
     Gen g;
     gen_base(s, g);
-    gen_pins(s, g);
+    KingLines kl = kh;
+    if (g.ks != kh.ks || g.white != kh.white) kl = king_lines(g.ks, g.white);
+    gen_pins_finish(g, gen_pins_aligned_kl(s, g, kl));
     const u64 empty = ~g.occ, tm = ~g.own & g.checkmask;
     const u64 eRQ = (s.r | s.q) & g.opp, eBQ = (s.b | s.q) & g.opp;
-    const SliderGens G = slider_gens(s, g);
+    const SliderGens G = slider_gens_kl(s, g, kl);
     u64 att = 0, ae, ao;
     int n = 0;
 #define GC_PAIR(SH, LEFT, GE, GO, WRAP)                  \
@@ -1014,7 +1037,11 @@ GC_HD int count_position(const Pos& s) {
         g.enemy_att = att | side_attacks_leapers(s, !g.white);
         gen_castles(s, g);
     }
-    return n + count_nonsliders(s, g);
+    return n + count_nonsliders_kl(s, g, kl);
+}
+GC_HD int count_position(const Pos& s) {
+    const bool white = (s.meta & M_WHITE) != 0;
+    return count_position_kl(s, king_lines(tracked_king(s, white), white));
 }
 
 // ---- pick by rank in ACTION-ID order (the random self-play policy) ----------------------

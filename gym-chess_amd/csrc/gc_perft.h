@@ -70,10 +70,12 @@ GC_HD uint64_t perft_small(const Pos& root, int depth, SA& sa, SB& sb) {
     gen_moves(root, g0, m0, sa);
     uint64_t nodes = 0;
     MoveWalk w0(g0);
+    // the children's side to move is the other side, whose king the root's moves leave in place
+    const KingLines k1l = king_lines(tracked_king(root, !g0.white), !g0.white);
     for (int k1 = 0; k1 < m0.total; k1++) {
         Pos c1 = child_of(root, g0.white, next_child(w0, root, g0, m0, sa, k1));
         if (depth == 2) {
-            nodes += (uint64_t)count_position(c1);
+            nodes += (uint64_t)count_position_kl(c1, k1l);
             continue;
         }
         Gen g1;
@@ -81,9 +83,10 @@ GC_HD uint64_t perft_small(const Pos& root, int depth, SA& sa, SB& sb) {
         gen_init(c1, g1);
         gen_moves(c1, g1, m1, sb);
         MoveWalk w1(g1);
+        const KingLines k2l = king_lines(tracked_king(c1, !g1.white), !g1.white);
         for (int k2 = 0; k2 < m1.total; k2++) {
             Pos c2 = child_of(c1, g1.white, next_child(w1, c1, g1, m1, sb, k2));
-            nodes += (uint64_t)count_position(c2);
+            nodes += (uint64_t)count_position_kl(c2, k2l);
         }
     }
     return nodes;
@@ -99,6 +102,7 @@ GC_HD uint64_t perft2(const Pos& root, SA& sa) {
     gen_moves(root, g0, m0, sa);
     uint64_t nodes = 0;
     MoveWalk w0(g0);
+    const KingLines k1l = king_lines(tracked_king(root, !g0.white), !g0.white);  // as perft_small
     for (int k1 = 0; k1 < m0.total; k1++) {
         Pos c1 = child_of(root, g0.white, next_child(w0, root, g0, m0, sa, k1));
 #ifdef GC_PERFT_UNFUSED  // A/B: the map and the count in two passes
@@ -106,7 +110,7 @@ GC_HD uint64_t perft2(const Pos& root, SA& sa) {
         gen_init(c1, g1);
         nodes += (uint64_t)count_moves(c1, g1);
 #else
-        nodes += (uint64_t)count_position(c1);
+        nodes += (uint64_t)count_position_kl(c1, k1l);
 #endif
     }
     return nodes;
