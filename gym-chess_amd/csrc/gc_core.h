@@ -429,14 +429,38 @@ GC_HD PinPart gen_pins_part(const Pos& s, const Gen& g) {
 struct KingLines {
     int ks;
     bool white;
+    u64 kings;           // the side's kings the lines were computed for
+
     u64 fm, rm, dm, am;  // file, rank, diagonal, anti-diagonal through the king
     u64 pawn, knight, king;  // squares from which an enemy pawn / knight / king attacks it
 };
-GC_HD KingLines king_lines(int ks, bool white) {
+GC_HD KingLines king_lines(int ks, bool white, u64 kings = 0) {
     const int kq = ks < 0 ? 0 : ks;
     const u64 kb = ks < 0 ? 0ull : bit(ks);
-    return KingLines{ks, white, file_mask(kq), row_mask(kq), diag_mask(kq), anti_mask(kq),
+    return KingLines{ks, white, kings, file_mask(kq), row_mask(kq), diag_mask(kq), anti_mask(kq),
                      pawn_att_set(kb, white), knight_set(kb), king_set(kb)};
+}
+// the lines of the side to move of s, with its kings recorded (the perft hint)
+GC_HD KingLines king_lines_of(const Pos& s, bool white) {
+    const u64 occ = occ_of(s), kings = s.k & (white ? s.w : (occ & ~s.w));
+    return king_lines(tracked_king(s, white), white, kings);
+}
+// gen_base with the tracked king taken from a hint whose side and kings match (else searched)
+GC_HD void gen_base_ks(const Pos& s, Gen& g, const KingLines& kh) {
+    const bool white = s.meta & M_WHITE;
+    g.white = white;
+    g.occ = occ_of(s);
+    g.own = white ? s.w : (g.occ & ~s.w);
+    g.opp = g.occ ^ g.own;
+    const u64 kings = s.k & g.own;
+    g.ks = kh.ks;
+    if (kings != kh.kings || white != kh.white) g.ks = tracked_king(s, white);
+    g.checkmask = ~0ull;
+    g.pinned = 0;
+    g.pinrays = 0;
+    g.enemy_att = 0;
+    g.castles = 0;
+    g.in_check = false;
 }
 GC_HD PinPart gen_pins_aligned_kl(const Pos& s, const Gen& g, const KingLines& kl) {
     PinPart p = {0, 0, 0, 0};
@@ -1011,7 +1035,7 @@ GC_HD void ray_fill_pair(u64 ge, u64 go, u64 empty, u64 wrap, u64& ae, u64& ao) 
 // once per subtree root); otherwise (a king captured, Q7) they are recomputed here
 GC_HD int count_position_kl(const Pos& s, const KingLines& kh) {
     Gen g;
-    gen_base(s, g);
+    gen_base_ks(s, g, kh);  // the tracked king from the hint while the side's kings are the hint's
     KingLines kl = kh;
     if (g.ks != kh.ks || g.white != kh.white) kl = king_lines(g.ks, g.white);
     gen_pins_finish(g, gen_pins_aligned_kl(s, g, kl));
@@ -1039,10 +1063,7 @@ GC_HD int count_position_kl(const Pos& s, const KingLines& kh) {
     }
     return n + count_nonsliders_kl(s, g, kl);
 }
-GC_HD int count_position(const Pos& s) {
-    const bool white = (s.meta & M_WHITE) != 0;
-    return count_position_kl(s, king_lines(tracked_king(s, white), white));
-}
+GC_HD int count_position(const Pos& s) { return count_position_kl(s, king_lines_of(s, (s.meta & M_WHITE) != 0)); }
 
 // ---- pick by rank in ACTION-ID order (the random self-play policy) ----------------------
 // The driver draws k uniformly in [0, #legal); k maps to the k-th legal action in ascending

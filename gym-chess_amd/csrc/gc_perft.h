@@ -71,7 +71,7 @@ GC_HD uint64_t perft_small(const Pos& root, int depth, SA& sa, SB& sb) {
     uint64_t nodes = 0;
     MoveWalk w0(g0);
     // the children's side to move is the other side, whose king the root's moves leave in place
-    const KingLines k1l = king_lines(tracked_king(root, !g0.white), !g0.white);
+    const KingLines k1l = king_lines_of(root, !g0.white);
     for (int k1 = 0; k1 < m0.total; k1++) {
         Pos c1 = child_of(root, g0.white, next_child(w0, root, g0, m0, sa, k1));
         if (depth == 2) {
@@ -83,7 +83,7 @@ GC_HD uint64_t perft_small(const Pos& root, int depth, SA& sa, SB& sb) {
         gen_init(c1, g1);
         gen_moves(c1, g1, m1, sb);
         MoveWalk w1(g1);
-        const KingLines k2l = king_lines(tracked_king(c1, !g1.white), !g1.white);
+        const KingLines k2l = king_lines_of(c1, !g1.white);
         for (int k2 = 0; k2 < m1.total; k2++) {
             Pos c2 = child_of(c1, g1.white, next_child(w1, c1, g1, m1, sb, k2));
             nodes += (uint64_t)count_position_kl(c2, k2l);
@@ -102,7 +102,7 @@ GC_HD uint64_t perft2(const Pos& root, SA& sa) {
     gen_moves(root, g0, m0, sa);
     uint64_t nodes = 0;
     MoveWalk w0(g0);
-    const KingLines k1l = king_lines(tracked_king(root, !g0.white), !g0.white);  // as perft_small
+    const KingLines k1l = king_lines_of(root, !g0.white);  // as perft_small
     for (int k1 = 0; k1 < m0.total; k1++) {
         Pos c1 = child_of(root, g0.white, next_child(w0, root, g0, m0, sa, k1));
 #ifdef GC_PERFT_UNFUSED  // A/B: the map and the count in two passes
