@@ -1889,31 +1889,87 @@ struct gc_engine {
     int cap_n = 0, cap_list = 0;
     u64* bb = nullptr; u32* meta = nullptr;       // input states
     u64* bb2 = nullptr; u32* meta2 = nullptr;     // output states
+    // The host-facing buffers of one call are views into ONE device block (dio), laid out for
+    // the call's n by engine_layout, mirrored by a pinned host block (hio): a call stages its
+    // inputs with one host-to-device copy and returns its outputs with one copy back (a
+    // single-board call is latency-bound: every copy is a round trip)
+    uint8_t* dio = nullptr; uint8_t* hio = nullptr; size_t io_cap = 0;
     int8_t* mbox = nullptr; uint8_t* m8 = nullptr; uint8_t* side = nullptr;
     uint16_t* acts = nullptr; int32_t* i32a = nullptr; int32_t* i32b = nullptr;
     uint16_t* list = nullptr; uint64_t* u64o = nullptr;
     int rules = 0;  // 0 reference (lib.rs), 1 FIDE (gc_fide.h)
 };
+// byte offsets of the views for n boards and a list capacity lc (256-B aligned)
+struct EngineLayout {
+    size_t mbox, m8, side, acts, i32a, i32b, list, end;
+};
+static EngineLayout engine_offsets(size_t n, size_t lc) {
+    auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    EngineLayout o;
+    o.mbox = 0;
+    o.m8 = up(o.mbox + 64 * n);
+    o.side = up(o.m8 + 8 * n);
+    o.acts = up(o.side + n);
+    o.i32a = up(o.acts + 2 * n);
+    o.i32b = up(o.i32a + 4 * n);
+    o.list = up(o.i32b + 4 * n);
+    o.end = up(o.list + 2 * lc * n);
+    return o;
+}
+static EngineLayout engine_layout(gc_engine* e, int n, int lc) {
+    EngineLayout o = engine_offsets((size_t)n, (size_t)lc);
+    e->mbox = reinterpret_cast<int8_t*>(e->dio + o.mbox);
+    e->m8 = e->dio + o.m8;
+    e->side = e->dio + o.side;
+    e->acts = reinterpret_cast<uint16_t*>(e->dio + o.acts);
+    e->i32a = reinterpret_cast<int32_t*>(e->dio + o.i32a);
+    e->i32b = reinterpret_cast<int32_t*>(e->dio + o.i32b);
+    e->list = reinterpret_cast<uint16_t*>(e->dio + o.list);
+    return o;
+}
 
 static void engine_free_bufs(gc_engine* e) {
-    void* ps[] = {e->bb, e->meta, e->bb2, e->meta2, e->mbox, e->m8, e->side, e->acts, e->i32a, e->i32b, e->list, e->u64o};
+    void* ps[] = {e->bb, e->meta, e->bb2, e->meta2, e->dio, e->u64o};
     for (void* p : ps) if (p) (void)hipFree(p);
-    e->bb = nullptr; e->meta = nullptr; e->bb2 = nullptr; e->meta2 = nullptr; e->mbox = nullptr; e->m8 = nullptr;
-    e->side = nullptr; e->acts = nullptr; e->i32a = nullptr; e->i32b = nullptr; e->list = nullptr; e->u64o = nullptr;
-    e->cap_n = 0; e->cap_list = 0;
+    if (e->hio) (void)hipHostFree(e->hio);
+    e->bb = nullptr; e->meta = nullptr; e->bb2 = nullptr; e->meta2 = nullptr; e->dio = nullptr; e->hio = nullptr;
+    e->mbox = nullptr; e->m8 = nullptr; e->side = nullptr; e->acts = nullptr; e->i32a = nullptr; e->i32b = nullptr;
+    e->list = nullptr; e->u64o = nullptr;
+    e->cap_n = 0; e->cap_list = 0; e->io_cap = 0;
 }
 
 static int engine_reserve(gc_engine* e, int n, int listcap) {
     if (n <= e->cap_n && listcap <= e->cap_list) return 0;
     int nn = n > e->cap_n ? n : e->cap_n, lc = listcap > e->cap_list ? listcap : e->cap_list;
     engine_free_bufs(e);
+    const size_t io = engine_offsets((size_t)nn, (size_t)lc).end;
     if (dalloc(&e->bb, (size_t)NBB * nn) || dalloc(&e->meta, nn) || dalloc(&e->bb2, (size_t)NBB * nn) ||
-        dalloc(&e->meta2, nn) || dalloc(&e->mbox, (size_t)64 * nn) || dalloc(&e->m8, (size_t)8 * nn) ||
-        dalloc(&e->side, nn) || dalloc(&e->acts, nn) || dalloc(&e->i32a, nn) || dalloc(&e->i32b, nn) ||
-        dalloc(&e->list, (size_t)lc * nn) || dalloc(&e->u64o, nn))
+        dalloc(&e->meta2, nn) || dalloc(&e->dio, io) || dalloc(&e->u64o, nn))
         return -1;
+    hipError_t he = hipHostMalloc((void**)&e->hio, io, hipHostMallocDefault);
+    if (he != hipSuccess) return fail(std::string("hipHostMalloc: ") + hipGetErrorString(he));
+    e->io_cap = io;
     e->cap_n = nn;
     e->cap_list = lc;
+    return 0;
+}
+// one call's staging: the inputs present (side / acts may be null) into the pinned block, one
+// copy to the device; the views laid out for (n, lc)
+static int engine_stage(gc_engine* e, int n, int lc, const int8_t* boards, const uint8_t* meta, const uint8_t* side,
+                        const uint16_t* acts, EngineLayout& o) {
+    o = engine_layout(e, n, lc);
+    std::memcpy(e->hio + o.mbox, boards, (size_t)64 * n);
+    std::memcpy(e->hio + o.m8, meta, (size_t)8 * n);
+    size_t end = o.m8 + (size_t)8 * n;
+    if (side) { std::memcpy(e->hio + o.side, side, (size_t)n); end = o.side + n; }
+    if (acts) { std::memcpy(e->hio + o.acts, acts, (size_t)2 * n); end = o.acts + (size_t)2 * n; }
+    HIPCHK(hipMemcpyAsync(e->dio, e->hio, end, hipMemcpyHostToDevice, e->stream));
+    return 0;
+}
+// the byte range [a, b) of the device block back into the pinned one, then wait
+static int engine_fetch(gc_engine* e, size_t a, size_t b) {
+    HIPCHK(hipMemcpyAsync(e->hio + a, e->dio + a, b - a, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
     return 0;
 }
 
@@ -1923,14 +1979,15 @@ static int check_boards(int n, const int8_t* boards) {
     return 0;
 }
 
-static int engine_upload(gc_engine* e, int n, const int8_t* boards, const uint8_t* meta, const uint8_t* side) {
+// side: staged when given, and the side to move of the import unless side_import is false
+static int engine_upload(gc_engine* e, int n, const int8_t* boards, const uint8_t* meta, const uint8_t* side,
+                         EngineLayout& o, int lc = 1, const uint16_t* acts = nullptr, bool side_import = true) {
     if (n <= 0) return fail("n must be > 0");
     if (!boards || !meta) return fail("null boards/meta");
     if (check_boards(n, boards)) return -1;
     HIPCHK(hipSetDevice(e->device));
-    HIPCHK(hipMemcpyAsync(e->mbox, boards, (size_t)64 * n, hipMemcpyHostToDevice, e->stream));
-    HIPCHK(hipMemcpyAsync(e->m8, meta, (size_t)8 * n, hipMemcpyHostToDevice, e->stream));
-    if (side) HIPCHK(hipMemcpyAsync(e->side, side, n, hipMemcpyHostToDevice, e->stream));
+    if (engine_stage(e, n, lc, boards, meta, side, acts, o)) return -1;
+    if (!side_import) side = nullptr;
     SoA st{e->bb, e->meta, n};
     if (e->rules) k_fimport<<<grid_for(n), BLOCK, 0, e->stream>>>(e->mbox, e->m8, side ? e->side : nullptr, st);
     else k_import<<<grid_for(n), BLOCK, 0, e->stream>>>(e->mbox, e->m8, side ? e->side : nullptr, st);
@@ -1981,13 +2038,14 @@ extern "C" int gc_engine_get_possible_moves(gc_engine* e, int n, const int8_t* b
     if (!e || !moves || !counts || !player_white) return fail("null argument");
     if (cap <= 0) return fail("cap must be > 0");
     if (engine_reserve(e, n, cap)) return -1;
-    if (engine_upload(e, n, boards, meta, player_white)) return -1;
+    EngineLayout o;
+    if (engine_upload(e, n, boards, meta, player_white, o, cap)) return -1;
     if (e->rules) k_flist<<<grid_for(n), BLOCK, 0, e->stream>>>(SoA{e->bb, e->meta, n}, attack ? 1 : 0, cap, e->list, e->i32a);
     else k_list<<<grid_for(n), BLOCK, 0, e->stream>>>(SoA{e->bb, e->meta, n}, attack ? 1 : 0, cap, e->list, e->i32a);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(moves, e->list, (size_t)2 * cap * n, hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(hipMemcpyAsync(counts, e->i32a, (size_t)4 * n, hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(hipStreamSynchronize(e->stream));
+    if (engine_fetch(e, o.i32a, o.list + (size_t)2 * cap * n)) return -1;
+    std::memcpy(moves, e->hio + o.list, (size_t)2 * cap * n);
+    std::memcpy(counts, e->hio + o.i32a, (size_t)4 * n);
     return 0;
 }
 
@@ -1995,7 +2053,8 @@ extern "C" int gc_engine_get_castle_moves(gc_engine* e, int n, const int8_t* boa
                                           const uint8_t* player_white, uint16_t* moves, int32_t* counts) {
     if (!e || !moves || !counts || !player_white) return fail("null argument");
     if (engine_reserve(e, n, 2)) return -1;
-    if (engine_upload(e, n, boards, meta, player_white)) return -1;
+    EngineLayout o;
+    if (engine_upload(e, n, boards, meta, player_white, o, 2)) return -1;
     std::vector<u64> mask((size_t)65 * n);
     u64* dmask = nullptr;
     if (dalloc(&dmask, (size_t)65 * n)) return -1;
@@ -2028,20 +2087,20 @@ extern "C" int gc_engine_next_state(gc_engine* e, int n, const int8_t* boards, c
     if (engine_reserve(e, n, 1)) return -1;
     // FIDE: the player argument is the side to move; reference: it only steers next_state's
     // promotion colour and rights logic (lib.rs:679-784), the state keeps current_player
-    if (engine_upload(e, n, boards, meta, e->rules ? player_white : nullptr)) return -1;
-    HIPCHK(hipMemcpyAsync(e->side, player_white, n, hipMemcpyHostToDevice, e->stream));
-    HIPCHK(hipMemcpyAsync(e->acts, actions, (size_t)2 * n, hipMemcpyHostToDevice, e->stream));
+    // the import reads side only under FIDE (the player argument is the side to move there)
+    EngineLayout o;
+    if (engine_upload(e, n, boards, meta, player_white, o, 1, actions, e->rules != 0)) return -1;
     SoA in{e->bb, e->meta, n}, out{e->bb2, e->meta2, n};
     if (e->rules) k_fnext_state<<<grid_for(n), BLOCK, 0, e->stream>>>(in, e->acts, out, e->i32a, e->i32b);
     else k_next_state<<<grid_for(n), BLOCK, 0, e->stream>>>(in, e->side, e->acts, out, e->i32a, e->i32b);
     HIPCHK(hipGetLastError());
     engine_export(e, out);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(out_boards, e->mbox, (size_t)64 * n, hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(hipMemcpyAsync(out_meta, e->m8, (size_t)8 * n, hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(hipMemcpyAsync(rewards, e->i32a, (size_t)4 * n, hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(hipMemcpyAsync(status, e->i32b, (size_t)4 * n, hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(hipStreamSynchronize(e->stream));
+    if (engine_fetch(e, 0, o.i32b + (size_t)4 * n)) return -1;
+    std::memcpy(out_boards, e->hio + o.mbox, (size_t)64 * n);
+    std::memcpy(out_meta, e->hio + o.m8, (size_t)8 * n);
+    std::memcpy(rewards, e->hio + o.i32a, (size_t)4 * n);
+    std::memcpy(status, e->hio + o.i32b, (size_t)4 * n);
     return 0;
 }
 
@@ -2049,16 +2108,17 @@ extern "C" int gc_engine_update_state(gc_engine* e, int n, const int8_t* boards,
                                       int8_t* out_boards, uint8_t* out_meta) {
     if (!e || !out_boards || !out_meta) return fail("null argument");
     if (engine_reserve(e, n, 1)) return -1;
-    if (engine_upload(e, n, boards, meta, nullptr)) return -1;
+    EngineLayout o;
+    if (engine_upload(e, n, boards, meta, nullptr, o)) return -1;
     SoA st{e->bb, e->meta, n};
     if (e->rules) k_fupdate_state<<<grid_for(n), BLOCK, 0, e->stream>>>(st);
     else k_update_state<<<grid_for(n), BLOCK, 0, e->stream>>>(st);
     HIPCHK(hipGetLastError());
     engine_export(e, st);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(out_boards, e->mbox, (size_t)64 * n, hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(hipMemcpyAsync(out_meta, e->m8, (size_t)8 * n, hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(hipStreamSynchronize(e->stream));
+    if (engine_fetch(e, 0, o.m8 + (size_t)8 * n)) return -1;
+    std::memcpy(out_boards, e->hio + o.mbox, (size_t)64 * n);
+    std::memcpy(out_meta, e->hio + o.m8, (size_t)8 * n);
     return 0;
 }
 
@@ -2300,7 +2360,8 @@ extern "C" int gc_engine_perft(gc_engine* e, int n, const int8_t* boards, const 
     if (!e || !nodes) return fail("null argument");
     if (depth < 0 || depth > PERFT_MAXD) return fail("depth must be in [0, 8]");
     if (engine_reserve(e, n, 1)) return -1;
-    if (engine_upload(e, n, boards, meta, nullptr)) return -1;
+    EngineLayout o;
+    if (engine_upload(e, n, boards, meta, nullptr, o)) return -1;
     if (perft_device(e->stream, SoA{e->bb, e->meta, n}, depth, e->u64o, e->rules)) return -1;
     HIPCHK(hipMemcpyAsync(nodes, e->u64o, (size_t)8 * n, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
