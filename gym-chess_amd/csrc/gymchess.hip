@@ -157,23 +157,24 @@ struct LdsScratch {
 // ----------------------------------------------------------------------------- engine kernels
 // import: mailbox int8[64] + meta8 {side, wkc, wqc, bkc, bqc, ...} -> bitboards, with the
 // State::new rights forcing (lib.rs:295-336).  `side` may override meta8[0] (player arg).
-__global__ void k_import(const int8_t* __restrict__ boards, const uint8_t* __restrict__ meta8,
-                         const uint8_t* __restrict__ side, SoA out) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= out.n) return;
+__device__ __forceinline__ Pos import_one(const int8_t* __restrict__ boards, const uint8_t* __restrict__ meta8,
+                                          const uint8_t* __restrict__ side, int i) {
     const uint8_t* m = meta8 + 8 * (size_t)i;
     bool white = side ? side[i] != 0 : m[0] != 0;
     u32 meta = (white ? M_WHITE : 0u) | (m[1] ? M_WKC : 0u) | (m[2] ? M_WQC : 0u) | (m[3] ? M_BKC : 0u) |
                (m[4] ? M_BQC : 0u) | (m[5] ? M_WCHK : 0u) | (m[6] ? M_BCHK : 0u) | ((u32)m[7] << M_MC_SHIFT);
     Pos s = from_mailbox(boards + 64 * (size_t)i, meta);
     s.meta = (s.meta & ~(u32)M_RIGHTS) | eff_rights(s);
-    out.store(i, s);
+    return s;
+}
+__global__ void k_import(const int8_t* __restrict__ boards, const uint8_t* __restrict__ meta8,
+                         const uint8_t* __restrict__ side, SoA out) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= out.n) return;
+    out.store(i, import_one(boards, meta8, side, i));
 }
 
-__global__ void k_export(SoA in, int8_t* __restrict__ boards, uint8_t* __restrict__ meta8) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= in.n) return;
-    Pos s = in.load(i);
+__device__ __forceinline__ void export_one(const Pos& s, int8_t* __restrict__ boards, uint8_t* __restrict__ meta8, int i) {
     if (boards) to_mailbox(s, boards + 64 * (size_t)i);
     if (meta8) {
         uint8_t* m = meta8 + 8 * (size_t)i;
@@ -182,13 +183,16 @@ __global__ void k_export(SoA in, int8_t* __restrict__ boards, uint8_t* __restric
         m[6] = (s.meta & M_BCHK) != 0; m[7] = (uint8_t)mc_of(s.meta);
     }
 }
+__global__ void k_export(SoA in, int8_t* __restrict__ boards, uint8_t* __restrict__ meta8) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= in.n) return;
+    export_one(in.load(i), boards, meta8, i);
+}
 
 // ordered move list in reference order (lib.rs:460-563 + 1468-1479); attack mode lists the
 // unfiltered attack-mode moves and no castles.  count may exceed cap (list truncated).
-__global__ void k_list(SoA in, int attack, int cap, uint16_t* __restrict__ out, int32_t* __restrict__ counts) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= in.n) return;
-    Pos s = in.load(i);
+__device__ __forceinline__ void list_one(const Pos& s, int attack, int cap, uint16_t* __restrict__ out,
+                                         int32_t* __restrict__ counts, int i) {
     Gen g;
     gen_init(s, g);
     uint16_t* o = out + (size_t)cap * i;
@@ -210,6 +214,20 @@ __global__ void k_list(SoA in, int attack, int cap, uint16_t* __restrict__ out, 
         if (g.castles & 2) { if (n < cap) o[n] = g.white ? A_KSW : A_KSB; n++; }
     }
     counts[i] = n;
+}
+__global__ void k_list(SoA in, int attack, int cap, uint16_t* __restrict__ out, int32_t* __restrict__ counts) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= in.n) return;
+    list_one(in.load(i), attack, cap, out, counts, i);
+}
+// the engine calls' one-launch forms (reference rules): mailbox in, the op, mailbox out -- a
+// single-board call pays one launch instead of three
+__global__ void k_list_mb(const int8_t* __restrict__ boards, const uint8_t* __restrict__ meta8,
+                          const uint8_t* __restrict__ side, int n, int attack, int cap, uint16_t* __restrict__ out,
+                          int32_t* __restrict__ counts) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    list_one(import_one(boards, meta8, side, i), attack, cap, out, counts, i);
 }
 
 // legal action mask: 64 words (from-square -> target bitboard) + 1 word of castle bits
@@ -236,11 +254,9 @@ __global__ void k_mask(SoA in, u64* __restrict__ mask, int32_t* __restrict__ cou
 
 // next_state (lib.rs:1422-1452): move + update_state; status 0 ok, 1 both kings checked,
 // -1 empty from-square (reference panics), -2 bad action
-__global__ void k_next_state(SoA in, const uint8_t* __restrict__ player_white, const uint16_t* __restrict__ actions,
-                             SoA out, int32_t* __restrict__ rewards, int32_t* __restrict__ status) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= in.n) return;
-    Pos s = in.load(i);
+__device__ __forceinline__ Pos next_state_one(Pos s, const uint8_t* __restrict__ player_white,
+                                              const uint16_t* __restrict__ actions, int32_t* __restrict__ rewards,
+                                              int32_t* __restrict__ status, int i) {
     int rw = 0;
     bool irrev;
     int rc = apply_move(s, player_white[i] != 0, actions[i], &rw, &irrev);
@@ -249,9 +265,24 @@ __global__ void k_next_state(SoA in, const uint8_t* __restrict__ player_white, c
         s.meta = (s.meta & ~(u32)(M_WCHK | M_BCHK)) | chk;
         if ((chk & (M_WCHK | M_BCHK)) == (M_WCHK | M_BCHK)) rc = 1;
     }
-    out.store(i, s);
     rewards[i] = rw;
     status[i] = rc;
+    return s;
+}
+__global__ void k_next_state(SoA in, const uint8_t* __restrict__ player_white, const uint16_t* __restrict__ actions,
+                             SoA out, int32_t* __restrict__ rewards, int32_t* __restrict__ status) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= in.n) return;
+    out.store(i, next_state_one(in.load(i), player_white, actions, rewards, status, i));
+}
+// mailbox in and out (in place: a thread reads and writes only its own board)
+__global__ void k_next_state_mb(int8_t* __restrict__ boards, uint8_t* __restrict__ meta8,
+                                const uint8_t* __restrict__ player_white, const uint16_t* __restrict__ actions, int n,
+                                int32_t* __restrict__ rewards, int32_t* __restrict__ status) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    export_one(next_state_one(import_one(boards, meta8, nullptr, i), player_white, actions, rewards, status, i),
+               boards, meta8, i);
 }
 
 // update_state (lib.rs:1502-1511)
@@ -2039,9 +2070,17 @@ extern "C" int gc_engine_get_possible_moves(gc_engine* e, int n, const int8_t* b
     if (cap <= 0) return fail("cap must be > 0");
     if (engine_reserve(e, n, cap)) return -1;
     EngineLayout o;
-    if (engine_upload(e, n, boards, meta, player_white, o, cap)) return -1;
-    if (e->rules) k_flist<<<grid_for(n), BLOCK, 0, e->stream>>>(SoA{e->bb, e->meta, n}, attack ? 1 : 0, cap, e->list, e->i32a);
-    else k_list<<<grid_for(n), BLOCK, 0, e->stream>>>(SoA{e->bb, e->meta, n}, attack ? 1 : 0, cap, e->list, e->i32a);
+    if (e->rules) {
+        if (engine_upload(e, n, boards, meta, player_white, o, cap)) return -1;
+        k_flist<<<grid_for(n), BLOCK, 0, e->stream>>>(SoA{e->bb, e->meta, n}, attack ? 1 : 0, cap, e->list, e->i32a);
+    } else {  // one launch: import + list
+        if (n <= 0) return fail("n must be > 0");
+        if (!boards || !meta) return fail("null boards/meta");
+        if (check_boards(n, boards)) return -1;
+        HIPCHK(hipSetDevice(e->device));
+        if (engine_stage(e, n, cap, boards, meta, player_white, nullptr, o)) return -1;
+        k_list_mb<<<grid_for(n), BLOCK, 0, e->stream>>>(e->mbox, e->m8, e->side, n, attack ? 1 : 0, cap, e->list, e->i32a);
+    }
     HIPCHK(hipGetLastError());
     if (engine_fetch(e, o.i32a, o.list + (size_t)2 * cap * n)) return -1;
     std::memcpy(moves, e->hio + o.list, (size_t)2 * cap * n);
@@ -2089,12 +2128,20 @@ extern "C" int gc_engine_next_state(gc_engine* e, int n, const int8_t* boards, c
     // promotion colour and rights logic (lib.rs:679-784), the state keeps current_player
     // the import reads side only under FIDE (the player argument is the side to move there)
     EngineLayout o;
-    if (engine_upload(e, n, boards, meta, player_white, o, 1, actions, e->rules != 0)) return -1;
-    SoA in{e->bb, e->meta, n}, out{e->bb2, e->meta2, n};
-    if (e->rules) k_fnext_state<<<grid_for(n), BLOCK, 0, e->stream>>>(in, e->acts, out, e->i32a, e->i32b);
-    else k_next_state<<<grid_for(n), BLOCK, 0, e->stream>>>(in, e->side, e->acts, out, e->i32a, e->i32b);
-    HIPCHK(hipGetLastError());
-    engine_export(e, out);
+    if (e->rules) {
+        if (engine_upload(e, n, boards, meta, player_white, o, 1, actions)) return -1;
+        SoA in{e->bb, e->meta, n}, out{e->bb2, e->meta2, n};
+        k_fnext_state<<<grid_for(n), BLOCK, 0, e->stream>>>(in, e->acts, out, e->i32a, e->i32b);
+        HIPCHK(hipGetLastError());
+        engine_export(e, out);
+    } else {  // one launch: import + next_state + export, in place on the staged mailbox
+        if (n <= 0) return fail("n must be > 0");
+        if (!boards || !meta) return fail("null boards/meta");
+        if (check_boards(n, boards)) return -1;
+        HIPCHK(hipSetDevice(e->device));
+        if (engine_stage(e, n, 1, boards, meta, player_white, actions, o)) return -1;
+        k_next_state_mb<<<grid_for(n), BLOCK, 0, e->stream>>>(e->mbox, e->m8, e->side, e->acts, n, e->i32a, e->i32b);
+    }
     HIPCHK(hipGetLastError());
     if (engine_fetch(e, 0, o.i32b + (size_t)4 * n)) return -1;
     std::memcpy(out_boards, e->hio + o.mbox, (size_t)64 * n);
