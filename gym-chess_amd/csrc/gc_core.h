@@ -1397,24 +1397,32 @@ GC_HD int apply_move(Pos& s, bool white_player, int action, int* reward, bool* i
 // unreachable (a pawn of the mover never reaches the row lib.rs:703-704 tests), a white king
 // move revokes both white rights, a white rook leaving column 0 / 7 revokes one (Q5).
 GC_HD void apply_legal(Pos& s, bool white, int action, int* reward, bool* irrev) {
-    if (action >= 4096) {  // castles (rare): the general path
-        apply_move(s, white, action, reward, irrev);
-        return;
-    }
-    int f = action >> 6, t = action & 63;
-    u64 fm = bit(f), tm = bit(t), clr = ~(fm | tm);
+    // castles (lib.rs:740-773) in the same branch-free form: the king's and rook's squares
+    // (and the ones between) cleared, king and rook put on their targets in the colour of the
+    // castle id; both rights of that colour revoked
+    const bool cs = action >= 4096;
+    const bool cw = action == A_KSW || action == A_QSW, cks = action == A_KSW || action == A_KSB;
+    const int base = cw ? 56 : 0;
+    const u64 cclr = cks ? (0xFull << (base + 4)) : (0x1Full << base);
+    const u64 ck = cs ? bit(base + (cks ? 6 : 2)) : 0ull, cr = cs ? bit(base + (cks ? 5 : 3)) : 0ull;
+    int f = (action >> 6) & 63, t = action & 63;
+    u64 fm = cs ? 0ull : bit(f), tm = cs ? 0ull : bit(t), clr = cs ? ~cclr : ~(fm | tm);
     // captured value (lib.rs:19-25, 698): Q 10, R 5, B/N 3, P 1, K 0
     // the target holds at most one piece: a sum of bit tests, no branch chain
     int v = 10 * (int)((s.q >> t) & 1) + 5 * (int)((s.r >> t) & 1) + 3 * (int)(((s.b | s.n) >> t) & 1) +
             (int)((s.p >> t) & 1);
-    *reward = v;
-    *irrev = ((s.p & fm) != 0) || ((occ_of(s) & tm) != 0);
+    *reward = cs ? 0 : v;
+    *irrev = !cs && (((s.p & fm) != 0) || ((occ_of(s) & tm) != 0));
     bool wk = (s.k & s.w & fm) != 0, wr = (s.r & s.w & fm) != 0;
 #define GC_MV(X) s.X = (s.X & clr) | ((s.X & fm) ? tm : 0ull)
     GC_MV(k); GC_MV(q); GC_MV(r); GC_MV(b); GC_MV(n); GC_MV(p); GC_MV(w);
 #undef GC_MV
+    s.k |= ck;
+    s.r |= cr;
+    s.w |= cw ? (ck | cr) : 0ull;
     u32 clear = (wk ? (u32)(M_WKC | M_WQC) : 0u) | ((wr && (f & 7) == 0) ? (u32)M_WQC : 0u) |
                 ((wr && (f & 7) == 7) ? (u32)M_WKC : 0u);
+    clear = cs ? (cw ? (u32)(M_WKC | M_WQC) : (u32)(M_BKC | M_BQC)) : clear;
     s.meta = (s.meta & ~clear) ^ M_WHITE;  // current_player = other (lib.rs:778-780)
 }
 
