@@ -406,10 +406,15 @@ def _weird_initial_boards():
     boards, _ = random_positions(10, 4711)
     crowd = DEFAULT_BOARD.copy()  # 20 white pieces: the per-square fallback, no reset cache
     crowd[[33, 35, 37, 39]] = 2
-    return list(boards) + [crowd]
+    # 27 white queens round the edge and one inside, a black rook, no black king: 279 legal
+    # moves for white, past the byte-sum pick (the set-wise pick's rolled scan)
+    queens = np.zeros(64, dtype=np.int8)
+    queens[[1, 2, 3, 4, 5, 6, 7, 8, 15, 16, 23, 24, 31, 32, 36, 39, 40, 47, 48, 55, 56, 57, 58, 59, 60, 61, 62]] = 2
+    queens[63], queens[0] = 1, -3
+    return list(boards) + [crowd, queens]
 
 
-@pytest.mark.parametrize("k", range(11))
+@pytest.mark.parametrize("k", range(12))
 def test_step_random_weird_initial_boards_vs_oracle(oracle, k):
     """k_env_step2 ply by ply from (and resetting to) a weird initial board: outputs, next
     action and final states vs the oracle driver with the same initial board.  70 boards:
