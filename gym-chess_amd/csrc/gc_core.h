@@ -426,19 +426,22 @@ GC_HD PinPart gen_pins_part(const Pos& s, const Gen& g) {
 // all of them and whose king did not move (the move was the other side's), so it computes this
 // once per subtree root (perft2) instead of once per child.  ks < 0: no king (all zero but the
 // masks of square 0, which nothing then uses: nothing is pinned).
+// (The file and rank masks are two shifts each: recomputed where used, which keeps the perft
+// leaf kernel's live registers down.)
 struct KingLines {
     int ks;
     bool white;
     u64 kings;           // the side's kings the lines were computed for
-
-    u64 fm, rm, dm, am;  // file, rank, diagonal, anti-diagonal through the king
+    u64 dm, am;          // diagonal, anti-diagonal through the king
     u64 pawn, knight, king;  // squares from which an enemy pawn / knight / king attacks it
+    GC_HDM u64 fm() const { return file_mask(ks < 0 ? 0 : ks); }
+    GC_HDM u64 rm() const { return row_mask(ks < 0 ? 0 : ks); }
 };
 GC_HD KingLines king_lines(int ks, bool white, u64 kings = 0) {
     const int kq = ks < 0 ? 0 : ks;
     const u64 kb = ks < 0 ? 0ull : bit(ks);
-    return KingLines{ks, white, kings, file_mask(kq), row_mask(kq), diag_mask(kq), anti_mask(kq),
-                     pawn_att_set(kb, white), knight_set(kb), king_set(kb)};
+    return KingLines{ks, white, kings, diag_mask(kq), anti_mask(kq), pawn_att_set(kb, white), knight_set(kb),
+                     king_set(kb)};
 }
 // the lines of the side to move of s, with its kings recorded (the perft hint)
 GC_HD KingLines king_lines_of(const Pos& s, bool white) {
@@ -468,7 +471,7 @@ GC_HD PinPart gen_pins_aligned_kl(const Pos& s, const Gen& g, const KingLines& k
     const int ks = g.ks;
     const u64 opp = g.opp, occ = g.occ, own = g.own;
     p.checkers = (kl.pawn & s.p & opp) | (kl.knight & s.n & opp) | (kl.king & s.k & opp);
-    const u64 fm = kl.fm, rm = kl.rm, dm = kl.dm, am = kl.am;
+    const u64 fm = kl.fm(), rm = kl.rm(), dm = kl.dm, am = kl.am;
     u64 cand = ((s.r | s.q) & opp & (fm | rm)) | ((s.b | s.q) & opp & (dm | am));
     while (cand) {
         const int x = ctz(cand);
@@ -886,7 +889,7 @@ GC_HD int sw_ksq(const Gen& g) { return g.ks < 0 ? 0 : g.ks; }
 GC_HD void sw_pawns_kl(const Pos& s, const Gen& g, const KingLines& kl, u64* t) {
     const u64 cm = g.checkmask, empty = ~g.occ, opp = g.opp, P = s.p & g.own, pr = g.pinrays;
     const u64 fp = P & ~g.pinned, pp = P & g.pinned;
-    const u64 pf = pp & kl.fm, pd = pp & kl.dm, pa = pp & kl.am;
+    const u64 pf = pp & kl.fm(), pd = pp & kl.dm, pa = pp & kl.am;
     if (g.white) {  // lib.rs:935-958, p = +1: toward row 0
         t[SW_P1] = ((fp >> 8) | ((pf >> 8) & pr)) & empty & cm;
         t[SW_P2] = (((fp & ROW6) >> 16) | (((pf & ROW6) >> 16) & pr)) & empty & cm;
@@ -976,7 +979,7 @@ struct SliderGens {
 GC_HD SliderGens slider_gens_kl(const Pos& s, const Gen& g, const KingLines& kl) {
     const u64 pin = g.pinned, oRQ = (s.r | s.q) & g.own, oBQ = (s.b | s.q) & g.own;
     const u64 fRQ = oRQ & ~pin, fBQ = oBQ & ~pin, pRQ = oRQ & pin, pBQ = oBQ & pin;
-    return SliderGens{fRQ | (pRQ & kl.fm), fRQ | (pRQ & kl.rm), fBQ | (pBQ & kl.dm), fBQ | (pBQ & kl.am)};
+    return SliderGens{fRQ | (pRQ & kl.fm()), fRQ | (pRQ & kl.rm()), fBQ | (pBQ & kl.dm), fBQ | (pBQ & kl.am)};
 }
 GC_HD SliderGens slider_gens(const Pos& s, const Gen& g) { return slider_gens_kl(s, g, king_lines(g.ks, g.white)); }
 // pawns (set-wise, pinned ones included), knights, kings (count_moves without the sliders)

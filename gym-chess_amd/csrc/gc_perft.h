@@ -101,10 +101,17 @@ GC_HD uint64_t perft2(const Pos& root, SA& sa) {
     gen_init(root, g0);
     gen_moves(root, g0, m0, sa);
     uint64_t nodes = 0;
-    MoveWalk w0(g0);
     const KingLines k1l = king_lines_of(root, !g0.white);  // as perft_small
+    if (m0.big) {  // more pieces than scratch slots (rare): children by rank
+        for (int k1 = 0; k1 < m0.total; k1++)
+            nodes += (uint64_t)count_position_kl(child_of(root, g0.white, select_action(root, g0, m0, sa, k1)), k1l);
+        return nodes;
+    }
+    // the walk alone (its own loop: the context and count planes the rank search would need are
+    // dead here, which keeps the loop's live registers down)
+    MoveWalk w0(g0);
     for (int k1 = 0; k1 < m0.total; k1++) {
-        Pos c1 = child_of(root, g0.white, next_child(w0, root, g0, m0, sa, k1));
+        Pos c1 = child_of(root, g0.white, w0.next(g0, m0, sa));
 #ifdef GC_PERFT_UNFUSED  // A/B: the map and the count in two passes
         Gen g1;
         gen_init(c1, g1);
