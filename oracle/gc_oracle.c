@@ -586,9 +586,9 @@ uint32_t oracle_policy_index(uint64_t seed, uint32_t board, uint32_t draw, uint3
     return (uint32_t)(((uint64_t)o[0] * n) >> 32);
 }
 
-/* The random policy is uniform over the legal list; rank k maps to the k-th legal action in
- * ascending action id (the order of a legal-action mask; the device pick uses the same
- * bijection).  Any fixed bijection gives the same uniform policy. */
+/* Rank k -> the k-th legal action in ascending action id: the order of a legal-action mask,
+ * which the device API step's `pick` output follows (the policy itself ranks in move-set
+ * order, kth_in_set_order).  Any fixed bijection gives the same uniform policy. */
 static int kth_in_action_order(const uint16_t *moves, int n, int k) {
     uint16_t tmp[MAXMOVES];
     for (int i = 0; i < n; i++) {  /* insertion sort: lists are short */
