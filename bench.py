@@ -4,15 +4,20 @@
 Workload (BASELINE.json configs[2], the config the metric is quoted on): 65 536 boards per
 GPU, random-policy self-play to terminal with auto-reset -- the reference's benchmark
 driver (/root/reference/gym_chess/test/v2/test_benchmark.py:9-43) vectorised.  One "step"
-= one env.step() on every board = one launch of the one-ply step kernel k_env_step2 (two
-waves per 64 boards): the policy's action through the full chess_v2.py step bookkeeping
-(next_state, update_state, 3-fold on the pre-move board, move cap, mate bonus), the
-opponent's legal move list, the Philox pick of the next action, reset of finished boards.
-State, repetition windows and outputs stay in HBM; nothing crosses PCIe in the timed region.
+= one env.step() on every board: the policy's action through the full chess_v2.py step
+bookkeeping (next_state, update_state, 3-fold on the pre-move board, move cap, mate bonus),
+the next side's legal move set, the Philox pick of the next action, reset of finished
+boards, and the step's outputs (action played, reward, done, reason) of every board written
+to a per-ply trace in HBM.  The K timed steps are ONE launch of the fused rollout kernel
+k_env_rollout2 (gc_env_rollout_device: the state stays in registers between plies; every
+ply's window probe / commit and outputs go through HBM).  State, repetition windows and
+outputs stay in HBM; nothing crosses PCIe in the timed region.  The launched form (one
+kernel launch per ply, k_env_step2 over two board-range streams) is timed beside it as
+"launched_step".
 
 The batch is first settled into steady state (a fused rollout of --settle plies, then
---warmup single-ply launches), so the timed launches see mid/late-game boards, resets and
-terminals in their steady-state proportions, whatever --warmup is.
+--warmup steps), so the timed steps see mid/late-game boards, resets and terminals in their
+steady-state proportions, whatever --warmup is.
 
   python bench.py [--gpus N --steps K --warmup W --boards B]
       N replicas in ONE process: one host thread + one env handle per device (no torch)
@@ -33,7 +38,15 @@ sys.path.insert(0, os.path.join(ROOT, "gym-chess_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip-level parameters (8.0 TB/s spec)
 
-# algorithmic bytes per board per step of k_env_step2:
+# algorithmic bytes per board per fused rollout ply (BASELINE.md CPU-baseline
+# plan): state read 80 + state write 80 + repetition history 8h + action 8 + outputs 5
+# = 173 + 8h B, h = the mean repetition-window length (boards since the last pawn move or
+# capture) measured over the timed steps
+def alg_bytes_fused(h):
+    return 173.0 + 8.0 * h
+
+
+# the launched step k_env_step2 (one kernel per ply; DESIGN.md §5 byte model):
 #   state 7x8 B bitboards + 4 B meta, read + write                     120
 #   action read + next-action write (u16)                                4
 #   Philox draw counter, step counter, window generation: read + write  24
@@ -42,9 +55,19 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip-level parameters (8.0 TB/s spe
 #   3-fold window: 64-B entry write (reversible plies; counted always)   64
 ALG_BYTES_PER_BOARD = 120 + 4 + 24 + 6 + 64 + 64
 
-# the PMC profile the traffic / VALU figures come from (rocprofv3 passes, tools/pmc_*.sh);
-# counters cannot be read from inside this process
-PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic_latest.json")
+# the PMC profiles the traffic / VALU figures come from (rocprofv3 passes, tools/gpu_run.sh
+# pmc*; tools/pmc_summary.py); counters cannot be read from inside this process
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_rollout_latest.json")
+PMC_STEP_FILE = os.path.join(ROOT, "profiles", "pmc_traffic_latest.json")
+
+
+def load_pmc(path):
+    if not os.path.exists(path):
+        return None
+    try:
+        return json.load(open(path))
+    except (OSError, ValueError):
+        return None
 
 
 def parse():
@@ -59,7 +82,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-boards", type=int, default=32768)
     ap.add_argument("--cpu-sample-plies", type=int, default=300)
-    ap.add_argument("--fused-plies", type=int, default=200, help="also time the fused rollout kernel (0 = skip)")
+    ap.add_argument("--cpu1-sample-boards", type=int, default=4096, help="boards of the single-core CPU sample")
+    ap.add_argument("--launched-steps", type=int, default=300,
+                    help="also time the launched step (one k_env_step2 launch per ply, 0 = skip)")
     ap.add_argument("--perft-roots", type=int, default=65536, help="perft leg on mid-game FEN roots (0 = skip)")
     ap.add_argument("--variant-steps", type=int, default=300,
                     help="also time step() with opponent='random' and with rules='fide' (SURVEY 8f rows 2, 4; 0 = skip)")
@@ -68,14 +93,17 @@ def parse():
     ap.add_argument("--single-episodes", type=int, default=10,
                     help="configs[0]: the reference benchmark driver on the single-board env (0 = skip)")
     ap.add_argument("--perft-depth", type=int, default=5)
+    ap.add_argument("--perft-subsample", type=int, default=256,
+                    help="roots of the fixed strided subsample checked (and CPU-timed) one ply shallower")
     ap.add_argument("--oracle-perft-roots", type=int, default=8,
                     help="roots of the perft leg checked against the oracle at --perft-depth (also its CPU baseline)")
     return ap.parse_args()
 
 
 def cpu_baseline(args):
-    """Oracle (C restatement of lib.rs + chess_v2.py, test infrastructure) on host threads:
-    the same random self-play driver on a bounded sample of boards."""
+    """Oracle (C restatement of lib.rs + chess_v2.py, test infrastructure) on the host: the
+    same random self-play driver on bounded samples of boards, on all host threads (up to 16,
+    the box's CPU share) and on one core (BASELINE.md CPU-baseline plan)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
 
@@ -85,6 +113,10 @@ def cpu_baseline(args):
     st = O.rollout_batch(args.seed, 0, args.cpu_sample_boards, args.cpu_sample_plies, threads=threads)
     dt = time.perf_counter() - t0
     steps = int(st[0])
+    t0 = time.perf_counter()
+    st1 = O.rollout_batch(args.seed, 0, args.cpu1_sample_boards, args.cpu_sample_plies, threads=1)
+    dt1 = time.perf_counter() - t0
+    steps1 = int(st1[0])
     return {
         "value": steps / dt,
         "unit": "env_steps/s",
@@ -92,6 +124,9 @@ def cpu_baseline(args):
         "kind": "port",
         "sample": f"{args.cpu_sample_boards} boards x {args.cpu_sample_plies} plies random self-play "
         f"({steps} env.step calls, {dt:.1f} s) with the C oracle restating lib.rs + chess_v2.py",
+        "single_core": {"value": steps1 / dt1, "unit": "env_steps/s", "cores": 1,
+                        "sample": f"{args.cpu1_sample_boards} boards x {args.cpu_sample_plies} plies "
+                                  f"({steps1} env.step calls, {dt1:.1f} s)"},
     }
 
 
@@ -188,18 +223,37 @@ def perft_leg(args, rep):
         import oracle as O
 
         threads = max(1, min(16, os.cpu_count() or 1))
+        # roots spread over the whole batch: the first, the last and evenly strided ones
+        idx = np.unique(np.linspace(0, args.perft_roots - 1, k).round().astype(np.int64))
         t0 = time.perf_counter()
-        cn = O.perft_by_children(b[:k], m[:k], args.perft_depth, threads=threads)
+        cn = O.perft_by_children(b[idx], m[idx], args.perft_depth, threads=threads)
         cdt = time.perf_counter() - t0
-        mism = np.nonzero(cn != res[0][:k])[0]
+        mism = idx[np.nonzero(cn != res[0][idx])[0]]
         assert len(mism) == 0, f"oracle perft({args.perft_depth}) disagrees with the device at roots {mism[:8]}"
-        out["oracle_checked_roots"] = int(k)
+        out["oracle_checked_roots"] = [int(x) for x in idx]
         out["oracle_checked_nodes"] = int(cn.sum())
+        # BASELINE.md's fixed subsample: 256 roots strided over the batch, one ply shallower
+        # (perft(5) of 256 mid-game roots is ~1e10 nodes: minutes of CPU), device vs oracle
+        sub = np.arange(0, args.perft_roots, max(1, args.perft_roots // args.perft_subsample))[: args.perft_subsample]
+        sd = max(1, args.perft_depth - 1)
+        eng = Engine(rep.local[0].device)
+        dn = eng.perft(b[sub], m[sub], sd)
+        eng.close()
+        t0 = time.perf_counter()
+        sn = O.perft_by_children(b[sub], m[sub], sd, threads=threads)
+        sdt = time.perf_counter() - t0
+        bad = sub[np.nonzero(sn != dn)[0]]
+        assert len(bad) == 0, f"oracle perft({sd}) disagrees with the device at roots {bad[:8]}"
+        out["oracle_subsample"] = {"roots": len(sub), "stride": int(sub[1] - sub[0]) if len(sub) > 1 else 0,
+                                   "depth": sd, "nodes": int(sn.sum()), "match": True}
         if rep.world_size == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = {"value": float(cn.sum()) / cdt, "unit": "perft_nodes/s", "cores": threads,
+            out["cpu_baseline"] = {"value": float(sn.sum()) / sdt, "unit": "perft_nodes/s", "cores": threads,
                                    "kind": "port",
-                                   "sample": f"first {k} roots x perft({args.perft_depth}) ({int(cn.sum())} nodes, "
-                                   f"{cdt:.1f} s) with the C oracle (children handed out across threads)"}
+                                   "sample": f"{len(sub)} roots strided over the batch x perft({sd}) "
+                                   f"({int(sn.sum())} nodes, {sdt:.1f} s) with the C oracle (children handed out "
+                                   f"across threads)",
+                                   "spread_roots_depth5": {"value": float(cn.sum()) / cdt, "roots": len(idx),
+                                                           "nodes": int(cn.sum()), "seconds": cdt}}
     return out
 
 
@@ -303,46 +357,88 @@ def single_env_leg(args, rep):
 def variant_legs(args, rep, n):
     """step() throughput of the SURVEY 8f variants at the same batch: the in-kernel random
     opponent (one step = the agent's ply + the opponent's reply) and FIDE rules.  Same timing
-    discipline as the main line, fewer steps."""
+    discipline as the main line (one fused launch of --variant-steps steps with the per-step
+    trace), plus the launched form (one kernel per step)."""
     from gym_chess_amd.env import BatchedChessEnv
 
     out = {}
+    k = args.variant_steps
     for name, kw in (("opponent_random", dict(opponent="random")), ("rules_fide", dict(rules="fide"))):
         def setup(rp):
             env = BatchedChessEnv(n, device=rp.device, seed=rp.board_seed(args.seed + 7), **kw)
+            tb = env.trace_buffer(k)
             env.step_random(max(args.warmup, 200))
+            env.rollout_device(k, tb)  # loads the fused kernel
             env.synchronize()
-            return env
+            return env, tb
 
-        envs = rep.run(setup)
-        s0 = [int(e.outputs()["nsteps"].sum()) for e in envs]
+        ctx = rep.run(setup)
+        s0 = [int(e.outputs()["nsteps"].sum()) for e, _ in ctx]
 
         def run(rp):
-            env = envs[rep.local.index(rp)]
+            env, tb = ctx[rep.local.index(rp)]
+            env.synchronize()
             t0 = time.perf_counter()
-            env.step_random(args.variant_steps)
+            env.rollout_device(k, tb)
             env.synchronize()
             return None, time.perf_counter() - t0
 
         _, dt = rep.timed(run)
-        s1 = [int(e.outputs()["nsteps"].sum()) for e in envs]
-        out[name] = {"value": rep.sum(sum(b - a for a, b in zip(s0, s1))) / dt, "unit": "env_steps/s",
-                     "steps": args.variant_steps}
-        if args.fused_plies > 0:  # the same variant's fused rollout (state in registers for the launch)
-            def fused(rp):
-                env = envs[rep.local.index(rp)]
-                env.rollout(1)
+        s1 = [int(e.outputs()["nsteps"].sum()) for e, _ in ctx]
+        out[name] = {"value": rep.sum(sum(b - a for a, b in zip(s0, s1))) / dt, "unit": "env_steps/s", "steps": k,
+                     "form": "one fused launch (gc_env_rollout_device) with the per-step trace"}
+        if args.launched_steps > 0:
+            def launched(rp):
+                env, _ = ctx[rep.local.index(rp)]
                 env.synchronize()
                 t0 = time.perf_counter()
-                st, _ = env.rollout(args.fused_plies)
+                env.step_random(k)
                 env.synchronize()
-                return float(st[0]), time.perf_counter() - t0
+                return None, time.perf_counter() - t0
 
-            fs, fdt = rep.timed(fused)
-            out[name]["fused_rollout"] = {"value": rep.sum(sum(fs)) / fdt, "unit": "env_steps/s",
-                                          "plies_per_launch": args.fused_plies}
-        for e in envs:
+            s0 = [int(e.outputs()["nsteps"].sum()) for e, _ in ctx]
+            _, ldt = rep.timed(launched)
+            s1 = [int(e.outputs()["nsteps"].sum()) for e, _ in ctx]
+            out[name]["launched_step"] = {"value": rep.sum(sum(b - a for a, b in zip(s0, s1))) / ldt,
+                                          "unit": "env_steps/s", "steps": k}
+        for e, tb in ctx:
+            tb.close()
             e.close()
+    return out
+
+
+def launched_leg(args, rep, envs, n):
+    """The launched form of the same step: one k_env_step2 launch per ply over two
+    board-range streams (gc_env_step_random), --launched-steps plies; roofline of k_env_step2
+    per ply by HIP events on the env's stream."""
+    for e in envs:
+        e.step_random(5)  # loads the step kernel
+        e.synchronize()
+    s0 = [int(e.outputs()["nsteps"].sum()) for e in envs]
+
+    def run(rp):
+        env = envs[rep.local.index(rp)]
+        env.synchronize()
+        t0 = time.perf_counter()
+        env.record_event(2)
+        env.step_random(args.launched_steps)
+        env.record_event(3)
+        env.synchronize()
+        return None, time.perf_counter() - t0
+
+    _, dt = rep.timed(run)
+    s1 = [int(e.outputs()["nsteps"].sum()) for e in envs]
+    ply_s = sum(e.elapsed_ms(2, 3) for e in envs) / len(envs) / 1e3 / args.launched_steps
+    ach = n * ALG_BYTES_PER_BOARD / ply_s / 1e9
+    out = {"value": rep.sum(sum(b - a for a, b in zip(s0, s1))) / dt, "unit": "env_steps/s",
+           "steps": args.launched_steps, "ms_per_step": dt * 1e3 / args.launched_steps,
+           "roofline": {"bound": "hbm", "kernel": "k_env_step2", "achieved": ach, "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "avg_ply_us": ply_s * 1e6,
+                        "alg_bytes_per_board": ALG_BYTES_PER_BOARD}}
+    pm = load_pmc(PMC_STEP_FILE)
+    if pm:
+        out["roofline"]["traffic"] = pm.get("bytes_per_launch")
+        out["roofline"]["pmc_source"] = {"file": os.path.relpath(PMC_STEP_FILE, ROOT), "profile": pm.get("profile")}
     return out
 
 
@@ -359,19 +455,20 @@ def main():
         env = BatchedChessEnv(n, device=rp.device, seed=rp.board_seed(args.seed))
         if args.settle > 0:  # into steady state: mid/late-game boards, resets, terminals
             env.rollout(args.settle)
-        env.step_random(args.warmup)
+        tb = env.trace_buffer(max(args.steps, args.warmup, 1))
+        env.rollout_device(args.warmup, tb)  # the W untimed warmup steps (also loads the kernel)
         env.synchronize()
-        return env, int(env.outputs()["nsteps"].sum()), env.window_sum()
+        return env, tb, int(env.outputs()["nsteps"].sum()), env.window_sum()
 
     ctx = rep.run(setup)
     envs = [c[0] for c in ctx]
 
     def step(rp):
-        env = envs[rep.local.index(rp)]
+        env, tb = ctx[rep.local.index(rp)][:2]
         env.synchronize()
         t0 = time.perf_counter()
         env.record_event(0)
-        env.step_random(args.steps)
+        env.rollout_device(args.steps, tb)  # K env.step() of every board, one launch, per-step trace
         env.record_event(1)
         env.synchronize()
         return None, time.perf_counter() - t0
@@ -380,47 +477,34 @@ def main():
     kern_ms = [e.elapsed_ms(0, 1) for e in envs]
     s1 = [int(e.outputs()["nsteps"].sum()) for e in envs]
     w1 = [e.window_sum() for e in envs]
-    steps_all = rep.sum(sum(b - c[1] for c, b in zip(ctx, s1)))
+    steps_all = rep.sum(sum(b - c[2] for c, b in zip(ctx, s1)))
     value = steps_all / dt_max
-    mean_window = sum(c[2] + w for c, w in zip(ctx, w1)) / (2.0 * n * len(envs))
+    mean_window = sum(c[3] + w for c, w in zip(ctx, w1)) / (2.0 * n * len(envs))
+    # the timed trace must hold every step of every board (a spot check of the last ply)
+    tr_last = ctx[0][1].fetch(args.steps)
+    assert (tr_last["done"][-1] <= 1).all() and (tr_last["reason"][-1] <= 10).all()
 
-    # roofline of the dominant kernel (k_env_step2, the paired one-ply step), per launch, from
-    # HIP events on the stream it is launched on (mean over this process's replicas)
-    bytes_per_launch = n * ALG_BYTES_PER_BOARD
-    avg_launch_s = sum(kern_ms) / len(kern_ms) / 1e3 / args.steps
-    achieved = bytes_per_launch / avg_launch_s / 1e9
-    traffic = valu = pmc_src = None
-    if os.path.exists(PMC_FILE):
-        try:
-            pmc = json.load(open(PMC_FILE))
-            traffic = pmc.get("bytes_per_launch")
-            valu = pmc.get("valu")
-            pmc_src = {"file": os.path.relpath(PMC_FILE, ROOT), "profile": pmc.get("profile"),
-                       "mean_window": pmc.get("mean_window"), "boards": pmc.get("boards"),
-                       "note": "rocprofv3 PMC passes of the same bench command (not this process); "
-                               "traffic = FETCH_SIZE x2 + WRITE_SIZE per launch"}
-        except (OSError, ValueError):
-            traffic = valu = pmc_src = None
+    # roofline of the dominant kernel (k_env_rollout2, the fused K-step launch), per launch,
+    # from HIP events on the env's stream (the stream it is launched on; mean over this
+    # process's replicas): SURVEY §8(d)'s 173 + 8h bytes per board per ply x N x K
+    alg = alg_bytes_fused(mean_window)
+    launch_s = sum(kern_ms) / len(kern_ms) / 1e3
+    achieved = n * args.steps * alg / launch_s / 1e9
+    pm = load_pmc(PMC_FILE)
+    traffic = pmc_src = valu = None
+    if pm:
+        traffic = pm.get("bytes_per_launch")
+        valu = pm.get("valu")
+        pmc_src = {"file": os.path.relpath(PMC_FILE, ROOT), "profile": pm.get("profile"),
+                   "plies_per_launch": pm.get("plies_per_launch"), "bytes_per_board_ply": pm.get("bytes_per_board_ply"),
+                   "note": "rocprofv3 PMC passes of the same bench command (not this process); "
+                           "traffic = FETCH_SIZE x2 + WRITE_SIZE per launch (MI355X guide, gfx950 correction)"}
 
     extra = {}
-    if args.fused_plies > 0:
-        for e in envs:
-            e.rollout(1)  # load the rollout kernel: a first launch would time code-object loading
-            e.synchronize()
-
-        def fused(rp):
-            env = envs[rep.local.index(rp)]
-            t0 = time.perf_counter()
-            env.record_event(2)
-            st, _ = env.rollout(args.fused_plies)
-            env.record_event(3)
-            env.synchronize()
-            return float(st[0]), time.perf_counter() - t0
-
-        fs, fdt = rep.timed(fused)
-        extra["fused_rollout"] = {"value": rep.sum(sum(fs)) / fdt, "unit": "env_steps/s",
-                                  "plies_per_launch": args.fused_plies, "kernel_ms": envs[0].elapsed_ms(2, 3)}
-    for e in envs:
+    if args.launched_steps > 0:
+        extra["launched_step"] = launched_leg(args, rep, envs, n)
+    for e, tb in ((c[0], c[1]) for c in ctx):
+        tb.close()
         e.close()
     if args.api_steps > 0:
         extra["api_step"] = api_step_leg(args, rep, n)
@@ -445,6 +529,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": dt_max * 1e3 / args.steps,
             "timed_region_ms": dt_max * 1e3,
+            "event_ms_per_step": launch_s * 1e3 / args.steps,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -453,11 +538,13 @@ def main():
             "config": {"workload": "configs[2]: 65536 boards/GPU random-policy rollout to terminal, step() throughput",
                        "boards_per_gpu": n, "global_boards": n * rep.world_size,
                        "parallelism": f"replicas{rep.world_size}", "replica_mode": rep.mode,
-                       "settle_plies": args.settle},
+                       "settle_plies": args.settle,
+                       "step_form": "K steps = one k_env_rollout2 launch (gc_env_rollout_device), per-step trace in HBM"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_env_step2", "avg_launch_us": avg_launch_s * 1e6,
-                         "alg_bytes_per_board": ALG_BYTES_PER_BOARD, "mean_window": mean_window,
+                         "kernel": "k_env_rollout2<false, 0>", "avg_launch_us": launch_s * 1e6,
+                         "plies_per_launch": args.steps, "alg_bytes_per_board_ply": alg,
+                         "alg_bytes_rule": "SURVEY 8(d) fused rollout ply: 173 + 8h", "mean_window": mean_window,
                          "valu": valu, "pmc_source": pmc_src},
             "cpu_baseline": cpu,
             **extra,

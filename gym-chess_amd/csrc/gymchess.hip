@@ -17,6 +17,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <atomic>
+#include <chrono>
 #include <mutex>
 #include <string>
 #include <type_traits>
@@ -1457,14 +1458,29 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
 #endif
 }
 
-// Fused K-ply random self-play on the paired step: the state stays in registers; the last
-// ply's outputs and per-board stats (as k_env_rollout) are written at the end.
+// One ply's env.step() outputs, packed for the per-ply trace [ply][N] (one coalesced 8-B
+// store per board per ply): action played (int16; -1 = none, the driver's no-move reset),
+// reward (int16), done (u8), reason (u8).  Unpacked by gc_env_rollout / bench consumers.
+__device__ __forceinline__ u64 trace_word(int played, const StepOut& o) {
+    return (u64)(uint16_t)(int16_t)played | ((u64)(uint16_t)(int16_t)o.reward << 16) | ((u64)(o.done & 0xFF) << 32) |
+           ((u64)(o.reason & 0xFF) << 40);
+}
+#define ROLLOUT_MAX_PLIES 16383  // plies per launch: rinfo bits 18..31
+
+// Fused K-ply random self-play on the paired step: the state stays in registers for the K
+// plies (K env.step() calls of every board in one launch); every ply's outputs go to the
+// optional trace [ply][N] (trace_word), the last ply's outputs, the state, window and counters
+// and the per-board stats (as k_env_rollout) are written at the end.  rinfo = plies << 18 |
+// ic.table << 16 | ic.total: with the trace pointer, all 16 argument dwords are preloaded.
 template <bool FIDE, int OPP = 0>
 __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
-    k_env_rollout2(uint8_t* __restrict__ slab, int nn, int blk0, uint64_t seed, u64* __restrict__ htab,
-                   const uint16_t* __restrict__ racts, const EnvDev::InitCache* __restrict__ icd, u32 rinfo, int plies,
-                   uint64_t* __restrict__ stats) {
+    k_env_rollout2(uint8_t* __restrict__ slab, int nn, uint64_t seed, u64* __restrict__ htab,
+                   const uint16_t* __restrict__ racts, const EnvDev::InitCache* __restrict__ icd, u32 rinfo,
+                   uint64_t* __restrict__ stats, u64* __restrict__ trace) {
     constexpr bool API = false;
+    constexpr int blk0 = 0;
+    const int plies = (int)(rinfo >> 18);
+    rinfo &= 0x1FFFFu;
     PAIR_PROLOGUE
     uint64_t steps = 0, rsum = 0;
     u32 e_mate = 0, e_rep = 0, e_cap = 0, e_nomove = 0, e_err = 0;
@@ -1472,6 +1488,7 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
     for (int p = 0; p < plies; p++) {
         int played = a;
         o = pair_step<OPP, true, FIDE>(Ls, L, C, role, l, i, live, rp, s, a, d, h, nst);
+        if (trace && role && live) trace[(size_t)p * nn + i] = trace_word(played == A_NONE ? -1 : played, o);
         if (played == A_NONE) {
             e_nomove++;
         } else {
@@ -1510,11 +1527,10 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
 }
 
 // Fused K-ply random self-play: state in registers for the whole launch.  Per-ply outputs
-// go to the optional trace [ply][N]; otherwise the last ply's outputs and per-board stats
+// go to the optional trace [ply][N] (trace_word); the last ply's outputs and per-board stats
 // [steps, reward_sum(two's complement), ends[0..5]] are written.
 template <bool OPP>
-__global__ void __launch_bounds__(BLOCK) k_env_rollout(EnvDev e, int plies, int16_t* tr_action, int16_t* tr_reward,
-                                                       uint8_t* tr_done, uint8_t* tr_reason, uint64_t* stats) {
+__global__ void __launch_bounds__(BLOCK) k_env_rollout(EnvDev e, int plies, u64* trace, uint64_t* stats) {
     LDS_SCRATCH_DECL;
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= e.n) return;
@@ -1554,13 +1570,7 @@ __global__ void __launch_bounds__(BLOCK) k_env_rollout(EnvDev e, int plies, int1
             }
         }
         if (OPP && !have) after_reset<OPP>(e, s, h, g, ms, scr, pc);
-        if (tr_action) {
-            size_t t = (size_t)p * e.n + i;
-            tr_action[t] = (int16_t)played;
-            tr_reward[t] = (int16_t)o.reward;
-            tr_done[t] = (uint8_t)o.done;
-            tr_reason[t] = (uint8_t)o.reason;
-        }
+        if (trace) trace[(size_t)p * e.n + i] = trace_word(played, o);
         a = selfplay_pick(s, pc);
         h.commit();
     }
@@ -2874,44 +2884,63 @@ extern "C" int gc_env_select_random(gc_env* e) {
     return 0;
 }
 
+// n_plies of fused random self-play after the work already on the env's stream (no host
+// sync): ROLLOUT_MAX_PLIES per launch; the per-ply trace (device memory, [n_plies][N] words,
+// trace_word) when d_trace is not NULL; with `stats`, per-board stats accumulate into e->stats.
+static int issue_rollout(gc_env* e, int n_plies, uint64_t* d_trace, bool stats) {
+    uint64_t* const st = stats ? e->stats : nullptr;
+    static const bool one_wave = getenv("GC_STEP1") != nullptr;
+    const bool pair = pair_ok(e) && (!one_wave || e->rules);
+    const EnvDev& d = e->d;
+    const ResetInfo r = reset_info(e);
+    const int grid = (e->n + PAIR_BOARDS * PAIRS_WG - 1) / (PAIR_BOARDS * PAIRS_WG), bs = 2 * PAIR_BOARDS * PAIRS_WG;
+    for (int p0 = 0; p0 < n_plies; p0 += ROLLOUT_MAX_PLIES) {
+        const int k = n_plies - p0 < ROLLOUT_MAX_PLIES ? n_plies - p0 : ROLLOUT_MAX_PLIES;
+        u64* tr = d_trace ? reinterpret_cast<u64*>(d_trace) + (size_t)p0 * e->n : nullptr;
+        const u32 ri = r.rinfo | ((u32)k << 18);
+        if (pair) {
+            switch (e->rules ? 3 : pair_opp(e)) {
+                case 3: k_env_rollout2<true><<<grid, bs, 0, e->stream>>>(e->slab, d.n, d.seed, d.htab, r.racts, r.icd, ri, st, tr); break;
+                case 0: k_env_rollout2<false><<<grid, bs, 0, e->stream>>>(e->slab, d.n, d.seed, d.htab, sw_table(r), r.icd, ri, st, tr); break;
+                case 1: k_env_rollout2<false, 1><<<grid, bs, 0, e->stream>>>(e->slab, d.n, d.seed, d.htab, sw_table(r), r.icd, ri, st, tr); break;
+                default: k_env_rollout2<false, 2><<<grid, bs, 0, e->stream>>>(e->slab, d.n, d.seed, d.htab, sw_table(r), r.icd, ri, st, tr); break;
+            }
+        } else if (e->d.opp) {
+            k_env_rollout<true><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d, k, tr, st);
+        } else {
+            k_env_rollout<false><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d, k, tr, st);
+        }
+        hipError_t le = hipGetLastError();
+        if (le != hipSuccess) return fail(std::string("rollout launch: ") + hipGetErrorString(le));
+    }
+    return 0;
+}
+
 extern "C" int gc_env_rollout(gc_env* e, int n_plies, int16_t* tr_action, int16_t* tr_reward, uint8_t* tr_done,
                               uint8_t* tr_reason, uint64_t* stats8) {
     if (!e) return fail("null env");
     if (n_plies < 0) return fail("n_plies must be >= 0");
     if (!e->policy_ready) return fail("policy actions stale: call gc_env_reset or gc_env_select_random first");
     HIPCHK(hipSetDevice(e->device));
-    bool trace = tr_action || tr_reward || tr_done || tr_reason;
-    if (e->rules && trace) return fail("fused rollout under FIDE rules: no per-ply traces (use gc_env_step_random)");
-    int16_t *da = nullptr, *dr = nullptr;
-    uint8_t *dd = nullptr, *dq = nullptr;
-    size_t cnt = (size_t)n_plies * e->n;
-    if (trace && (dalloc(&da, cnt) || dalloc(&dr, cnt) || dalloc(&dd, cnt) || dalloc(&dq, cnt))) return -1;
+    const bool trace = tr_action || tr_reward || tr_done || tr_reason;
+    const size_t cnt = (size_t)n_plies * e->n;
+    u64* dt = nullptr;
+    if (trace && cnt && dalloc(&dt, cnt)) return -1;
     HIPCHK(hipMemsetAsync(e->stats, 0, (size_t)64 * e->n, e->stream));
-    static const bool one_wave = getenv("GC_STEP1") != nullptr;
-    if (!trace && pair_ok(e) && (!one_wave || e->rules)) {  // the paired kernel (per-ply traces: the one-wave kernel)
-        const EnvDev& d = e->d;
-        const ResetInfo r = reset_info(e);
-        const int grid = (e->n + PAIR_BOARDS * PAIRS_WG - 1) / (PAIR_BOARDS * PAIRS_WG), bs = 2 * PAIR_BOARDS * PAIRS_WG;
-        switch (e->rules ? 3 : pair_opp(e)) {
-            case 3: k_env_rollout2<true><<<grid, bs, 0, e->stream>>>(e->slab, d.n, 0, d.seed, d.htab, r.racts, r.icd, r.rinfo, n_plies, e->stats); break;
-            case 0: k_env_rollout2<false><<<grid, bs, 0, e->stream>>>(e->slab, d.n, 0, d.seed, d.htab, sw_table(r), r.icd, r.rinfo, n_plies, e->stats); break;
-            case 1: k_env_rollout2<false, 1><<<grid, bs, 0, e->stream>>>(e->slab, d.n, 0, d.seed, d.htab, sw_table(r), r.icd, r.rinfo, n_plies, e->stats); break;
-            default: k_env_rollout2<false, 2><<<grid, bs, 0, e->stream>>>(e->slab, d.n, 0, d.seed, d.htab, sw_table(r), r.icd, r.rinfo, n_plies, e->stats); break;
+    if (issue_rollout(e, n_plies, dt, true)) { (void)hipFree(dt); return -1; }
+    if (trace && cnt) {
+        std::vector<u64> h(cnt);
+        hipError_t ce = hipMemcpyAsync(h.data(), dt, cnt * 8, hipMemcpyDeviceToHost, e->stream);
+        if (ce == hipSuccess) ce = hipStreamSynchronize(e->stream);
+        (void)hipFree(dt);
+        if (ce != hipSuccess) return fail(std::string("rollout trace: ") + hipGetErrorString(ce));
+        for (size_t t = 0; t < cnt; t++) {
+            const u64 w = h[t];
+            if (tr_action) tr_action[t] = (int16_t)(uint16_t)w;
+            if (tr_reward) tr_reward[t] = (int16_t)(uint16_t)(w >> 16);
+            if (tr_done) tr_done[t] = (uint8_t)(w >> 32);
+            if (tr_reason) tr_reason[t] = (uint8_t)(w >> 40);
         }
-    } else if (e->d.opp) {
-        k_env_rollout<true><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d, n_plies, da, dr, dd, dq, e->stats);
-    } else {
-        k_env_rollout<false><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d, n_plies, da, dr, dd, dq, e->stats);
-    }
-    hipError_t le = hipGetLastError();
-    if (le != hipSuccess) return fail(std::string("rollout launch: ") + hipGetErrorString(le));
-    if (trace) {
-        if (tr_action) HIPCHK(hipMemcpyAsync(tr_action, da, cnt * 2, hipMemcpyDeviceToHost, e->stream));
-        if (tr_reward) HIPCHK(hipMemcpyAsync(tr_reward, dr, cnt * 2, hipMemcpyDeviceToHost, e->stream));
-        if (tr_done) HIPCHK(hipMemcpyAsync(tr_done, dd, cnt, hipMemcpyDeviceToHost, e->stream));
-        if (tr_reason) HIPCHK(hipMemcpyAsync(tr_reason, dq, cnt, hipMemcpyDeviceToHost, e->stream));
-        HIPCHK(hipStreamSynchronize(e->stream));
-        (void)hipFree(da); (void)hipFree(dr); (void)hipFree(dd); (void)hipFree(dq);
     }
     if (stats8) {
         uint64_t* sums = e->stats + (size_t)8 * e->n;
@@ -2922,6 +2951,18 @@ extern "C" int gc_env_rollout(gc_env* e, int n_plies, int16_t* tr_action, int16_
         HIPCHK(hipStreamSynchronize(e->stream));
     }
     return 0;
+}
+
+// n_plies env.step() calls of every board under the random self-play policy in one launch
+// (per ROLLOUT_MAX_PLIES), asynchronous on the env's stream; each ply's outputs land in the
+// device trace [n_plies][N] (trace_word) when d_trace is not NULL.  State, windows, counters
+// and the last ply's outputs afterwards are those of n_plies gc_env_step_random plies.
+extern "C" int gc_env_rollout_device(gc_env* e, int n_plies, uint64_t* d_trace) {
+    if (!e) return fail("null env");
+    if (n_plies < 0) return fail("n_plies must be >= 0");
+    if (!e->policy_ready) return fail("policy actions stale: call gc_env_reset or gc_env_select_random first");
+    HIPCHK(hipSetDevice(e->device));
+    return issue_rollout(e, n_plies, d_trace, false);
 }
 
 extern "C" int gc_env_get_outputs(gc_env* e, int32_t* reward, uint8_t* done, uint8_t* reason, uint16_t* next_action,
@@ -3152,9 +3193,22 @@ extern "C" int gc_env_legal_mask(gc_env* e, uint64_t* mask, int32_t* counts) {
     return 0;
 }
 
+// Wait for the env's stream.  Spin on hipStreamQuery first (bounded): a blocking
+// hipStreamSynchronize can sleep on the completion interrupt and pays its wake-up on every
+// short wait; after GC_SPIN_US (default 20 000 us) of spinning it blocks.
 extern "C" int gc_env_synchronize(gc_env* e) {
     if (!e) return fail("null env");
     HIPCHK(hipSetDevice(e->device));
+    static const long spin_us = getenv("GC_SPIN_US") ? atol(getenv("GC_SPIN_US")) : 20000;
+    if (spin_us > 0) {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (;;) {
+            const hipError_t q = hipStreamQuery(e->stream);
+            if (q == hipSuccess) return 0;
+            if (q != hipErrorNotReady) return fail(std::string("stream: ") + hipGetErrorString(q));
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin_us)) break;
+        }
+    }
     HIPCHK(hipStreamSynchronize(e->stream));
     return 0;
 }

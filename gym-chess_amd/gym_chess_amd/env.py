@@ -217,6 +217,18 @@ class BatchedChessEnv:
         _lib.check(self._L.gc_env_rollout(self._h, int(n_plies), None, None, None, None, _lib.ptr(st)))
         return st, None
 
+    def rollout_device(self, n_plies, trace=None):
+        """n_plies env.step() calls of every board under the random self-play policy in one
+        launch, asynchronous (gc_env_rollout_device).  trace: None, or a TraceBuffer with room
+        for n_plies plies: every ply's outputs land in it on the device."""
+        if trace is not None and trace.plies < n_plies:
+            raise ValueError(f"trace buffer holds {trace.plies} plies, need {n_plies}")
+        _lib.check(self._L.gc_env_rollout_device(self._h, int(n_plies), trace.ptr if trace is not None else None))
+
+    def trace_buffer(self, plies):
+        """device memory for rollout_device's per-ply outputs ([plies][N] packed words)"""
+        return TraceBuffer(self, plies)
+
     def synchronize(self):
         _lib.check(self._L.gc_env_synchronize(self._h))
 
@@ -282,6 +294,41 @@ class BatchedChessEnv:
     def load_from(self, path):
         with open(path, "rb") as f:
             self.load(f.read())
+
+
+class TraceBuffer:
+    """Device trace of rollout_device: one uint64 word per board per ply ([ply][board]):
+    action played (int16, -1 = the driver's no-move reset), reward (int16), done, reason."""
+
+    def __init__(self, env, plies):
+        self.env = env
+        self.plies = int(plies)
+        v = ctypes.c_void_p()
+        _lib.check(env._L.gc_device_alloc(env.device, ctypes.c_uint64(8 * self.plies * env.num_boards),
+                                          ctypes.byref(v)))
+        self.ptr = v.value
+
+    def fetch(self, plies=None):
+        """host copy of the first `plies` plies as dict(action, reward, done, reason) [ply][board]"""
+        k = self.plies if plies is None else int(plies)
+        w = np.zeros((k, self.env.num_boards), dtype=np.uint64)
+        if w.size:
+            _lib.check(self.env._L.gc_env_copy(self.env._h, _lib.ptr(w), self.ptr, ctypes.c_uint64(w.nbytes), 2))
+        return dict(action=(w & np.uint64(0xFFFF)).astype(np.uint16).view(np.int16),
+                    reward=((w >> np.uint64(16)) & np.uint64(0xFFFF)).astype(np.uint16).view(np.int16),
+                    done=((w >> np.uint64(32)) & np.uint64(0xFF)).astype(np.uint8),
+                    reason=((w >> np.uint64(40)) & np.uint64(0xFF)).astype(np.uint8))
+
+    def close(self):
+        if self.ptr:
+            self.env._L.gc_device_free(self.env.device, ctypes.c_void_p(self.ptr))
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class DeviceIO:

@@ -146,6 +146,14 @@ int gc_env_select_random(gc_env* e);
  * reason 0..5} summed over boards (may be NULL). */
 int gc_env_rollout(gc_env* e, int n_plies, int16_t* tr_action, int16_t* tr_reward, uint8_t* tr_done,
                    uint8_t* tr_reason, uint64_t* stats8);
+/* n_plies env.step() calls of every board under the random self-play policy (the
+ * test_benchmark.py:17-31 driver, opponent as configured), issued as ONE launch per 16 383
+ * plies with the state held in registers, asynchronous on the env's stream (no host sync).
+ * d_trace: NULL, or device memory of n_plies*n uint64 words ([ply][board]) receiving every
+ * ply's outputs: bits 0-15 action played (int16, -1 = none: the driver's no-move reset),
+ * 16-31 reward (int16), 32-39 done, 40-47 reason.  Afterwards the env is in the state
+ * n_plies gc_env_step_random plies leave it in (outputs = the last ply's). */
+int gc_env_rollout_device(gc_env* e, int n_plies, uint64_t* d_trace);
 int gc_env_get_outputs(gc_env* e, int32_t* reward, uint8_t* done, uint8_t* reason, uint16_t* next_action,
                        uint32_t* nsteps);
 int gc_env_get_states(gc_env* e, int8_t* boards, uint8_t* meta);
@@ -154,6 +162,7 @@ int gc_env_set_states(gc_env* e, const int8_t* boards, const uint8_t* meta);
 int gc_env_legal_moves(gc_env* e, uint16_t* moves, int cap, int32_t* counts);
 /* legal action mask per board: 64 words (from -> targets) + 1 word (bit c: action 4096+c) */
 int gc_env_legal_mask(gc_env* e, uint64_t* mask, int32_t* counts);
+/* wait for the env's stream (spin-polls up to GC_SPIN_US, default 20 ms, then blocks) */
 int gc_env_synchronize(gc_env* e);
 /* FEN (host-side, no GPU): placement rank 8 first (board row 0), side to move, castling ->
  * the four *_castle_is_possible flags (chess_v2.py:301-313); en passant and the half-move

@@ -211,6 +211,33 @@ def test_fide_fused_rollout_matches_step_random():
 
 
 @pytest.mark.gpu
+def test_fide_rollout_trace_matches_step_random():
+    """The FIDE fused rollout's per-ply trace (rollout_device, host rollout(trace=True)) ==
+    the outputs of K launches of the one-ply step, ply by ply, 130 boards x 300 plies."""
+    from gym_chess_amd.env import BatchedChessEnv
+
+    n, plies = 130, 300
+    a = BatchedChessEnv(n, device=0, seed=91, rules="fide")
+    b = BatchedChessEnv(n, device=0, seed=91, rules="fide")
+    c = BatchedChessEnv(n, device=0, seed=91, rules="fide")
+    tb = b.trace_buffer(plies)
+    b.rollout_device(plies, tb)
+    tr = tb.fetch()
+    _, th = c.rollout(plies, trace=True)
+    for p in range(plies):
+        played = a.outputs()["next_action"].astype(np.int32)
+        a.step_random(1)
+        o = a.outputs()
+        assert (tr["action"][p] == np.where(played == 0xFFFF, -1, played)).all(), p
+        for k in ("reward", "done", "reason"):
+            assert (tr[k][p] == o[k]).all(), (p, k)
+            assert (th[k][p] == tr[k][p]).all(), (p, k)
+    ba, ma = a.boards()
+    bb, mb = b.boards()
+    assert (ba == bb).all() and (ma == mb).all()
+
+
+@pytest.mark.gpu
 def test_fide_env_external_steps_and_fens():
     from gym_chess_amd.env import BatchedChessEnv
 
@@ -229,8 +256,6 @@ def test_fide_env_external_steps_and_fens():
     assert b[3][1] == 2 and rw[3] == -10 + 10  # promotion to a queen, +10
     rw, dn, why = env.step(np.array([4100] * 4, dtype=np.uint16))
     assert (rw == -10).all() and (why == 6).all()  # RESIGN is never a legal action
-    with pytest.raises(Exception):
-        env.rollout(10, trace=True)  # the FIDE fused rollout keeps no per-ply traces
 
 
 @pytest.mark.gpu

@@ -359,6 +359,46 @@ def test_rollout_trajectories_vs_oracle(oracle, plies):
     b, m = env.boards()
 
 
+def test_rollout_device_trace_vs_oracle(oracle):
+    """gc_env_rollout_device (the bench's headline form: K steps in one launch, every ply's
+    outputs in the device trace) vs the oracle driver: actions played, rewards, done, reasons
+    of every ply and the final states.  200 boards: a partial last workgroup."""
+    from gym_chess_amd.env import BatchedChessEnv
+
+    n, plies, seed = 200, 500, 2024
+    env = BatchedChessEnv(n, device=0, seed=seed)
+    tb = env.trace_buffer(plies)
+    env.rollout_device(plies, tb)
+    env.synchronize()
+    tr = tb.fetch()
+    b, m = env.boards()
+    for i in range(n):
+        ref = oracle.rollout_trace(seed, i, plies)
+        for k in ("action", "reward", "done", "reason"):
+            assert (tr[k][:, i] == ref[k]).all(), (i, k, np.nonzero(tr[k][:, i] != ref[k])[0][:3])
+        assert (b[i] == ref["final_board"]).all() and list(m[i]) == list(ref["final_meta"]), i
+
+
+def test_rollout_device_past_one_launch(oracle):
+    """More plies than one launch holds (ROLLOUT_MAX_PLIES = 16 383): the chunks continue one
+    another exactly -- final states and next actions == the oracle's."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from gym_chess_amd.env import BatchedChessEnv
+
+    n, plies, seed = 64, 16383 + 617, 55
+    env = BatchedChessEnv(n, device=0, seed=seed)
+    env.rollout_device(plies)
+    b, m = env.boards()
+    nxt = env.outputs()["next_action"]
+    with ThreadPoolExecutor(8) as ex:
+        refs = list(ex.map(lambda i: oracle.rollout_trace(seed, i, plies + 1), range(n)))
+    for i, r in enumerate(refs):
+        fin = oracle.rollout_trace(seed, i, plies)
+        assert (b[i] == fin["final_board"]).all() and list(m[i]) == list(fin["final_meta"]), i
+        assert nxt[i] == (0xFFFF if r["action"][plies] < 0 else r["action"][plies]), i
+
+
 def test_step_random_matches_fused_rollout():
     """The one-ply step kernel (bench path) and the fused rollout kernel are the same driver."""
     from gym_chess_amd.env import BatchedChessEnv

@@ -76,7 +76,7 @@ def test_bench_threaded_two_replicas_line():
         env.pop(k, None)
     out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "20", "--warmup",
                           "5", "--settle", "300", "--boards", "8192", "--perft-roots", "0", "--variant-steps", "0",
-                          "--no-cpu-baseline", "--fused-plies", "0"], capture_output=True, text=True, env=env,
+                          "--no-cpu-baseline", "--launched-steps", "0"], capture_output=True, text=True, env=env,
                          timeout=300, check=True)
     line = json.loads(out.stdout.strip().splitlines()[-1])
     assert line["n_gpus"] == 2 and line["config"]["global_boards"] == 2 * 8192
@@ -105,7 +105,7 @@ def test_bench_torchrun_two_ranks_line():
                           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(root, "bench.py"),
                           "--gpus", "2", "--steps", "20", "--warmup", "5", "--settle", "300", "--boards", "8192",
                           "--perft-roots", "0", "--variant-steps", "0", "--api-steps", "0", "--single-episodes", "0",
-                          "--no-cpu-baseline", "--fused-plies", "0"], capture_output=True, text=True, env=env,
+                          "--no-cpu-baseline", "--launched-steps", "0"], capture_output=True, text=True, env=env,
                          timeout=240, check=True)
     lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, out.stdout[-2000:]

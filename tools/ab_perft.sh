@@ -2,7 +2,7 @@
 # Diagnostic: the bench's perft leg for the in-tree library and each tools/_lib_<tag>.so given
 cd ${GRAFT_REPO_ROOT:-.}
 mkdir -p gpurun_out
-B="--steps 5 --warmup 5 --settle 0 --fused-plies 0 --variant-steps 0 --api-steps 0 --single-episodes 0 --no-cpu-baseline --oracle-perft-roots 0"
+B="--steps 5 --warmup 5 --settle 0 --launched-steps 0 --variant-steps 0 --api-steps 0 --single-episodes 0 --no-cpu-baseline --oracle-perft-roots 0"
 show() { python -c "
 import json
 d=json.loads([l for l in open('$2') if l.startswith('{')][-1]); p=d['perft']

@@ -9,6 +9,6 @@ for r in $(seq ${R:-3}); do
     python -c "
 import json
 d=json.loads([l for l in open('gpurun_out/ab_$t.log').read().splitlines() if l.startswith('{')][-1])
-print('$t', round(d['value']/1e9,3), round(d['roofline']['avg_launch_us'],2), 'us; fused', round(d['fused_rollout']['value']/1e9,3))"
+print('$t', round(d['value']/1e9,3), round(d['roofline']['avg_launch_us'],2), 'us; launched', round(d.get('launched_step',{}).get('value',0)/1e9,3))"
   done
 done

@@ -11,5 +11,5 @@ for v in ${VARIANTS:-"s1:GC_STREAMS=1" "s2:GC_STREAMS=2" "s4:GC_STREAMS=4"}; do
   env $ev timeout -k 10 120 $B > gpurun_out/ab_$n.log 2>&1 || { tail -5 gpurun_out/ab_$n.log; exit 1; }
   python -c "
 import json
-d=json.loads(open('gpurun_out/ab_$n.log').read().strip().splitlines()[-1]); print('$n', round(d['value']/1e9,3), 'e9', round(d['roofline']['avg_launch_us'],2), 'us; fused', round(d['fused_rollout']['value']/1e9,3), 'e9')"
+d=json.loads(open('gpurun_out/ab_$n.log').read().strip().splitlines()[-1]); print('$n', round(d['value']/1e9,3), 'e9', round(d['roofline']['avg_launch_us'],2), 'us; launched', round(d.get('launched_step',{}).get('value',0)/1e9,3), 'e9')"
 done

@@ -17,22 +17,33 @@ step() {
 }
 # PMC passes time the bench's own steady-state launches (bench defaults: --settle 1000
 # --warmup 50), 20 of them; one counter group per pass (rocprofv3 does not split passes)
-PMCB="python bench.py --no-cpu-baseline --steps 20 --fused-plies 0 --perft-roots 0 --variant-steps 0"
+PMCB="python bench.py --no-cpu-baseline --steps 20 --launched-steps 20 --api-steps 0 --single-episodes 0 --perft-roots 0 --variant-steps 0"
+# the headline: the driver's own shape (--steps 20 --warmup 5), the fused launch of 20 steps is
+# the LAST k_env_rollout2<false, 0> dispatch of the process
+PMCR="python bench.py --no-cpu-baseline --steps 20 --warmup 5 --launched-steps 0 --api-steps 0 --single-episodes 0 --perft-roots 0 --variant-steps 0"
+MIXC="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAVE_CYCLES GRBM_GUI_ACTIVE"
 # perft passes: the bench's perft leg (65 536 mid-game FEN roots, perft(5)) without the step legs
-PERFTB="python bench.py --no-cpu-baseline --steps 5 --warmup 5 --settle 0 --fused-plies 0 --variant-steps 0 --oracle-perft-roots 0"
+PERFTB="python bench.py --no-cpu-baseline --steps 5 --warmup 5 --settle 0 --launched-steps 0 --api-steps 0 --single-episodes 0 --variant-steps 0 --oracle-perft-roots 0"
 for s in ${STEPS:-smoke pytest bench prof}; do
   case $s in
     smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     pytest) step pytest 1100 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread ;;
     bench)  step bench 600 python bench.py ${BENCH_ARGS:-} ;;
     prof)   step prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --no-cpu-baseline --oracle-perft-roots 0 ;;  # bench defaults: the same launches bench.py times
+    profs)  step profs 300 rocprofv3 --kernel-trace --stats -d $OUT/profs -o run --output-format csv -- python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --oracle-perft-roots 0 ;;  # the driver's command
     pmcf)   step pmcf 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-format csv -- $PMCB ;;
     pmcw)   step pmcw 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run --output-format csv -- $PMCB ;;
     pmcv)   step pmcv 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU -d $OUT/pmc_valu -o run --output-format csv -- $PMCB ;;
     pmcm)   step pmcm 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VALU2 SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d $OUT/pmc_mix -o run --output-format csv -- $PMCB ;;
     pmcpf)  step pmcpf 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_perft_fetch -o run --output-format csv -- $PERFTB ;;
     pmcpw)  step pmcpw 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_perft_write -o run --output-format csv -- $PERFTB ;;
-    pmcpm)  step pmcpm 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES -d $OUT/pmc_perft_mix -o run --output-format csv -- $PERFTB ;;
+    pmcpm)  step pmcpm 300 rocprofv3 --pmc $MIXC -d $OUT/pmc_perft_mix -o run --output-format csv -- $PERFTB ;;
+    pmcrf)  step pmcrf 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_roll_fetch -o run --output-format csv -- $PMCR ;;
+    pmcrw)  step pmcrw 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_roll_write -o run --output-format csv -- $PMCR ;;
+    pmcrm)  step pmcrm 300 rocprofv3 --pmc $MIXC -d $OUT/pmc_roll_mix -o run --output-format csv -- $PMCR ;;
+    calib)  step calib 120 rocprofv3 --pmc $MIXC -d $OUT/pmc_calib -o run --output-format csv -- tools/_valu_calib ;;
+    short)  for i in 1 2 3; do step short$i 300 python bench.py --gpus 1 --steps 20 --warmup 5; done
+            step long 300 python bench.py --gpus 1 --steps 1000 --warmup 5 --launched-steps 0 --api-steps 0 --single-episodes 0 --variant-steps 0 --perft-roots 0 --no-cpu-baseline ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
@@ -40,9 +51,13 @@ done
 if [ -n "${PROFILE_TAG:-}" ]; then
   mkdir -p $OUT/summary/$PROFILE_TAG
   [ -f $OUT/prof/run_kernel_stats.csv ] && cp $OUT/prof/run_kernel_stats.csv $OUT/summary/$PROFILE_TAG/kernel_stats.csv
+  [ -f $OUT/profs/run_kernel_stats.csv ] && cp $OUT/profs/run_kernel_stats.csv $OUT/summary/$PROFILE_TAG/kernel_stats_driver_cmd.csv
   [ -d $OUT/pmc_fetch ] && python tools/pmc_summary.py $OUT $OUT/summary/$PROFILE_TAG --kernel "k_env_step2<false, 0>" --dispatches-per-ply ${GC_STREAMS:-2} > /dev/null
   [ -d $OUT/pmc_perft_fetch ] && python tools/pmc_summary.py $OUT $OUT/summary/$PROFILE_TAG --perft > /dev/null
+  [ -d $OUT/pmc_roll_fetch ] && python tools/pmc_summary.py $OUT $OUT/summary/$PROFILE_TAG --rollout > /dev/null
+  [ -d $OUT/pmc_calib ] && python tools/pmc_summary.py $OUT $OUT/summary/$PROFILE_TAG --calib > /dev/null
+  for f in short1 short2 short3 long; do [ -f $OUT/$f.log ] && grep '^{' $OUT/$f.log | tail -1 > $OUT/summary/$PROFILE_TAG/$f.json; done
   for f in bench pmcf; do [ -f $OUT/$f.log ] && grep '^{' $OUT/$f.log | tail -1 > $OUT/summary/$PROFILE_TAG/$f.json; done
-  rm -rf $OUT/prof $OUT/pmc_*
+  rm -rf $OUT/prof $OUT/profs $OUT/pmc_*
 fi
 echo ALLDONE

@@ -2,7 +2,7 @@
 cd ${GRAFT_REPO_ROOT:-.}
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-B="python bench.py --no-cpu-baseline --steps 20 --warmup 400 --fused-plies 0 --perft-roots 0"
+B="python bench.py --no-cpu-baseline --steps 20 --warmup 400 --launched-steps 0 --perft-roots 0"
 for v in "pair:X=1" "one:GC_STEP1=1"; do
   n=${v%%:*}; ev=${v#*:}
   env $ev timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQC_ICACHE_REQ SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQ_IFETCH -d gpurun_out/pmc_ic_$n -o run --output-format csv -- $B > gpurun_out/pmc_ic_$n.log 2>&1 || { tail -5 gpurun_out/pmc_ic_$n.log; exit 1; }

@@ -2,7 +2,7 @@
 cd ${GRAFT_REPO_ROOT:-.}
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-B="python bench.py --no-cpu-baseline --steps 20 --warmup 400 --fused-plies 0 --perft-roots 0"
+B="python bench.py --no-cpu-baseline --steps 20 --warmup 400 --launched-steps 0 --perft-roots 0"
 timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VALU2 SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d gpurun_out/pmc_mix -o run --output-format csv -- $B > gpurun_out/pmc_mix.log 2>&1 || { tail -5 gpurun_out/pmc_mix.log; exit 1; }
 python - <<'PY'
 import csv, collections

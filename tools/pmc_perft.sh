@@ -2,7 +2,7 @@
 cd ${GRAFT_REPO_ROOT:-.}
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES -d gpurun_out/pmc_perft -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 10 --warmup 10 --fused-plies 0 --perft-roots 8192 > gpurun_out/pmc_perft.log 2>&1 || { tail -5 gpurun_out/pmc_perft.log; exit 1; }
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES -d gpurun_out/pmc_perft -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 10 --warmup 10 --launched-steps 0 --perft-roots 8192 > gpurun_out/pmc_perft.log 2>&1 || { tail -5 gpurun_out/pmc_perft.log; exit 1; }
 python - <<'PY'
 import csv, collections
 d = collections.defaultdict(lambda: collections.defaultdict(float))
