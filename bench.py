@@ -467,9 +467,7 @@ def main():
         env, tb = ctx[rep.local.index(rp)][:2]
         env.synchronize()
         t0 = time.perf_counter()
-        env.record_event(0)
-        env.rollout_device(args.steps, tb)  # K env.step() of every board, one launch, per-step trace
-        env.record_event(1)
+        env.rollout_device(args.steps, tb, events=(0, 1))  # K env.step() of every board, one launch, per-step trace
         env.synchronize()
         return None, time.perf_counter() - t0
 

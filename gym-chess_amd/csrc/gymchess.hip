@@ -2957,12 +2957,18 @@ extern "C" int gc_env_rollout(gc_env* e, int n_plies, int16_t* tr_action, int16_
 // (per ROLLOUT_MAX_PLIES), asynchronous on the env's stream; each ply's outputs land in the
 // device trace [n_plies][N] (trace_word) when d_trace is not NULL.  State, windows, counters
 // and the last ply's outputs afterwards are those of n_plies gc_env_step_random plies.
-extern "C" int gc_env_rollout_device(gc_env* e, int n_plies, uint64_t* d_trace) {
+// ev_begin / ev_end: event slots (gc_env_record_event) recorded on the env's stream right
+// before / after the launches, -1 = none (one C-ABI call brackets the timed work).
+extern "C" int gc_env_rollout_device(gc_env* e, int n_plies, uint64_t* d_trace, int ev_begin, int ev_end) {
     if (!e) return fail("null env");
     if (n_plies < 0) return fail("n_plies must be >= 0");
+    if (ev_begin < -1 || ev_begin >= 8 || ev_end < -1 || ev_end >= 8) return fail("event slots: -1 or 0..7");
     if (!e->policy_ready) return fail("policy actions stale: call gc_env_reset or gc_env_select_random first");
     HIPCHK(hipSetDevice(e->device));
-    return issue_rollout(e, n_plies, d_trace, false);
+    if (ev_begin >= 0) HIPCHK(hipEventRecord(e->ev[ev_begin], e->stream));
+    if (issue_rollout(e, n_plies, d_trace, false)) return -1;
+    if (ev_end >= 0) HIPCHK(hipEventRecord(e->ev[ev_end], e->stream));
+    return 0;
 }
 
 extern "C" int gc_env_get_outputs(gc_env* e, int32_t* reward, uint8_t* done, uint8_t* reason, uint16_t* next_action,

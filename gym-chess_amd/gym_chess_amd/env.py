@@ -217,13 +217,15 @@ class BatchedChessEnv:
         _lib.check(self._L.gc_env_rollout(self._h, int(n_plies), None, None, None, None, _lib.ptr(st)))
         return st, None
 
-    def rollout_device(self, n_plies, trace=None):
+    def rollout_device(self, n_plies, trace=None, events=(-1, -1)):
         """n_plies env.step() calls of every board under the random self-play policy in one
         launch, asynchronous (gc_env_rollout_device).  trace: None, or a TraceBuffer with room
-        for n_plies plies: every ply's outputs land in it on the device."""
+        for n_plies plies: every ply's outputs land in it on the device.  events: event slots
+        recorded right before / after the launches (-1 = none; elapsed_ms reads them)."""
         if trace is not None and trace.plies < n_plies:
             raise ValueError(f"trace buffer holds {trace.plies} plies, need {n_plies}")
-        _lib.check(self._L.gc_env_rollout_device(self._h, int(n_plies), trace.ptr if trace is not None else None))
+        _lib.check(self._L.gc_env_rollout_device(self._h, int(n_plies), trace.ptr if trace is not None else None,
+                                                 int(events[0]), int(events[1])))
 
     def trace_buffer(self, plies):
         """device memory for rollout_device's per-ply outputs ([plies][N] packed words)"""

@@ -152,8 +152,10 @@ int gc_env_rollout(gc_env* e, int n_plies, int16_t* tr_action, int16_t* tr_rewar
  * d_trace: NULL, or device memory of n_plies*n uint64 words ([ply][board]) receiving every
  * ply's outputs: bits 0-15 action played (int16, -1 = none: the driver's no-move reset),
  * 16-31 reward (int16), 32-39 done, 40-47 reason.  Afterwards the env is in the state
- * n_plies gc_env_step_random plies leave it in (outputs = the last ply's). */
-int gc_env_rollout_device(gc_env* e, int n_plies, uint64_t* d_trace);
+ * n_plies gc_env_step_random plies leave it in (outputs = the last ply's).  ev_begin /
+ * ev_end: event slots (see gc_env_record_event) recorded right before / after the launches,
+ * -1 = none. */
+int gc_env_rollout_device(gc_env* e, int n_plies, uint64_t* d_trace, int ev_begin, int ev_end);
 int gc_env_get_outputs(gc_env* e, int32_t* reward, uint8_t* done, uint8_t* reason, uint16_t* next_action,
                        uint32_t* nsteps);
 int gc_env_get_states(gc_env* e, int8_t* boards, uint8_t* meta);

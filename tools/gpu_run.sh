@@ -34,7 +34,7 @@ for s in ${STEPS:-smoke pytest bench prof}; do
     pmcf)   step pmcf 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-format csv -- $PMCB ;;
     pmcw)   step pmcw 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run --output-format csv -- $PMCB ;;
     pmcv)   step pmcv 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU -d $OUT/pmc_valu -o run --output-format csv -- $PMCB ;;
-    pmcm)   step pmcm 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VALU2 SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d $OUT/pmc_mix -o run --output-format csv -- $PMCB ;;
+    pmcm)   step pmcm 300 rocprofv3 --pmc $MIXC -d $OUT/pmc_mix -o run --output-format csv -- $PMCB ;;
     pmcpf)  step pmcpf 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_perft_fetch -o run --output-format csv -- $PERFTB ;;
     pmcpw)  step pmcpw 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_perft_write -o run --output-format csv -- $PERFTB ;;
     pmcpm)  step pmcpm 300 rocprofv3 --pmc $MIXC -d $OUT/pmc_perft_mix -o run --output-format csv -- $PERFTB ;;
@@ -52,10 +52,11 @@ if [ -n "${PROFILE_TAG:-}" ]; then
   mkdir -p $OUT/summary/$PROFILE_TAG
   [ -f $OUT/prof/run_kernel_stats.csv ] && cp $OUT/prof/run_kernel_stats.csv $OUT/summary/$PROFILE_TAG/kernel_stats.csv
   [ -f $OUT/profs/run_kernel_stats.csv ] && cp $OUT/profs/run_kernel_stats.csv $OUT/summary/$PROFILE_TAG/kernel_stats_driver_cmd.csv
+  [ -d $OUT/pmc_calib ] && python tools/pmc_summary.py $OUT $OUT/summary/$PROFILE_TAG --calib > /dev/null
+  [ -f $OUT/pmc_calib/run_counter_collection.csv ] && cp $OUT/pmc_calib/run_counter_collection.csv $OUT/summary/$PROFILE_TAG/calib_counters.csv
   [ -d $OUT/pmc_fetch ] && python tools/pmc_summary.py $OUT $OUT/summary/$PROFILE_TAG --kernel "k_env_step2<false, 0>" --dispatches-per-ply ${GC_STREAMS:-2} > /dev/null
   [ -d $OUT/pmc_perft_fetch ] && python tools/pmc_summary.py $OUT $OUT/summary/$PROFILE_TAG --perft > /dev/null
   [ -d $OUT/pmc_roll_fetch ] && python tools/pmc_summary.py $OUT $OUT/summary/$PROFILE_TAG --rollout > /dev/null
-  [ -d $OUT/pmc_calib ] && python tools/pmc_summary.py $OUT $OUT/summary/$PROFILE_TAG --calib > /dev/null
   for f in short1 short2 short3 long; do [ -f $OUT/$f.log ] && grep '^{' $OUT/$f.log | tail -1 > $OUT/summary/$PROFILE_TAG/$f.json; done
   for f in bench pmcf; do [ -f $OUT/$f.log ] && grep '^{' $OUT/$f.log | tail -1 > $OUT/summary/$PROFILE_TAG/$f.json; done
   rm -rf $OUT/prof $OUT/profs $OUT/pmc_*

@@ -34,9 +34,17 @@ def main():
                     help="dispatches of the kernel per ply (bench.py's board-range streams, GC_STREAMS)")
     ap.add_argument("--perft", action="store_true",
                     help="perft leaf kernel (k_perft2_perm) passes pmc_perft_{fetch,write,mix} -> pmc_perft.json")
+    ap.add_argument("--rollout", action="store_true",
+                    help="the headline kernel (last k_env_rollout2<false, 0> dispatch) passes pmc_roll_* -> pmc_rollout.json")
+    ap.add_argument("--calib", action="store_true",
+                    help="tools/_valu_calib under the mix counters (pmc_calib + calib.log) -> valu_calib.json")
     a = ap.parse_args()
+    if a.calib:
+        return calib_summary(a)
     if a.perft:
         return perft_summary(a)
+    if a.rollout:
+        return rollout_summary(a)
     mean = lambda rows, k: sum(r[k] for r in rows) / len(rows)  # noqa: E731
     f = per_dispatch(os.path.join(a.src, "pmc_fetch/run_counter_collection.csv"), a.kernel)[-a.last:]
     w = per_dispatch(os.path.join(a.src, "pmc_write/run_counter_collection.csv"), a.kernel)[-a.last:]
@@ -60,14 +68,16 @@ def main():
     if os.path.exists(mp):  # VALU utilisation (SURVEY 8d asks for it beside the HBM figure)
         v = per_dispatch(mp, a.kernel)[-a.last:]
         waves = mean(v, "SQ_WAVES")
-        simds_per_se = 1024 / 32  # MI355X: 256 CUs x 4 SIMDs over 8 XCDs x 4 SEs
         out["valu"] = {
             "insts_per_wave": mean(v, "SQ_INSTS_VALU") / waves,
             "lane_utilisation": mean(v, "SQ_THREAD_CYCLES_VALU") / (mean(v, "SQ_ACTIVE_INST_VALU") * 64),
-            "busy_frac": mean(v, "SQ_ACTIVE_INST_VALU") * 4 / (mean(v, "SQ_BUSY_CYCLES") * simds_per_se),
-            "note": "busy_frac = SQ_ACTIVE_INST_VALU x 4 cycles / (SQ_BUSY_CYCLES x SIMDs per SE), whole launch "
-                    "incl. ramp and tail; lane_utilisation = active lanes per VALU instruction / 64",
+            "wait_any_share": mean(v, "SQ_WAIT_ANY") / mean(v, "SQ_WAVE_CYCLES"),
+            "note": "lane_utilisation = active lanes per VALU instruction / 64; issue_frac: calibrated class costs "
+                    "(tools/valu_calib.hip) over SIMDs x dispatch cycles (GRBM_GUI_ACTIVE / XCDs)",
         }
+        cal = load_calib(a.dst)
+        if cal:
+            out["valu"].update(valu_issue({k: mean(v, k) for k in v[0]}, cal))
     bl = bench_line(os.path.join(a.src, "pmcf.log"))
     if bl:  # the steady state the counters describe
         out["mean_window"] = bl["roofline"]["mean_window"]
@@ -76,6 +86,94 @@ def main():
     os.makedirs(a.dst, exist_ok=True)
     for p in (os.path.join(a.dst, "pmc_traffic.json"),):
         json.dump(out, open(p, "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+SIMDS = 1024  # MI355X: 256 CUs x 4 SIMDs
+XCDS = 8      # GRBM_GUI_ACTIVE is summed over the XCDs (MI355X_MICROARCH.md, DVFS give-back)
+CALIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "valu_calib.json")
+
+
+def calib_summary(a):
+    """What the VALU counters count, from kernels of known instruction count and class
+    (tools/valu_calib.hip: every SIMD at 4 waves issuing independent chains of one class).
+    cyc_per_winst = cycles each SIMD spends per wave-instruction at full issue =
+    (GRBM_GUI_ACTIVE / XCDs) * SIMDs / wave-instructions."""
+    known = [json.loads(ln) for ln in open(os.path.join(a.src, "calib.log")) if ln.startswith('{"mode"')]
+    rows = per_dispatch(os.path.join(a.src, "pmc_calib", "run_counter_collection.csv"), "k_cal")
+    # two dispatches per mode (warm, timed), in mode order
+    out = {"modes": []}
+    for j, kn in enumerate(known):
+        r = rows[2 * j + 1]
+        wi = kn["wave_insts"]
+        cyc = r["GRBM_GUI_ACTIVE"] / XCDS
+        out["modes"].append({"op": kn["op"], "wave_insts": wi, "ms": kn["ms"],
+                             "insts_valu_per_winst": r["SQ_INSTS_VALU"] / wi,
+                             "int32_per_winst": r["SQ_INSTS_VALU_INT32"] / wi,
+                             "int64_per_winst": r["SQ_INSTS_VALU_INT64"] / wi,
+                             "active_inst_valu_per_winst": r["SQ_ACTIVE_INST_VALU"] / wi,
+                             "thread_cycles_valu_per_winst": r["SQ_THREAD_CYCLES_VALU"] / wi,
+                             "clock_ghz": cyc / (kn["ms"] * 1e-3) / 1e9,
+                             "cyc_per_winst": cyc * SIMDS / wi})
+    m = {x["op"]: x for x in out["modes"]}
+    out["c32"] = m["v_xor_b32"]["cyc_per_winst"]
+    out["c64"] = m["v_lshlrev_b64"]["cyc_per_winst"]
+    out["c32_slow"] = m["v_bcnt_u32_b32"]["cyc_per_winst"]
+    out["note"] = ("VALU issue fraction of a kernel = (INT64 x c64 + (VALU - INT64) x c32) / (SIMDs x GRBM_GUI_ACTIVE / "
+                   "XCDs); c32_slow (v_bcnt class) bounds it from above for 32-bit work")
+    out["profile"] = os.path.basename(a.dst.rstrip("/"))
+    os.makedirs(a.dst, exist_ok=True)
+    json.dump(out, open(os.path.join(a.dst, "valu_calib.json"), "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+def load_calib(dst):
+    """this session's calibration (dst/valu_calib.json) or the committed one"""
+    for p in (os.path.join(dst, "valu_calib.json"), CALIB):
+        if os.path.exists(p):
+            return json.load(open(p))
+    return None
+
+
+def valu_issue(rows_sum, calib):
+    """VALU issue fraction of summed dispatch counters, by the calibrated class costs."""
+    v, i64 = rows_sum["SQ_INSTS_VALU"], rows_sum.get("SQ_INSTS_VALU_INT64", 0.0)
+    cyc = rows_sum["GRBM_GUI_ACTIVE"] / XCDS * SIMDS
+    issued = i64 * calib["c64"] + (v - i64) * calib["c32"]
+    issued_hi = i64 * calib["c64"] + (v - i64) * calib["c32_slow"]
+    return {"issue_frac": issued / cyc, "issue_frac_upper": issued_hi / cyc, "int64_share": i64 / v,
+            "clock_ghz_note": "GRBM_GUI_ACTIVE / XCDs = cycles of the dispatch"}
+
+
+def rollout_summary(a):
+    """The headline kernel: the LAST k_env_rollout2<false, 0> dispatch of the bench command
+    (its timed launch of K steps).  HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE), per
+    board per ply; VALU instructions per wave, lane utilisation, INT64 share, issue fraction
+    (calibrated, tools/valu_calib.hip); SQ_WAIT_ANY share of wave cycles."""
+    kern = "k_env_rollout2<false, 0>"
+    f = per_dispatch(os.path.join(a.src, "pmc_roll_fetch", "run_counter_collection.csv"), kern)[-1]
+    w = per_dispatch(os.path.join(a.src, "pmc_roll_write", "run_counter_collection.csv"), kern)[-1]
+    bl = bench_line(os.path.join(a.src, "pmcrf.log")) or {}
+    plies = bl.get("steps", 20)
+    fetch, write = f["FETCH_SIZE"] * 1024 * 2, w["WRITE_SIZE"] * 1024
+    out = {"kernel": kern, "boards": a.boards, "plies_per_launch": plies, "fetch_bytes_corrected": fetch,
+           "write_bytes": write, "bytes_per_launch": fetch + write,
+           "bytes_per_board_ply": (fetch + write) / a.boards / plies,
+           "mean_window": bl.get("roofline", {}).get("mean_window"),
+           "note": "the timed launch of the driver-shaped bench command (--steps 20 --warmup 5); FETCH_SIZE x2"}
+    mp = os.path.join(a.src, "pmc_roll_mix", "run_counter_collection.csv")
+    if os.path.exists(mp):
+        m = per_dispatch(mp, kern)[-1]
+        waves = m["SQ_WAVES"]
+        out["valu"] = {"insts_per_wave_per_ply": m["SQ_INSTS_VALU"] / waves / plies,
+                       "lane_utilisation": m["SQ_THREAD_CYCLES_VALU"] / (m["SQ_ACTIVE_INST_VALU"] * 64),
+                       "wait_any_share": m["SQ_WAIT_ANY"] / m["SQ_WAVE_CYCLES"]}
+        cal = load_calib(a.dst)
+        if cal:
+            out["valu"].update(valu_issue(m, cal))
+    out["profile"] = os.path.basename(a.dst.rstrip("/"))
+    os.makedirs(a.dst, exist_ok=True)
+    json.dump(out, open(os.path.join(a.dst, "pmc_rollout.json"), "w"), indent=1)
     print(json.dumps(out, indent=1))
 
 
@@ -100,18 +198,18 @@ def perft_summary(a):
     f, w, m = rows("pmc_perft_fetch"), rows("pmc_perft_write"), rows("pmc_perft_mix")
     tot = lambda rs, k: sum(r[k] for r in rs)  # noqa: E731
     waves = tot(m, "SQ_WAVES")
-    simds_per_se = 1024 / 32
     out = {"kernel": kern, "launches": len(m),
            "hbm_bytes_total": tot(f, "FETCH_SIZE") * 1024 * 2 + tot(w, "WRITE_SIZE") * 1024,
            "subtrees_total": waves * 64,
            "alg_bytes_per_subtree": 72,
            "valu": {"insts_per_wave": tot(m, "SQ_INSTS_VALU") / waves,
                     "lane_utilisation": tot(m, "SQ_THREAD_CYCLES_VALU") / (tot(m, "SQ_ACTIVE_INST_VALU") * 64),
-                    "busy_frac": tot(m, "SQ_ACTIVE_INST_VALU") * 4 / (tot(m, "SQ_BUSY_CYCLES") * simds_per_se),
-                    "lds_insts_per_wave": tot(m, "SQ_INSTS_LDS") / waves,
-                    "salu_insts_per_wave": tot(m, "SQ_INSTS_SALU") / waves},
+                    "wait_any_share": tot(m, "SQ_WAIT_ANY") / tot(m, "SQ_WAVE_CYCLES")},
            "profile": os.path.basename(a.dst.rstrip("/"))}
     out["hbm_bytes_per_subtree"] = out["hbm_bytes_total"] / max(out["subtrees_total"], 1)
+    cal = load_calib(a.dst)
+    if cal:
+        out["valu"].update(valu_issue({k: tot(m, k) for k in m[0]}, cal))
     os.makedirs(a.dst, exist_ok=True)
     for p in (os.path.join(a.dst, "pmc_perft.json"),):
         json.dump(out, open(p, "w"), indent=1)

@@ -43,13 +43,13 @@ def main():
             for r in range(a.reps):
                 env.synchronize()
                 t0 = time.perf_counter()
-                env.record_event(0)
                 if a.fused:
-                    env.rollout_device(k, tb)
+                    env.rollout_device(k, tb, events=(0, 1))
                 else:
+                    env.record_event(0)
                     env.step_random(k)
+                    env.record_event(1)
                 t_enq = time.perf_counter()
-                env.record_event(1)
                 env.synchronize()
                 t1 = time.perf_counter()
                 ev = env.elapsed_ms(0, 1) * 1e3
