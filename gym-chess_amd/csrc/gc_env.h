@@ -28,14 +28,16 @@ namespace gc {
 
 // Window capacity.  With opponent "none" (and a WHITE agent) the move cap bounds a window to
 // ~301 boards; a BLACK agent's move_count never advances (chess_v2.py:291-292), so its
-// window is unbounded in the reference: a window that would exceed hist_cap ends the episode
-// with R_WINDOW_FULL (the oracle does the same).
-// The table size is per env (H::bits()):
+// window is unbounded in the reference (saved_boards grows for the whole game,
+// chess_v2.py:192, 404-407).  The per-board table size is per env (H::bits()):
 //  * 2^9 = 512 entries (32 KiB per board, 2 GiB at 65 536 boards) when the move cap bounds
 //    the games (opponent "none", or a WHITE agent): windows of <= ~301 boards, load <= 0.59;
-//    a window may hold HIST_CAP = 384 boards (load 0.75);
-//  * 2^10 = 1024 entries for a BLACK agent, whose games have no move cap: a window may hold
-//    511 boards (the 9-bit window-length field of the meta word), load 0.5.
+//    a window may hold HIST_CAP = 384 boards there (load 0.75);
+//  * 2^10 = 1024 entries for a BLACK agent, whose games have no move cap: the table holds
+//    511 boards of a window (the 9-bit window-length field of the meta word, load 0.5), and
+//    every further board of that window goes to the env's SPILL table (below), so no window
+//    length ends an episode.  R_WINDOW_FULL now means only that the spill table itself ran
+//    out of probes -- the host grows it long before (gc_env_*), and reports the error.
 static constexpr int HTAB_BITS = 9;                 // the move-capped envs (all paired kernels)
 static constexpr int HTAB_BITS_UNCAPPED = 10;       // BLACK agent
 static constexpr int HTAB = 1 << HTAB_BITS;
@@ -77,6 +79,67 @@ GC_HD bool rep_same(const RepEntry& e, const Pos& s) {
 // H (per-board table storage) provides:
 //   int bits(); u32 gen(); void bump_gen(); RepEntry load(int pos); void store_hdr(int pos, u64);
 //   void store(int pos, const RepEntry&)
+// and the spill table (one per env, shared by its boards; only for a BLACK agent's windows
+// past hist_cap, whose table is full -- hl saturates at hist_cap while a window spills):
+//   u32 spill_mask() (0: no spill table), u32 owner() (the board), u64 sp_hdr(u32 slot)
+//   (coherent load), bool sp_cas(u32 slot, u64& expect, u64 desired) (device-wide; on failure
+//   expect := the current value), void sp_set_hdr(u32 slot, u64), void sp_put(u32 slot, const
+//   Pos&), bool sp_same(u32 slot, const Pos&), u32 sp_owner_gen(u32 owner) (its generation as
+//   last published; may lag, never leads), void sp_claimed() (one more slot in use),
+//   void sp_fail() (no free slot within SPILL_PROBES: sticky error for the host).
+// Spill entry (64 B): hdr = (owner + 1) | count << 28 | generation << 32, then 7 bitboards.
+// A slot once claimed never becomes empty again (a dead entry -- its owner's generation moved
+// on -- is reclaimed in place), so a probe sequence stops only at an empty slot and every live
+// entry lies within SPILL_PROBES of its home.
+static constexpr int SPILL_PROBES = 4096;
+GC_HD u64 sp_make(u32 owner, u32 gen, u32 cnt) { return (u64)(owner + 1) | ((u64)cnt << 28) | ((u64)gen << 32); }
+GC_HD u32 sp_owner1(u64 h) { return (u32)h & 0x0FFFFFFFu; }  // owner + 1 (0: empty)
+GC_HD u32 sp_cnt(u64 h) { return ((u32)h >> 28) & 0xFu; }
+GC_HD u32 sp_gen(u64 h) { return (u32)(h >> 32); }
+GC_HD u32 sp_home(u32 key, u32 owner, u32 mask) { return ((key ^ (owner * 0x9E3779B1u)) * 0x85EBCA6Bu >> 7) & mask; }
+
+// the count of board s in the spill part of board owner()'s window after this occurrence
+// (the entry is updated), 0 if it is not there
+template <class H>
+GC_HD int spill_find(H& h, const Pos& s, u32 key) {
+    const u32 mask = h.spill_mask(), me1 = h.owner() + 1, g = h.gen();
+    u32 slot = sp_home(key, h.owner(), mask);
+    for (int probe = 0; probe < SPILL_PROBES; probe++, slot = (slot + 1) & mask) {
+        const u64 e = h.sp_hdr(slot);
+        if (sp_owner1(e) == 0) return 0;
+        if (sp_owner1(e) == me1 && sp_gen(e) == g && h.sp_same(slot, s)) {
+            const u32 c = sp_cnt(e) + 1;
+            h.sp_set_hdr(slot, sp_make(h.owner(), g, c));
+            return (int)c;
+        }
+    }
+    return 0;
+}
+
+// a new board of board owner()'s window into the spill table: 1, or 0 when no slot is free
+// within SPILL_PROBES (sp_fail)
+template <class H>
+GC_HD int spill_insert(H& h, const Pos& s, u32 key) {
+    const u32 mask = h.spill_mask(), g = h.gen();
+    const u64 mine = sp_make(h.owner(), g, 1);
+    u32 slot = sp_home(key, h.owner(), mask);
+    for (int probe = 0; probe < SPILL_PROBES; probe++, slot = (slot + 1) & mask) {
+        u64 e = h.sp_hdr(slot);
+        for (;;) {
+            const u32 o1 = sp_owner1(e);
+            // free, or dead: its owner's published generation is newer than the entry's
+            const bool dead = o1 != 0 && (int)(h.sp_owner_gen(o1 - 1) - sp_gen(e)) > 0;
+            if (o1 != 0 && !dead) break;
+            if (h.sp_cas(slot, e, mine)) {
+                h.sp_put(slot, s);
+                if (o1 == 0) h.sp_claimed();
+                return 1;
+            }  // lost the race: e is the slot's new value, look again
+        }
+    }
+    h.sp_fail();
+    return 0;
+}
 struct RepProbe {
     u32 key;
     RepEntry e0;  // the first probe, loaded early
@@ -108,12 +171,16 @@ GC_HD int rep_commit(H& h, const Pos& s, const RepProbe& pr, u32& hl, bool irrev
         }
         pos = (pos + 1) & size_mask;
     }
+    // a full table means the window spills: the rest of it is in the spill table
+    const bool spilled = h.spill_mask() != 0 && (int)hl >= hist_cap(bits);
+    if (!c && spilled) c = spill_find(h, s, pr.key);
     if (irrev) {  // nothing before this move can recur: clear the window
         h.bump_gen();
         hl = 0;
         return c ? c : 1;
     }
     if (c) return c;
+    if (spilled) return spill_insert(h, s, pr.key);
     if ((int)hl >= hist_cap(bits)) return 0;
     RepEntry ne = {(u64)gen | ((u64)tag << 32) | (1ull << 56), s.k, s.q, s.r, s.b, s.n, s.p, s.w};
     h.store((int)pos, ne);

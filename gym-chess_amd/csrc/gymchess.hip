@@ -100,6 +100,15 @@ struct SoA {
     }
 };
 
+// The env's spill table (gc_env.h spill_find / spill_insert): 64-B entries shared by the
+// boards of a BLACK-agent env whose windows outgrow their per-board tables; ctr[0] = slots
+// ever claimed, ctr[1] = sticky "no free slot" flag (both read by the host, gc_env_*).
+struct SpillTab {
+    u64* ent;  // [mask + 1][8]
+    u32* ctr;
+    u32 mask;  // 0: no spill table (every env but a BLACK agent's)
+};
+
 // repetition window of board i (gc_env.h rep_prefetch / rep_commit): HTAB 64-byte entries
 // per board (entry() below), one cache line each (4 x 16-B loads); generation [N]
 struct DevHist {
@@ -143,6 +152,33 @@ struct DevHist {
         }
         wkind = 0;
     }
+    // the spill table (gc_env.h): headers through device-coherent atomics -- other boards'
+    // lanes, on any XCD, claim slots concurrently; a board's own entry bodies are written and
+    // read only by its own lane (or by later launches)
+    SpillTab sp = {nullptr, nullptr, 0};
+    __device__ u32 spill_mask() const { return sp.mask; }
+    __device__ u32 owner() const { return (u32)i; }
+    __device__ u64 sp_hdr(u32 slot) const {
+        return __hip_atomic_load(sp.ent + (size_t)slot * 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __device__ bool sp_cas(u32 slot, u64& expect, u64 desired) const {
+        return __hip_atomic_compare_exchange_strong(sp.ent + (size_t)slot * 8, &expect, desired, __ATOMIC_RELAXED,
+                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __device__ void sp_set_hdr(u32 slot, u64 v) const {
+        __hip_atomic_store(sp.ent + (size_t)slot * 8, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __device__ void sp_put(u32 slot, const Pos& s) const {
+        u64* d = sp.ent + (size_t)slot * 8;
+        d[1] = s.k; d[2] = s.q; d[3] = s.r; d[4] = s.b; d[5] = s.n; d[6] = s.p; d[7] = s.w;
+    }
+    __device__ bool sp_same(u32 slot, const Pos& s) const {
+        const u64* d = sp.ent + (size_t)slot * 8;
+        return d[1] == s.k && d[2] == s.q && d[3] == s.r && d[4] == s.b && d[5] == s.n && d[6] == s.p && d[7] == s.w;
+    }
+    __device__ u32 sp_owner_gen(u32 o) const { return __hip_atomic_load(hgen + o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+    __device__ void sp_claimed() const { __hip_atomic_fetch_add(sp.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+    __device__ void sp_fail() const { __hip_atomic_fetch_or(sp.ctr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 };
 
 // per-lane move-target scratch in LDS: slot j of lane t at lds[j*BLOCK + t] (each wave's
@@ -423,9 +459,16 @@ struct EnvDev {
         int usable;  // 0: the start position needs the per-square fallback (> 16 pieces)
         int table;   // reset_acts holds all `total` actions
         int open_safe;  // no opening move leaves both kings in check (paired BLACK-agent kernel)
+        // not the start position's: the env's spill table, carried in this device-memory
+        // block because the paired kernels' arguments are full (rewritten when it grows)
+        SpillTab spill;
     } ic;
     int hbits;        // log2 window-table entries per board (DevHist::nb)
-    __device__ DevHist hist(int i, u32 g) const { return DevHist{htab, hgen, g, i, hbits}; }
+    __device__ DevHist hist(int i, u32 g) const {
+        DevHist h{htab, hgen, g, i, hbits};
+        h.sp = ic.spill;
+        return h;
+    }
 };
 
 // The env's per-board fields live in ONE allocation (the "slab"), at offsets that are a
@@ -1414,7 +1457,8 @@ __device__ __forceinline__ PairIO store_io(uint8_t* slab, int nn) {
     pin(s); pin(ua); pin(g0); pin(nst); pin(d);                                                             \
     GC_STAMP(1);                                                                                            \
     int a = (int)ua;                                                                                        \
-    DevHist h = DevHist{htab, in_io.hgen, g0, ii, OPP == 2 ? HTAB_BITS_UNCAPPED : HTAB_BITS};
+    DevHist h = DevHist{htab, in_io.hgen, g0, ii, OPP == 2 ? HTAB_BITS_UNCAPPED : HTAB_BITS};                \
+    if constexpr (OPP == 2) h.sp = icd->spill; /* a BLACK agent's windows may spill */
 
 // One step of the paired driver: opponent "none" (OPP 0: pair_ply) or the random opponent
 // with a WHITE (1) or BLACK (2) agent (pair_step_vs).
@@ -2460,6 +2504,12 @@ struct gc_env {
     hipStream_t sub[GC_MAX_SUBSTREAMS] = {};
     hipEvent_t sub_ev[GC_MAX_SUBSTREAMS] = {};
     hipEvent_t fork_ev = nullptr;
+    // the spill table of a BLACK agent's windows (gc_env.h; SpillTab): its slot counters are
+    // copied to pinned host memory after every stepping call and checked before the next one
+    int sp_bits = 0;
+    u32* sp_ctr_h = nullptr;  // pinned: {slots claimed, failed}
+    hipEvent_t sp_ev = nullptr;
+    int sp_pending = 0;       // stepping calls since the last counter copy was read
 };
 
 static void env_free(gc_env* e) {
@@ -2473,7 +2523,181 @@ static void env_free(gc_env* e) {
     }
     if (e->fork_ev) (void)hipEventDestroy(e->fork_ev);
     if (e->graph_exec) (void)hipGraphExecDestroy(e->graph_exec);
+    if (e->d.ic.spill.ent) (void)hipFree(e->d.ic.spill.ent);
+    if (e->d.ic.spill.ctr) (void)hipFree(e->d.ic.spill.ctr);
+    if (e->sp_ctr_h) (void)hipHostFree(e->sp_ctr_h);
+    if (e->sp_ev) (void)hipEventDestroy(e->sp_ev);
     if (e->stream) (void)hipStreamDestroy(e->stream);
+}
+
+// ----------------------------------------------------------------------------- spill table
+// A BLACK agent's games have no move cap (chess_v2.py:291-292), so its 3-fold window is
+// unbounded (saved_boards, chess_v2.py:192, 404-407).  Boards of a window past its per-board
+// table's hist_cap go to the env's spill table (gc_env.h spill_find / spill_insert).  The
+// host keeps the table's load under 1/4: after each stepping call the slot counters are
+// copied to pinned memory; before the next call (or, when the copy has not landed, after at
+// most SPILL_CHECK_LAG calls, synchronously) they are read, and a table past 1/4 is rehashed
+// -- dead entries dropped, doubled when the live ones pass 1/8.  A failed insert (no free
+// slot within SPILL_PROBES) sets a sticky flag: the next call reports it as an error.
+#define SPILL_CHECK_LAG 4
+
+__global__ void k_spill_rehash(const u64* __restrict__ old, u32 old_mask, SpillTab nt, const u32* __restrict__ hgen) {
+    const size_t slot = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (slot > old_mask) return;
+    const u64* e = old + slot * 8;
+    const u64 hdr = e[0];
+    const u32 o1 = sp_owner1(hdr);
+    if (o1 == 0 || sp_gen(hdr) != hgen[o1 - 1]) return;  // empty or dead
+    Pos b = {e[1], e[2], e[3], e[4], e[5], e[6], e[7], 0};
+    DevHist h{nullptr, const_cast<u32*>(hgen), sp_gen(hdr), (int)(o1 - 1), HTAB_BITS_UNCAPPED};
+    h.sp = nt;
+    u32 t = sp_home(board_key(b), o1 - 1, nt.mask);
+    for (int probe = 0; probe < SPILL_PROBES; probe++, t = (t + 1) & nt.mask) {
+        u64 z = 0;
+        if (h.sp_cas(t, z, hdr)) {
+            h.sp_put(t, b);
+            h.sp_claimed();
+            return;
+        }
+    }
+    h.sp_fail();
+}
+
+static int spill_bits_for(int n) {
+    int b = 14;
+    while (b < 22 && (1 << (b - 4)) < n) b++;  // 2^20 entries (64 MiB) at 65 536 boards
+    return b;
+}
+
+// publish e->d.ic.spill to the device copy the paired kernels read
+static int spill_publish(gc_env* e) {
+    HIPCHK(hipMemcpyAsync(&e->icd->spill, &e->d.ic.spill, sizeof(SpillTab), hipMemcpyHostToDevice, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return 0;
+}
+
+static int spill_alloc(gc_env* e, int bits) {
+    SpillTab t = {nullptr, nullptr, (1u << bits) - 1};
+    if (dalloc(&t.ent, (size_t)8 << bits)) return -1;
+    if (dalloc(&t.ctr, 2)) { (void)hipFree(t.ent); return -1; }
+    hipError_t he = hipMemsetAsync(t.ent, 0, (size_t)64 << bits, e->stream);
+    if (he == hipSuccess) he = hipMemsetAsync(t.ctr, 0, 8, e->stream);
+    if (he == hipSuccess && !e->sp_ctr_h) he = hipHostMalloc(&e->sp_ctr_h, 8, hipHostMallocDefault);
+    if (he == hipSuccess && !e->sp_ev) he = hipEventCreateWithFlags(&e->sp_ev, hipEventDisableTiming);
+    if (he != hipSuccess) { (void)hipFree(t.ent); (void)hipFree(t.ctr); return fail(std::string("spill table: ") + hipGetErrorString(he)); }
+    if (e->d.ic.spill.ent) (void)hipFree(e->d.ic.spill.ent);
+    if (e->d.ic.spill.ctr) (void)hipFree(e->d.ic.spill.ctr);
+    e->d.ic.spill = t;
+    e->sp_bits = bits;
+    e->sp_pending = 0;
+    e->sp_ctr_h[0] = e->sp_ctr_h[1] = 0;
+    return spill_publish(e);
+}
+
+static void spill_drop(gc_env* e) {
+    if (e->d.ic.spill.ent) (void)hipFree(e->d.ic.spill.ent);
+    if (e->d.ic.spill.ctr) (void)hipFree(e->d.ic.spill.ctr);
+    e->d.ic.spill = SpillTab{nullptr, nullptr, 0};
+    e->sp_bits = 0;
+    e->sp_pending = 0;
+}
+
+// rehash the live entries into a table of 2^bits slots (the stream is idle)
+static int spill_rehash(gc_env* e, int bits) {
+    const SpillTab old = e->d.ic.spill;
+    SpillTab t = {nullptr, nullptr, (1u << bits) - 1};
+    if (dalloc(&t.ent, (size_t)8 << bits)) return -1;
+    if (dalloc(&t.ctr, 2)) { (void)hipFree(t.ent); return -1; }
+    u32 c[2] = {0, 0};
+    hipError_t he = hipMemsetAsync(t.ent, 0, (size_t)64 << bits, e->stream);
+    if (he == hipSuccess) he = hipMemsetAsync(t.ctr, 0, 8, e->stream);
+    if (he == hipSuccess) {
+        const size_t slots = (size_t)old.mask + 1;
+        k_spill_rehash<<<(unsigned)((slots + BLOCK - 1) / BLOCK), BLOCK, 0, e->stream>>>(old.ent, old.mask, t, e->d.hgen);
+        he = hipGetLastError();
+    }
+    if (he == hipSuccess) he = hipMemcpyAsync(c, t.ctr, 8, hipMemcpyDeviceToHost, e->stream);
+    if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
+    if (he != hipSuccess || c[1]) {
+        (void)hipFree(t.ent); (void)hipFree(t.ctr);
+        return fail(he != hipSuccess ? std::string("spill rehash: ") + hipGetErrorString(he)
+                                     : std::string("spill rehash: no free slot (table of 2^") + std::to_string(bits) + ")");
+    }
+    (void)hipFree(old.ent);
+    (void)hipFree(old.ctr);
+    e->d.ic.spill = t;
+    e->sp_bits = bits;
+    e->sp_pending = 0;
+    e->sp_ctr_h[0] = c[0];
+    e->sp_ctr_h[1] = 0;
+    return spill_publish(e);
+}
+
+// before a stepping call: the counters of the last copy that landed
+static int spill_before(gc_env* e) {
+    if (!e->d.ic.spill.ent || !e->sp_pending) return 0;
+    if (e->sp_pending >= SPILL_CHECK_LAG) HIPCHK(hipEventSynchronize(e->sp_ev));
+    else if (hipEventQuery(e->sp_ev) != hipSuccess) return 0;  // not landed yet: check next call
+    e->sp_pending = 0;
+    const u32 used = e->sp_ctr_h[0], failed = e->sp_ctr_h[1];
+    if (failed)
+        return fail("repetition spill table: an insert found no free slot (a window outgrew 2^" +
+                    std::to_string(e->sp_bits) + " shared entries); results since the previous call are invalid");
+    const u32 cap = 1u << e->sp_bits;
+    if (used > cap / 4) {
+        HIPCHK(hipStreamSynchronize(e->stream));
+        if (spill_rehash(e, e->sp_bits)) return -1;  // drops the dead entries
+        if (e->sp_ctr_h[0] > cap / 8 && spill_rehash(e, e->sp_bits + 1)) return -1;
+    }
+    return 0;
+}
+
+// after a stepping call: copy the counters (asynchronously) for the next check
+static int spill_after(gc_env* e) {
+    if (!e->d.ic.spill.ent) return 0;
+    HIPCHK(hipMemcpyAsync(e->sp_ctr_h, e->d.ic.spill.ctr, 8, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipEventRecord(e->sp_ev, e->stream));
+    e->sp_pending++;
+    return 0;
+}
+
+// the spill table's state (synchronous): log2 slots (0: none), slots in use (live + dead),
+// live entries
+__global__ void k_spill_live(const u64* __restrict__ ent, u32 mask, const u32* __restrict__ hgen,
+                             unsigned long long* __restrict__ live) {
+    const size_t slot = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (slot > mask) return;
+    const u64 hdr = ent[slot * 8];
+    const u32 o1 = sp_owner1(hdr);
+    if (o1 != 0 && sp_gen(hdr) == hgen[o1 - 1]) atomicAdd(live, 1ull);
+}
+extern "C" int gc_env_spill_info(gc_env* e, int* bits, uint64_t* used, uint64_t* live) {
+    if (!e || !bits || !used || !live) return fail("null argument");
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    *bits = e->sp_bits;
+    *used = *live = 0;
+    const SpillTab& sp = e->d.ic.spill;
+    if (!sp.ent) return 0;
+    unsigned long long* d = nullptr;
+    if (dalloc(&d, 1)) return -1;
+    u32 c[2] = {0, 0};
+    unsigned long long lv = 0;
+    hipError_t he = hipMemsetAsync(d, 0, 8, e->stream);
+    if (he == hipSuccess) {
+        const size_t slots = (size_t)sp.mask + 1;
+        k_spill_live<<<(unsigned)((slots + BLOCK - 1) / BLOCK), BLOCK, 0, e->stream>>>(sp.ent, sp.mask, e->d.hgen, d);
+        he = hipGetLastError();
+    }
+    if (he == hipSuccess) he = hipMemcpyAsync(&lv, d, 8, hipMemcpyDeviceToHost, e->stream);
+    if (he == hipSuccess) he = hipMemcpyAsync(c, sp.ctr, 8, hipMemcpyDeviceToHost, e->stream);
+    if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
+    (void)hipFree(d);
+    if (he != hipSuccess) return fail(std::string("spill info: ") + hipGetErrorString(he));
+    *used = c[0];
+    *live = lv;
+    if (c[1]) return fail("repetition spill table: an insert found no free slot");
+    return 0;
 }
 
 // kernel dispatch on the env's opponent mode (a kernel-argument-uniform choice made once per
@@ -2644,6 +2868,13 @@ extern "C" int gc_env_set_opponent(gc_env* e, int opponent, int agent_white) {
         e->d.hbits = bits;
         if (e->graph_exec) { (void)hipGraphExecDestroy(e->graph_exec); e->graph_exec = nullptr; }
     }
+    if (!agent_white && !e->d.ic.spill.ent) {  // a BLACK agent's windows may outgrow the table
+        if (spill_alloc(e, spill_bits_for(e->n))) return -1;
+    } else if (agent_white && e->d.ic.spill.ent) {
+        HIPCHK(hipStreamSynchronize(e->stream));
+        spill_drop(e);
+        if (spill_publish(e)) return -1;
+    }
     e->d.opp = opponent;
     e->d.agent_black = agent_white ? 0 : 1;
     HIPCHK(hipMemsetAsync(e->d.draw, 0, (size_t)4 * e->n, e->stream));  // fresh policy streams
@@ -2706,9 +2937,11 @@ extern "C" int gc_env_step(gc_env* e, const uint16_t* actions, int32_t* reward, 
     for (int i = 0; i < e->n; i++)
         if (actions[i] > A_RESIGN) return fail("action out of range [0, 4100] at index " + std::to_string(i));
     HIPCHK(hipSetDevice(e->device));
+    if (spill_before(e)) return -1;
     HIPCHK(hipMemcpyAsync(e->d.act, actions, (size_t)2 * e->n, hipMemcpyHostToDevice, e->stream));
     launch_step<false>(e);
     HIPCHK(hipGetLastError());
+    if (spill_after(e)) return -1;
     e->policy_ready = false;
     if (reward) HIPCHK(hipMemcpyAsync(reward, e->d.reward, (size_t)4 * e->n, hipMemcpyDeviceToHost, e->stream));
     if (done) HIPCHK(hipMemcpyAsync(done, e->d.done, e->n, hipMemcpyDeviceToHost, e->stream));
@@ -2727,6 +2960,7 @@ extern "C" int gc_env_step_device(gc_env* e, const uint16_t* d_actions, int32_t*
     if (e->rules) return fail("gc_env_step_device: reference rules only (FIDE: gc_env_step)");
     if (flags & ~1) return fail("flags: bit 0 = auto-reset");
     HIPCHK(hipSetDevice(e->device));
+    if (spill_before(e)) return -1;
     const int ar = flags & 1;
     static const bool one_wave = getenv("GC_STEP1") != nullptr;  // A/B switch to the one-wave kernel
     if (!e->d.opp && e->d.ic.usable && e->d.ic.table && !one_wave) {
@@ -2752,6 +2986,7 @@ extern "C" int gc_env_step_device(gc_env* e, const uint16_t* d_actions, int32_t*
         k_env_step_api<false><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d, d_actions, d_reward, d_done, d_reason,
                                                                        d_mask, d_obs, d_count, d_pick, ar);
     HIPCHK(hipGetLastError());
+    if (spill_after(e)) return -1;
     e->policy_ready = d_pick != nullptr;
     return 0;
 }
@@ -2814,10 +3049,15 @@ static int issue_plies(gc_env* e, int n) {
 
 // device-resident random self-play: n_plies launches of the one-ply step kernel (no host
 // traffic, no sync).  Outputs of the LAST ply stay in device buffers (gc_env_get_outputs).
+static int step_random(gc_env* e, int n_plies);
 extern "C" int gc_env_step_random(gc_env* e, int n_plies) {
     if (!e) return fail("null env");
     if (!e->policy_ready) return fail("policy actions stale: call gc_env_reset or gc_env_select_random first");
     HIPCHK(hipSetDevice(e->device));
+    if (spill_before(e) || step_random(e, n_plies)) return -1;
+    return spill_after(e);
+}
+static int step_random(gc_env* e, int n_plies) {
     static const bool one_wave = getenv("GC_STEP1") != nullptr;  // A/B switch to k_env_step<true, false>
     static const int graph_chunk = getenv("GC_GRAPH") ? atoi(getenv("GC_GRAPH")) : 0;
     const bool pair = pair_ok(e) && !one_wave;  // the paired kernel (pair_ok: all but rare opponent setups)
@@ -2926,8 +3166,9 @@ extern "C" int gc_env_rollout(gc_env* e, int n_plies, int16_t* tr_action, int16_
     const size_t cnt = (size_t)n_plies * e->n;
     u64* dt = nullptr;
     if (trace && cnt && dalloc(&dt, cnt)) return -1;
+    if (spill_before(e)) { (void)hipFree(dt); return -1; }
     HIPCHK(hipMemsetAsync(e->stats, 0, (size_t)64 * e->n, e->stream));
-    if (issue_rollout(e, n_plies, dt, true)) { (void)hipFree(dt); return -1; }
+    if (issue_rollout(e, n_plies, dt, true) || spill_after(e)) { (void)hipFree(dt); return -1; }
     if (trace && cnt) {
         std::vector<u64> h(cnt);
         hipError_t ce = hipMemcpyAsync(h.data(), dt, cnt * 8, hipMemcpyDeviceToHost, e->stream);
@@ -2965,10 +3206,11 @@ extern "C" int gc_env_rollout_device(gc_env* e, int n_plies, uint64_t* d_trace, 
     if (ev_begin < -1 || ev_begin >= 8 || ev_end < -1 || ev_end >= 8) return fail("event slots: -1 or 0..7");
     if (!e->policy_ready) return fail("policy actions stale: call gc_env_reset or gc_env_select_random first");
     HIPCHK(hipSetDevice(e->device));
+    if (spill_before(e)) return -1;
     if (ev_begin >= 0) HIPCHK(hipEventRecord(e->ev[ev_begin], e->stream));
     if (issue_rollout(e, n_plies, d_trace, false)) return -1;
     if (ev_end >= 0) HIPCHK(hipEventRecord(e->ev[ev_end], e->stream));
-    return 0;
+    return spill_after(e);
 }
 
 extern "C" int gc_env_get_outputs(gc_env* e, int32_t* reward, uint8_t* done, uint8_t* reason, uint16_t* next_action,
@@ -3320,21 +3562,31 @@ extern "C" int gc_env_set_en_passant(gc_env* e, const int8_t* files) {
 // ----------------------------------------------------------------------------- checkpoint
 // Bit-exact save / restore of a whole env (SURVEY.md §5 "save/load = memcpy of state +
 // repetition history"; the reference keeps its history in ChessEnvV2.saved_boards,
-// chess_v2.py:192, 404-407, beside the state dict, 301-323).  Blob layout:
+// chess_v2.py:192, 404-407, beside the state dict, 301-323).  Blob layout (version 2):
 //   CkptHeader | slab (Slab::BYTES_PER_BOARD * n: bitboards, meta, window generation, Philox
-//   draw counter, step counter, last outputs, next action) | the live window entries, board
-//   by board (hl_of(meta[i]) entries of 8 u64: header {tag | count << 56}, 7 bitboards).
-// Only live entries travel (<= ~301 per board, not the table): restoring re-inserts them
-// under a fresh generation, so a restored board answers every later probe exactly as before
-// (same boards, same counts; slot positions may differ, which no result depends on).
+//   draw counter, step counter, last outputs, next action) | spill counts u32[n] (live spill
+//   entries per board, zero unless a BLACK agent's window spilled) | the live window-table
+//   entries, board by board (hl_of(meta[i]) entries of 8 u64: header {tag | count << 56}, 7
+//   bitboards) | the live spill entries, board by board (8 u64: count, 7 bitboards).
+// Only live entries travel: restoring re-inserts them under a fresh generation, so a restored
+// board answers every later probe exactly as before (same boards, same counts; slot positions
+// may differ, which no result depends on).  The header pins the slab's field layout
+// (CKPT_LAYOUT); a blob whose windows do not fit the env's tables is refused before anything
+// of the env changes.
 struct CkptHeader {
-    char magic[8];  // "GCCKPT1"
+    char magic[8];  // "GCCKPT2"
     uint32_t version, n, rules, opp, agent_black, policy_ready;
     uint64_t seed;
     uint64_t init[NBB];  // the env's initial board (resets land on it)
-    uint64_t entries;
+    uint64_t entries;        // window-table entries
+    uint64_t spill_entries;  // spill-table entries
+    uint64_t layout;         // CKPT_LAYOUT of the writer
 };
-static const char CKPT_MAGIC[8] = {'G', 'C', 'C', 'K', 'P', 'T', '1', 0};
+static const char CKPT_MAGIC[8] = {'G', 'C', 'C', 'K', 'P', 'T', '2', 0};
+// the slab's size and field offsets per board (a writer with another layout is refused)
+static constexpr uint64_t CKPT_LAYOUT = (uint64_t)Slab::BYTES_PER_BOARD | (56ull << 8) | (60ull << 16) | (64ull << 24) |
+                                        (68ull << 32) | (72ull << 40) | (76ull << 48) | (78ull << 56);
+static_assert(Slab::BYTES_PER_BOARD == 80, "update CKPT_LAYOUT with the slab");
 
 __global__ void k_hl_of(const u32* __restrict__ meta, int n, uint32_t* __restrict__ hl) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -3366,6 +3618,24 @@ __global__ void k_ckpt_pack(const u64* __restrict__ htab, const u32* __restrict_
     if (k != hl) atomicOr(bad, 1u);
 }
 
+// live spill entries per board (cnt zeroed by the caller); with out: packed at
+// out[offs[owner] + fill[owner]++] as {count, 7 bitboards}
+__global__ void k_spill_collect(const u64* __restrict__ ent, u32 mask, const u32* __restrict__ hgen,
+                                uint32_t* __restrict__ cnt, const uint32_t* __restrict__ offs, u64* __restrict__ out) {
+    const size_t slot = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (slot > mask) return;
+    const u64* e = ent + slot * 8;
+    const u64 hdr = e[0];
+    const u32 o1 = sp_owner1(hdr);
+    if (o1 == 0 || sp_gen(hdr) != hgen[o1 - 1]) return;
+    const u32 k = atomicAdd(cnt + (o1 - 1), 1u);
+    if (!out) return;
+    u64* d = out + ((size_t)offs[o1 - 1] + k) * 8;
+    d[0] = sp_cnt(hdr);
+#pragma unroll
+    for (int j = 1; j < 8; j++) d[j] = e[j];
+}
+
 // fresh generation per board: above both the live table's and the saved one, so no entry of
 // the live table can pass for a restored one
 __global__ void k_ckpt_gen(const u32* __restrict__ live_hgen, const u32* __restrict__ saved_hgen, int n,
@@ -3374,16 +3644,30 @@ __global__ void k_ckpt_gen(const u32* __restrict__ live_hgen, const u32* __restr
     if (i < n) gnew[i] = (live_hgen[i] > saved_hgen[i] ? live_hgen[i] : saved_hgen[i]) + 1u;
 }
 
+// refuse a blob whose windows do not fit the env's tables (before the env changes): a window
+// longer than hist_cap, or spill entries without a full table or without a spill table
+__global__ void k_ckpt_check(const u32* __restrict__ meta, const uint32_t* __restrict__ scnt, int n, int nb, int spill,
+                             uint32_t* __restrict__ bad) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int hl = (int)hl_of(meta[i]);
+    if (hl > hist_cap(nb)) atomicOr(bad, 1u);
+    if (scnt[i] && (!spill || hl < hist_cap(nb))) atomicOr(bad, 2u);
+}
+
 // board i takes generation gnew[i] and its saved entries are inserted by the probe rule of
-// rep_commit (gc_env.h): home slot = key & (HTAB-1), linear probing
+// rep_commit (gc_env.h): home slot = key & (HTAB-1), linear probing; its spill entries by
+// spill_insert's
 __global__ void k_ckpt_unpack(u64* __restrict__ htab, u32* __restrict__ hgen, const u32* __restrict__ meta, int n,
                               int nb, const uint32_t* __restrict__ gnew, const uint32_t* __restrict__ offs,
-                              const u64* __restrict__ in, uint32_t* __restrict__ bad) {
+                              const u64* __restrict__ in, SpillTab sp, const uint32_t* __restrict__ scnt,
+                              const uint32_t* __restrict__ soffs, const u64* __restrict__ sin, uint32_t* __restrict__ bad) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const u32 g = gnew[i];
     hgen[i] = g;
     DevHist h{htab, hgen, g, i, nb};
+    h.sp = sp;
     const u32 hl = hl_of(meta[i]);
     const int size = 1 << nb;
     for (u32 k = 0; k < hl; k++) {
@@ -3399,21 +3683,31 @@ __global__ void k_ckpt_unpack(u64* __restrict__ htab, u32* __restrict__ hgen, co
 #pragma unroll
         for (int j = 1; j < 8; j++) d[j] = e[j];
     }
+    for (u32 k = 0; k < (scnt ? scnt[i] : 0u); k++) {
+        const u64* e = sin + ((size_t)soffs[i] + k) * 8;
+        Pos b = {e[1], e[2], e[3], e[4], e[5], e[6], e[7], 0};
+        if (!spill_insert(h, b, board_key(b))) { atomicOr(bad, 4u); return; }
+        u32 t = sp_home(board_key(b), (u32)i, sp.mask);  // the entry just inserted: set its count
+        for (int probe = 0; probe < SPILL_PROBES; probe++, t = (t + 1) & sp.mask) {
+            const u64 x = h.sp_hdr(t);
+            if (sp_owner1(x) == (u32)i + 1 && sp_gen(x) == g && h.sp_same(t, b)) {
+                h.sp_set_hdr(t, sp_make((u32)i, g, (u32)e[0]));
+                break;
+            }
+        }
+    }
 }
 
-// exclusive scan of the window lengths of `meta` (the saved or live slab's) -> offs; returns
-// the total entry count
-static int ckpt_offsets(gc_env* e, const u32* meta, uint32_t* hl, uint32_t* offs, uint64_t* total) {
-    const int n = e->n;
-    k_hl_of<<<grid_for(n), BLOCK, 0, e->stream>>>(meta, n, hl);
+// exclusive scan of v (n entries) -> offs; returns the total
+static int scan_u32(gc_env* e, const uint32_t* v, uint32_t* offs, int n, uint64_t* total) {
     size_t tb = 0;
     void* tmp = nullptr;
-    hipError_t he = hipcub::DeviceScan::ExclusiveSum(nullptr, tb, hl, offs, n, e->stream);
+    hipError_t he = hipcub::DeviceScan::ExclusiveSum(nullptr, tb, v, offs, n, e->stream);
     if (he == hipSuccess && dalloc((char**)&tmp, tb ? tb : 1)) return -1;
-    if (he == hipSuccess) he = hipcub::DeviceScan::ExclusiveSum(tmp, tb, hl, offs, n, e->stream);
+    if (he == hipSuccess) he = hipcub::DeviceScan::ExclusiveSum(tmp, tb, v, offs, n, e->stream);
     uint32_t lo = 0, lc = 0;
     if (he == hipSuccess) he = hipMemcpyAsync(&lo, offs + n - 1, 4, hipMemcpyDeviceToHost, e->stream);
-    if (he == hipSuccess) he = hipMemcpyAsync(&lc, hl + n - 1, 4, hipMemcpyDeviceToHost, e->stream);
+    if (he == hipSuccess) he = hipMemcpyAsync(&lc, v + n - 1, 4, hipMemcpyDeviceToHost, e->stream);
     if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
     (void)hipFree(tmp);
     if (he != hipSuccess) return fail(std::string("checkpoint scan: ") + hipGetErrorString(he));
@@ -3421,20 +3715,42 @@ static int ckpt_offsets(gc_env* e, const u32* meta, uint32_t* hl, uint32_t* offs
     return 0;
 }
 
-static size_t ckpt_bytes(int n, uint64_t entries) {
-    return sizeof(CkptHeader) + Slab::BYTES_PER_BOARD * (size_t)n + 64 * (size_t)entries;
+// exclusive scan of the window lengths of `meta` (the saved or live slab's) -> offs; returns
+// the total entry count
+static int ckpt_offsets(gc_env* e, const u32* meta, uint32_t* hl, uint32_t* offs, uint64_t* total) {
+    k_hl_of<<<grid_for(e->n), BLOCK, 0, e->stream>>>(meta, e->n, hl);
+    return scan_u32(e, hl, offs, e->n, total);
+}
+
+// live spill entries per board (scnt) and their offsets (soffs); total
+static int spill_offsets(gc_env* e, uint32_t* scnt, uint32_t* soffs, uint64_t* total) {
+    HIPCHK(hipMemsetAsync(scnt, 0, (size_t)4 * e->n, e->stream));
+    const SpillTab& sp = e->d.ic.spill;
+    if (sp.ent) {
+        const size_t slots = (size_t)sp.mask + 1;
+        k_spill_collect<<<(unsigned)((slots + BLOCK - 1) / BLOCK), BLOCK, 0, e->stream>>>(sp.ent, sp.mask, e->d.hgen, scnt,
+                                                                                          nullptr, nullptr);
+        HIPCHK(hipGetLastError());
+    }
+    return scan_u32(e, scnt, soffs, e->n, total);
+}
+
+static size_t ckpt_bytes(int n, uint64_t entries, uint64_t spill_entries) {
+    return sizeof(CkptHeader) + (Slab::BYTES_PER_BOARD + 4) * (size_t)n + 64 * (size_t)(entries + spill_entries);
 }
 
 extern "C" int gc_env_checkpoint_bytes(gc_env* e, uint64_t* bytes) {
     if (!e || !bytes) return fail("null argument");
     HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipStreamSynchronize(e->stream));
     uint32_t *hl = nullptr, *offs = nullptr;
     if (dalloc(&hl, e->n) || dalloc(&offs, e->n)) { (void)hipFree(hl); return -1; }
-    uint64_t total = 0;
+    uint64_t total = 0, stotal = 0;
     int rc = ckpt_offsets(e, e->meta, hl, offs, &total);
+    if (!rc) rc = spill_offsets(e, hl, offs, &stotal);
     (void)hipFree(hl); (void)hipFree(offs);
     if (rc) return rc;
-    *bytes = ckpt_bytes(e->n, total);
+    *bytes = ckpt_bytes(e->n, total, stotal);
     return 0;
 }
 
@@ -3443,36 +3759,53 @@ extern "C" int gc_env_save(gc_env* e, void* buf, uint64_t cap, uint64_t* written
     HIPCHK(hipSetDevice(e->device));
     HIPCHK(hipStreamSynchronize(e->stream));
     const int n = e->n;
-    uint32_t *hl = nullptr, *offs = nullptr, *bad = nullptr;
-    u64* ents = nullptr;
-    auto release = [&]() { (void)hipFree(hl); (void)hipFree(offs); (void)hipFree(bad); (void)hipFree(ents); };
-    if (dalloc(&hl, n) || dalloc(&offs, n) || dalloc(&bad, 1)) { release(); return -1; }
-    uint64_t total = 0;
-    if (ckpt_offsets(e, e->meta, hl, offs, &total)) { release(); return -1; }
-    const size_t need = ckpt_bytes(n, total);
+    uint32_t *hl = nullptr, *offs = nullptr, *bad = nullptr, *scnt = nullptr, *soffs = nullptr, *fill = nullptr;
+    u64 *ents = nullptr, *sents = nullptr;
+    auto release = [&]() {
+        (void)hipFree(hl); (void)hipFree(offs); (void)hipFree(bad); (void)hipFree(ents);
+        (void)hipFree(scnt); (void)hipFree(soffs); (void)hipFree(fill); (void)hipFree(sents);
+    };
+    if (dalloc(&hl, n) || dalloc(&offs, n) || dalloc(&bad, 1) || dalloc(&scnt, n) || dalloc(&soffs, n) ||
+        dalloc(&fill, n)) { release(); return -1; }
+    uint64_t total = 0, stotal = 0;
+    if (ckpt_offsets(e, e->meta, hl, offs, &total) || spill_offsets(e, scnt, soffs, &stotal)) { release(); return -1; }
+    const size_t need = ckpt_bytes(n, total, stotal);
     if (written) *written = need;
     if (cap < need) { release(); return fail("checkpoint buffer too small: need " + std::to_string(need) + " bytes"); }
-    if (dalloc(&ents, 8 * (total ? total : 1))) { release(); return -1; }
+    if (dalloc(&ents, 8 * (total ? total : 1)) || dalloc(&sents, 8 * (stotal ? stotal : 1))) { release(); return -1; }
     CkptHeader hd = {};
     memcpy(hd.magic, CKPT_MAGIC, 8);
-    hd.version = 1; hd.n = (uint32_t)n; hd.rules = (uint32_t)e->rules; hd.opp = (uint32_t)e->d.opp;
+    hd.version = 2; hd.n = (uint32_t)n; hd.rules = (uint32_t)e->rules; hd.opp = (uint32_t)e->d.opp;
     hd.agent_black = (uint32_t)e->d.agent_black; hd.policy_ready = e->policy_ready ? 1u : 0u;
     hd.seed = e->seed;
     for (int j = 0; j < NBB; j++) hd.init[j] = e->d.init[j];
     hd.entries = total;
+    hd.spill_entries = stotal;
+    hd.layout = CKPT_LAYOUT;
     uint8_t* out = static_cast<uint8_t*>(buf);
     memcpy(out, &hd, sizeof hd);
+    const size_t o_slab = sizeof hd, o_scnt = o_slab + Slab::BYTES_PER_BOARD * (size_t)n, o_ent = o_scnt + 4 * (size_t)n,
+                 o_sent = o_ent + 64 * (size_t)total;
     uint32_t flag = 0;
     hipError_t he = hipMemsetAsync(bad, 0, 4, e->stream);
     if (he == hipSuccess) {
         k_ckpt_pack<<<grid_for(n), BLOCK, 0, e->stream>>>(e->d.htab, e->d.hgen, e->meta, n, e->d.hbits, offs, ents, bad);
         he = hipGetLastError();
     }
-    if (he == hipSuccess)
-        he = hipMemcpyAsync(out + sizeof hd, e->slab, Slab::BYTES_PER_BOARD * (size_t)n, hipMemcpyDeviceToHost, e->stream);
-    if (he == hipSuccess && total)
-        he = hipMemcpyAsync(out + sizeof hd + Slab::BYTES_PER_BOARD * (size_t)n, ents, 64 * total, hipMemcpyDeviceToHost,
-                            e->stream);
+    if (he == hipSuccess && stotal) {
+        const SpillTab& sp = e->d.ic.spill;
+        const size_t slots = (size_t)sp.mask + 1;
+        he = hipMemsetAsync(fill, 0, (size_t)4 * n, e->stream);
+        if (he == hipSuccess) {
+            k_spill_collect<<<(unsigned)((slots + BLOCK - 1) / BLOCK), BLOCK, 0, e->stream>>>(sp.ent, sp.mask, e->d.hgen,
+                                                                                              fill, soffs, sents);
+            he = hipGetLastError();
+        }
+    }
+    if (he == hipSuccess) he = hipMemcpyAsync(out + o_slab, e->slab, Slab::BYTES_PER_BOARD * (size_t)n, hipMemcpyDeviceToHost, e->stream);
+    if (he == hipSuccess) he = hipMemcpyAsync(out + o_scnt, scnt, 4 * (size_t)n, hipMemcpyDeviceToHost, e->stream);
+    if (he == hipSuccess && total) he = hipMemcpyAsync(out + o_ent, ents, 64 * total, hipMemcpyDeviceToHost, e->stream);
+    if (he == hipSuccess && stotal) he = hipMemcpyAsync(out + o_sent, sents, 64 * stotal, hipMemcpyDeviceToHost, e->stream);
     if (he == hipSuccess) he = hipMemcpyAsync(&flag, bad, 4, hipMemcpyDeviceToHost, e->stream);
     if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
     release();
@@ -3486,39 +3819,71 @@ extern "C" int gc_env_load(gc_env* e, const void* buf, uint64_t size) {
     if (size < sizeof(CkptHeader)) return fail("checkpoint: truncated header");
     CkptHeader hd;
     memcpy(&hd, buf, sizeof hd);
-    if (memcmp(hd.magic, CKPT_MAGIC, 8) != 0 || hd.version != 1) return fail("checkpoint: not a gc_env checkpoint (v1)");
+    if (memcmp(hd.magic, CKPT_MAGIC, 8) != 0 || hd.version != 2) return fail("checkpoint: not a gc_env checkpoint (v2)");
+    if (hd.layout != CKPT_LAYOUT) return fail("checkpoint: written by a build with another slab layout");
     if ((int)hd.n != e->n) return fail("checkpoint: it holds " + std::to_string(hd.n) + " boards, the env " + std::to_string(e->n));
     if ((int)hd.rules != e->rules || (int)hd.opp != e->d.opp || (int)hd.agent_black != e->d.agent_black)
         return fail("checkpoint: rules / opponent / player colour differ from the env's");
     if (hd.seed != e->seed) return fail("checkpoint: the env's seed differs (the policy streams would not continue)");
     for (int j = 0; j < NBB; j++)
         if (hd.init[j] != e->d.init[j]) return fail("checkpoint: the env's initial board differs");
-    if (size != ckpt_bytes(e->n, hd.entries)) return fail("checkpoint: size does not match its header");
+    if (size != ckpt_bytes(e->n, hd.entries, hd.spill_entries)) return fail("checkpoint: size does not match its header");
+    if (hd.spill_entries && !e->d.ic.spill.ent) return fail("checkpoint: spill entries, but the env has no spill table");
     HIPCHK(hipSetDevice(e->device));
     HIPCHK(hipStreamSynchronize(e->stream));
     const int n = e->n;
     const uint8_t* in = static_cast<const uint8_t*>(buf);
+    const size_t o_slab = sizeof hd, o_scnt = o_slab + Slab::BYTES_PER_BOARD * (size_t)n, o_ent = o_scnt + 4 * (size_t)n,
+                 o_sent = o_ent + 64 * (size_t)hd.entries;
     uint8_t* slab = nullptr;
-    u64* ents = nullptr;
-    uint32_t *hl = nullptr, *offs = nullptr, *gnew = nullptr, *bad = nullptr;
+    u64 *ents = nullptr, *sents = nullptr;
+    uint32_t *hl = nullptr, *offs = nullptr, *gnew = nullptr, *bad = nullptr, *scnt = nullptr, *soffs = nullptr;
     auto release = [&]() {
         (void)hipFree(slab); (void)hipFree(ents); (void)hipFree(hl); (void)hipFree(offs); (void)hipFree(gnew);
-        (void)hipFree(bad);
+        (void)hipFree(bad); (void)hipFree(sents); (void)hipFree(scnt); (void)hipFree(soffs);
     };
     if (dalloc(&slab, Slab::BYTES_PER_BOARD * (size_t)n) || dalloc(&ents, 8 * (hd.entries ? hd.entries : 1)) ||
-        dalloc(&hl, n) || dalloc(&offs, n) || dalloc(&gnew, n) || dalloc(&bad, 1)) {
+        dalloc(&sents, 8 * (hd.spill_entries ? hd.spill_entries : 1)) || dalloc(&hl, n) || dalloc(&offs, n) ||
+        dalloc(&gnew, n) || dalloc(&bad, 1) || dalloc(&scnt, n) || dalloc(&soffs, n)) {
         release();
         return -1;
     }
-    hipError_t he = hipMemcpyAsync(slab, in + sizeof hd, Slab::BYTES_PER_BOARD * (size_t)n, hipMemcpyHostToDevice, e->stream);
+    // stage everything and validate it against the env's tables before touching the env
+    hipError_t he = hipMemcpyAsync(slab, in + o_slab, Slab::BYTES_PER_BOARD * (size_t)n, hipMemcpyHostToDevice, e->stream);
+    if (he == hipSuccess) he = hipMemcpyAsync(scnt, in + o_scnt, 4 * (size_t)n, hipMemcpyHostToDevice, e->stream);
     if (he == hipSuccess && hd.entries)
-        he = hipMemcpyAsync(ents, in + sizeof hd + Slab::BYTES_PER_BOARD * (size_t)n, 64 * hd.entries,
-                            hipMemcpyHostToDevice, e->stream);
+        he = hipMemcpyAsync(ents, in + o_ent, 64 * hd.entries, hipMemcpyHostToDevice, e->stream);
+    if (he == hipSuccess && hd.spill_entries)
+        he = hipMemcpyAsync(sents, in + o_sent, 64 * hd.spill_entries, hipMemcpyHostToDevice, e->stream);
     if (he != hipSuccess) { release(); return fail(std::string("checkpoint load: ") + hipGetErrorString(he)); }
-    uint64_t total = 0;
+    uint64_t total = 0, stotal = 0;
     const u32* smeta = reinterpret_cast<const u32*>(slab + Slab::meta(n));
-    if (ckpt_offsets(e, smeta, hl, offs, &total)) { release(); return -1; }
-    if (total != hd.entries) { release(); return fail("checkpoint: window lengths do not match the entries it holds"); }
+    if (ckpt_offsets(e, smeta, hl, offs, &total) || scan_u32(e, scnt, soffs, n, &stotal)) { release(); return -1; }
+    if (total != hd.entries || stotal != hd.spill_entries) {
+        release();
+        return fail("checkpoint: window lengths do not match the entries it holds");
+    }
+    uint32_t flag = 0;
+    he = hipMemsetAsync(bad, 0, 4, e->stream);
+    if (he == hipSuccess) {
+        k_ckpt_check<<<grid_for(n), BLOCK, 0, e->stream>>>(smeta, scnt, n, e->d.hbits, e->d.ic.spill.ent != nullptr, bad);
+        he = hipGetLastError();
+    }
+    if (he == hipSuccess) he = hipMemcpyAsync(&flag, bad, 4, hipMemcpyDeviceToHost, e->stream);
+    if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
+    if (he != hipSuccess || flag) {
+        release();
+        return fail(he != hipSuccess ? std::string("checkpoint load: ") + hipGetErrorString(he)
+                                     : std::string("checkpoint: its repetition windows do not fit this env's tables"));
+    }
+    // the spill table, emptied (every entry would be dead under the fresh generations) and
+    // sized for the restored entries at a load <= 1/8
+    if (e->d.ic.spill.ent) {
+        int bits = e->sp_bits;
+        while (((uint64_t)1 << bits) < 8 * stotal) bits++;
+        if (spill_alloc(e, bits)) { release(); return -1; }
+    }
+    // from here on the env changes; a failure resets every board (never a half-restored env)
     k_ckpt_gen<<<grid_for(n), BLOCK, 0, e->stream>>>(e->d.hgen, reinterpret_cast<const u32*>(slab + Slab::hgen(n)), n,
                                                      gnew);
     he = hipGetLastError();
@@ -3527,15 +3892,24 @@ extern "C" int gc_env_load(gc_env* e, const void* buf, uint64_t size) {
     if (he == hipSuccess) he = hipMemsetAsync(bad, 0, 4, e->stream);
     if (he == hipSuccess) {
         k_ckpt_unpack<<<grid_for(n), BLOCK, 0, e->stream>>>(e->d.htab, e->d.hgen, e->meta, n, e->d.hbits, gnew, offs,
-                                                            ents, bad);
+                                                            ents, e->d.ic.spill, stotal ? scnt : nullptr, soffs, sents,
+                                                            bad);
         he = hipGetLastError();
     }
-    uint32_t flag = 0;
     if (he == hipSuccess) he = hipMemcpyAsync(&flag, bad, 4, hipMemcpyDeviceToHost, e->stream);
     if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
     release();
-    if (he != hipSuccess) return fail(std::string("checkpoint load: ") + hipGetErrorString(he));
-    if (flag) return fail("checkpoint load: a repetition window does not fit the table");
+    if (he != hipSuccess || flag) {
+        std::string m = he != hipSuccess ? std::string("checkpoint load: ") + hipGetErrorString(he)
+                                         : std::string("checkpoint load: a repetition window did not fit the table");
+        if (he == hipSuccess) {  // the env is half-restored: start every board afresh
+            launch_reset(e, nullptr, 1);
+            (void)hipStreamSynchronize(e->stream);
+            e->policy_ready = true;
+            m += " (every board was reset)";
+        }
+        return fail(m);
+    }
     e->policy_ready = hd.policy_ready != 0;
     return 0;
 }

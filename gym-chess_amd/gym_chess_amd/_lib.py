@@ -51,6 +51,7 @@ SIGNATURES = {
     "gc_env_copy": (_I, [_P, _P, _P, _U64, _I]),
     "gc_env_rollout": (_I, [_P, _I, _P, _P, _P, _P, _P]),
     "gc_env_rollout_device": (_I, [_P, _I, _P, _I, _I]),
+    "gc_env_spill_info": (_I, [_P, _P, _P, _P]),
     "gc_env_get_outputs": (_I, [_P, _P, _P, _P, _P, _P]),
     "gc_env_get_states": (_I, [_P, _P, _P]),
     "gc_env_set_states": (_I, [_P, _P, _P]),

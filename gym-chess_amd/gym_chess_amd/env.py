@@ -25,7 +25,8 @@ from . import _lib
 from . import codec as C
 
 REASONS = {0: "none", 1: "mate", 2: "repetition", 3: "move_cap", 4: "no_moves", 5: "both_kings_checked",
-           6: "invalid_action", 7: "already_done", 8: "mated_by_opponent", 9: "opponent_no_move"}
+           6: "invalid_action", 7: "already_done", 8: "mated_by_opponent", 9: "opponent_no_move",
+           10: "repetition_table_exhausted"}
 
 
 class BatchedChessEnv:
@@ -230,6 +231,13 @@ class BatchedChessEnv:
     def trace_buffer(self, plies):
         """device memory for rollout_device's per-ply outputs ([plies][N] packed words)"""
         return TraceBuffer(self, plies)
+
+    def spill_info(self):
+        """the repetition spill table of a BLACK-agent env: dict(bits, used, live)"""
+        b = ctypes.c_int()
+        u, lv = ctypes.c_uint64(), ctypes.c_uint64()
+        _lib.check(self._L.gc_env_spill_info(self._h, ctypes.byref(b), ctypes.byref(u), ctypes.byref(lv)))
+        return dict(bits=b.value, used=u.value, live=lv.value)
 
     def synchronize(self):
         _lib.check(self._L.gc_env_synchronize(self._h))

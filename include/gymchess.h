@@ -164,6 +164,11 @@ int gc_env_set_states(gc_env* e, const int8_t* boards, const uint8_t* meta);
 int gc_env_legal_moves(gc_env* e, uint16_t* moves, int cap, int32_t* counts);
 /* legal action mask per board: 64 words (from -> targets) + 1 word (bit c: action 4096+c) */
 int gc_env_legal_mask(gc_env* e, uint64_t* mask, int32_t* counts);
+/* The repetition spill table of a player_color BLACK env (whose games have no move cap, so a
+ * 3-fold window can outgrow its per-board table; chess_v2.py:291-292): log2 of its slots (0 =
+ * none), slots in use and live entries.  Synchronous; an error if an insert ever found no
+ * free slot (the table grows long before that, between calls). */
+int gc_env_spill_info(gc_env* e, int* bits, uint64_t* used, uint64_t* live);
 /* wait for the env's stream (spin-polls up to GC_SPIN_US, default 20 ms, then blocks) */
 int gc_env_synchronize(gc_env* e);
 /* FEN (host-side, no GPU): placement rank 8 first (board row 0), side to move, castling ->

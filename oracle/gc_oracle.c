@@ -430,13 +430,11 @@ typedef struct {
     uint64_t seed;
     uint32_t board, draw;
     /* distinct pre-move boards of reversible moves since the last pawn move / capture: the
-     * device's window length.  A BLACK agent's move_count never advances (291-292), so its
-     * games have no move cap; a window that would pass WINDOW_CAP ends the episode (reason
-     * 10) on the device and here alike. */
+     * device's window length (unbounded: a BLACK agent's move_count never advances,
+     * 291-292, so its games have no move cap and saved_boards grows for the whole game --
+     * the device spills such windows past its per-board table, gc_env.h) */
     int win;
 } OEnv;
-/* = gc_env.h hist_cap(): 384 boards for the move-capped games, 511 for a BLACK agent's */
-#define WINDOW_CAP(e) ((e)->agent_black ? 511 : 384)
 
 uint32_t oracle_policy_index(uint64_t seed, uint32_t board, uint32_t draw, uint32_t n);
 static int kth_in_action_order(const uint16_t *moves, int n, int k);
@@ -473,8 +471,7 @@ static int env_policy_pick(OEnv *e) {
 
 /* player_move (chess_v2.py:393-412) + the state setter + switch_player + the next
  * get_possible_moves: returns 1 on the both-kings-checked error (env unchanged), else 0
- * with *mr = capture value and *rep = the 3-fold verdict on the PRE-move board, or 2 (move
- * applied) when the window passes WINDOW_CAP. */
+ * with *mr = capture value and *rep = the 3-fold verdict on the PRE-move board. */
 static int env_player_move(OEnv *e, int action, int *mr, int *rep) {
     OState s, ns;
     env_engine_state(e, &s);
@@ -485,9 +482,8 @@ static int env_player_move(OEnv *e, int action, int *mr, int *rep) {
     if (ns.wchk && ns.bchk) return 1;                                                    /* lib.rs:1442 */
     int c = env_saved_inc(e, e->st.b);
     *rep = c >= 3;                                                                       /* 404-407 */
-    int full = 0;
     if (irrev) e->win = 0;
-    else if (c == 1) { if (e->win >= WINDOW_CAP(e)) full = 1; else e->win++; }
+    else if (c == 1) e->win++;
     /* state setter (315-323): board, rights, checks; current_player is NOT taken from the dict */
     memcpy(e->st.b, ns.b, 64);
     e->st.wkc = ns.wkc; e->st.wqc = ns.wqc; e->st.bkc = ns.bkc; e->st.bqc = ns.bqc;
@@ -496,7 +492,7 @@ static int env_player_move(OEnv *e, int action, int *mr, int *rep) {
     OState s2;
     env_engine_state(e, &s2);
     e->nmoves = o_get_possible_moves(&s2, e->st.player, 0, e->moves, MAXMOVES);
-    return full ? 2 : 0;
+    return 0;
 }
 
 /* chess_v2.py:183-217.  With player_color=BLACK the opponent opens as WHITE (208-216):
@@ -525,7 +521,7 @@ void o_env_reset(OEnv *e) {
  * reward / done out.  Reason: 0 none, 1 opponent mated (+100), 2 3-fold, 3 move cap,
  * 6 invalid action, 7 already done, 8 agent mated by the opponent's reply (-100),
  * 9 the opponent has no legal reply and no check (the reference's policy returns "resign",
- * which maps to no action: the reference raises; here the env ends), 10 window full. */
+ * which maps to no action: the reference raises; here the env ends). */
 int o_env_step(OEnv *e, int action, int *reward, int *done, int *reason) {
     *reason = 0;
     int valid = 0;
@@ -537,9 +533,8 @@ int o_env_step(OEnv *e, int action, int *reward, int *done, int *reason) {
     int mr, rep;
     int pm = env_player_move(e, action, &mr, &rep);
     if (pm == 1) { *reward = 0; *done = 0; return 1; }
-    e->done = rep || pm == 2;
+    e->done = rep;
     if (rep) *reason = 2;
-    if (pm == 2) *reason = 10;
     rw += mr;
     int opp_chk = e->st.player == WHITE ? e->st.wchk : e->st.bchk;
     if (e->nmoves == 0 && opp_chk) { e->done = 1; rw += 100; *reason = 1; }              /* 270-272 */
@@ -549,9 +544,8 @@ int o_env_step(OEnv *e, int action, int *reward, int *done, int *reason) {
         int omr, orep;
         pm = env_player_move(e, env_policy_pick(e), &omr, &orep);
         if (pm == 1) { *reward = rw; *done = 1; return 1; }
-        e->done = orep || pm == 2;
+        e->done = orep;
         if (orep) *reason = 2;
-        if (pm == 2) *reason = 10;
         rw -= omr;
         int my_chk = e->st.player == WHITE ? e->st.wchk : e->st.bchk;
         if (e->nmoves == 0 && my_chk) { e->done = 1; rw -= 100; *reason = 8; }
@@ -644,7 +638,7 @@ static int kth_in_set_order(const int8_t *b, const uint16_t *moves, int n, int k
  * else action = moves[policy_index(...)], step; if done -> reset.
  * Trajectory out (optional, length plies): action, reward, done, reason per ply.
  * Counters: steps taken; episodes by reason [0 none,1 mate,2 rep,3 cap,4 stalemate,5 error]. */
-typedef struct { uint64_t steps, reward_sum, ends[6]; } OStats; /* ends[0] unused */
+typedef struct { uint64_t steps, reward_sum, ends[6]; int max_win; } OStats; /* ends[0] unused; max_win: longest window */
 
 static int stats_slot(int reason) { return reason == 8 ? 1 : (reason == 9 ? 4 : (reason == 10 ? 5 : reason)); }
 
@@ -670,6 +664,7 @@ static void rollout_board(const int8_t *init, uint64_t seed, uint32_t board, int
             st->steps++;
             st->reward_sum += (uint64_t)(int64_t)rw;
             if (rc == 1) { reason = 5; dn = 1; }
+            if (e.win > st->max_win) st->max_win = e.win;
             if (dn) { st->ends[stats_slot(reason)]++; o_env_reset(&e); }
         }
         if (tr_action) {
@@ -748,6 +743,15 @@ void oracle_rollout_trace3(const int8_t *init, uint64_t seed, uint32_t board, in
     if (stats8) { stats8[0] = st.steps; stats8[1] = st.reward_sum; for (int i = 0; i < 6; i++) stats8[2 + i] = st.ends[i]; }
 }
 
+/* the longest 3-fold window (distinct pre-move boards since the last pawn move / capture)
+ * along the same trajectory as oracle_rollout_trace3 */
+int oracle_rollout_max_window(const int8_t *init, uint64_t seed, uint32_t board, int plies, int opp, int agent_white) {
+    OStats st;
+    memset(&st, 0, sizeof(st));
+    rollout_board(init, seed, board, plies, opp, !agent_white, -1, NULL, NULL, NULL, NULL, NULL, NULL, NULL, &st);
+    return st.max_win;
+}
+
 void oracle_rollout_trace2(const int8_t *init, uint64_t seed, uint32_t board, int plies, int opp, int agent_white,
                            int16_t *tr_action, int16_t *tr_reward, uint8_t *tr_done, uint8_t *tr_reason,
                            int8_t *final_board, uint8_t *final_meta, uint64_t *stats8) {
@@ -813,3 +817,6 @@ void oracle_env_state(void *h, int8_t *board, uint8_t *meta) {
     meta[5] = e->st.wchk; meta[6] = e->st.bchk; meta[7] = (uint8_t)e->move_count;
 }
 int oracle_env_done(void *h) { return ((OEnv *)h)->done; }
+/* distinct pre-move boards since the last pawn move / capture (the device's window length,
+ * which its per-board table holds up to hist_cap and its spill table beyond) */
+int oracle_env_window(void *h) { return ((OEnv *)h)->win; }

@@ -90,6 +90,10 @@ def lib():
         L.oracle_env_state.argtypes = [P, P, P]
         L.oracle_env_done.argtypes = [P]
         L.oracle_env_done.restype = i32
+        L.oracle_rollout_max_window.argtypes = [P, u64, u32, i32, i32, i32]
+        L.oracle_rollout_max_window.restype = i32
+        L.oracle_env_window.argtypes = [P]
+        L.oracle_env_window.restype = i32
         _lib = L
     return _lib
 
@@ -200,6 +204,13 @@ def rollout_trace(seed, board_id, plies, init=DEFAULT_BOARD, opponent=0, agent_w
     return dict(action=a, reward=r, done=d, reason=why, final_board=fb, final_meta=fm, stats=st)
 
 
+def rollout_max_window(seed, board_id, plies, init=DEFAULT_BOARD, opponent=0, agent_white=True):
+    """the longest 3-fold window along rollout_trace's trajectory (the device spills a BLACK
+    agent's windows past 511 boards)"""
+    init = np.ascontiguousarray(init, dtype=np.int8).reshape(64)
+    return int(lib().oracle_rollout_max_window(_p(init), seed, board_id, plies, int(opponent), int(bool(agent_white))))
+
+
 def rollout_batch(seed, b_begin, n_boards, plies, threads=1, init=DEFAULT_BOARD, opponent=0, agent_white=True):
     init = np.ascontiguousarray(init, dtype=np.int8).reshape(64)
     st = np.zeros(8, dtype=np.uint64)
@@ -251,3 +262,8 @@ class OracleEnv:
     @property
     def done(self):
         return bool(lib().oracle_env_done(self.h))
+
+    @property
+    def window(self):
+        """distinct pre-move boards since the last pawn move / capture"""
+        return int(lib().oracle_env_window(self.h))

@@ -219,6 +219,35 @@ struct HostHist {  // same contract as the device DevHist (gc_env.h rep_prefetch
     void store_hdr(int p, u64 h) { tabv[p].hdr = h; }
     void store(int p, const RepEntry& e) { tabv[p] = e; }
     void commit() {}  // host stores are immediate
+    // the spill table (gc_env.h): one board, so the owner is 0 and its generation is g;
+    // enabled (2^14 entries) for a BLACK agent as on the device
+    std::vector<u64> spv;
+    u32 spmask = 0, used = 0, failed = 0;
+    void enable_spill(int bits) {
+        spmask = (1u << bits) - 1;
+        spv.assign((size_t)8 << bits, 0);
+    }
+    u32 spill_mask() const { return spmask; }
+    u32 owner() const { return 0; }
+    u64 sp_hdr(u32 slot) const { return spv[(size_t)slot * 8]; }
+    bool sp_cas(u32 slot, u64& expect, u64 desired) {
+        u64& h = spv[(size_t)slot * 8];
+        if (h != expect) { expect = h; return false; }
+        h = desired;
+        return true;
+    }
+    void sp_set_hdr(u32 slot, u64 v) { spv[(size_t)slot * 8] = v; }
+    void sp_put(u32 slot, const Pos& s) {
+        u64* d = &spv[(size_t)slot * 8];
+        d[1] = s.k; d[2] = s.q; d[3] = s.r; d[4] = s.b; d[5] = s.n; d[6] = s.p; d[7] = s.w;
+    }
+    bool sp_same(u32 slot, const Pos& s) const {
+        const u64* d = &spv[(size_t)slot * 8];
+        return d[1] == s.k && d[2] == s.q && d[3] == s.r && d[4] == s.b && d[5] == s.n && d[6] == s.p && d[7] == s.w;
+    }
+    u32 sp_owner_gen(u32) const { return g; }
+    void sp_claimed() { used++; }
+    void sp_fail() { failed = 1; }
 };
 
 struct HostScratch {
@@ -304,6 +333,7 @@ extern "C" void host_rollout_trace2(const int8_t* init, uint64_t seed, uint32_t 
     e.opp = opp;
     e.agent_black = !agent_white;
     e.h.nbits = e.agent_black ? HTAB_BITS_UNCAPPED : HTAB_BITS;
+    if (e.agent_black) e.h.enable_spill(14);
     e.pc = PolicyCtx{seed, board, 0};
     e.reset();
     int a = e.pick();
@@ -357,6 +387,7 @@ extern "C" void* host_env_new2(const int8_t* init, int opp, int agent_white, uin
     e->opp = opp;
     e->agent_black = !agent_white;
     e->h.nbits = e->agent_black ? HTAB_BITS_UNCAPPED : HTAB_BITS;
+    if (e->agent_black) e->h.enable_spill(14);
     e->pc = PolicyCtx{seed, board, 0};
     e->reset();
     return e;
