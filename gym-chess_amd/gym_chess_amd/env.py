@@ -406,7 +406,9 @@ class MultiDeviceChessEnv:
     def __init__(self, num_boards, device_ids=(0,), seed=0, **kw):
         from .replicas import Replicas
 
-        self.rep = Replicas(gpus=len(device_ids), devices=device_ids)
+        # one thread per device in THIS process, even inside a launched (torchrun) job: the
+        # device_ids contract does not depend on WORLD_SIZE
+        self.rep = Replicas(gpus=len(device_ids), devices=device_ids, mode="threads")
         self.num_boards = int(num_boards)
         self.envs = self.rep.run(lambda rp: BatchedChessEnv(num_boards, device=rp.device, seed=rp.board_seed(seed), **kw))
 
@@ -415,7 +417,7 @@ class MultiDeviceChessEnv:
         return self.num_boards * len(self.envs)
 
     def _each(self, fn):
-        return self.rep.run(lambda rp: fn(self.envs[rp.index]))
+        return self.rep.run(lambda rp: fn(self.envs[self.rep.local.index(rp)]))
 
     def _split(self, x):
         x = np.asarray(x)
@@ -423,16 +425,16 @@ class MultiDeviceChessEnv:
 
     def reset(self, mask=None):
         parts = self._split(mask) if mask is not None else [None] * len(self.envs)
-        self.rep.run(lambda rp: self.envs[rp.index].reset(parts[rp.index]))
+        self.rep.run(lambda rp: self.envs[self.rep.local.index(rp)].reset(parts[self.rep.local.index(rp)]))
 
     def step(self, actions):
         parts = self._split(actions)
-        out = self.rep.run(lambda rp: self.envs[rp.index].step(parts[rp.index]))
+        out = self.rep.run(lambda rp: self.envs[self.rep.local.index(rp)].step(parts[self.rep.local.index(rp)]))
         return tuple(np.concatenate([o[k] for o in out]) for k in range(3))
 
     def set_streams(self, k):
-        """step_random over k board ranges on k device streams (gc_env_set_streams)."""
-        _lib.check(self._L.gc_env_set_streams(self._h, int(k)))
+        """step_random over k board ranges on k device streams, on every device"""
+        self._each(lambda e: e.set_streams(k))
 
     def step_random(self, n_plies=1):
         self._each(lambda e: e.step_random(n_plies))

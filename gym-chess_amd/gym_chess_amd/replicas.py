@@ -111,8 +111,15 @@ class _FileGroup:
 
 
 class Replicas:
-    def __init__(self, gpus=None, world_size=None, rank=None, local_rank=None, devices=None):
-        if "WORLD_SIZE" in os.environ or world_size is not None:  # one process per GPU
+    """mode: None = "processes" under a launcher (WORLD_SIZE in the environment or world_size
+    given), else "threads"; "threads" forces one process with a thread per device whatever
+    the environment says (MultiDeviceChessEnv's device_ids contract inside a launched job)."""
+
+    def __init__(self, gpus=None, world_size=None, rank=None, local_rank=None, devices=None, mode=None):
+        if mode not in (None, "threads", "processes"):
+            raise ValueError(f"mode must be None, 'threads' or 'processes', not {mode!r}")
+        procs = mode == "processes" or (mode is None and ("WORLD_SIZE" in os.environ or world_size is not None))
+        if procs:  # one process per GPU
             self.mode = "processes"
             self.world_size = int(os.environ.get("WORLD_SIZE", "1")) if world_size is None else int(world_size)
             self.rank = int(os.environ.get("RANK", "0")) if rank is None else int(rank)
@@ -146,7 +153,13 @@ class Replicas:
                     dist.init_process_group("gloo", rank=self.rank, world_size=self.world_size)
                 self._dist = dist
             else:
-                key = os.environ.get("GC_REPLICA_KEY") or f"{os.getppid()}_{os.environ.get('MASTER_PORT', '0')}"
+                # the launcher's pid and port, and its restart count: workers restarted by
+                # torchrun (--max-restarts) keep pid and port but must not read the previous
+                # attempt's records
+                key = os.environ.get("GC_REPLICA_KEY") or "_".join(
+                    (str(os.getppid()), os.environ.get("MASTER_PORT", "0"),
+                     os.environ.get("TORCHELASTIC_RESTART_COUNT", "0"),
+                     "".join(c for c in os.environ.get("TORCHELASTIC_RUN_ID", "") if c.isalnum())[:32]))
                 self._group = _FileGroup(self.rank, self.world_size, key)
         return self
 

@@ -44,9 +44,22 @@ def test_multi_device_env_on_one_gpu():
     from gym_chess_amd.env import BatchedChessEnv, MultiDeviceChessEnv
 
     n, seed = 1024, 99
-    me = MultiDeviceChessEnv(n, device_ids=(0, 0), seed=seed)
-    assert me.total_boards == 2 * n
+    import os
+
+    # inside a launched job (WORLD_SIZE / RANK set) the device_ids contract still holds
+    saved = {k: os.environ.get(k) for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    os.environ.update(WORLD_SIZE="2", RANK="1", LOCAL_RANK="1")
+    try:
+        me = MultiDeviceChessEnv(n, device_ids=(0, 0), seed=seed)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    assert me.total_boards == 2 * n and me.rep.mode == "threads"
     st = me.rollout(200)
+    me.set_streams(2)  # forwarded to every env
     me.step_random(50)
     b, m = me.boards()
     ref = np.zeros(8, dtype=np.uint64)

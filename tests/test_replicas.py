@@ -131,3 +131,36 @@ def test_single_process_defaults(monkeypatch):
     r.barrier()
     r.close()
     assert np.uint64(Replica(7, 0).board_seed(1)) == np.uint64(1 + (7 << 40))
+
+
+def test_forced_thread_mode_under_a_launcher(monkeypatch):
+    """MultiDeviceChessEnv's replicas stay threads inside a launched job."""
+    sys.path.insert(0, os.path.join(ROOT, "gym-chess_amd"))
+    from gym_chess_amd.replicas import Replicas
+
+    monkeypatch.setenv("WORLD_SIZE", "4")
+    monkeypatch.setenv("RANK", "3")
+    r = Replicas(gpus=2, devices=(0, 0), mode="threads").init()
+    assert r.mode == "threads" and r.world_size == 2 and [x.index for x in r.local] == [0, 1]
+    assert r.run(lambda rp: r.local.index(rp)) == [0, 1]
+    r.close()
+    with pytest.raises(ValueError):
+        Replicas(mode="mpi")
+
+
+def test_file_group_key_changes_with_restart(monkeypatch, tmp_path):
+    """a torchrun worker restart (same launcher pid and port) must not read the
+    previous attempt's rank records: the restart count is part of the group key."""
+    sys.path.insert(0, os.path.join(ROOT, "gym-chess_amd"))
+    import gym_chess_amd.replicas as R
+
+    monkeypatch.setattr(R.tempfile, "gettempdir", lambda: str(tmp_path))
+    monkeypatch.delenv("GC_REPLICA_KEY", raising=False)
+    monkeypatch.setenv("MASTER_PORT", "29555")
+    dirs = []
+    for restart in ("0", "1"):
+        monkeypatch.setenv("TORCHELASTIC_RESTART_COUNT", restart)
+        r = R.Replicas(world_size=2, rank=0, local_rank=0)
+        r.init()
+        dirs.append(r._group.dir)
+    assert dirs[0] != dirs[1]
