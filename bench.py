@@ -332,25 +332,44 @@ def reference_driver(env, episodes, steps, seed):
 def single_env_leg(args, rep):
     """configs[0] / the reference's own benchmark (test_benchmark.py: 10 episodes x <= 100
     steps, published 312 us per step for the Rust v2 engine): the chess_v2.py-shaped
-    single-board env on this package's ChessEngine (one C-ABI call + GPU launch per engine
-    call).  CPU baseline: the same driver over the C oracle's ChessEngine on one core."""
+    single-board env (one device launch per step: gc_env_single_call, its result in a
+    host-mapped record).  CPU baseline: the same driver and env class over the C oracle's
+    restatement of the same ops on one core.  Beside it, one ChessEngine.get_possible_moves
+    call on the start-position dict (README.md:372-374 publishes 240 us for the v2 engine)."""
+    from gym_chess_amd import codec as C
+    from gym_chess_amd.engine import ChessEngine
     from gym_chess_amd.single import ChessEnv
 
     rp = rep.local[0]
     env = ChessEnv(opponent="none", log=False, device=rp.device)
-    reference_driver(env, 1, 10, 1)  # load the engine kernels
+    reference_driver(env, 1, 10, 1)  # load the kernel
     steps, dt = reference_driver(env, args.single_episodes, 100, 0x5EED)
     out = {"value": dt / steps * 1e6, "unit": "us/step", "higher_is_better": False, "steps": steps,
-           "episodes": args.single_episodes, "reference_published_us_per_step": 312.0}
+           "episodes": args.single_episodes, "reference_published_us_per_step": 312.0,
+           "form": "one gc_env_single_call launch per step (device bookkeeping, host-mapped record)"}
+    env.close()
+    eng = ChessEngine(rp.device)
+    state = dict(board=C.DEFAULT_BOARD, current_player="WHITE", white_king_castle_is_possible=True,
+                 white_queen_castle_is_possible=True, black_king_castle_is_possible=True,
+                 black_queen_castle_is_possible=True)
+    for _ in range(20):
+        eng.get_possible_moves(state, "WHITE")
+    calls = 500
+    t0 = time.perf_counter()
+    for _ in range(calls):
+        eng.get_possible_moves(state, "WHITE")
+    out["engine_get_possible_moves"] = {"value": (time.perf_counter() - t0) / calls * 1e6, "unit": "us/call",
+                                        "calls": calls, "reference_published_us_per_call": 240.0,
+                                        "state": "DEFAULT_BOARD dict, WHITE"}
     if rep.rank == 0 and rep.world_size == 1 and not args.no_cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         sys.path.insert(0, os.path.join(ROOT, "tests"))
-        from oracle_engine import OracleChessEngine
+        from oracle_engine import OracleBoard
 
-        cenv = ChessEnv(opponent="none", log=False, engine=OracleChessEngine())
+        cenv = ChessEnv(opponent="none", log=False, backend=OracleBoard())
         cs, cdt = reference_driver(cenv, args.single_episodes, 100, 0x5EED)
         out["cpu_baseline"] = {"value": cdt / cs * 1e6, "unit": "us/step", "cores": 1, "kind": "port",
-                               "sample": f"the same driver, {cs} steps over the C oracle's ChessEngine"}
+                               "sample": f"the same driver and env class, {cs} steps over the C oracle's env ops"}
     return out
 
 

@@ -1634,6 +1634,139 @@ __global__ void __launch_bounds__(BLOCK) k_env_rollout(EnvDev e, int plies, u64*
     }
 }
 
+// ----------------------------------------------------------------------------- single-board env ops
+// The primitive ops of one ChessEnvV2.step() for a host-side opponent policy (the
+// single-board env gym_chess_amd.single.ChessEnv: the reference's opponents are host
+// callables, "random" draws from numpy's global generator, chess_v2.py:116-127).  The env's
+// bookkeeping (chess_v2.py:219-294) runs here on the device, split where the host policy
+// must see the move list: AGENT = the agent's step up to the opponent's turn (validation,
+// done / move-cap early returns, player_move incl. the 3-fold count of the pre-move board,
+// the engine's both-kings-checked error, mate +100, and the move-count rule when no
+// opponent follows), REPLY = the opponent's player_move (-its capture value, -100 if the
+// agent is mated, the move-count rule), RESET = reset() up to the BLACK opening, OPEN = the
+// opponent's opening move (3-fold verdict discarded, move_count 1), SYNC = no change.  Every
+// op writes the resulting state, outputs and the side to move's move list in reference order
+// into one host-mapped record (gc_single_record): one launch, no copy.
+enum { SOP_RESET = 0, SOP_AGENT = 1, SOP_REPLY = 2, SOP_OPEN = 3, SOP_SYNC = 4 };
+static_assert(sizeof(gc_single_record) == 728, "gym_chess_amd.single._REC mirrors this layout");
+__global__ void __launch_bounds__(64) k_single(EnvDev e, int i, int op, int action, int flags,
+                                               gc_single_record* __restrict__ rec) {
+    __shared__ u64 lds_scr[SCRATCH_SLOTS * BLOCK];
+    LdsScratch scr{lds_scr + threadIdx.x};
+    if (threadIdx.x != 0) return;
+    Pos s = e.st.load(i);
+    const u32 g0 = e.hgen[i];
+    DevHist h = e.hist(i, g0);
+    int status = 0, reward = 0, done = 0, reason = R_NONE;
+    Gen g;
+    MoveSet ms;
+    int mr = 0;
+    bool rep = false, chk = false;
+    if (op == SOP_RESET) {  // chess_v2.py:183-206
+        s = e.ic.pos;
+        h.bump_gen();
+    } else if (op == SOP_AGENT) {
+        Gen gs;
+        gen_init(s, gs);
+        if (!action_legal(s, gs, action)) {  // 239-242: the state stays, done as it was
+            reward = -10;
+            done = (s.meta & M_DONE) ? 1 : 0;
+            reason = R_INVALID;
+        } else if (s.meta & M_DONE) {  // 245-251
+            done = 1;
+            reason = R_DONE_ALREADY;
+        } else if (mc_of(s.meta) > MOVES_MAX) {  // 252-258
+            done = 1;
+            reason = R_MOVE_CAP;
+        } else {
+            const bool white = (s.meta & M_WHITE) != 0;
+            const int rc = env_ply(s, h, action, g, ms, scr, &mr, &rep, &chk);
+            if (rc == 1) {
+                status = 1;  // lib.rs:1442-1446: the engine raises, nothing changes
+            } else {
+                reward = -10 + mr;  // 261-264 (Q9)
+                if (rep) { done = 1; reason = R_REPETITION; }
+                if (rc == 2) { done = 1; reason = R_WINDOW_FULL; }
+                if (ms.total == 0 && chk) {  // 269-272
+                    s.meta |= M_DONE;
+                    done = 1;
+                    reward += 100;
+                    reason = R_MATE;
+                }
+                if (!done && !(flags & 1) && !white) s.meta += (1u << M_MC_SHIFT);  // 291-292, no opponent
+            }
+        }
+    } else if (op == SOP_REPLY) {  // 275-292
+        const int rc = env_ply(s, h, action, g, ms, scr, &mr, &rep, &chk);
+        if (rc == 1) {
+            status = 1;
+        } else {
+            reward = -mr;
+            if (rep) { done = 1; reason = R_REPETITION; }
+            if (rc == 2) { done = 1; reason = R_WINDOW_FULL; }
+            if (ms.total == 0 && chk) {
+                s.meta |= M_DONE;
+                done = 1;
+                reward -= 100;
+                reason = R_MATED;
+            }
+            if (s.meta & M_WHITE) s.meta += (1u << M_MC_SHIFT);
+        }
+    } else if (op == SOP_OPEN) {  // 208-216
+        const int rc = env_ply(s, h, action, g, ms, scr, &mr, &rep, &chk);
+        if (rc == 1) status = 1;
+        else s.meta = (s.meta & ~(u32)M_DONE) + (1u << M_MC_SHIFT);
+    }
+    if (status == 0 && op != SOP_SYNC) {
+        h.commit();
+        e.st.store(i, s);
+        h.flush(g0);
+    }
+    rec->status = status;
+    rec->reward = reward;
+    rec->done = (uint8_t)done;
+    rec->reason = (uint8_t)reason;
+    rec->env_done = (s.meta & M_DONE) ? 1 : 0;
+    rec->white_to_move = (s.meta & M_WHITE) ? 1 : 0;
+    rec->rights[0] = (s.meta & M_WKC) != 0; rec->rights[1] = (s.meta & M_WQC) != 0;
+    rec->rights[2] = (s.meta & M_BKC) != 0; rec->rights[3] = (s.meta & M_BQC) != 0;
+    rec->checked[0] = (s.meta & M_WCHK) != 0; rec->checked[1] = (s.meta & M_BCHK) != 0;
+    rec->move_count = (uint16_t)mc_of(s.meta);
+    to_mailbox(s, rec->board);
+    list_one(s, 0, GC_SINGLE_MOVES_CAP, rec->moves, &rec->nmoves, 0);
+    __threadfence_system();  // the record lives in host memory
+}
+
+// the live 3-fold window of board i (its table entries, then its spill entries): boards and
+// occurrence counts (diagnostic readout; ChessEnv.saved_boards)
+__global__ void k_window_boards(EnvDev e, int i, int8_t* __restrict__ boards, uint8_t* __restrict__ counts, int cap,
+                                int* __restrict__ n) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const u32 g = e.hgen[i];
+    DevHist h = e.hist(i, g);
+    int k = 0;
+    for (int pos = 0; pos < (1 << h.bits()); pos++) {
+        const RepEntry x = h.load(pos);
+        if ((u32)x.hdr != g) continue;
+        if (k < cap) {
+            to_mailbox(Pos{x.k, x.q, x.r, x.b, x.n, x.p, x.w, 0}, boards + 64 * (size_t)k);
+            counts[k] = (uint8_t)(x.hdr >> 56);
+        }
+        k++;
+    }
+    const SpillTab& sp = h.sp;
+    for (u32 t = 0; sp.ent && t <= sp.mask; t++) {
+        const u64* x = sp.ent + (size_t)t * 8;
+        if (sp_owner1(x[0]) != (u32)i + 1 || sp_gen(x[0]) != g) continue;
+        if (k < cap) {
+            to_mailbox(Pos{x[1], x[2], x[3], x[4], x[5], x[6], x[7], 0}, boards + 64 * (size_t)k);
+            counts[k] = (uint8_t)sp_cnt(x[0]);
+        }
+        k++;
+    }
+    *n = k;
+}
+
 // Column sums of the per-board rollout stats [n][8] into out[8] (zeroed by the caller): a
 // wave-level butterfly per column, one atomic per column per wave.  Copying the 64 B/board
 // table to the host and summing there cost more than the rollout itself at 65 536 boards.
@@ -2510,6 +2643,8 @@ struct gc_env {
     u32* sp_ctr_h = nullptr;  // pinned: {slots claimed, failed}
     hipEvent_t sp_ev = nullptr;
     int sp_pending = 0;       // stepping calls since the last counter copy was read
+    gc_single_record* srec = nullptr;  // gc_env_single_call's host-mapped record
+    gc_single_record* srec_d = nullptr;  // its device address
 };
 
 static void env_free(gc_env* e) {
@@ -2527,6 +2662,7 @@ static void env_free(gc_env* e) {
     if (e->d.ic.spill.ctr) (void)hipFree(e->d.ic.spill.ctr);
     if (e->sp_ctr_h) (void)hipHostFree(e->sp_ctr_h);
     if (e->sp_ev) (void)hipEventDestroy(e->sp_ev);
+    if (e->srec) (void)hipHostFree(e->srec);
     if (e->stream) (void)hipStreamDestroy(e->stream);
 }
 
@@ -2700,6 +2836,30 @@ extern "C" int gc_env_spill_info(gc_env* e, int* bits, uint64_t* used, uint64_t*
     return 0;
 }
 
+// The repetition tables for move-capped games (HTAB_BITS) or for a BLACK agent's uncapped
+// ones (HTAB_BITS_UNCAPPED + the spill table); the stream is idle, the windows are cleared.
+static int set_window_kind(gc_env* e, bool uncapped) {
+    const int bits = uncapped ? HTAB_BITS_UNCAPPED : HTAB_BITS;
+    if (bits != e->d.hbits) {
+        size_t nb64 = ((size_t)e->n + 63) / 64 * 64;
+        u64* t = nullptr;
+        if (dalloc(&t, ((size_t)8 << bits) * nb64)) return -1;
+        HIPCHK(hipMemsetAsync(t, 0, ((size_t)64 << bits) * nb64, e->stream));
+        (void)hipFree(e->d.htab);
+        e->d.htab = t;
+        e->d.hbits = bits;
+        if (e->graph_exec) { (void)hipGraphExecDestroy(e->graph_exec); e->graph_exec = nullptr; }
+    }
+    if (uncapped && !e->d.ic.spill.ent) {  // a BLACK agent's windows may outgrow the table
+        if (spill_alloc(e, spill_bits_for(e->n))) return -1;
+    } else if (!uncapped && e->d.ic.spill.ent) {
+        HIPCHK(hipStreamSynchronize(e->stream));
+        spill_drop(e);
+        if (spill_publish(e)) return -1;
+    }
+    return 0;
+}
+
 // kernel dispatch on the env's opponent mode (a kernel-argument-uniform choice made once per
 // launch on the host, so the opponent="none" kernels carry no opponent code)
 static void launch_reset(gc_env* e, const uint8_t* mask, int select) {
@@ -2857,24 +3017,7 @@ extern "C" int gc_env_set_opponent(gc_env* e, int opponent, int agent_white) {
     if (opponent && e->rules) return fail("the FIDE rules mode supports opponent \"none\" only");
     HIPCHK(hipSetDevice(e->device));
     HIPCHK(hipStreamSynchronize(e->stream));
-    const int bits = agent_white ? HTAB_BITS : HTAB_BITS_UNCAPPED;  // a BLACK agent's games have no move cap
-    if (bits != e->d.hbits) {
-        size_t nb64 = ((size_t)e->n + 63) / 64 * 64;
-        u64* t = nullptr;
-        if (dalloc(&t, ((size_t)8 << bits) * nb64)) return -1;
-        HIPCHK(hipMemsetAsync(t, 0, ((size_t)64 << bits) * nb64, e->stream));
-        (void)hipFree(e->d.htab);
-        e->d.htab = t;
-        e->d.hbits = bits;
-        if (e->graph_exec) { (void)hipGraphExecDestroy(e->graph_exec); e->graph_exec = nullptr; }
-    }
-    if (!agent_white && !e->d.ic.spill.ent) {  // a BLACK agent's windows may outgrow the table
-        if (spill_alloc(e, spill_bits_for(e->n))) return -1;
-    } else if (agent_white && e->d.ic.spill.ent) {
-        HIPCHK(hipStreamSynchronize(e->stream));
-        spill_drop(e);
-        if (spill_publish(e)) return -1;
-    }
+    if (set_window_kind(e, !agent_white)) return -1;
     e->d.opp = opponent;
     e->d.agent_black = agent_white ? 0 : 1;
     HIPCHK(hipMemsetAsync(e->d.draw, 0, (size_t)4 * e->n, e->stream));  // fresh policy streams
@@ -2929,6 +3072,62 @@ extern "C" int gc_env_reset(gc_env* e, const uint8_t* mask) {
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(e->stream));
     e->policy_ready = true;
+    return 0;
+}
+
+// ---- single-board env ops (k_single)
+extern "C" int gc_env_single_setup(gc_env* e, int agent_white) {
+    if (!e) return fail("null env");
+    if (e->rules) return fail("the single-board env ops follow the reference's rules");
+    if (e->d.opp) return fail("the single-board env ops drive the opponent from the host (opponent 0)");
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    if (set_window_kind(e, !agent_white)) return -1;
+    if (!e->srec) {
+        HIPCHK(hipHostMalloc(&e->srec, sizeof(gc_single_record), hipHostMallocMapped));
+        HIPCHK(hipHostGetDevicePointer((void**)&e->srec_d, e->srec, 0));
+    }
+    return 0;
+}
+
+extern "C" int gc_env_single_call(gc_env* e, int board, int op, int action, int flags, const gc_single_record** rec) {
+    if (!e || !rec) return fail("null argument");
+    if (!e->srec) return fail("call gc_env_single_setup first");
+    if (board < 0 || board >= e->n) return fail("board index out of range");
+    if (op < SOP_RESET || op > SOP_SYNC) return fail("op: 0 reset, 1 agent, 2 reply, 3 open, 4 sync");
+    if (op != SOP_RESET && op != SOP_SYNC && (action < 0 || action > A_RESIGN))
+        return fail("action out of range [0, 4100]");
+    HIPCHK(hipSetDevice(e->device));
+    if (spill_before(e)) return -1;
+    k_single<<<1, 64, 0, e->stream>>>(e->d, board, op, action, flags, e->srec_d);
+    HIPCHK(hipGetLastError());
+    if (spill_after(e) || gc_env_synchronize(e)) return -1;
+    e->policy_ready = false;
+    *rec = e->srec;
+    return 0;
+}
+
+extern "C" int gc_env_window_boards(gc_env* e, int board, int8_t* boards, uint8_t* counts, int cap, int* n) {
+    if (!e || !n || (cap > 0 && (!boards || !counts))) return fail("null argument");
+    if (board < 0 || board >= e->n) return fail("board index out of range");
+    HIPCHK(hipSetDevice(e->device));
+    int8_t* db = nullptr;
+    uint8_t* dc = nullptr;
+    int* dn = nullptr;
+    const int c = cap > 0 ? cap : 0;
+    if (dalloc(&db, (size_t)64 * (c ? c : 1)) || dalloc(&dc, c ? c : 1) || dalloc(&dn, 1)) {
+        (void)hipFree(db); (void)hipFree(dc);
+        return -1;
+    }
+    k_window_boards<<<1, 64, 0, e->stream>>>(e->d, board, db, dc, c, dn);
+    hipError_t he = hipGetLastError();
+    if (he == hipSuccess) he = hipMemcpyAsync(n, dn, sizeof(int), hipMemcpyDeviceToHost, e->stream);
+    if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
+    const int k = *n < c ? *n : c;
+    if (he == hipSuccess && k) he = hipMemcpy(boards, db, (size_t)64 * k, hipMemcpyDeviceToHost);
+    if (he == hipSuccess && k) he = hipMemcpy(counts, dc, (size_t)k, hipMemcpyDeviceToHost);
+    (void)hipFree(db); (void)hipFree(dc); (void)hipFree(dn);
+    if (he != hipSuccess) return fail(std::string("window readout: ") + hipGetErrorString(he));
     return 0;
 }
 

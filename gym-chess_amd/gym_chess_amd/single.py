@@ -1,31 +1,35 @@
-"""Single-board ChessEnvV2 on the GPU engine.
+"""Single-board ChessEnvV2 on the device.
 
-`ChessEnv` is the reference's `ChessEnvV2` (/root/reference/gym_chess/envs/chess_v2.py:132-602)
-re-stated over this package's `ChessEngine` (one gc_engine_* launch per engine call), so
-user code written against the reference env runs unchanged:
+`ChessEnv` has the surface of the reference's `ChessEnvV2`
+(/root/reference/gym_chess/envs/chess_v2.py:132-602), so user code written against the
+reference env runs unchanged:
 
     env = ChessEnv(player_color="WHITE", opponent="random", log=False)
     state = env.reset()
     state, reward, done, info = env.step(action)
 
-Behaviour kept from the reference, including its quirks:
-  * step(): invalid action -> INVALID_ACTION_REWARD with the state unchanged, checked before
-    `done` (chess_v2.py:239-242); done / move_count > 149 -> (state, 0.0, True, info)
-    (245-258); a valid move scores -10 + the captured value (261-264); opponent mated ->
-    +100 (269-272); with an opponent, -opp_reward and -100 when the agent is mated
-    (275-288); move_count advances when WHITE is to move after the step (291-292).
-  * 3-fold repetition counts the PRE-move board only (player_move, 393-412: Q8).
-  * reset() with player_color=BLACK lets the opponent open as WHITE (208-216).
-  * the "random" opponent draws with numpy's GLOBAL generator (`np.random.choice` over the
-    move list, 116-127), so a seeded driver reproduces the reference's games move for move;
-    with no legal move it returns "resign", which maps to no action and fails in
-    action_to_move (TypeError), as in the reference.
-  * the engine raises SystemError when both kings end up in check (lib.rs:1442-1446).
-Deliberate difference: action_to_move_str returns the move string (the reference's
-version references an undefined name, chess_v2.py:532).
+The env's bookkeeping -- validation, the done / move-cap early returns, player_move with
+the 3-fold count of the PRE-move board (Q8), rewards, mate, the move count, the BLACK
+opening -- runs on the device, in the batched env's step code (gc_env.h), on one board of a
+gc_env: each step() is ONE launch (gc_env_single_call) whose result (state, outputs and the
+next move list in reference order) lands in a host-mapped record -- no copy, no second
+copy of chess_v2.py here.  Only the opponent policy runs on the host, as in the reference:
+a callable, or "random" = numpy's GLOBAL generator over the move list (116-127), so a seeded
+driver replays the reference's games move for move; a step with an opponent is split where
+the policy must see the list (AGENT, then REPLY: two launches).  With no legal move the
+random policy returns "resign", which maps to no action and fails in action_to_move
+(TypeError), and the engine's both-kings-checked error raises SystemError (lib.rs:1442-1446),
+both as in the reference.
 
-`engine=` accepts any object with the ChessEngine protocol (the tests plug in the CPU
-oracle to check this class itself on a machine without a GPU).
+Differences: action_to_move_str returns the move string (the reference's version references
+an undefined name, chess_v2.py:532); saved_boards reads the live 3-fold window from the
+device -- the boards since the last pawn move or capture, the only ones that can recur --
+where the reference keeps every board since reset; assigning env.state restarts the window.
+
+`backend=` takes any object with the single-board op protocol (`call(op, action, flags)` ->
+record); the tests plug in the CPU oracle's restatement to check this class without a GPU.
+`engine` (lazily a ChessEngine on the same device) serves the stateless helpers
+get_possible_moves / get_castle_moves / next_state with explicit states.
 """
 import sys
 from io import StringIO
@@ -90,26 +94,104 @@ def make_random_policy(np_random, bot_player):
     return random_policy
 
 
+OP_RESET, OP_AGENT, OP_REPLY, OP_OPEN, OP_SYNC = 0, 1, 2, 3, 4  # gc_env_single_call ops
+R_REPETITION, R_INVALID, R_DONE_ALREADY, R_MOVE_CAP = 2, 6, 7, 3  # reason codes (env.REASONS)
+_BOTH_CHECKED = "Both Kings are in check: this position is impossible"  # lib.rs:1442-1446
+
+
+class DeviceBoard:
+    """One board of a gc_env driven by gc_env_single_call: the env's step bookkeeping on the
+    device, its result read from the host-mapped gc_single_record."""
+
+    def __init__(self, initial_board, agent_white, device=0):
+        import ctypes
+
+        from . import _lib
+
+        self._ct = ctypes
+        self._L = _lib.load()
+        self._check = _lib.check
+        ib = C.board_to_array(initial_board)
+        h = ctypes.c_void_p()
+        self._check(self._L.gc_env_create(int(device), 1, ctypes.c_uint64(0), _lib.ptr(ib), ctypes.byref(h)))
+        self._h = h
+        self._check(self._L.gc_env_single_setup(self._h, int(bool(agent_white))))
+        self._rec = ctypes.c_void_p()
+        self._view = None
+
+    def call(self, op, action=0, flags=0):
+        self._check(self._L.gc_env_single_call(self._h, 0, int(op), int(action), int(flags), self._ct.byref(self._rec)))
+        if self._view is None:  # the record's address is fixed per env
+            buf = (self._ct.c_uint8 * _REC.itemsize).from_address(self._rec.value)
+            self._view = np.frombuffer(buf, dtype=_REC, count=1)[0]
+        return self._view
+
+    def set_state(self, board, meta):
+        """board int8[64], meta uint8[8]; restarts the window (gc_env_set_states)"""
+        b = np.ascontiguousarray(board, dtype=np.int8).reshape(64)
+        m = np.ascontiguousarray(meta, dtype=np.uint8).reshape(8)
+        self._check(self._L.gc_env_set_states(self._h, b.ctypes.data_as(self._ct.c_void_p),
+                                              m.ctypes.data_as(self._ct.c_void_p)))
+
+    def window(self):
+        """the live 3-fold window: {board bytes: count}"""
+        ct = self._ct
+        n = ct.c_int()
+        self._check(self._L.gc_env_window_boards(self._h, 0, None, None, 0, ct.byref(n)))
+        b = np.zeros((max(n.value, 1), 64), dtype=np.int8)
+        c = np.zeros(max(n.value, 1), dtype=np.uint8)
+        self._check(self._L.gc_env_window_boards(self._h, 0, b.ctypes.data_as(ct.c_void_p), c.ctypes.data_as(ct.c_void_p),
+                                                 n.value, ct.byref(n)))
+        return {b[k].tobytes(): int(c[k]) for k in range(n.value)}
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.gc_env_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+# gc_single_record (include/gymchess.h)
+_REC = np.dtype([("status", "<i4"), ("reward", "<i4"), ("done", "u1"), ("reason", "u1"), ("env_done", "u1"),
+                 ("white_to_move", "u1"), ("rights", "u1", (4,)), ("checked", "u1", (2,)), ("move_count", "<u2"),
+                 ("nmoves", "<i4"), ("board", "i1", (64,)), ("moves", "<u2", (320,))])
+assert _REC.itemsize == 728  # = sizeof(gc_single_record), static_assert in gymchess.hip
+
+_ACTION_MOVE = [C.action_to_move(a) if a < 4096 else C.ACTION_TO_CASTLE.get(a) for a in range(C.N_ACTIONS - 1)]
+
+
 class ChessEnv:
     metadata = {"render.modes": ["human", "string"]}
 
     def __init__(self, player_color=WHITE, opponent="random", log=True, initial_board=DEFAULT_BOARD, device=0,
-                 engine=None):
+                 backend=None, engine=None):
         self.moves_max = MOVES_MAX
         self.log = log
         self.initial_board = initial_board
-        if engine is None:
-            from .engine import ChessEngine
-
-            engine = ChessEngine(device)
-        self.engine = engine
+        self.device = device
+        self._engine = engine
         self.observation_space = Box(-6, 6, (8, 8))
         self.action_space = Discrete(C.N_ACTIONS)
         self.player = player_color
         self.player_2 = self.get_other_player(player_color)
         self.opponent = opponent
         self.seed()
+        self._b = backend if backend is not None else DeviceBoard(initial_board, player_color == WHITE, device)
         self.reset()
+
+    @property
+    def engine(self):
+        """the stateless engine of the explicit-state helpers (chess_v2.py:146)"""
+        if self._engine is None:
+            from .engine import ChessEngine
+
+            self._engine = ChessEngine(self.device)
+        return self._engine
 
     # ---------------------------------------------------------------- lifecycle
     def seed(self, seed=None):
@@ -125,64 +207,65 @@ class ChessEnv:
             self.opponent_policy = self.opponent
         return [seed]
 
+    def _take(self, rec):
+        """mirror the device record: state, side to move, done, move count, move list"""
+        if rec["status"]:
+            print(_BOTH_CHECKED)
+            raise SystemError(_BOTH_CHECKED)
+        self.board = rec["board"].reshape(8, 8).tolist()
+        r, c = rec["rights"], rec["checked"]
+        self.white_king_castle_is_possible, self.white_queen_castle_is_possible = bool(r[0]), bool(r[1])
+        self.black_king_castle_is_possible, self.black_queen_castle_is_possible = bool(r[2]), bool(r[3])
+        self.white_king_is_checked, self.black_king_is_checked = bool(c[0]), bool(c[1])
+        self.current_player = WHITE if rec["white_to_move"] else BLACK
+        self.done = bool(rec["env_done"])
+        self.move_count = int(rec["move_count"])
+        n = int(rec["nmoves"])
+        if n > len(rec["moves"]):
+            raise RuntimeError(f"{n} legal moves: more than the record holds")
+        self._possible_moves = [_ACTION_MOVE[a] for a in rec["moves"][:n].tolist()]
+        return rec
+
+    def _ply(self, op, action, flags=0):
+        """one player_move on the device; with log, the reference's print + render of the
+        pre-move board (chess_v2.py:409-411, skipped when the move ends by 3-fold)"""
+        if op != OP_AGENT and action is None:
+            self.action_to_move(action)  # the random policy's "resign": TypeError, as the reference
+        mover, pre = self.current_player, self.board
+        rec = self._take(self._b.call(op, action, flags))
+        if self.log and rec["reason"] not in (R_INVALID, R_DONE_ALREADY, R_MOVE_CAP, R_REPETITION):
+            board, self.board = self.board, pre
+            print(" " * 10, ">" * 10, mover)
+            self.render_moves([self.action_to_move(action)], mode="human")
+            self.board = board
+        return rec
+
     def reset(self):
-        self.board = self.initial_board
-        self.done = False
-        self.current_player = WHITE
-        self.saved_boards = {}
         self.repetitions = 0
-        self.move_count = 0
-        self.white_king_castle_is_possible = True
-        self.white_queen_castle_is_possible = True
-        self.black_king_castle_is_possible = True
-        self.black_queen_castle_is_possible = True
-        self.white_king_is_checked = False
-        self.black_king_is_checked = False
-        self.white_king_on_the_board = self.piece_is_on_board(self.board, KING_ID)
-        self.black_king_on_the_board = self.piece_is_on_board(self.board, -KING_ID)
-        self.state = self.engine.update_state(self.state)
-        self.possible_moves = self.get_possible_moves(state=self.state, player=WHITE)
+        self.white_king_on_the_board = self.piece_is_on_board(self.initial_board, KING_ID)
+        self.black_king_on_the_board = self.piece_is_on_board(self.initial_board, -KING_ID)
+        self._take(self._b.call(OP_RESET))
         if self.player == BLACK:  # the opponent opens as WHITE (chess_v2.py:208-216)
-            first = self.move_to_action(self.opponent_policy(self))
-            self.state, _, _ = self.player_move(first)
-            self.move_count += 1
-            self.current_player = BLACK
-            self.possible_moves = self.get_possible_moves(state=self.state, player=BLACK)
+            self._ply(OP_OPEN, self.move_to_action(self.opponent_policy(self)))
         return self.state
 
     def step(self, action):
         assert self.action_space.contains(action), "ACTION ERROR {}".format(action)
-        if action not in self.possible_actions:
+        opp = self.opponent_policy is not None
+        rec = self._ply(OP_AGENT, int(action), 1 if opp else 0)
+        why = int(rec["reason"])
+        if why == R_INVALID:  # 239-242
             return self.state, INVALID_ACTION_REWARD, self.done, self.info
-        if self.done:
+        if why in (R_DONE_ALREADY, R_MOVE_CAP):  # 245-258
             return self.state, 0.0, True, self.info
-        if self.move_count > self.moves_max:
-            return self.state, 0.0, True, self.info
-        reward = INVALID_ACTION_REWARD
-        self.state, move_reward, self.done = self.player_move(action)
-        reward += move_reward
-        other = self.switch_player()
-        self.possible_moves = self.get_possible_moves(player=other)
-        if not self.possible_moves and self.king_is_checked(player=other):
-            self.done = True
-            reward += WIN_REWARD
-        if self.done:
+        reward = int(rec["reward"])
+        if self.done or not opp:
             return self.state, reward, self.done, self.info
-        if self.opponent_policy:
-            opp_action = self.move_to_action(self.opponent_policy(self))
-            self.state, opp_reward, self.done = self.player_move(opp_action)
-            agent = self.switch_player()
-            self.possible_moves = self.get_possible_moves(player=agent)
-            reward -= opp_reward
-            if not self.possible_moves and self.king_is_checked(player=agent):
-                self.done = True
-                reward += LOSS_REWARD
-        if self.current_player == WHITE:
-            self.move_count += 1
-        return self.state, reward, self.done, self.info
+        rec = self._ply(OP_REPLY, self.move_to_action(self.opponent_policy(self)))  # 275-288
+        return self.state, reward + int(rec["reward"]), self.done, self.info
 
     def close(self):
-        pass
+        self._b.close()
 
     # ---------------------------------------------------------------- state
     def switch_player(self):
@@ -204,13 +287,19 @@ class ChessEnv:
 
     @state.setter
     def state(self, state):  # current_player is NOT taken from the dict (chess_v2.py:316-324)
-        self.board = state.get("board")
-        self.white_king_castle_is_possible = state.get("white_king_castle_is_possible")
-        self.white_queen_castle_is_possible = state.get("white_queen_castle_is_possible")
-        self.black_king_castle_is_possible = state.get("black_king_castle_is_possible")
-        self.black_queen_castle_is_possible = state.get("black_queen_castle_is_possible")
-        self.white_king_is_checked = state.get("white_king_is_checked")
-        self.black_king_is_checked = state.get("black_king_is_checked")
+        if not hasattr(self._b, "set_state"):
+            raise NotImplementedError("this backend cannot take a state")
+        meta = [int(self.current_player == WHITE), state.get("white_king_castle_is_possible"),
+                state.get("white_queen_castle_is_possible"), state.get("black_king_castle_is_possible"),
+                state.get("black_queen_castle_is_possible"), state.get("white_king_is_checked"),
+                state.get("black_king_is_checked"), self.move_count]
+        self._b.set_state(C.board_to_array(state.get("board")), np.array(meta, dtype=np.uint8))
+        self._take(self._b.call(OP_SYNC))
+
+    @property
+    def saved_boards(self):
+        """the live 3-fold window {board bytes: pre-move occurrences} (read from the device)"""
+        return self._b.window()
 
     @property
     def possible_moves(self):
@@ -268,22 +357,8 @@ class ChessEnv:
     def get_other_player(player):
         return BLACK if player == WHITE else WHITE
 
-    def player_move(self, action):
-        """-> (state, reward, done); the PRE-move board feeds the 3-fold count."""
-        if self.is_resignation(action):
-            return self.state, LOSS_REWARD, True
-        move = self.action_to_move(action)
-        new_state, reward = self.next_state(self.state, self.current_player, move)
-        key = self.encode_board()
-        self.saved_boards[key] = self.saved_boards.get(key, 0) + 1
-        if self.saved_boards[key] >= 3:
-            return new_state, reward, True
-        if self.log:
-            print(" " * 10, ">" * 10, self.current_player)
-            self.render_moves([move], mode="human")
-        return new_state, reward, False
-
     def next_state(self, state, player, move):
+        """the engine's next_state of an explicit state (no env change)"""
         if state is None:
             state = self.state
         return self.engine.next_state(state, player, self.move_to_str_code(move))

@@ -556,6 +556,53 @@ int o_env_step(OEnv *e, int action, int *reward, int *done, int *reason) {
     return 0;
 }
 
+/* The single-board env's primitive ops (the device's gc_env_single_call, k_single): one
+ * ChessEnvV2.step() (chess_v2.py:219-294) split where a host opponent policy must see the
+ * move list.  op 0 reset (183-206, no opening), 1 the agent's step up to the opponent's turn
+ * (flags bit 0: an opponent follows, so the move count waits for it), 2 the opponent's reply,
+ * 3 the opponent's opening (208-216), 4 nothing.  out = {status (1: both kings checked, the
+ * engine raises, nothing changes), reward, done, reason} with the batched step's reasons. */
+int oracle_single_op(void *h, int op, int action, int flags, int *out) {
+    OEnv *e = (OEnv *)h;
+    int status = 0, reward = 0, done = 0, reason = 0, mr = 0, rep = 0;
+    if (op == 0) {
+        int opp = e->opp;
+        e->opp = 0;
+        o_env_reset(e);
+        e->opp = opp;
+    } else if (op == 1) {
+        int valid = 0;
+        for (int k = 0; k < e->nmoves; k++) if (e->moves[k] == action) { valid = 1; break; }
+        if (!valid) { reward = -10; done = e->done; reason = 6; }                          /* 239-242 */
+        else if (e->done) { done = 1; reason = 7; }                                        /* 245-251 */
+        else if (e->move_count > 149) { done = 1; reason = 3; }                            /* 252-258 */
+        else if (env_player_move(e, action, &mr, &rep) == 1) status = 1;                    /* lib.rs:1442 */
+        else {
+            reward = -10 + mr;                                                              /* 261-264 */
+            e->done = rep;
+            if (rep) { done = 1; reason = 2; }
+            int chk = e->st.player == WHITE ? e->st.wchk : e->st.bchk;
+            if (e->nmoves == 0 && chk) { e->done = 1; done = 1; reward += 100; reason = 1; } /* 269-272 */
+            if (!done && !(flags & 1) && e->st.player == WHITE) e->move_count++;           /* 291-292 */
+        }
+    } else if (op == 2) {                                                                   /* 275-292 */
+        if (env_player_move(e, action, &mr, &rep) == 1) status = 1;
+        else {
+            reward = -mr;
+            e->done = rep;
+            if (rep) { done = 1; reason = 2; }
+            int chk = e->st.player == WHITE ? e->st.wchk : e->st.bchk;
+            if (e->nmoves == 0 && chk) { e->done = 1; done = 1; reward -= 100; reason = 8; }
+            if (e->st.player == WHITE) e->move_count++;
+        }
+    } else if (op == 3) {                                                                   /* 208-216 */
+        if (env_player_move(e, action, &mr, &rep) == 1) status = 1;
+        else { e->done = 0; e->move_count = 1; }
+    }
+    out[0] = status; out[1] = reward; out[2] = done; out[3] = reason;
+    return status;
+}
+
 /* ---- Philox4x32-10 (Salmon et al. 2011) for the on-device random policy --- */
 static void philox(uint32_t c[4], const uint32_t k0in, const uint32_t k1in, uint32_t out[4]) {
     uint32_t k0 = k0in, k1 = k1in;

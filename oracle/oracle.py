@@ -92,6 +92,8 @@ def lib():
         L.oracle_env_done.restype = i32
         L.oracle_rollout_max_window.argtypes = [P, u64, u32, i32, i32, i32]
         L.oracle_rollout_max_window.restype = i32
+        L.oracle_single_op.argtypes = [P, i32, i32, i32, P]
+        L.oracle_single_op.restype = i32
         L.oracle_env_window.argtypes = [P]
         L.oracle_env_window.restype = i32
         _lib = L
@@ -262,6 +264,13 @@ class OracleEnv:
     @property
     def done(self):
         return bool(lib().oracle_env_done(self.h))
+
+    def single_op(self, op, action=0, flags=0):
+        """the device's gc_env_single_call ops (the single-board env's split step) ->
+        (status, reward, done, reason)"""
+        out = np.zeros(4, dtype=np.int32)
+        lib().oracle_single_op(self.h, int(op), int(action), int(flags), _p(out))
+        return tuple(int(x) for x in out)
 
     @property
     def window(self):

@@ -29,3 +29,39 @@ class OracleChessEngine:
         b, m = C.dict_to_arrays(state)
         nb, nm = O.update_state(b, m)
         return C.arrays_to_dict(nb, nm)
+
+
+class OracleBoard:
+    """The single-board op protocol of gym_chess_amd.single.DeviceBoard over the C oracle's
+    restatement of chess_v2.py (oracle_single_op): lets the CPU suite (and bench.py's
+    configs[0] CPU baseline) run the same ChessEnv without a GPU."""
+
+    def __init__(self, initial_board=None):
+        import numpy as np
+
+        from gym_chess_amd.single import _REC
+
+        init = O.DEFAULT_BOARD if initial_board is None else C.board_to_array(initial_board)
+        self._e = O.OracleEnv(init, opponent=0, agent_white=True)
+        self._rec = np.zeros(1, dtype=_REC)[0]
+        self._np = np
+
+    def call(self, op, action=0, flags=0):
+        np = self._np
+        status, reward, done, reason = self._e.single_op(op, 0 if action is None else action, flags)
+        b, m = self._e.state()
+        mv = self._e.moves()
+        r = self._rec
+        r["status"], r["reward"], r["done"], r["reason"] = status, reward, done, reason
+        r["env_done"], r["white_to_move"] = int(self._e.done), m[0]
+        r["rights"], r["checked"], r["move_count"] = m[1:5], m[5:7], m[7]
+        r["board"] = b
+        r["nmoves"] = len(mv)
+        r["moves"][: len(mv)] = np.array(mv, dtype=np.uint16)
+        return r
+
+    def window(self):
+        raise NotImplementedError("the oracle keeps every board since reset")
+
+    def close(self):
+        pass

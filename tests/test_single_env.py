@@ -1,8 +1,9 @@
-"""Single-board ChessEnv (gym_chess_amd.single, chess_v2.py:132-602 restated) against the
-reference ChessEnvV2's own recorded traces (tests/golden/v2_env_traces.json.gz, written by
-make_golden.py from the reference env): opponent "none" and "random" (numpy's global
-generator, so the seeded driver below replays the reference's games move for move),
-invalid actions, 3-fold, kingless play.  CPU: on the oracle engine; GPU: on the HIP engine.
+"""Single-board ChessEnv (gym_chess_amd.single: the ChessEnvV2 surface, its bookkeeping in
+one device launch per step) against the reference ChessEnvV2's own recorded traces
+(tests/golden/v2_env_traces.json.gz, written by make_golden.py from the reference env):
+opponent "none" and "random" (numpy's global generator, so the seeded driver below replays
+the reference's games move for move), invalid actions, 3-fold, kingless play.  CPU: over the
+oracle's restatement of the same ops (tests/oracle_engine.OracleBoard); GPU: on the device.
 """
 import numpy as np
 import pytest
@@ -77,22 +78,22 @@ def _check(env, out, s):
 
 def test_single_env_traces_on_oracle_engine():
     from gym_chess_amd.single import ChessEnv
-    from oracle_engine import OracleChessEngine
+    from oracle_engine import OracleBoard, OracleChessEngine
 
     eng = OracleChessEngine()
     n = 0
     for t in load_golden("v2_env_traces.json.gz"):
-        n += _replay(lambda **kw: ChessEnv(engine=eng, **kw), t)
+        n += _replay(lambda **kw: ChessEnv(backend=OracleBoard(kw.get("initial_board")), engine=eng, **kw), t)
     assert n > 3000
 
 
 def test_single_env_black_player_and_errors():
     from gym_chess_amd import codec as C
     from gym_chess_amd.single import ChessEnv
-    from oracle_engine import OracleChessEngine
+    from oracle_engine import OracleBoard
 
     np.random.seed(5)
-    env = ChessEnv(player_color=C.BLACK, opponent="random", log=False, engine=OracleChessEngine())
+    env = ChessEnv(player_color=C.BLACK, opponent="random", log=False, backend=OracleBoard())
     assert env.current_player == C.BLACK and env.move_count == 1
     assert sum(1 for row in env.board for v in row if v > 0) == 16
     acts = env.possible_actions
@@ -101,10 +102,10 @@ def test_single_env_black_player_and_errors():
         env.step(4101)
     _, r, d, _ = env.step(0)  # a8a8: not legal -> -10, state unchanged
     assert r == -10 and not d and env.move_count == 1
-    env2 = ChessEnv(opponent="none", log=False, engine=OracleChessEngine())
+    env2 = ChessEnv(opponent="none", log=False, backend=OracleBoard())
     assert env2.render(mode="string").count("\n") == 11
     with pytest.raises(ValueError):
-        ChessEnv(opponent="bogus", log=False, engine=OracleChessEngine())
+        ChessEnv(opponent="bogus", log=False, backend=OracleBoard())
 
 
 @pytest.mark.gpu
@@ -117,3 +118,33 @@ def test_single_env_traces_on_gpu_engine():
     for t in load_golden("v2_env_traces.json.gz"):
         n += _replay(lambda **kw: ChessEnv(engine=eng, **kw), t)
     assert n > 3000
+
+
+@pytest.mark.gpu
+def test_single_env_device_extras():
+    """BLACK agent with a callable opponent, the live window readout (saved_boards), logging,
+    state assignment, and the stateless helpers on the device engine."""
+    import contextlib
+    import io
+
+    from gym_chess_amd import codec as C
+    from gym_chess_amd.single import ChessEnv
+
+    np.random.seed(11)
+    env = ChessEnv(player_color=C.BLACK, opponent=lambda e: e.possible_moves[0], log=False)
+    assert env.current_player == C.BLACK and env.move_count == 1
+    for _ in range(6):  # knights out and back: the pre-move boards recur
+        moves = env.possible_moves
+        env.step(env.move_to_action(moves[0]))
+    sb = env.saved_boards
+    assert sb and all(1 <= v <= 2 for v in sb.values())
+    buf = io.StringIO()
+    env.log = True
+    with contextlib.redirect_stdout(buf):
+        env.step(env.possible_actions[0])
+    assert ">>>>>>>>>>" in buf.getvalue()
+    st = env.state
+    st["board"] = C.DEFAULT_BOARD
+    env.state = st
+    assert env.board == np.asarray(C.DEFAULT_BOARD).reshape(8, 8).tolist() and env.saved_boards == {}
+    assert len(env.get_possible_moves(state=env.state, player=C.WHITE)) == 20
