@@ -364,16 +364,44 @@ __global__ void __launch_bounds__(BLOCK) k_perft_small_perm(SoA in, const int32_
 #ifndef PERFT2_WPE
 #define PERFT2_WPE 3  // 168 VGPRs: 3 waves per SIMD -- 1.12e12 nodes/s vs 1.06 at 4 (128 VGPRs, ~110 spilled) and 1.03 at 2
 #endif
+// The split leaf pass (perft_split_leaves) keeps its depth-2 subtree roots as one 64-byte
+// record each (7 bitboards + meta: one cache line) instead of 7 + 1 SoA rows: the leaf
+// kernel visits them in the order of a sort by move count, so every root is a gather --
+// one line per root here, eight with the SoA rows (PMC r02: 370 B per subtree).
+struct alignas(64) Node64 {
+    u64 k, q, r, b, n, p, w;
+    u32 meta, pad;
+};
+__device__ __forceinline__ Pos node_load(const Node64* __restrict__ v, size_t j) {
+    const ulonglong2* x = reinterpret_cast<const ulonglong2*>(v + j);
+    const ulonglong2 a = x[0], b = x[1], c = x[2], d = x[3];
+    return Pos{a.x, a.y, b.x, b.y, c.x, c.y, d.x, (u32)d.y};
+}
+__device__ __forceinline__ void node_store(Node64* __restrict__ v, size_t j, const Pos& s) {
+    ulonglong2* x = reinterpret_cast<ulonglong2*>(v + j);
+    x[0] = make_ulonglong2(s.k, s.q);
+    x[1] = make_ulonglong2(s.r, s.b);
+    x[2] = make_ulonglong2(s.n, s.p);
+    x[3] = make_ulonglong2(s.w, (u64)s.meta);
+}
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(PERFT2_WPE)))
-k_perft2_perm(SoA in, const int32_t* __restrict__ perm,
-                                                       uint64_t* __restrict__ nodes) {
+k_perft2_perm_rec(const Node64* __restrict__ in, int n, const int32_t* __restrict__ perm, uint64_t* __restrict__ nodes) {
     __shared__ u64 lds_a[SCRATCH_SLOTS * BLOCK];
     LdsScratch sa{lds_a + threadIdx.x};
     int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= in.n) return;
+    if (i >= n) return;
     int j = perm[i];
-    nodes[j] = perft2(in.load(j), sa);
+    nodes[j] = perft2(node_load(in, j), sa);
 }
+__global__ void k_count_children_rec(const Node64* __restrict__ in, int n, int32_t* __restrict__ cnt) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Pos s = node_load(in, i);
+    Gen g;
+    gen_init(s, g);
+    cnt[i] = count_moves(s, g);
+}
+
 __global__ void k_iota(int32_t* __restrict__ v, int n) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) v[i] = i;
@@ -415,6 +443,29 @@ __global__ void k_expand_range(SoA in, int a, int c, const T* __restrict__ offs,
     if (g.castles & 1) out.store(o++, child_of(s, g.white, g.white ? A_QSW : A_QSB));
     if (g.castles & 2) out.store(o++, child_of(s, g.white, g.white ? A_KSW : A_KSB));
 }
+// the same into 64-byte records (the split leaf pass)
+__global__ void k_expand_range_rec(SoA in, int a, int c, const int32_t* __restrict__ offs, Node64* __restrict__ out) {
+    int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= c) return;
+    Pos s = in.load(a + t);
+    Gen g;
+    gen_init(s, g);
+    size_t o = (size_t)offs[t];
+    u64 pcs = g.own;
+    while (pcs) {
+        int sq = ctz(pcs);
+        pcs &= pcs - 1;
+        u64 tg = legal_targets(s, g, sq, type_at(s, sq));
+        while (tg) {
+            int tt = ctz(tg);
+            tg &= tg - 1;
+            node_store(out, o++, child_of(s, g.white, sq * 64 + tt));
+        }
+    }
+    if (g.castles & 1) node_store(out, o++, child_of(s, g.white, g.white ? A_QSW : A_QSB));
+    if (g.castles & 2) node_store(out, o++, child_of(s, g.white, g.white ? A_KSW : A_KSB));
+}
+
 // parent value = sum of its children's values (children of one parent are contiguous)
 template <class T>
 __global__ void k_sum_children(const T* __restrict__ offs, const T* __restrict__ cnt,
@@ -2372,20 +2423,19 @@ static int perft_split_leaves(hipStream_t st, SoA leaf, uint64_t* leaf_out) {
     std::vector<hipEvent_t> evs;  // pairs around the leaf launches
     uint64_t subtrees = 0;
     int32_t *kc = nullptr, *offs = nullptr, *kc2 = nullptr, *ks = nullptr, *ix = nullptr, *is = nullptr;
-    u64* cb = nullptr;
-    u32* cm = nullptr;
+    Node64* cr = nullptr;
     uint64_t* cval = nullptr;
     void* tmp = nullptr;
     size_t tmp_bytes = 0;
     int rc = 0;
     std::string err;
     auto done = [&]() {
-        void* ps[] = {kc, offs, kc2, ks, ix, is, cb, cm, cval, tmp};
+        void* ps[] = {kc, offs, kc2, ks, ix, is, cr, cval, tmp};
         for (void* q : ps) (void)hipFree(q);
         for (hipEvent_t ev : evs) (void)hipEventDestroy(ev);
     };
     if (dalloc(&kc, leaf.n) || dalloc(&offs, chunk) || dalloc(&kc2, cap) || dalloc(&ks, cap) || dalloc(&ix, cap) ||
-        dalloc(&is, cap) || dalloc(&cb, (size_t)NBB * cap) || dalloc(&cm, cap) || dalloc(&cval, cap)) {
+        dalloc(&is, cap) || dalloc(&cr, cap) || dalloc(&cval, cap)) {
         done();
         return -1;
     }
@@ -2410,9 +2460,8 @@ static int perft_split_leaves(hipStream_t st, SoA leaf, uint64_t* leaf_out) {
         int64_t total = (int64_t)lo + lc;
         if (total > cap) { chunk /= 2; continue; }  // an unusually bushy chunk: halve and retry
         if (total > 0) {
-            SoA ch{cb, cm, (int)total};
-            k_expand_range<int32_t><<<grid_for(c), BLOCK, 0, st>>>(leaf, a, c, offs, ch);
-            k_count_children<int32_t><<<grid_for((int)total), BLOCK, 0, st>>>(ch, kc2);
+            k_expand_range_rec<<<grid_for(c), BLOCK, 0, st>>>(leaf, a, c, offs, cr);
+            k_count_children_rec<<<grid_for((int)total), BLOCK, 0, st>>>(cr, (int)total, kc2);
             k_iota<<<grid_for((int)total), BLOCK, 0, st>>>(ix, (int)total);
             tb = tmp_bytes;
             he = hipcub::DeviceRadixSort::SortPairs(tmp, tb, kc2, ks, ix, is, (int)total, 0, 10, st);
@@ -2421,7 +2470,7 @@ static int perft_split_leaves(hipStream_t st, SoA leaf, uint64_t* leaf_out) {
             if (hipEventCreate(&e0) == hipSuccess) evs.push_back(e0);
             if (hipEventCreate(&e1) == hipSuccess) evs.push_back(e1);
             if (e0 && e1) (void)hipEventRecord(e0, st);
-            k_perft2_perm<<<grid_for((int)total), BLOCK, 0, st>>>(ch, is, cval);
+            k_perft2_perm_rec<<<grid_for((int)total), BLOCK, 0, st>>>(cr, (int)total, is, cval);
             if (e0 && e1) (void)hipEventRecord(e1, st);
             subtrees += (uint64_t)total;
         }

@@ -130,19 +130,21 @@ def test_single_env_device_extras():
     from gym_chess_amd import codec as C
     from gym_chess_amd.single import ChessEnv
 
+    def knight_move(e):  # reversible moves only: the window keeps growing
+        return next(m for m in e.possible_moves if not isinstance(m, str) and abs(e.board[m[0][0]][m[0][1]]) == 5)
+
     np.random.seed(11)
-    env = ChessEnv(player_color=C.BLACK, opponent=lambda e: e.possible_moves[0], log=False)
+    env = ChessEnv(player_color=C.BLACK, opponent=knight_move, log=False)
     assert env.current_player == C.BLACK and env.move_count == 1
-    for _ in range(6):  # knights out and back: the pre-move boards recur
-        moves = env.possible_moves
-        env.step(env.move_to_action(moves[0]))
+    for _ in range(6):
+        env.step(env.move_to_action(knight_move(env)))
     sb = env.saved_boards
-    assert sb and all(1 <= v <= 2 for v in sb.values())
+    assert len(sb) >= 3 and sum(sb.values()) >= 6 and all(1 <= v <= 2 for v in sb.values()), sb.values()
+    env = ChessEnv(opponent="none", log=True)
     buf = io.StringIO()
-    env.log = True
     with contextlib.redirect_stdout(buf):
         env.step(env.possible_actions[0])
-    assert ">>>>>>>>>>" in buf.getvalue()
+    assert ">>>>>>>>>>" in buf.getvalue() and "WHITE" in buf.getvalue()
     st = env.state
     st["board"] = C.DEFAULT_BOARD
     env.state = st

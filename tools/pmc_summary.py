@@ -33,7 +33,7 @@ def main():
     ap.add_argument("--dispatches-per-ply", type=int, default=1,
                     help="dispatches of the kernel per ply (bench.py's board-range streams, GC_STREAMS)")
     ap.add_argument("--perft", action="store_true",
-                    help="perft leaf kernel (k_perft2_perm) passes pmc_perft_{fetch,write,mix} -> pmc_perft.json")
+                    help="perft leaf kernel (k_perft2_perm_rec) passes pmc_perft_{fetch,write,mix} -> pmc_perft.json")
     ap.add_argument("--rollout", action="store_true",
                     help="the headline kernel (last k_env_rollout2<false, 0> dispatch) passes pmc_roll_* -> pmc_rollout.json")
     ap.add_argument("--calib", action="store_true",
@@ -188,12 +188,12 @@ def bench_line(path):
 
 
 def perft_summary(a):
-    """k_perft2_perm (the split leaf pass: one lane = one depth-2 subtree, bulk-counted last
+    """k_perft2_perm_rec (the split leaf pass: one lane = one depth-2 subtree, bulk-counted last
     ply) over the bench's perft leg.  Per launch: HBM bytes (FETCH_SIZE x2 + WRITE_SIZE),
     VALU instructions per wave, lane utilisation, VALU busy fraction.  Algorithmic bytes per
-    subtree: the root's 7 bitboards + meta (60) + its permutation index (4) read, its count
-    (8) written = 72 B; the leaves never touch memory."""
-    kern = "k_perft2_perm"
+    subtree: the root's 64-byte record (7 bitboards + meta) + its permutation index (4) read,
+    its count (8) written = 76 B; the leaves never touch memory."""
+    kern = "k_perft2_perm_rec"
     rows = lambda sub: per_dispatch(os.path.join(a.src, sub, "run_counter_collection.csv"), kern)  # noqa: E731
     f, w, m = rows("pmc_perft_fetch"), rows("pmc_perft_write"), rows("pmc_perft_mix")
     tot = lambda rs, k: sum(r[k] for r in rs)  # noqa: E731
@@ -201,7 +201,7 @@ def perft_summary(a):
     out = {"kernel": kern, "launches": len(m),
            "hbm_bytes_total": tot(f, "FETCH_SIZE") * 1024 * 2 + tot(w, "WRITE_SIZE") * 1024,
            "subtrees_total": waves * 64,
-           "alg_bytes_per_subtree": 72,
+           "alg_bytes_per_subtree": 76,
            "valu": {"insts_per_wave": tot(m, "SQ_INSTS_VALU") / waves,
                     "lane_utilisation": tot(m, "SQ_THREAD_CYCLES_VALU") / (tot(m, "SQ_ACTIVE_INST_VALU") * 64),
                     "wait_any_share": tot(m, "SQ_WAIT_ANY") / tot(m, "SQ_WAVE_CYCLES")},
