@@ -370,28 +370,34 @@ __global__ void __launch_bounds__(BLOCK) k_perft_small_perm(SoA in, const int32_
 // one line per root here, eight with the SoA rows (PMC r02: 370 B per subtree).
 struct alignas(64) Node64 {
     u64 k, q, r, b, n, p, w;
-    u32 meta, pad;
+    u32 meta, parent;  // parent: the root's parent in the chunk (its count is added there)
 };
 __device__ __forceinline__ Pos node_load(const Node64* __restrict__ v, size_t j) {
     const ulonglong2* x = reinterpret_cast<const ulonglong2*>(v + j);
     const ulonglong2 a = x[0], b = x[1], c = x[2], d = x[3];
     return Pos{a.x, a.y, b.x, b.y, c.x, c.y, d.x, (u32)d.y};
 }
-__device__ __forceinline__ void node_store(Node64* __restrict__ v, size_t j, const Pos& s) {
+__device__ __forceinline__ void node_store(Node64* __restrict__ v, size_t j, const Pos& s, u32 parent) {
     ulonglong2* x = reinterpret_cast<ulonglong2*>(v + j);
     x[0] = make_ulonglong2(s.k, s.q);
     x[1] = make_ulonglong2(s.r, s.b);
     x[2] = make_ulonglong2(s.n, s.p);
-    x[3] = make_ulonglong2(s.w, (u64)s.meta);
+    x[3] = make_ulonglong2(s.w, (u64)s.meta | ((u64)parent << 32));
 }
+// one lane = one depth-2 subtree, visited in move-count order (perm); its count goes straight
+// into its parent's total (a 64-bit atomic into the chunk's parent sums, zeroed by the
+// caller: <= 2^21 parents, 16 MiB, cache-resident) -- no per-subtree value array, no
+// scattered value write, no summing pass
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(PERFT2_WPE)))
-k_perft2_perm_rec(const Node64* __restrict__ in, int n, const int32_t* __restrict__ perm, uint64_t* __restrict__ nodes) {
+k_perft2_perm_rec(const Node64* __restrict__ in, int n, const int32_t* __restrict__ perm,
+                  unsigned long long* __restrict__ parent_sum) {
     __shared__ u64 lds_a[SCRATCH_SLOTS * BLOCK];
     LdsScratch sa{lds_a + threadIdx.x};
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    int j = perm[i];
-    nodes[j] = perft2(node_load(in, j), sa);
+    const int j = perm[i];
+    const u32 parent = reinterpret_cast<const u32*>(in + j)[15];
+    atomicAdd(parent_sum + parent, (unsigned long long)perft2(node_load(in, j), sa));
 }
 __global__ void k_count_children_rec(const Node64* __restrict__ in, int n, int32_t* __restrict__ cnt) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -459,11 +465,11 @@ __global__ void k_expand_range_rec(SoA in, int a, int c, const int32_t* __restri
         while (tg) {
             int tt = ctz(tg);
             tg &= tg - 1;
-            node_store(out, o++, child_of(s, g.white, sq * 64 + tt));
+            node_store(out, o++, child_of(s, g.white, sq * 64 + tt), (u32)t);
         }
     }
-    if (g.castles & 1) node_store(out, o++, child_of(s, g.white, g.white ? A_QSW : A_QSB));
-    if (g.castles & 2) node_store(out, o++, child_of(s, g.white, g.white ? A_KSW : A_KSB));
+    if (g.castles & 1) node_store(out, o++, child_of(s, g.white, g.white ? A_QSW : A_QSB), (u32)t);
+    if (g.castles & 2) node_store(out, o++, child_of(s, g.white, g.white ? A_KSW : A_KSB), (u32)t);
 }
 
 // parent value = sum of its children's values (children of one parent are contiguous)
@@ -1700,11 +1706,24 @@ __global__ void __launch_bounds__(BLOCK) k_env_rollout(EnvDev e, int plies, u64*
 // into one host-mapped record (gc_single_record): one launch, no copy.
 enum { SOP_RESET = 0, SOP_AGENT = 1, SOP_REPLY = 2, SOP_OPEN = 3, SOP_SYNC = 4 };
 static_assert(sizeof(gc_single_record) == 728, "gym_chess_amd.single._REC mirrors this layout");
+__device__ __noinline__ void single_op(const EnvDev& e, int i, int op, int action, int flags, LdsScratch& scr,
+                                       gc_single_record* __restrict__ rec);
 __global__ void __launch_bounds__(64) k_single(EnvDev e, int i, int op, int action, int flags,
-                                               gc_single_record* __restrict__ rec) {
+                                               gc_single_record* __restrict__ hrec) {
     __shared__ u64 lds_scr[SCRATCH_SLOTS * BLOCK];
+    __shared__ gc_single_record lrec;  // built here, then written to host memory by every lane
     LdsScratch scr{lds_scr + threadIdx.x};
-    if (threadIdx.x != 0) return;
+    if (threadIdx.x == 0) single_op(e, i, op, action, flags, scr, &lrec);
+    __syncthreads();
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(&lrec);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(hrec);
+    const int words = (int)(offsetof(gc_single_record, moves) / 4) + (lrec.nmoves < GC_SINGLE_MOVES_CAP ? lrec.nmoves : GC_SINGLE_MOVES_CAP + 1) / 2 + 1;
+    for (int k = threadIdx.x; k < words && k < (int)(sizeof(gc_single_record) / 4); k += 64) dst[k] = src[k];
+    __threadfence_system();  // the record lives in host memory
+}
+
+__device__ __noinline__ void single_op(const EnvDev& e, int i, int op, int action, int flags, LdsScratch& scr,
+                                       gc_single_record* __restrict__ rec) {
     Pos s = e.st.load(i);
     const u32 g0 = e.hgen[i];
     DevHist h = e.hist(i, g0);
@@ -1785,7 +1804,6 @@ __global__ void __launch_bounds__(64) k_single(EnvDev e, int i, int op, int acti
     rec->move_count = (uint16_t)mc_of(s.meta);
     to_mailbox(s, rec->board);
     list_one(s, 0, GC_SINGLE_MOVES_CAP, rec->moves, &rec->nmoves, 0);
-    __threadfence_system();  // the record lives in host memory
 }
 
 // the live 3-fold window of board i (its table entries, then its spill entries): boards and
@@ -2424,18 +2442,17 @@ static int perft_split_leaves(hipStream_t st, SoA leaf, uint64_t* leaf_out) {
     uint64_t subtrees = 0;
     int32_t *kc = nullptr, *offs = nullptr, *kc2 = nullptr, *ks = nullptr, *ix = nullptr, *is = nullptr;
     Node64* cr = nullptr;
-    uint64_t* cval = nullptr;
     void* tmp = nullptr;
     size_t tmp_bytes = 0;
     int rc = 0;
     std::string err;
     auto done = [&]() {
-        void* ps[] = {kc, offs, kc2, ks, ix, is, cr, cval, tmp};
+        void* ps[] = {kc, offs, kc2, ks, ix, is, cr, tmp};
         for (void* q : ps) (void)hipFree(q);
         for (hipEvent_t ev : evs) (void)hipEventDestroy(ev);
     };
     if (dalloc(&kc, leaf.n) || dalloc(&offs, chunk) || dalloc(&kc2, cap) || dalloc(&ks, cap) || dalloc(&ix, cap) ||
-        dalloc(&is, cap) || dalloc(&cr, cap) || dalloc(&cval, cap)) {
+        dalloc(&is, cap) || dalloc(&cr, cap)) {
         done();
         return -1;
     }
@@ -2459,6 +2476,8 @@ static int perft_split_leaves(hipStream_t st, SoA leaf, uint64_t* leaf_out) {
         if (he != hipSuccess) { err = std::string("perft split: ") + hipGetErrorString(he); rc = -1; break; }
         int64_t total = (int64_t)lo + lc;
         if (total > cap) { chunk /= 2; continue; }  // an unusually bushy chunk: halve and retry
+        he = hipMemsetAsync(leaf_out + a, 0, (size_t)8 * c, st);  // the parents' sums
+        if (he != hipSuccess) { err = std::string("perft split: ") + hipGetErrorString(he); rc = -1; break; }
         if (total > 0) {
             k_expand_range_rec<<<grid_for(c), BLOCK, 0, st>>>(leaf, a, c, offs, cr);
             k_count_children_rec<<<grid_for((int)total), BLOCK, 0, st>>>(cr, (int)total, kc2);
@@ -2470,11 +2489,11 @@ static int perft_split_leaves(hipStream_t st, SoA leaf, uint64_t* leaf_out) {
             if (hipEventCreate(&e0) == hipSuccess) evs.push_back(e0);
             if (hipEventCreate(&e1) == hipSuccess) evs.push_back(e1);
             if (e0 && e1) (void)hipEventRecord(e0, st);
-            k_perft2_perm_rec<<<grid_for((int)total), BLOCK, 0, st>>>(cr, (int)total, is, cval);
+            k_perft2_perm_rec<<<grid_for((int)total), BLOCK, 0, st>>>(
+                cr, (int)total, is, reinterpret_cast<unsigned long long*>(leaf_out + a));
             if (e0 && e1) (void)hipEventRecord(e1, st);
             subtrees += (uint64_t)total;
         }
-        k_sum_children<int32_t><<<grid_for(c), BLOCK, 0, st>>>(offs, kc + a, cval, c, leaf_out + a);
         he = hipGetLastError();
         if (he != hipSuccess) { err = std::string("perft split kernels: ") + hipGetErrorString(he); rc = -1; break; }
         a += c;
