@@ -1485,15 +1485,27 @@ __device__ __forceinline__ PairIO store_io(uint8_t* slab, int nn) {
 // every launch -- measured ~2-3k cycles, paid wherever the compiler sinks it, and with SGPRs
 // scarce it sank it next to a spill that forced the wait in phase 1.  The reset position and
 // move set come from a device-memory copy (icd) instead.
+// Which pair and role wave w of a workgroup takes (GC_PAIR_MAP; diagnostic builds compare):
+// 0: pair w / 2, role w % 2 (a pair's two waves adjacent); 1: pair w % PAIRS_WG, role
+// w / PAIRS_WG (with 4 pairs, waves w and w + 4 -- one SIMD under round-robin placement --
+// form a pair); 2: pair w / 2, role alternating across pairs (a SIMD hosts both roles).
+#ifndef GC_PAIR_MAP
+#define GC_PAIR_MAP 2  // r03 A/B (fused, 65 536 boards): 0 -> 11.2e9, 2 -> 11.37e9, 1 with 4 pairs -> 10.9e9
+#endif
+__device__ __forceinline__ int pair_of_wave(int w) { return GC_PAIR_MAP == 1 ? w % PAIRS_WG : w >> 1; }
+__device__ __forceinline__ int role_of_wave(int w) {
+    return GC_PAIR_MAP == 1 ? w / PAIRS_WG : GC_PAIR_MAP == 2 ? ((w ^ (w >> 1)) & 1) : (w & 1);
+}
 #define PAIR_PROLOGUE PAIR_PROLOGUE_ACT(in_io.act, )
 // ACTS: the action source (the env's next action, or the caller's for the API step);
 // ENTRY: more entry loads, waited for with the reset position's
 #define PAIR_PROLOGUE_ACT(ACTS, ENTRY)                                                                      \
     using LdsT = typename std::conditional<OPP != 0 || API, PairLdsVs, PairLds>::type;                      \
     __shared__ LdsT Ls[PAIRS_WG];                                                                           \
-    const int pw = PAIRS_WG > 1 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 7)) : 0;              \
+    const int wv_ = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); /* wave-uniform */            \
+    const int pw = PAIRS_WG > 1 ? pair_of_wave(wv_) : 0;                                                    \
     LdsT& L = Ls[pw];                                                                                       \
-    const int role = __builtin_amdgcn_readfirstlane((int)((threadIdx.x >> 6) & 1)); /* wave-uniform */     \
+    const int role = role_of_wave(wv_);                                                                     \
     const int l = threadIdx.x & (PAIR_BOARDS - 1);                                                          \
     const int blk = blockIdx.x * PAIRS_WG + pw + blk0; /* board block (a launch may cover a sub-range) */   \
     const int i = blk * PAIR_BOARDS + l;                                                                    \
