@@ -2160,6 +2160,250 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
     }
 }
 
+// ----------------------------------------------------------------------------- API step, paired, random opponent
+// k_env_step_api<true> (the random opponent answers inside the step: env_step_vs,
+// chess_v2.py:219-294 with opponent_policy set) on the paired driver.  Half A: the agent's
+// validated action with set-wise generation (W0 picks the opponent's reply in move-set
+// order, draw d); half B: the reply -- or, for a board whose state stays or whose episode
+// ended with the agent's move, its own moves again -- with the per-piece generation the
+// mask needs; for a BLACK agent, half C (run only when some board of the workgroup resets):
+// the opponent's opening from the reset position (move-set order table, the next draw).  A
+// WHITE agent's reset board takes the start position's cached moves.  The agent's pick (the
+// next draw, action order) and the outputs as in k_env_step_api2.  Same draws in the same
+// order as the one-wave kernel.
+template <bool BLACK>
+__global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
+    k_env_step_api2_vs(uint8_t* __restrict__ slab, uint64_t seed, u64* __restrict__ htab,
+                       const uint16_t* __restrict__ racts, const EnvDev::InitCache* __restrict__ icd,
+                       const uint16_t* __restrict__ acts, const ApiOut* __restrict__ outp, int nn,
+                       u32 rinfo /* autoreset << 17 | ic.table << 16 | ic.total */) {
+    constexpr int OPP = BLACK ? 2 : 1;
+    constexpr bool API = true;
+    constexpr int blk0 = 0;
+    const int autoreset = (rinfo >> 17) & 1;
+    rinfo &= 0x1FFFFu;
+    ApiOut out;
+    PAIR_PROLOGUE_ACT(acts, out = *outp; asm volatile("" : "+s"(out.rw), "+s"(out.dn), "+s"(out.rs), "+s"(out.mask),
+                                                                  "+s"(out.obs), "+s"(out.cnt), "+s"(out.pick));)
+    PairScratch scr{&L.slots[0][l]};
+    const uint16_t* const sw_tab = C.racts + RESET_ACTS_MAX;  // the start position's picks in move-set order
+    const bool done0 = (s.meta & M_DONE) != 0;              // chess_v2.py:245-251
+    const bool cap = mc_of(s.meta) > MOVES_MAX;             // 252-258
+    const bool white = (s.meta & M_WHITE) != 0;             // the agent's colour
+    const bool pre = live && !done0 && !cap;
+    bool valid = false;
+    if (role == 0) {  // chess_v2.py:240-242, on the pre-move board
+        valid = quick_legal(s, a);
+        L.act[l] = valid ? 1u : 0u;
+        L.draw[l] = (pre && valid) ? 1u : 0u;  // W1 reads it in phase 1 (MV_LDS)
+    }
+    u32 x0 = 0, x1 = 0, x2 = 0;
+    PairHalf H;
+    // ---- half A: the agent's move; the opponent's position generated set-wise
+    pair_half<false, false, true, true>(
+        L, role, l, role == 0 ? (pre && valid) : pre, false, s, a, nullptr, L.draw, h, H,
+        [&] {
+            x0 = philox_x0(C.seed, (u32)i, d);
+            x1 = philox_x0(C.seed, (u32)i, d + 1);
+            x2 = philox_x0(C.seed, (u32)i, d + 2);
+            L.x0[l] = x0;
+            L.x1[l] = x1;
+            L.x2[l] = x2;
+        },
+        PairNoop{});
+    if (role) valid = L.act[l] != 0;
+    else {
+        x0 = L.x0[l];
+        x1 = L.x1[l];
+        x2 = L.x2[l];
+    }
+    StepOut o = {0, 0, R_NONE, 0};
+    bool cont = false;  // the opponent replies
+    if (!valid) {
+        o.reward = -10;
+        o.done = done0 ? 1 : 0;
+        o.reason = R_INVALID;
+    } else if (done0) {
+        o.done = 1;
+        o.reason = R_DONE_ALREADY;
+    } else if (cap) {
+        o.done = 1;
+        o.reason = R_MOVE_CAP;
+    } else if (H.both) {
+        o.done = 1;
+        o.reason = R_BOTH_CHECKED;
+    } else {
+        s = pair_settle(H, white);
+        o.reward = -10 + H.mr;  // Q9
+        o.moved = 1;
+        if (H.c >= 3) { o.done = 1; o.reason = R_REPETITION; }
+        if (H.c == 0) { o.done = 1; o.reason = R_WINDOW_FULL; }
+        if (H.ms.total == 0 && H.opp_chk) {  // 270-272
+            s.meta |= M_DONE;
+            o.done = 1;
+            o.reward += 100;
+            o.reason = R_MATE;
+        }
+        if (!o.done && H.ms.total == 0) {  // 120-122: the opponent's policy "resigns"
+            s.meta |= M_DONE;
+            o.done = 1;
+            o.reason = R_OPP_NO_MOVE;
+        }
+        cont = !o.done;
+    }
+    int nd = cont ? 1 : 0;  // draws taken so far
+    int oa = A_NONE;
+    if (role == 0) {
+        if (cont) oa = sw_pick_lds(L, l, H.g, H.cw, H.ms.total, (int)scale_rank(x0, (u32)H.ms.total));
+        L.oa[l] = (u32)oa;
+    } else if (live) {
+        h.commit();  // the agent ply's window write lands before the reply probes the table
+    }
+    // ---- half B: the reply, or the board's own moves again (per-piece, for the mask)
+    const Pos s1 = s;
+    pair_half<false, true>(L, role, l, cont, live && !cont, s1, oa, L.oa, nullptr, h, H, PairNoop{}, PairNoop{});
+    bool alone = false;  // the state stays but no moves were generated for it
+    if (cont) {
+        if (H.both) {  // the reply left both kings checked: the engine raises, the env ends
+            o.reason = R_BOTH_CHECKED;
+            o.done = 1;
+            alone = true;
+        } else {
+            s = pair_settle(H, !white);
+            o.reward -= H.mr;  // 283
+            if (H.c >= 3) { o.done = 1; o.reason = R_REPETITION; }
+            if (H.c == 0) { o.done = 1; o.reason = R_WINDOW_FULL; }
+            if (H.ms.total == 0 && H.opp_chk) {  // 285-288
+                s.meta |= M_DONE;
+                o.done = 1;
+                o.reward -= 100;
+                o.reason = R_MATED;
+            }
+            if (s.meta & M_WHITE) s.meta += (1u << M_MC_SHIFT);  // 291-292
+        }
+    }
+    nst += 1;
+    const bool reset = live && autoreset && o.done;
+    if (reset) {  // chess_v2.py:183-206
+        s = rp;
+        h.bump_gen();
+        alone = false;
+    }
+    if constexpr (BLACK) {
+        // ---- half C: the opponent's opening after a reset (208-216), when some board of the
+        // workgroup needs it; the other boards keep half B's generation
+        const unsigned long long vote = __ballot(reset);
+        if (l == 0) L.vote[role] = vote != 0 ? 1u : 0u;
+        if (role && live) h.commit();
+        pair_barrier();
+        bool any = false;
+#pragma unroll
+        for (int q = 0; q < PAIRS_WG; q++) any = any || Ls[q].vote[0] != 0 || Ls[q].vote[1] != 0;
+        if (any) {
+            const Gen gB = H.g;
+            const MoveSet msB = H.ms;
+            const u32 xo = nd ? x1 : x0;
+            const int op = (int)sw_tab[scale_rank(xo, C.rtotal)];
+            if (role == 0) L.oa[l] = (u32)op;
+            const Pos s0 = s;
+            pair_half<false, true>(L, role, l, reset, false, s0, op, L.oa, nullptr, h, H, PairNoop{}, PairNoop{});
+            if (reset) {
+                s = pair_settle(H, true);
+                s.meta = (s.meta & ~(u32)M_DONE) + (1u << M_MC_SHIFT);
+                nd += 1;
+            } else {
+                H.g = gB;
+                H.ms = msB;
+            }
+        }
+    }
+    // W0: every own piece's targets into its slot (fast pawns from their origin sets; a WHITE
+    // agent's reset board from the start position's cache); castles and the enemy map to W1
+    const bool cached = reset && !BLACK;
+    if (role == 0) {
+        if (cached) {
+#pragma unroll
+            for (int j = 0; j < SCRATCH_SLOTS; j++) scr.put(j, C.icd->slots[j]);
+        } else if (!H.ms.big) {
+            for (u64 fp = H.ms.fastp; fp; fp &= fp - 1) {
+                const int sq = ctz(fp);
+                scr.put(ordinal(H.g.own, sq), fast_pawn_targets(H.ms, sq, H.g.white));
+            }
+        }
+        L.nmeta[l] = H.g.castles;
+        L.enemy[l] = H.g.enemy_att;
+    }
+    pair_barrier();
+    Gen g = H.g;
+    MoveSet ms = H.ms;
+    if (role) {
+        g.castles = L.nmeta[l];
+        g.enemy_att = L.enemy[l];
+    }
+    if (cached) ic_moves(*C.icd, g, ms);
+    if (alone && live) {  // the big-board path: legal targets per piece, no slots
+        gen_init(s, g);
+        moveset_clear(ms);
+        ms.big = true;
+        ms.total = count_legal(s, g);
+    }
+    if (out.mask && live) {
+        u64* om = out.mask + i;
+        const size_t N = (size_t)nn;
+        if (!ms.big) {  // W1 squares 0..31, W0 32..63 and the castles word
+            const int q0 = role ? 0 : 32;
+            int j = popc(g.own & below(q0));
+#pragma unroll 8
+            for (int sq = q0; sq < q0 + 32; sq++) {
+                const bool b = (g.own >> sq) & 1;
+                const u64 v = scr.get(j & (SCRATCH_SLOTS - 1));
+                om[sq * N] = b ? v : 0ull;
+                j += b ? 1 : 0;
+            }
+            if (role == 0) {
+                u64 c = 0;
+                if (g.castles & 1) c |= g.white ? (1ull << 1) : (1ull << 3);
+                if (g.castles & 2) c |= g.white ? (1ull << 0) : (1ull << 2);
+                om[64 * N] = c;
+            }
+        } else if (role) {
+            write_mask(s, g, ms, scr, om, N);
+        }
+    }
+    const PairIO io = store_io(slab, nn);
+    if (role == 0) {
+        if (live) {
+            const u32 xp = nd == 0 ? x0 : nd == 1 ? x1 : x2;
+            uint16_t p = (uint16_t)A_NONE;
+            u32 dn = d + (u32)nd;
+            if (out.pick) {
+                if (cached && C.rtable) {
+                    p = C.racts[scale_rank(xp, C.rtotal)];
+                } else if (ms.total > 0) {
+                    p = (uint16_t)select_action_swar(s, g, ms, scr, (int)scale_rank(xp, (u32)ms.total));
+                }
+                dn += ms.total > 0 ? 1u : 0u;
+                out.pick[i] = p;
+                io.act[i] = p;
+            }
+            io.draw[i] = dn;
+        }
+    } else if (live) {
+        if (out.obs) write_obs(s, out.obs + 64 * (size_t)i);
+        if (out.cnt) out.cnt[i] = ms.total;
+        out.rw[i] = o.reward;
+        out.dn[i] = (uint8_t)o.done;
+        out.rs[i] = (uint8_t)o.reason;
+        h.commit();
+        io.store(i, s);
+        h.flush(g0);
+        io.nsteps[i] = nst;
+        io.reward[i] = o.reward;
+        io.done[i] = (uint8_t)o.done;
+        io.reason[i] = (uint8_t)o.reason;
+    }
+}
+
 __global__ void __launch_bounds__(BLOCK) k_select(EnvDev e) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= e.n) return;
@@ -2782,6 +3026,8 @@ __global__ void k_spill_rehash(const u64* __restrict__ old, u32 old_mask, SpillT
 static int spill_bits_for(int n) {
     int b = 14;
     while (b < 22 && (1 << (b - 4)) < n) b++;  // 2^20 entries (64 MiB) at 65 536 boards
+    const char* v = getenv("GC_SPILL_BITS");   // tests: start small to drive the rehash / growth path
+    if (v && atoi(v) >= 6 && atoi(v) <= 30) b = atoi(v);
     return b;
 }
 
@@ -3258,6 +3504,27 @@ extern "C" int gc_env_step_device(gc_env* e, const uint16_t* d_actions, int32_t*
         }
         k_env_step_api2<<<(nb + PAIRS_WG - 1) / PAIRS_WG, 2 * PAIR_BOARDS * PAIRS_WG, 0, e->stream>>>(
             e->slab, d.seed, d.htab, r.racts, r.icd, d_actions, e->api_out, d.n, r.rinfo | ((u32)ar << 17));
+    } else if (e->d.opp && pair_ok(e) && !one_wave) {  // the random opponent on the paired driver
+        const EnvDev& d = e->d;
+        const ResetInfo r = reset_info(e);
+        const int nb = (e->n + PAIR_BOARDS - 1) / PAIR_BOARDS;
+        const ApiOut o = {d_reward, d_done, d_reason, d_mask, d_obs, d_count, d_pick};
+        if (!e->api_out) {
+            if (dalloc(&e->api_out, 1)) return -1;
+            e->api_host = {};
+        }
+        if (memcmp(&o, &e->api_host, sizeof o) != 0) {
+            e->api_host = o;
+            HIPCHK(hipMemcpyAsync(e->api_out, &e->api_host, sizeof o, hipMemcpyHostToDevice, e->stream));
+            HIPCHK(hipStreamSynchronize(e->stream));
+        }
+        const dim3 grid((nb + PAIRS_WG - 1) / PAIRS_WG), block(2 * PAIR_BOARDS * PAIRS_WG);
+        if (d.agent_black)
+            k_env_step_api2_vs<true><<<grid, block, 0, e->stream>>>(e->slab, d.seed, d.htab, r.racts, r.icd, d_actions,
+                                                                     e->api_out, d.n, r.rinfo | ((u32)ar << 17));
+        else
+            k_env_step_api2_vs<false><<<grid, block, 0, e->stream>>>(e->slab, d.seed, d.htab, r.racts, r.icd, d_actions,
+                                                                      e->api_out, d.n, r.rinfo | ((u32)ar << 17));
     } else if (e->d.opp)
         k_env_step_api<true><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d, d_actions, d_reward, d_done, d_reason,
                                                                       d_mask, d_obs, d_count, d_pick, ar);

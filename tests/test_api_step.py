@@ -134,3 +134,69 @@ def test_step_device_weird_boards_equal_host_step(oracle, autoreset):
         assert (_mask_bits(o["mask"]) == b.legal_mask()).all(), ply
         assert (o["count"] == np.array([len(x) for x in b.possible_actions()])).all(), ply
     assert {0, 6}.issubset(reasons), reasons
+
+
+@pytest.mark.parametrize("color", ["WHITE", "BLACK"])
+@pytest.mark.parametrize("autoreset", [False, True])
+def test_step_device_random_opponent_vs_oracle(oracle, color, autoreset):
+    """The random opponent's device-buffer step on the paired driver (k_env_step_api2_vs: the
+    agent's half-ply, the reply, a BLACK agent's opening after a reset) in lockstep with the
+    oracle env (chess_v2.py:219-294 with the opponent policy): rewards / done / reasons,
+    states, observation, mask, count; and every pick == the k-th legal action in action-id
+    order for the oracle's draw counter.  Actions: mostly the previous pick, some other legal
+    ones, some invalid; 200 boards (a partial last workgroup)."""
+    from gym_chess_amd.env import BatchedChessEnv
+
+    n, plies, seed = 200, 150, 0x0A11
+    env = BatchedChessEnv(n, device=0, seed=seed, opponent="random", player_color=color)
+    assert env.paired()
+    io = env.device_io()  # pick = the env's creation-time picks (one draw each)
+    ors = [oracle.OracleEnv(opponent=1, agent_white=color == "WHITE", seed=seed, board=i) for i in range(n)]
+    for o in ors:
+        o.pick()
+    act_buf = env.device_io(mask=False, obs=False, count=False, pick=True, select=False)
+    rng = np.random.RandomState(12)
+    prev = io.fetch("pick")["pick"].astype(np.int64)
+    for ply in range(plies):
+        acts = prev.copy()
+        for i, o in enumerate(ors):
+            r = rng.rand()
+            if r < 0.1:
+                acts[i] = rng.randint(4101)
+            elif r < 0.3 and o.moves():
+                mv = o.moves()
+                acts[i] = mv[rng.randint(len(mv))]
+            elif acts[i] == 0xFFFF:
+                acts[i] = 0
+        act_buf.upload_actions(acts.astype(np.uint16))
+        env.step_device(io, actions=act_buf.ptr["pick"], autoreset=autoreset)
+        out = io.fetch()
+        b, m = env.boards()
+        ends = np.zeros(n, dtype=np.uint8)
+        for i, o in enumerate(ors):
+            rc, rw, dn, why = o.step(int(acts[i]))
+            if rc == 1:  # both kings checked (kings are capturable, Q7): the engine raises, the env ends
+                dn, why = 1, 5
+            assert (rw, dn, why) == (int(out["reward"][i]), int(out["done"][i]), int(out["reason"][i])), (ply, i)
+            if dn and autoreset:
+                o.reset()
+            ob, om = o.state()
+            assert (b[i] == ob).all() and list(m[i]) == list(om), (ply, i)
+            assert (out["obs"][i] == ob).all(), (ply, i)
+            legal = sorted(o.moves())
+            got = np.nonzero(_mask_bits(out["mask"][i:i + 1])[0])[0].tolist()
+            assert got == legal and out["count"][i] == len(legal), (ply, i)
+            if legal:
+                k = oracle.policy_index(seed, i, o.draw, len(legal))
+                assert out["pick"][i] == legal[k], (ply, i)
+                o.pick()  # the pick's draw
+            else:
+                assert out["pick"][i] == 0xFFFF
+            if dn and not autoreset:
+                ends[i] = 1
+        if ends.any():  # the host reset picks a policy action too (one more draw)
+            env.reset(ends)
+            for i in np.nonzero(ends)[0]:
+                ors[i].reset()
+                ors[i].pick()
+        prev = env.outputs()["next_action"].astype(np.int64) if ends.any() else out["pick"].astype(np.int64)

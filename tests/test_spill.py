@@ -170,3 +170,28 @@ def test_gpu_external_actions_spill_and_checkpoint(oracle):
     for i, o in enumerate(ors):
         ob, om = o.state()
         assert (b1[i] == ob).all(), i
+
+
+@pytest.mark.gpu
+def test_gpu_spill_table_growth(oracle, long_boards, monkeypatch):
+    """The host-side growth path: a spill table started at 2^10 slots (GC_SPILL_BITS) is
+    rehashed and doubled between calls as the windows outgrow it; trajectories still equal
+    the oracle's."""
+    from gym_chess_amd.env import BatchedChessEnv
+
+    monkeypatch.setenv("GC_SPILL_BITS", "10")
+    init = kb_board()
+    n, plies = 96, 2000
+    env = BatchedChessEnv(n, device=0, seed=SEED, initial_board=init, opponent="random", player_color="BLACK")
+    assert env.spill_info()["bits"] == 10
+    for _ in range(plies):
+        env.step_random(1)
+    info = env.spill_info()
+    assert info["bits"] > 10 and info["live"] > 0, info
+    b, m = env.boards()
+    with _pool() as ex:
+        fins = list(ex.map(lambda i: oracle.rollout_trace(SEED, i, plies, init=init, opponent=1, agent_white=False),
+                           range(n)))
+    for i in range(n):
+        assert (b[i] == fins[i]["final_board"]).all() and list(m[i]) == list(fins[i]["final_meta"]), i
+    env.close()
