@@ -264,7 +264,7 @@ def perft_leg(args, rep):
 ALG_BYTES_API = 120 + 2 + 24 + 128 + 12 + 520 + 64 + 4 + 4
 
 
-def api_step_leg(args, rep, n):
+def api_step_leg(args, rep, n, **env_kw):
     """The reference's call shape (chess_v2.py:219-294 + possible_actions 333-335) on device
     buffers: per step an external action per board in (here: the previous step's random-policy
     pick, so no host round trip), reward / done / reason, the int8 observation, the legal-action
@@ -273,7 +273,7 @@ def api_step_leg(args, rep, n):
     from gym_chess_amd.env import BatchedChessEnv
 
     def setup(rp):
-        env = BatchedChessEnv(n, device=rp.device, seed=rp.board_seed(args.seed + 11))
+        env = BatchedChessEnv(n, device=rp.device, seed=rp.board_seed(args.seed + 11), **env_kw)
         if args.settle > 0:
             env.rollout(args.settle)
         io = env.device_io()
@@ -301,10 +301,13 @@ def api_step_leg(args, rep, n):
         env.close()
     avg = kms / 1e3 / args.api_steps
     ach = n * ALG_BYTES_API / avg / 1e9
-    return {"value": rep.world_size * n * args.api_steps / dt, "unit": "env_steps/s", "steps": args.api_steps,
-            "roofline": {"bound": "hbm", "kernel": "k_env_step_api2", "achieved": ach, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "avg_launch_us": avg * 1e6,
-                         "alg_bytes_per_board": ALG_BYTES_API}}
+    out = {"value": rep.world_size * n * args.api_steps / dt, "unit": "env_steps/s", "steps": args.api_steps,
+           "roofline": {"bound": "hbm", "kernel": "k_env_step_api2" + ("_vs" if env_kw else ""), "achieved": ach,
+                        "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "avg_launch_us": avg * 1e6,
+                        "alg_bytes_per_board": ALG_BYTES_API}}
+    if env_kw:
+        out["env"] = env_kw
+    return out
 
 
 def reference_driver(env, episodes, steps, seed):
@@ -528,6 +531,8 @@ def main():
         e.close()
     if args.api_steps > 0:
         extra["api_step"] = api_step_leg(args, rep, n)
+        # the random opponent answering inside each step (chess_v2.py:275-288), paired driver
+        extra["api_step"]["opponent_random"] = api_step_leg(args, rep, n, opponent="random")
     if args.single_episodes > 0:
         extra["single_env"] = single_env_leg(args, rep)
     if args.variant_steps > 0:

@@ -47,6 +47,25 @@ __device__ __forceinline__ void gc_stamp(int k) {
 }
 #define GC_STAMP(k) gc_stamp(k)
 #endif
+#ifdef GC_PSTAMPS
+// diagnostic build only: per wave, the cycles of each segment of the fused ply (phase work
+// and barrier waits), summed over the launch's plies (tools/pstamp_probe.py)
+__shared__ unsigned long long gc_pst[8][9];  // [wave][segment 0..7, last stamp]
+__device__ unsigned long long* g_pst_out;
+__device__ __forceinline__ void gc_pst_mark(int k) {
+    __builtin_amdgcn_sched_barrier(0);
+    const unsigned long long t = __builtin_amdgcn_s_memtime();
+    if ((threadIdx.x & 63) == 0) {
+        const int w = threadIdx.x >> 6;
+        gc_pst[w][k] += t - gc_pst[w][8];
+        gc_pst[w][8] = t;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+}
+#define PST(k) gc_pst_mark(k)
+#else
+#define PST(k)
+#endif
 #include "gc_core.h"
 #include "gc_env.h"
 #include "gc_perft.h"
@@ -913,7 +932,9 @@ __device__ __forceinline__ void pair_half(PairLds& L, int role, int l, bool mv, 
         if (mv) rep_prefetch(h, s, pr);
         w1_issue();
     }
+    PST(0);
     pair_barrier();
+    PST(1);
 
     // ---- phase 1: W0 pins / checkers and the enemy's diagonal slider attacks; W1 the enemy's
     // leaper and orthogonal slider attacks and the mover's own check flag (FIDE: en passant)
@@ -982,7 +1003,9 @@ __device__ __forceinline__ void pair_half(PairLds& L, int role, int l, bool mv, 
         }
     }
     GC_STAMP(2);
+    PST(2);
     pair_barrier();
+    PST(3);
     GC_STAMP(3);
 
     // ---- phase 2
@@ -1092,7 +1115,9 @@ __device__ __forceinline__ void pair_half(PairLds& L, int role, int l, bool mv, 
     }
     L.part[role][l] = (u32)part;
     GC_STAMP(4);
+    PST(4);
     pair_barrier();
+    PST(5);
     GC_STAMP(5);
 
     // ---- phase 3 opens: both waves merge the count planes (SW: W0 takes W1's slider sets), W0
@@ -1261,7 +1286,9 @@ __device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, int ro
         }
     }
     if (SHARE_ACT) {  // the next action and draw counter to W1; LDS free for the next ply
+        PST(6);
         pair_barrier();
+        PST(7);
         if (role) {
             a = (int)L.act[l];
             d = L.draw[l];
@@ -1598,6 +1625,12 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
     uint64_t steps = 0, rsum = 0;
     u32 e_mate = 0, e_rep = 0, e_cap = 0, e_nomove = 0, e_err = 0;
     StepOut o = {0, 0, R_NONE, 0};
+#ifdef GC_PSTAMPS
+    if (l == 0) {
+        for (int k = 0; k < 8; k++) gc_pst[threadIdx.x >> 6][k] = 0;
+        gc_pst[threadIdx.x >> 6][8] = __builtin_amdgcn_s_memtime();
+    }
+#endif
     for (int p = 0; p < plies; p++) {
         int played = a;
         o = pair_step<OPP, true, FIDE>(Ls, L, C, role, l, i, live, rp, s, a, d, h, nst);
@@ -1617,6 +1650,12 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
         }
         if (role) h.commit();  // this ply's window write lands before the next ply's probe
     }
+#ifdef GC_PSTAMPS
+    if (g_pst_out != nullptr && l == 0) {
+        const size_t w = (size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+        for (int k = 0; k < 8; k++) g_pst_out[w * 8 + k] = gc_pst[threadIdx.x >> 6][k];
+    }
+#endif
     const PairIO io = store_io(slab, nn);
     if (live) {
         if (role == 0) {
@@ -4041,6 +4080,26 @@ extern "C" int gc_env_window_sum(gc_env* e, uint64_t* sum) {
     (void)hipFree(d);
     return 0;
 }
+
+#ifdef GC_PSTAMPS
+// per wave (global wave index = block * waves per block + wave): the 8 segment cycle sums of
+// one fused launch of n_plies (reference rules, opponent "none")
+extern "C" int gc_debug_pstamps(gc_env* e, int n_plies, uint64_t* out /* waves * 8 */) {
+    unsigned long long* d = nullptr;
+    const size_t waves = (size_t)((e->n + PAIR_BOARDS * PAIRS_WG - 1) / (PAIR_BOARDS * PAIRS_WG)) * 2 * PAIRS_WG;
+    if (dalloc(&d, waves * 8)) return -1;
+    HIPCHK(hipMemsetAsync(d, 0, waves * 64, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_pst_out), &d, sizeof(d)));
+    if (issue_rollout(e, n_plies, nullptr, false)) return -1;
+    HIPCHK(hipMemcpyAsync(out, d, waves * 64, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    unsigned long long* z = nullptr;
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_pst_out), &z, sizeof(z)));
+    (void)hipFree(d);
+    return 0;
+}
+#endif
 
 #ifdef GC_STAMPS
 extern "C" int gc_debug_stamps(gc_env* e, int n_plies, uint64_t* out /* (n/64)*8 */) {

@@ -1,0 +1,36 @@
+"""Diagnostic only: where a fused ply's time goes, per role -- the cycles of each segment of
+k_env_rollout2<false, 0> (phase work and barrier waits, s_memtime), summed over a launch of
+--plies plies and averaged per ply over the waves (build: tools/build_variants.sh pst
+"-DGC_PSTAMPS" -> tools/_lib_pst.so).  Segments: phase 0 | wait A | phase 1 | wait B |
+phase 2 | wait C | phase 3 (outcome, pick / commit) | wait D (next action to W1)."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+L = ctypes.CDLL(os.environ.get("PST_LIB") or os.path.join(ROOT, "tools", "_lib_pst.so"))
+P = ctypes.c_void_p
+L.gc_env_create.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint64, P, P]
+L.gc_env_rollout.argtypes = [P, ctypes.c_int, P, P, P, P, P]
+L.gc_debug_pstamps.argtypes = [P, ctypes.c_int, P]
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+plies = int(sys.argv[2]) if len(sys.argv) > 2 else 200
+pmap = int(os.environ.get("PST_MAP", "2"))
+h = P()
+assert L.gc_env_create(0, n, 0x5EED + 3, None, ctypes.byref(h)) == 0
+assert L.gc_env_rollout(h, 1000, None, None, None, None, None) == 0  # steady state
+waves = ((n + 127) // 128) * 4
+out = np.zeros(waves * 8, dtype=np.uint64)
+assert L.gc_debug_pstamps(h, plies, out.ctypes.data_as(P)) == 0
+st = out.reshape(-1, 8).astype(np.float64) / plies
+w = np.arange(waves) % 4
+role = np.where(pmap == 2, (w ^ (w >> 1)) & 1, w & 1)
+names = ["phase 0", "wait A", "phase 1", "wait B", "phase 2", "wait C", "phase 3", "wait D"]
+for r in (0, 1):
+    s = st[role == r]
+    tot = s.sum(axis=1).mean()
+    print(f"[W{r}] {len(s)} waves, {tot:.0f} cycles per ply")
+    for k in range(8):
+        print(f"   {names[k]:>8}: {s[:, k].mean():7.0f}  ({s[:, k].mean() / tot:5.1%})")
