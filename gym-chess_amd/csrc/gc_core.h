@@ -937,6 +937,19 @@ GC_HD void sw_diag(const Pos& s, const Gen& g, u64* t, u64 xm = ~0ull) {
     t[SW_DIAG + 2] = ray_fill_att<9, true>(gd, empty, ~FILE_A) & tm;
     t[SW_DIAG + 3] = ray_fill_att<7, true>(ga, empty, ~FILE_H) & tm;
 }
+// the diagonal sets SW_DIAG + lo .. SW_DIAG + hi - 1 only (the paired driver splits them
+// between its two waves)
+template <int lo, int hi>
+GC_HD void sw_diag_part(const Pos& s, const Gen& g, u64* t, u64 xm = ~0ull) {
+    const int kq = sw_ksq(g);
+    const u64 S = (s.b | s.q) & g.own, fr = S & ~g.pinned, pp = S & g.pinned;
+    const u64 empty = ~g.occ, tm = ~g.own & g.checkmask & xm;
+    const u64 gd = fr | (pp & diag_mask(kq)), ga = fr | (pp & anti_mask(kq));
+    if (lo <= 0 && 0 < hi) t[SW_DIAG + 0] = ray_fill_att<7, false>(ga, empty, ~FILE_A) & tm;
+    if (lo <= 1 && 1 < hi) t[SW_DIAG + 1] = ray_fill_att<9, false>(gd, empty, ~FILE_H) & tm;
+    if (lo <= 2 && 2 < hi) t[SW_DIAG + 2] = ray_fill_att<9, true>(gd, empty, ~FILE_A) & tm;
+    if (lo <= 3 && 3 < hi) t[SW_DIAG + 3] = ray_fill_att<7, true>(ga, empty, ~FILE_H) & tm;
+}
 GC_HD void sw_kings(const Pos& s, const Gen& g, u64* t, u64 xm = ~0ull) {
     const u64 K = s.k & g.own, ok = ~g.own & ~g.enemy_att & xm;
     t[SW_K + 0] = (K >> 8) & ok;              // target = origin - 8

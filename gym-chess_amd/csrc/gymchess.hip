@@ -897,6 +897,13 @@ struct PairHalf {
     u64 T[SW_SETS];  // SW: the next side's move sets (each wave its own; all in LDS after phase 2)
     u64 cw[4];       // SW, W0: every set's count, one byte per set (gc_core.h sw_pack)
 };
+// Diagonal slider sets computed by W0 instead of W1 in the set-wise phase 2 (reference rules):
+// balances the two waves' phase-2 work (tools/pstamp_probe.py: W1 3 840 vs W0 2 810 cycles
+// per ply with 0)
+#ifndef GC_SW_SPLIT
+#define GC_SW_SPLIT 0
+#endif
+static_assert(GC_SW_SPLIT >= 0 && GC_SW_SPLIT <= 4, "GC_SW_SPLIT: 0..4 diagonal sets on W0");
 struct PairNoop {
     __device__ void operator()() const {}
 };
@@ -1046,7 +1053,8 @@ __device__ __forceinline__ void pair_half(PairLds& L, int role, int l, bool mv, 
     int c = 0;
     u32 hl = hl_of(s.meta);
     if (role == 0) {
-        if constexpr (SW) {  // pawn, knight and king sets; castles counted here
+        if constexpr (SW) {  // pawn, knight and king sets (+ GC_SW_SPLIT diagonal sets); castles counted here
+            constexpr int W0_FROM = FIDE ? SW_K : SW_K - GC_SW_SPLIT;  // W0's sets: [0, SW_ORTH) and [W0_FROM, SW_SETS)
             H.cw[0] = H.cw[1] = H.cw[2] = H.cw[3] = 0;
             if (gen) {
                 if constexpr (FIDE) {
@@ -1054,15 +1062,16 @@ __device__ __forceinline__ void pair_half(PairLds& L, int role, int l, bool mv, 
                 } else {
                     sw_pawns(ns, g, H.T);
                     sw_knights(ns, g, H.T);
+                    sw_diag_part<4 - GC_SW_SPLIT, 4>(ns, g, H.T);
                     sw_kings(ns, g, H.T);
                 }
                 sw_pack(H.T, 0, SW_ORTH, H.cw);
-                sw_pack(H.T, SW_K, SW_SETS, H.cw);
-                part = sw_popc(H.T, 0, SW_ORTH) + sw_popc(H.T, SW_K, SW_SETS) + popc(g.castles);
+                sw_pack(H.T, W0_FROM, SW_SETS, H.cw);
+                part = sw_popc(H.T, 0, SW_ORTH) + sw_popc(H.T, W0_FROM, SW_SETS) + popc(g.castles);
 #pragma unroll
                 for (int j = 0; j < SW_ORTH; j++) L.sets[j][l] = H.T[j];
 #pragma unroll
-                for (int j = SW_K; j < SW_SETS; j++) L.sets[j][l] = H.T[j];
+                for (int j = W0_FROM; j < SW_SETS; j++) L.sets[j][l] = H.T[j];
             }
         } else if constexpr (FIDE) {  // castles counted here (W1 does not know them)
             if (gen) {
@@ -1078,18 +1087,19 @@ __device__ __forceinline__ void pair_half(PairLds& L, int role, int l, bool mv, 
         }
     } else {
         if constexpr (SW) {  // the slider direction sets and their byte counts, to W0 through LDS
+            constexpr int W1_TO = FIDE ? SW_K : SW_K - GC_SW_SPLIT;  // W1's sets: [SW_ORTH, W1_TO)
             u64 cw[4] = {0, 0, 0, 0};
             if (gen) {
                 if constexpr (FIDE) {
                     gcf::fsw_gen_b(ns, gcf::FGen{g, 0, -1}, H.T);
                 } else {
                     sw_orth(ns, g, H.T);
-                    sw_diag(ns, g, H.T);
+                    sw_diag_part<0, 4 - GC_SW_SPLIT>(ns, g, H.T);
                 }
-                sw_pack(H.T, SW_ORTH, SW_K, cw);
-                part = sw_popc(H.T, SW_ORTH, SW_K);
+                sw_pack(H.T, SW_ORTH, W1_TO, cw);
+                part = sw_popc(H.T, SW_ORTH, W1_TO);
 #pragma unroll
-                for (int j = SW_ORTH; j < SW_K; j++) L.sets[j][l] = H.T[j];
+                for (int j = SW_ORTH; j < W1_TO; j++) L.sets[j][l] = H.T[j];
             }
             L.swc[0][l] = cw[1];
             L.swc[1][l] = cw[2];
@@ -1621,19 +1631,27 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
     constexpr int blk0 = 0;
     const int plies = (int)(rinfo >> 18);
     rinfo &= 0x1FFFFu;
+#ifdef GC_PSTAMPS
+    const unsigned long long g_pst_entry = __builtin_amdgcn_s_memrealtime();  // wave start, before the entry loads
+#endif
     PAIR_PROLOGUE
     uint64_t steps = 0, rsum = 0;
     u32 e_mate = 0, e_rep = 0, e_cap = 0, e_nomove = 0, e_err = 0;
     StepOut o = {0, 0, R_NONE, 0};
 #ifdef GC_PSTAMPS
+    unsigned long long rt0 = 0, rt1 = 0;  // 100 MHz wall clock: after the entry loads, after the first ply
     if (l == 0) {
         for (int k = 0; k < 8; k++) gc_pst[threadIdx.x >> 6][k] = 0;
         gc_pst[threadIdx.x >> 6][8] = __builtin_amdgcn_s_memtime();
     }
+    rt0 = __builtin_amdgcn_s_memrealtime();
 #endif
     for (int p = 0; p < plies; p++) {
         int played = a;
         o = pair_step<OPP, true, FIDE>(Ls, L, C, role, l, i, live, rp, s, a, d, h, nst);
+#ifdef GC_PSTAMPS
+        if (p == 0) rt1 = __builtin_amdgcn_s_memrealtime();
+#endif
         if (trace && role && live) trace[(size_t)p * nn + i] = trace_word(played == A_NONE ? -1 : played, o);
         if (played == A_NONE) {
             e_nomove++;
@@ -1653,7 +1671,11 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
 #ifdef GC_PSTAMPS
     if (g_pst_out != nullptr && l == 0) {
         const size_t w = (size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-        for (int k = 0; k < 8; k++) g_pst_out[w * 8 + k] = gc_pst[threadIdx.x >> 6][k];
+        for (int k = 0; k < 8; k++) g_pst_out[w * 12 + k] = gc_pst[threadIdx.x >> 6][k];
+        g_pst_out[w * 12 + 8] = g_pst_entry;  // (set below)
+        g_pst_out[w * 12 + 9] = rt0;
+        g_pst_out[w * 12 + 10] = rt1;
+        g_pst_out[w * 12 + 11] = __builtin_amdgcn_s_memrealtime();
     }
 #endif
     const PairIO io = store_io(slab, nn);
@@ -4083,16 +4105,17 @@ extern "C" int gc_env_window_sum(gc_env* e, uint64_t* sum) {
 
 #ifdef GC_PSTAMPS
 // per wave (global wave index = block * waves per block + wave): the 8 segment cycle sums of
-// one fused launch of n_plies (reference rules, opponent "none")
-extern "C" int gc_debug_pstamps(gc_env* e, int n_plies, uint64_t* out /* waves * 8 */) {
+// one fused launch of n_plies (reference rules, opponent "none"), then 4 s_memrealtime stamps:
+// wave start, entry loads done, first ply done, last ply done
+extern "C" int gc_debug_pstamps(gc_env* e, int n_plies, uint64_t* out /* waves * 12 */) {
     unsigned long long* d = nullptr;
     const size_t waves = (size_t)((e->n + PAIR_BOARDS * PAIRS_WG - 1) / (PAIR_BOARDS * PAIRS_WG)) * 2 * PAIRS_WG;
-    if (dalloc(&d, waves * 8)) return -1;
-    HIPCHK(hipMemsetAsync(d, 0, waves * 64, e->stream));
+    if (dalloc(&d, waves * 12)) return -1;
+    HIPCHK(hipMemsetAsync(d, 0, waves * 96, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
     HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_pst_out), &d, sizeof(d)));
     if (issue_rollout(e, n_plies, nullptr, false)) return -1;
-    HIPCHK(hipMemcpyAsync(out, d, waves * 64, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(out, d, waves * 96, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
     unsigned long long* z = nullptr;
     HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_pst_out), &z, sizeof(z)));

@@ -22,9 +22,17 @@ h = P()
 assert L.gc_env_create(0, n, 0x5EED + 3, None, ctypes.byref(h)) == 0
 assert L.gc_env_rollout(h, 1000, None, None, None, None, None) == 0  # steady state
 waves = ((n + 127) // 128) * 4
-out = np.zeros(waves * 8, dtype=np.uint64)
+out = np.zeros(waves * 12, dtype=np.uint64)
 assert L.gc_debug_pstamps(h, plies, out.ctypes.data_as(P)) == 0
-st = out.reshape(-1, 8).astype(np.float64) / plies
+raw = out.reshape(-1, 12)
+st = raw[:, :8].astype(np.float64) / plies
+rt = raw[:, 8:].astype(np.int64)  # 100 MHz: wave start, entry loads done, first ply done, last ply done
+t0 = rt[:, 0].min()
+us = (rt - t0) / 100.0
+print(f"launch anatomy ({plies} plies, us from the first wave's start): last wave start {us[:, 0].max():.2f}; "
+      f"entry loads mean {(us[:, 1] - us[:, 0]).mean():.2f}; first ply mean {(us[:, 2] - us[:, 1]).mean():.2f}, "
+      f"later plies mean {((us[:, 3] - us[:, 2]) / max(plies - 1, 1)).mean():.3f}; wave end mean {us[:, 3].mean():.2f}, "
+      f"p90 {np.percentile(us[:, 3], 90):.2f}, max {us[:, 3].max():.2f}")
 w = np.arange(waves) % 4
 role = np.where(pmap == 2, (w ^ (w >> 1)) & 1, w & 1)
 names = ["phase 0", "wait A", "phase 1", "wait B", "phase 2", "wait C", "phase 3", "wait D"]
