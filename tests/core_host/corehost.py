@@ -19,7 +19,10 @@ def lib():
         hdr = [os.path.join(_HERE, "..", "..", "gym-chess_amd", "csrc", h) for h in ("gc_core.h", "gc_env.h", "gc_fide.h")]
         if not os.path.exists(_SO) or os.path.getmtime(_SO) < max(os.path.getmtime(p) for p in [src] + hdr):
             os.makedirs(os.path.dirname(_SO), exist_ok=True)
-            subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wno-unknown-pragmas", "-o", _SO, src], check=True)
+            tmp = f"{_SO}.{os.getpid()}.tmp"  # build aside, then rename: parallel test workers never load a partial file
+            subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wno-unknown-pragmas", "-o", tmp, src],
+                           check=True)
+            os.replace(tmp, _SO)
         L = ctypes.CDLL(_SO)
         L.host_between.restype = ctypes.c_uint64
         L.host_pins_agree.argtypes = [P, P, ctypes.c_int]
