@@ -1632,7 +1632,15 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
     const int plies = (int)(rinfo >> 18);
     rinfo &= 0x1FFFFu;
 #ifdef GC_PSTAMPS
-    const unsigned long long g_pst_entry = __builtin_amdgcn_s_memrealtime();  // wave start, before the entry loads
+    unsigned long long g_pst_entry = __builtin_amdgcn_s_memrealtime();  // wave start, before the entry loads
+    {  // the wave's placement in bits 44+: cu | sh | se | simd | xcc (as GC_STAMPS_REAL)
+        unsigned hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)\n\ts_getreg_b32 %1, hwreg(HW_REG_XCC_ID)"
+                     : "=s"(hw), "=s"(xcc));
+        const unsigned long long where = ((hw >> 8) & 0xF) | (((hw >> 12) & 1) << 4) | (((hw >> 13) & 3) << 5) |
+                                         (((hw >> 4) & 3) << 7) | ((unsigned long long)(xcc & 0xF) << 9);
+        g_pst_entry = (g_pst_entry & ((1ull << 44) - 1)) | (where << 44);
+    }
 #endif
     PAIR_PROLOGUE
     uint64_t steps = 0, rsum = 0;
@@ -3814,6 +3822,8 @@ extern "C" int gc_env_rollout_device(gc_env* e, int n_plies, uint64_t* d_trace, 
     if (!e->policy_ready) return fail("policy actions stale: call gc_env_reset or gc_env_select_random first");
     HIPCHK(hipSetDevice(e->device));
     if (spill_before(e)) return -1;
+    // marker events around the launches (r03 probe: timing the launches by hipExtLaunchKernel's
+    // own start / stop events cost ~8 us more host time per call at K = 20 -- tools/short_probe.py)
     if (ev_begin >= 0) HIPCHK(hipEventRecord(e->ev[ev_begin], e->stream));
     if (issue_rollout(e, n_plies, d_trace, false)) return -1;
     if (ev_end >= 0) HIPCHK(hipEventRecord(e->ev[ev_end], e->stream));

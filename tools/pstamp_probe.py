@@ -26,6 +26,8 @@ out = np.zeros(waves * 12, dtype=np.uint64)
 assert L.gc_debug_pstamps(h, plies, out.ctypes.data_as(P)) == 0
 raw = out.reshape(-1, 12)
 st = raw[:, :8].astype(np.float64) / plies
+where = (raw[:, 8] >> np.uint64(44)).astype(np.int64)  # placement: cu | sh | se | simd | xcc
+raw[:, 8] &= np.uint64((1 << 44) - 1)
 rt = raw[:, 8:].astype(np.int64)  # 100 MHz: wave start, entry loads done, first ply done, last ply done
 t0 = rt[:, 0].min()
 us = (rt - t0) / 100.0
@@ -42,3 +44,22 @@ for r in (0, 1):
     print(f"[W{r}] {len(s)} waves, {tot:.0f} cycles per ply")
     for k in range(8):
         print(f"   {names[k]:>8}: {s[:, k].mean():7.0f}  ({s[:, k].mean() / tot:5.1%})")
+
+# where the slow waves run: wave end by XCD, by CU load and by SIMD load
+xcc = where >> 9
+cu_key = where & 0x7F | (xcc << 7)        # cu, sh, se within the XCD
+simd_key = where | 0
+end = us[:, 3]
+print("wave end by XCD (mean / max us):", " ".join(f"{x}:{end[xcc == x].mean():.1f}/{end[xcc == x].max():.1f}"
+                                                    for x in np.unique(xcc)))
+_, cu_inv, cu_cnt = np.unique(cu_key, return_inverse=True, return_counts=True)
+_, si_inv, si_cnt = np.unique(simd_key, return_inverse=True, return_counts=True)
+print(f"CUs used {len(cu_cnt)}, waves per CU: " + ", ".join(f"{c}x{n}" for c, n in zip(*np.unique(cu_cnt, return_counts=True))))
+print(f"SIMDs used {len(si_cnt)}, waves per SIMD: " + ", ".join(f"{c}x{n}" for c, n in zip(*np.unique(si_cnt, return_counts=True))))
+wl = si_cnt[si_inv]
+for c in np.unique(wl):
+    print(f"  waves on a SIMD with {c} waves: end mean {end[wl == c].mean():.1f} max {end[wl == c].max():.1f} "
+          f"per-ply {((us[:, 3] - us[:, 2]) / max(plies - 1, 1))[wl == c].mean():.3f}")
+blk = np.arange(waves) // 4
+print("wave end by block % 8:", " ".join(f"{b}:{end[blk % 8 == b].mean():.1f}" for b in range(8)))
+print("end percentiles (us):", " ".join(f"p{q}:{np.percentile(end, q):.1f}" for q in (0, 10, 25, 50, 75, 90, 99, 100)))

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--boards", type=int, default=65536)
     ap.add_argument("--settle", type=int, default=1000)
     ap.add_argument("--fused", action="store_true", help="time rollout_device(K) with a per-ply trace instead")
+    ap.add_argument("--no-events", action="store_true", help="fused: no event slots (wall clock only)")
     a = ap.parse_args()
     from gym_chess_amd.env import BatchedChessEnv
 
@@ -44,7 +45,7 @@ def main():
                 env.synchronize()
                 t0 = time.perf_counter()
                 if a.fused:
-                    env.rollout_device(k, tb, events=(0, 1))
+                    env.rollout_device(k, tb, events=(-1, -1) if a.no_events else (0, 1))
                 else:
                     env.record_event(0)
                     env.step_random(k)
@@ -52,7 +53,7 @@ def main():
                 t_enq = time.perf_counter()
                 env.synchronize()
                 t1 = time.perf_counter()
-                ev = env.elapsed_ms(0, 1) * 1e3
+                ev = 0.0 if a.no_events else env.elapsed_ms(0, 1) * 1e3
                 row = {"fused": a.fused, "streams": s, "k": k, "rep": r, "wall_us_per_ply": (t1 - t0) * 1e6 / k,
                        "event_us_per_ply": ev / k, "enqueue_us": (t_enq - t0) * 1e6, "wall_us": (t1 - t0) * 1e6,
                        "event_us": ev}
@@ -60,6 +61,13 @@ def main():
                 print(json.dumps({k2: (round(v, 2) if isinstance(v, float) else v) for k2, v in row.items()}),
                       flush=True)
     env.close()
+    import numpy as np
+
+    for k in sorted({r["k"] for r in res}):
+        w = np.median([r["wall_us"] for r in res if r["k"] == k])
+        e = np.median([r["event_us"] for r in res if r["k"] == k])
+        print(f"# k={k}: median wall {w:.1f} us ({w / k:.3f}/ply), event {e:.1f} us ({e / k:.3f}/ply), "
+              f"markers={'GC_MARKER_EVENTS' in os.environ}", flush=True)
 
 
 if __name__ == "__main__":
