@@ -907,9 +907,16 @@ static_assert(GC_SW_SPLIT >= 0 && GC_SW_SPLIT <= 4, "GC_SW_SPLIT: 0..4 diagonal 
 struct PairNoop {
     __device__ void operator()() const {}
 };
+// A role known at compile time (the fused kernels run one loop per role): every `role` test
+// in the pair driver folds, so a wave's loop holds only its own role's code -- no role
+// branches, and nothing the other role alone needs (the stats on W0, the pick on W1).
+template <int R>
+struct RoleC {
+    __device__ constexpr operator int() const { return R; }
+};
 
-template <bool FIDE, bool ACT_LDS, bool MV_LDS = false, bool SW = false, class W1Issue, class W1Late>
-__device__ __forceinline__ void pair_half(PairLds& L, int role, int l, bool mv, bool regen, const Pos& s, int a,
+template <bool FIDE, bool ACT_LDS, bool MV_LDS = false, bool SW = false, class RT = int, class W1Issue, class W1Late>
+__device__ __forceinline__ void pair_half(PairLds& L, RT role, int l, bool mv, bool regen, const Pos& s, int a,
                                           const u32* act_lds, const u32* mv_lds, DevHist& h, PairHalf& H,
                                           W1Issue&& w1_issue, W1Late&& w1_late) {
     PairScratch scr{&L.slots[0][l]};
@@ -1196,8 +1203,8 @@ __device__ __forceinline__ int sw_pick_lds(const PairLds& L, int l, const Gen& g
 // table write is left deferred in h), the step counter nst.  Returns the ply's env.step()
 // outputs; on return both waves hold the same s, and with SHARE_ACT the same next action a
 // (W0 picks it; it crosses to W1 through LDS).
-template <bool SHARE_ACT, bool FIDE = false>
-__device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, int role, int l, int i,
+template <bool SHARE_ACT, bool FIDE = false, class RT = int>
+__device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, RT role, int l, int i,
                                             bool live, const Pos& rp, Pos& s, int& a, u32& d, DevHist& h,
                                             u32& nst) {
     constexpr bool SW = true;  // the self-play policy's move-set order (gc_core.h sw_*), both rule sets
@@ -1324,8 +1331,8 @@ struct PairLdsVs : PairLds {
     u32 vote[2];          // per wave: some board of it resets (BLACK: the opening half-ply runs)
 };
 
-template <bool BLACK, bool SHARE_ACT>
-__device__ __forceinline__ StepOut pair_step_vs(PairLdsVs* Ls, PairLdsVs& L, const PairCtx& C, int role, int l,
+template <bool BLACK, bool SHARE_ACT, class RT = int>
+__device__ __forceinline__ StepOut pair_step_vs(PairLdsVs* Ls, PairLdsVs& L, const PairCtx& C, RT role, int l,
                                                 int i, bool live, const Pos& rp, Pos& s, int& a, u32& d, DevHist& h,
                                                 u32& nst) {
     const bool none = a == A_NONE;                           // empty list: driver reset
@@ -1568,11 +1575,11 @@ __device__ __forceinline__ int role_of_wave(int w) {
 
 // One step of the paired driver: opponent "none" (OPP 0: pair_ply) or the random opponent
 // with a WHITE (1) or BLACK (2) agent (pair_step_vs).
-template <int OPP, bool SHARE_ACT, bool FIDE, class LdsT>
-__device__ __forceinline__ StepOut pair_step(LdsT* Ls, LdsT& L, const PairCtx& C, int role, int l, int i, bool live,
+template <int OPP, bool SHARE_ACT, bool FIDE, class LdsT, class RT>
+__device__ __forceinline__ StepOut pair_step(LdsT* Ls, LdsT& L, const PairCtx& C, RT role, int l, int i, bool live,
                                              const Pos& rp, Pos& s, int& a, u32& d, DevHist& h, u32& nst) {
-    if constexpr (OPP == 0) return pair_ply<SHARE_ACT, FIDE>(L, C, role, l, i, live, rp, s, a, d, h, nst);
-    else return pair_step_vs<OPP == 2, SHARE_ACT>(Ls, L, C, role, l, i, live, rp, s, a, d, h, nst);
+    if constexpr (OPP == 0) return pair_ply<SHARE_ACT, FIDE, RT>(L, C, role, l, i, live, rp, s, a, d, h, nst);
+    else return pair_step_vs<OPP == 2, SHARE_ACT, RT>(Ls, L, C, role, l, i, live, rp, s, a, d, h, nst);
 }
 
 template <bool FIDE, int OPP = 0>
@@ -1607,6 +1614,31 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
         for (int q = 0; q < 8; q++) g_stamp_out[((size_t)blk * 2 + role) * 8 + q] = gc_stamp_lds[threadIdx.x >> 6][q];
 #endif
 }
+
+// Fair share of a CU between the two workgroups it hosts (GC_FAIR).  Each SIMD runs one wave
+// of each workgroup, and the SQ issues the older wave first when both are ready: left alone,
+// the workgroup dispatched first runs ~25 % ahead of its neighbour for the whole launch, and
+// the launch ends with the neighbour's tail on a half-empty CU (tools/pstamp_probe.py: wave
+// ends bimodal, p25 5 377 / p75 6 679 us over 1 000 plies).  Feedback instead: the two
+// workgroups of a CU publish their ply counts in a per-CU pair of words; every ply each wave
+// reads its neighbour's count (issued one ply ahead of its use) and the one that is ahead
+// drops to the lowest issue priority.  A neighbour from another launch, or none, only ever
+// reads as ahead or behind: priorities matter only against co-resident waves, so a stale word
+// costs nothing.  Vector loads / stores of device memory (agent scope).
+#ifndef GC_FAIR
+#define GC_FAIR 0  // r03 A/B: fair, but slower in total (a CU's throughput is what it is: the ahead
+                   // workgroup's lead costs nothing, equal progress costs issue slots) -- 8.45 vs 8.78e9
+                   // env.steps/s at --steps 20, 11.18 vs 11.32e9 at 1 000
+#endif
+#if GC_FAIR
+__device__ u32 g_fair_claim[2048];
+__device__ u32 g_fair_prog[2048][2];
+__device__ __forceinline__ u32 fair_cu() {  // this CU in the device: xcc | se | sh | cu
+    u32 hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)\n\ts_getreg_b32 %1, hwreg(HW_REG_XCC_ID)" : "=s"(hw), "=s"(xcc));
+    return ((xcc & 0xF) << 7) | (((hw >> 13) & 3) << 5) | (((hw >> 12) & 1) << 4) | ((hw >> 8) & 0xF);
+}
+#endif
 
 // One ply's env.step() outputs, packed for the per-ply trace [ply][N] (one coalesced 8-B
 // store per board per ply): action played (int16; -1 = none, the driver's no-move reset),
@@ -1646,6 +1678,14 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
     uint64_t steps = 0, rsum = 0;
     u32 e_mate = 0, e_rep = 0, e_cap = 0, e_nomove = 0, e_err = 0;
     StepOut o = {0, 0, R_NONE, 0};
+#if GC_FAIR
+    // the workgroup's slot of its CU's pair: claimed by wave 0, read by every wave after the
+    // first barrier (LDS); the neighbour's count, loaded one ply ahead of its use
+    __shared__ u32 fair_slot_lds;
+    const u32 fcu = fair_cu();
+    if (threadIdx.x == 0) fair_slot_lds = atomicAdd(&g_fair_claim[fcu], 1u) & 1u;
+    u32 fslot = 2, fnb = 0;  // 2: not read yet
+#endif
 #ifdef GC_PSTAMPS
     unsigned long long rt0 = 0, rt1 = 0;  // 100 MHz wall clock: after the entry loads, after the first ply
     if (l == 0) {
@@ -1654,58 +1694,83 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
     }
     rt0 = __builtin_amdgcn_s_memrealtime();
 #endif
-    for (int p = 0; p < plies; p++) {
-        int played = a;
-        o = pair_step<OPP, true, FIDE>(Ls, L, C, role, l, i, live, rp, s, a, d, h, nst);
+    // one loop per role (RoleC): each wave runs only its own role's code
+    auto plies_loop = [&](auto R) {
+        for (int p = 0; p < plies; p++) {
+            int played = a;
+            o = pair_step<OPP, true, FIDE>(Ls, L, C, R, l, i, live, rp, s, a, d, h, nst);
 #ifdef GC_PSTAMPS
-        if (p == 0) rt1 = __builtin_amdgcn_s_memrealtime();
+            if (p == 0) rt1 = __builtin_amdgcn_s_memrealtime();
 #endif
-        if (trace && role && live) trace[(size_t)p * nn + i] = trace_word(played == A_NONE ? -1 : played, o);
-        if (played == A_NONE) {
-            e_nomove++;
-        } else {
-            steps++;
-            rsum += (uint64_t)(int64_t)o.reward;
-            if (o.done) {
-                e_mate += o.reason == R_MATE || o.reason == R_MATED;
-                e_rep += o.reason == R_REPETITION;
-                e_cap += o.reason == R_MOVE_CAP;
-                e_err += o.reason == R_BOTH_CHECKED || o.reason == R_WINDOW_FULL;
-                e_nomove += o.reason == R_OPP_NO_MOVE;
+            if (R) {  // W1: the ply's outputs (trace, stats) and the window write
+                if (trace && live) trace[(size_t)p * nn + i] = trace_word(played == A_NONE ? -1 : played, o);
+                if (played == A_NONE) {
+                    e_nomove++;
+                } else {
+                    steps++;
+                    rsum += (uint64_t)(int64_t)o.reward;
+                    if (o.done) {
+                        e_mate += o.reason == R_MATE || o.reason == R_MATED;
+                        e_rep += o.reason == R_REPETITION;
+                        e_cap += o.reason == R_MOVE_CAP;
+                        e_err += o.reason == R_BOTH_CHECKED || o.reason == R_WINDOW_FULL;
+                        e_nomove += o.reason == R_OPP_NO_MOVE;
+                    }
+                }
+                h.commit();  // this ply's window write lands before the next ply's probe
+            }
+#if GC_FAIR
+            if (fslot == 2) fslot = fair_slot_lds;  // written before ply 0's first barrier
+            {
+                const u32 nb = __builtin_amdgcn_readfirstlane(fnb);  // the neighbour's count, read last ply
+                if (nb > (u32)p + 1) __builtin_amdgcn_s_setprio(2);  // behind: first
+                else __builtin_amdgcn_s_setprio(0);
+                if (threadIdx.x == 0) __hip_atomic_store(&g_fair_prog[fcu][fslot], (u32)p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                fnb = __hip_atomic_load(&g_fair_prog[fcu][fslot ^ 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+#endif
+        }
+        // the launch's end (in the role's own code: nothing of the other role's state stays live)
+#if GC_FAIR
+        __builtin_amdgcn_s_setprio(0);
+#endif
+#ifdef GC_PSTAMPS
+        if (g_pst_out != nullptr && l == 0) {
+            const size_t w = (size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+            for (int k = 0; k < 8; k++) g_pst_out[w * 12 + k] = gc_pst[threadIdx.x >> 6][k];
+            g_pst_out[w * 12 + 8] = g_pst_entry;  // (set below)
+            g_pst_out[w * 12 + 9] = rt0;
+            g_pst_out[w * 12 + 10] = rt1;
+            g_pst_out[w * 12 + 11] = __builtin_amdgcn_s_memrealtime();
+        }
+#endif
+        const PairIO io = store_io(slab, nn);
+        if (live) {
+            if (R == 0) {
+                io.act[i] = (uint16_t)a;
+                io.draw[i] = d;
+            } else {
+                io.store(i, s);
+                h.flush(g0);
+                io.nsteps[i] = nst;
+                io.reward[i] = o.reward;
+                io.done[i] = (uint8_t)o.done;
+                io.reason[i] = (uint8_t)o.reason;
+                if (stats) {
+                    uint64_t* so = stats + 8 * (size_t)i;
+                    so[0] += steps; so[1] += rsum;
+                    so[2 + R_MATE] += e_mate; so[2 + R_REPETITION] += e_rep; so[2 + R_MOVE_CAP] += e_cap;
+                    so[2 + R_NO_MOVES] += e_nomove; so[2 + R_BOTH_CHECKED] += e_err;
+                }
             }
         }
-        if (role) h.commit();  // this ply's window write lands before the next ply's probe
-    }
-#ifdef GC_PSTAMPS
-    if (g_pst_out != nullptr && l == 0) {
-        const size_t w = (size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-        for (int k = 0; k < 8; k++) g_pst_out[w * 12 + k] = gc_pst[threadIdx.x >> 6][k];
-        g_pst_out[w * 12 + 8] = g_pst_entry;  // (set below)
-        g_pst_out[w * 12 + 9] = rt0;
-        g_pst_out[w * 12 + 10] = rt1;
-        g_pst_out[w * 12 + 11] = __builtin_amdgcn_s_memrealtime();
-    }
+    };
+#ifdef GC_ROLE_RUNTIME  // A/B: one loop for both roles
+    plies_loop(role);
+#else
+    if (role == 0) plies_loop(RoleC<0>{});
+    else plies_loop(RoleC<1>{});
 #endif
-    const PairIO io = store_io(slab, nn);
-    if (live) {
-        if (role == 0) {
-            io.act[i] = (uint16_t)a;
-            io.draw[i] = d;
-        } else {
-            io.store(i, s);
-            h.flush(g0);
-            io.nsteps[i] = nst;
-            io.reward[i] = o.reward;
-            io.done[i] = (uint8_t)o.done;
-            io.reason[i] = (uint8_t)o.reason;
-            if (stats) {
-                uint64_t* so = stats + 8 * (size_t)i;
-                so[0] += steps; so[1] += rsum;
-                so[2 + R_MATE] += e_mate; so[2 + R_REPETITION] += e_rep; so[2 + R_MOVE_CAP] += e_cap;
-                so[2 + R_NO_MOVES] += e_nomove; so[2 + R_BOTH_CHECKED] += e_err;
-            }
-        }
-    }
 }
 
 // Fused K-ply random self-play: state in registers for the whole launch.  Per-ply outputs

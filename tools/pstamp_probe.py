@@ -27,7 +27,8 @@ assert L.gc_debug_pstamps(h, plies, out.ctypes.data_as(P)) == 0
 raw = out.reshape(-1, 12)
 st = raw[:, :8].astype(np.float64) / plies
 where = (raw[:, 8] >> np.uint64(44)).astype(np.int64)  # placement: cu | sh | se | simd | xcc
-raw[:, 8] &= np.uint64((1 << 44) - 1)
+hi = ~np.uint64((1 << 44) - 1)
+raw[:, 8] = (raw[:, 8] & np.uint64((1 << 44) - 1)) | (raw[:, 9] & hi)  # the clock's own top bits back
 rt = raw[:, 8:].astype(np.int64)  # 100 MHz: wave start, entry loads done, first ply done, last ply done
 t0 = rt[:, 0].min()
 us = (rt - t0) / 100.0
@@ -63,3 +64,19 @@ for c in np.unique(wl):
 blk = np.arange(waves) // 4
 print("wave end by block % 8:", " ".join(f"{b}:{end[blk % 8 == b].mean():.1f}" for b in range(8)))
 print("end percentiles (us):", " ".join(f"p{q}:{np.percentile(end, q):.1f}" for q in (0, 10, 25, 50, 75, 90, 99, 100)))
+
+# the two workgroups sharing a CU: the one dispatched first (lower block index) against the other
+cu_ids = np.unique(cu_key)
+d_first, first_wins = [], 0
+for c in cu_ids:
+    m = np.nonzero(cu_key == c)[0]
+    bl = np.unique(blk[m])
+    if len(bl) != 2:
+        continue
+    e0, e1 = end[m[blk[m] == bl[0]]].mean(), end[m[blk[m] == bl[1]]].mean()
+    d_first.append(e1 - e0)
+    first_wins += e0 < e1
+d_first = np.array(d_first)
+print(f"CUs with two workgroups: {len(d_first)}; lower block index finishes first on {first_wins}; "
+      f"end(later WG) - end(earlier WG): mean {d_first.mean():.1f} us, |mean| {np.abs(d_first).mean():.1f}, "
+      f"block distance of the pair: {sorted(set(int(np.diff(np.unique(blk[cu_key == c]))[0]) for c in cu_ids[:64] if len(np.unique(blk[cu_key == c])) == 2))[:8]}")
