@@ -66,6 +66,25 @@ GC_HD int popc(u64 x) { return __builtin_popcountll(x); }
 GC_HD int ctz(u64 x) { return __builtin_ctzll(x); }
 GC_HD int msb(u64 x) { return 63 - __builtin_clzll(x); }
 GC_HD u64 bit(int s) { return 1ull << s; }
+// Three-input bitwise ops on bitboards: one v_bitop3_b32 per 32-bit half on gfx950 (truth
+// table over a = 0xF0, b = 0xCC, c = 0xAA).  The compiler fuses few of these itself once the
+// 64-bit ops are split into halves, and the Kogge-Stone fills and the set masks are chains of
+// exactly this shape; the host build (CPU tests) evaluates the same expression in C.
+template <unsigned TT>
+GC_HD u64 bop3(u64 a, u64 b, u64 c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const unsigned lo = __builtin_amdgcn_bitop3_b32((unsigned)a, (unsigned)b, (unsigned)c, TT);
+    const unsigned hi = __builtin_amdgcn_bitop3_b32((unsigned)(a >> 32), (unsigned)(b >> 32), (unsigned)(c >> 32), TT);
+    return ((u64)hi << 32) | lo;
+#else
+    u64 r = 0;
+    for (int k = 0; k < 8; k++)
+        if (TT >> k & 1) r |= ((k & 4) ? a : ~a) & ((k & 2) ? b : ~b) & ((k & 1) ? c : ~c);
+    return r;
+#endif
+}
+GC_HD u64 and_or(u64 a, u64 b, u64 c) { return bop3<0xEA>(a, b, c); }  // (a & b) | c
+GC_HD u64 and3(u64 a, u64 b, u64 c) { return bop3<0x80>(a, b, c); }    // a & b & c
 // squares below s (s < 64): shift-only, so no 64-bit subtract (a VCC carry chain, and on
 // gfx950 a wait state before the carry is consumed)
 GC_HD u64 below(int s) { return ~(~0ull << s); }
@@ -214,12 +233,23 @@ GC_HD u64 sh(u64 x) { return LEFT ? (x << SH) : (x >> SH); }
 template <int SH, bool LEFT>
 GC_HD u64 ray_fill_att(u64 gen, u64 empty, u64 wrap) {
     u64 pro = empty & wrap;
-    gen |= pro & sh<SH, LEFT>(gen);
+    gen = and_or(pro, sh<SH, LEFT>(gen), gen);
     pro &= sh<SH, LEFT>(pro);
-    gen |= pro & sh<2 * SH, LEFT>(gen);
+    gen = and_or(pro, sh<2 * SH, LEFT>(gen), gen);
     pro &= sh<2 * SH, LEFT>(pro);
-    gen |= pro & sh<4 * SH, LEFT>(gen);
+    gen = and_or(pro, sh<4 * SH, LEFT>(gen), gen);
     return sh<SH, LEFT>(gen) & wrap;
+}
+// the same fill's targets within a mask tm: sh(gen) & wrap & tm in one op per half
+template <int SH, bool LEFT>
+GC_HD u64 ray_fill_to(u64 gen, u64 empty, u64 wrap, u64 tm) {
+    u64 pro = empty & wrap;
+    gen = and_or(pro, sh<SH, LEFT>(gen), gen);
+    pro &= sh<SH, LEFT>(pro);
+    gen = and_or(pro, sh<2 * SH, LEFT>(gen), gen);
+    pro &= sh<2 * SH, LEFT>(pro);
+    gen = and_or(pro, sh<4 * SH, LEFT>(gen), gen);
+    return and3(sh<SH, LEFT>(gen), wrap, tm);
 }
 
 // the map in three parts (the quad step kernel computes them on different waves)
@@ -891,15 +921,15 @@ GC_HD void sw_pawns_kl(const Pos& s, const Gen& g, const KingLines& kl, u64* t) 
     const u64 fp = P & ~g.pinned, pp = P & g.pinned;
     const u64 pf = pp & kl.fm(), pd = pp & kl.dm, pa = pp & kl.am;
     if (g.white) {  // lib.rs:935-958, p = +1: toward row 0
-        t[SW_P1] = ((fp >> 8) | ((pf >> 8) & pr)) & empty & cm;
-        t[SW_P2] = (((fp & ROW6) >> 16) | (((pf & ROW6) >> 16) & pr)) & empty & cm;
-        t[SW_PL] = (((fp >> 7) | ((pa >> 7) & pr)) & ~FILE_A) & opp & cm;  // row-1 col+1: anti-diagonal
-        t[SW_PR] = (((fp >> 9) | ((pd >> 9) & pr)) & ~FILE_H) & opp & cm;  // row-1 col-1: diagonal
+        t[SW_P1] = and3(and_or(pf >> 8, pr, fp >> 8), empty, cm);
+        t[SW_P2] = and3(and_or((pf & ROW6) >> 16, pr, (fp & ROW6) >> 16), empty, cm);
+        t[SW_PL] = and3(and_or(pa >> 7, pr, fp >> 7), opp & ~FILE_A, cm);  // row-1 col+1: anti-diagonal
+        t[SW_PR] = and3(and_or(pd >> 9, pr, fp >> 9), opp & ~FILE_H, cm);  // row-1 col-1: diagonal
     } else {
-        t[SW_P1] = ((fp << 8) | ((pf << 8) & pr)) & empty & cm;
-        t[SW_P2] = (((fp & ROW1) << 16) | (((pf & ROW1) << 16) & pr)) & empty & cm;
-        t[SW_PL] = (((fp << 9) | ((pd << 9) & pr)) & ~FILE_A) & opp & cm;  // row+1 col+1: diagonal
-        t[SW_PR] = (((fp << 7) | ((pa << 7) & pr)) & ~FILE_H) & opp & cm;  // row+1 col-1: anti-diagonal
+        t[SW_P1] = and3(and_or(pf << 8, pr, fp << 8), empty, cm);
+        t[SW_P2] = and3(and_or((pf & ROW1) << 16, pr, (fp & ROW1) << 16), empty, cm);
+        t[SW_PL] = and3(and_or(pd << 9, pr, fp << 9), opp & ~FILE_A, cm);  // row+1 col+1: diagonal
+        t[SW_PR] = and3(and_or(pa << 7, pr, fp << 7), opp & ~FILE_H, cm);  // row+1 col-1: anti-diagonal
     }
 }
 GC_HD void sw_pawns(const Pos& s, const Gen& g, u64* t) { sw_pawns_kl(s, g, king_lines(g.ks, g.white), t); }
@@ -922,20 +952,20 @@ GC_HD void sw_orth(const Pos& s, const Gen& g, u64* t, u64 xm = ~0ull) {
     const u64 S = (s.r | s.q) & g.own, fr = S & ~g.pinned, pp = S & g.pinned;
     const u64 empty = ~g.occ, tm = ~g.own & g.checkmask & xm;
     const u64 gf = fr | (pp & file_mask(kq)), gr = fr | (pp & row_mask(kq));
-    t[SW_ORTH + 0] = ray_fill_att<8, false>(gf, empty, ~0ull) & tm;
-    t[SW_ORTH + 1] = ray_fill_att<8, true>(gf, empty, ~0ull) & tm;
-    t[SW_ORTH + 2] = ray_fill_att<1, true>(gr, empty, ~FILE_A) & tm;
-    t[SW_ORTH + 3] = ray_fill_att<1, false>(gr, empty, ~FILE_H) & tm;
+    t[SW_ORTH + 0] = ray_fill_to<8, false>(gf, empty, ~0ull, tm);
+    t[SW_ORTH + 1] = ray_fill_to<8, true>(gf, empty, ~0ull, tm);
+    t[SW_ORTH + 2] = ray_fill_to<1, true>(gr, empty, ~FILE_A, tm);
+    t[SW_ORTH + 3] = ray_fill_to<1, false>(gr, empty, ~FILE_H, tm);
 }
 GC_HD void sw_diag(const Pos& s, const Gen& g, u64* t, u64 xm = ~0ull) {
     const int kq = sw_ksq(g);
     const u64 S = (s.b | s.q) & g.own, fr = S & ~g.pinned, pp = S & g.pinned;
     const u64 empty = ~g.occ, tm = ~g.own & g.checkmask & xm;
     const u64 gd = fr | (pp & diag_mask(kq)), ga = fr | (pp & anti_mask(kq));
-    t[SW_DIAG + 0] = ray_fill_att<7, false>(ga, empty, ~FILE_A) & tm;
-    t[SW_DIAG + 1] = ray_fill_att<9, false>(gd, empty, ~FILE_H) & tm;
-    t[SW_DIAG + 2] = ray_fill_att<9, true>(gd, empty, ~FILE_A) & tm;
-    t[SW_DIAG + 3] = ray_fill_att<7, true>(ga, empty, ~FILE_H) & tm;
+    t[SW_DIAG + 0] = ray_fill_to<7, false>(ga, empty, ~FILE_A, tm);
+    t[SW_DIAG + 1] = ray_fill_to<9, false>(gd, empty, ~FILE_H, tm);
+    t[SW_DIAG + 2] = ray_fill_to<9, true>(gd, empty, ~FILE_A, tm);
+    t[SW_DIAG + 3] = ray_fill_to<7, true>(ga, empty, ~FILE_H, tm);
 }
 // the diagonal sets SW_DIAG + lo .. SW_DIAG + hi - 1 only (the paired driver splits them
 // between its two waves)
@@ -945,21 +975,21 @@ GC_HD void sw_diag_part(const Pos& s, const Gen& g, u64* t, u64 xm = ~0ull) {
     const u64 S = (s.b | s.q) & g.own, fr = S & ~g.pinned, pp = S & g.pinned;
     const u64 empty = ~g.occ, tm = ~g.own & g.checkmask & xm;
     const u64 gd = fr | (pp & diag_mask(kq)), ga = fr | (pp & anti_mask(kq));
-    if (lo <= 0 && 0 < hi) t[SW_DIAG + 0] = ray_fill_att<7, false>(ga, empty, ~FILE_A) & tm;
-    if (lo <= 1 && 1 < hi) t[SW_DIAG + 1] = ray_fill_att<9, false>(gd, empty, ~FILE_H) & tm;
-    if (lo <= 2 && 2 < hi) t[SW_DIAG + 2] = ray_fill_att<9, true>(gd, empty, ~FILE_A) & tm;
-    if (lo <= 3 && 3 < hi) t[SW_DIAG + 3] = ray_fill_att<7, true>(ga, empty, ~FILE_H) & tm;
+    if (lo <= 0 && 0 < hi) t[SW_DIAG + 0] = ray_fill_to<7, false>(ga, empty, ~FILE_A, tm);
+    if (lo <= 1 && 1 < hi) t[SW_DIAG + 1] = ray_fill_to<9, false>(gd, empty, ~FILE_H, tm);
+    if (lo <= 2 && 2 < hi) t[SW_DIAG + 2] = ray_fill_to<9, true>(gd, empty, ~FILE_A, tm);
+    if (lo <= 3 && 3 < hi) t[SW_DIAG + 3] = ray_fill_to<7, true>(ga, empty, ~FILE_H, tm);
 }
 GC_HD void sw_kings(const Pos& s, const Gen& g, u64* t, u64 xm = ~0ull) {
     const u64 K = s.k & g.own, ok = ~g.own & ~g.enemy_att & xm;
     t[SW_K + 0] = (K >> 8) & ok;              // target = origin - 8
     t[SW_K + 1] = (K << 8) & ok;              // + 8
-    t[SW_K + 2] = ((K >> 1) & ~FILE_H) & ok;  // - 1
-    t[SW_K + 3] = ((K << 1) & ~FILE_A) & ok;  // + 1
-    t[SW_K + 4] = ((K >> 9) & ~FILE_H) & ok;  // - 9
-    t[SW_K + 5] = ((K >> 7) & ~FILE_A) & ok;  // - 7
-    t[SW_K + 6] = ((K << 7) & ~FILE_H) & ok;  // + 7
-    t[SW_K + 7] = ((K << 9) & ~FILE_A) & ok;  // + 9
+    t[SW_K + 2] = and3(K >> 1, ~FILE_H, ok);  // - 1
+    t[SW_K + 3] = and3(K << 1, ~FILE_A, ok);  // + 1
+    t[SW_K + 4] = and3(K >> 9, ~FILE_H, ok);  // - 9
+    t[SW_K + 5] = and3(K >> 7, ~FILE_A, ok);  // - 7
+    t[SW_K + 6] = and3(K << 7, ~FILE_H, ok);  // + 7
+    t[SW_K + 7] = and3(K << 9, ~FILE_A, ok);  // + 9
 }
 // all sets of a position whose Gen is complete (gen_init); returns the move count
 GC_HD int sw_gen(const Pos& s, const Gen& g, u64* t) {
@@ -979,7 +1009,7 @@ GC_HD int sw_gen(const Pos& s, const Gen& g, u64* t) {
 // (rare) and the kings one at a time, as gen_moves.  Any number of pieces (no slots).
 template <int SH, bool LEFT>
 GC_HD int ray_count(u64 gen, u64 empty, u64 wrap, u64 tmask) {
-    return popc(ray_fill_att<SH, LEFT>(gen, empty, wrap) & tmask);
+    return popc(ray_fill_to<SH, LEFT>(gen, empty, wrap, tmask));
 }
 // Pinned pieces need no loop either (the set-wise generation below, sw_*): a pinned slider
 // fills only along its pin line -- its ray there ends at its king and at the pinner -- and a
@@ -1036,14 +1066,14 @@ GC_HD int count_moves(const Pos& s, const Gen& g) {
 template <int SH, bool LEFT>
 GC_HD void ray_fill_pair(u64 ge, u64 go, u64 empty, u64 wrap, u64& ae, u64& ao) {
     u64 pro = empty & wrap;
-    ge |= pro & sh<SH, LEFT>(ge);
-    go |= pro & sh<SH, LEFT>(go);
+    ge = and_or(pro, sh<SH, LEFT>(ge), ge);
+    go = and_or(pro, sh<SH, LEFT>(go), go);
     pro &= sh<SH, LEFT>(pro);
-    ge |= pro & sh<2 * SH, LEFT>(ge);
-    go |= pro & sh<2 * SH, LEFT>(go);
+    ge = and_or(pro, sh<2 * SH, LEFT>(ge), ge);
+    go = and_or(pro, sh<2 * SH, LEFT>(go), go);
     pro &= sh<2 * SH, LEFT>(pro);
-    ge |= pro & sh<4 * SH, LEFT>(ge);
-    go |= pro & sh<4 * SH, LEFT>(go);
+    ge = and_or(pro, sh<4 * SH, LEFT>(ge), ge);
+    go = and_or(pro, sh<4 * SH, LEFT>(go), go);
     ae = sh<SH, LEFT>(ge) & wrap;
     ao = sh<SH, LEFT>(go) & wrap;
 }

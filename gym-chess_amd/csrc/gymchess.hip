@@ -1694,8 +1694,9 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
     }
     rt0 = __builtin_amdgcn_s_memrealtime();
 #endif
-    // one loop per role (RoleC): each wave runs only its own role's code
-    auto plies_loop = [&](auto R) {
+    // one loop per role (RoleC): each wave runs only its own role's code; and one with the
+    // per-board stats (gc_env_rollout), one without (the device form: no counters per ply)
+    auto plies_loop = [&](auto R, auto ST) {
         for (int p = 0; p < plies; p++) {
             int played = a;
             o = pair_step<OPP, true, FIDE>(Ls, L, C, R, l, i, live, rp, s, a, d, h, nst);
@@ -1704,7 +1705,8 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
 #endif
             if (R) {  // W1: the ply's outputs (trace, stats) and the window write
                 if (trace && live) trace[(size_t)p * nn + i] = trace_word(played == A_NONE ? -1 : played, o);
-                if (played == A_NONE) {
+                if (!ST) {
+                } else if (played == A_NONE) {
                     e_nomove++;
                 } else {
                     steps++;
@@ -1756,7 +1758,7 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
                 io.reward[i] = o.reward;
                 io.done[i] = (uint8_t)o.done;
                 io.reason[i] = (uint8_t)o.reason;
-                if (stats) {
+                if (ST) {
                     uint64_t* so = stats + 8 * (size_t)i;
                     so[0] += steps; so[1] += rsum;
                     so[2 + R_MATE] += e_mate; so[2 + R_REPETITION] += e_rep; so[2 + R_MOVE_CAP] += e_cap;
@@ -1766,10 +1768,11 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
         }
     };
 #ifdef GC_ROLE_RUNTIME  // A/B: one loop for both roles
-    plies_loop(role);
+    plies_loop(role, stats != nullptr);
 #else
-    if (role == 0) plies_loop(RoleC<0>{});
-    else plies_loop(RoleC<1>{});
+    if (role == 0) plies_loop(RoleC<0>{}, std::false_type{});  // W0 keeps no stats
+    else if (stats) plies_loop(RoleC<1>{}, std::true_type{});
+    else plies_loop(RoleC<1>{}, std::false_type{});
 #endif
 }
 
