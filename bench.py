@@ -477,10 +477,16 @@ def main():
         env = BatchedChessEnv(n, device=rp.device, seed=rp.board_seed(args.seed))
         if args.settle > 0:  # into steady state: mid/late-game boards, resets, terminals
             env.rollout(args.settle)
-        tb = env.trace_buffer(max(args.steps, args.warmup, 1))
-        env.rollout_device(args.warmup, tb)  # the W untimed warmup steps (also loads the kernel)
+        tb = env.trace_buffer(max(args.steps, 1))
+        tbw = env.trace_buffer(max(args.warmup, 1))
+        s0, w0 = int(env.outputs()["nsteps"].sum()), env.window_sum()
+        # the W untimed warmup steps through the timed region's own call, and nothing after them:
+        # the env's counters are read before the warmup, and the timed steps are counted from the
+        # trace (a D2H read of the counters between warmup and timed region left the region ~10 us
+        # longer: tools/region_probe.py vs bench)
+        env.rollout_device(args.warmup, tbw, events=(0, 1))
         env.synchronize()
-        return env, tb, int(env.outputs()["nsteps"].sum()), env.window_sum()
+        return env, tb, tbw, s0, w0
 
     ctx = rep.run(setup)
     envs = [c[0] for c in ctx]
@@ -497,12 +503,21 @@ def main():
     kern_ms = [e.elapsed_ms(0, 1) for e in envs]
     s1 = [int(e.outputs()["nsteps"].sum()) for e in envs]
     w1 = [e.window_sum() for e in envs]
-    steps_all = rep.sum(sum(b - c[2] for c, b in zip(ctx, s1)))
+    # env.step() calls in the timed region, from its per-step trace (action -1: the driver's
+    # no-move reset, not a step), cross-checked against the env's step counters, which also
+    # count the warmup's steps
+    steps_local = 0
+    for (env, tb, tbw, s0, _), b in zip(ctx, s1):
+        tr = tb.fetch(args.steps)
+        timed = int((tr["action"] != -1).sum())
+        warm = int((tbw.fetch(args.warmup)["action"] != -1).sum()) if args.warmup > 0 else 0
+        assert b - s0 == timed + warm, f"step counters {b - s0} != trace {timed} + {warm}"
+        assert (tr["done"][-1] <= 1).all() and (tr["reason"][-1] <= 10).all()  # the last ply was written
+        steps_local += timed
+        del tr
+    steps_all = rep.sum(steps_local)
     value = steps_all / dt_max
-    mean_window = sum(c[3] + w for c, w in zip(ctx, w1)) / (2.0 * n * len(envs))
-    # the timed trace must hold every step of every board (a spot check of the last ply)
-    tr_last = ctx[0][1].fetch(args.steps)
-    assert (tr_last["done"][-1] <= 1).all() and (tr_last["reason"][-1] <= 10).all()
+    mean_window = sum(c[4] + w for c, w in zip(ctx, w1)) / (2.0 * n * len(envs))
 
     # roofline of the dominant kernel (k_env_rollout2, the fused K-step launch), per launch,
     # from HIP events on the env's stream (the stream it is launched on; mean over this
@@ -526,8 +541,9 @@ def main():
     extra = {}
     if args.launched_steps > 0:
         extra["launched_step"] = launched_leg(args, rep, envs, n)
-    for e, tb in ((c[0], c[1]) for c in ctx):
+    for e, tb, tbw in ((c[0], c[1], c[2]) for c in ctx):
         tb.close()
+        tbw.close()
         e.close()
     if args.api_steps > 0:
         extra["api_step"] = api_step_leg(args, rep, n)

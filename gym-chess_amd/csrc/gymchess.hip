@@ -912,6 +912,7 @@ struct PairNoop {
 // branches, and nothing the other role alone needs (the stats on W0, the pick on W1).
 template <int R>
 struct RoleC {
+    static constexpr int value = R;
     __device__ constexpr operator int() const { return R; }
 };
 
@@ -1180,7 +1181,8 @@ __device__ __forceinline__ Pos pair_settle(const PairHalf& H, bool white) {
 // The self-play pick from the move sets in LDS (pair_half with SW): the set holding rank k by
 // the byte counts (gc_core.h sw_locate), then that one set from LDS; more moves than byte sums
 // hold (never in play) take a rolled scan over LDS.  k < tot.
-__device__ __forceinline__ int sw_pick_lds(const PairLds& L, int l, const Gen& g, const u64* cw, int tot, int k) {
+template <class LdsT>
+__device__ __forceinline__ int sw_pick_lds(const LdsT& L, int l, const Gen& g, const u64* cw, int tot, int k) {
     const int normal = tot - popc(g.castles);
     int r = k, j;
     if (tot < 256) {
@@ -1773,6 +1775,393 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
     if (role == 0) plies_loop(RoleC<0>{}, std::false_type{});  // W0 keeps no stats
     else if (stats) plies_loop(RoleC<1>{}, std::true_type{});
     else plies_loop(RoleC<1>{}, std::false_type{});
+#endif
+}
+
+// ----------------------------------------------------------------------------- quad step
+// k_env_rollout4: the headline rollout (opponent "none", reference rules, move-set order) with
+// FOUR waves per 64 boards.  With two (k_env_rollout2) a SIMD holds 2 waves -- all 65 536
+// boards give -- and a wave's ply is one long dependency chain: a lone wave runs its ply in
+// 3.75 us, two share the SIMD at 6.0 us each (tools/pstamp_probe.py), VALU issue ~35 % busy.
+// The ply's parallel parts -- the enemy map's three parts, the own slider sets' two halves --
+// go to their own waves, so each wave's chain is shorter and a SIMD holds four of them:
+//
+//   phase 0   Q0: applies the action (post-move board to LDS)
+//             Q1: the 3-fold probe of the pre-move board, the Philox word, the reset table read
+//   phase 1   Q0: checkers, check mask, pins                   Q1: enemy leaper attacks, the
+//             Q2: enemy orthogonal slider attacks                   mover's own check flag
+//             Q3: enemy diagonal slider attacks
+//   phase 2   Q0: castles, pawn / knight / king sets            Q1: the 3-fold commit
+//             Q2: the own rook/queen direction sets            Q3: the bishop/queen ones
+//   phase 3   Q0: the outcome and the pick of the next action   Q1: the outcome, the stores
+//
+// Q0 and Q1 carry the board's state between plies; Q2 and Q3 are stateless (the post-move
+// board and the pins come through LDS) and compute their sets unconditionally -- ignored,
+// like the totals, when no generation is due.  Same decisions in the same order as
+// pair_ply (and so as k_env_step<true, false> and the oracle): tests/test_gpu_parity.py and
+// tests/test_full_size.py run the fused rollouts against the oracle and the launched kernel.
+#define QUAD_BOARDS 64
+#ifndef QUADS_WG
+#define QUADS_WG 2  // two quads per workgroup; the second's roles rotated by 2 so that every SIMD
+                    // hosts a state-carrying and a stateless role of each workgroup
+#endif
+struct QuadLds {
+    u64 sets[SW_SETS][QUAD_BOARDS];  // the next side's move sets (Q0: pawns / knights / kings, Q2, Q3)
+    u64 ns[NBB][QUAD_BOARDS];        // Q0 -> all: the post-move board (phase 0)
+    u32 nmeta[QUAD_BOARDS];
+    int32_t mr[QUAD_BOARDS];         //           its capture reward
+    u32 irrev[QUAD_BOARDS];          //           irreversible move
+    u64 pin3[3][QUAD_BOARDS];        // Q0 -> Q2, Q3: check mask, pinned, pin rays
+    u32 f0[QUAD_BOARDS];             // Q0 -> Q1: the side to move is in check
+    u64 enemy[3][QUAD_BOARDS];       // Q1 / Q2 / Q3 -> Q0: the enemy map's leaper, orthogonal, diagonal parts
+    u32 f1[QUAD_BOARDS];             // Q1 -> Q0: the mover is in check after its move
+    u64 cwx[2][QUAD_BOARDS];         // Q2 / Q3 -> Q0: their sets' byte counts (words 1 and 2)
+    u32 part[4][QUAD_BOARDS];        // partial move totals (Q0's holds the castles)
+    u32 rep[QUAD_BOARDS];            // Q1 -> Q0: 3-fold count | window length << 8
+    u32 x0[QUAD_BOARDS];             // Q1 -> Q0: the Philox word of the next draw
+    u32 ra[QUAD_BOARDS];             // Q1 -> Q0: the start-position table pick
+    u32 act[QUAD_BOARDS];            // Q0 -> Q1: the next action
+    u32 draw[QUAD_BOARDS];           // Q0 -> Q1: the draw counter
+    Pos rp;                          // the reset position (read at a reset: no registers held for it)
+};
+// one set of the next side's moves into LDS, its count into the packed byte counts and the total
+struct QuadSets {
+    QuadLds& L;
+    int l;
+    u64 cw[4];
+    int part;
+    __device__ void put(int j, u64 t) {
+        L.sets[j][l] = t;
+        const int c = popc(t);
+        cw[j >> 3] |= (u64)c << (8 * (j & 7));
+        part += c;
+    }
+    template <int LO, int HI>
+    __device__ void put_all(const u64* t) {
+#pragma unroll
+        for (int j = LO; j < HI; j++) put(j, t[j - LO]);
+    }
+};
+
+// One ply of board i for role R of its quad (RoleC<0..3>).  Q0 / Q1: in/out as pair_ply (s, a,
+// d, h, nst); both return the same s and a.  Q2 / Q3: s, a, d, h, nst unused.
+template <int R>
+__device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l, int i, bool live, Pos& s, int& a,
+                                            u32& d, DevHist& h, u32& nst) {
+    constexpr bool CARRY = R < 2;  // Q0 / Q1 hold the state
+    const bool none = a == A_NONE;                           // empty list: driver reset
+    const bool done0 = (s.meta & M_DONE) != 0;               // chess_v2.py:245-251
+    const bool cap = mc_of(s.meta) > MOVES_MAX;              // 252-258
+    const bool mv = live && !none && !done0 && !cap;         // env_ply runs
+    const bool white = (s.meta & M_WHITE) != 0;
+    u32 x0 = 0;
+    uint16_t ra = (uint16_t)A_NONE;
+    int mr = 0;
+    bool irrev = false;
+    Pos ns;
+    RepProbe pr;
+    // ---- phase 0
+    if (R == 0) {
+        ns = s;
+        ns.meta = (ns.meta & ~(u32)M_RIGHTS) | eff_rights(s);  // State::new
+        if (mv) apply_legal(ns, white, a, &mr, &irrev);
+        L.ns[0][l] = ns.k; L.ns[1][l] = ns.q; L.ns[2][l] = ns.r; L.ns[3][l] = ns.b;
+        L.ns[4][l] = ns.n; L.ns[5][l] = ns.p; L.ns[6][l] = ns.w;
+        L.nmeta[l] = ns.meta;
+        L.mr[l] = mr;
+        L.irrev[l] = irrev ? 1u : 0u;
+    } else if (R == 1) {
+        if (mv) rep_prefetch(h, s, pr);
+        x0 = philox_x0(C.seed, (u32)i, d);  // the next draw (independent of the position)
+        if (C.rtable) ra = C.racts[scale_rank(x0, C.rtotal)];
+        L.x0[l] = x0;
+    }
+    pair_barrier();
+    // ---- phase 1
+    Gen g;
+    bool my_chk = false;
+    if (R != 0) {
+        ns.k = L.ns[0][l]; ns.q = L.ns[1][l]; ns.r = L.ns[2][l]; ns.b = L.ns[3][l];
+        ns.n = L.ns[4][l]; ns.p = L.ns[5][l]; ns.w = L.ns[6][l];
+        ns.meta = L.nmeta[l];
+    }
+    if (R == 1) {
+        mr = L.mr[l];
+        irrev = L.irrev[l] != 0;
+    }
+    gen_base(ns, g);
+    if (R == 0) {
+        gen_pins(ns, g);
+        L.pin3[0][l] = g.checkmask;
+        L.pin3[1][l] = g.pinned;
+        L.pin3[2][l] = g.pinrays;
+        L.f0[l] = g.in_check ? 1u : 0u;
+    } else if (R == 1) {
+        L.enemy[0][l] = g.ks >= 0 ? side_attacks_leapers(ns, !g.white) : 0ull;
+        my_chk = mv && mover_checked(s, ns, white, a);
+        L.f1[l] = my_chk ? 1u : 0u;
+    } else if (R == 2) {
+        L.enemy[1][l] = g.ks >= 0 ? side_attacks_orth(ns, !g.white) : 0ull;
+    } else {
+        L.enemy[2][l] = g.ks >= 0 ? side_attacks_diag(ns, !g.white) : 0ull;
+    }
+    pair_barrier();
+    // ---- phase 2
+    if (R == 0) {
+        g.enemy_att = L.enemy[0][l] | L.enemy[1][l] | L.enemy[2][l];
+        gen_castles(ns, g);  // lib.rs:578-610 with the whole enemy map
+        my_chk = L.f1[l] != 0;
+    } else if (R == 1) {
+        g.in_check = L.f0[l] != 0;
+    } else {
+        g.checkmask = L.pin3[0][l];
+        g.pinned = L.pin3[1][l];
+        g.pinrays = L.pin3[2][l];
+    }
+    const bool opp_chk = g.in_check;
+    const bool both = opp_chk && my_chk;  // lib.rs:1442-1446
+    const bool gen = mv && !both;
+    QuadSets Q{L, l, {0, 0, 0, 0}, 0};  // sets go to LDS as they are made: no 28-set array held
+    int c = 0;
+    u32 hl = hl_of(s.meta);
+    if (R == 0) {  // pawn, knight and king sets; castles counted here
+        if (gen) {
+            u64 T[SW_SETS];
+            sw_pawns(ns, g, T);
+            Q.put_all<SW_P1, SW_N>(T + SW_P1);
+            sw_knights(ns, g, T);
+            Q.put_all<SW_N, SW_ORTH>(T + SW_N);
+            sw_kings(ns, g, T);
+            Q.put_all<SW_K, SW_SETS>(T + SW_K);
+            Q.part += popc(g.castles);
+        }
+    } else if (R == 1) {
+        if (mv && !both) {
+            pin(pr.e0.hdr); pin(pr.e0.k); pin(pr.e0.q); pin(pr.e0.r);
+            pin(pr.e0.b); pin(pr.e0.n); pin(pr.e0.p); pin(pr.e0.w);
+            c = rep_commit(h, s, pr, hl, irrev);  // table write deferred to h.commit()
+        }
+        L.rep[l] = (u32)c | (hl << 8);
+        L.ra[l] = ra;
+    } else if (R == 2) {  // unconditional: ignored unless generation is due
+        u64 T[SW_SETS];
+        sw_orth(ns, g, T);
+        Q.put_all<SW_ORTH, SW_DIAG>(T + SW_ORTH);
+        L.part[2][l] = (u32)Q.part;
+        L.cwx[0][l] = Q.cw[1];
+    } else {
+        u64 T[SW_SETS];
+        sw_diag(ns, g, T);
+        Q.put_all<SW_DIAG, SW_K>(T + SW_DIAG);
+        L.part[3][l] = (u32)Q.part;
+        L.cwx[1][l] = Q.cw[2];
+    }
+    if (R == 0) L.part[0][l] = (u32)Q.part;
+    pair_barrier();
+    // ---- phase 3: the outcome (Q0 and Q1, identical arithmetic), Q0's pick
+    StepOut o = {0, 0, R_NONE, 0};
+    if constexpr (CARRY) {
+        const int total = gen ? (R == 0 ? Q.part : (int)L.part[0][l]) + (int)L.part[2][l] + (int)L.part[3][l] : 0;
+        u64* const cw = Q.cw;
+        if (R == 0) {
+            if (gen) {
+                cw[1] |= L.cwx[0][l];
+                cw[2] |= L.cwx[1][l];
+            }
+            const u32 rpk = L.rep[l];
+            c = (int)(rpk & 0xFFu);
+            hl = rpk >> 8;
+            x0 = L.x0[l];
+            ra = (uint16_t)L.ra[l];
+        } else {
+            h.commit();  // the window write, issued before the outcome
+        }
+        int set_act = A_NONE;
+        if (R == 0 && total > 0) set_act = sw_pick_lds(L, l, g, cw, total, (int)scale_rank(x0, (u32)total));
+        bool have = false;
+        if (none) {
+            o.reason = R_NO_MOVES;
+        } else {
+            nst += 1;
+            if (done0) { o.done = 1; o.reason = R_DONE_ALREADY; }
+            else if (cap) { o.done = 1; o.reason = R_MOVE_CAP; }
+            else if (both) { o.done = 1; o.reason = R_BOTH_CHECKED; }
+            else {
+                const u32 chk = white ? ((my_chk ? M_WCHK : 0u) | (opp_chk ? M_BCHK : 0u))
+                                      : ((opp_chk ? M_WCHK : 0u) | (my_chk ? M_BCHK : 0u));
+                s = ns;
+                s.meta = with_hl((ns.meta & ~(u32)(M_WCHK | M_BCHK | M_DONE)) | chk | ((c >= 3 || c == 0) ? M_DONE : 0u), hl);
+                o.reward = -10 + mr;
+                o.moved = 1;
+                if (c >= 3) { o.done = 1; o.reason = R_REPETITION; }  // chess_v2.py:404-407
+                if (c == 0) { o.done = 1; o.reason = R_WINDOW_FULL; }
+                if (total == 0 && opp_chk) {  // 270-272
+                    s.meta |= M_DONE;
+                    o.done = 1;
+                    o.reward += 100;
+                    o.reason = R_MATE;
+                }
+                if (!o.done && !white) s.meta += (1u << M_MC_SHIFT);  // 291-292
+                have = true;
+            }
+            if (o.done) have = false;
+        }
+        if (!have) {  // reset (chess_v2.py:183-206), also the no-move driver reset
+            s = L.rp;
+            h.bump_gen();
+        }
+        if (R == 0) {
+            uint16_t act = (uint16_t)set_act;
+            int tot = total;
+            if (!have && C.rtable) {  // the start position's table
+                act = ra;
+                tot = (int)C.rtotal;
+            } else if (!have) {  // the start position without a table (rare): generated, through LDS
+                gen_init(s, g);
+                QuadSets Z{L, l, {0, 0, 0, 0}, 0};
+                u64 T[SW_SETS];
+                sw_pawns(s, g, T);
+                Z.put_all<SW_P1, SW_N>(T + SW_P1);
+                sw_knights(s, g, T);
+                Z.put_all<SW_N, SW_ORTH>(T + SW_N);
+                sw_orth(s, g, T);
+                Z.put_all<SW_ORTH, SW_DIAG>(T + SW_ORTH);
+                sw_diag(s, g, T);
+                Z.put_all<SW_DIAG, SW_K>(T + SW_DIAG);
+                sw_kings(s, g, T);
+                Z.put_all<SW_K, SW_SETS>(T + SW_K);
+                tot = Z.part + popc(g.castles);
+                act = (uint16_t)(tot > 0 ? sw_pick_lds(L, l, g, Z.cw, tot, (int)scale_rank(x0, (u32)tot)) : A_NONE);
+            }
+            a = act;
+            d += tot > 0 ? 1u : 0u;
+            L.act[l] = act;
+            L.draw[l] = d;
+        }
+    }
+    pair_barrier();  // the next action and draw counter to Q1; LDS free for the next ply
+    if (R == 1) {
+        a = (int)L.act[l];
+        d = L.draw[l];
+    }
+    return o;
+}
+
+// The quads' LDS (static, shared by the role functions below: a direct reference keeps every
+// access a ds_ instruction)
+__shared__ QuadLds g_quad_lds[QUADS_WG];
+
+// One role's whole launch (its K plies and its stores), NOT inlined into the kernel: the four
+// roles' register needs are allocated apart (each fits 128 VGPRs alone -- Q0 93, Q1 117, Q2 31,
+// Q3 27 -- inlined together under one switch they spill), and the kernel takes their maximum.
+// (a function's arguments arrive in VGPRs: the launch-uniform ones go back to SGPRs first)
+__device__ __forceinline__ u64 uni64(u64 v) {
+    return (u64)(u32)__builtin_amdgcn_readfirstlane((int)(u32)v) |
+           ((u64)(u32)__builtin_amdgcn_readfirstlane((int)(u32)(v >> 32)) << 32);
+}
+template <class T>
+__device__ __forceinline__ T* uni_ptr(T* p) { return reinterpret_cast<T*>(uni64(reinterpret_cast<u64>(p))); }
+template <int RR, bool ST>
+__device__ __noinline__ void quad_run(uint8_t* __restrict__ slab, int nn, uint64_t seed, u64* __restrict__ htab,
+                                      const uint16_t* __restrict__ racts, const EnvDev::InitCache* __restrict__ icd,
+                                      u32 rinfo, int plies, uint64_t* __restrict__ stats, u64* __restrict__ trace,
+                                      int qw, int l, int i) {
+    slab = uni_ptr(slab); htab = uni_ptr(htab); racts = uni_ptr(racts); icd = uni_ptr(icd);
+    stats = uni_ptr(stats); trace = uni_ptr(trace);
+    nn = __builtin_amdgcn_readfirstlane(nn);
+    seed = uni64(seed);
+    rinfo = (u32)__builtin_amdgcn_readfirstlane((int)rinfo);
+    plies = __builtin_amdgcn_readfirstlane(plies);
+    qw = __builtin_amdgcn_readfirstlane(qw);
+    QuadLds& L = g_quad_lds[qw];
+    const bool live = i < nn;
+    const int ii = live ? i : nn - 1;  // dead lanes read a valid board, store nothing
+    const PairIO in_io(slab, nn);
+    const PairCtx C = {seed, htab, in_io.hgen, racts, icd, (rinfo >> 16) != 0, rinfo & 0xFFFFu};
+    Pos s{};
+    u32 ua = 0, g0 = 0, nst = 0, d = 0;
+    if (RR < 2) {
+        s = in_io.load(ii);
+        ua = in_io.act[ii];
+        g0 = in_io.hgen[ii];
+        nst = in_io.nsteps[ii];
+        d = in_io.draw[ii];
+        pin(s); pin(ua); pin(g0); pin(nst); pin(d);
+    }
+    if (RR == 0 && l == 0) L.rp = icd->pos;  // read after ply 0's first barrier
+    int a = (int)ua;
+    DevHist h = DevHist{htab, in_io.hgen, g0, ii, HTAB_BITS};
+    uint64_t steps = 0, rsum = 0;
+    u32 e_mate = 0, e_rep = 0, e_cap = 0, e_nomove = 0, e_err = 0;
+    StepOut o = {0, 0, R_NONE, 0};
+    for (int p = 0; p < plies; p++) {
+        const int played = a;
+        o = quad_ply<RR>(L, C, l, i, live, s, a, d, h, nst);
+        if (RR == 1) {  // the ply's outputs (trace, stats) and the window write
+            if (trace && live) trace[(size_t)p * nn + i] = trace_word(played == A_NONE ? -1 : played, o);
+            if (!ST) {
+            } else if (played == A_NONE) {
+                e_nomove++;
+            } else {
+                steps++;
+                rsum += (uint64_t)(int64_t)o.reward;
+                if (o.done) {
+                    e_mate += o.reason == R_MATE || o.reason == R_MATED;
+                    e_rep += o.reason == R_REPETITION;
+                    e_cap += o.reason == R_MOVE_CAP;
+                    e_err += o.reason == R_BOTH_CHECKED || o.reason == R_WINDOW_FULL;
+                    e_nomove += o.reason == R_OPP_NO_MOVE;
+                }
+            }
+            h.commit();  // this ply's window write lands before the next ply's probe
+        }
+    }
+    if (!live || RR >= 2) return;
+    const PairIO io = store_io(slab, nn);
+    if (RR == 0) {
+        io.act[i] = (uint16_t)a;
+        io.draw[i] = d;
+    } else {
+        io.store(i, s);
+        h.flush(g0);
+        io.nsteps[i] = nst;
+        io.reward[i] = o.reward;
+        io.done[i] = (uint8_t)o.done;
+        io.reason[i] = (uint8_t)o.reason;
+        if (ST) {
+            uint64_t* so = stats + 8 * (size_t)i;
+            so[0] += steps; so[1] += rsum;
+            so[2 + R_MATE] += e_mate; so[2 + R_REPETITION] += e_rep; so[2 + R_MOVE_CAP] += e_cap;
+            so[2 + R_NO_MOVES] += e_nomove; so[2 + R_BOTH_CHECKED] += e_err;
+        }
+    }
+}
+
+// The fused K-ply rollout on quads (k_env_rollout2's contract: same arguments, state, trace
+// and stats).  Q0 writes the next action and draw counter, Q1 the rest, as W0 / W1 there.
+__global__ void __launch_bounds__(4 * QUAD_BOARDS * QUADS_WG) __attribute__((amdgpu_waves_per_eu(4)))
+    k_env_rollout4(uint8_t* __restrict__ slab, int nn, uint64_t seed, u64* __restrict__ htab,
+                   const uint16_t* __restrict__ racts, const EnvDev::InitCache* __restrict__ icd, u32 rinfo,
+                   uint64_t* __restrict__ stats, u64* __restrict__ trace) {
+    const int plies = (int)(rinfo >> 18);
+    rinfo &= 0x1FFFFu;
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int qw = wv >> 2;  // the quad of this wave within the workgroup
+    const int role = (wv & 3) ^ ((qw & 1) << 1);
+    const int l = threadIdx.x & (QUAD_BOARDS - 1);
+    const int i = (blockIdx.x * QUADS_WG + qw) * QUAD_BOARDS + l;
+#ifdef GC_QUAD_ONLY  // diagnostic builds: one role's register needs
+    quad_run<GC_QUAD_ONLY, false>(slab, nn, seed, htab, racts, icd, rinfo, plies, stats, trace, qw, l, i);
+#else
+    switch (role) {
+        case 0: quad_run<0, false>(slab, nn, seed, htab, racts, icd, rinfo, plies, stats, trace, qw, l, i); break;
+        case 1:
+            if (stats) quad_run<1, true>(slab, nn, seed, htab, racts, icd, rinfo, plies, stats, trace, qw, l, i);
+            else quad_run<1, false>(slab, nn, seed, htab, racts, icd, rinfo, plies, stats, trace, qw, l, i);
+            break;
+        case 2: quad_run<2, false>(slab, nn, seed, htab, racts, icd, rinfo, plies, stats, trace, qw, l, i); break;
+        default: quad_run<3, false>(slab, nn, seed, htab, racts, icd, rinfo, plies, stats, trace, qw, l, i); break;
+    }
 #endif
 }
 
@@ -3821,7 +4210,12 @@ static int issue_rollout(gc_env* e, int n_plies, uint64_t* d_trace, bool stats) 
         const int k = n_plies - p0 < ROLLOUT_MAX_PLIES ? n_plies - p0 : ROLLOUT_MAX_PLIES;
         u64* tr = d_trace ? reinterpret_cast<u64*>(d_trace) + (size_t)p0 * e->n : nullptr;
         const u32 ri = r.rinfo | ((u32)k << 18);
-        if (pair) {
+        static const bool no_quad = getenv("GC_NO_QUAD") != nullptr;  // A/B: the paired kernel
+        if (pair && !e->rules && pair_opp(e) == 0 && !no_quad) {
+            const int qg = (e->n + QUAD_BOARDS * QUADS_WG - 1) / (QUAD_BOARDS * QUADS_WG);
+            k_env_rollout4<<<qg, 4 * QUAD_BOARDS * QUADS_WG, 0, e->stream>>>(e->slab, d.n, d.seed, d.htab, sw_table(r),
+                                                                             r.icd, ri, st, tr);
+        } else if (pair) {
             switch (e->rules ? 3 : pair_opp(e)) {
                 case 3: k_env_rollout2<true><<<grid, bs, 0, e->stream>>>(e->slab, d.n, d.seed, d.htab, r.racts, r.icd, ri, st, tr); break;
                 case 0: k_env_rollout2<false><<<grid, bs, 0, e->stream>>>(e->slab, d.n, d.seed, d.htab, sw_table(r), r.icd, ri, st, tr); break;

@@ -1,0 +1,9 @@
+#!/bin/bash
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail -20 gpurun_out/smoke.log; exit 3; }
+tail -1 gpurun_out/smoke.log
+M=gym-chess_amd/gym_chess_amd/libgymchess.so
+PYTEST=1 REPS=2 LIBS="$M@GC_NO_QUAD=1 $M" bash tools/r3_ab.sh
+bash tools/r3_s9.sh
