@@ -9,7 +9,7 @@ bookkeeping (next_state, update_state, 3-fold on the pre-move board, move cap, m
 the next side's legal move set, the Philox pick of the next action, reset of finished
 boards, and the step's outputs (action played, reward, done, reason) of every board written
 to a per-ply trace in HBM.  The K timed steps are ONE launch of the fused rollout kernel
-k_env_rollout2 (gc_env_rollout_device: the state stays in registers between plies; every
+k_env_rollout4 (four waves per 64 boards; gc_env_rollout_device: the state stays in registers between plies; every
 ply's window probe / commit and outputs go through HBM).  State, repetition windows and
 outputs stay in HBM; nothing crosses PCIe in the timed region.  The launched form (one
 kernel launch per ply, k_env_step2 over two board-range streams) is timed beside it as
@@ -44,6 +44,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip-level parameters (8.0 TB/s spe
 # capture) measured over the timed steps
 def alg_bytes_fused(h):
     return 173.0 + 8.0 * h
+
+
+# the fused rollout's kernel by waves per 64 boards (gc_env_rollout_waves)
+ROLLOUT_KERNEL = {4: "k_env_rollout4", 2: "k_env_rollout2<false, 0>", 1: "k_env_rollout<false>"}
 
 
 # the launched step k_env_step2 (one kernel per ply; DESIGN.md §5 byte model):
@@ -490,6 +494,7 @@ def main():
 
     ctx = rep.run(setup)
     envs = [c[0] for c in ctx]
+    rollout_kernel = ROLLOUT_KERNEL[envs[0].rollout_waves()]
 
     def step(rp):
         env, tb = ctx[rep.local.index(rp)][:2]
@@ -519,7 +524,7 @@ def main():
     value = steps_all / dt_max
     mean_window = sum(c[4] + w for c, w in zip(ctx, w1)) / (2.0 * n * len(envs))
 
-    # roofline of the dominant kernel (k_env_rollout2, the fused K-step launch), per launch,
+    # roofline of the dominant kernel (the fused K-step launch, k_env_rollout4), per launch,
     # from HIP events on the env's stream (the stream it is launched on; mean over this
     # process's replicas): SURVEY §8(d)'s 173 + 8h bytes per board per ply x N x K
     alg = alg_bytes_fused(mean_window)
@@ -580,10 +585,11 @@ def main():
                        "boards_per_gpu": n, "global_boards": n * rep.world_size,
                        "parallelism": f"replicas{rep.world_size}", "replica_mode": rep.mode,
                        "settle_plies": args.settle,
-                       "step_form": "K steps = one k_env_rollout2 launch (gc_env_rollout_device), per-step trace in HBM"},
+                       "step_form": f"K steps = one {rollout_kernel} launch (gc_env_rollout_device), "
+                                    "per-step trace in HBM"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_env_rollout2<false, 0>", "avg_launch_us": launch_s * 1e6,
+                         "kernel": rollout_kernel, "avg_launch_us": launch_s * 1e6,
                          "plies_per_launch": args.steps, "alg_bytes_per_board_ply": alg,
                          "alg_bytes_rule": "SURVEY 8(d) fused rollout ply: 173 + 8h", "mean_window": mean_window,
                          "valu": valu, "pmc_source": pmc_src},

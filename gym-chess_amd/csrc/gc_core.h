@@ -1503,6 +1503,9 @@ GC_HD void to_mailbox(const Pos& s, int8_t* b) {
 GC_HD u32 philox_x0(u64 seed, u32 board, u32 draw) {
     u32 k0 = (u32)seed, k1 = (u32)(seed >> 32);
     u32 x0 = board, x1 = draw, x2 = 0x5EEDu, x3 = 0u;
+    // straight-line: a rolled loop here made the step kernels wait for every outstanding load
+    // (the window probe in flight) at its header
+#pragma unroll
     for (int i = 0; i < 10; i++) {
         u64 p0 = (u64)0xD2511F53u * x0;
         u64 p1 = (u64)0xCD9E8D57u * x2;

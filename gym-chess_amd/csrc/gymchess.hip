@@ -1617,30 +1617,6 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
 #endif
 }
 
-// Fair share of a CU between the two workgroups it hosts (GC_FAIR).  Each SIMD runs one wave
-// of each workgroup, and the SQ issues the older wave first when both are ready: left alone,
-// the workgroup dispatched first runs ~25 % ahead of its neighbour for the whole launch, and
-// the launch ends with the neighbour's tail on a half-empty CU (tools/pstamp_probe.py: wave
-// ends bimodal, p25 5 377 / p75 6 679 us over 1 000 plies).  Feedback instead: the two
-// workgroups of a CU publish their ply counts in a per-CU pair of words; every ply each wave
-// reads its neighbour's count (issued one ply ahead of its use) and the one that is ahead
-// drops to the lowest issue priority.  A neighbour from another launch, or none, only ever
-// reads as ahead or behind: priorities matter only against co-resident waves, so a stale word
-// costs nothing.  Vector loads / stores of device memory (agent scope).
-#ifndef GC_FAIR
-#define GC_FAIR 0  // r03 A/B: fair, but slower in total (a CU's throughput is what it is: the ahead
-                   // workgroup's lead costs nothing, equal progress costs issue slots) -- 8.45 vs 8.78e9
-                   // env.steps/s at --steps 20, 11.18 vs 11.32e9 at 1 000
-#endif
-#if GC_FAIR
-__device__ u32 g_fair_claim[2048];
-__device__ u32 g_fair_prog[2048][2];
-__device__ __forceinline__ u32 fair_cu() {  // this CU in the device: xcc | se | sh | cu
-    u32 hw, xcc;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)\n\ts_getreg_b32 %1, hwreg(HW_REG_XCC_ID)" : "=s"(hw), "=s"(xcc));
-    return ((xcc & 0xF) << 7) | (((hw >> 13) & 3) << 5) | (((hw >> 12) & 1) << 4) | ((hw >> 8) & 0xF);
-}
-#endif
 
 // One ply's env.step() outputs, packed for the per-ply trace [ply][N] (one coalesced 8-B
 // store per board per ply): action played (int16; -1 = none, the driver's no-move reset),
@@ -1680,14 +1656,6 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
     uint64_t steps = 0, rsum = 0;
     u32 e_mate = 0, e_rep = 0, e_cap = 0, e_nomove = 0, e_err = 0;
     StepOut o = {0, 0, R_NONE, 0};
-#if GC_FAIR
-    // the workgroup's slot of its CU's pair: claimed by wave 0, read by every wave after the
-    // first barrier (LDS); the neighbour's count, loaded one ply ahead of its use
-    __shared__ u32 fair_slot_lds;
-    const u32 fcu = fair_cu();
-    if (threadIdx.x == 0) fair_slot_lds = atomicAdd(&g_fair_claim[fcu], 1u) & 1u;
-    u32 fslot = 2, fnb = 0;  // 2: not read yet
-#endif
 #ifdef GC_PSTAMPS
     unsigned long long rt0 = 0, rt1 = 0;  // 100 MHz wall clock: after the entry loads, after the first ply
     if (l == 0) {
@@ -1723,21 +1691,8 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
                 }
                 h.commit();  // this ply's window write lands before the next ply's probe
             }
-#if GC_FAIR
-            if (fslot == 2) fslot = fair_slot_lds;  // written before ply 0's first barrier
-            {
-                const u32 nb = __builtin_amdgcn_readfirstlane(fnb);  // the neighbour's count, read last ply
-                if (nb > (u32)p + 1) __builtin_amdgcn_s_setprio(2);  // behind: first
-                else __builtin_amdgcn_s_setprio(0);
-                if (threadIdx.x == 0) __hip_atomic_store(&g_fair_prog[fcu][fslot], (u32)p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                fnb = __hip_atomic_load(&g_fair_prog[fcu][fslot ^ 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-#endif
         }
         // the launch's end (in the role's own code: nothing of the other role's state stays live)
-#if GC_FAIR
-        __builtin_amdgcn_s_setprio(0);
-#endif
 #ifdef GC_PSTAMPS
         if (g_pst_out != nullptr && l == 0) {
             const size_t w = (size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
@@ -4186,6 +4141,18 @@ extern "C" int gc_env_paired(gc_env* e) {
     return pair_ok(e) && !one_wave ? 1 : 0;
 }
 
+static bool use_quad(const gc_env* e) {
+    static const bool no_quad = getenv("GC_NO_QUAD") != nullptr;  // A/B: the paired kernel
+    return !no_quad && !e->rules && pair_opp(e) == 0;
+}
+
+extern "C" int gc_env_rollout_waves(gc_env* e) {
+    if (!e) return fail("null env");
+    static const bool one_wave = getenv("GC_STEP1") != nullptr;
+    const bool pair = pair_ok(e) && (!one_wave || e->rules);
+    return pair ? (use_quad(e) ? 4 : 2) : 1;
+}
+
 extern "C" int gc_env_select_random(gc_env* e) {
     if (!e) return fail("null env");
     HIPCHK(hipSetDevice(e->device));
@@ -4210,8 +4177,7 @@ static int issue_rollout(gc_env* e, int n_plies, uint64_t* d_trace, bool stats) 
         const int k = n_plies - p0 < ROLLOUT_MAX_PLIES ? n_plies - p0 : ROLLOUT_MAX_PLIES;
         u64* tr = d_trace ? reinterpret_cast<u64*>(d_trace) + (size_t)p0 * e->n : nullptr;
         const u32 ri = r.rinfo | ((u32)k << 18);
-        static const bool no_quad = getenv("GC_NO_QUAD") != nullptr;  // A/B: the paired kernel
-        if (pair && !e->rules && pair_opp(e) == 0 && !no_quad) {
+        if (pair && use_quad(e)) {
             const int qg = (e->n + QUAD_BOARDS * QUADS_WG - 1) / (QUAD_BOARDS * QUADS_WG);
             k_env_rollout4<<<qg, 4 * QUAD_BOARDS * QUADS_WG, 0, e->stream>>>(e->slab, d.n, d.seed, d.htab, sw_table(r),
                                                                              r.icd, ri, st, tr);

@@ -190,6 +190,13 @@ class BatchedChessEnv:
             _lib.check(r)
         return bool(r)
 
+    def rollout_waves(self):
+        """waves per 64 boards of the fused rollout: 4 (quads), 2 (pairs) or 1 (gc_env_rollout_waves)"""
+        r = self._L.gc_env_rollout_waves(self._h)
+        if r < 0:
+            _lib.check(r)
+        return int(r)
+
     def step_random(self, n_plies=1):
         _lib.check(self._L.gc_env_step_random(self._h, int(n_plies)))
 

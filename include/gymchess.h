@@ -172,6 +172,10 @@ int gc_env_set_streams(gc_env* e, int k);
  * random opponent from a start position without a pick table, or whose opening can leave
  * both kings checked), -1 on error.  Results are the same either way. */
 int gc_env_paired(gc_env* e);
+/* waves per 64 boards of this env's fused rollout (gc_env_rollout / gc_env_rollout_device):
+ * 4 (k_env_rollout4: self-play under the reference rules, unless GC_NO_QUAD is set), 2 (the
+ * paired k_env_rollout2) or 1 (the one-wave kernels); -1 on error.  Results are the same. */
+int gc_env_rollout_waves(gc_env* e);
 /* re-pick policy actions for the current states (after set_states / external steps) */
 int gc_env_select_random(gc_env* e);
 /* Same driver fused into ONE launch of n_plies plies (state kept in registers).  Optional

@@ -19,7 +19,7 @@ step() {
 # --warmup 50), 20 of them; one counter group per pass (rocprofv3 does not split passes)
 PMCB="python bench.py --no-cpu-baseline --steps 20 --launched-steps 20 --api-steps 0 --single-episodes 0 --perft-roots 0 --variant-steps 0"
 # the headline: the driver's own shape (--steps 20 --warmup 5), the fused launch of 20 steps is
-# the LAST k_env_rollout2<false, 0> dispatch of the process
+# the LAST k_env_rollout4 dispatch of the process
 PMCR="python bench.py --no-cpu-baseline --steps 20 --warmup 5 --launched-steps 0 --api-steps 0 --single-episodes 0 --perft-roots 0 --variant-steps 0"
 MIXC="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAVE_CYCLES GRBM_GUI_ACTIVE"
 # perft passes: the bench's perft leg (65 536 mid-game FEN roots, perft(5)) without the step legs

@@ -35,7 +35,9 @@ def main():
     ap.add_argument("--perft", action="store_true",
                     help="perft leaf kernel (k_perft2_perm_rec) passes pmc_perft_{fetch,write,mix} -> pmc_perft.json")
     ap.add_argument("--rollout", action="store_true",
-                    help="the headline kernel (last k_env_rollout2<false, 0> dispatch) passes pmc_roll_* -> pmc_rollout.json")
+                    help="the headline kernel (last dispatch of --rollout-kernel) passes pmc_roll_* -> pmc_rollout.json")
+    ap.add_argument("--rollout-kernel", default="k_env_rollout4",
+                    help="the fused rollout's kernel: k_env_rollout4 (quads), k_env_rollout2<false, 0> (pairs)")
     ap.add_argument("--calib", action="store_true",
                     help="tools/_valu_calib under the mix counters (pmc_calib + calib.log) -> valu_calib.json")
     a = ap.parse_args()
@@ -146,11 +148,11 @@ def valu_issue(rows_sum, calib):
 
 
 def rollout_summary(a):
-    """The headline kernel: the LAST k_env_rollout2<false, 0> dispatch of the bench command
+    """The headline kernel: the LAST dispatch of the fused rollout of the bench command
     (its timed launch of K steps).  HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE), per
     board per ply; VALU instructions per wave, lane utilisation, INT64 share, issue fraction
     (calibrated, tools/valu_calib.hip); SQ_WAIT_ANY share of wave cycles."""
-    kern = "k_env_rollout2<false, 0>"
+    kern = a.rollout_kernel
     f = per_dispatch(os.path.join(a.src, "pmc_roll_fetch", "run_counter_collection.csv"), kern)[-1]
     w = per_dispatch(os.path.join(a.src, "pmc_roll_write", "run_counter_collection.csv"), kern)[-1]
     bl = bench_line(os.path.join(a.src, "pmcrf.log")) or {}
