@@ -202,15 +202,18 @@ def perft_leg(args, rep):
            "nodes": tot, "seconds": dtm,
            "leaf_pass": {k: paths1[k] - paths0[k] for k in paths0},
            "roots_with": {"castle_right": castle, "pawn_on_7th": prom, "side_in_check": check}}
-    # the leaf kernel (k_perft2_perm_rec: one lane = one depth-2 subtree, last ply bulk-counted):
-    # where the time goes.  It is VALU-bound -- 76 algorithmic HBM bytes per subtree (root
-    # state + index in, count out) against ~1e3 leaves -- so its roof is the VALU issue rate:
-    # busy_frac and lane use from the PMC profile (tools/gpu_run.sh pmcp*)
+    # the leaf kernel (k_perft2_rec: one lane = one depth-2 subtree, read in order, last ply
+    # bulk-counted): where the time goes.  It is VALU-bound -- 72 algorithmic HBM bytes per
+    # subtree (the 64-B root record in, its count added into the parent's sum) against ~1e3
+    # leaves -- so its roof is the VALU issue rate (PMC profile, tools/gpu_run.sh pmcp*).
+    # GC_PERFT_GATHER: the earlier form, gathering through a sorted permutation (+ 4 B index)
+    gather = bool(os.environ.get("GC_PERFT_GATHER"))
+    alg_sub = 76 if gather else 72
     la, sub, kms = (b - a for a, b in zip(leaf0, leaf1))
     if la:
-        roof = {"bound": "valu", "kernel": "k_perft2_perm_rec", "launches": la, "subtrees": sub,
-                "kernel_ms": kms, "share_of_perft_time": kms / 1e3 / len(rep.local) / dtm,
-                "alg_bytes_per_subtree": 76, "hbm_achieved_gbs": 76.0 * sub / (kms / 1e3) / 1e9}
+        roof = {"bound": "valu", "kernel": "k_perft2_perm_rec" if gather else "k_perft2_rec", "launches": la,
+                "subtrees": sub, "kernel_ms": kms, "share_of_perft_time": kms / 1e3 / len(rep.local) / dtm,
+                "alg_bytes_per_subtree": alg_sub, "hbm_achieved_gbs": alg_sub * sub / (kms / 1e3) / 1e9}
         pf = os.path.join(ROOT, "profiles", "pmc_perft_latest.json")
         if os.path.exists(pf):
             try:

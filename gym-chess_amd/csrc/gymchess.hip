@@ -491,6 +491,88 @@ __global__ void k_expand_range_rec(SoA in, int a, int c, const int32_t* __restri
     if (g.castles & 2) node_store(out, o++, child_of(s, g.white, g.white ? A_KSW : A_KSB), (u32)t);
 }
 
+// The split pass's depth-2 roots placed in move-count order as they are made (round 3), so
+// the leaf kernel reads them in order -- one coalesced 64-B record per lane, no gather through
+// a sorted permutation (PMC r03_v5: 137 B per subtree, the 64-B records fetched as random
+// 128-B lines).  A counting sort over the expansion: pass A (k_expand_count) generates every
+// chunk parent's children, counts each child's moves and keeps per-block histograms
+// [bin][block]; an exclusive scan of those gives every (bin, block) its range; pass B
+// (k_expand_place) generates the children again and writes each record at its bin's next slot
+// of its block's range (an LDS cursor per bin: the order within a bin and block is arbitrary,
+// which no sum depends on).  Counts past the last bin share it (never in play: > 254 moves).
+#define SPLIT_BINS 256
+template <class F>
+__device__ __forceinline__ void for_each_child(const Pos& s, const Gen& g, F&& f) {
+    u64 pcs = g.own;
+    while (pcs) {
+        int sq = ctz(pcs);
+        pcs &= pcs - 1;
+        u64 tg = legal_targets(s, g, sq, type_at(s, sq));
+        while (tg) {
+            int tt = ctz(tg);
+            tg &= tg - 1;
+            f(child_of(s, g.white, sq * 64 + tt));
+        }
+    }
+    if (g.castles & 1) f(child_of(s, g.white, g.white ? A_QSW : A_QSB));
+    if (g.castles & 2) f(child_of(s, g.white, g.white ? A_KSW : A_KSB));
+}
+__device__ __forceinline__ int split_bin(const Pos& ch) {
+    Gen g;
+    gen_init(ch, g);
+    const int n = count_moves(ch, g);
+    return n < SPLIT_BINS - 1 ? n : SPLIT_BINS - 1;
+}
+__global__ void __launch_bounds__(BLOCK) k_expand_count(SoA in, int a, int c, uint8_t* __restrict__ bins,
+                                                        const int32_t* __restrict__ offs, u32* __restrict__ hist,
+                                                        int nblk) {
+    __shared__ u32 h[SPLIT_BINS];
+    for (int b = threadIdx.x; b < SPLIT_BINS; b += blockDim.x) h[b] = 0;
+    __syncthreads();
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < c) {
+        const Pos s = in.load(a + t);
+        Gen g;
+        gen_init(s, g);
+        size_t o = (size_t)offs[t];
+        for_each_child(s, g, [&](const Pos& ch) {
+            const int b = split_bin(ch);
+            bins[o++] = (uint8_t)b;
+            atomicAdd(&h[b], 1u);
+        });
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < SPLIT_BINS; b += blockDim.x) hist[(size_t)b * nblk + blockIdx.x] = h[b];
+}
+__global__ void __launch_bounds__(BLOCK) k_expand_place(SoA in, int a, int c, const uint8_t* __restrict__ bins,
+                                                        const int32_t* __restrict__ offs,
+                                                        const u32* __restrict__ base, int nblk,
+                                                        Node64* __restrict__ out) {
+    __shared__ u32 cur[SPLIT_BINS];
+    for (int b = threadIdx.x; b < SPLIT_BINS; b += blockDim.x) cur[b] = base[(size_t)b * nblk + blockIdx.x];
+    __syncthreads();
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= c) return;
+    const Pos s = in.load(a + t);
+    Gen g;
+    gen_init(s, g);
+    size_t o = (size_t)offs[t];
+    for_each_child(s, g, [&](const Pos& ch) {
+        const u32 slot = atomicAdd(&cur[bins[o++]], 1u);
+        node_store(out, slot, ch, (u32)t);
+    });
+}
+// one lane = one depth-2 subtree, the records in move-count order (k_expand_place)
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(PERFT2_WPE)))
+k_perft2_rec(const Node64* __restrict__ in, int n, unsigned long long* __restrict__ parent_sum) {
+    __shared__ u64 lds_a[SCRATCH_SLOTS * BLOCK];
+    LdsScratch sa{lds_a + threadIdx.x};
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const u32 parent = reinterpret_cast<const u32*>(in + i)[15];
+    atomicAdd(parent_sum + parent, (unsigned long long)perft2(node_load(in, i), sa));
+}
+
 // parent value = sum of its children's values (children of one parent are contiguous)
 template <class T>
 __global__ void k_sum_children(const T* __restrict__ offs, const T* __restrict__ cnt,
@@ -3177,26 +3259,37 @@ static int perft_split_leaves(hipStream_t st, SoA leaf, uint64_t* leaf_out) {
     int chunk = 1 << 21;
     std::vector<hipEvent_t> evs;  // pairs around the leaf launches
     uint64_t subtrees = 0;
+    // GC_PERFT_GATHER (A/B): the round-2/3 form -- records in expansion order, a radix sort by
+    // move count, the leaf kernel gathering through the permutation
+    static const bool gather = getenv("GC_PERFT_GATHER") != nullptr;
     int32_t *kc = nullptr, *offs = nullptr, *kc2 = nullptr, *ks = nullptr, *ix = nullptr, *is = nullptr;
+    uint8_t* bins = nullptr;
+    u32 *hist = nullptr, *hbase = nullptr;
+    const int max_blk = (chunk + BLOCK - 1) / BLOCK;
     Node64* cr = nullptr;
     void* tmp = nullptr;
     size_t tmp_bytes = 0;
     int rc = 0;
     std::string err;
     auto done = [&]() {
-        void* ps[] = {kc, offs, kc2, ks, ix, is, cr, tmp};
+        void* ps[] = {kc, offs, kc2, ks, ix, is, cr, tmp, bins, hist, hbase};
         for (void* q : ps) (void)hipFree(q);
         for (hipEvent_t ev : evs) (void)hipEventDestroy(ev);
     };
-    if (dalloc(&kc, leaf.n) || dalloc(&offs, chunk) || dalloc(&kc2, cap) || dalloc(&ks, cap) || dalloc(&ix, cap) ||
-        dalloc(&is, cap) || dalloc(&cr, cap)) {
+    if (dalloc(&kc, leaf.n) || dalloc(&offs, chunk) || dalloc(&cr, cap) ||
+        (gather ? (dalloc(&kc2, cap) || dalloc(&ks, cap) || dalloc(&ix, cap) || dalloc(&is, cap))
+                : (dalloc(&bins, cap) || dalloc(&hist, (size_t)SPLIT_BINS * max_blk) ||
+                   dalloc(&hbase, (size_t)SPLIT_BINS * max_blk)))) {
         done();
         return -1;
     }
     {  // scratch for the largest scan and sort of a chunk
         size_t b1 = 0, b2 = 0;
         hipError_t he = hipcub::DeviceScan::ExclusiveSum(nullptr, b1, kc, offs, chunk, st);
-        if (he == hipSuccess) he = hipcub::DeviceRadixSort::SortPairs(nullptr, b2, kc2, ks, ix, is, (int)cap, 0, 10, st);
+        if (he == hipSuccess && gather)
+            he = hipcub::DeviceRadixSort::SortPairs(nullptr, b2, kc2, ks, ix, is, (int)cap, 0, 10, st);
+        if (he == hipSuccess && !gather)
+            he = hipcub::DeviceScan::ExclusiveSum(nullptr, b2, hist, hbase, SPLIT_BINS * max_blk, st);
         tmp_bytes = b1 > b2 ? b1 : b2;
         if (he != hipSuccess) { done(); return fail(std::string("perft split: ") + hipGetErrorString(he)); }
         if (dalloc((char**)&tmp, tmp_bytes)) { done(); return -1; }
@@ -3215,7 +3308,22 @@ static int perft_split_leaves(hipStream_t st, SoA leaf, uint64_t* leaf_out) {
         if (total > cap) { chunk /= 2; continue; }  // an unusually bushy chunk: halve and retry
         he = hipMemsetAsync(leaf_out + a, 0, (size_t)8 * c, st);  // the parents' sums
         if (he != hipSuccess) { err = std::string("perft split: ") + hipGetErrorString(he); rc = -1; break; }
-        if (total > 0) {
+        if (total > 0 && !gather) {  // the records in move-count order, then read in order
+            const int nb = grid_for(c);
+            k_expand_count<<<nb, BLOCK, 0, st>>>(leaf, a, c, bins, offs, hist, nb);
+            tb = tmp_bytes;
+            he = hipcub::DeviceScan::ExclusiveSum(tmp, tb, hist, hbase, SPLIT_BINS * nb, st);
+            if (he != hipSuccess) { err = std::string("perft split scan: ") + hipGetErrorString(he); rc = -1; break; }
+            k_expand_place<<<nb, BLOCK, 0, st>>>(leaf, a, c, bins, offs, hbase, nb, cr);
+            hipEvent_t e0 = nullptr, e1 = nullptr;
+            if (hipEventCreate(&e0) == hipSuccess) evs.push_back(e0);
+            if (hipEventCreate(&e1) == hipSuccess) evs.push_back(e1);
+            if (e0 && e1) (void)hipEventRecord(e0, st);
+            k_perft2_rec<<<grid_for((int)total), BLOCK, 0, st>>>(cr, (int)total,
+                                                                  reinterpret_cast<unsigned long long*>(leaf_out + a));
+            if (e0 && e1) (void)hipEventRecord(e1, st);
+            subtrees += (uint64_t)total;
+        } else if (total > 0) {
             k_expand_range_rec<<<grid_for(c), BLOCK, 0, st>>>(leaf, a, c, offs, cr);
             k_count_children_rec<<<grid_for((int)total), BLOCK, 0, st>>>(cr, (int)total, kc2);
             k_iota<<<grid_for((int)total), BLOCK, 0, st>>>(ix, (int)total);
