@@ -517,10 +517,9 @@ __device__ __forceinline__ void for_each_child(const Pos& s, const Gen& g, F&& f
     if (g.castles & 1) f(child_of(s, g.white, g.white ? A_QSW : A_QSB));
     if (g.castles & 2) f(child_of(s, g.white, g.white ? A_KSW : A_KSB));
 }
-__device__ __forceinline__ int split_bin(const Pos& ch) {
-    Gen g;
-    gen_init(ch, g);
-    const int n = count_moves(ch, g);
+// the child's move count (perft2's fused count, the side to move's king lines from the parent)
+__device__ __forceinline__ int split_bin(const Pos& ch, const KingLines& kl) {
+    const int n = count_position_kl(ch, kl);
     return n < SPLIT_BINS - 1 ? n : SPLIT_BINS - 1;
 }
 __global__ void __launch_bounds__(BLOCK) k_expand_count(SoA in, int a, int c, uint8_t* __restrict__ bins,
@@ -535,8 +534,9 @@ __global__ void __launch_bounds__(BLOCK) k_expand_count(SoA in, int a, int c, ui
         Gen g;
         gen_init(s, g);
         size_t o = (size_t)offs[t];
+        const KingLines kl = king_lines_of(s, !g.white);  // every child's side to move, its king unmoved
         for_each_child(s, g, [&](const Pos& ch) {
-            const int b = split_bin(ch);
+            const int b = split_bin(ch, kl);
             bins[o++] = (uint8_t)b;
             atomicAdd(&h[b], 1u);
         });
