@@ -1850,9 +1850,9 @@ struct QuadLds {
     u32 irrev[QUAD_BOARDS];          //           irreversible move
     u64 pin3[3][QUAD_BOARDS];        // Q0 -> Q2, Q3: check mask, pinned, pin rays
     u32 f0[QUAD_BOARDS];             // Q0 -> Q1: the side to move is in check
-    u64 enemy[3][QUAD_BOARDS];       // Q1 / Q2 / Q3 -> Q0: the enemy map's leaper, orthogonal, diagonal parts
+    u64 enemy[3][QUAD_BOARDS];       // Q2 / Q3 -> Q0, Q2: the enemy map's leaper + orthogonal ([1]), diagonal ([2]) parts
     u32 f1[QUAD_BOARDS];             // Q1 -> Q0: the mover is in check after its move
-    u64 cwx[2][QUAD_BOARDS];         // Q2 / Q3 -> Q0: their sets' byte counts (words 1 and 2)
+    u64 cwx[2][4][QUAD_BOARDS];      // Q2 / Q3 -> Q0: their sets' byte counts (all four words)
     u32 part[4][QUAD_BOARDS];        // partial move totals (Q0's holds the castles)
     u32 rep[QUAD_BOARDS];            // Q1 -> Q0: 3-fold count | window length << 8
     u32 x0[QUAD_BOARDS];             // Q1 -> Q0: the Philox word of the next draw
@@ -1897,6 +1897,7 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
     bool irrev = false;
     Pos ns;
     RepProbe pr;
+    PST(7);  // (GC_PSTAMPS: the segments as in the paired kernel, phase 0 .. wait D)
     // ---- phase 0
     if (R == 0) {
         ns = s;
@@ -1913,7 +1914,9 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
         if (C.rtable) ra = C.racts[scale_rank(x0, C.rtotal)];
         L.x0[l] = x0;
     }
+    PST(0);
     pair_barrier();
+    PST(1);
     // ---- phase 1
     Gen g;
     bool my_chk = false;
@@ -1933,19 +1936,20 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
         L.pin3[1][l] = g.pinned;
         L.pin3[2][l] = g.pinrays;
         L.f0[l] = g.in_check ? 1u : 0u;
-    } else if (R == 1) {
-        L.enemy[0][l] = g.ks >= 0 ? side_attacks_leapers(ns, !g.white) : 0ull;
+    } else if (R == 1) {  // (the leaper attacks went to Q2: phase 1 was Q1's longest)
         my_chk = mv && mover_checked(s, ns, white, a);
         L.f1[l] = my_chk ? 1u : 0u;
     } else if (R == 2) {
-        L.enemy[1][l] = g.ks >= 0 ? side_attacks_orth(ns, !g.white) : 0ull;
+        L.enemy[1][l] = g.ks >= 0 ? side_attacks_leapers(ns, !g.white) | side_attacks_orth(ns, !g.white) : 0ull;
     } else {
         L.enemy[2][l] = g.ks >= 0 ? side_attacks_diag(ns, !g.white) : 0ull;
     }
+    PST(2);
     pair_barrier();
+    PST(3);
     // ---- phase 2
     if (R == 0) {
-        g.enemy_att = L.enemy[0][l] | L.enemy[1][l] | L.enemy[2][l];
+        g.enemy_att = L.enemy[1][l] | L.enemy[2][l];
         gen_castles(ns, g);  // lib.rs:578-610 with the whole enemy map
         my_chk = L.f1[l] != 0;
     } else if (R == 1) {
@@ -1954,6 +1958,7 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
         g.checkmask = L.pin3[0][l];
         g.pinned = L.pin3[1][l];
         g.pinrays = L.pin3[2][l];
+        if (R == 2) g.enemy_att = L.enemy[1][l] | L.enemy[2][l];  // for the king sets
     }
     const bool opp_chk = g.in_check;
     const bool both = opp_chk && my_chk;  // lib.rs:1442-1446
@@ -1961,15 +1966,11 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
     QuadSets Q{L, l, {0, 0, 0, 0}, 0};  // sets go to LDS as they are made: no 28-set array held
     int c = 0;
     u32 hl = hl_of(s.meta);
-    if (R == 0) {  // pawn, knight and king sets; castles counted here
+    if (R == 0) {  // pawn sets; castles counted here (phase 2 was Q0's longest: knights to Q3, kings to Q2)
         if (gen) {
             u64 T[SW_SETS];
             sw_pawns(ns, g, T);
             Q.put_all<SW_P1, SW_N>(T + SW_P1);
-            sw_knights(ns, g, T);
-            Q.put_all<SW_N, SW_ORTH>(T + SW_N);
-            sw_kings(ns, g, T);
-            Q.put_all<SW_K, SW_SETS>(T + SW_K);
             Q.part += popc(g.castles);
         }
     } else if (R == 1) {
@@ -1984,17 +1985,25 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
         u64 T[SW_SETS];
         sw_orth(ns, g, T);
         Q.put_all<SW_ORTH, SW_DIAG>(T + SW_ORTH);
+        sw_kings(ns, g, T);
+        Q.put_all<SW_K, SW_SETS>(T + SW_K);
         L.part[2][l] = (u32)Q.part;
-        L.cwx[0][l] = Q.cw[1];
+#pragma unroll
+        for (int k = 0; k < 4; k++) L.cwx[0][k][l] = Q.cw[k];
     } else {
         u64 T[SW_SETS];
+        sw_knights(ns, g, T);
+        Q.put_all<SW_N, SW_ORTH>(T + SW_N);
         sw_diag(ns, g, T);
         Q.put_all<SW_DIAG, SW_K>(T + SW_DIAG);
         L.part[3][l] = (u32)Q.part;
-        L.cwx[1][l] = Q.cw[2];
+#pragma unroll
+        for (int k = 0; k < 4; k++) L.cwx[1][k][l] = Q.cw[k];
     }
     if (R == 0) L.part[0][l] = (u32)Q.part;
+    PST(4);
     pair_barrier();
+    PST(5);
     // ---- phase 3: the outcome (Q0 and Q1, identical arithmetic), Q0's pick
     StepOut o = {0, 0, R_NONE, 0};
     if constexpr (CARRY) {
@@ -2002,8 +2011,8 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
         u64* const cw = Q.cw;
         if (R == 0) {
             if (gen) {
-                cw[1] |= L.cwx[0][l];
-                cw[2] |= L.cwx[1][l];
+#pragma unroll
+                for (int k = 0; k < 4; k++) cw[k] |= L.cwx[0][k][l] | L.cwx[1][k][l];
             }
             const u32 rpk = L.rep[l];
             c = (int)(rpk & 0xFFu);
@@ -2076,6 +2085,7 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
             L.draw[l] = d;
         }
     }
+    PST(6);
     pair_barrier();  // the next action and draw counter to Q1; LDS free for the next ply
     if (R == 1) {
         a = (int)L.act[l];
@@ -2128,12 +2138,24 @@ __device__ __noinline__ void quad_run(uint8_t* __restrict__ slab, int nn, uint64
     if (RR == 0 && l == 0) L.rp = icd->pos;  // read after ply 0's first barrier
     int a = (int)ua;
     DevHist h = DevHist{htab, in_io.hgen, g0, ii, HTAB_BITS};
+#ifdef GC_PSTAMPS
+    const unsigned long long g_pst_entry = __builtin_amdgcn_s_memrealtime();
+    unsigned long long rt1 = 0;
+    if (l == 0) {
+        for (int k = 0; k < 8; k++) gc_pst[threadIdx.x >> 6][k] = 0;
+        gc_pst[threadIdx.x >> 6][8] = __builtin_amdgcn_s_memtime();
+    }
+    const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
     uint64_t steps = 0, rsum = 0;
     u32 e_mate = 0, e_rep = 0, e_cap = 0, e_nomove = 0, e_err = 0;
     StepOut o = {0, 0, R_NONE, 0};
     for (int p = 0; p < plies; p++) {
         const int played = a;
         o = quad_ply<RR>(L, C, l, i, live, s, a, d, h, nst);
+#ifdef GC_PSTAMPS
+        if (p == 0) rt1 = __builtin_amdgcn_s_memrealtime();
+#endif
         if (RR == 1) {  // the ply's outputs (trace, stats) and the window write
             if (trace && live) trace[(size_t)p * nn + i] = trace_word(played == A_NONE ? -1 : played, o);
             if (!ST) {
@@ -2153,6 +2175,16 @@ __device__ __noinline__ void quad_run(uint8_t* __restrict__ slab, int nn, uint64
             h.commit();  // this ply's window write lands before the next ply's probe
         }
     }
+#ifdef GC_PSTAMPS
+    if (g_pst_out != nullptr && l == 0) {
+        const size_t w = (size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+        for (int k = 0; k < 8; k++) g_pst_out[w * 12 + k] = gc_pst[threadIdx.x >> 6][k];
+        g_pst_out[w * 12 + 8] = g_pst_entry;
+        g_pst_out[w * 12 + 9] = rt0;
+        g_pst_out[w * 12 + 10] = rt1;
+        g_pst_out[w * 12 + 11] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
     if (!live || RR >= 2) return;
     const PairIO io = store_io(slab, nn);
     if (RR == 0) {
@@ -4655,7 +4687,9 @@ extern "C" int gc_env_window_sum(gc_env* e, uint64_t* sum) {
 // wave start, entry loads done, first ply done, last ply done
 extern "C" int gc_debug_pstamps(gc_env* e, int n_plies, uint64_t* out /* waves * 12 */) {
     unsigned long long* d = nullptr;
-    const size_t waves = (size_t)((e->n + PAIR_BOARDS * PAIRS_WG - 1) / (PAIR_BOARDS * PAIRS_WG)) * 2 * PAIRS_WG;
+    // waves of the fused launch: pairs (2 per 64 boards) or quads (4 per 64 boards)
+    const size_t waves = use_quad(e) ? (size_t)((e->n + QUAD_BOARDS * QUADS_WG - 1) / (QUAD_BOARDS * QUADS_WG)) * 4 * QUADS_WG
+                                     : (size_t)((e->n + PAIR_BOARDS * PAIRS_WG - 1) / (PAIR_BOARDS * PAIRS_WG)) * 2 * PAIRS_WG;
     if (dalloc(&d, waves * 12)) return -1;
     HIPCHK(hipMemsetAsync(d, 0, waves * 96, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));

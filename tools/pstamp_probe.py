@@ -21,7 +21,8 @@ pmap = int(os.environ.get("PST_MAP", "2"))
 h = P()
 assert L.gc_env_create(0, n, 0x5EED + 3, None, ctypes.byref(h)) == 0
 assert L.gc_env_rollout(h, 1000, None, None, None, None, None) == 0  # steady state
-waves = ((n + 127) // 128) * 4
+quad = os.environ.get("PST_QUAD") == "1"  # the quad kernel (k_env_rollout4): 4 waves per 64 boards
+waves = ((n + 127) // 128) * (8 if quad else 4)
 out = np.zeros(waves * 12, dtype=np.uint64)
 assert L.gc_debug_pstamps(h, plies, out.ctypes.data_as(P)) == 0
 raw = out.reshape(-1, 12)
@@ -36,15 +37,24 @@ print(f"launch anatomy ({plies} plies, us from the first wave's start): last wav
       f"entry loads mean {(us[:, 1] - us[:, 0]).mean():.2f}; first ply mean {(us[:, 2] - us[:, 1]).mean():.2f}, "
       f"later plies mean {((us[:, 3] - us[:, 2]) / max(plies - 1, 1)).mean():.3f}; wave end mean {us[:, 3].mean():.2f}, "
       f"p90 {np.percentile(us[:, 3], 90):.2f}, max {us[:, 3].max():.2f}")
-w = np.arange(waves) % 4
-role = np.where(pmap == 2, (w ^ (w >> 1)) & 1, w & 1)
-names = ["phase 0", "wait A", "phase 1", "wait B", "phase 2", "wait C", "phase 3", "wait D"]
-for r in (0, 1):
+if quad:  # k_env_rollout4: 8 waves per workgroup, roles (w & 3) ^ 2 * quad
+    w = np.arange(waves) % 8
+    role = (w & 3) ^ (((w >> 2) & 1) << 1)
+    names = ["phase 0", "wait A", "phase 1", "wait B", "phase 2", "wait C", "phase 3", "wait D"]
+    roles = (0, 1, 2, 3)
+else:
+    w = np.arange(waves) % 4
+    role = np.where(pmap == 2, (w ^ (w >> 1)) & 1, w & 1)
+    names = ["phase 0", "wait A", "phase 1", "wait B", "phase 2", "wait C", "phase 3", "wait D"]
+    roles = (0, 1)
+for r in roles:
     s = st[role == r]
     tot = s.sum(axis=1).mean()
-    print(f"[W{r}] {len(s)} waves, {tot:.0f} cycles per ply")
-    for k in range(8):
+    print(f"[{'Q' if quad else 'W'}{r}] {len(s)} waves, {tot:.0f} cycles per ply")
+    for k in range(len(names)):
         print(f"   {names[k]:>8}: {s[:, k].mean():7.0f}  ({s[:, k].mean() / tot:5.1%})")
+if quad:
+    sys.exit(0)
 
 # where the slow waves run: wave end by XCD, by CU load and by SIMD load
 xcc = where >> 9
