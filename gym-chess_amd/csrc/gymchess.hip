@@ -1884,7 +1884,7 @@ struct QuadSets {
 // d, h, nst); both return the same s and a.  Q2 / Q3: s, a, d, h, nst unused.
 template <int R>
 __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l, int i, bool live, Pos& s, int& a,
-                                            u32& d, DevHist& h, u32& nst) {
+                                            u32& d, DevHist& h, u32& nst, RepProbe& pr) {
     constexpr bool CARRY = R < 2;  // Q0 / Q1 hold the state
     const bool none = a == A_NONE;                           // empty list: driver reset
     const bool done0 = (s.meta & M_DONE) != 0;               // chess_v2.py:245-251
@@ -1896,7 +1896,6 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
     int mr = 0;
     bool irrev = false;
     Pos ns;
-    RepProbe pr;
     PST(7);  // (GC_PSTAMPS: the segments as in the paired kernel, phase 0 .. wait D)
     // ---- phase 0
     if (R == 0) {
@@ -1908,8 +1907,7 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
         L.nmeta[l] = ns.meta;
         L.mr[l] = mr;
         L.irrev[l] = irrev ? 1u : 0u;
-    } else if (R == 1) {
-        if (mv) rep_prefetch(h, s, pr);
+    } else if (R == 1) {  // (the probe of s was issued at the end of the last ply: pr)
         x0 = philox_x0(C.seed, (u32)i, d);  // the next draw (independent of the position)
         if (C.rtable) ra = C.racts[scale_rank(x0, C.rtotal)];
         L.x0[l] = x0;
@@ -2056,6 +2054,9 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
             s = L.rp;
             h.bump_gen();
         }
+        // Q1: the next ply's probe, its pre-move board settled, while Q0 still picks (Q1 waits at
+        // the next barrier anyway); after this ply's window write, so it sees it
+        if (R == 1 && live) rep_prefetch(h, s, pr);
         if (R == 0) {
             uint16_t act = (uint16_t)set_act;
             int tot = total;
@@ -2098,28 +2099,14 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
 // access a ds_ instruction)
 __shared__ QuadLds g_quad_lds[QUADS_WG];
 
-// One role's whole launch (its K plies and its stores), NOT inlined into the kernel: the four
-// roles' register needs are allocated apart (each fits 128 VGPRs alone -- Q0 93, Q1 117, Q2 31,
-// Q3 27 -- inlined together under one switch they spill), and the kernel takes their maximum.
-// (a function's arguments arrive in VGPRs: the launch-uniform ones go back to SGPRs first)
-__device__ __forceinline__ u64 uni64(u64 v) {
-    return (u64)(u32)__builtin_amdgcn_readfirstlane((int)(u32)v) |
-           ((u64)(u32)__builtin_amdgcn_readfirstlane((int)(u32)(v >> 32)) << 32);
-}
-template <class T>
-__device__ __forceinline__ T* uni_ptr(T* p) { return reinterpret_cast<T*>(uni64(reinterpret_cast<u64>(p))); }
+// One role's whole launch (its K plies and its stores), inlined into the kernel's switch on the
+// role: a non-inlined function takes generic pointers -- flat memory instructions, which count
+// in lgkmcnt too, so every barrier's lgkmcnt(0) waited for the window probe in flight.
 template <int RR, bool ST>
-__device__ __noinline__ void quad_run(uint8_t* __restrict__ slab, int nn, uint64_t seed, u64* __restrict__ htab,
+__device__ __forceinline__ void quad_run(uint8_t* __restrict__ slab, int nn, uint64_t seed, u64* __restrict__ htab,
                                       const uint16_t* __restrict__ racts, const EnvDev::InitCache* __restrict__ icd,
                                       u32 rinfo, int plies, uint64_t* __restrict__ stats, u64* __restrict__ trace,
                                       int qw, int l, int i) {
-    slab = uni_ptr(slab); htab = uni_ptr(htab); racts = uni_ptr(racts); icd = uni_ptr(icd);
-    stats = uni_ptr(stats); trace = uni_ptr(trace);
-    nn = __builtin_amdgcn_readfirstlane(nn);
-    seed = uni64(seed);
-    rinfo = (u32)__builtin_amdgcn_readfirstlane((int)rinfo);
-    plies = __builtin_amdgcn_readfirstlane(plies);
-    qw = __builtin_amdgcn_readfirstlane(qw);
     QuadLds& L = g_quad_lds[qw];
     const bool live = i < nn;
     const int ii = live ? i : nn - 1;  // dead lanes read a valid board, store nothing
@@ -2138,6 +2125,8 @@ __device__ __noinline__ void quad_run(uint8_t* __restrict__ slab, int nn, uint64
     if (RR == 0 && l == 0) L.rp = icd->pos;  // read after ply 0's first barrier
     int a = (int)ua;
     DevHist h = DevHist{htab, in_io.hgen, g0, ii, HTAB_BITS};
+    RepProbe pr;  // Q1: the window probe of the coming ply's pre-move board
+    if (RR == 1 && live) rep_prefetch(h, s, pr);
 #ifdef GC_PSTAMPS
     const unsigned long long g_pst_entry = __builtin_amdgcn_s_memrealtime();
     unsigned long long rt1 = 0;
@@ -2152,7 +2141,7 @@ __device__ __noinline__ void quad_run(uint8_t* __restrict__ slab, int nn, uint64
     StepOut o = {0, 0, R_NONE, 0};
     for (int p = 0; p < plies; p++) {
         const int played = a;
-        o = quad_ply<RR>(L, C, l, i, live, s, a, d, h, nst);
+        o = quad_ply<RR>(L, C, l, i, live, s, a, d, h, nst, pr);
 #ifdef GC_PSTAMPS
         if (p == 0) rt1 = __builtin_amdgcn_s_memrealtime();
 #endif
