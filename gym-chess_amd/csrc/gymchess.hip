@@ -1857,8 +1857,10 @@ struct QuadLds {
     u32 rep[QUAD_BOARDS];            // Q1 -> Q0: 3-fold count | window length << 8
     u32 x0[QUAD_BOARDS];             // Q1 -> Q0: the Philox word of the next draw
     u32 ra[QUAD_BOARDS];             // Q1 -> Q0: the start-position table pick
-    u32 act[QUAD_BOARDS];            // Q0 -> Q1: the next action
-    u32 draw[QUAD_BOARDS];           // Q0 -> Q1: the draw counter
+    u32 act[QUAD_BOARDS];            // Q0 -> Q1: this ply's action (phase 0)
+    u32 pick[QUAD_BOARDS];           // Q2 -> Q0: the policy's pick from this ply's move sets (phase 3)
+    u32 castles[QUAD_BOARDS];        // Q0 -> Q2: the castles (phase 2)
+    u64 cw0[QUAD_BOARDS];            // Q0 -> Q2: its sets' byte counts (word 0)
     Pos rp;                          // the reset position (read at a reset: no registers held for it)
 };
 // one set of the next side's moves into LDS, its count into the packed byte counts and the total
@@ -1880,23 +1882,46 @@ struct QuadSets {
     }
 };
 
+// Q0's choice of the next action, left for the start of the next ply: Q2 makes the pick from
+// the move sets in phase 3 while Q0 and Q1 settle the outcome (the pick was phase 3's longest
+// chain); a board that resets takes the start position's table pick instead.
+struct QuadPend {
+    bool pending;  // false: `a` is already the action (the launch's first ply)
+    bool have;     // the move stood: Q2's pick
+    uint16_t ra;   // else: the table pick
+    __device__ int resolve(const QuadLds& L, int l, int a) const {
+        return !pending ? a : have ? (int)L.pick[l] : (int)ra;
+    }
+};
+
 // One ply of board i for role R of its quad (RoleC<0..3>).  Q0 / Q1: in/out as pair_ply (s, a,
 // d, h, nst); both return the same s and a.  Q2 / Q3: s, a, d, h, nst unused.
 template <int R>
 __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l, int i, bool live, Pos& s, int& a,
-                                            u32& d, DevHist& h, u32& nst, RepProbe& pr) {
+                                            u32& d, DevHist& h, u32& nst, RepProbe& pr, QuadPend& pend) {
     constexpr bool CARRY = R < 2;  // Q0 / Q1 hold the state
+    if (R == 0) a = pend.resolve(L, l, a);  // the last ply's action: Q2's pick, or the reset table's
+    u32 x0 = 0;
+    uint16_t ra = (uint16_t)A_NONE;
+    if (R == 1) {  // phase 0 work first: it does not depend on the action, which Q1 learns after it
+        x0 = philox_x0(C.seed, (u32)i, d);  // the next draw (independent of the position)
+        if (C.rtable) ra = C.racts[scale_rank(x0, C.rtotal)];
+        L.x0[l] = x0;
+    }
+    if (R == 0) L.act[l] = (u32)a;
+    PST(7);  // (GC_PSTAMPS: the segments as in the paired kernel, phase 0 .. wait D)
+    if (R == 1) {
+        pair_barrier();  // (Q1's phase 0 is above; it meets the others' barrier A here)
+        a = (int)L.act[l];
+    }
     const bool none = a == A_NONE;                           // empty list: driver reset
     const bool done0 = (s.meta & M_DONE) != 0;               // chess_v2.py:245-251
     const bool cap = mc_of(s.meta) > MOVES_MAX;              // 252-258
     const bool mv = live && !none && !done0 && !cap;         // env_ply runs
     const bool white = (s.meta & M_WHITE) != 0;
-    u32 x0 = 0;
-    uint16_t ra = (uint16_t)A_NONE;
     int mr = 0;
     bool irrev = false;
     Pos ns;
-    PST(7);  // (GC_PSTAMPS: the segments as in the paired kernel, phase 0 .. wait D)
     // ---- phase 0
     if (R == 0) {
         ns = s;
@@ -1907,13 +1932,9 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
         L.nmeta[l] = ns.meta;
         L.mr[l] = mr;
         L.irrev[l] = irrev ? 1u : 0u;
-    } else if (R == 1) {  // (the probe of s was issued at the end of the last ply: pr)
-        x0 = philox_x0(C.seed, (u32)i, d);  // the next draw (independent of the position)
-        if (C.rtable) ra = C.racts[scale_rank(x0, C.rtotal)];
-        L.x0[l] = x0;
     }
     PST(0);
-    pair_barrier();
+    if (R != 1) pair_barrier();
     PST(1);
     // ---- phase 1
     Gen g;
@@ -1971,6 +1992,8 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
             Q.put_all<SW_P1, SW_N>(T + SW_P1);
             Q.part += popc(g.castles);
         }
+        L.cw0[l] = Q.cw[0];
+        L.castles[l] = g.castles;
     } else if (R == 1) {
         if (mv && !both) {
             pin(pr.e0.hdr); pin(pr.e0.k); pin(pr.e0.q); pin(pr.e0.r);
@@ -2002,8 +2025,19 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
     PST(4);
     pair_barrier();
     PST(5);
-    // ---- phase 3: the outcome (Q0 and Q1, identical arithmetic), Q0's pick
+    // ---- phase 3: the outcome (Q0 and Q1, identical arithmetic); Q2 picks the next action
+    // from the move sets (Q0 takes it, or the reset table's, at the start of the next ply)
     StepOut o = {0, 0, R_NONE, 0};
+    if (R == 2) {
+        const int total = (int)L.part[0][l] + Q.part + (int)L.part[3][l];
+        u64 cw[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) cw[k] = Q.cw[k] | L.cwx[1][k][l];
+        cw[0] |= L.cw0[l];
+        g.castles = L.castles[l];
+        // (a board whose generation is not due reads stale sets here: its pick is not taken)
+        L.pick[l] = total > 0 ? (u32)sw_pick_lds(L, l, g, cw, total, (int)scale_rank(L.x0[l], (u32)total)) : (u32)A_NONE;
+    }
     if constexpr (CARRY) {
         const int total = gen ? (R == 0 ? Q.part : (int)L.part[0][l]) + (int)L.part[2][l] + (int)L.part[3][l] : 0;
         u64* const cw = Q.cw;
@@ -2015,13 +2049,11 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
             const u32 rpk = L.rep[l];
             c = (int)(rpk & 0xFFu);
             hl = rpk >> 8;
-            x0 = L.x0[l];
             ra = (uint16_t)L.ra[l];
         } else {
             h.commit();  // the window write, issued before the outcome
         }
-        int set_act = A_NONE;
-        if (R == 0 && total > 0) set_act = sw_pick_lds(L, l, g, cw, total, (int)scale_rank(x0, (u32)total));
+        (void)cw;
         bool have = false;
         if (none) {
             o.reason = R_NO_MOVES;
@@ -2057,41 +2089,14 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
         // Q1: the next ply's probe, its pre-move board settled, while Q0 still picks (Q1 waits at
         // the next barrier anyway); after this ply's window write, so it sees it
         if (R == 1 && live) rep_prefetch(h, s, pr);
-        if (R == 0) {
-            uint16_t act = (uint16_t)set_act;
-            int tot = total;
-            if (!have && C.rtable) {  // the start position's table
-                act = ra;
-                tot = (int)C.rtotal;
-            } else if (!have) {  // the start position without a table (rare): generated, through LDS
-                gen_init(s, g);
-                QuadSets Z{L, l, {0, 0, 0, 0}, 0};
-                u64 T[SW_SETS];
-                sw_pawns(s, g, T);
-                Z.put_all<SW_P1, SW_N>(T + SW_P1);
-                sw_knights(s, g, T);
-                Z.put_all<SW_N, SW_ORTH>(T + SW_N);
-                sw_orth(s, g, T);
-                Z.put_all<SW_ORTH, SW_DIAG>(T + SW_ORTH);
-                sw_diag(s, g, T);
-                Z.put_all<SW_DIAG, SW_K>(T + SW_DIAG);
-                sw_kings(s, g, T);
-                Z.put_all<SW_K, SW_SETS>(T + SW_K);
-                tot = Z.part + popc(g.castles);
-                act = (uint16_t)(tot > 0 ? sw_pick_lds(L, l, g, Z.cw, tot, (int)scale_rank(x0, (u32)tot)) : A_NONE);
-            }
-            a = act;
-            d += tot > 0 ? 1u : 0u;
-            L.act[l] = act;
-            L.draw[l] = d;
-        }
+        // the draw counter (both: the quads run only with the start position's pick table, so a
+        // reset's pick count is its total) and Q0's pending choice of the next action
+        const int tot = have ? total : (int)C.rtotal;
+        d += tot > 0 ? 1u : 0u;
+        if (R == 0) pend = QuadPend{true, have, ra};
     }
     PST(6);
-    pair_barrier();  // the next action and draw counter to Q1; LDS free for the next ply
-    if (R == 1) {
-        a = (int)L.act[l];
-        d = L.draw[l];
-    }
+    pair_barrier();  // Q2's pick to Q0; LDS free for the next ply
     return o;
 }
 
@@ -2127,6 +2132,7 @@ __device__ __forceinline__ void quad_run(uint8_t* __restrict__ slab, int nn, uin
     DevHist h = DevHist{htab, in_io.hgen, g0, ii, HTAB_BITS};
     RepProbe pr;  // Q1: the window probe of the coming ply's pre-move board
     if (RR == 1 && live) rep_prefetch(h, s, pr);
+    QuadPend pend{false, false, 0};  // Q0: the first ply's action is the env's
 #ifdef GC_PSTAMPS
     const unsigned long long g_pst_entry = __builtin_amdgcn_s_memrealtime();
     unsigned long long rt1 = 0;
@@ -2140,8 +2146,8 @@ __device__ __forceinline__ void quad_run(uint8_t* __restrict__ slab, int nn, uin
     u32 e_mate = 0, e_rep = 0, e_cap = 0, e_nomove = 0, e_err = 0;
     StepOut o = {0, 0, R_NONE, 0};
     for (int p = 0; p < plies; p++) {
-        const int played = a;
-        o = quad_ply<RR>(L, C, l, i, live, s, a, d, h, nst, pr);
+        o = quad_ply<RR>(L, C, l, i, live, s, a, d, h, nst, pr, pend);
+        const int played = a;  // (Q0: resolved at the ply's start; Q1: read after its barrier A)
 #ifdef GC_PSTAMPS
         if (p == 0) rt1 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -2177,6 +2183,7 @@ __device__ __forceinline__ void quad_run(uint8_t* __restrict__ slab, int nn, uin
     if (!live || RR >= 2) return;
     const PairIO io = store_io(slab, nn);
     if (RR == 0) {
+        a = pend.resolve(L, l, a);  // the next action (Q2's last pick arrived before the last barrier)
         io.act[i] = (uint16_t)a;
         io.draw[i] = d;
     } else {
