@@ -2212,7 +2212,10 @@ __global__ void __launch_bounds__(4 * QUAD_BOARDS * QUADS_WG) __attribute__((amd
     rinfo &= 0x1FFFFu;
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int qw = wv >> 2;  // the quad of this wave within the workgroup
-    const int role = (wv & 3) ^ ((qw & 1) << 1);
+#ifndef GC_QXOR
+#define GC_QXOR 2  // the roles of a workgroup's second quad: SIMD s holds roles s and s ^ GC_QXOR
+#endif
+    const int role = (wv & 3) ^ ((qw & 1) ? GC_QXOR : 0);
     const int l = threadIdx.x & (QUAD_BOARDS - 1);
     const int i = (blockIdx.x * QUADS_WG + qw) * QUAD_BOARDS + l;
 #ifdef GC_QUAD_ONLY  // diagnostic builds: one role's register needs
