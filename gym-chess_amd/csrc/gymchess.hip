@@ -2028,11 +2028,15 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
     // ---- phase 3: the outcome (Q0 and Q1, identical arithmetic); Q2 picks the next action
     // from the move sets (Q0 takes it, or the reset table's, at the start of the next ply)
     StepOut o = {0, 0, R_NONE, 0};
-    if (R == 2) {
-        const int total = (int)L.part[0][l] + Q.part + (int)L.part[3][l];
+#ifndef GC_PICK_ROLE
+#define GC_PICK_ROLE 2
+#endif
+    if (R == GC_PICK_ROLE) {
+        constexpr int OTHER = GC_PICK_ROLE == 2 ? 1 : 0;  // the other stateless role's byte counts
+        const int total = (int)L.part[0][l] + Q.part + (int)L.part[5 - GC_PICK_ROLE][l];
         u64 cw[4];
 #pragma unroll
-        for (int k = 0; k < 4; k++) cw[k] = Q.cw[k] | L.cwx[1][k][l];
+        for (int k = 0; k < 4; k++) cw[k] = Q.cw[k] | L.cwx[OTHER][k][l];
         cw[0] |= L.cw0[l];
         g.castles = L.castles[l];
         // (a board whose generation is not due reads stale sets here: its pick is not taken)
@@ -2040,12 +2044,7 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
     }
     if constexpr (CARRY) {
         const int total = gen ? (R == 0 ? Q.part : (int)L.part[0][l]) + (int)L.part[2][l] + (int)L.part[3][l] : 0;
-        u64* const cw = Q.cw;
         if (R == 0) {
-            if (gen) {
-#pragma unroll
-                for (int k = 0; k < 4; k++) cw[k] |= L.cwx[0][k][l] | L.cwx[1][k][l];
-            }
             const u32 rpk = L.rep[l];
             c = (int)(rpk & 0xFFu);
             hl = rpk >> 8;
@@ -2053,7 +2052,6 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
         } else {
             h.commit();  // the window write, issued before the outcome
         }
-        (void)cw;
         bool have = false;
         if (none) {
             o.reason = R_NO_MOVES;
