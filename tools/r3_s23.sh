@@ -5,4 +5,4 @@ mkdir -p gpurun_out
 M=gym-chess_amd/gym_chess_amd/libgymchess.so
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail -20 gpurun_out/smoke.log; exit 3; }
 tail -1 gpurun_out/smoke.log
-PYTEST=1 REPS=2 LIBS="tools/_lib_q11.so $M" bash tools/r3_ab.sh
+PYTEST=1 REPS=2 LIBS="tools/_lib_q12.so $M" bash tools/r3_ab.sh
