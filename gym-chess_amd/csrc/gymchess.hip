@@ -1900,6 +1900,10 @@ template <int R>
 __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l, int i, bool live, Pos& s, int& a,
                                             u32& d, DevHist& h, u32& nst, RepProbe& pr, QuadPend& pend) {
     constexpr bool CARRY = R < 2;  // Q0 / Q1 hold the state
+#ifndef GC_NO_QPRIO_DYN  // Q2's pick (phase 3's longest) ahead of Q0's outcome there: 14.43-14.63 -> 14.90-15.12e9
+    if (R == 0) __builtin_amdgcn_s_setprio(2);
+    if (R == 2) __builtin_amdgcn_s_setprio(0);
+#endif
     if (R == 0) a = pend.resolve(L, l, a);  // the last ply's action: Q2's pick, or the reset table's
     u32 x0 = 0;
     uint16_t ra = (uint16_t)A_NONE;
@@ -2028,6 +2032,10 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
     // ---- phase 3: the outcome (Q0 and Q1, identical arithmetic); Q2 picks the next action
     // from the move sets (Q0 takes it, or the reset table's, at the start of the next ply)
     StepOut o = {0, 0, R_NONE, 0};
+#ifndef GC_NO_QPRIO_DYN
+    if (R == 0) __builtin_amdgcn_s_setprio(0);
+    if (R == 2) __builtin_amdgcn_s_setprio(2);
+#endif
 #ifndef GC_PICK_ROLE
 #define GC_PICK_ROLE 2
 #endif
@@ -2216,6 +2224,19 @@ __global__ void __launch_bounds__(4 * QUAD_BOARDS * QUADS_WG) __attribute__((amd
     const int role = (wv & 3) ^ ((qw & 1) ? GC_QXOR : 0);
     const int l = threadIdx.x & (QUAD_BOARDS - 1);
     const int i = (blockIdx.x * QUADS_WG + qw) * QUAD_BOARDS + l;
+    // Issue priority: a SIMD hosts Q0 + Q2 or Q1 + Q3 (of both quads of a workgroup and of the
+    // CU's other workgroup); the state-carrying roles hold the longer chains, so their waves
+    // issue first (same-box A/B: 13.39-13.46 -> 14.21-14.25e9; Q1 alone 13.99-14.17).  Packed
+    // 2-bit priority per role, GC_QPRIO for diagnostic builds.
+#ifndef GC_QPRIO
+#define GC_QPRIO 0x0A  // Q0 2, Q1 2, Q2 0, Q3 0
+#endif
+    switch ((GC_QPRIO >> (2 * role)) & 3) {  // (s_setprio takes an immediate)
+        case 1: __builtin_amdgcn_s_setprio(1); break;
+        case 2: __builtin_amdgcn_s_setprio(2); break;
+        case 3: __builtin_amdgcn_s_setprio(3); break;
+        default: break;
+    }
 #ifdef GC_QUAD_ONLY  // diagnostic builds: one role's register needs
     quad_run<GC_QUAD_ONLY, false>(slab, nn, seed, htab, racts, icd, rinfo, plies, stats, trace, qw, l, i);
 #else
