@@ -1904,6 +1904,10 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
     if (R == 0) __builtin_amdgcn_s_setprio(2);
     if (R == 2) __builtin_amdgcn_s_setprio(0);
 #endif
+#ifdef GC_QPRIO_MID  // diagnostic: phases 1-2 at priorities GC_QPRIO_MID (Q0, Q1) / GC_QPRIO_MID23 (Q2, Q3)
+    if (R == 1) __builtin_amdgcn_s_setprio(2);
+    if (R == 3) __builtin_amdgcn_s_setprio(0);
+#endif
     if (R == 0) a = pend.resolve(L, l, a);  // the last ply's action: Q2's pick, or the reset table's
     u32 x0 = 0;
     uint16_t ra = (uint16_t)A_NONE;
@@ -1941,6 +1945,10 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
     if (R != 1) pair_barrier();
     PST(1);
     // ---- phase 1
+#ifdef GC_QPRIO_MID
+    if (R < 2) __builtin_amdgcn_s_setprio(GC_QPRIO_MID);
+    else __builtin_amdgcn_s_setprio(GC_QPRIO_MID23);
+#endif
     Gen g;
     bool my_chk = false;
     if (R != 0) {
@@ -2035,6 +2043,10 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
 #ifndef GC_NO_QPRIO_DYN
     if (R == 0) __builtin_amdgcn_s_setprio(0);
     if (R == 2) __builtin_amdgcn_s_setprio(2);
+#endif
+#ifdef GC_QPRIO_MID
+    if (R == 1) __builtin_amdgcn_s_setprio(2);
+    if (R == 3) __builtin_amdgcn_s_setprio(0);
 #endif
 #ifndef GC_PICK_ROLE
 #define GC_PICK_ROLE 2
