@@ -92,6 +92,12 @@ static int fail(const std::string& m) {
 
 extern "C" const char* gc_last_error(void) { return g_err.c_str(); }
 extern "C" int gc_version(void) { return GC_ABI_VERSION; }
+// The build's source hash (sha256 of the sources and the compile flags, set by
+// __graft_entry__.build_hip): the loader refuses a library built from other sources.
+#ifndef GC_SRC_HASH
+#define GC_SRC_HASH "unhashed"
+#endif
+extern "C" const char* gc_build_hash(void) { return "gymchess-src-hash:" GC_SRC_HASH; }
 extern "C" int gc_get_device_count(int* n) {
     if (!n) return fail("null out pointer");
     HIPCHK(hipGetDeviceCount(n));
@@ -4311,9 +4317,13 @@ extern "C" int gc_env_paired(gc_env* e) {
     return pair_ok(e) && !one_wave ? 1 : 0;
 }
 
+// The quads take a reset board's pick from the start position's table only (Q1 reads it in
+// phase 0, before the ply's outcome is known); a start position without one (> 16 own pieces,
+// or more than RESET_ACTS_MAX moves) runs on the paired kernel, whose pair_ply regenerates the
+// start position's move sets at a reset.
 static bool use_quad(const gc_env* e) {
     static const bool no_quad = getenv("GC_NO_QUAD") != nullptr;  // A/B: the paired kernel
-    return !no_quad && !e->rules && pair_opp(e) == 0;
+    return !no_quad && !e->rules && pair_opp(e) == 0 && e->d.ic.table;
 }
 
 extern "C" int gc_env_rollout_waves(gc_env* e) {

@@ -5,10 +5,43 @@ There is no CPU fallback: if the library is missing or no GPU is visible every c
 fails loudly.
 """
 import ctypes
+import hashlib
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libgymchess.so")
+CSRC = os.path.join(os.path.dirname(_HERE), "csrc")
+HEADER = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "gymchess.h")
+
+# hipcc flags of libgymchess.so (__graft_entry__.build_hip); kernarg preload: the leading
+# arguments of the step kernels arrive in SGPRs
+BUILD_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
+               "-mllvm", "-amdgpu-kernarg-preload-count=16"]
+HASH_TAG = b"gymchess-src-hash:"
+
+
+def source_hash():
+    """sha256 prefix of the library's sources (csrc/*, include/gymchess.h) and BUILD_FLAGS, or
+    None when the sources are not beside the package (an installed copy)"""
+    if not os.path.isdir(CSRC) or not os.path.exists(HEADER):
+        return None
+    h = hashlib.sha256(" ".join(BUILD_FLAGS).encode())
+    for p in sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC)) + [HEADER]:
+        if os.path.isfile(p):
+            h.update(os.path.basename(p).encode() + b"\0")
+            with open(p, "rb") as f:
+                h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def built_hash(path=LIB_PATH):
+    """the source hash embedded in a built library (gc_build_hash's string), read from the file"""
+    with open(path, "rb") as f:
+        data = f.read()
+    k = data.find(HASH_TAG)
+    if k < 0:
+        return None
+    return data[k + len(HASH_TAG): k + len(HASH_TAG) + 16].decode(errors="replace")
 
 # every symbol declared in include/gymchess.h: name -> (restype, argtypes)
 _P = ctypes.c_void_p
@@ -17,6 +50,7 @@ _U64 = ctypes.c_uint64
 SIGNATURES = {
     "gc_last_error": (ctypes.c_char_p, []),
     "gc_version": (_I, []),
+    "gc_build_hash": (ctypes.c_char_p, []),
     "gc_get_device_count": (_I, [_P]),
     "gc_engine_create": (_I, [_I, _P]),
     "gc_engine_destroy": (_I, [_P]),
@@ -89,6 +123,13 @@ def load(path=LIB_PATH):
         raise GymChessError(
             f"{path} not found: the HIP extension is not built (python -c 'import __graft_entry__ as g; g.build()')"
         )
+    if path == LIB_PATH and os.environ.get("GC_ALLOW_STALE_LIB") != "1":
+        want = source_hash()
+        if want is not None and built_hash(path) != want:
+            raise GymChessError(
+                f"{path} was built from other sources (hash {built_hash(path)}, sources {want}): rebuild it "
+                "(python -c 'import __graft_entry__ as g; g.build()')"
+            )
     lib = ctypes.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)

@@ -28,6 +28,9 @@ extern "C" {
 
 const char* gc_last_error(void);
 int gc_version(void);
+/* "gymchess-src-hash:<hex>": the sha256 prefix of the sources and compile flags this library
+ * was built from (the Python loader refuses a library whose hash differs from its sources') */
+const char* gc_build_hash(void);
 int gc_get_device_count(int* n);
 
 /* ---------------------------------------------------------------------------------

@@ -36,6 +36,27 @@ def test_ctypes_binding_covers_header():
     assert sorted(_lib.SIGNATURES) == header_symbols()
     L = _lib.load()  # loads without a GPU; resolves every symbol
     assert L.gc_version() == 1
+    # the library is the build of the sources beside it (content hash, not mtimes)
+    assert L.gc_build_hash().decode() == "gymchess-src-hash:" + _lib.source_hash()
+
+
+def test_loader_refuses_a_library_from_other_sources(tmp_path):
+    """A stale libgymchess.so (its embedded source hash differs from the sources') fails
+    loudly at load instead of being tested silently (in a child process: the loader caches)."""
+    import sys
+
+    from gym_chess_amd import _lib
+
+    stale = tmp_path / "libgymchess.so"
+    data = open(_lib.LIB_PATH, "rb").read()
+    k = data.find(_lib.HASH_TAG) + len(_lib.HASH_TAG)
+    stale.write_bytes(data[:k] + b"0" * 16 + data[k + 16:])
+    code = (f"import sys; sys.path.insert(0, {os.path.join(ROOT, 'gym-chess_amd')!r})\n"
+            "from gym_chess_amd import _lib\n"
+            f"_lib.LIB_PATH = {str(stale)!r}\n"
+            "try:\n    _lib.load(_lib.LIB_PATH)\nexcept _lib.GymChessError as e:\n    print('refused', e)\n")
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, check=True).stdout
+    assert out.startswith("refused") and "other sources" in out, out
 
 
 def test_product_has_no_oracle_dependency():

@@ -480,6 +480,44 @@ def test_step_random_weird_initial_boards_vs_oracle(oracle, k):
         assert (b[i] == fin[i]["final_board"]).all() and list(m[i]) == list(fin[i]["final_meta"]), (k, i)
 
 
+@pytest.mark.parametrize("k", range(12))
+def test_fused_rollouts_weird_initial_boards_vs_oracle(oracle, k):
+    """The fused rollouts (rollout(trace=True) and rollout_device with a device trace) from and
+    resetting to every weird initial board: each ply's action / reward / done / reason, the next
+    action and the final states vs the oracle driver (chess_v2.py:183-217 resets to
+    initial_board; test_benchmark.py:17-31 drives it).  The crowd board (> 16 own pieces) and the
+    279-queens board have no reset pick table, so they must not run on the quads (whose reset
+    pick is the table's) -- rollout_waves says which kernel runs."""
+    from gym_chess_amd.env import BatchedChessEnv
+
+    ib = _weird_initial_boards()[k]
+    n, plies, seed = 70, 300, 2000 + k
+    refs = [oracle.rollout_trace(seed, i, plies + 1, init=ib) for i in range(n)]
+    fin = [oracle.rollout_trace(seed, i, plies, init=ib) for i in range(n)]
+    want = {name: np.stack([r[name][:plies] for r in refs], axis=1) for name in ("action", "reward", "done", "reason")}
+    nxt = np.array([0xFFFF if r["action"][plies] < 0 else r["action"][plies] for r in refs], dtype=np.uint16)
+    for form in ("rollout", "device"):
+        env = BatchedChessEnv(n, device=0, seed=seed, initial_board=ib)
+        if k >= 10:  # the crowd and queens boards: no table, the paired kernel
+            assert env.rollout_waves() == 2, (k, env.rollout_waves())
+        if form == "rollout":
+            _, tr = env.rollout(plies, trace=True)
+        else:
+            buf = env.trace_buffer(plies)
+            env.rollout_device(plies, trace=buf)
+            tr = buf.fetch()
+            buf.close()
+        for name in ("action", "reward", "done", "reason"):
+            got = tr[name]
+            bad = np.argwhere(got != want[name])
+            assert bad.size == 0, (k, form, name, bad[:4].tolist())
+        assert (env.outputs()["next_action"] == nxt).all(), (k, form)
+        b, m = env.boards()
+        for i in range(n):
+            assert (b[i] == fin[i]["final_board"]).all() and list(m[i]) == list(fin[i]["final_meta"]), (k, form, i)
+        env.close()
+
+
 def test_fused_rollout_stats_and_states_vs_oracle(oracle):
     """The paired fused-rollout kernel (k_env_rollout2, no trace): per-board final states and
     the aggregate episode stats of 200 boards x 500 plies == the oracle driver's."""
