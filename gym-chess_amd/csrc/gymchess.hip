@@ -3624,6 +3624,7 @@ struct gc_env {
     u32* sp_ctr_h = nullptr;  // pinned: {slots claimed, failed}
     hipEvent_t sp_ev = nullptr;
     int sp_pending = 0;       // stepping calls since the last counter copy was read
+    bool sp_failed = false;   // an insert failed: every stepping call fails until the windows are cleared
     gc_single_record* srec = nullptr;  // gc_env_single_call's host-mapped record
     gc_single_record* srec_d = nullptr;  // its device address
 };
@@ -3655,8 +3656,29 @@ static void env_free(gc_env* e) {
 // copied to pinned memory; before the next call (or, when the copy has not landed, after at
 // most SPILL_CHECK_LAG calls, synchronously) they are read, and a table past 1/4 is rehashed
 // -- dead entries dropped, doubled when the live ones pass 1/8.  A failed insert (no free
-// slot within SPILL_PROBES) sets a sticky flag: the next call reports it as an error.
+// slot within SPILL_PROBES) sets a sticky flag: the next call reports it as an error, and so
+// does every stepping call after it until every window is cleared (gc_env_reset of all
+// boards, gc_env_set_states, gc_env_load), which starts a fresh table.
+// Multi-step calls (gc_env_step_random, the fused rollouts) cannot wait for the next call:
+// a launch's window generations are published only when it ends, so no entry it makes dead
+// is reclaimed within it.  They run in chunks (spill_chunk): before each, the counters and a
+// census of the windows within SPILL_PER_STEP x SPILL_CHUNK boards of the per-board cap are
+// read, and the chunk is sized so that even if every such window spilled at every step the
+// slots in use stay under half the table (rehashed / doubled first when that leaves fewer
+// than SPILL_CHUNK_MIN steps).
 #define SPILL_CHECK_LAG 4
+#define SPILL_CHUNK 128      // steps per launch of a spill-enabled multi-step call, at most
+#define SPILL_CHUNK_MIN 16   // below this many steps of room the table is rehashed / doubled first
+#define SPILL_PER_STEP 2     // window boards one step adds: the agent's and the opponent's pre-move boards
+#define SPILL_BITS_MAX 30    // 2^30 entries = 64 GiB
+
+// boards whose window is within SPILL_PER_STEP x SPILL_CHUNK boards of the per-board cap
+__global__ void k_spill_census(const u32* __restrict__ meta, int n, u32 thresh, u32* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool near = i < n && hl_of(meta[i]) >= thresh;
+    const unsigned long long b = __ballot(near);
+    if ((threadIdx.x & 63) == 0 && b) atomicAdd(out, (u32)__popcll(b));
+}
 
 __global__ void k_spill_rehash(const u64* __restrict__ old, u32 old_mask, SpillTab nt, const u32* __restrict__ hgen) {
     const size_t slot = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -3680,6 +3702,11 @@ __global__ void k_spill_rehash(const u64* __restrict__ old, u32 old_mask, SpillT
     h.sp_fail();
 }
 
+static int spill_bits_max() {
+    const char* v = getenv("GC_SPILL_BITS_MAX");  // tests: cap the growth to force a failed insert
+    return v && atoi(v) >= 6 && atoi(v) < SPILL_BITS_MAX ? atoi(v) : SPILL_BITS_MAX;
+}
+
 static int spill_bits_for(int n) {
     int b = 14;
     while (b < 22 && (1 << (b - 4)) < n) b++;  // 2^20 entries (64 MiB) at 65 536 boards
@@ -3698,10 +3725,10 @@ static int spill_publish(gc_env* e) {
 static int spill_alloc(gc_env* e, int bits) {
     SpillTab t = {nullptr, nullptr, (1u << bits) - 1};
     if (dalloc(&t.ent, (size_t)8 << bits)) return -1;
-    if (dalloc(&t.ctr, 2)) { (void)hipFree(t.ent); return -1; }
+    if (dalloc(&t.ctr, 4)) { (void)hipFree(t.ent); return -1; }
     hipError_t he = hipMemsetAsync(t.ent, 0, (size_t)64 << bits, e->stream);
-    if (he == hipSuccess) he = hipMemsetAsync(t.ctr, 0, 8, e->stream);
-    if (he == hipSuccess && !e->sp_ctr_h) he = hipHostMalloc(&e->sp_ctr_h, 8, hipHostMallocDefault);
+    if (he == hipSuccess) he = hipMemsetAsync(t.ctr, 0, 16, e->stream);
+    if (he == hipSuccess && !e->sp_ctr_h) he = hipHostMalloc(&e->sp_ctr_h, 16, hipHostMallocDefault);
     if (he == hipSuccess && !e->sp_ev) he = hipEventCreateWithFlags(&e->sp_ev, hipEventDisableTiming);
     if (he != hipSuccess) { (void)hipFree(t.ent); (void)hipFree(t.ctr); return fail(std::string("spill table: ") + hipGetErrorString(he)); }
     if (e->d.ic.spill.ent) (void)hipFree(e->d.ic.spill.ent);
@@ -3709,7 +3736,8 @@ static int spill_alloc(gc_env* e, int bits) {
     e->d.ic.spill = t;
     e->sp_bits = bits;
     e->sp_pending = 0;
-    e->sp_ctr_h[0] = e->sp_ctr_h[1] = 0;
+    e->sp_failed = false;
+    e->sp_ctr_h[0] = e->sp_ctr_h[1] = e->sp_ctr_h[2] = 0;
     return spill_publish(e);
 }
 
@@ -3726,10 +3754,10 @@ static int spill_rehash(gc_env* e, int bits) {
     const SpillTab old = e->d.ic.spill;
     SpillTab t = {nullptr, nullptr, (1u << bits) - 1};
     if (dalloc(&t.ent, (size_t)8 << bits)) return -1;
-    if (dalloc(&t.ctr, 2)) { (void)hipFree(t.ent); return -1; }
+    if (dalloc(&t.ctr, 4)) { (void)hipFree(t.ent); return -1; }
     u32 c[2] = {0, 0};
     hipError_t he = hipMemsetAsync(t.ent, 0, (size_t)64 << bits, e->stream);
-    if (he == hipSuccess) he = hipMemsetAsync(t.ctr, 0, 8, e->stream);
+    if (he == hipSuccess) he = hipMemsetAsync(t.ctr, 0, 16, e->stream);
     if (he == hipSuccess) {
         const size_t slots = (size_t)old.mask + 1;
         k_spill_rehash<<<(unsigned)((slots + BLOCK - 1) / BLOCK), BLOCK, 0, e->stream>>>(old.ent, old.mask, t, e->d.hgen);
@@ -3752,23 +3780,71 @@ static int spill_rehash(gc_env* e, int bits) {
     return spill_publish(e);
 }
 
+static int spill_failed(gc_env* e) {
+    e->sp_failed = true;
+    return fail("repetition spill table: an insert found no free slot (a window outgrew 2^" + std::to_string(e->sp_bits) +
+                " shared entries); results since then are invalid until every window is cleared (gc_env_reset of all "
+                "boards, gc_env_set_states or gc_env_load)");
+}
+
+// every window was cleared (the stream is idle): a failed table starts afresh
+static int spill_windows_cleared(gc_env* e) {
+    if (!e->d.ic.spill.ent || !e->sp_failed) return 0;
+    return spill_alloc(e, e->sp_bits);
+}
+
 // before a stepping call: the counters of the last copy that landed
 static int spill_before(gc_env* e) {
-    if (!e->d.ic.spill.ent || !e->sp_pending) return 0;
+    if (!e->d.ic.spill.ent) return 0;
+    if (e->sp_failed) return spill_failed(e);
+    if (!e->sp_pending) return 0;
     if (e->sp_pending >= SPILL_CHECK_LAG) HIPCHK(hipEventSynchronize(e->sp_ev));
     else if (hipEventQuery(e->sp_ev) != hipSuccess) return 0;  // not landed yet: check next call
     e->sp_pending = 0;
     const u32 used = e->sp_ctr_h[0], failed = e->sp_ctr_h[1];
-    if (failed)
-        return fail("repetition spill table: an insert found no free slot (a window outgrew 2^" +
-                    std::to_string(e->sp_bits) + " shared entries); results since the previous call are invalid");
+    if (failed) return spill_failed(e);
     const u32 cap = 1u << e->sp_bits;
     if (used > cap / 4) {
         HIPCHK(hipStreamSynchronize(e->stream));
         if (spill_rehash(e, e->sp_bits)) return -1;  // drops the dead entries
-        if (e->sp_ctr_h[0] > cap / 8 && spill_rehash(e, e->sp_bits + 1)) return -1;
+        if (e->sp_ctr_h[0] > cap / 8 && e->sp_bits < spill_bits_max() && spill_rehash(e, e->sp_bits + 1)) return -1;
     }
     return 0;
+}
+
+// the steps the next launch of a multi-step call may take (<= want; synchronous): see above
+static int spill_chunk(gc_env* e, int want) {
+    if (!e->d.ic.spill.ent || want <= 0) return want;
+    if (e->sp_failed) return spill_failed(e);
+    const u32 thresh = (u32)(hist_cap(HTAB_BITS_UNCAPPED) - SPILL_PER_STEP * SPILL_CHUNK);
+    bool rehashed = false;
+    for (;;) {
+        u32* ctr = e->d.ic.spill.ctr;
+        HIPCHK(hipMemsetAsync(ctr + 2, 0, 4, e->stream));
+        k_spill_census<<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d.st.meta, e->n, thresh, ctr + 2);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(e->sp_ctr_h, ctr, 12, hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream));
+        e->sp_pending = 0;
+        const u32 used = e->sp_ctr_h[0], near = e->sp_ctr_h[2];
+        if (e->sp_ctr_h[1]) return spill_failed(e);
+        const uint64_t half = (uint64_t)1 << (e->sp_bits - 1);
+        const uint64_t room = half > used ? half - used : 0;
+        uint64_t steps = near ? room / ((uint64_t)SPILL_PER_STEP * near) : (uint64_t)SPILL_CHUNK;
+        if (steps > SPILL_CHUNK) steps = SPILL_CHUNK;
+        if (steps > (uint64_t)want) steps = (uint64_t)want;
+        const uint64_t enough = want < SPILL_CHUNK_MIN ? (uint64_t)want : (uint64_t)SPILL_CHUNK_MIN;
+        if (steps >= enough) return (int)steps;
+        if (e->sp_bits >= spill_bits_max()) {
+            if (steps >= 1 || rehashed) return steps >= 1 ? (int)steps : 1;  // (a failed insert would be reported)
+            if (spill_rehash(e, e->sp_bits)) return -1;  // the dead entries, at least
+            rehashed = true;
+            continue;
+        }
+        // too little room: drop the dead entries first, then double
+        if (spill_rehash(e, rehashed ? e->sp_bits + 1 : e->sp_bits)) return -1;
+        rehashed = true;
+    }
 }
 
 // after a stepping call: copy the counters (asynchronously) for the next check
@@ -4054,6 +4130,7 @@ extern "C" int gc_env_reset(gc_env* e, const uint8_t* mask) {
     launch_reset(e, mask ? e->mask : nullptr, 1);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(e->stream));
+    if (!mask && spill_windows_cleared(e)) return -1;
     e->policy_ready = true;
     return 0;
 }
@@ -4257,7 +4334,12 @@ extern "C" int gc_env_step_random(gc_env* e, int n_plies) {
     if (!e) return fail("null env");
     if (!e->policy_ready) return fail("policy actions stale: call gc_env_reset or gc_env_select_random first");
     HIPCHK(hipSetDevice(e->device));
-    if (spill_before(e) || step_random(e, n_plies)) return -1;
+    if (spill_before(e)) return -1;
+    for (int p = 0; p < n_plies;) {  // one chunk unless the env spills (spill_chunk)
+        const int k = spill_chunk(e, n_plies - p);
+        if (k < 0 || step_random(e, k)) return -1;
+        p += k;
+    }
     return spill_after(e);
 }
 static int step_random(gc_env* e, int n_plies) {
@@ -4353,8 +4435,9 @@ static int issue_rollout(gc_env* e, int n_plies, uint64_t* d_trace, bool stats) 
     const EnvDev& d = e->d;
     const ResetInfo r = reset_info(e);
     const int grid = (e->n + PAIR_BOARDS * PAIRS_WG - 1) / (PAIR_BOARDS * PAIRS_WG), bs = 2 * PAIR_BOARDS * PAIRS_WG;
-    for (int p0 = 0; p0 < n_plies; p0 += ROLLOUT_MAX_PLIES) {
-        const int k = n_plies - p0 < ROLLOUT_MAX_PLIES ? n_plies - p0 : ROLLOUT_MAX_PLIES;
+    for (int p0 = 0, k = 0; p0 < n_plies; p0 += k) {
+        k = spill_chunk(e, n_plies - p0 < ROLLOUT_MAX_PLIES ? n_plies - p0 : ROLLOUT_MAX_PLIES);
+        if (k < 0) return -1;
         u64* tr = d_trace ? reinterpret_cast<u64*>(d_trace) + (size_t)p0 * e->n : nullptr;
         const u32 ri = r.rinfo | ((u32)k << 18);
         if (pair && use_quad(e)) {
@@ -4473,6 +4556,7 @@ extern "C" int gc_env_set_states(gc_env* e, const int8_t* boards, const uint8_t*
     else k_env_import<<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->mbox, e->m8, e->d, 0);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(e->stream));
+    if (spill_windows_cleared(e)) return -1;
     e->policy_ready = false;
     return 0;
 }

@@ -195,3 +195,106 @@ def test_gpu_spill_table_growth(oracle, long_boards, monkeypatch):
     for i in range(n):
         assert (b[i] == fins[i]["final_board"]).all() and list(m[i]) == list(fins[i]["final_meta"]), i
     env.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("form", ["device", "launched"])
+def test_gpu_spill_table_grows_within_one_call(oracle, long_boards, monkeypatch, form):
+    """one multi-step call can outgrow the table -- a launch publishes its window
+    generations only when it ends, so nothing is reclaimed inside it.  Multi-step calls run in
+    chunks sized by a census of the windows near the per-board cap (spill_chunk), growing the
+    table between them: a table started at 2^10 slots survives ONE 2 000-step call (the fused
+    rollout with its trace, or the launched step), every step == the oracle's."""
+    from gym_chess_amd.env import BatchedChessEnv
+
+    monkeypatch.setenv("GC_SPILL_BITS", "10")
+    init = kb_board()
+    n, plies = 96, 2000
+    env = BatchedChessEnv(n, device=0, seed=SEED, initial_board=init, opponent="random", player_color="BLACK")
+    assert env.spill_info()["bits"] == 10
+    tb = env.trace_buffer(plies) if form == "device" else None
+    if form == "device":
+        env.rollout_device(plies, tb)
+    else:
+        env.step_random(plies)
+    info = env.spill_info()  # raises if an insert failed
+    assert info["bits"] > 10 and info["live"] > 0, info
+    with _pool() as ex:
+        refs = list(ex.map(lambda i: oracle.rollout_trace(SEED, i, plies, init=init, opponent=1, agent_white=False),
+                           range(n)))
+    b, m = env.boards()
+    tr = tb.fetch() if tb is not None else None
+    for i, ref in enumerate(refs):
+        assert (b[i] == ref["final_board"]).all() and list(m[i]) == list(ref["final_meta"]), i
+        if tr is not None:
+            for k in ("action", "reward", "done", "reason"):
+                assert (tr[k][:, i] == ref[k]).all(), (i, k, np.nonzero(tr[k][:, i] != ref[k])[0][:3])
+    env.close()
+
+
+@pytest.mark.gpu
+def test_gpu_spill_full_size_black_agent_rollout(oracle):
+    """configs[2]'s 65 536 boards, a BLACK agent from the sparse board, 3 000 steps in ONE
+    rollout_device call with the default table: no episode ends for a window's length (reason
+    10 never appears), no insert fails, and 8 boards spread over the batch equal the oracle
+    step for step (the full-size spill path was untested)."""
+    from gym_chess_amd.env import BatchedChessEnv
+
+    init = kb_board()
+    n, plies = 65536, PLIES
+    env = BatchedChessEnv(n, device=0, seed=SEED, initial_board=init, opponent="random", player_color="BLACK")
+    bits0 = env.spill_info()["bits"]
+    tb = env.trace_buffer(plies)
+    env.rollout_device(plies, tb)
+    info = env.spill_info()
+    assert info["live"] > 0, info
+    tr = tb.fetch()
+    tb.close()
+    assert not (tr["reason"] == 10).any()
+    ids = [int(x) for x in np.linspace(0, n - 1, 8).round()]
+    with _pool() as ex:
+        refs = list(ex.map(lambda i: oracle.rollout_trace(SEED, i, plies, init=init, opponent=1, agent_white=False), ids))
+    b, m = env.boards()
+    for i, ref in zip(ids, refs):
+        for k in ("action", "reward", "done", "reason"):
+            assert (tr[k][:, i] == ref[k]).all(), (i, k, np.nonzero(tr[k][:, i] != ref[k])[0][:3])
+        assert (b[i] == ref["final_board"]).all() and list(m[i]) == list(ref["final_meta"]), i
+    print(f"spill table 2^{bits0} -> 2^{info['bits']}, {info['used']} slots used, {info['live']} live")
+    env.close()
+
+
+@pytest.mark.gpu
+def test_gpu_spill_failure_is_sticky(oracle, monkeypatch):
+    """after a failed insert every stepping call fails (not every other one) until
+    all windows are cleared; a full reset starts a fresh table and play goes on.  Forced with
+    a 2^6-slot table that may not grow (GC_SPILL_BITS_MAX) and single-step API calls."""
+    from gym_chess_amd._lib import GymChessError
+    from gym_chess_amd.env import BatchedChessEnv
+
+    monkeypatch.setenv("GC_SPILL_BITS", "6")
+    monkeypatch.setenv("GC_SPILL_BITS_MAX", "6")
+    init = kb_board()
+    n = 96
+    env = BatchedChessEnv(n, device=0, seed=SEED, initial_board=init, opponent="random", player_color="BLACK")
+    io = env.device_io(mask=False, obs=False, count=False)
+    failed_at = None
+    for t in range(PLIES):
+        try:
+            env.step_device(io, autoreset=True)
+            env.synchronize()
+        except GymChessError as e:
+            assert "no free slot" in str(e), str(e)
+            failed_at = t
+            break
+    assert failed_at is not None, "the 64-slot table never overflowed"
+    for _ in range(3):  # sticky: every stepping call fails, not every other one
+        with pytest.raises(GymChessError, match="no free slot"):
+            env.step_device(io, autoreset=True)
+        with pytest.raises(GymChessError, match="no free slot"):
+            env.step_random(1)
+    env.reset()  # every window cleared: a fresh table
+    assert env.spill_info()["used"] == 0
+    env.step_random(50)
+    assert env.spill_info()["bits"] == 6
+    io.close()
+    env.close()
