@@ -176,18 +176,18 @@ def test_gpu_external_actions_spill_and_checkpoint(oracle):
 def test_gpu_spill_table_growth(oracle, long_boards, monkeypatch):
     """The host-side growth path: a spill table started at 2^10 slots (GC_SPILL_BITS) is
     rehashed and doubled between calls as the windows outgrow it; trajectories still equal
-    the oracle's."""
+    the oracle's.  (2^8 slots: ~120 live entries need a larger table.)"""
     from gym_chess_amd.env import BatchedChessEnv
 
-    monkeypatch.setenv("GC_SPILL_BITS", "10")
+    monkeypatch.setenv("GC_SPILL_BITS", "8")
     init = kb_board()
     n, plies = 96, 2000
     env = BatchedChessEnv(n, device=0, seed=SEED, initial_board=init, opponent="random", player_color="BLACK")
-    assert env.spill_info()["bits"] == 10
+    assert env.spill_info()["bits"] == 8
     for _ in range(plies):
         env.step_random(1)
     info = env.spill_info()
-    assert info["bits"] > 10 and info["live"] > 0, info
+    assert info["bits"] > 8 and info["live"] > 0, info
     b, m = env.boards()
     with _pool() as ex:
         fins = list(ex.map(lambda i: oracle.rollout_trace(SEED, i, plies, init=init, opponent=1, agent_white=False),
@@ -203,22 +203,22 @@ def test_gpu_spill_table_grows_within_one_call(oracle, long_boards, monkeypatch,
     """one multi-step call can outgrow the table -- a launch publishes its window
     generations only when it ends, so nothing is reclaimed inside it.  Multi-step calls run in
     chunks sized by a census of the windows near the per-board cap (spill_chunk), growing the
-    table between them: a table started at 2^10 slots survives ONE 2 000-step call (the fused
+    table between them: a table started at 2^8 slots survives ONE 2 000-step call (the fused
     rollout with its trace, or the launched step), every step == the oracle's."""
     from gym_chess_amd.env import BatchedChessEnv
 
-    monkeypatch.setenv("GC_SPILL_BITS", "10")
+    monkeypatch.setenv("GC_SPILL_BITS", "8")
     init = kb_board()
     n, plies = 96, 2000
     env = BatchedChessEnv(n, device=0, seed=SEED, initial_board=init, opponent="random", player_color="BLACK")
-    assert env.spill_info()["bits"] == 10
+    assert env.spill_info()["bits"] == 8
     tb = env.trace_buffer(plies) if form == "device" else None
     if form == "device":
         env.rollout_device(plies, tb)
     else:
         env.step_random(plies)
     info = env.spill_info()  # raises if an insert failed
-    assert info["bits"] > 10 and info["live"] > 0, info
+    assert info["bits"] > 8 and info["live"] > 0, info
     with _pool() as ex:
         refs = list(ex.map(lambda i: oracle.rollout_trace(SEED, i, plies, init=init, opponent=1, agent_white=False),
                            range(n)))

@@ -27,7 +27,7 @@ PERFTB="python bench.py --no-cpu-baseline --steps 5 --warmup 5 --settle 0 --laun
 for s in ${STEPS:-smoke pytest bench prof}; do
   case $s in
     smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    pytest) step pytest 1100 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread ;;
+    pytest) step pytest 1100 python -u -m pytest ${PYTEST_ARGS:-tests} -x -v -m gpu --timeout 300 --timeout-method thread ;;  # PYTEST_ARGS: a subset
     bench)  step bench 600 python bench.py ${BENCH_ARGS:-} ;;
     prof)   step prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --no-cpu-baseline --oracle-perft-roots 0 ;;  # bench defaults: the same launches bench.py times
     profs)  step profs 300 rocprofv3 --kernel-trace --stats -d $OUT/profs -o run --output-format csv -- python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --oracle-perft-roots 0 ;;  # the driver's command
