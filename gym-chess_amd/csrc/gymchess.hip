@@ -1829,14 +1829,14 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
 // The ply's parallel parts -- the enemy map's three parts, the own slider sets' two halves --
 // go to their own waves, so each wave's chain is shorter and a SIMD holds four of them:
 //
-//   phase 0   Q0: applies the action (post-move board to LDS)
-//             Q1: the 3-fold probe of the pre-move board, the Philox word, the reset table read
-//   phase 1   Q0: checkers, check mask, pins                   Q1: enemy leaper attacks, the
-//             Q2: enemy orthogonal slider attacks                   mover's own check flag
-//             Q3: enemy diagonal slider attacks
-//   phase 2   Q0: castles, pawn / knight / king sets            Q1: the 3-fold commit
-//             Q2: the own rook/queen direction sets            Q3: the bishop/queen ones
-//   phase 3   Q0: the outcome and the pick of the next action   Q1: the outcome, the stores
+//   phase 0   Q0: applies the action (the last ply's pick) -> post-move board to LDS
+//             Q1: the Philox word, the reset table read (its window probe is in flight)
+//   phase 1   Q0: checkers, check mask, pins                   Q1: the mover's own check flag
+//             Q2: enemy leaper + orthogonal slider attacks     Q3: enemy diagonal slider attacks
+//   phase 2   Q0: castles, pawn and knight sets                Q1: the 3-fold commit
+//             Q2: the own rook/queen direction sets, king sets Q3: the bishop/queen ones
+//   phase 3   Q0: the outcome                                  Q1: the outcome, the stores, the
+//             Q2: the pick of the next action                      next ply's window probe
 //
 // Q0 and Q1 carry the board's state between plies; Q2 and Q3 are stateless (the post-move
 // board and the pins come through LDS) and compute their sets unconditionally -- ignored,
@@ -1866,7 +1866,8 @@ struct QuadLds {
     u32 act[QUAD_BOARDS];            // Q0 -> Q1: this ply's action (phase 0)
     u32 pick[QUAD_BOARDS];           // Q2 -> Q0: the policy's pick from this ply's move sets (phase 3)
     u32 castles[QUAD_BOARDS];        // Q0 -> Q2: the castles (phase 2)
-    u64 cw0[QUAD_BOARDS];            // Q0 -> Q2: its sets' byte counts (word 0)
+    u64 cw0[QUAD_BOARDS];            // Q0 -> Q2: its sets' byte counts (words 0, 1: pawns, knights)
+    u64 cw1[QUAD_BOARDS];
     Pos rp;                          // the reset position (read at a reset: no registers held for it)
 };
 // one set of the next side's moves into LDS, its count into the packed byte counts and the total
@@ -1976,7 +1977,7 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
     } else if (R == 1) {  // (the leaper attacks went to Q2: phase 1 was Q1's longest)
         my_chk = mv && mover_checked(s, ns, white, a);
         L.f1[l] = my_chk ? 1u : 0u;
-    } else if (R == 2) {
+    } else if (R == 2) {  // (the leaper attacks on Q1 instead -- its SIMDs the lighter pair here -- measured neutral)
         L.enemy[1][l] = g.ks >= 0 ? side_attacks_leapers(ns, !g.white) | side_attacks_orth(ns, !g.white) : 0ull;
     } else {
         L.enemy[2][l] = g.ks >= 0 ? side_attacks_diag(ns, !g.white) : 0ull;
@@ -1985,8 +1986,9 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
     pair_barrier();
     PST(3);
     // ---- phase 2
+#define QUAD_ENEMY(l) (L.enemy[1][l] | L.enemy[2][l])
     if (R == 0) {
-        g.enemy_att = L.enemy[1][l] | L.enemy[2][l];
+        g.enemy_att = QUAD_ENEMY(l);
         gen_castles(ns, g);  // lib.rs:578-610 with the whole enemy map
         my_chk = L.f1[l] != 0;
     } else if (R == 1) {
@@ -1995,7 +1997,7 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
         g.checkmask = L.pin3[0][l];
         g.pinned = L.pin3[1][l];
         g.pinrays = L.pin3[2][l];
-        if (R == 2) g.enemy_att = L.enemy[1][l] | L.enemy[2][l];  // for the king sets
+        if (R == 2) g.enemy_att = QUAD_ENEMY(l);  // for the king sets
     }
     const bool opp_chk = g.in_check;
     const bool both = opp_chk && my_chk;  // lib.rs:1442-1446
@@ -2008,9 +2010,14 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
             u64 T[SW_SETS];
             sw_pawns(ns, g, T);
             Q.put_all<SW_P1, SW_N>(T + SW_P1);
+            // the knight sets here, not on Q3: Q0's SIMDs (Q0 + Q2) are the lighter pair in phase 2
+            // (same-box A/B: 14.81 vs 14.59e9 at K = 1 000, 4.62 vs 4.70 us per ply at K = 20)
+            sw_knights(ns, g, T);
+            Q.put_all<SW_N, SW_ORTH>(T + SW_N);
             Q.part += popc(g.castles);
         }
         L.cw0[l] = Q.cw[0];
+        L.cw1[l] = Q.cw[1];
         L.castles[l] = g.castles;
     } else if (R == 1) {
         if (mv && !both) {
@@ -2031,8 +2038,6 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
         for (int k = 0; k < 4; k++) L.cwx[0][k][l] = Q.cw[k];
     } else {
         u64 T[SW_SETS];
-        sw_knights(ns, g, T);
-        Q.put_all<SW_N, SW_ORTH>(T + SW_N);
         sw_diag(ns, g, T);
         Q.put_all<SW_DIAG, SW_K>(T + SW_DIAG);
         L.part[3][l] = (u32)Q.part;
@@ -2064,6 +2069,7 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
 #pragma unroll
         for (int k = 0; k < 4; k++) cw[k] = Q.cw[k] | L.cwx[OTHER][k][l];
         cw[0] |= L.cw0[l];
+        cw[1] |= L.cw1[l];
         g.castles = L.castles[l];
         // (a board whose generation is not due reads stale sets here: its pick is not taken)
         L.pick[l] = total > 0 ? (u32)sw_pick_lds(L, l, g, cw, total, (int)scale_rank(L.x0[l], (u32)total)) : (u32)A_NONE;
@@ -2212,7 +2218,9 @@ __device__ __forceinline__ void quad_run(uint8_t* __restrict__ slab, int nn, uin
         io.draw[i] = d;
     } else {
         io.store(i, s);
-        h.flush(g0);
+        // (h.flush through io's freshly derived pointer: h's own, kept from the entry load across
+        // the whole loop, was the kernel's one spill -- and a private segment slows every wave's launch)
+        if (h.gen() != g0) io.hgen[i] = h.gen();
         io.nsteps[i] = nst;
         io.reward[i] = o.reward;
         io.done[i] = (uint8_t)o.done;
