@@ -96,6 +96,8 @@ def parse():
                     help="also time the API-shaped step on device buffers (mask + obs out; 0 = skip)")
     ap.add_argument("--single-episodes", type=int, default=10,
                     help="configs[0]: the reference benchmark driver on the single-board env (0 = skip)")
+    ap.add_argument("--concurrent-ms", type=float, default=0.0,
+                    help="replicas' common-interval leg (>= this many ms per replica); always on (250 ms) for N > 1")
     ap.add_argument("--perft-depth", type=int, default=5)
     ap.add_argument("--perft-subsample", type=int, default=256,
                     help="roots of the fixed strided subsample checked (and CPU-timed) one ply shallower")
@@ -436,6 +438,38 @@ def variant_legs(args, rep, n):
     return out
 
 
+def concurrent_leg(args, rep, ctx, n, s_per_step):
+    """Replicas measured over a common interval: the headline's K-step
+    regions are ~0.1 ms, far below the replicas' barrier skew, so they need not overlap and N
+    of them say nothing about contention.  Here every replica repeats the same K-step launch
+    R times back to back, R chosen (the same on every rank) so a region lasts >= --concurrent-ms;
+    each region's begin / end on CLOCK_MONOTONIC (node-wide) gives the union wall time and the
+    fraction of the longest region common to all (min_overlap)."""
+    ms = args.concurrent_ms if args.concurrent_ms > 0 else 250.0
+    reps = max(1, int(-(-ms / 1e3 // (s_per_step * max(args.steps, 1)))))
+    reps = int(rep.max(reps))
+    s0 = [int(c[0].outputs()["nsteps"].sum()) for c in ctx]
+
+    def run(rp):
+        env, tb = ctx[rep.local.index(rp)][:2]
+        env.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            env.rollout_device(args.steps, tb)
+        env.synchronize()
+        return None, time.perf_counter() - t0, t0
+
+    _, dt = rep.timed(run)
+    ov = rep.last_overlap
+    s1 = [int(c[0].outputs()["nsteps"].sum()) for c in ctx]
+    steps = rep.sum(sum(b - a for a, b in zip(s0, s1)))
+    wall = ov["union_wall_s"] if ov else dt
+    return {"value": steps / wall, "unit": "env_steps/s", "launches_per_replica": reps, "steps_per_launch": args.steps,
+            "env_steps": steps, "union_wall_s": wall, "max_region_s": dt, "overlap": ov,
+            "form": "every replica repeats the headline's K-step launch back to back over a common interval; "
+                    "value = all replicas' env.steps / the union of their regions"}
+
+
 def launched_leg(args, rep, envs, n):
     """The launched form of the same step: one k_env_step2 launch per ply over two
     board-range streams (gc_env_step_random), --launched-steps plies; roofline of k_env_step2
@@ -505,9 +539,10 @@ def main():
         t0 = time.perf_counter()
         env.rollout_device(args.steps, tb, events=(0, 1))  # K env.step() of every board, one launch, per-step trace
         env.synchronize()
-        return None, time.perf_counter() - t0
+        return None, time.perf_counter() - t0, t0
 
     _, dt_max = rep.timed(step)
+    region_overlap = rep.last_overlap
     kern_ms = [e.elapsed_ms(0, 1) for e in envs]
     s1 = [int(e.outputs()["nsteps"].sum()) for e in envs]
     w1 = [e.window_sum() for e in envs]
@@ -547,6 +582,8 @@ def main():
                            "x this launch's steps"}
 
     extra = {}
+    if rep.world_size > 1 or args.concurrent_ms > 0:
+        extra["concurrent"] = concurrent_leg(args, rep, ctx, n, dt_max / max(args.steps, 1))
     if args.launched_steps > 0:
         extra["launched_step"] = launched_leg(args, rep, envs, n)
     for e, tb, tbw in ((c[0], c[1], c[2]) for c in ctx):
@@ -590,6 +627,7 @@ def main():
                        "settle_plies": args.settle,
                        "step_form": f"K steps = one {rollout_kernel} launch (gc_env_rollout_device), "
                                     "per-step trace in HBM"},
+            "region_overlap": region_overlap,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": rollout_kernel, "avg_launch_us": launch_s * 1e6,

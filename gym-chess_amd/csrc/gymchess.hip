@@ -2355,16 +2355,19 @@ __global__ void __launch_bounds__(BLOCK) k_env_rollout(EnvDev e, int plies, u64*
 // opponent's opening move (3-fold verdict discarded, move_count 1), SYNC = no change.  Every
 // op writes the resulting state, outputs and the side to move's move list in reference order
 // into one host-mapped record (gc_single_record): one launch, no copy.
-enum { SOP_RESET = 0, SOP_AGENT = 1, SOP_REPLY = 2, SOP_OPEN = 3, SOP_SYNC = 4 };
+// SET = the state setter (chess_v2.py:315-323): the board and the six flags from the record's
+// own fields (written by the host before the launch); the side to move, move_count, done and
+// the 3-fold window stay, as in the reference.
+enum { SOP_RESET = 0, SOP_AGENT = 1, SOP_REPLY = 2, SOP_OPEN = 3, SOP_SYNC = 4, SOP_SET = 5 };
 static_assert(sizeof(gc_single_record) == 728, "gym_chess_amd.single._REC mirrors this layout");
 __device__ __noinline__ void single_op(const EnvDev& e, int i, int op, int action, int flags, LdsScratch& scr,
-                                       gc_single_record* __restrict__ rec);
+                                       gc_single_record* __restrict__ rec, const gc_single_record* in);
 __global__ void __launch_bounds__(64) k_single(EnvDev e, int i, int op, int action, int flags,
                                                gc_single_record* __restrict__ hrec) {
     __shared__ u64 lds_scr[SCRATCH_SLOTS * BLOCK];
     __shared__ gc_single_record lrec;  // built here, then written to host memory by every lane
     LdsScratch scr{lds_scr + threadIdx.x};
-    if (threadIdx.x == 0) single_op(e, i, op, action, flags, scr, &lrec);
+    if (threadIdx.x == 0) single_op(e, i, op, action, flags, scr, &lrec, hrec);
     __syncthreads();
     const uint32_t* src = reinterpret_cast<const uint32_t*>(&lrec);
     uint32_t* dst = reinterpret_cast<uint32_t*>(hrec);
@@ -2374,7 +2377,7 @@ __global__ void __launch_bounds__(64) k_single(EnvDev e, int i, int op, int acti
 }
 
 __device__ __noinline__ void single_op(const EnvDev& e, int i, int op, int action, int flags, LdsScratch& scr,
-                                       gc_single_record* __restrict__ rec) {
+                                       gc_single_record* __restrict__ rec, const gc_single_record* in) {
     Pos s = e.st.load(i);
     const u32 g0 = e.hgen[i];
     DevHist h = e.hist(i, g0);
@@ -2437,6 +2440,11 @@ __device__ __noinline__ void single_op(const EnvDev& e, int i, int op, int actio
         const int rc = env_ply(s, h, action, g, ms, scr, &mr, &rep, &chk);
         if (rc == 1) status = 1;
         else s.meta = (s.meta & ~(u32)M_DONE) + (1u << M_MC_SHIFT);
+    } else if (op == SOP_SET) {  // 315-323: board, rights, checks; nothing else changes
+        const u32 m = (s.meta & ~(u32)(M_RIGHTS | M_WCHK | M_BCHK)) | (in->rights[0] ? M_WKC : 0u) |
+                      (in->rights[1] ? M_WQC : 0u) | (in->rights[2] ? M_BKC : 0u) | (in->rights[3] ? M_BQC : 0u) |
+                      (in->checked[0] ? M_WCHK : 0u) | (in->checked[1] ? M_BCHK : 0u);
+        s = from_mailbox(in->board, m);
     }
     if (status == 0 && op != SOP_SYNC) {
         h.commit();
@@ -4162,7 +4170,7 @@ extern "C" int gc_env_single_call(gc_env* e, int board, int op, int action, int 
     if (!e || !rec) return fail("null argument");
     if (!e->srec) return fail("call gc_env_single_setup first");
     if (board < 0 || board >= e->n) return fail("board index out of range");
-    if (op < SOP_RESET || op > SOP_SYNC) return fail("op: 0 reset, 1 agent, 2 reply, 3 open, 4 sync");
+    if (op < SOP_RESET || op > SOP_SYNC) return fail("op: 0 reset, 1 agent, 2 reply, 3 open, 4 sync (5 set: gc_env_single_set)");
     if (op != SOP_RESET && op != SOP_SYNC && (action < 0 || action > A_RESIGN))
         return fail("action out of range [0, 4100]");
     HIPCHK(hipSetDevice(e->device));
@@ -4170,6 +4178,28 @@ extern "C" int gc_env_single_call(gc_env* e, int board, int op, int action, int 
     k_single<<<1, 64, 0, e->stream>>>(e->d, board, op, action, flags, e->srec_d);
     HIPCHK(hipGetLastError());
     if (spill_after(e) || gc_env_synchronize(e)) return -1;
+    e->policy_ready = false;
+    *rec = e->srec;
+    return 0;
+}
+
+// the state setter (chess_v2.py:315-323) of one board: its pieces and the six flags; the side
+// to move, move_count, done and the 3-fold window stay (k_single's SET)
+extern "C" int gc_env_single_set(gc_env* e, int board, const int8_t* board64, const uint8_t* flags6,
+                                 const gc_single_record** rec) {
+    if (!e || !board64 || !flags6 || !rec) return fail("null argument");
+    if (!e->srec) return fail("call gc_env_single_setup first");
+    if (board < 0 || board >= e->n) return fail("board index out of range");
+    for (int k = 0; k < 64; k++)
+        if (board64[k] < -6 || board64[k] > 6) return fail("board: piece ids are -6..6");
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipStreamSynchronize(e->stream));  // the record is the launch's input here
+    memcpy(e->srec->board, board64, 64);
+    for (int k = 0; k < 4; k++) e->srec->rights[k] = flags6[k] ? 1 : 0;
+    for (int k = 0; k < 2; k++) e->srec->checked[k] = flags6[4 + k] ? 1 : 0;
+    k_single<<<1, 64, 0, e->stream>>>(e->d, board, SOP_SET, 0, 0, e->srec_d);
+    HIPCHK(hipGetLastError());
+    if (gc_env_synchronize(e)) return -1;
     e->policy_ready = false;
     *rec = e->srec;
     return 0;

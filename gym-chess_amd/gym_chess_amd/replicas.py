@@ -110,6 +110,22 @@ class _FileGroup:
         return out
 
 
+def overlap(spans):
+    """How the timed regions [begin, end) of N replicas overlapped in wall time: union_wall_s
+    (first begin to last end), the common interval (last begin to first end) as a fraction of
+    the longest region (min_overlap: 1 = all ran over the same interval, 0 = some two never
+    overlapped) and the begin skew."""
+    spans = [(float(a), float(b)) for a, b in spans]
+    if not spans:
+        return None
+    first, last = min(a for a, _ in spans), max(b for _, b in spans)
+    common = min(b for _, b in spans) - max(a for a, _ in spans)
+    longest = max(b - a for a, b in spans)
+    return {"replicas": len(spans), "union_wall_s": last - first,
+            "min_overlap": max(0.0, common) / longest if longest > 0 else 1.0,
+            "begin_skew_s": max(a for a, _ in spans) - first, "longest_s": longest}
+
+
 class Replicas:
     """mode: None = "processes" under a launcher (WORLD_SIZE in the environment or world_size
     given), else "threads"; "threads" forces one process with a thread per device whatever
@@ -142,6 +158,7 @@ class Replicas:
             self.local = [Replica(r, d) for r, d in enumerate(devs)]
         self._group = None
         self._dist = None
+        self.last_overlap = None
 
     def init(self):
         if self.mode == "processes" and self.world_size > 1:
@@ -190,7 +207,10 @@ class Replicas:
     def timed(self, fn):
         """Barrier, then fn(replica) on every local replica started together (a thread
         barrier), each timing itself; returns (results, the max of the replicas' seconds over
-        the whole job).  fn must return (result, seconds)."""
+        the whole job).  fn returns (result, seconds) or (result, seconds, t_begin) with t_begin
+        its region's start by time.perf_counter() -- CLOCK_MONOTONIC, one clock for every
+        process of the node -- and then self.last_overlap describes how the regions of all
+        replicas of all ranks overlapped (overlap())."""
         gate = threading.Barrier(len(self.local))
 
         def body(rp):
@@ -199,7 +219,22 @@ class Replicas:
 
         self.barrier()
         out = self.run(body)
-        return [r for r, _ in out], self.max(max(dt for _, dt in out))
+        spans = [(o[2], o[2] + o[1]) for o in out if len(o) > 2]
+        self.last_overlap = overlap(self.allgather(spans)) if len(spans) == len(out) else None
+        return [o[0] for o in out], self.max(max(o[1] for o in out))
+
+    def allgather(self, value):
+        """every rank's value (JSON-able), in rank order, concatenated when they are lists"""
+        if self._group is not None:
+            vals = self._group.allgather(value)
+        elif self._dist is not None:
+            vals = [None] * self.world_size
+            self._dist.all_gather_object(vals, value)
+        else:
+            vals = [value]
+        if all(isinstance(v, list) for v in vals):
+            return [x for v in vals for x in v]
+        return vals
 
     # ------------------------------------------------------------------ across processes
     def barrier(self):

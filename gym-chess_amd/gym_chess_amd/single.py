@@ -21,10 +21,19 @@ random policy returns "resign", which maps to no action and fails in action_to_m
 (TypeError), and the engine's both-kings-checked error raises SystemError (lib.rs:1442-1446),
 both as in the reference.
 
+saved_boards is the reference's dict (chess_v2.py:192, 404-405: every pre-move board since
+reset, keyed by encode_board's string) kept on the host beside the device's 3-fold window
+(device_window(): the boards since the last pawn move or capture, the only ones that can
+recur, with which the device decides the 3-fold end).  Assigning env.state (315-323) changes
+the board and the six flags only: the side to move, move_count, done, saved_boards and the
+device window stay, and possible_moves stays the list of the board before, as in the
+reference -- the next step() validates against it.
+
 Differences: action_to_move_str returns the move string (the reference's version references
-an undefined name, chess_v2.py:532); saved_boards reads the live 3-fold window from the
-device -- the boards since the last pawn move or capture, the only ones that can recur --
-where the reference keeps every board since reset; assigning env.state restarts the window.
+an undefined name, chess_v2.py:532); a state dict missing a flag sets it False (the reference
+stores None, which its engine then rejects); after a state assignment, an action that the
+stale list holds but the new board does not allow raises NotImplementedError (the reference
+would apply it unchecked through next_state, lib.rs:679-784).
 
 `backend=` takes any object with the single-board op protocol (`call(op, action, flags)` ->
 record); the tests plug in the CPU oracle's restatement to check this class without a GPU.
@@ -32,6 +41,7 @@ record); the tests plug in the CPU oracle's restatement to check this class with
 get_possible_moves / get_castle_moves / next_state with explicit states.
 """
 import sys
+from collections import defaultdict
 from io import StringIO
 
 import numpy as np
@@ -42,6 +52,7 @@ from .codec import (BLACK, CASTLE_KING_SIDE_BLACK, CASTLE_KING_SIDE_WHITE, CASTL
                     WIN_REWARD)
 
 MOVES_MAX = 149  # chess_v2.py:141
+_ENCODE = "0ABCDEFfedcba"  # chess_v2.py:600: piece id -> character (negative ids from the end)
 
 # chess_v2.py:64-84 (icons and descriptions by piece id)
 _ICON = {-6: "♙", -5: "♘", -4: "♗", -3: "♖", -2: "♕", -1: "♔", 0: ".",
@@ -126,12 +137,17 @@ class DeviceBoard:
             self._view = np.frombuffer(buf, dtype=_REC, count=1)[0]
         return self._view
 
-    def set_state(self, board, meta):
-        """board int8[64], meta uint8[8]; restarts the window (gc_env_set_states)"""
+    def set_state(self, board, flags6):
+        """the state setter: board int8[64], flags6 = the 4 rights + 2 check flags; the side to
+        move, move_count, done and the window stay (gc_env_single_set) -> the record"""
         b = np.ascontiguousarray(board, dtype=np.int8).reshape(64)
-        m = np.ascontiguousarray(meta, dtype=np.uint8).reshape(8)
-        self._check(self._L.gc_env_set_states(self._h, b.ctypes.data_as(self._ct.c_void_p),
-                                              m.ctypes.data_as(self._ct.c_void_p)))
+        f = np.ascontiguousarray(flags6, dtype=np.uint8).reshape(6)
+        self._check(self._L.gc_env_single_set(self._h, 0, b.ctypes.data_as(self._ct.c_void_p),
+                                              f.ctypes.data_as(self._ct.c_void_p), self._ct.byref(self._rec)))
+        if self._view is None:
+            buf = (self._ct.c_uint8 * _REC.itemsize).from_address(self._rec.value)
+            self._view = np.frombuffer(buf, dtype=_REC, count=1)[0]
+        return self._view
 
     def window(self):
         """the live 3-fold window: {board bytes: count}"""
@@ -231,8 +247,16 @@ class ChessEnv:
         pre-move board (chess_v2.py:409-411, skipped when the move ends by 3-fold)"""
         if op != OP_AGENT and action is None:
             self.action_to_move(action)  # the random policy's "resign": TypeError, as the reference
-        mover, pre = self.current_player, self.board
+        mover, pre, key = self.current_player, self.board, self.encode_board()
+        stale = self._stale
         rec = self._take(self._b.call(op, action, flags))
+        if stale and rec["reason"] == R_INVALID:
+            raise NotImplementedError(
+                f"action {action} is in possible_moves from before the state assignment but not legal on the "
+                "assigned board: the reference would apply it unchecked (next_state, lib.rs:679-784)")
+        self._stale = False
+        if rec["reason"] not in (R_INVALID, R_DONE_ALREADY, R_MOVE_CAP):
+            self._saved[key] += 1  # player_move ran (chess_v2.py:404-405)
         if self.log and rec["reason"] not in (R_INVALID, R_DONE_ALREADY, R_MOVE_CAP, R_REPETITION):
             board, self.board = self.board, pre
             print(" " * 10, ">" * 10, mover)
@@ -242,6 +266,8 @@ class ChessEnv:
 
     def reset(self):
         self.repetitions = 0
+        self._saved = defaultdict(int)  # saved_boards (chess_v2.py:192)
+        self._stale = False
         self.white_king_on_the_board = self.piece_is_on_board(self.initial_board, KING_ID)
         self.black_king_on_the_board = self.piece_is_on_board(self.initial_board, -KING_ID)
         self._take(self._b.call(OP_RESET))
@@ -251,6 +277,11 @@ class ChessEnv:
 
     def step(self, action):
         assert self.action_space.contains(action), "ACTION ERROR {}".format(action)
+        if self._stale:  # after a state assignment: 239-258 against the stale list and done
+            if action not in self.possible_actions:
+                return self.state, INVALID_ACTION_REWARD, self.done, self.info
+            if self.done or self.move_count > self.moves_max:
+                return self.state, 0.0, True, self.info
         opp = self.opponent_policy is not None
         rec = self._ply(OP_AGENT, int(action), 1 if opp else 0)
         why = int(rec["reason"])
@@ -286,19 +317,26 @@ class ChessEnv:
         )
 
     @state.setter
-    def state(self, state):  # current_player is NOT taken from the dict (chess_v2.py:316-324)
+    def state(self, state):  # chess_v2.py:315-323: the board and the six flags only
         if not hasattr(self._b, "set_state"):
             raise NotImplementedError("this backend cannot take a state")
-        meta = [int(self.current_player == WHITE), state.get("white_king_castle_is_possible"),
-                state.get("white_queen_castle_is_possible"), state.get("black_king_castle_is_possible"),
-                state.get("black_queen_castle_is_possible"), state.get("white_king_is_checked"),
-                state.get("black_king_is_checked"), self.move_count]
-        self._b.set_state(C.board_to_array(state.get("board")), np.array(meta, dtype=np.uint8))
-        self._take(self._b.call(OP_SYNC))
+        flags = [bool(state.get(k)) for k in ("white_king_castle_is_possible", "white_queen_castle_is_possible",
+                                              "black_king_castle_is_possible", "black_queen_castle_is_possible",
+                                              "white_king_is_checked", "black_king_is_checked")]
+        moves, done = self._possible_moves, self.done
+        self._take(self._b.set_state(C.board_to_array(state.get("board")), np.array(flags, dtype=np.uint8)))
+        self._possible_moves, self.done = moves, done  # the reference's possible_moves stay until a move
+        self._stale = True
 
     @property
     def saved_boards(self):
-        """the live 3-fold window {board bytes: pre-move occurrences} (read from the device)"""
+        """chess_v2.py's saved_boards: {encode_board(): pre-move occurrences} of every
+        player_move since reset (the device decides the 3-fold end from its own window)"""
+        return self._saved
+
+    def device_window(self):
+        """the device's live 3-fold window {board bytes: pre-move occurrences}: the boards since
+        the last pawn move or capture"""
         return self._b.window()
 
     @property
@@ -363,8 +401,8 @@ class ChessEnv:
             state = self.state
         return self.engine.next_state(state, player, self.move_to_str_code(move))
 
-    def encode_board(self):
-        return np.asarray(self.board, dtype=np.int8).reshape(64).tobytes()
+    def encode_board(self):  # chess_v2.py:599-602
+        return "".join(_ENCODE[int(v)] for v in np.asarray(self.board).reshape(64))
 
     # ---------------------------------------------------------------- moves
     def get_possible_actions(self):

@@ -126,6 +126,10 @@ typedef struct {
 } gc_single_record;
 int gc_env_single_setup(gc_env* e, int agent_white);
 int gc_env_single_call(gc_env* e, int board, int op, int action, int flags, const gc_single_record** rec);
+/* the env's state setter (chess_v2.py:315-323) on board `board`: its pieces (int8[64]) and
+ * flags6 = {wkc, wqc, bkc, bqc, white_checked, black_checked}; the side to move, move_count,
+ * done and the 3-fold window stay.  *rec as gc_env_single_call (the new position's list). */
+int gc_env_single_set(gc_env* e, int board, const int8_t* board64, const uint8_t* flags6, const gc_single_record** rec);
 /* The live 3-fold window of one board (the boards since its last pawn move / capture and
  * their pre-move occurrence counts; chess_v2.py's saved_boards minus the boards that can no
  * longer recur): up to cap boards int8[64] and counts; *n = the window's length. */

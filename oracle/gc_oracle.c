@@ -864,6 +864,19 @@ void oracle_env_state(void *h, int8_t *board, uint8_t *meta) {
     meta[5] = e->st.wchk; meta[6] = e->st.bchk; meta[7] = (uint8_t)e->move_count;
 }
 int oracle_env_done(void *h) { return ((OEnv *)h)->done; }
+/* the state setter (chess_v2.py:315-323): board, the four rights, the two check flags;
+ * current_player, move_count, done and saved_boards stay.  The move list is that of the new
+ * board (the device's SET does the same; the single-board env keeps the reference's stale
+ * possible_moves on the host). */
+void oracle_env_set_board(void *h, const int8_t *board, const uint8_t *flags6) {
+    OEnv *e = (OEnv *)h;
+    memcpy(e->st.b, board, 64);
+    e->st.wkc = flags6[0] != 0; e->st.wqc = flags6[1] != 0; e->st.bkc = flags6[2] != 0; e->st.bqc = flags6[3] != 0;
+    e->st.wchk = flags6[4] != 0; e->st.bchk = flags6[5] != 0;
+    OState s;
+    env_engine_state(e, &s);
+    e->nmoves = o_get_possible_moves(&s, e->st.player, 0, e->moves, MAXMOVES);
+}
 /* distinct pre-move boards since the last pawn move / capture (the device's window length,
  * which its per-board table holds up to hist_cap and its spill table beyond) */
 int oracle_env_window(void *h) { return ((OEnv *)h)->win; }

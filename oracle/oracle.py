@@ -96,6 +96,8 @@ def lib():
         L.oracle_single_op.restype = i32
         L.oracle_env_window.argtypes = [P]
         L.oracle_env_window.restype = i32
+        L.oracle_env_set_board.argtypes = [P, P, P]
+        L.oracle_env_set_board.restype = None
         _lib = L
     return _lib
 
@@ -271,6 +273,12 @@ class OracleEnv:
         out = np.zeros(4, dtype=np.int32)
         lib().oracle_single_op(self.h, int(op), int(action), int(flags), _p(out))
         return tuple(int(x) for x in out)
+
+    def set_board(self, board, flags6):
+        """the env's state setter (chess_v2.py:315-323): board + rights + checks"""
+        b = np.ascontiguousarray(board, dtype=np.int8).reshape(64)
+        f = np.ascontiguousarray(flags6, dtype=np.uint8).reshape(6)
+        lib().oracle_env_set_board(self.h, _p(b), _p(f))
 
     @property
     def window(self):

@@ -20,6 +20,8 @@ Outputs (data only -- inputs + expected outputs, no reference source):
                            (whose asserts passed) with its inputs and outputs
   v2_env_traces.json.gz    ChessEnvV2 step() traces (reward/done/move_count/3-fold/
                            invalid actions; opponent "none" and "random")
+  v2_setter_traces.json.gz ChessEnvV2 with state assignments between steps: outputs and
+                           the whole saved_boards dict after every step
 
 Usage:  python tests/golden/make_golden.py [--deep]
 """
@@ -484,6 +486,86 @@ def gen_env_traces(v2):
     return traces
 
 
+def trace_setter(v2, seed, n_ops):
+    """ChessEnvV2 (opponent "none") with state assignments (chess_v2.py:315-323) between steps:
+    every 9th op the board and the six flags of a mid-game position from a second env (its
+    current_player ignored by the setter); steps with actions from the env's possible_actions --
+    stale after an assignment -- and, after one, also actions outside the stale list (-10) and
+    actions both lists hold.  Actions the stale list holds but the new board does not are not
+    played (the reference applies them unchecked).  Every step records its outputs and the
+    whole saved_boards dict (192, 404-405)."""
+    rng = np.random.RandomState(seed)
+    env = v2.ChessEnvV2(opponent="none", log=False)
+    src = v2.ChessEnvV2(opponent="none", log=False)
+    ops = []
+    stale = False
+    for k in range(n_ops):
+        if k % 9 == 8:
+            for _ in range(int(rng.randint(1, 7))):
+                if not src.possible_moves:
+                    src.reset()
+                _, _, d, _ = src.step(src.move_to_action(src.possible_moves[rng.randint(len(src.possible_moves))]))
+                if d:
+                    src.reset()
+            st = src.state
+            env.state = st
+            stale = True
+            ops.append(dict(kind="set", board=C.board_to_text(np.asarray(st["board"]).reshape(64)),
+                            flags=[int(bool(st[f])) for f in ("white_king_castle_is_possible",
+                                                              "white_queen_castle_is_possible",
+                                                              "black_king_castle_is_possible",
+                                                              "black_queen_castle_is_possible",
+                                                              "white_king_is_checked", "black_king_is_checked")]))
+            continue
+        acts = env.possible_actions
+        if stale:
+            try:
+                now = set(env.move_to_action(m) for m in env.get_possible_moves(state=env.state,
+                                                                               player=env.current_player))
+            except SystemError:
+                now = set()
+            both = [a for a in acts if a in now]
+            outside = [a for a in range(4100) if a not in acts]
+            if both and rng.rand() < 0.7:
+                action = int(both[rng.randint(len(both))])
+            else:
+                action = int(outside[rng.randint(len(outside))])
+        elif not acts:
+            env.reset()
+            ops.append(dict(kind="reset"))
+            continue
+        else:
+            action = int(acts[rng.randint(len(acts))])
+        played = action in acts and not env.done and env.move_count <= env.moves_max  # 239-258
+        try:
+            state, reward, done, info = env.step(action)
+        except SystemError:
+            ops.append(dict(kind="error", action=action))
+            env.reset()
+            stale = False
+            continue
+        if played:
+            stale = False  # player_move ran: possible_moves refreshed (268, 278)
+        ops.append(dict(kind="step", action=action, reward=float(reward), done=bool(done),
+                        board=C.board_to_text(np.asarray(state["board"]).reshape(64)),
+                        meta=[int(env.current_player == "WHITE"), int(state["white_king_castle_is_possible"]),
+                              int(state["white_queen_castle_is_possible"]),
+                              int(state["black_king_castle_is_possible"]),
+                              int(state["black_queen_castle_is_possible"]),
+                              int(bool(state["white_king_is_checked"])), int(bool(state["black_king_is_checked"]))],
+                        move_count=int(info["move_count"]), n_moves=len(env.possible_moves),
+                        saved=sorted([key, int(c)] for key, c in env.saved_boards.items())))
+        if done:
+            env.reset()
+            stale = False
+            ops.append(dict(kind="reset"))
+    return dict(seed=seed, ops=ops)
+
+
+def gen_setter_traces(v2):
+    return [trace_setter(v2, 3000 + s, 400) for s in range(3)]
+
+
 # the device policy's move-set order (gym-chess_amd/csrc/gc_core.h sw_gen / sw_select; the
 # oracle's set_key): pawn single / double push / capture toward col+1 / col-1, the eight knight
 # jumps, slider directions (orthogonal, then diagonal), the eight king steps; by target square
@@ -605,11 +687,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--deep", action="store_true", help="also v1 perft(5) (~4 min on 8 cores)")
     ap.add_argument("--games", type=int, default=10)
-    ap.add_argument("--only", choices=["opp"], help="regenerate one fixture only")
+    ap.add_argument("--only", choices=["opp", "setter"], help="regenerate one fixture only")
     args = ap.parse_args()
     v1, v2 = load_reference()
     if args.only == "opp":
         dump("v2_opp_traces.json.gz", gen_opp_traces(v2), gz=True)
+        return
+    if args.only == "setter":
+        dump("v2_setter_traces.json.gz", gen_setter_traces(v2), gz=True)
         return
     dump("perft_startpos.json", gen_perft_startpos(v1, args.deep))
     games, mid = gen_v1_games(v1, args.games, 320)
@@ -618,6 +703,7 @@ def main():
     dump("v2_known_answers.json", gen_v2_known_answers())
     dump("v2_env_traces.json.gz", gen_env_traces(v2), gz=True)
     dump("v2_opp_traces.json.gz", gen_opp_traces(v2), gz=True)
+    dump("v2_setter_traces.json.gz", gen_setter_traces(v2), gz=True)
 
 
 if __name__ == "__main__":

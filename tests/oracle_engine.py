@@ -60,6 +60,12 @@ class OracleBoard:
         r["moves"][: len(mv)] = np.array(mv, dtype=np.uint16)
         return r
 
+    def set_state(self, board, flags6):
+        """the state setter (oracle_env_set_board): the side to move, move_count, done and the
+        window stay -> the record"""
+        self._e.set_board(board, flags6)
+        return self.call(4)
+
     def window(self):
         raise NotImplementedError("the oracle keeps every board since reset")
 

@@ -94,6 +94,9 @@ def test_bench_threaded_two_replicas_line():
     line = json.loads(out.stdout.strip().splitlines()[-1])
     assert line["n_gpus"] == 2 and line["config"]["global_boards"] == 2 * 8192
     assert line["config"]["replica_mode"] == "threads" and line["value"] > 0
+    # the replicas' common-interval leg ran concurrently
+    ov = line["concurrent"]["overlap"]
+    assert ov["replicas"] == 2 and ov["min_overlap"] >= 0.9 and line["concurrent"]["max_region_s"] >= 0.2, ov
 
 
 def test_bench_torchrun_two_ranks_line():
@@ -125,3 +128,7 @@ def test_bench_torchrun_two_ranks_line():
     line = json.loads(lines[0])
     assert line["n_gpus"] == 2 and line["config"]["global_boards"] == 2 * 8192
     assert line["config"]["replica_mode"] == "processes" and line["value"] > 0
+    # the two ranks' >= 200 ms regions overlap >= 90 % on the node's clock
+    ov = line["concurrent"]["overlap"]
+    assert ov["replicas"] == 2 and ov["min_overlap"] >= 0.9 and line["concurrent"]["max_region_s"] >= 0.2, ov
+    assert line["region_overlap"]["replicas"] == 2
