@@ -456,7 +456,7 @@ def concurrent_leg(args, rep, ctx, n, s_per_step):
         t0 = time.perf_counter()
         for _ in range(reps):
             env.rollout_device(args.steps, tb)
-        env.synchronize()
+        env.wait_rollout()
         return None, time.perf_counter() - t0, t0
 
     _, dt = rep.timed(run)
@@ -538,11 +538,13 @@ def main():
         env.synchronize()
         t0 = time.perf_counter()
         env.rollout_device(args.steps, tb, events=(0, 1))  # K env.step() of every board, one launch, per-step trace
-        env.synchronize()
+        env.wait_rollout()  # the launch's completion word (its last workgroup, host-mapped)
         return None, time.perf_counter() - t0, t0
 
     _, dt_max = rep.timed(step)
     region_overlap = rep.last_overlap
+    for e in envs:
+        e.synchronize()  # (off the clock: the stream's own completion)
     kern_ms = [e.elapsed_ms(0, 1) for e in envs]
     s1 = [int(e.outputs()["nsteps"].sum()) for e in envs]
     w1 = [e.window_sum() for e in envs]
@@ -626,7 +628,10 @@ def main():
                        "parallelism": f"replicas{rep.world_size}", "replica_mode": rep.mode,
                        "settle_plies": args.settle,
                        "step_form": f"K steps = one {rollout_kernel} launch (gc_env_rollout_device), "
-                                    "per-step trace in HBM"},
+                                    "per-step trace in HBM", "steps_per_launch": args.steps,
+                       "region_end": "the launch's completion word (written to host-mapped memory by its last "
+                                     "workgroup after every workgroup's stores: gc_env_wait_rollout); the stream "
+                                     "sync follows off the clock"},
             "region_overlap": region_overlap,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

@@ -626,6 +626,13 @@ struct EnvDev {
         // not the start position's: the env's spill table, carried in this device-memory
         // block because the paired kernels' arguments are full (rewritten when it grows)
         SpillTab spill;
+        // the fused rollout's completion word (gc_env_wait_rollout): workgroups finished
+        // (device), launches finished (device), the last count written to host-mapped memory
+        struct DoneWord {
+            u32* ctr;
+            u32* seq;
+            u32* host;
+        } done;
     } ic;
     int hbits;        // log2 window-table entries per board (DevHist::nb)
     __device__ DevHist hist(int i, u32 g) const {
@@ -2276,6 +2283,24 @@ __global__ void __launch_bounds__(4 * QUAD_BOARDS * QUADS_WG) __attribute__((amd
         default: quad_run<3, false>(slab, nn, seed, htab, racts, icd, rinfo, plies, stats, trace, qw, l, i); break;
     }
 #endif
+    // The completion word: every workgroup, its stores done (the barrier's fence), counts
+    // itself; the last one bumps the launch count and writes it to host-mapped memory, where
+    // gc_env_wait_rollout sees it ~5 us before the stream's completion signal would tell
+    // (the end-of-kernel write-back and the command processor's signal: tools/region_anatomy.hip).
+    const EnvDev::InitCache::DoneWord dw = icd->done;
+    if (dw.ctr) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __threadfence();
+            const u32 prev = __hip_atomic_fetch_add(dw.ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+            if (prev == gridDim.x - 1) {
+                __hip_atomic_store(dw.ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const u32 v = __hip_atomic_fetch_add(dw.seq, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+                __threadfence_system();
+                __hip_atomic_store(dw.host, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
+    }
 }
 
 // Fused K-ply random self-play: state in registers for the whole launch.  Per-ply outputs
@@ -3643,6 +3668,13 @@ struct gc_env {
     bool sp_failed = false;   // an insert failed: every stepping call fails until the windows are cleared
     gc_single_record* srec = nullptr;  // gc_env_single_call's host-mapped record
     gc_single_record* srec_d = nullptr;  // its device address
+    // the quad rollout's completion word (EnvDev::InitCache::DoneWord): its host-mapped copy,
+    // the launches issued so far, and the count the last gc_env_rollout_device call waits for
+    // (0: the last call's work was not a quad launch -- gc_env_wait_rollout syncs the stream)
+    u32* done_host = nullptr;
+    u32* done_dev = nullptr;  // {ctr, seq}
+    u32 done_issued = 0;
+    u32 done_expect = 0;
 };
 
 static void env_free(gc_env* e) {
@@ -3661,6 +3693,8 @@ static void env_free(gc_env* e) {
     if (e->sp_ctr_h) (void)hipHostFree(e->sp_ctr_h);
     if (e->sp_ev) (void)hipEventDestroy(e->sp_ev);
     if (e->srec) (void)hipHostFree(e->srec);
+    if (e->done_host) (void)hipHostFree(e->done_host);
+    if (e->done_dev) (void)hipFree(e->done_dev);
     if (e->stream) (void)hipStreamDestroy(e->stream);
 }
 
@@ -4067,6 +4101,19 @@ extern "C" int gc_env_create(int device, int n_boards, uint64_t seed, const int8
         if (he == hipSuccess) he = hipMemcpyAsync(&e->d.ic, dic, sizeof(EnvDev::InitCache), hipMemcpyDeviceToHost, e->stream);
         if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
         if (he != hipSuccess) { env_free(e); delete e; return fail(std::string("init cache: ") + hipGetErrorString(he)); }
+        // the completion word of the quad rollout (host-mapped, fine-grained)
+        u32* hw = nullptr;
+        he = hipHostMalloc(&hw, 4, hipHostMallocMapped | hipHostMallocCoherent);
+        if (he == hipSuccess) { e->done_host = hw; *hw = 0; he = hipMalloc(&e->done_dev, 8); }
+        if (he == hipSuccess) he = hipMemsetAsync(e->done_dev, 0, 8, e->stream);
+        u32* hwd = nullptr;
+        if (he == hipSuccess) he = hipHostGetDevicePointer((void**)&hwd, hw, 0);
+        if (he == hipSuccess) {
+            e->d.ic.done = EnvDev::InitCache::DoneWord{e->done_dev, e->done_dev + 1, hwd};
+            he = hipMemcpyAsync(&dic->done, &e->d.ic.done, sizeof(e->d.ic.done), hipMemcpyHostToDevice, e->stream);
+        }
+        if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
+        if (he != hipSuccess) { env_free(e); delete e; return fail(std::string("completion word: ") + hipGetErrorString(he)); }
     }
     launch_reset(e, nullptr, 1);
     he = hipGetLastError();
@@ -4478,10 +4525,12 @@ static int issue_rollout(gc_env* e, int n_plies, uint64_t* d_trace, bool stats) 
         if (k < 0) return -1;
         u64* tr = d_trace ? reinterpret_cast<u64*>(d_trace) + (size_t)p0 * e->n : nullptr;
         const u32 ri = r.rinfo | ((u32)k << 18);
+        e->done_expect = 0;
         if (pair && use_quad(e)) {
             const int qg = (e->n + QUAD_BOARDS * QUADS_WG - 1) / (QUAD_BOARDS * QUADS_WG);
             k_env_rollout4<<<qg, 4 * QUAD_BOARDS * QUADS_WG, 0, e->stream>>>(e->slab, d.n, d.seed, d.htab, sw_table(r),
                                                                              r.icd, ri, st, tr);
+            e->done_expect = ++e->done_issued;
         } else if (pair) {
             switch (e->rules ? 3 : pair_opp(e)) {
                 case 3: k_env_rollout2<true><<<grid, bs, 0, e->stream>>>(e->slab, d.n, d.seed, d.htab, r.racts, r.icd, ri, st, tr); break;
@@ -4806,6 +4855,25 @@ extern "C" int gc_env_synchronize(gc_env* e) {
     }
     HIPCHK(hipStreamSynchronize(e->stream));
     return 0;
+}
+
+// Wait for the work of the last gc_env_rollout_device call: when it ended with a quad launch,
+// until that launch's completion word reaches host memory (every workgroup's stores done),
+// else until the stream is idle.  Work enqueued after the launch (an event record) may still
+// be pending; reads through the env's stream stay ordered after it.  Spins with a stream
+// query now and then, so a word that never comes cannot hang the caller.
+extern "C" int gc_env_wait_rollout(gc_env* e) {
+    if (!e) return fail("null env");
+    if (!e->done_expect || !e->done_host) return gc_env_synchronize(e);
+    const u32 want = e->done_expect;
+    for (unsigned k = 0;; k++) {
+        if ((int)(__atomic_load_n(e->done_host, __ATOMIC_ACQUIRE) - want) >= 0) return 0;
+        if ((k & 255) == 255) {
+            const hipError_t q = hipStreamQuery(e->stream);
+            if (q == hipSuccess) return 0;
+            if (q != hipErrorNotReady) return fail(std::string("stream: ") + hipGetErrorString(q));
+        }
+    }
 }
 
 extern "C" int gc_env_record_event(gc_env* e, int slot) {

@@ -97,6 +97,7 @@ SIGNATURES = {
     "gc_env_legal_moves": (_I, [_P, _P, _I, _P]),
     "gc_env_legal_mask": (_I, [_P, _P, _P]),
     "gc_env_synchronize": (_I, [_P]),
+    "gc_env_wait_rollout": (_I, [_P]),
     "gc_env_record_event": (_I, [_P, _I]),
     "gc_env_elapsed_ms": (_I, [_P, _I, _I, _P]),
     "gc_env_device_bytes": (_U64, [_P]),

@@ -249,6 +249,11 @@ class BatchedChessEnv:
     def synchronize(self):
         _lib.check(self._L.gc_env_synchronize(self._h))
 
+    def wait_rollout(self):
+        """wait for the last rollout_device call's work: its launch's completion word in
+        host-mapped memory (quad kernel), else the stream (gc_env_wait_rollout)"""
+        _lib.check(self._L.gc_env_wait_rollout(self._h))
+
     def record_event(self, slot):
         _lib.check(self._L.gc_env_record_event(self._h, int(slot)))
 

@@ -215,6 +215,12 @@ int gc_env_legal_mask(gc_env* e, uint64_t* mask, int32_t* counts);
 int gc_env_spill_info(gc_env* e, int* bits, uint64_t* used, uint64_t* live);
 /* wait for the env's stream (spin-polls up to GC_SPIN_US, default 20 ms, then blocks) */
 int gc_env_synchronize(gc_env* e);
+/* wait for the work of the last gc_env_rollout_device call: when it was a quad launch
+ * (gc_env_rollout_waves = 4), until its completion word -- written to host-mapped memory by
+ * the launch's last workgroup after every workgroup's stores -- arrives, else as
+ * gc_env_synchronize.  Later work on the env's stream (an event record) may still be pending;
+ * anything read through that stream stays ordered after the launch. */
+int gc_env_wait_rollout(gc_env* e);
 /* FEN (host-side, no GPU): placement rank 8 first (board row 0), side to move, castling ->
  * the four *_castle_is_possible flags (chess_v2.py:301-313); en passant and the half-move
  * clock are ignored (not part of the reference's rules); full-move number n -> move_count

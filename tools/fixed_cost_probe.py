@@ -46,7 +46,7 @@ def main():
         L.gc_env_num_boards(env._h)
         t.append(time.perf_counter() - t0)
     out = {"ctypes_call_us": float(np.median(t)) * 1e6, "k": {}}
-    for ev in (True, False):
+    for ev, wait in ((True, "sync"), (True, "word"), (False, "sync")):
         rows = {}
         for k in ks:
             wall, enq, evt = [], [], []
@@ -55,8 +55,9 @@ def main():
                 t0 = time.perf_counter()
                 env.rollout_device(k, tb, events=(0, 1) if ev else (-1, -1))
                 t1 = time.perf_counter()
-                env.synchronize()
+                env.synchronize() if wait == "sync" else env.wait_rollout()
                 t2 = time.perf_counter()
+                env.synchronize()
                 wall.append(t2 - t0)
                 enq.append(t1 - t0)
                 if ev:
@@ -71,7 +72,7 @@ def main():
             el = np.array([rows[k]["event_us"] for k in ks])
             fe = np.polyfit(kk, el, 1)
             res["event_fit"] = {"per_k_us": fe[0], "fixed_us": fe[1]}
-        out["k"]["events" if ev else "no_events"] = res
+        out["k"][("events" if ev else "no_events") + "_" + wait] = res
     print(json.dumps(out), flush=True)
 
 
