@@ -446,17 +446,20 @@ def concurrent_leg(args, rep, ctx, n, s_per_step):
     each region's begin / end on CLOCK_MONOTONIC (node-wide) gives the union wall time and the
     fraction of the longest region common to all (min_overlap)."""
     ms = args.concurrent_ms if args.concurrent_ms > 0 else 250.0
-    reps = max(1, int(-(-ms / 1e3 // (s_per_step * max(args.steps, 1)))))
-    reps = int(rep.max(reps))
+    batch = max(1, int(0.01 / (s_per_step * max(args.steps, 1))))  # ~10 ms of launches between clock checks
     s0 = [int(c[0].outputs()["nsteps"].sum()) for c in ctx]
+    launches = [0] * len(ctx)
 
     def run(rp):
-        env, tb = ctx[rep.local.index(rp)][:2]
+        k = rep.local.index(rp)
+        env, tb = ctx[k][:2]
         env.synchronize()
         t0 = time.perf_counter()
-        for _ in range(reps):
-            env.rollout_device(args.steps, tb)
-        env.wait_rollout()
+        while time.perf_counter() - t0 < ms / 1e3:
+            for _ in range(batch):
+                env.rollout_device(args.steps, tb)
+            env.wait_rollout()
+            launches[k] += batch
         return None, time.perf_counter() - t0, t0
 
     _, dt = rep.timed(run)
@@ -464,7 +467,7 @@ def concurrent_leg(args, rep, ctx, n, s_per_step):
     s1 = [int(c[0].outputs()["nsteps"].sum()) for c in ctx]
     steps = rep.sum(sum(b - a for a, b in zip(s0, s1)))
     wall = ov["union_wall_s"] if ov else dt
-    return {"value": steps / wall, "unit": "env_steps/s", "launches_per_replica": reps, "steps_per_launch": args.steps,
+    return {"value": steps / wall, "unit": "env_steps/s", "launches_per_replica": launches, "steps_per_launch": args.steps,
             "env_steps": steps, "union_wall_s": wall, "max_region_s": dt, "overlap": ov,
             "form": "every replica repeats the headline's K-step launch back to back over a common interval; "
                     "value = all replicas' env.steps / the union of their regions"}

@@ -41,6 +41,8 @@ for s in ${STEPS:-smoke pytest bench prof}; do
     pmcrf)  step pmcrf 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_roll_fetch -o run --output-format csv -- $PMCR ;;
     pmcrw)  step pmcrw 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_roll_write -o run --output-format csv -- $PMCR ;;
     pmcrm)  step pmcrm 300 rocprofv3 --pmc $MIXC -d $OUT/pmc_roll_mix -o run --output-format csv -- $PMCR ;;
+    fcp)    step fcp 300 python tools/fixed_cost_probe.py ;;  # the timed region's fixed cost, by K and wait
+    anat)   step anat 120 tools/_region_anatomy ;;  # one launch's round trip by parts (build it first)
     calib)  step calib 120 rocprofv3 --pmc $MIXC -d $OUT/pmc_calib -o run --output-format csv -- tools/_valu_calib ;;
     short)  for i in 1 2 3; do step short$i 300 python bench.py --gpus 1 --steps 20 --warmup 5; done
             step long 300 python bench.py --gpus 1 --steps 1000 --warmup 5 --launched-steps 0 --api-steps 0 --single-episodes 0 --variant-steps 0 --perft-roots 0 --no-cpu-baseline ;;
