@@ -2492,6 +2492,58 @@ __device__ __noinline__ void single_op(const EnvDev& e, int i, int op, int actio
     list_one(s, 0, GC_SINGLE_MOVES_CAP, rec->moves, &rec->nmoves, 0);
 }
 
+// ----------------------------------------------------------------------------- single-board server
+// The single-board env's ops without a launch each (one step paid a
+// ~25 us launch round trip -- tools/region_anatomy.hip -- plus k_single's cold loads): one
+// wave stays resident on its own stream and serves requests through a host-mapped mailbox.
+// The host writes the request, then bumps req_seq; the wave polls req_seq (system-scope loads,
+// s_sleep between), runs the same single_op, writes the record to host memory and then
+// resp_seq.  It exits on QUIT, or when no request came for SRV_IDLE_MS (so it has always
+// drained before its process can end); the host starts it again on the next request.
+struct SrvBox {
+    u32 req_seq, op, flags, pad0;
+    int32_t action, pad1[3];
+    u32 resp_seq, pad2[15];  // own cache line
+    u32 exited, pad3[15];    // the launch id of the last server that exited
+};
+#define SRV_QUIT 99
+#define SRV_IDLE_MS 50
+__device__ __forceinline__ u32 srv_load(const u32* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); }
+__device__ __forceinline__ void srv_store(u32* p, u32 v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); }
+__global__ void __launch_bounds__(64) k_single_server(EnvDev e, int i, SrvBox* box, gc_single_record* __restrict__ hrec,
+                                                      u32 done_seq, u32 launch_id) {
+    __shared__ u64 lds_scr[SCRATCH_SLOTS * BLOCK];
+    __shared__ gc_single_record lrec;
+    LdsScratch scr{lds_scr + threadIdx.x};
+    unsigned long long idle0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
+    for (;;) {
+        const u32 req = __builtin_amdgcn_readfirstlane(srv_load(&box->req_seq));
+        if (req == done_seq) {
+            if (__builtin_amdgcn_s_memrealtime() - idle0 > (unsigned long long)SRV_IDLE_MS * 100000ull) break;
+            __builtin_amdgcn_s_sleep(8);
+            continue;
+        }
+        __atomic_thread_fence(__ATOMIC_ACQUIRE);  // the request's fields (and SET's inputs) after req_seq
+        const int op = (int)__builtin_amdgcn_readfirstlane(srv_load(&box->op));
+        if (op == SRV_QUIT) break;
+        const int action = (int)__builtin_amdgcn_readfirstlane(srv_load(reinterpret_cast<u32*>(&box->action)));
+        const int flags = (int)__builtin_amdgcn_readfirstlane(srv_load(&box->flags));
+        if (threadIdx.x == 0) single_op(e, i, op, action, flags, scr, &lrec, hrec);
+        __syncthreads();
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(&lrec);
+        uint32_t* dst = reinterpret_cast<uint32_t*>(hrec);
+        const int words = (int)(offsetof(gc_single_record, moves) / 4) + (lrec.nmoves < GC_SINGLE_MOVES_CAP ? lrec.nmoves : GC_SINGLE_MOVES_CAP + 1) / 2 + 1;
+        for (int k = threadIdx.x; k < words && k < (int)(sizeof(gc_single_record) / 4); k += 64) dst[k] = src[k];
+        __threadfence_system();  // the record, then the response
+        __syncthreads();
+        if (threadIdx.x == 0) srv_store(&box->resp_seq, req);
+        done_seq = req;
+        idle0 = __builtin_amdgcn_s_memrealtime();
+    }
+    __threadfence_system();  // every op's state stores, then the exit mark
+    if (threadIdx.x == 0) srv_store(&box->exited, launch_id);
+}
+
 // the live 3-fold window of board i (its table entries, then its spill entries): boards and
 // occurrence counts (diagnostic readout; ChessEnv.saved_boards)
 __global__ void k_window_boards(EnvDev e, int i, int8_t* __restrict__ boards, uint8_t* __restrict__ counts, int cap,
@@ -3677,7 +3729,17 @@ struct gc_env {
     u32* done_dev = nullptr;  // {ctr, seq}
     u32 done_issued = 0;
     u32 done_expect = 0;
+    // the single-board server (k_single_server): its mailbox (host-mapped), stream, the launch
+    // running (0: none), the last request served
+    SrvBox* srv = nullptr;
+    SrvBox* srv_d = nullptr;
+    hipStream_t srv_stream = nullptr;
+    u32 srv_launch = 0, srv_next_launch = 0, srv_seq = 0;
+    int srv_board = -1;
 };
+
+static int srv_stop(gc_env* e);  // (the single-board server, below)
+#define SRV_QUIESCE(e) do { if ((e)->srv_launch && srv_stop(e)) return -1; } while (0)
 
 static void env_free(gc_env* e) {
     void* ps[] = {e->api_out, e->reset_acts, e->icd, e->icd_f, e->racts_f, e->ep, e->slab, e->d.htab, e->mbox, e->m8, e->mask,
@@ -3696,6 +3758,8 @@ static void env_free(gc_env* e) {
     if (e->sp_ev) (void)hipEventDestroy(e->sp_ev);
     if (e->srec) (void)hipHostFree(e->srec);
     if (e->done_host) (void)hipHostFree(e->done_host);
+    if (e->srv) (void)hipHostFree(e->srv);
+    if (e->srv_stream) (void)hipStreamDestroy(e->srv_stream);
     if (e->done_dev) (void)hipFree(e->done_dev);
     if (e->stream) (void)hipStreamDestroy(e->stream);
 }
@@ -3920,6 +3984,7 @@ __global__ void k_spill_live(const u64* __restrict__ ent, u32 mask, const u32* _
 }
 extern "C" int gc_env_spill_info(gc_env* e, int* bits, uint64_t* used, uint64_t* live) {
     if (!e || !bits || !used || !live) return fail("null argument");
+    SRV_QUIESCE(e);
     HIPCHK(hipSetDevice(e->device));
     HIPCHK(hipStreamSynchronize(e->stream));
     *bits = e->sp_bits;
@@ -4136,6 +4201,7 @@ extern "C" int gc_env_create(int device, int n_boards, uint64_t seed, const int8
 // reference's reset calls the opponent policy to open).  Resets every board.
 extern "C" int gc_env_set_opponent(gc_env* e, int opponent, int agent_white) {
     if (!e) return fail("null env");
+    SRV_QUIESCE(e);
     if (opponent != 0 && opponent != 1) return fail("opponent must be 0 (none) or 1 (random)");
     if (!agent_white && !opponent) return fail("player_color BLACK needs an opponent (chess_v2.py:208-212)");
     if (opponent && e->rules) return fail("the FIDE rules mode supports opponent \"none\" only");
@@ -4156,6 +4222,7 @@ extern "C" int gc_env_set_opponent(gc_env* e, int opponent, int agent_white) {
 // every board and restarts the policy streams.
 extern "C" int gc_env_set_rules(gc_env* e, int rules) {
     if (!e) return fail("null env");
+    SRV_QUIESCE(e);
     if (rules != 0 && rules != 1) return fail("rules must be 0 (reference) or 1 (fide)");
     if (rules && e->d.opp) return fail("the FIDE rules mode supports opponent \"none\" only");
     HIPCHK(hipSetDevice(e->device));
@@ -4180,6 +4247,7 @@ extern "C" int gc_env_set_rules(gc_env* e, int rules) {
 extern "C" int gc_env_destroy(gc_env* e) {
     if (!e) return 0;
     (void)hipSetDevice(e->device);
+    (void)srv_stop(e);
     (void)hipStreamSynchronize(e->stream);
     env_free(e);
     delete e;
@@ -4190,6 +4258,7 @@ extern "C" int gc_env_num_boards(gc_env* e) { return e ? e->n : -1; }
 
 extern "C" int gc_env_reset(gc_env* e, const uint8_t* mask) {
     if (!e) return fail("null env");
+    SRV_QUIESCE(e);
     HIPCHK(hipSetDevice(e->device));
     if (mask) HIPCHK(hipMemcpyAsync(e->mask, mask, e->n, hipMemcpyHostToDevice, e->stream));
     launch_reset(e, mask ? e->mask : nullptr, 1);
@@ -4203,6 +4272,7 @@ extern "C" int gc_env_reset(gc_env* e, const uint8_t* mask) {
 // ---- single-board env ops (k_single)
 extern "C" int gc_env_single_setup(gc_env* e, int agent_white) {
     if (!e) return fail("null env");
+    SRV_QUIESCE(e);
     if (e->rules) return fail("the single-board env ops follow the reference's rules");
     if (e->d.opp) return fail("the single-board env ops drive the opponent from the host (opponent 0)");
     HIPCHK(hipSetDevice(e->device));
@@ -4215,6 +4285,61 @@ extern "C" int gc_env_single_setup(gc_env* e, int agent_white) {
     return 0;
 }
 
+// ---- the single-board server's host side
+static bool srv_enabled() {
+    static const bool off = getenv("GC_SINGLE_SERVER") && atoi(getenv("GC_SINGLE_SERVER")) == 0;
+    return !off;
+}
+// stop the server (if one runs) and wait until it has drained: every other op on this env
+// reads or writes the board's memory through other kernels
+static int srv_stop(gc_env* e) {
+    if (!e->srv_launch) return 0;
+    SrvBox* b = e->srv;
+    __atomic_store_n(&b->op, (u32)SRV_QUIT, __ATOMIC_RELAXED);
+    __atomic_store_n(&b->req_seq, e->srv_seq + 1, __ATOMIC_RELEASE);  // (never served: QUIT)
+    const hipError_t he = hipStreamSynchronize(e->srv_stream);
+    __atomic_store_n(&b->req_seq, e->srv_seq, __ATOMIC_RELEASE);
+    e->srv_launch = 0;
+    if (he != hipSuccess) return fail(std::string("single-board server: ") + hipGetErrorString(he));
+    return 0;
+}
+// one op through the server (started on demand); the record lands in e->srec
+static int srv_call(gc_env* e, int board, int op, int action, int flags) {
+    HIPCHK(hipSetDevice(e->device));
+    if (!e->srv) {
+        HIPCHK(hipHostMalloc(&e->srv, sizeof(SrvBox), hipHostMallocMapped | hipHostMallocCoherent));
+        memset(e->srv, 0, sizeof(SrvBox));
+        HIPCHK(hipHostGetDevicePointer((void**)&e->srv_d, e->srv, 0));
+        HIPCHK(hipStreamCreateWithFlags(&e->srv_stream, hipStreamNonBlocking));
+    }
+    if (e->srv_launch && e->srv_board != board && srv_stop(e)) return -1;
+    SrvBox* b = e->srv;
+    const u32 seq = e->srv_seq + 1;
+    b->op = (u32)op;
+    b->action = action;
+    b->flags = (u32)flags;
+    __atomic_store_n(&b->req_seq, seq, __ATOMIC_RELEASE);
+    for (unsigned k = 0;; k++) {
+        if (!e->srv_launch || __atomic_load_n(&b->exited, __ATOMIC_ACQUIRE) == e->srv_launch) {
+            // no server, or it exited (idle) before seeing this request: (re)start it after the
+            // env's own work; it serves every request past done_seq
+            if (e->srv_launch) HIPCHK(hipStreamSynchronize(e->srv_stream));
+            HIPCHK(hipStreamSynchronize(e->stream));
+            e->srv_launch = ++e->srv_next_launch;
+            e->srv_board = board;
+            k_single_server<<<1, 64, 0, e->srv_stream>>>(e->d, board, e->srv_d, e->srec_d, e->srv_seq, e->srv_launch);
+            HIPCHK(hipGetLastError());
+        }
+        if (__atomic_load_n(&b->resp_seq, __ATOMIC_ACQUIRE) == seq) break;
+        if ((k & 1023) == 1023) {  // a faulted server: the stream says so
+            const hipError_t q = hipStreamQuery(e->srv_stream);
+            if (q != hipSuccess && q != hipErrorNotReady) return fail(std::string("single-board server: ") + hipGetErrorString(q));
+        }
+    }
+    e->srv_seq = seq;
+    return 0;
+}
+
 extern "C" int gc_env_single_call(gc_env* e, int board, int op, int action, int flags, const gc_single_record** rec) {
     if (!e || !rec) return fail("null argument");
     if (!e->srec) return fail("call gc_env_single_setup first");
@@ -4223,10 +4348,16 @@ extern "C" int gc_env_single_call(gc_env* e, int board, int op, int action, int 
     if (op != SOP_RESET && op != SOP_SYNC && (action < 0 || action > A_RESIGN))
         return fail("action out of range [0, 4100]");
     HIPCHK(hipSetDevice(e->device));
-    if (spill_before(e)) return -1;
-    k_single<<<1, 64, 0, e->stream>>>(e->d, board, op, action, flags, e->srec_d);
-    HIPCHK(hipGetLastError());
-    if (spill_after(e) || gc_env_synchronize(e)) return -1;
+    if (e->d.ic.spill.ent) {  // a BLACK agent: the spill table's host checks need the stream
+        if (srv_stop(e) || spill_before(e)) return -1;
+    }
+    if (srv_enabled() && !e->d.ic.spill.ent) {
+        if (srv_call(e, board, op, action, flags)) return -1;
+    } else {
+        k_single<<<1, 64, 0, e->stream>>>(e->d, board, op, action, flags, e->srec_d);
+        HIPCHK(hipGetLastError());
+        if (spill_after(e) || gc_env_synchronize(e)) return -1;
+    }
     e->policy_ready = false;
     *rec = e->srec;
     return 0;
@@ -4246,9 +4377,14 @@ extern "C" int gc_env_single_set(gc_env* e, int board, const int8_t* board64, co
     memcpy(e->srec->board, board64, 64);
     for (int k = 0; k < 4; k++) e->srec->rights[k] = flags6[k] ? 1 : 0;
     for (int k = 0; k < 2; k++) e->srec->checked[k] = flags6[4 + k] ? 1 : 0;
-    k_single<<<1, 64, 0, e->stream>>>(e->d, board, SOP_SET, 0, 0, e->srec_d);
-    HIPCHK(hipGetLastError());
-    if (gc_env_synchronize(e)) return -1;
+    if (srv_enabled() && !e->d.ic.spill.ent) {
+        if (srv_call(e, board, SOP_SET, 0, 0)) return -1;
+    } else {
+        if (srv_stop(e)) return -1;
+        k_single<<<1, 64, 0, e->stream>>>(e->d, board, SOP_SET, 0, 0, e->srec_d);
+        HIPCHK(hipGetLastError());
+        if (gc_env_synchronize(e)) return -1;
+    }
     e->policy_ready = false;
     *rec = e->srec;
     return 0;
@@ -4256,6 +4392,7 @@ extern "C" int gc_env_single_set(gc_env* e, int board, const int8_t* board64, co
 
 extern "C" int gc_env_window_boards(gc_env* e, int board, int8_t* boards, uint8_t* counts, int cap, int* n) {
     if (!e || !n || (cap > 0 && (!boards || !counts))) return fail("null argument");
+    SRV_QUIESCE(e);
     if (board < 0 || board >= e->n) return fail("board index out of range");
     HIPCHK(hipSetDevice(e->device));
     int8_t* db = nullptr;
@@ -4280,6 +4417,7 @@ extern "C" int gc_env_window_boards(gc_env* e, int board, int8_t* boards, uint8_
 
 extern "C" int gc_env_step(gc_env* e, const uint16_t* actions, int32_t* reward, uint8_t* done, uint8_t* reason) {
     if (!e || !actions) return fail("null argument");
+    SRV_QUIESCE(e);
     for (int i = 0; i < e->n; i++)
         if (actions[i] > A_RESIGN) return fail("action out of range [0, 4100] at index " + std::to_string(i));
     HIPCHK(hipSetDevice(e->device));
@@ -4303,6 +4441,7 @@ extern "C" int gc_env_step_device(gc_env* e, const uint16_t* d_actions, int32_t*
                                   uint8_t* d_reason, uint64_t* d_mask, int8_t* d_obs, int32_t* d_count,
                                   uint16_t* d_pick, int flags) {
     if (!e || !d_actions || !d_reward || !d_done || !d_reason) return fail("null argument");
+    SRV_QUIESCE(e);
     if (e->rules) return fail("gc_env_step_device: reference rules only (FIDE: gc_env_step)");
     if (flags & ~1) return fail("flags: bit 0 = auto-reset");
     HIPCHK(hipSetDevice(e->device));
@@ -4419,6 +4558,7 @@ static int issue_plies(gc_env* e, int n) {
 static int step_random(gc_env* e, int n_plies);
 extern "C" int gc_env_step_random(gc_env* e, int n_plies) {
     if (!e) return fail("null env");
+    SRV_QUIESCE(e);
     if (!e->policy_ready) return fail("policy actions stale: call gc_env_reset or gc_env_select_random first");
     HIPCHK(hipSetDevice(e->device));
     if (spill_before(e)) return -1;
@@ -4504,6 +4644,7 @@ extern "C" int gc_env_rollout_waves(gc_env* e) {
 
 extern "C" int gc_env_select_random(gc_env* e) {
     if (!e) return fail("null env");
+    SRV_QUIESCE(e);
     HIPCHK(hipSetDevice(e->device));
     if (e->rules) k_fenv_select<<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d);
     else k_select<<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d);
@@ -4554,6 +4695,7 @@ static int issue_rollout(gc_env* e, int n_plies, uint64_t* d_trace, bool stats) 
 extern "C" int gc_env_rollout(gc_env* e, int n_plies, int16_t* tr_action, int16_t* tr_reward, uint8_t* tr_done,
                               uint8_t* tr_reason, uint64_t* stats8) {
     if (!e) return fail("null env");
+    SRV_QUIESCE(e);
     if (n_plies < 0) return fail("n_plies must be >= 0");
     if (!e->policy_ready) return fail("policy actions stale: call gc_env_reset or gc_env_select_random first");
     HIPCHK(hipSetDevice(e->device));
@@ -4597,6 +4739,7 @@ extern "C" int gc_env_rollout(gc_env* e, int n_plies, int16_t* tr_action, int16_
 // before / after the launches, -1 = none (one C-ABI call brackets the timed work).
 extern "C" int gc_env_rollout_device(gc_env* e, int n_plies, uint64_t* d_trace, int ev_begin, int ev_end) {
     if (!e) return fail("null env");
+    SRV_QUIESCE(e);
     if (n_plies < 0) return fail("n_plies must be >= 0");
     if (ev_begin < -1 || ev_begin >= 8 || ev_end < -1 || ev_end >= 8) return fail("event slots: -1 or 0..7");
     if (!e->policy_ready) return fail("policy actions stale: call gc_env_reset or gc_env_select_random first");
@@ -4613,6 +4756,7 @@ extern "C" int gc_env_rollout_device(gc_env* e, int n_plies, uint64_t* d_trace, 
 extern "C" int gc_env_get_outputs(gc_env* e, int32_t* reward, uint8_t* done, uint8_t* reason, uint16_t* next_action,
                                   uint32_t* nsteps) {
     if (!e) return fail("null env");
+    SRV_QUIESCE(e);
     HIPCHK(hipSetDevice(e->device));
     if (reward) HIPCHK(hipMemcpyAsync(reward, e->d.reward, (size_t)4 * e->n, hipMemcpyDeviceToHost, e->stream));
     if (done) HIPCHK(hipMemcpyAsync(done, e->d.done, e->n, hipMemcpyDeviceToHost, e->stream));
@@ -4625,6 +4769,7 @@ extern "C" int gc_env_get_outputs(gc_env* e, int32_t* reward, uint8_t* done, uin
 
 extern "C" int gc_env_get_states(gc_env* e, int8_t* boards, uint8_t* meta) {
     if (!e) return fail("null env");
+    SRV_QUIESCE(e);
     HIPCHK(hipSetDevice(e->device));
     k_export<<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d.st, e->mbox, e->m8);
     HIPCHK(hipGetLastError());
@@ -4637,6 +4782,7 @@ extern "C" int gc_env_get_states(gc_env* e, int8_t* boards, uint8_t* meta) {
 // set states (FEN/dict ingest). meta8[7] = move_count; repetition windows are cleared.
 extern "C" int gc_env_set_states(gc_env* e, const int8_t* boards, const uint8_t* meta) {
     if (!e || !boards || !meta) return fail("null argument");
+    SRV_QUIESCE(e);
     if (check_boards(e->n, boards)) return -1;
     HIPCHK(hipSetDevice(e->device));
     HIPCHK(hipMemcpyAsync(e->mbox, boards, (size_t)64 * e->n, hipMemcpyHostToDevice, e->stream));
@@ -4779,6 +4925,7 @@ extern "C" int gc_state_to_fen_rules(const int8_t* board, const uint8_t* meta, c
 // repetition windows cleared (like gc_env_set_states)
 extern "C" int gc_env_set_fens(gc_env* e, const char* const* fens) {
     if (!e || !fens) return fail("null argument");
+    SRV_QUIESCE(e);
     std::vector<int8_t> b((size_t)64 * e->n), ep(e->n, -1);
     std::vector<uint8_t> m((size_t)8 * e->n);
     for (int i = 0; i < e->n; i++) {
@@ -4808,6 +4955,7 @@ extern "C" int gc_env_set_fens(gc_env* e, const char* const* fens) {
 
 extern "C" int gc_env_legal_moves(gc_env* e, uint16_t* moves, int cap, int32_t* counts) {
     if (!e || !moves || !counts) return fail("null argument");
+    SRV_QUIESCE(e);
     if (cap <= 0) return fail("cap must be > 0");
     HIPCHK(hipSetDevice(e->device));
     if (cap > e->list_cap) {
@@ -4828,6 +4976,7 @@ extern "C" int gc_env_legal_moves(gc_env* e, uint16_t* moves, int cap, int32_t* 
 
 extern "C" int gc_env_legal_mask(gc_env* e, uint64_t* mask, int32_t* counts) {
     if (!e || !mask) return fail("null argument");
+    SRV_QUIESCE(e);
     HIPCHK(hipSetDevice(e->device));
     if (!e->lmask && dalloc(&e->lmask, (size_t)65 * e->n)) return -1;
     if (e->rules) k_fmask<<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d.st, e->lmask, e->counts);
@@ -4901,6 +5050,7 @@ __global__ void k_window_sum(SoA st, unsigned long long* out) {
 
 extern "C" int gc_env_window_sum(gc_env* e, uint64_t* sum) {
     if (!e || !sum) return fail("null argument");
+    SRV_QUIESCE(e);
     HIPCHK(hipSetDevice(e->device));
     unsigned long long* d = nullptr;
     if (dalloc(&d, 1)) return -1;
@@ -5196,6 +5346,7 @@ extern "C" int gc_env_checkpoint_bytes(gc_env* e, uint64_t* bytes) {
 
 extern "C" int gc_env_save(gc_env* e, void* buf, uint64_t cap, uint64_t* written) {
     if (!e || !buf) return fail("null argument");
+    SRV_QUIESCE(e);
     HIPCHK(hipSetDevice(e->device));
     HIPCHK(hipStreamSynchronize(e->stream));
     const int n = e->n;
@@ -5256,6 +5407,7 @@ extern "C" int gc_env_save(gc_env* e, void* buf, uint64_t cap, uint64_t* written
 
 extern "C" int gc_env_load(gc_env* e, const void* buf, uint64_t size) {
     if (!e || !buf) return fail("null argument");
+    SRV_QUIESCE(e);
     if (size < sizeof(CkptHeader)) return fail("checkpoint: truncated header");
     CkptHeader hd;
     memcpy(&hd, buf, sizeof hd);
