@@ -4319,6 +4319,7 @@ static int srv_call(gc_env* e, int board, int op, int action, int flags) {
     b->action = action;
     b->flags = (u32)flags;
     __atomic_store_n(&b->req_seq, seq, __ATOMIC_RELEASE);
+    const auto t0 = std::chrono::steady_clock::now();
     for (unsigned k = 0;; k++) {
         if (!e->srv_launch || __atomic_load_n(&b->exited, __ATOMIC_ACQUIRE) == e->srv_launch) {
             // no server, or it exited (idle) before seeing this request: (re)start it after the
@@ -4334,6 +4335,10 @@ static int srv_call(gc_env* e, int board, int op, int action, int flags) {
         if ((k & 1023) == 1023) {  // a faulted server: the stream says so
             const hipError_t q = hipStreamQuery(e->srv_stream);
             if (q != hipSuccess && q != hipErrorNotReady) return fail(std::string("single-board server: ") + hipGetErrorString(q));
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) {
+                (void)srv_stop(e);
+                return fail("single-board server: no answer within 10 s");
+            }
         }
     }
     e->srv_seq = seq;
