@@ -277,6 +277,35 @@ __device__ __forceinline__ void list_one(const Pos& s, int attack, int cap, uint
     }
     counts[i] = n;
 }
+// list_one with the wave's 64 lanes (every lane holds the same s): lane = square, each own
+// piece's legal targets in reference order at its exclusive prefix-sum offset (the list is
+// row-major over the squares, lib.rs:501-563), the castles after them
+__device__ __forceinline__ void list_par(const Pos& s, int cap, uint16_t* out, int32_t* count) {
+    Gen g;
+    gen_init(s, g);
+    const int sq = (int)(threadIdx.x & 63);
+    const bool mine = (g.own >> sq) & 1;
+    const int t = mine ? type_at(s, sq) : 0;
+    const u64 tg = mine ? legal_targets(s, g, sq, t) : 0ull;
+    const int c = popc(tg);
+    int off = c;  // inclusive prefix sum over the lanes
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int v = __shfl_up(off, d, 64);
+        if (sq >= d) off += v;
+    }
+    const int n = __shfl(off, 63, 64);
+    off -= c;
+    for (int k = 0; k < c; k++)
+        if (off + k < cap) out[off + k] = (uint16_t)(sq * 64 + kth_target(tg, sq, t, g.white, k));
+    int m = n;
+    if (sq == 0) {
+        if (g.castles & 1) { if (m < cap) out[m] = g.white ? A_QSW : A_QSB; m++; }
+        if (g.castles & 2) { if (m < cap) out[m] = g.white ? A_KSW : A_KSB; m++; }
+        *count = m;
+    }
+}
+
 __global__ void k_list(SoA in, int attack, int cap, uint16_t* __restrict__ out, int32_t* __restrict__ counts) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= in.n) return;
@@ -2388,13 +2417,16 @@ __global__ void __launch_bounds__(BLOCK) k_env_rollout(EnvDev e, int plies, u64*
 enum { SOP_RESET = 0, SOP_AGENT = 1, SOP_REPLY = 2, SOP_OPEN = 3, SOP_SYNC = 4, SOP_SET = 5 };
 static_assert(sizeof(gc_single_record) == 728, "gym_chess_amd.single._REC mirrors this layout");
 __device__ __noinline__ void single_op(const EnvDev& e, int i, int op, int action, int flags, LdsScratch& scr,
-                                       gc_single_record* __restrict__ rec, const gc_single_record* in);
+                                       gc_single_record* __restrict__ rec, const gc_single_record* in, Pos* out_s);
 __global__ void __launch_bounds__(64) k_single(EnvDev e, int i, int op, int action, int flags,
                                                gc_single_record* __restrict__ hrec) {
     __shared__ u64 lds_scr[SCRATCH_SLOTS * BLOCK];
     __shared__ gc_single_record lrec;  // built here, then written to host memory by every lane
     LdsScratch scr{lds_scr + threadIdx.x};
-    if (threadIdx.x == 0) single_op(e, i, op, action, flags, scr, &lrec, hrec);
+    __shared__ Pos lpos;
+    if (threadIdx.x == 0) single_op(e, i, op, action, flags, scr, &lrec, hrec, &lpos);
+    __syncthreads();
+    list_par(lpos, GC_SINGLE_MOVES_CAP, lrec.moves, &lrec.nmoves);  // the move list: every lane
     __syncthreads();
     const uint32_t* src = reinterpret_cast<const uint32_t*>(&lrec);
     uint32_t* dst = reinterpret_cast<uint32_t*>(hrec);
@@ -2404,7 +2436,7 @@ __global__ void __launch_bounds__(64) k_single(EnvDev e, int i, int op, int acti
 }
 
 __device__ __noinline__ void single_op(const EnvDev& e, int i, int op, int action, int flags, LdsScratch& scr,
-                                       gc_single_record* __restrict__ rec, const gc_single_record* in) {
+                                       gc_single_record* __restrict__ rec, const gc_single_record* in, Pos* out_s) {
     Pos s = e.st.load(i);
     const u32 g0 = e.hgen[i];
     DevHist h = e.hist(i, g0);
@@ -2431,7 +2463,7 @@ __device__ __noinline__ void single_op(const EnvDev& e, int i, int op, int actio
             reason = R_MOVE_CAP;
         } else {
             const bool white = (s.meta & M_WHITE) != 0;
-            const int rc = env_ply(s, h, action, g, ms, scr, &mr, &rep, &chk);
+            const int rc = env_ply<true>(s, h, action, g, ms, scr, &mr, &rep, &chk);
             if (rc == 1) {
                 status = 1;  // lib.rs:1442-1446: the engine raises, nothing changes
             } else {
@@ -2448,7 +2480,7 @@ __device__ __noinline__ void single_op(const EnvDev& e, int i, int op, int actio
             }
         }
     } else if (op == SOP_REPLY) {  // 275-292
-        const int rc = env_ply(s, h, action, g, ms, scr, &mr, &rep, &chk);
+        const int rc = env_ply<true>(s, h, action, g, ms, scr, &mr, &rep, &chk);
         if (rc == 1) {
             status = 1;
         } else {
@@ -2464,7 +2496,7 @@ __device__ __noinline__ void single_op(const EnvDev& e, int i, int op, int actio
             if (s.meta & M_WHITE) s.meta += (1u << M_MC_SHIFT);
         }
     } else if (op == SOP_OPEN) {  // 208-216
-        const int rc = env_ply(s, h, action, g, ms, scr, &mr, &rep, &chk);
+        const int rc = env_ply<true>(s, h, action, g, ms, scr, &mr, &rep, &chk);
         if (rc == 1) status = 1;
         else s.meta = (s.meta & ~(u32)M_DONE) + (1u << M_MC_SHIFT);
     } else if (op == SOP_SET) {  // 315-323: board, rights, checks; nothing else changes
@@ -2489,7 +2521,7 @@ __device__ __noinline__ void single_op(const EnvDev& e, int i, int op, int actio
     rec->checked[0] = (s.meta & M_WCHK) != 0; rec->checked[1] = (s.meta & M_BCHK) != 0;
     rec->move_count = (uint16_t)mc_of(s.meta);
     to_mailbox(s, rec->board);
-    list_one(s, 0, GC_SINGLE_MOVES_CAP, rec->moves, &rec->nmoves, 0);
+    *out_s = s;  // the move list follows on every lane (list_par)
 }
 
 // ----------------------------------------------------------------------------- single-board server
@@ -2514,6 +2546,7 @@ __global__ void __launch_bounds__(64) k_single_server(EnvDev e, int i, SrvBox* b
                                                       u32 done_seq, u32 launch_id) {
     __shared__ u64 lds_scr[SCRATCH_SLOTS * BLOCK];
     __shared__ gc_single_record lrec;
+    __shared__ Pos lpos;
     LdsScratch scr{lds_scr + threadIdx.x};
     unsigned long long idle0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
     for (;;) {
@@ -2528,7 +2561,9 @@ __global__ void __launch_bounds__(64) k_single_server(EnvDev e, int i, SrvBox* b
         if (op == SRV_QUIT) break;
         const int action = (int)__builtin_amdgcn_readfirstlane(srv_load(reinterpret_cast<u32*>(&box->action)));
         const int flags = (int)__builtin_amdgcn_readfirstlane(srv_load(&box->flags));
-        if (threadIdx.x == 0) single_op(e, i, op, action, flags, scr, &lrec, hrec);
+        if (threadIdx.x == 0) single_op(e, i, op, action, flags, scr, &lrec, hrec, &lpos);
+        __syncthreads();
+        list_par(lpos, GC_SINGLE_MOVES_CAP, lrec.moves, &lrec.nmoves);
         __syncthreads();
         const uint32_t* src = reinterpret_cast<const uint32_t*>(&lrec);
         uint32_t* dst = reinterpret_cast<uint32_t*>(hrec);

@@ -53,6 +53,7 @@ from .codec import (BLACK, CASTLE_KING_SIDE_BLACK, CASTLE_KING_SIDE_WHITE, CASTL
 
 MOVES_MAX = 149  # chess_v2.py:141
 _ENCODE = "0ABCDEFfedcba"  # chess_v2.py:600: piece id -> character (negative ids from the end)
+_ENC_TABLE = bytes(ord(_ENCODE[(b if b < 128 else b - 256)]) if (b < 7 or b > 249) else 63 for b in range(256))
 
 # chess_v2.py:64-84 (icons and descriptions by piece id)
 _ICON = {-6: "♙", -5: "♘", -4: "♗", -3: "♖", -2: "♕", -1: "♔", 0: ".",
@@ -229,6 +230,7 @@ class ChessEnv:
             print(_BOTH_CHECKED)
             raise SystemError(_BOTH_CHECKED)
         self.board = rec["board"].reshape(8, 8).tolist()
+        self._key = rec["board"].tobytes().translate(_ENC_TABLE).decode("ascii")  # encode_board of it
         r, c = rec["rights"], rec["checked"]
         self.white_king_castle_is_possible, self.white_queen_castle_is_possible = bool(r[0]), bool(r[1])
         self.black_king_castle_is_possible, self.black_queen_castle_is_possible = bool(r[2]), bool(r[3])
@@ -247,7 +249,7 @@ class ChessEnv:
         pre-move board (chess_v2.py:409-411, skipped when the move ends by 3-fold)"""
         if op != OP_AGENT and action is None:
             self.action_to_move(action)  # the random policy's "resign": TypeError, as the reference
-        mover, pre, key = self.current_player, self.board, self.encode_board()
+        mover, pre, key = self.current_player, self.board, self._key
         stale = self._stale
         rec = self._take(self._b.call(op, action, flags))
         if stale and rec["reason"] == R_INVALID:
@@ -402,7 +404,7 @@ class ChessEnv:
         return self.engine.next_state(state, player, self.move_to_str_code(move))
 
     def encode_board(self):  # chess_v2.py:599-602
-        return "".join(_ENCODE[int(v)] for v in np.asarray(self.board).reshape(64))
+        return np.asarray(self.board, dtype=np.int8).reshape(64).tobytes().translate(_ENC_TABLE).decode("ascii")
 
     # ---------------------------------------------------------------- moves
     def get_possible_actions(self):
