@@ -40,6 +40,7 @@ record); the tests plug in the CPU oracle's restatement to check this class with
 `engine` (lazily a ChessEngine on the same device) serves the stateless helpers
 get_possible_moves / get_castle_moves / next_state with explicit states.
 """
+import struct
 import sys
 from collections import defaultdict
 from io import StringIO
@@ -133,9 +134,12 @@ class DeviceBoard:
 
     def call(self, op, action=0, flags=0):
         self._check(self._L.gc_env_single_call(self._h, 0, int(op), int(action), int(flags), self._ct.byref(self._rec)))
-        if self._view is None:  # the record's address is fixed per env
-            buf = (self._ct.c_uint8 * _REC.itemsize).from_address(self._rec.value)
-            self._view = np.frombuffer(buf, dtype=_REC, count=1)[0]
+        return self._mapped()
+
+    def _mapped(self):
+        """the host-mapped record (its address is fixed per env) as a memoryview"""
+        if self._view is None:
+            self._view = memoryview((self._ct.c_uint8 * _REC.itemsize).from_address(self._rec.value))
         return self._view
 
     def set_state(self, board, flags6):
@@ -145,10 +149,7 @@ class DeviceBoard:
         f = np.ascontiguousarray(flags6, dtype=np.uint8).reshape(6)
         self._check(self._L.gc_env_single_set(self._h, 0, b.ctypes.data_as(self._ct.c_void_p),
                                               f.ctypes.data_as(self._ct.c_void_p), self._ct.byref(self._rec)))
-        if self._view is None:
-            buf = (self._ct.c_uint8 * _REC.itemsize).from_address(self._rec.value)
-            self._view = np.frombuffer(buf, dtype=_REC, count=1)[0]
-        return self._view
+        return self._mapped()
 
     def window(self):
         """the live 3-fold window: {board bytes: count}"""
@@ -178,7 +179,13 @@ _REC = np.dtype([("status", "<i4"), ("reward", "<i4"), ("done", "u1"), ("reason"
                  ("white_to_move", "u1"), ("rights", "u1", (4,)), ("checked", "u1", (2,)), ("move_count", "<u2"),
                  ("nmoves", "<i4"), ("board", "i1", (64,)), ("moves", "<u2", (320,))])
 assert _REC.itemsize == 728  # = sizeof(gc_single_record), static_assert in gymchess.hip
+_HDR = struct.Struct("<iiBBBB4B2BHi")  # the record's fields before the board (_REC's layout)
+_BOARD_AT = _REC.fields["board"][1]
+_MOVES_AT = _REC.fields["moves"][1]
+assert _HDR.size == _BOARD_AT
+_ROWS = [struct.Struct("8b")] * 8
 
+GC_SINGLE_MOVES_CAP = 320
 _ACTION_MOVE = [C.action_to_move(a) if a < 4096 else C.ACTION_TO_CASTLE.get(a) for a in range(C.N_ACTIONS - 1)]
 
 
@@ -225,24 +232,29 @@ class ChessEnv:
         return [seed]
 
     def _take(self, rec):
-        """mirror the device record: state, side to move, done, move count, move list"""
-        if rec["status"]:
+        """mirror the device record (a buffer in gc_single_record's layout: the host-mapped
+        record itself, or a numpy record): state, side to move, done, move count, move list;
+        returns {status, reward, reason}"""
+        if isinstance(rec, np.void):
+            rec = rec.tobytes()
+        (status, reward, _, reason, env_done, wtm, r0, r1, r2, r3, c0, c1, mc, n) = _HDR.unpack_from(rec)
+        if status:
             print(_BOTH_CHECKED)
             raise SystemError(_BOTH_CHECKED)
-        self.board = rec["board"].reshape(8, 8).tolist()
-        self._key = rec["board"].tobytes().translate(_ENC_TABLE).decode("ascii")  # encode_board of it
-        r, c = rec["rights"], rec["checked"]
-        self.white_king_castle_is_possible, self.white_queen_castle_is_possible = bool(r[0]), bool(r[1])
-        self.black_king_castle_is_possible, self.black_queen_castle_is_possible = bool(r[2]), bool(r[3])
-        self.white_king_is_checked, self.black_king_is_checked = bool(c[0]), bool(c[1])
-        self.current_player = WHITE if rec["white_to_move"] else BLACK
-        self.done = bool(rec["env_done"])
-        self.move_count = int(rec["move_count"])
-        n = int(rec["nmoves"])
-        if n > len(rec["moves"]):
+        bb = bytes(rec[_BOARD_AT:_BOARD_AT + 64])
+        self.board = [list(_ROWS[0].unpack_from(bb, 8 * r)) for r in range(8)]
+        self._key = bb.translate(_ENC_TABLE).decode("ascii")  # encode_board of it
+        self.white_king_castle_is_possible, self.white_queen_castle_is_possible = bool(r0), bool(r1)
+        self.black_king_castle_is_possible, self.black_queen_castle_is_possible = bool(r2), bool(r3)
+        self.white_king_is_checked, self.black_king_is_checked = bool(c0), bool(c1)
+        self.current_player = WHITE if wtm else BLACK
+        self.done = bool(env_done)
+        self.move_count = mc
+        if n > GC_SINGLE_MOVES_CAP:
             raise RuntimeError(f"{n} legal moves: more than the record holds")
-        self._possible_moves = [_ACTION_MOVE[a] for a in rec["moves"][:n].tolist()]
-        return rec
+        am = _ACTION_MOVE
+        self._possible_moves = [am[a] for a in struct.unpack_from(f"<{n}H", rec, _MOVES_AT)]
+        return {"status": status, "reward": reward, "reason": reason}
 
     def _ply(self, op, action, flags=0):
         """one player_move on the device; with log, the reference's print + render of the
