@@ -2765,10 +2765,10 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
     k_env_step_api2(uint8_t* __restrict__ slab, uint64_t seed, u64* __restrict__ htab,
                     const uint16_t* __restrict__ racts, const EnvDev::InitCache* __restrict__ icd,
                     const uint16_t* __restrict__ acts, const ApiOut* __restrict__ outp, int nn,
-                    u32 rinfo /* autoreset << 17 | ic.table << 16 | ic.total */) {
+                    u32 rinfo /* first block << 18 | autoreset << 17 | ic.table << 16 | ic.total */) {
     constexpr int OPP = 0;
     constexpr bool API = true;
-    constexpr int blk0 = 0;
+    const int blk0 = (int)(rinfo >> 18);  // a launch may cover a sub-range of the board blocks
     const int autoreset = (rinfo >> 17) & 1;
     rinfo &= 0x1FFFFu;
     ApiOut out;
@@ -4502,8 +4502,29 @@ extern "C" int gc_env_step_device(gc_env* e, const uint16_t* d_actions, int32_t*
             HIPCHK(hipMemcpyAsync(e->api_out, &e->api_host, sizeof o, hipMemcpyHostToDevice, e->stream));
             HIPCHK(hipStreamSynchronize(e->stream));  // api_host may change again before a lazy copy ran
         }
-        k_env_step_api2<<<(nb + PAIRS_WG - 1) / PAIRS_WG, 2 * PAIR_BOARDS * PAIRS_WG, 0, e->stream>>>(
-            e->slab, d.seed, d.htab, r.racts, r.icd, d_actions, e->api_out, d.n, r.rinfo | ((u32)ar << 17));
+        // over the board-range streams (as gc_env_step_random): a range's next step waits only
+        // for its own last one, so one range's store tail (the mask: 520 B per board) overlaps
+        // the other's generation
+        static const int api_streams = getenv("GC_API_STREAMS") ? atoi(getenv("GC_API_STREAMS")) : 0;
+        const int k0 = api_streams > 0 ? (api_streams < e->n_sub ? api_streams : e->n_sub) : e->n_sub;
+        const int k = k0 < nb ? k0 : nb;
+        const u32 ri = r.rinfo | ((u32)ar << 17);
+        if (k <= 1) {
+            k_env_step_api2<<<(nb + PAIRS_WG - 1) / PAIRS_WG, 2 * PAIR_BOARDS * PAIRS_WG, 0, e->stream>>>(
+                e->slab, d.seed, d.htab, r.racts, r.icd, d_actions, e->api_out, d.n, ri);
+        } else {
+            const int per = ((nb + k - 1) / k + PAIRS_WG - 1) / PAIRS_WG * PAIRS_WG;  // whole workgroups
+            HIPCHK(hipEventRecord(e->fork_ev, e->stream));
+            for (int j = 0; j < k; j++) {
+                const int b0 = j * per, nbj = nb - b0 < per ? nb - b0 : per;
+                if (nbj <= 0) continue;
+                HIPCHK(hipStreamWaitEvent(e->sub[j], e->fork_ev, 0));
+                k_env_step_api2<<<(nbj + PAIRS_WG - 1) / PAIRS_WG, 2 * PAIR_BOARDS * PAIRS_WG, 0, e->sub[j]>>>(
+                    e->slab, d.seed, d.htab, r.racts, r.icd, d_actions, e->api_out, d.n, ri | ((u32)b0 << 18));
+                HIPCHK(hipEventRecord(e->sub_ev[j], e->sub[j]));
+                HIPCHK(hipStreamWaitEvent(e->stream, e->sub_ev[j], 0));
+            }
+        }
     } else if (e->d.opp && pair_ok(e) && !one_wave) {  // the random opponent on the paired driver
         const EnvDev& d = e->d;
         const ResetInfo r = reset_info(e);
