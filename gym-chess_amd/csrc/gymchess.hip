@@ -2537,6 +2537,7 @@ struct SrvBox {
     int32_t action, pad1[3];
     u32 resp_seq, pad2[15];  // own cache line
     u32 exited, pad3[15];    // the launch id of the last server that exited
+    u32 stamps[4];           // the last op's segments (10 ns ticks): the op, the list, the record copy, the idle wait
 };
 #define SRV_QUIT 99
 #define SRV_IDLE_MS 50
@@ -2556,6 +2557,7 @@ __global__ void __launch_bounds__(64) k_single_server(EnvDev e, int i, SrvBox* b
             __builtin_amdgcn_s_sleep(8);
             continue;
         }
+        const unsigned long long t_seen = __builtin_amdgcn_s_memrealtime();
         __atomic_thread_fence(__ATOMIC_ACQUIRE);  // the request's fields (and SET's inputs) after req_seq
         const int op = (int)__builtin_amdgcn_readfirstlane(srv_load(&box->op));
         if (op == SRV_QUIT) break;
@@ -2563,15 +2565,24 @@ __global__ void __launch_bounds__(64) k_single_server(EnvDev e, int i, SrvBox* b
         const int flags = (int)__builtin_amdgcn_readfirstlane(srv_load(&box->flags));
         if (threadIdx.x == 0) single_op(e, i, op, action, flags, scr, &lrec, hrec, &lpos);
         __syncthreads();
+        const unsigned long long t_op = __builtin_amdgcn_s_memrealtime();
         list_par(lpos, GC_SINGLE_MOVES_CAP, lrec.moves, &lrec.nmoves);
         __syncthreads();
+        const unsigned long long t_list = __builtin_amdgcn_s_memrealtime();
         const uint32_t* src = reinterpret_cast<const uint32_t*>(&lrec);
         uint32_t* dst = reinterpret_cast<uint32_t*>(hrec);
         const int words = (int)(offsetof(gc_single_record, moves) / 4) + (lrec.nmoves < GC_SINGLE_MOVES_CAP ? lrec.nmoves : GC_SINGLE_MOVES_CAP + 1) / 2 + 1;
         for (int k = threadIdx.x; k < words && k < (int)(sizeof(gc_single_record) / 4); k += 64) dst[k] = src[k];
         __threadfence_system();  // the record, then the response
         __syncthreads();
-        if (threadIdx.x == 0) srv_store(&box->resp_seq, req);
+        if (threadIdx.x == 0) {
+            const unsigned long long t_copy = __builtin_amdgcn_s_memrealtime();
+            srv_store(&box->stamps[0], (u32)(t_op - t_seen));
+            srv_store(&box->stamps[1], (u32)(t_list - t_op));
+            srv_store(&box->stamps[2], (u32)(t_copy - t_list));
+            srv_store(&box->stamps[3], (u32)(t_seen - idle0));
+            srv_store(&box->resp_seq, req);
+        }
         done_seq = req;
         idle0 = __builtin_amdgcn_s_memrealtime();
     }
@@ -4377,6 +4388,13 @@ static int srv_call(gc_env* e, int board, int op, int action, int flags) {
         }
     }
     e->srv_seq = seq;
+    return 0;
+}
+
+// diagnostic: the server's segments of its last op (10 ns ticks): op, list, record copy, idle
+extern "C" int gc_env_single_stamps(gc_env* e, uint32_t* out4) {
+    if (!e || !out4) return fail("null argument");
+    for (int k = 0; k < 4; k++) out4[k] = e->srv ? __atomic_load_n(&e->srv->stamps[k], __ATOMIC_ACQUIRE) : 0u;
     return 0;
 }
 

@@ -90,6 +90,7 @@ SIGNATURES = {
     "gc_env_single_setup": (_I, [_P, _I]),
     "gc_env_single_call": (_I, [_P, _I, _I, _I, _I, _P]),
     "gc_env_single_set": (_I, [_P, _I, _P, _P, _P]),
+    "gc_env_single_stamps": (_I, [_P, _P]),
     "gc_env_window_boards": (_I, [_P, _I, _P, _P, _I, _P]),
     "gc_env_get_outputs": (_I, [_P, _P, _P, _P, _P, _P]),
     "gc_env_get_states": (_I, [_P, _P, _P]),

@@ -43,6 +43,21 @@ def main():
         n, dt = bench.reference_driver(env, 10, 100, 0x5EED)
         res = {"step_us": dt / n * 1e6, "op_us": spent[0] / n * 1e6, "steps": n}
         if isinstance(b, DeviceBoard):
+            import ctypes
+
+            st = np.zeros(4, dtype=np.uint32)
+            acc = np.zeros(4)
+            for _ in range(200):  # AGENT ops of a fresh game: the server's segments
+                acts = env.possible_actions
+                if not acts:
+                    env.reset()
+                    continue
+                env.step(acts[len(acts) // 2])
+                b._L.gc_env_single_stamps(b._h, st.ctypes.data_as(ctypes.c_void_p))
+                acc += st
+                if env.done:
+                    env.reset()
+            res["server_segments_us"] = dict(zip(("op", "list", "record_copy", "idle_wait"), (acc / 200 / 100).tolist()))
             t = []
             for _ in range(500):
                 t0 = time.perf_counter()
