@@ -198,10 +198,11 @@ GC_HD int rep_commit(H& h, const Pos& s, const RepProbe& pr, u32& hl, bool irrev
 // `g`/`ms`/`scr` describe the side now to move; *mr = capture value, *rep = 3-fold verdict,
 // *nchk = the side now to move is in check.  Returns 1 (state unchanged) when both kings
 // end up in check (lib.rs:1442-1446), 2 (move applied, M_DONE) when the window is full.
-// Never touches move_count.  COUNT_ONLY: ms.total only (set-wise count_moves, no parked
-// targets) -- for callers that need the next side's count, not its moves (the single-board env
-// lists them itself).
-template <bool COUNT_ONLY = false, class H, class S>
+// Never touches move_count.
+// GEN: 2 = the next side's move set (gen_moves), 1 = its count only (set-wise count_moves, no
+// parked targets), 0 = neither (g = gen_init of the new position; the caller counts the moves
+// itself -- the single-board env lists them anyway).
+template <int GEN = 2, class H, class S>
 GC_HD int env_ply(Pos& s, H& hist, int action, Gen& g, MoveSet& ms, S& scr, int* mr, bool* rep, bool* nchk) {
     RepProbe pr;
     rep_prefetch(hist, s, pr);  // in flight during the move generation below
@@ -218,11 +219,11 @@ GC_HD int env_ply(Pos& s, H& hist, int action, Gen& g, MoveSet& ms, S& scr, int*
     bool my_chk = mover_checked(s, ns, white, action);
     GC_STAMP(3);
     if (opp_chk && my_chk) return 1;
-    if (COUNT_ONLY) {
-        moveset_clear(ms);
-        ms.total = count_moves(ns, g);
-    } else {
+    if (GEN == 2) {
         gen_moves(ns, g, ms, scr);  // the next side's possible moves (chess_v2.py:268 / 278)
+    } else {
+        moveset_clear(ms);
+        ms.total = GEN == 1 ? count_moves(ns, g) : 0;
     }
     GC_STAMP(4);
     u32 chk = white ? ((my_chk ? M_WCHK : 0u) | (opp_chk ? M_BCHK : 0u))

@@ -280,9 +280,10 @@ __device__ __forceinline__ void list_one(const Pos& s, int attack, int cap, uint
 // list_one with the wave's 64 lanes (every lane holds the same s): lane = square, each own
 // piece's legal targets in reference order at its exclusive prefix-sum offset (the list is
 // row-major over the squares, lib.rs:501-563), the castles after them
-__device__ __forceinline__ void list_par(const Pos& s, int cap, uint16_t* out, int32_t* count) {
+__device__ __forceinline__ void list_par(const Pos& s, int cap, uint16_t* out, int32_t* count, const Gen* g0 = nullptr) {
     Gen g;
-    gen_init(s, g);
+    if (g0) g = *g0;  // (gen_init of s, made by the caller)
+    else gen_init(s, g);
     const int sq = (int)(threadIdx.x & 63);
     const bool mine = (g.own >> sq) & 1;
     const int t = mine ? type_at(s, sq) : 0;
@@ -2416,42 +2417,42 @@ __global__ void __launch_bounds__(BLOCK) k_env_rollout(EnvDev e, int plies, u64*
 // the 3-fold window stay, as in the reference.
 enum { SOP_RESET = 0, SOP_AGENT = 1, SOP_REPLY = 2, SOP_OPEN = 3, SOP_SYNC = 4, SOP_SET = 5 };
 static_assert(sizeof(gc_single_record) == 728, "gym_chess_amd.single._REC mirrors this layout");
-__device__ __noinline__ void single_op(const EnvDev& e, int i, int op, int action, int flags, LdsScratch& scr,
-                                       gc_single_record* __restrict__ rec, const gc_single_record* in, Pos* out_s);
-__global__ void __launch_bounds__(64) k_single(EnvDev e, int i, int op, int action, int flags,
-                                               gc_single_record* __restrict__ hrec) {
-    __shared__ u64 lds_scr[SCRATCH_SLOTS * BLOCK];
-    __shared__ gc_single_record lrec;  // built here, then written to host memory by every lane
-    LdsScratch scr{lds_scr + threadIdx.x};
-    __shared__ Pos lpos;
-    if (threadIdx.x == 0) single_op(e, i, op, action, flags, scr, &lrec, hrec, &lpos);
-    __syncthreads();
-    list_par(lpos, GC_SINGLE_MOVES_CAP, lrec.moves, &lrec.nmoves);  // the move list: every lane
-    __syncthreads();
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(&lrec);
-    uint32_t* dst = reinterpret_cast<uint32_t*>(hrec);
-    const int words = (int)(offsetof(gc_single_record, moves) / 4) + (lrec.nmoves < GC_SINGLE_MOVES_CAP ? lrec.nmoves : GC_SINGLE_MOVES_CAP + 1) / 2 + 1;
-    for (int k = threadIdx.x; k < words && k < (int)(sizeof(gc_single_record) / 4); k += 64) dst[k] = src[k];
-    __threadfence_system();  // the record lives in host memory
-}
+// One op in three parts: single_begin (one lane: validation, the ply, the window) leaves the
+// position in LDS; list_par (every lane) lists the side to move's moves -- their count decides
+// a mate; single_end (one lane) settles the outcome, stores the state and fills the record.
+struct SingleCtx {
+    Pos s;
+    Gen g;               // gen_init of s after a ply (shared with list_par)
+    DevHist h;
+    u32 g0;
+    int status, reward, done, reason, chk, pend, white, flags, op, has_g;
+};
+enum { SPEND_NONE = 0, SPEND_AGENT = 1, SPEND_REPLY = 2 };
 
-__device__ __noinline__ void single_op(const EnvDev& e, int i, int op, int action, int flags, LdsScratch& scr,
-                                       gc_single_record* __restrict__ rec, const gc_single_record* in, Pos* out_s) {
+// valid: the action's validity when the caller knows it (the server: membership in the list it
+// made for this position), else -1 (action_legal on the position)
+__device__ __noinline__ void single_begin(const EnvDev& e, int i, int op, int action, int flags, int valid,
+                                          LdsScratch& scr, const gc_single_record* in, SingleCtx& c) {
     Pos s = e.st.load(i);
     const u32 g0 = e.hgen[i];
     DevHist h = e.hist(i, g0);
-    int status = 0, reward = 0, done = 0, reason = R_NONE;
+    int status = 0, reward = 0, done = 0, reason = R_NONE, pend = SPEND_NONE;
     Gen g;
     MoveSet ms;
     int mr = 0;
     bool rep = false, chk = false;
+    bool has_g = false;
+    const bool white = (s.meta & M_WHITE) != 0;
     if (op == SOP_RESET) {  // chess_v2.py:183-206
         s = e.ic.pos;
         h.bump_gen();
     } else if (op == SOP_AGENT) {
-        Gen gs;
-        gen_init(s, gs);
-        if (!action_legal(s, gs, action)) {  // 239-242: the state stays, done as it was
+        if (valid < 0) {
+            Gen gs;
+            gen_init(s, gs);
+            valid = action_legal(s, gs, action) ? 1 : 0;
+        }
+        if (!valid) {  // 239-242: the state stays, done as it was
             reward = -10;
             done = (s.meta & M_DONE) ? 1 : 0;
             reason = R_INVALID;
@@ -2462,58 +2463,71 @@ __device__ __noinline__ void single_op(const EnvDev& e, int i, int op, int actio
             done = 1;
             reason = R_MOVE_CAP;
         } else {
-            const bool white = (s.meta & M_WHITE) != 0;
-            const int rc = env_ply<true>(s, h, action, g, ms, scr, &mr, &rep, &chk);
+            const int rc = env_ply<0>(s, h, action, g, ms, scr, &mr, &rep, &chk);
             if (rc == 1) {
                 status = 1;  // lib.rs:1442-1446: the engine raises, nothing changes
             } else {
+                has_g = true;
                 reward = -10 + mr;  // 261-264 (Q9)
                 if (rep) { done = 1; reason = R_REPETITION; }
                 if (rc == 2) { done = 1; reason = R_WINDOW_FULL; }
-                if (ms.total == 0 && chk) {  // 269-272
-                    s.meta |= M_DONE;
-                    done = 1;
-                    reward += 100;
-                    reason = R_MATE;
-                }
-                if (!done && !(flags & 1) && !white) s.meta += (1u << M_MC_SHIFT);  // 291-292, no opponent
+                pend = SPEND_AGENT;  // the mate test and the move-count rule wait for the list
             }
         }
     } else if (op == SOP_REPLY) {  // 275-292
-        const int rc = env_ply<true>(s, h, action, g, ms, scr, &mr, &rep, &chk);
+        const int rc = env_ply<0>(s, h, action, g, ms, scr, &mr, &rep, &chk);
         if (rc == 1) {
             status = 1;
         } else {
+            has_g = true;
             reward = -mr;
             if (rep) { done = 1; reason = R_REPETITION; }
             if (rc == 2) { done = 1; reason = R_WINDOW_FULL; }
-            if (ms.total == 0 && chk) {
-                s.meta |= M_DONE;
-                done = 1;
-                reward -= 100;
-                reason = R_MATED;
-            }
-            if (s.meta & M_WHITE) s.meta += (1u << M_MC_SHIFT);
+            pend = SPEND_REPLY;
         }
     } else if (op == SOP_OPEN) {  // 208-216
-        const int rc = env_ply<true>(s, h, action, g, ms, scr, &mr, &rep, &chk);
+        const int rc = env_ply<0>(s, h, action, g, ms, scr, &mr, &rep, &chk);
         if (rc == 1) status = 1;
-        else s.meta = (s.meta & ~(u32)M_DONE) + (1u << M_MC_SHIFT);
+        else { has_g = true; s.meta = (s.meta & ~(u32)M_DONE) + (1u << M_MC_SHIFT); }
     } else if (op == SOP_SET) {  // 315-323: board, rights, checks; nothing else changes
         const u32 m = (s.meta & ~(u32)(M_RIGHTS | M_WCHK | M_BCHK)) | (in->rights[0] ? M_WKC : 0u) |
                       (in->rights[1] ? M_WQC : 0u) | (in->rights[2] ? M_BKC : 0u) | (in->rights[3] ? M_BQC : 0u) |
                       (in->checked[0] ? M_WCHK : 0u) | (in->checked[1] ? M_BCHK : 0u);
         s = from_mailbox(in->board, m);
     }
-    if (status == 0 && op != SOP_SYNC) {
-        h.commit();
-        e.st.store(i, s);
-        h.flush(g0);
+    c.s = s; c.g = g; c.h = h; c.g0 = g0;
+    c.status = status; c.reward = reward; c.done = done; c.reason = reason; c.chk = chk ? 1 : 0;
+    c.pend = pend; c.white = white ? 1 : 0; c.flags = flags; c.op = op; c.has_g = has_g ? 1 : 0;
+}
+
+__device__ __noinline__ void single_end(const EnvDev& e, int i, int nmoves, SingleCtx& c, gc_single_record* __restrict__ rec) {
+    Pos s = c.s;
+    if (c.pend == SPEND_AGENT) {
+        if (nmoves == 0 && c.chk) {  // 269-272
+            s.meta |= M_DONE;
+            c.done = 1;
+            c.reward += 100;
+            c.reason = R_MATE;
+        }
+        if (!c.done && !(c.flags & 1) && !c.white) s.meta += (1u << M_MC_SHIFT);  // 291-292, no opponent
+    } else if (c.pend == SPEND_REPLY) {
+        if (nmoves == 0 && c.chk) {
+            s.meta |= M_DONE;
+            c.done = 1;
+            c.reward -= 100;
+            c.reason = R_MATED;
+        }
+        if (s.meta & M_WHITE) s.meta += (1u << M_MC_SHIFT);
     }
-    rec->status = status;
-    rec->reward = reward;
-    rec->done = (uint8_t)done;
-    rec->reason = (uint8_t)reason;
+    if (c.status == 0 && c.op != SOP_SYNC) {
+        c.h.commit();
+        e.st.store(i, s);
+        c.h.flush(c.g0);
+    }
+    rec->status = c.status;
+    rec->reward = c.reward;
+    rec->done = (uint8_t)c.done;
+    rec->reason = (uint8_t)c.reason;
     rec->env_done = (s.meta & M_DONE) ? 1 : 0;
     rec->white_to_move = (s.meta & M_WHITE) ? 1 : 0;
     rec->rights[0] = (s.meta & M_WKC) != 0; rec->rights[1] = (s.meta & M_WQC) != 0;
@@ -2521,7 +2535,38 @@ __device__ __noinline__ void single_op(const EnvDev& e, int i, int op, int actio
     rec->checked[0] = (s.meta & M_WCHK) != 0; rec->checked[1] = (s.meta & M_BCHK) != 0;
     rec->move_count = (uint16_t)mc_of(s.meta);
     to_mailbox(s, rec->board);
-    *out_s = s;  // the move list follows on every lane (list_par)
+}
+
+// the three parts of one op on a 64-lane workgroup (c, lrec in LDS); valid as single_begin's
+__device__ __forceinline__ void single_run(const EnvDev& e, int i, int op, int action, int flags, int valid,
+                                           LdsScratch& scr, const gc_single_record* in, SingleCtx& c,
+                                           gc_single_record& lrec) {
+    if (threadIdx.x == 0) single_begin(e, i, op, action, flags, valid, scr, in, c);
+    __syncthreads();
+    list_par(c.s, GC_SINGLE_MOVES_CAP, lrec.moves, &lrec.nmoves, c.has_g ? &c.g : nullptr);  // every lane
+    __syncthreads();
+    if (threadIdx.x == 0) single_end(e, i, lrec.nmoves, c, &lrec);
+    __syncthreads();
+}
+
+// copy the record (LDS) to the host-mapped one, every lane
+__device__ __forceinline__ void single_publish(const gc_single_record& lrec, gc_single_record* __restrict__ hrec) {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(&lrec);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(hrec);
+    const int words = (int)(offsetof(gc_single_record, moves) / 4) + (lrec.nmoves < GC_SINGLE_MOVES_CAP ? lrec.nmoves : GC_SINGLE_MOVES_CAP + 1) / 2 + 1;
+    for (int k = threadIdx.x; k < words && k < (int)(sizeof(gc_single_record) / 4); k += 64) dst[k] = src[k];
+    __threadfence_system();  // the record lives in host memory
+}
+
+__global__ void __launch_bounds__(64) k_single(EnvDev e, int i, int op, int action, int flags,
+                                               gc_single_record* __restrict__ hrec) {
+    __shared__ u64 lds_scr[SCRATCH_SLOTS * BLOCK];
+    __shared__ gc_single_record lrec;  // built here, then written to host memory by every lane
+    __shared__ __attribute__((aligned(16))) unsigned char c_raw[sizeof(SingleCtx)];  // (SingleCtx has default member initialisers)
+    SingleCtx& c = *reinterpret_cast<SingleCtx*>(c_raw);
+    LdsScratch scr{lds_scr + threadIdx.x};
+    single_run(e, i, op, action, flags, -1, scr, hrec, c, lrec);
+    single_publish(lrec, hrec);
 }
 
 // ----------------------------------------------------------------------------- single-board server
@@ -2529,7 +2574,7 @@ __device__ __noinline__ void single_op(const EnvDev& e, int i, int op, int actio
 // ~25 us launch round trip -- tools/region_anatomy.hip -- plus k_single's cold loads): one
 // wave stays resident on its own stream and serves requests through a host-mapped mailbox.
 // The host writes the request, then bumps req_seq; the wave polls req_seq (system-scope loads,
-// s_sleep between), runs the same single_op, writes the record to host memory and then
+// s_sleep between), runs the same single_run, writes the record to host memory and then
 // resp_seq.  It exits on QUIT, or when no request came for SRV_IDLE_MS (so it has always
 // drained before its process can end); the host starts it again on the next request.
 struct SrvBox {
@@ -2537,7 +2582,7 @@ struct SrvBox {
     int32_t action, pad1[3];
     u32 resp_seq, pad2[15];  // own cache line
     u32 exited, pad3[15];    // the launch id of the last server that exited
-    u32 stamps[4];           // the last op's segments (10 ns ticks): the op, the list, the record copy, the idle wait
+    u32 stamps[4];           // the last op's segments (10 ns ticks): validation, the op (with its list), the record copy, the idle wait
 };
 #define SRV_QUIT 99
 #define SRV_IDLE_MS 50
@@ -2546,9 +2591,11 @@ __device__ __forceinline__ void srv_store(u32* p, u32 v) { __hip_atomic_store(p,
 __global__ void __launch_bounds__(64) k_single_server(EnvDev e, int i, SrvBox* box, gc_single_record* __restrict__ hrec,
                                                       u32 done_seq, u32 launch_id) {
     __shared__ u64 lds_scr[SCRATCH_SLOTS * BLOCK];
-    __shared__ gc_single_record lrec;
-    __shared__ Pos lpos;
+    __shared__ gc_single_record lrec;  // the last op's record: its move list validates the next AGENT
+    __shared__ __attribute__((aligned(16))) unsigned char c_raw[sizeof(SingleCtx)];  // (SingleCtx has default member initialisers)
+    SingleCtx& c = *reinterpret_cast<SingleCtx*>(c_raw);
     LdsScratch scr{lds_scr + threadIdx.x};
+    single_run(e, i, SOP_SYNC, 0, 0, 0, scr, hrec, c, lrec);  // the current position's list
     unsigned long long idle0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
     for (;;) {
         const u32 req = __builtin_amdgcn_readfirstlane(srv_load(&box->req_seq));
@@ -2563,17 +2610,15 @@ __global__ void __launch_bounds__(64) k_single_server(EnvDev e, int i, SrvBox* b
         if (op == SRV_QUIT) break;
         const int action = (int)__builtin_amdgcn_readfirstlane(srv_load(reinterpret_cast<u32*>(&box->action)));
         const int flags = (int)__builtin_amdgcn_readfirstlane(srv_load(&box->flags));
-        if (threadIdx.x == 0) single_op(e, i, op, action, flags, scr, &lrec, hrec, &lpos);
+        // chess_v2.py:240: the action against the list this server made for the position
+        bool hit = false;
+        for (int k = (int)threadIdx.x; k < lrec.nmoves && k < GC_SINGLE_MOVES_CAP; k += 64) hit |= lrec.moves[k] == (uint16_t)action;
+        const int valid = __ballot(hit) != 0 ? 1 : 0;
         __syncthreads();
         const unsigned long long t_op = __builtin_amdgcn_s_memrealtime();
-        list_par(lpos, GC_SINGLE_MOVES_CAP, lrec.moves, &lrec.nmoves);
-        __syncthreads();
+        single_run(e, i, op, action, flags, valid, scr, hrec, c, lrec);
         const unsigned long long t_list = __builtin_amdgcn_s_memrealtime();
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(&lrec);
-        uint32_t* dst = reinterpret_cast<uint32_t*>(hrec);
-        const int words = (int)(offsetof(gc_single_record, moves) / 4) + (lrec.nmoves < GC_SINGLE_MOVES_CAP ? lrec.nmoves : GC_SINGLE_MOVES_CAP + 1) / 2 + 1;
-        for (int k = threadIdx.x; k < words && k < (int)(sizeof(gc_single_record) / 4); k += 64) dst[k] = src[k];
-        __threadfence_system();  // the record, then the response
+        single_publish(lrec, hrec);  // the record, then the response
         __syncthreads();
         if (threadIdx.x == 0) {
             const unsigned long long t_copy = __builtin_amdgcn_s_memrealtime();
