@@ -678,6 +678,39 @@ GC_HD int kth_target(u64 tg, int sq, int t, bool white, int k) {
     }
 }
 
+// f(target) for every target of the piece (type t) on sq in reference order -- kth_target's
+// order in one pass: a leaper's offsets in order; a slider's rays in order, each outward
+// (ascending bits above the square, descending below)
+template <class F>
+GC_HD void for_targets_ordered(u64 tg, int sq, int t, bool white, F&& f) {
+    if (t == KING || t == KNIGHT || t == PAWN) {
+        const u64 pk = t == KING ? pack8(8, -8, 1, -1, 9, 7, -7, -9)
+                     : t == KNIGHT ? pack8(-17, -15, 15, 17, -10, -6, 6, 10)
+                     : white ? pack8(-8, -16, -7, -9, 99, 99, 99, 99) : pack8(8, 16, 9, 7, 99, 99, 99, 99);
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const int to = sq + (int)(signed char)(pk >> (8 * j));
+            if (to >= 0 && to < 64 && ((tg >> to) & 1)) f(to);
+        }
+    } else if (tg) {
+        const u64 lo = below(sq), hi = ~lo & ~bit(sq);
+        const bool rook = t == ROOK || t == QUEEN, bish = t == BISHOP || t == QUEEN;
+        const u64 fm = file_mask(sq), rm = row_mask(sq), dm = diag_mask(sq), am = anti_mask(sq);
+        const u64 ray[8] = {rook ? tg & fm & lo : 0, rook ? tg & fm & hi : 0, rook ? tg & rm & lo : 0,
+                            rook ? tg & rm & hi : 0, bish ? tg & dm & lo : 0, bish ? tg & am & lo : 0,
+                            bish ? tg & am & hi : 0, bish ? tg & dm & hi : 0};
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const bool desc = j == 0 || j == 2 || j == 4 || j == 5;  // toward lower indices: high -> low
+            for (u64 m = ray[j]; m;) {
+                const int to = desc ? msb(m) : ctz(m);
+                f(to);
+                m &= ~bit(to);
+            }
+        }
+    }
+}
+
 // ---- whole-position enumeration --------------------------------------------------------
 GC_HD int count_legal(const Pos& s, const Gen& g) {
     int n = 0;

@@ -265,11 +265,7 @@ __device__ __forceinline__ void list_one(const Pos& s, int attack, int cap, uint
         pcs &= pcs - 1;
         int t = type_at(s, sq);
         u64 tg = attack ? attack_targets(s, g, sq, t) : legal_targets(s, g, sq, t);
-        int c = popc(tg);
-        for (int k = 0; k < c; k++) {
-            if (n < cap) o[n] = (uint16_t)(sq * 64 + kth_target(tg, sq, t, g.white, k));
-            n++;
-        }
+        for_targets_ordered(tg, sq, t, g.white, [&](int to) { if (n < cap) o[n] = (uint16_t)(sq * 64 + to); n++; });
     }
     if (!attack) {
         if (g.castles & 1) { if (n < cap) o[n] = g.white ? A_QSW : A_QSB; n++; }
@@ -297,8 +293,8 @@ __device__ __forceinline__ void list_par(const Pos& s, int cap, uint16_t* out, i
     }
     const int n = __shfl(off, 63, 64);
     off -= c;
-    for (int k = 0; k < c; k++)
-        if (off + k < cap) out[off + k] = (uint16_t)(sq * 64 + kth_target(tg, sq, t, g.white, k));
+    int w = off;
+    for_targets_ordered(tg, sq, t, g.white, [&](int to) { if (w < cap) out[w] = (uint16_t)(sq * 64 + to); w++; });
     int m = n;
     if (sq == 0) {
         if (g.castles & 1) { if (m < cap) out[m] = g.white ? A_QSW : A_QSB; m++; }

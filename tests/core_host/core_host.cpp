@@ -50,6 +50,25 @@ extern "C" int host_list(const int8_t* b, const uint8_t* m, int white, int attac
     return n;
 }
 
+// the same list through for_targets_ordered (the device's list_one / list_par emit)
+extern "C" int host_list_emit(const int8_t* b, const uint8_t* m, int white, int attack, uint16_t* out, int cap) {
+    Pos s = import_state(b, m, white);
+    Gen g;
+    gen_init(s, g);
+    int n = 0;
+    for (u64 pcs = g.own; pcs; pcs &= pcs - 1) {
+        int sq = ctz(pcs);
+        int t = type_at(s, sq);
+        u64 tg = attack ? attack_targets(s, g, sq, t) : legal_targets(s, g, sq, t);
+        for_targets_ordered(tg, sq, t, g.white, [&](int to) { if (n < cap) out[n] = (uint16_t)(sq * 64 + to); n++; });
+    }
+    if (!attack) {
+        if (g.castles & 1) { if (n < cap) out[n] = g.white ? A_QSW : A_QSB; n++; }
+        if (g.castles & 2) { if (n < cap) out[n] = g.white ? A_KSW : A_KSB; n++; }
+    }
+    return n;
+}
+
 extern "C" int host_count(const int8_t* b, const uint8_t* m, int white) {
     Pos s = import_state(b, m, white);
     Gen g;

@@ -41,6 +41,7 @@ def lib():
         L.host_perft_small.restype = ctypes.c_uint64
         L.host_perft_small.argtypes = [P, P, ctypes.c_int]
         L.host_list.argtypes = [P, P, ctypes.c_int, ctypes.c_int, P, ctypes.c_int]
+        L.host_list_emit.argtypes = [P, P, ctypes.c_int, ctypes.c_int, P, ctypes.c_int]
         L.host_count.argtypes = [P, P, ctypes.c_int]
         L.host_count2.argtypes = [P, P, ctypes.c_int]
         L.host_select2.argtypes = [P, P, ctypes.c_int, ctypes.c_int]
@@ -87,6 +88,14 @@ def get_list(board, meta, white, attack=False):
     b, m = _bm(board, meta)
     out = np.zeros(1024, dtype=np.uint16)
     n = lib().host_list(_p(b), _p(m), int(white), int(bool(attack)), _p(out), 1024)
+    return [int(x) for x in out[:n]]
+
+
+def get_list_emit(board, meta, white, attack=False):
+    """get_list through for_targets_ordered (the device's one-pass emit)"""
+    b, m = _bm(board, meta)
+    out = np.zeros(1024, dtype=np.uint16)
+    n = lib().host_list_emit(_p(b), _p(m), int(white), int(bool(attack)), _p(out), 1024)
     return [int(x) for x in out[:n]]
 
 

@@ -67,6 +67,7 @@ def test_v1_games(oracle):
             b = C.text_to_board(p["board"])
             m = oracle.make_meta(p["white"], *p["rights"])
             assert H.get_list(b, m, p["white"]) == p["moves"]
+            assert H.get_list_emit(b, m, p["white"]) == p["moves"]
 
 
 def test_perft_startpos(oracle):
@@ -83,6 +84,7 @@ def test_fuzz_positions(oracle, seed):
         for white in (0, 1):
             ref = oracle.get_possible_moves(b, m, white)
             assert H.get_list(b, m, white) == ref, (i, white)
+            assert H.get_list_emit(b, m, white) == ref, (i, white)  # for_targets_ordered (list_one / list_par)
             assert H.count(b, m, white) == len(ref)
             assert H.count2(b, m, white) == len(ref)
             srt = sorted(ref)
@@ -94,6 +96,7 @@ def test_fuzz_positions(oracle, seed):
             for a in list(legal)[:5] + [int(x) for x in rng.randint(0, 4101, size=5)]:
                 assert H.action_legal(b, m, white, a) == (a in legal)
             assert H.get_list(b, m, white, attack=True) == oracle.get_possible_moves(b, m, white, True)
+            assert H.get_list_emit(b, m, white, attack=True) == oracle.get_possible_moves(b, m, white, True)
         rb, rm = oracle.update_state(b, m)
         hb, hm = H.update_state(b, m)
         assert list(hm[:7]) == list(rm[:7])
