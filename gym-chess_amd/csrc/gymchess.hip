@@ -2827,6 +2827,9 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
     PAIR_PROLOGUE_ACT(acts, out = *outp; asm volatile("" : "+s"(out.rw), "+s"(out.dn), "+s"(out.rs), "+s"(out.mask),
                                                                   "+s"(out.obs), "+s"(out.cnt), "+s"(out.pick));)
     PairScratch scr{&L.slots[0][l]};
+#ifdef GC_API_PRIO  // diagnostic: issue priority 2 for W0 (1) or W1 (2)
+    if ((GC_API_PRIO == 1 && role == 0) || (GC_API_PRIO == 2 && role == 1)) __builtin_amdgcn_s_setprio(2);
+#endif
     const bool done0 = (s.meta & M_DONE) != 0;              // chess_v2.py:245-251
     const bool cap = mc_of(s.meta) > MOVES_MAX;             // 252-258
     const bool white = (s.meta & M_WHITE) != 0;
