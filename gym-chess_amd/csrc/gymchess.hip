@@ -2422,6 +2422,8 @@ struct SingleCtx {
     DevHist h;
     u32 g0;
     int status, reward, done, reason, chk, pend, white, flags, op, has_g;
+    int cached;          // (the server) s and h.g hold the board's state and window generation
+    unsigned long long t[3];  // (the server) begin / list / end done (s_memrealtime)
 };
 enum { SPEND_NONE = 0, SPEND_AGENT = 1, SPEND_REPLY = 2 };
 
@@ -2429,8 +2431,9 @@ enum { SPEND_NONE = 0, SPEND_AGENT = 1, SPEND_REPLY = 2 };
 // made for this position), else -1 (action_legal on the position)
 __device__ __noinline__ void single_begin(const EnvDev& e, int i, int op, int action, int flags, int valid,
                                           LdsScratch& scr, const gc_single_record* in, SingleCtx& c) {
-    Pos s = e.st.load(i);
-    const u32 g0 = e.hgen[i];
+    // the board's state: the server's copy from its last op, else from the env's memory
+    Pos s = c.cached ? c.s : e.st.load(i);
+    const u32 g0 = c.cached ? c.h.g : e.hgen[i];
     DevHist h = e.hist(i, g0);
     int status = 0, reward = 0, done = 0, reason = R_NONE, pend = SPEND_NONE;
     Gen g;
@@ -2520,6 +2523,7 @@ __device__ __noinline__ void single_end(const EnvDev& e, int i, int nmoves, Sing
         e.st.store(i, s);
         c.h.flush(c.g0);
     }
+    c.s = s;  // (the server keeps it for its next op)
     rec->status = c.status;
     rec->reward = c.reward;
     rec->done = (uint8_t)c.done;
@@ -2537,11 +2541,18 @@ __device__ __noinline__ void single_end(const EnvDev& e, int i, int nmoves, Sing
 __device__ __forceinline__ void single_run(const EnvDev& e, int i, int op, int action, int flags, int valid,
                                            LdsScratch& scr, const gc_single_record* in, SingleCtx& c,
                                            gc_single_record& lrec) {
-    if (threadIdx.x == 0) single_begin(e, i, op, action, flags, valid, scr, in, c);
+    if (threadIdx.x == 0) {
+        single_begin(e, i, op, action, flags, valid, scr, in, c);
+        c.t[0] = __builtin_amdgcn_s_memrealtime();
+    }
     __syncthreads();
     list_par(c.s, GC_SINGLE_MOVES_CAP, lrec.moves, &lrec.nmoves, c.has_g ? &c.g : nullptr);  // every lane
     __syncthreads();
-    if (threadIdx.x == 0) single_end(e, i, lrec.nmoves, c, &lrec);
+    if (threadIdx.x == 0) {
+        c.t[1] = __builtin_amdgcn_s_memrealtime();
+        single_end(e, i, lrec.nmoves, c, &lrec);
+        c.t[2] = __builtin_amdgcn_s_memrealtime();
+    }
     __syncthreads();
 }
 
@@ -2561,6 +2572,7 @@ __global__ void __launch_bounds__(64) k_single(EnvDev e, int i, int op, int acti
     __shared__ __attribute__((aligned(16))) unsigned char c_raw[sizeof(SingleCtx)];  // (SingleCtx has default member initialisers)
     SingleCtx& c = *reinterpret_cast<SingleCtx*>(c_raw);
     LdsScratch scr{lds_scr + threadIdx.x};
+    if (threadIdx.x == 0) c.cached = 0;
     single_run(e, i, op, action, flags, -1, scr, hrec, c, lrec);
     single_publish(lrec, hrec);
 }
@@ -2574,11 +2586,15 @@ __global__ void __launch_bounds__(64) k_single(EnvDev e, int i, int op, int acti
 // resp_seq.  It exits on QUIT, or when no request came for SRV_IDLE_MS (so it has always
 // drained before its process can end); the host starts it again on the next request.
 struct SrvBox {
-    u32 req_seq, op, flags, pad0;
-    int32_t action, pad1[3];
+    // the request: one 16-byte read on the device (the host writes op / action / flags, then seq)
+    u32 req_seq, op;
+    int32_t action;
+    u32 flags;
+    u32 pad1[12];
     u32 resp_seq, pad2[15];  // own cache line
     u32 exited, pad3[15];    // the launch id of the last server that exited
-    u32 stamps[4];           // the last op's segments (10 ns ticks): validation, the op (with its list), the record copy, the idle wait
+    // the last op's segments (10 ns ticks): request read + validation, begin, list, end, record copy, idle wait
+    u32 stamps[6];
 };
 #define SRV_QUIT 99
 #define SRV_IDLE_MS 50
@@ -2591,21 +2607,27 @@ __global__ void __launch_bounds__(64) k_single_server(EnvDev e, int i, SrvBox* b
     __shared__ __attribute__((aligned(16))) unsigned char c_raw[sizeof(SingleCtx)];  // (SingleCtx has default member initialisers)
     SingleCtx& c = *reinterpret_cast<SingleCtx*>(c_raw);
     LdsScratch scr{lds_scr + threadIdx.x};
+    if (threadIdx.x == 0) c.cached = 0;
     single_run(e, i, SOP_SYNC, 0, 0, 0, scr, hrec, c, lrec);  // the current position's list
+    if (threadIdx.x == 0) c.cached = 1;  // from here on the board's state lives here (and is stored after every op)
     unsigned long long idle0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
     for (;;) {
-        const u32 req = __builtin_amdgcn_readfirstlane(srv_load(&box->req_seq));
+        // the request in one 16-byte read from host memory: {seq, op, action, flags} (the host
+        // writes seq last, so a new seq comes with its fields)
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 rq = *reinterpret_cast<const volatile u32x4*>(box);
+        const u32 req = __builtin_amdgcn_readfirstlane(rq.x);
         if (req == done_seq) {
             if (__builtin_amdgcn_s_memrealtime() - idle0 > (unsigned long long)SRV_IDLE_MS * 100000ull) break;
             __builtin_amdgcn_s_sleep(8);
             continue;
         }
         const unsigned long long t_seen = __builtin_amdgcn_s_memrealtime();
-        __atomic_thread_fence(__ATOMIC_ACQUIRE);  // the request's fields (and SET's inputs) after req_seq
-        const int op = (int)__builtin_amdgcn_readfirstlane(srv_load(&box->op));
+        __atomic_thread_fence(__ATOMIC_ACQUIRE);  // SET's inputs (the record) after req_seq
+        const int op = (int)__builtin_amdgcn_readfirstlane(rq.y);
         if (op == SRV_QUIT) break;
-        const int action = (int)__builtin_amdgcn_readfirstlane(srv_load(reinterpret_cast<u32*>(&box->action)));
-        const int flags = (int)__builtin_amdgcn_readfirstlane(srv_load(&box->flags));
+        const int action = (int)__builtin_amdgcn_readfirstlane(rq.z);
+        const int flags = (int)__builtin_amdgcn_readfirstlane(rq.w);
         // chess_v2.py:240: the action against the list this server made for the position
         bool hit = false;
         for (int k = (int)threadIdx.x; k < lrec.nmoves && k < GC_SINGLE_MOVES_CAP; k += 64) hit |= lrec.moves[k] == (uint16_t)action;
@@ -2619,9 +2641,11 @@ __global__ void __launch_bounds__(64) k_single_server(EnvDev e, int i, SrvBox* b
         if (threadIdx.x == 0) {
             const unsigned long long t_copy = __builtin_amdgcn_s_memrealtime();
             srv_store(&box->stamps[0], (u32)(t_op - t_seen));
-            srv_store(&box->stamps[1], (u32)(t_list - t_op));
-            srv_store(&box->stamps[2], (u32)(t_copy - t_list));
-            srv_store(&box->stamps[3], (u32)(t_seen - idle0));
+            srv_store(&box->stamps[1], (u32)(c.t[0] - t_op));
+            srv_store(&box->stamps[2], (u32)(c.t[1] - c.t[0]));
+            srv_store(&box->stamps[3], (u32)(c.t[2] - c.t[1]));
+            srv_store(&box->stamps[4], (u32)(t_copy - t_list));
+            srv_store(&box->stamps[5], (u32)(t_seen - idle0));
             srv_store(&box->resp_seq, req);
         }
         done_seq = req;
@@ -4405,10 +4429,10 @@ static int srv_call(gc_env* e, int board, int op, int action, int flags) {
     if (e->srv_launch && e->srv_board != board && srv_stop(e)) return -1;
     SrvBox* b = e->srv;
     const u32 seq = e->srv_seq + 1;
-    b->op = (u32)op;
-    b->action = action;
-    b->flags = (u32)flags;
-    __atomic_store_n(&b->req_seq, seq, __ATOMIC_RELEASE);
+    __atomic_store_n(&b->op, (u32)op, __ATOMIC_RELAXED);
+    __atomic_store_n(&b->action, action, __ATOMIC_RELAXED);
+    __atomic_store_n(&b->flags, (u32)flags, __ATOMIC_RELAXED);
+    __atomic_store_n(&b->req_seq, seq, __ATOMIC_RELEASE);  // last: the device reads the four words at once
     const auto t0 = std::chrono::steady_clock::now();
     for (unsigned k = 0;; k++) {
         if (!e->srv_launch || __atomic_load_n(&b->exited, __ATOMIC_ACQUIRE) == e->srv_launch) {
@@ -4436,9 +4460,9 @@ static int srv_call(gc_env* e, int board, int op, int action, int flags) {
 }
 
 // diagnostic: the server's segments of its last op (10 ns ticks): op, list, record copy, idle
-extern "C" int gc_env_single_stamps(gc_env* e, uint32_t* out4) {
-    if (!e || !out4) return fail("null argument");
-    for (int k = 0; k < 4; k++) out4[k] = e->srv ? __atomic_load_n(&e->srv->stamps[k], __ATOMIC_ACQUIRE) : 0u;
+extern "C" int gc_env_single_stamps(gc_env* e, uint32_t* out6) {
+    if (!e || !out6) return fail("null argument");
+    for (int k = 0; k < 6; k++) out6[k] = e->srv ? __atomic_load_n(&e->srv->stamps[k], __ATOMIC_ACQUIRE) : 0u;
     return 0;
 }
 

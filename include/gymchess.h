@@ -126,9 +126,10 @@ typedef struct {
 } gc_single_record;
 int gc_env_single_setup(gc_env* e, int agent_white);
 int gc_env_single_call(gc_env* e, int board, int op, int action, int flags, const gc_single_record** rec);
-/* diagnostic: the single-board server's last op by segment, in 10 ns ticks: {the op, the move
- * list, the record's copy to host memory, the wait for the request} */
-int gc_env_single_stamps(gc_env* e, uint32_t* out4);
+/* diagnostic: the single-board server's last op by segment, in 10 ns ticks: {the request's read
+ * and validation, the ply, the move list, the outcome and stores, the record's copy to host
+ * memory, the wait for the request} */
+int gc_env_single_stamps(gc_env* e, uint32_t* out6);
 /* the env's state setter (chess_v2.py:315-323) on board `board`: its pieces (int8[64]) and
  * flags6 = {wkc, wqc, bkc, bqc, white_checked, black_checked}; the side to move, move_count,
  * done and the 3-fold window stay.  *rec as gc_env_single_call (the new position's list). */

@@ -45,8 +45,8 @@ def main():
         if isinstance(b, DeviceBoard):
             import ctypes
 
-            st = np.zeros(4, dtype=np.uint32)
-            acc = np.zeros(4)
+            st = np.zeros(6, dtype=np.uint32)
+            acc = np.zeros(6)
             for _ in range(200):  # AGENT ops of a fresh game: the server's segments
                 acts = env.possible_actions
                 if not acts:
@@ -57,7 +57,7 @@ def main():
                 acc += st
                 if env.done:
                     env.reset()
-            res["server_segments_us"] = dict(zip(("op", "list", "record_copy", "idle_wait"), (acc / 200 / 100).tolist()))
+            res["server_segments_us"] = dict(zip(("request_validate", "begin", "list", "end", "record_copy", "idle_wait"), (acc / 200 / 100).tolist()))
             t = []
             for _ in range(500):
                 t0 = time.perf_counter()
