@@ -2533,8 +2533,7 @@ __device__ __noinline__ void single_end(const EnvDev& e, int i, int nmoves, Sing
     rec->rights[0] = (s.meta & M_WKC) != 0; rec->rights[1] = (s.meta & M_WQC) != 0;
     rec->rights[2] = (s.meta & M_BKC) != 0; rec->rights[3] = (s.meta & M_BQC) != 0;
     rec->checked[0] = (s.meta & M_WCHK) != 0; rec->checked[1] = (s.meta & M_BCHK) != 0;
-    rec->move_count = (uint16_t)mc_of(s.meta);
-    to_mailbox(s, rec->board);
+    rec->move_count = (uint16_t)mc_of(s.meta);  // (the board: every lane, single_run)
 }
 
 // the three parts of one op on a 64-lane workgroup (c, lrec in LDS); valid as single_begin's
@@ -2553,6 +2552,8 @@ __device__ __forceinline__ void single_run(const EnvDev& e, int i, int op, int a
         single_end(e, i, lrec.nmoves, c, &lrec);
         c.t[2] = __builtin_amdgcn_s_memrealtime();
     }
+    __syncthreads();
+    lrec.board[threadIdx.x & 63] = (int8_t)id_at(c.s, (int)(threadIdx.x & 63));  // the mailbox, a square per lane
     __syncthreads();
 }
 
