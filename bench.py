@@ -167,7 +167,7 @@ def perft_leg(args, rep):
     depth and must match exactly; at N=1 that run is also the perft CPU baseline."""
     import numpy as np
 
-    from gym_chess_amd.engine import Engine, perft_leaf_stats, perft_path_counts
+    from gym_chess_amd.engine import Engine, perft_dedup_stats, perft_leaf_stats, perft_path_counts
     from gym_chess_amd.fen import fen_to_arrays
 
     def prep(rp):
@@ -183,6 +183,7 @@ def perft_leg(args, rep):
     ctx = rep.run(prep)
     paths0 = perft_path_counts()
     leaf0 = perft_leaf_stats()
+    dd0 = perft_dedup_stats()
 
     def run(rp):
         eng, b, m = ctx[rep.local.index(rp)]
@@ -193,6 +194,7 @@ def perft_leg(args, rep):
     res, dtm = rep.timed(run)
     paths1 = perft_path_counts()
     leaf1 = perft_leaf_stats()
+    dd1 = perft_dedup_stats()
     for eng, _, _ in ctx:
         eng.close()
     tot = rep.sum(float(sum(float(r.sum()) for r in res)))
@@ -209,11 +211,20 @@ def perft_leg(args, rep):
     # subtree (the 64-B root record in, its count added into the parent's sum) against ~1e3
     # leaves -- so its roof is the VALU issue rate (PMC profile, tools/gpu_run.sh pmcp*).
     # GC_PERFT_GATHER: the earlier form, gathering through a sorted permutation (+ 4 B index)
+    # Transpositions (round 4): the split pass counts one depth-2 subtree per distinct position
+    # of a chunk (k_dedup, exact: whole-record compare) and adds that count to every parent the
+    # position occurs under; GC_PERFT_DEDUP=0 counts every record
     gather = bool(os.environ.get("GC_PERFT_GATHER"))
-    alg_sub = 76 if gather else 72
+    dedup = not gather and os.environ.get("GC_PERFT_DEDUP", "1") != "0"
+    alg_sub = 76 if gather else (84 if dedup else 72)  # + the 4-B leader index and the 8-B count kept
     la, sub, kms = (b - a for a, b in zip(leaf0, leaf1))
+    recs, counted = (b - a for a, b in zip(dd0, dd1))
+    if recs:
+        out["transpositions"] = {"records": recs, "counted": counted, "records_per_counted": recs / max(1, counted),
+                                 "merged": dedup}
     if la:
-        roof = {"bound": "valu", "kernel": "k_perft2_perm_rec" if gather else "k_perft2_rec", "launches": la,
+        kname = "k_perft2_perm_rec" if gather else ("k_perft2_lead" if dedup else "k_perft2_rec")
+        roof = {"bound": "valu", "kernel": kname, "launches": la,
                 "subtrees": sub, "kernel_ms": kms, "share_of_perft_time": kms / 1e3 / len(rep.local) / dtm,
                 "alg_bytes_per_subtree": alg_sub, "hbm_achieved_gbs": alg_sub * sub / (kms / 1e3) / 1e9}
         pf = os.path.join(ROOT, "profiles", "pmc_perft_latest.json")

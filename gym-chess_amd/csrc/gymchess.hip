@@ -605,6 +605,90 @@ k_perft2_rec(const Node64* __restrict__ in, int n, unsigned long long* __restric
     atomicAdd(parent_sum + parent, (unsigned long long)perft2(node_load(in, i), sa));
 }
 
+// Transpositions among the depth-2 roots (round 4): a chunk's ply-3 records repeat -- m1, x,
+// m3 and m3, x, m1 reach one position -- ~1.7 records per distinct position over mid-game
+// roots.  perft2 is a function of the Pos alone, so one record per position (its leader) is
+// counted and the others (followers) add the leader's count into their own parents.
+// k_dedup: every record claims a slot of an open-addressed table keyed by a hash of its Pos
+// (entry = hash tag << 32 | record index, 0 = empty); a hash match is confirmed by comparing
+// the two whole records (written by k_expand_place, the previous launch), so a merge is exact.
+// Leaders are flagged for the order-keeping compaction (the leaf kernel still reads them in
+// move-count order); followers append (parent, leader) to a list, one atomic per wave.
+__device__ __forceinline__ u64 pos_hash(const Pos& s) {
+    u64 h = s.meta * 0x9E3779B97F4A7C15ull;
+    const u64 f[7] = {s.k, s.q, s.r, s.b, s.n, s.p, s.w};
+#pragma unroll
+    for (int k = 0; k < 7; k++) {
+        h ^= f[k] + 0x632BE59BD9B4E019ull + (h << 6) + (h >> 2);
+        h *= 0xBF58476D1CE4E5B9ull;
+    }
+    return h ^ (h >> 31);
+}
+__device__ __forceinline__ bool pos_equal(const Pos& a, const Pos& b) {
+    return ((a.k ^ b.k) | (a.q ^ b.q) | (a.r ^ b.r) | (a.b ^ b.b) | (a.n ^ b.n) | (a.p ^ b.p) | (a.w ^ b.w)) == 0 &&
+           a.meta == b.meta;
+}
+__global__ void __launch_bounds__(BLOCK) k_dedup(const Node64* __restrict__ in, int n, u64* __restrict__ table,
+                                                 u32 mask, uint8_t* __restrict__ leader, u32* __restrict__ nfol,
+                                                 uint2* __restrict__ fol) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    bool follower = false;
+    u32 lead = 0, parent = 0;
+    if (i < n) {
+        const Pos s = node_load(in, i);
+        parent = reinterpret_cast<const u32*>(in + i)[15];
+        const u64 h = pos_hash(s);
+        const u64 tag = (h >> 32) | 1u;
+        const u64 mine = (tag << 32) | (u32)i;
+        u32 slot = (u32)h & mask;
+        for (;;) {
+            u64 e = __hip_atomic_load(table + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (e == 0) {
+                e = atomicCAS(reinterpret_cast<unsigned long long*>(table + slot), 0ull, (unsigned long long)mine);
+                if (e == 0) break;  // this record leads its position
+            }
+            if ((e >> 32) == tag && pos_equal(node_load(in, (u32)e), s)) {
+                follower = true;
+                lead = (u32)e;
+                break;
+            }
+            slot = (slot + 1) & mask;
+        }
+        leader[i] = follower ? 0 : 1;
+    }
+    // wave-aggregated append of the followers
+    const u64 bal = __ballot(follower);
+    if (bal == 0) return;
+    const int lane = threadIdx.x & 63;
+    const int first = __ffsll((long long)bal) - 1;
+    u32 base = 0;
+    if (lane == first) base = atomicAdd(nfol, (u32)__popcll(bal));
+    base = __shfl(base, first);
+    if (follower) fol[base + __popcll(bal & ((1ull << lane) - 1))] = make_uint2(parent, lead);
+}
+// the leaders (compacted, in record order) counted; their counts kept for the followers
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(PERFT2_WPE)))
+k_perft2_lead(const Node64* __restrict__ in, const int32_t* __restrict__ idx, int n, uint64_t* __restrict__ val,
+              unsigned long long* __restrict__ parent_sum) {
+    __shared__ u64 lds_a[SCRATCH_SLOTS * BLOCK];
+    LdsScratch sa{lds_a + threadIdx.x};
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int j = idx[i];
+    const u32 parent = reinterpret_cast<const u32*>(in + j)[15];
+    const uint64_t c = perft2(node_load(in, j), sa);
+    val[j] = c;
+    atomicAdd(parent_sum + parent, (unsigned long long)c);
+}
+__global__ void k_followers(const uint2* __restrict__ fol, const u32* __restrict__ nfol,
+                            const uint64_t* __restrict__ val, unsigned long long* __restrict__ parent_sum) {
+    const u32 n = *nfol;
+    for (u32 i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint2 f = fol[i];
+        atomicAdd(parent_sum + f.x, (unsigned long long)val[f.y]);
+    }
+}
+
 // parent value = sum of its children's values (children of one parent are contiguous)
 template <class T>
 __global__ void k_sum_children(const T* __restrict__ offs, const T* __restrict__ cnt,
@@ -3529,46 +3613,62 @@ extern "C" int gc_engine_update_state(gc_engine* e, int n, const int8_t* boards,
 // leaf-kernel time of the split pass (gc_perft_leaf_stats): HIP events around every
 // k_perft2_perm launch, on the stream it runs on; summed once the pass has synchronised
 static std::mutex g_leaf_mu;
-static uint64_t g_leaf_launches = 0, g_leaf_subtrees = 0;
+static uint64_t g_leaf_launches = 0, g_leaf_subtrees = 0, g_leaf_records = 0;
 static double g_leaf_ms = 0.0;
 
 static int perft_split_leaves(hipStream_t st, SoA leaf, uint64_t* leaf_out) {
     const int64_t cap = (int64_t)1 << 27;  // children per chunk (7.5 GiB of boards)
     int chunk = 1 << 21;
     std::vector<hipEvent_t> evs;  // pairs around the leaf launches
-    uint64_t subtrees = 0;
+    uint64_t subtrees = 0, records = 0;  // subtrees counted by the leaf kernel, of records made
     // GC_PERFT_GATHER (A/B): the round-2/3 form -- records in expansion order, a radix sort by
     // move count, the leaf kernel gathering through the permutation
     static const bool gather = getenv("GC_PERFT_GATHER") != nullptr;
+    // GC_PERFT_DEDUP=0 (per call; A/B and tests): every record counted, transpositions too
+    const char* dd = getenv("GC_PERFT_DEDUP");
+    const bool dedup = !gather && !(dd && dd[0] == '0');
     int32_t *kc = nullptr, *offs = nullptr, *kc2 = nullptr, *ks = nullptr, *ix = nullptr, *is = nullptr;
     uint8_t* bins = nullptr;
     u32 *hist = nullptr, *hbase = nullptr;
     const int max_blk = (chunk + BLOCK - 1) / BLOCK;
     Node64* cr = nullptr;
+    // the transposition pass (k_dedup): table of 2x the chunk's records, leader indices,
+    // follower (parent, leader) pairs, the leaders' counts, the two list sizes
+    u64* table = nullptr;
+    int32_t* lidx = nullptr;
+    uint2* fol = nullptr;
+    uint64_t* val = nullptr;
+    u32* nsel = nullptr;  // [0] leaders, [1] followers
     void* tmp = nullptr;
     size_t tmp_bytes = 0;
     int rc = 0;
     std::string err;
     auto done = [&]() {
-        void* ps[] = {kc, offs, kc2, ks, ix, is, cr, tmp, bins, hist, hbase};
+        void* ps[] = {kc, offs, kc2, ks, ix, is, cr, tmp, bins, hist, hbase, table, lidx, fol, val, nsel};
         for (void* q : ps) (void)hipFree(q);
         for (hipEvent_t ev : evs) (void)hipEventDestroy(ev);
     };
     if (dalloc(&kc, leaf.n) || dalloc(&offs, chunk) || dalloc(&cr, cap) ||
         (gather ? (dalloc(&kc2, cap) || dalloc(&ks, cap) || dalloc(&ix, cap) || dalloc(&is, cap))
                 : (dalloc(&bins, cap) || dalloc(&hist, (size_t)SPLIT_BINS * max_blk) ||
-                   dalloc(&hbase, (size_t)SPLIT_BINS * max_blk)))) {
+                   dalloc(&hbase, (size_t)SPLIT_BINS * max_blk))) ||
+        (dedup && (dalloc(&table, 2 * cap) || dalloc(&lidx, cap) || dalloc(&fol, cap) || dalloc(&val, cap) ||
+                   dalloc(&nsel, 2)))) {
         done();
         return -1;
     }
     {  // scratch for the largest scan and sort of a chunk
-        size_t b1 = 0, b2 = 0;
+        size_t b1 = 0, b2 = 0, b3 = 0;
         hipError_t he = hipcub::DeviceScan::ExclusiveSum(nullptr, b1, kc, offs, chunk, st);
         if (he == hipSuccess && gather)
             he = hipcub::DeviceRadixSort::SortPairs(nullptr, b2, kc2, ks, ix, is, (int)cap, 0, 10, st);
         if (he == hipSuccess && !gather)
             he = hipcub::DeviceScan::ExclusiveSum(nullptr, b2, hist, hbase, SPLIT_BINS * max_blk, st);
+        if (he == hipSuccess && dedup)
+            he = hipcub::DeviceSelect::Flagged(nullptr, b3, hipcub::CountingInputIterator<int32_t>(0), bins, lidx,
+                                               nsel, (int64_t)cap, st);
         tmp_bytes = b1 > b2 ? b1 : b2;
+        tmp_bytes = tmp_bytes > b3 ? tmp_bytes : b3;
         if (he != hipSuccess) { done(); return fail(std::string("perft split: ") + hipGetErrorString(he)); }
         if (dalloc((char**)&tmp, tmp_bytes)) { done(); return -1; }
     }
@@ -3593,14 +3693,36 @@ static int perft_split_leaves(hipStream_t st, SoA leaf, uint64_t* leaf_out) {
             he = hipcub::DeviceScan::ExclusiveSum(tmp, tb, hist, hbase, SPLIT_BINS * nb, st);
             if (he != hipSuccess) { err = std::string("perft split scan: ") + hipGetErrorString(he); rc = -1; break; }
             k_expand_place<<<nb, BLOCK, 0, st>>>(leaf, a, c, bins, offs, hbase, nb, cr);
+            unsigned long long* psum = reinterpret_cast<unsigned long long*>(leaf_out + a);
+            int lead_n = 0;
+            u32 tsize = 2;
+            while ((int64_t)tsize < 2 * total) tsize <<= 1;
+            if (dedup) {  // bins (the records' move counts, placed) are free again: the leader flags
+                he = hipMemsetAsync(table, 0, (size_t)8 * tsize, st);
+                if (he == hipSuccess) he = hipMemsetAsync(nsel, 0, 8, st);
+                if (he == hipSuccess)
+                    k_dedup<<<grid_for((int)total), BLOCK, 0, st>>>(cr, (int)total, table, tsize - 1, bins, nsel + 1,
+                                                                    fol);
+                tb = tmp_bytes;
+                if (he == hipSuccess)
+                    he = hipcub::DeviceSelect::Flagged(tmp, tb, hipcub::CountingInputIterator<int32_t>(0), bins, lidx,
+                                                       nsel, (int64_t)total, st);
+                u32 nl = 0;  // the leaf grid sized to the leaders (one round trip per chunk)
+                if (he == hipSuccess) he = hipMemcpyAsync(&nl, nsel, 4, hipMemcpyDeviceToHost, st);
+                if (he == hipSuccess) he = hipStreamSynchronize(st);
+                if (he != hipSuccess) { err = std::string("perft split dedup: ") + hipGetErrorString(he); rc = -1; break; }
+                lead_n = (int)nl;
+            }
             hipEvent_t e0 = nullptr, e1 = nullptr;
             if (hipEventCreate(&e0) == hipSuccess) evs.push_back(e0);
             if (hipEventCreate(&e1) == hipSuccess) evs.push_back(e1);
             if (e0 && e1) (void)hipEventRecord(e0, st);
-            k_perft2_rec<<<grid_for((int)total), BLOCK, 0, st>>>(cr, (int)total,
-                                                                  reinterpret_cast<unsigned long long*>(leaf_out + a));
+            if (dedup) k_perft2_lead<<<grid_for(lead_n), BLOCK, 0, st>>>(cr, lidx, lead_n, val, psum);
+            else k_perft2_rec<<<grid_for((int)total), BLOCK, 0, st>>>(cr, (int)total, psum);
             if (e0 && e1) (void)hipEventRecord(e1, st);
-            subtrees += (uint64_t)total;
+            if (dedup) k_followers<<<2048, BLOCK, 0, st>>>(fol, nsel + 1, val, psum);
+            records += (uint64_t)total;
+            subtrees += (uint64_t)(dedup ? lead_n : total);
         } else if (total > 0) {
             k_expand_range_rec<<<grid_for(c), BLOCK, 0, st>>>(leaf, a, c, offs, cr);
             k_count_children_rec<<<grid_for((int)total), BLOCK, 0, st>>>(cr, (int)total, kc2);
@@ -3616,6 +3738,7 @@ static int perft_split_leaves(hipStream_t st, SoA leaf, uint64_t* leaf_out) {
                 cr, (int)total, is, reinterpret_cast<unsigned long long*>(leaf_out + a));
             if (e0 && e1) (void)hipEventRecord(e1, st);
             subtrees += (uint64_t)total;
+            records += (uint64_t)total;
         }
         he = hipGetLastError();
         if (he != hipSuccess) { err = std::string("perft split kernels: ") + hipGetErrorString(he); rc = -1; break; }
@@ -3632,6 +3755,7 @@ static int perft_split_leaves(hipStream_t st, SoA leaf, uint64_t* leaf_out) {
         std::lock_guard<std::mutex> lk(g_leaf_mu);
         g_leaf_launches += evs.size() / 2;
         g_leaf_subtrees += subtrees;
+        g_leaf_records += records;
         g_leaf_ms += ms;
     }
     done();
@@ -3777,6 +3901,14 @@ extern "C" int gc_perft_leaf_stats(uint64_t* launches, uint64_t* subtrees, doubl
     *launches = g_leaf_launches;
     *subtrees = g_leaf_subtrees;
     *kernel_ms = g_leaf_ms;
+    return 0;
+}
+
+extern "C" int gc_perft_dedup_stats(uint64_t* records, uint64_t* counted) {
+    if (!records || !counted) return fail("null argument");
+    std::lock_guard<std::mutex> lk(g_leaf_mu);
+    *records = g_leaf_records;
+    *counted = g_leaf_subtrees;
     return 0;
 }
 

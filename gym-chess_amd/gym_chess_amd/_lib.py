@@ -61,6 +61,7 @@ SIGNATURES = {
     "gc_engine_perft": (_I, [_P, _I, _P, _P, _I, _P]),
     "gc_perft_path_counts": (_I, [_P]),
     "gc_perft_leaf_stats": (_I, [_P, _P, _P]),
+    "gc_perft_dedup_stats": (_I, [_P, _P]),
     "gc_engine_set_rules": (_I, [_P, _I]),
     "gc_env_create": (_I, [_I, _I, _U64, _P, _P]),
     "gc_env_destroy": (_I, [_P]),

@@ -174,3 +174,11 @@ def perft_leaf_stats():
     la, st, ms = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_double()
     _lib.check(_lib.load().gc_perft_leaf_stats(ctypes.byref(la), ctypes.byref(st), ctypes.byref(ms)))
     return int(la.value), int(st.value), float(ms.value)
+
+
+def perft_dedup_stats():
+    """Diagnostics: the split pass's depth-2 roots in this process -> (records made, subtrees
+    counted); counted < records when the transposition pass merged equal positions."""
+    r, c = ctypes.c_uint64(), ctypes.c_uint64()
+    _lib.check(_lib.load().gc_perft_dedup_stats(ctypes.byref(r), ctypes.byref(c)))
+    return int(r.value), int(c.value)

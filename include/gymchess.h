@@ -70,9 +70,13 @@ int gc_engine_perft(gc_engine* e, int n, const int8_t* boards, const uint8_t* me
  * (depth-3 subtrees split to depth-2, sorted), sorted (subtrees by move count), small
  * (unsorted nested loops), fide} */
 int gc_perft_path_counts(uint64_t* out4);
-/* diagnostics: the split pass's leaf kernel (k_perft2_perm, one lane = one depth-2 subtree)
- * in this process -- launches, subtrees and summed kernel time (HIP events on its stream) */
+/* diagnostics: the split pass's leaf kernel (k_perft2_rec / k_perft2_lead, one lane = one
+ * depth-2 subtree) in this process -- launches, subtrees counted and summed kernel time (HIP
+ * events on its stream) */
 int gc_perft_leaf_stats(uint64_t* launches, uint64_t* subtrees, double* kernel_ms);
+/* diagnostics: the split pass's depth-2 roots made (records) and counted (one per distinct
+ * position of a chunk when the transposition pass runs, GC_PERFT_DEDUP != 0) in this process */
+int gc_perft_dedup_stats(uint64_t* records, uint64_t* counted);
 /* Rules of every later call on this engine (not in the reference):
  * 0 = the reference's (default, lib.rs), 1 = FIDE (gym-chess_amd/csrc/gc_fide.h: en passant,
  * promotion, per-side castling through unattacked squares, no king captures).  Under FIDE

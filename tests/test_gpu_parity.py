@@ -186,6 +186,29 @@ def test_perft_split_leaves_matches_depth3_subtrees(engine):
     assert (split == whole).all() and split.sum() > 200 * 10**6, np.nonzero(split != whole)[0][:4]
 
 
+def test_perft_split_transpositions_merged_exactly(engine):
+    """The split pass's transposition pass (k_dedup: one leaf count per distinct depth-2 root
+    of a chunk, the other records adding the leader's count to their own parents) == every
+    record counted (GC_PERFT_DEDUP=0), per root; the merge happened (counted < records)."""
+    import os
+
+    from gym_chess_amd.engine import perft_dedup_stats
+
+    b, m = _midgame_roots(200, 21, 0x5EED + 5)
+    r0, c0 = perft_dedup_stats()
+    merged = engine.perft(b, m, 5)
+    r1, c1 = perft_dedup_stats()
+    os.environ["GC_PERFT_DEDUP"] = "0"
+    try:
+        every = engine.perft(b, m, 5)
+    finally:
+        del os.environ["GC_PERFT_DEDUP"]
+    r2, c2 = perft_dedup_stats()
+    assert (merged == every).all(), np.nonzero(merged != every)[0][:4]
+    assert r1 - r0 == r2 - r1 == c2 - c1 > 0
+    assert c1 - c0 < 0.8 * (r1 - r0), (r1 - r0, c1 - c0)
+
+
 def _midgame_roots(n, plies, seed):
     from gym_chess_amd.env import BatchedChessEnv
 
