@@ -160,8 +160,9 @@ def check(rc):
 
 
 def ptr(a):
-    """numpy array -> void* (the array must stay alive for the call)."""
-    return a.ctypes.data_as(ctypes.c_void_p)
+    """numpy array -> its data address for a void* argument (the array must stay alive for the
+    call; an int converts at the call, ~5x cheaper than ctypes.data_as)."""
+    return a.ctypes.data
 
 
 def device_count():

@@ -60,15 +60,28 @@ INVALID_ACTION_REWARD = -10
 _COLS = "abcdefgh"
 
 
-def action_to_str(a):
-    """action -> reference engine move string (lib.rs:1278-1290 / castle names)."""
-    a = int(a)
+def _action_str(a):
     if a >= 4096:
         return ACTION_TO_CASTLE[a] if a in ACTION_TO_CASTLE else RESIGN
     f, t = divmod(a, 64)
     fr, fc = divmod(f, 8)
     tr, tc = divmod(t, 8)
     return f"{_COLS[fc]}{8 - fr}{_COLS[tc]}{8 - tr}"
+
+
+_ACTION_STRS = [_action_str(a) for a in range(N_ACTIONS)]  # one lookup per move of a list
+
+
+def action_to_str(a):
+    """action -> reference engine move string (lib.rs:1278-1290 / castle names)."""
+    a = int(a)
+    return _ACTION_STRS[a] if 0 <= a < N_ACTIONS else _action_str(a)
+
+
+def actions_to_strs(actions):
+    """a move list (uint16 array of engine actions) -> reference move strings"""
+    t = _ACTION_STRS
+    return [t[a] if a < N_ACTIONS else _action_str(a) for a in actions.tolist()]
 
 
 def str_to_action(s):
@@ -109,9 +122,30 @@ def rust_move_to_coords(s):
     return action_to_move(str_to_action(s))
 
 
+def _board_list(board):
+    """the common case -- a list of 8 lists of 8 Python ints (the reference's state dicts) --
+    without numpy's per-element inference; None when board is anything else"""
+    if type(board) is not list or len(board) != 8:
+        return None
+    flat = []
+    for r in board:
+        if type(r) is not list or len(r) != 8:
+            return None
+        flat.extend(r)
+    for x in flat:
+        if type(x) is not int:
+            return None
+    if min(flat) < -6 or max(flat) > 6:
+        raise ValueError("piece id out of range [-6, 6]")
+    return np.array(flat, dtype=np.int8)
+
+
 def board_to_array(board):
     """list-of-lists / ndarray (8x8, or flat 64) -> int8[64]; raises TypeError like
     convert_py_state."""
+    fast = _board_list(board)
+    if fast is not None:
+        return fast
     a = np.asarray(board)
     if a.shape == (64,):
         a = a.reshape(8, 8)
@@ -150,14 +184,13 @@ def dict_to_arrays(state):
         if k not in state:
             raise KeyError(k)
     b = board_to_array(state["board"])
-    meta = np.zeros(8, dtype=np.uint8)
-    meta[0] = player_to_white(state["current_player"])
-    for i, k in enumerate(_STATE_KEYS[2:]):
+    m = [1 if player_to_white(state["current_player"]) else 0]
+    for k in _STATE_KEYS[2:]:
         v = state[k]
         if not isinstance(v, (bool, np.bool_)):
             raise TypeError(f"{k} must be a bool")
-        meta[1 + i] = bool(v)
-    return b, meta
+        m.append(1 if v else 0)
+    return b, np.array(m + [0, 0, 0], dtype=np.uint8)
 
 
 def arrays_to_dict(board, meta):

@@ -128,6 +128,13 @@ class ChessEngine:
 
     def __init__(self, device=0):
         self._e = Engine(device)
+        # one position per call: the outputs' buffers made once (their pointers too); the
+        # result is converted to Python objects before the call returns
+        self._moves = np.zeros(MAX_LIST, dtype=np.uint16)
+        self._cnt = np.zeros(1, dtype=np.int32)
+        self._white = (np.ones(1, dtype=np.uint8), np.zeros(1, dtype=np.uint8))
+        self._p_moves, self._p_cnt = _lib.ptr(self._moves), _lib.ptr(self._cnt)
+        self._p_white = (_lib.ptr(self._white[0]), _lib.ptr(self._white[1]))
 
     def next_state(self, state, player, move):
         b, m = C.dict_to_arrays(state)
@@ -145,16 +152,19 @@ class ChessEngine:
     def get_possible_moves(self, state, player, attack=False):
         b, m = C.dict_to_arrays(state)
         white = self._player(player)
-        out, cnt = self._e.possible_moves(b, m, white, attack)
-        n = int(cnt[0])
-        if n > out.shape[1]:
-            out, cnt = self._e.possible_moves(b, m, white, attack, cap=n)
-        return [C.action_to_str(x) for x in out[0, :n]]
+        e = self._e
+        _lib.check(e._L.gc_engine_get_possible_moves(e._h, 1, _lib.ptr(b), _lib.ptr(m), self._p_white[0 if white else 1],
+                                                     1 if attack else 0, self._p_moves, MAX_LIST, self._p_cnt))
+        n = int(self._cnt[0])
+        if n > MAX_LIST:
+            out, cnt = e.possible_moves(b, m, white, attack, cap=n)
+            return C.actions_to_strs(out[0, :n])
+        return C.actions_to_strs(self._moves[:n])
 
     def get_castle_moves(self, state, player):
         b, m = C.dict_to_arrays(state)
         out, cnt = self._e.castle_moves(b, m, self._player(player))
-        return [C.action_to_str(x) for x in out[0, : int(cnt[0])]]
+        return C.actions_to_strs(out[0, : int(cnt[0])])
 
     def update_state(self, state):
         b, m = C.dict_to_arrays(state)

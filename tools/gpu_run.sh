@@ -43,6 +43,8 @@ for s in ${STEPS:-smoke pytest bench prof}; do
     pmcrm)  step pmcrm 300 rocprofv3 --pmc $MIXC -d $OUT/pmc_roll_mix -o run --output-format csv -- $PMCR ;;
     perftab) step perft_dedup 300 $PERFTB --perft-roots 65536 &&  # the perft leg, transpositions merged / not
             GC_PERFT_DEDUP=0 step perft_every 300 $PERFTB --perft-roots 65536 ;;
+    profp)  step profp 300 rocprofv3 --kernel-trace --stats -d $OUT/profp -o run --output-format csv -- $PERFTB &&
+            cp $OUT/profp/run_kernel_stats.csv $OUT/perft_kernel_stats.csv ;;  # the perft leg's kernels
     fcp)    step fcp 300 python tools/fixed_cost_probe.py ;;  # the timed region's fixed cost, by K and wait
     anat)   step anat 120 tools/_region_anatomy ;;  # one launch's round trip by parts (build it first)
     calib)  step calib 120 rocprofv3 --pmc $MIXC -d $OUT/pmc_calib -o run --output-format csv -- tools/_valu_calib ;;

@@ -139,14 +139,27 @@ def load_calib(dst):
     return None
 
 
-def valu_issue(rows_sum, calib):
-    """VALU issue fraction of summed dispatch counters, by the calibrated class costs."""
+def valu_issue(rows_sum, calib, mix=None):
+    """VALU issue fraction of summed dispatch counters, by the calibrated class costs.  With a
+    static class mix of the kernel's ISA (tools/isa_mix.py) the fraction at that mix replaces
+    the bracket's upper end (every non-INT64 instruction at the slow class)."""
     v, i64 = rows_sum["SQ_INSTS_VALU"], rows_sum.get("SQ_INSTS_VALU_INT64", 0.0)
     cyc = rows_sum["GRBM_GUI_ACTIVE"] / XCDS * SIMDS
     issued = i64 * calib["c64"] + (v - i64) * calib["c32"]
-    issued_hi = i64 * calib["c64"] + (v - i64) * calib["c32_slow"]
-    return {"issue_frac": issued / cyc, "issue_frac_upper": issued_hi / cyc, "int64_share": i64 / v,
-            "clock_ghz_note": "GRBM_GUI_ACTIVE / XCDs = cycles of the dispatch"}
+    out = {"issue_frac": issued / cyc, "int64_share": i64 / v,
+           "clock_ghz_note": "GRBM_GUI_ACTIVE / XCDs = cycles of the dispatch"}
+    if mix:
+        sl = mix["slow_share"]
+        out["issue_frac_mix"] = v * (sl * calib["c32_slow"] + (1 - sl) * calib["c32"]) / cyc
+        out["mix_source"] = {"slow_share": sl, "valu_static": mix["valu_static"], "tool": "tools/isa_mix.py"}
+    else:
+        out["issue_frac_upper"] = (i64 * calib["c64"] + (v - i64) * calib["c32_slow"]) / cyc
+    return out
+
+
+def load_mix(kern):
+    p = os.path.join(os.path.dirname(CALIB), f"isa_mix_{kern}.json")
+    return json.load(open(p)) if os.path.exists(p) else None
 
 
 def rollout_summary(a):
@@ -197,8 +210,8 @@ def perft_summary(a):
     VALU instructions per wave, lane utilisation, VALU busy fraction.  Algorithmic bytes per
     subtree: the root's 64-byte record (7 bitboards + meta, read in order) + its count (8) added
     into the parent's sum = 72 B, + the 4-B leader index and the 8-B count kept for the merged
-    records = 84 B; the leaves never touch memory.  (--perft-kernel k_perft2_rec: every record
-    counted, 72 B; k_perft2_perm_rec: the earlier gathering form, + a 4-B permutation index.)"""
+    records = 84 B; the leaves never touch memory.  (--perft-kernel k_perft2_rec: every record counted, 72 B;
+    k_perft2_perm_rec: the earlier gathering form, + a 4-B permutation index.)"""
     kern = a.perft_kernel
     rows = lambda sub: per_dispatch(os.path.join(a.src, sub, "run_counter_collection.csv"), kern)  # noqa: E731
     f, w, m = rows("pmc_perft_fetch"), rows("pmc_perft_write"), rows("pmc_perft_mix")
@@ -215,7 +228,7 @@ def perft_summary(a):
     out["hbm_bytes_per_subtree"] = out["hbm_bytes_total"] / max(out["subtrees_total"], 1)
     cal = load_calib(a.dst)
     if cal:
-        out["valu"].update(valu_issue({k: tot(m, k) for k in m[0]}, cal))
+        out["valu"].update(valu_issue({k: tot(m, k) for k in m[0]}, cal, load_mix(kern)))
     os.makedirs(a.dst, exist_ok=True)
     for p in (os.path.join(a.dst, "pmc_perft.json"),):
         json.dump(out, open(p, "w"), indent=1)
