@@ -276,14 +276,17 @@ __device__ __forceinline__ void list_one(const Pos& s, int attack, int cap, uint
 // list_one with the wave's 64 lanes (every lane holds the same s): lane = square, each own
 // piece's legal targets in reference order at its exclusive prefix-sum offset (the list is
 // row-major over the squares, lib.rs:501-563), the castles after them
-__device__ __forceinline__ void list_par(const Pos& s, int cap, uint16_t* out, int32_t* count, const Gen* g0 = nullptr) {
+// (attack: the attack-mode list, lib.rs:460-486 with attack = true -- no legality filter, no
+// castles)
+__device__ __forceinline__ void list_par(const Pos& s, int cap, uint16_t* out, int32_t* count, const Gen* g0 = nullptr,
+                                         bool attack = false) {
     Gen g;
     if (g0) g = *g0;  // (gen_init of s, made by the caller)
     else gen_init(s, g);
     const int sq = (int)(threadIdx.x & 63);
     const bool mine = (g.own >> sq) & 1;
     const int t = mine ? type_at(s, sq) : 0;
-    const u64 tg = mine ? legal_targets(s, g, sq, t) : 0ull;
+    const u64 tg = mine ? (attack ? attack_targets(s, g, sq, t) : legal_targets(s, g, sq, t)) : 0ull;
     const int c = popc(tg);
     int off = c;  // inclusive prefix sum over the lanes
 #pragma unroll
@@ -297,8 +300,8 @@ __device__ __forceinline__ void list_par(const Pos& s, int cap, uint16_t* out, i
     for_targets_ordered(tg, sq, t, g.white, [&](int to) { if (w < cap) out[w] = (uint16_t)(sq * 64 + to); w++; });
     int m = n;
     if (sq == 0) {
-        if (g.castles & 1) { if (m < cap) out[m] = g.white ? A_QSW : A_QSB; m++; }
-        if (g.castles & 2) { if (m < cap) out[m] = g.white ? A_KSW : A_KSB; m++; }
+        if (!attack && (g.castles & 1)) { if (m < cap) out[m] = g.white ? A_QSW : A_QSB; m++; }
+        if (!attack && (g.castles & 2)) { if (m < cap) out[m] = g.white ? A_KSW : A_KSB; m++; }
         *count = m;
     }
 }
@@ -338,6 +341,19 @@ __global__ void k_mask(SoA in, u64* __restrict__ mask, int32_t* __restrict__ cou
     if (g.castles & 2) c |= g.white ? (1ull << 0) : (1ull << 2);
     o[64] = c;
     if (counts) counts[i] = n + popc(c);
+}
+
+// the castle bits alone (k_mask's word 64): what get_castle_moves returns
+__global__ void k_castle_word(SoA in, int32_t* __restrict__ out) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= in.n) return;
+    Pos s = in.load(i);
+    Gen g;
+    gen_init(s, g);
+    int c = 0;
+    if (g.castles & 1) c |= g.white ? (1 << 1) : (1 << 3);
+    if (g.castles & 2) c |= g.white ? (1 << 0) : (1 << 2);
+    out[i] = c;
 }
 
 // next_state (lib.rs:1422-1452): move + update_state; status 0 ok, 1 both kings checked,
@@ -641,12 +657,9 @@ __global__ void __launch_bounds__(BLOCK) k_dedup(const Node64* __restrict__ in, 
         const u64 tag = (h >> 32) | 1u;
         const u64 mine = (tag << 32) | (u32)i;
         u32 slot = (u32)h & mask;
-        for (;;) {
-            u64 e = __hip_atomic_load(table + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (e == 0) {
-                e = atomicCAS(reinterpret_cast<unsigned long long*>(table + slot), 0ull, (unsigned long long)mine);
-                if (e == 0) break;  // this record leads its position
-            }
+        for (;;) {  // (a relaxed load ahead of the CAS: 11.4 ms per chunk; the CAS alone: see DESIGN §5)
+            const u64 e = atomicCAS(reinterpret_cast<unsigned long long*>(table + slot), 0ull, (unsigned long long)mine);
+            if (e == 0) break;  // this record leads its position
             if ((e >> 32) == tag && pos_equal(node_load(in, (u32)e), s)) {
                 follower = true;
                 lead = (u32)e;
@@ -2740,6 +2753,109 @@ __global__ void __launch_bounds__(64) k_single_server(EnvDev e, int i, SrvBox* b
     if (threadIdx.x == 0) srv_store(&box->exited, launch_id);
 }
 
+// ----------------------------------------------------------------------------- engine server
+// The drop-in ChessEngine's one-position calls (n = 1, reference rules) without a launch each:
+// the single-board server's scheme (one resident wave, a host-mapped mailbox, s_sleep polling,
+// idle exit) over stateless ops -- the request carries the state dict's board and flags, the
+// response the list / castle word / next state.  Same device functions as the batched kernels
+// (list_par = list_one with the lanes, next_state_one, check_flags).
+enum { ENG_LIST = 1, ENG_CASTLE = 2, ENG_NEXT = 3, ENG_UPDATE = 4 };
+#define ENG_SRV_CAP 320
+struct EngBox {
+    u32 req_seq, op, white, arg;  // arg: attack (LIST) or the action (NEXT); the host writes req_seq last
+    u32 pad0[12];
+    int8_t board[64];             // the request's state (mailbox + the import's meta bytes)
+    uint8_t meta[8];
+    u32 pad1[14];
+    u32 resp_seq, count;          // count: the list's length, or the castle word
+    int32_t reward, status;
+    u32 pad2[12];
+    int8_t out_board[64];
+    uint8_t out_meta[8];
+    u32 pad3[14];
+    uint16_t moves[ENG_SRV_CAP];
+    u32 exited, pad4[15];
+};
+__global__ void __launch_bounds__(64) k_engine_server(EngBox* box, u32 done_seq, u32 launch_id) {
+    __shared__ __attribute__((aligned(16))) int8_t in[80];  // board 64 + meta 8 (+ pad)
+    __shared__ __attribute__((aligned(16))) int8_t ob[64];
+    __shared__ uint8_t om[8];
+    __shared__ uint16_t mv[ENG_SRV_CAP];
+    __shared__ int32_t cnt, rw, st;
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const int lane = (int)threadIdx.x;
+    unsigned long long idle0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        const u32x4 rq = *reinterpret_cast<const volatile u32x4*>(box);
+        const u32 req = __builtin_amdgcn_readfirstlane(rq.x);
+        if (req == done_seq) {
+            if (__builtin_amdgcn_s_memrealtime() - idle0 > (unsigned long long)SRV_IDLE_MS * 100000ull) break;
+            __builtin_amdgcn_s_sleep(8);
+            continue;
+        }
+        __atomic_thread_fence(__ATOMIC_ACQUIRE);  // the state after req_seq
+        const int op = (int)__builtin_amdgcn_readfirstlane(rq.y);
+        if (op == SRV_QUIT) break;
+        const bool white = __builtin_amdgcn_readfirstlane(rq.z) != 0;
+        const int arg = (int)__builtin_amdgcn_readfirstlane(rq.w);
+        if (lane < 5)  // the 72 request bytes in five 16-byte reads
+            reinterpret_cast<u32x4*>(in)[lane] = reinterpret_cast<const volatile u32x4*>(box->board)[lane];
+        __syncthreads();
+        const uint8_t side = white ? 1 : 0;
+        // LIST / CASTLE: the player argument is the side to generate for (lib.rs:1454-1499);
+        // NEXT / UPDATE keep the state's own current_player
+        const Pos s = import_one(in, reinterpret_cast<const uint8_t*>(in + 64),
+                                 (op == ENG_LIST || op == ENG_CASTLE) ? &side : nullptr, 0);
+        int nout = 0;  // result u32 words to copy
+        if (op == ENG_LIST) {
+            list_par(s, ENG_SRV_CAP, mv, &cnt, nullptr, arg != 0);
+            __syncthreads();
+            nout = (cnt < ENG_SRV_CAP ? cnt : ENG_SRV_CAP) + 1;
+            nout /= 2;
+        } else if (op == ENG_CASTLE) {
+            if (lane == 0) {
+                Gen g;
+                gen_init(s, g);
+                int c = 0;
+                if (g.castles & 1) c |= g.white ? (1 << 1) : (1 << 3);
+                if (g.castles & 2) c |= g.white ? (1 << 0) : (1 << 2);
+                cnt = c;
+            }
+        } else if (lane == 0) {  // NEXT / UPDATE
+            Pos t = s;
+            if (op == ENG_NEXT) {
+                const uint16_t a = (uint16_t)arg;
+                t = next_state_one(s, &side, &a, &rw, &st, 0);
+            } else {
+                t.meta = (t.meta & ~(u32)(M_WCHK | M_BCHK)) | check_flags(t);
+                rw = 0;
+                st = 0;
+            }
+            export_one(t, ob, om, 0);
+        }
+        __syncthreads();
+        // the response: results, a system-scope fence, then resp_seq
+        if (op == ENG_LIST) {
+            for (int k = lane; k < nout; k += 64) reinterpret_cast<u32*>(box->moves)[k] = reinterpret_cast<const u32*>(mv)[k];
+        } else if (op == ENG_NEXT || op == ENG_UPDATE) {
+            if (lane < 16) reinterpret_cast<u32*>(box->out_board)[lane] = reinterpret_cast<const u32*>(ob)[lane];
+            else if (lane < 18) reinterpret_cast<u32*>(box->out_meta)[lane - 16] = reinterpret_cast<const u32*>(om)[lane - 16];
+            if (lane == 0) {
+                box->reward = rw;
+                box->status = st;
+            }
+        }
+        if (lane == 0) box->count = (u32)cnt;
+        __threadfence_system();
+        __syncthreads();
+        if (lane == 0) srv_store(&box->resp_seq, req);
+        done_seq = req;
+        idle0 = __builtin_amdgcn_s_memrealtime();
+    }
+    __threadfence_system();
+    if (lane == 0) srv_store(&box->exited, launch_id);
+}
+
 // the live 3-fold window of board i (its table entries, then its spill entries): boards and
 // occurrence counts (diagnostic readout; ChessEnv.saved_boards)
 __global__ void k_window_boards(EnvDev e, int i, int8_t* __restrict__ boards, uint8_t* __restrict__ counts, int cap,
@@ -3366,7 +3482,16 @@ struct gc_engine {
     uint16_t* acts = nullptr; int32_t* i32a = nullptr; int32_t* i32b = nullptr;
     uint16_t* list = nullptr; uint64_t* u64o = nullptr;
     int rules = 0;  // 0 reference (lib.rs), 1 FIDE (gc_fide.h)
+    // small calls (a layout within ENGINE_ZC_BYTES) stage in host-mapped coherent memory that
+    // the kernels read and write directly: one launch and no copy per call, where the
+    // staged form paid a copy each way (two more dispatches) around it
+    uint8_t* zc = nullptr; uint8_t* zcd = nullptr; bool zc_on = false;
+    // one-position calls under the reference rules go to the engine server (k_engine_server)
+    struct EngBox* srv = nullptr; struct EngBox* srv_d = nullptr;
+    hipStream_t srv_stream = nullptr;
+    uint32_t srv_seq = 0, srv_launch = 0, srv_next_launch = 0;
 };
+#define ENGINE_ZC_BYTES 65536
 // byte offsets of the views for n boards and a list capacity lc (256-B aligned)
 struct EngineLayout {
     size_t mbox, m8, side, acts, i32a, i32b, list, end;
@@ -3384,22 +3509,28 @@ static EngineLayout engine_offsets(size_t n, size_t lc) {
     o.end = up(o.list + 2 * lc * n);
     return o;
 }
-static EngineLayout engine_layout(gc_engine* e, int n, int lc) {
+static EngineLayout engine_layout(gc_engine* e, int n, int lc, uint8_t* base) {
     EngineLayout o = engine_offsets((size_t)n, (size_t)lc);
-    e->mbox = reinterpret_cast<int8_t*>(e->dio + o.mbox);
-    e->m8 = e->dio + o.m8;
-    e->side = e->dio + o.side;
-    e->acts = reinterpret_cast<uint16_t*>(e->dio + o.acts);
-    e->i32a = reinterpret_cast<int32_t*>(e->dio + o.i32a);
-    e->i32b = reinterpret_cast<int32_t*>(e->dio + o.i32b);
-    e->list = reinterpret_cast<uint16_t*>(e->dio + o.list);
+    e->mbox = reinterpret_cast<int8_t*>(base + o.mbox);
+    e->m8 = base + o.m8;
+    e->side = base + o.side;
+    e->acts = reinterpret_cast<uint16_t*>(base + o.acts);
+    e->i32a = reinterpret_cast<int32_t*>(base + o.i32a);
+    e->i32b = reinterpret_cast<int32_t*>(base + o.i32b);
+    e->list = reinterpret_cast<uint16_t*>(base + o.list);
     return o;
+}
+static bool engine_zc_enabled() {
+    static const bool off = getenv("GC_ENGINE_ZC") && atoi(getenv("GC_ENGINE_ZC")) == 0;  // A/B
+    return !off;
 }
 
 static void engine_free_bufs(gc_engine* e) {
     void* ps[] = {e->bb, e->meta, e->bb2, e->meta2, e->dio, e->u64o};
     for (void* p : ps) if (p) (void)hipFree(p);
     if (e->hio) (void)hipHostFree(e->hio);
+    if (e->zc) (void)hipHostFree(e->zc);
+    e->zc = nullptr; e->zcd = nullptr; e->zc_on = false;
     e->bb = nullptr; e->meta = nullptr; e->bb2 = nullptr; e->meta2 = nullptr; e->dio = nullptr; e->hio = nullptr;
     e->mbox = nullptr; e->m8 = nullptr; e->side = nullptr; e->acts = nullptr; e->i32a = nullptr; e->i32b = nullptr;
     e->list = nullptr; e->u64o = nullptr;
@@ -3425,19 +3556,27 @@ static int engine_reserve(gc_engine* e, int n, int listcap) {
 // copy to the device; the views laid out for (n, lc)
 static int engine_stage(gc_engine* e, int n, int lc, const int8_t* boards, const uint8_t* meta, const uint8_t* side,
                         const uint16_t* acts, EngineLayout& o) {
-    o = engine_layout(e, n, lc);
-    std::memcpy(e->hio + o.mbox, boards, (size_t)64 * n);
-    std::memcpy(e->hio + o.m8, meta, (size_t)8 * n);
+    e->zc_on = engine_zc_enabled() && engine_offsets((size_t)n, (size_t)lc).end <= ENGINE_ZC_BYTES;
+    if (e->zc_on && !e->zc) {
+        HIPCHK(hipHostMalloc((void**)&e->zc, ENGINE_ZC_BYTES, hipHostMallocMapped | hipHostMallocCoherent));
+        HIPCHK(hipHostGetDevicePointer((void**)&e->zcd, e->zc, 0));
+    }
+    uint8_t* h = e->zc_on ? e->zc : e->hio;
+    o = engine_layout(e, n, lc, e->zc_on ? e->zcd : e->dio);
+    std::memcpy(h + o.mbox, boards, (size_t)64 * n);
+    std::memcpy(h + o.m8, meta, (size_t)8 * n);
     size_t end = o.m8 + (size_t)8 * n;
-    if (side) { std::memcpy(e->hio + o.side, side, (size_t)n); end = o.side + n; }
-    if (acts) { std::memcpy(e->hio + o.acts, acts, (size_t)2 * n); end = o.acts + (size_t)2 * n; }
-    HIPCHK(hipMemcpyAsync(e->dio, e->hio, end, hipMemcpyHostToDevice, e->stream));
+    if (side) { std::memcpy(h + o.side, side, (size_t)n); end = o.side + n; }
+    if (acts) { std::memcpy(h + o.acts, acts, (size_t)2 * n); end = o.acts + (size_t)2 * n; }
+    if (!e->zc_on) HIPCHK(hipMemcpyAsync(e->dio, e->hio, end, hipMemcpyHostToDevice, e->stream));
     return 0;
 }
-// the byte range [a, b) of the device block back into the pinned one, then wait
+// the byte range [a, b) of the device block back into the pinned one, then wait (a small
+// call's outputs are already in host memory: only the wait, and the range into hio)
 static int engine_fetch(gc_engine* e, size_t a, size_t b) {
-    HIPCHK(hipMemcpyAsync(e->hio + a, e->dio + a, b - a, hipMemcpyDeviceToHost, e->stream));
+    if (!e->zc_on) HIPCHK(hipMemcpyAsync(e->hio + a, e->dio + a, b - a, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
+    if (e->zc_on) std::memcpy(e->hio + a, e->zc + a, b - a);
     return 0;
 }
 
@@ -3490,9 +3629,68 @@ extern "C" int gc_engine_create(int device, gc_engine** out) {
     return 0;
 }
 
+// ---- the engine server's host side (the single-board server's protocol, srv_call)
+static bool eng_srv_enabled() {
+    static const bool off = getenv("GC_ENGINE_SERVER") && atoi(getenv("GC_ENGINE_SERVER")) == 0;  // A/B
+    return !off;
+}
+static int eng_srv_stop(gc_engine* e) {
+    if (!e->srv_launch) return 0;
+    EngBox* b = e->srv;
+    __atomic_store_n(&b->op, (u32)SRV_QUIT, __ATOMIC_RELAXED);
+    __atomic_store_n(&b->req_seq, e->srv_seq + 1, __ATOMIC_RELEASE);  // (never served: QUIT)
+    const hipError_t he = hipStreamSynchronize(e->srv_stream);
+    __atomic_store_n(&b->req_seq, e->srv_seq, __ATOMIC_RELEASE);
+    e->srv_launch = 0;
+    if (he != hipSuccess) return fail(std::string("engine server: ") + hipGetErrorString(he));
+    return 0;
+}
+// one op on one position; the response lands in e->srv
+static int eng_srv_call(gc_engine* e, int op, const int8_t* board, const uint8_t* meta, bool white, int arg) {
+    HIPCHK(hipSetDevice(e->device));
+    if (!e->srv) {
+        HIPCHK(hipHostMalloc((void**)&e->srv, sizeof(EngBox), hipHostMallocMapped | hipHostMallocCoherent));
+        memset(e->srv, 0, sizeof(EngBox));
+        HIPCHK(hipHostGetDevicePointer((void**)&e->srv_d, e->srv, 0));
+        HIPCHK(hipStreamCreateWithFlags(&e->srv_stream, hipStreamNonBlocking));
+    }
+    EngBox* b = e->srv;
+    const u32 seq = e->srv_seq + 1;
+    memcpy(b->board, board, 64);
+    memcpy(b->meta, meta, 8);
+    __atomic_store_n(&b->op, (u32)op, __ATOMIC_RELAXED);
+    __atomic_store_n(&b->white, white ? 1u : 0u, __ATOMIC_RELAXED);
+    __atomic_store_n(&b->arg, (u32)arg, __ATOMIC_RELAXED);
+    __atomic_store_n(&b->req_seq, seq, __ATOMIC_RELEASE);  // last
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned k = 0;; k++) {
+        if (!e->srv_launch || __atomic_load_n(&b->exited, __ATOMIC_ACQUIRE) == e->srv_launch) {
+            if (e->srv_launch) HIPCHK(hipStreamSynchronize(e->srv_stream));  // drained (idle exit)
+            e->srv_launch = ++e->srv_next_launch;
+            k_engine_server<<<1, 64, 0, e->srv_stream>>>(e->srv_d, e->srv_seq, e->srv_launch);
+            HIPCHK(hipGetLastError());
+        }
+        if (__atomic_load_n(&b->resp_seq, __ATOMIC_ACQUIRE) == seq) break;
+        if ((k & 1023) == 1023) {
+            const hipError_t q = hipStreamQuery(e->srv_stream);
+            if (q != hipSuccess && q != hipErrorNotReady) return fail(std::string("engine server: ") + hipGetErrorString(q));
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) {
+                (void)eng_srv_stop(e);
+                return fail("engine server: no answer within 10 s");
+            }
+        }
+    }
+    e->srv_seq = seq;
+    return 0;
+}
+static bool eng_srv_use(const gc_engine* e, int n) { return n == 1 && !e->rules && eng_srv_enabled(); }
+
 extern "C" int gc_engine_destroy(gc_engine* e) {
     if (!e) return 0;
     (void)hipSetDevice(e->device);
+    (void)eng_srv_stop(e);
+    if (e->srv_stream) (void)hipStreamDestroy(e->srv_stream);
+    if (e->srv) (void)hipHostFree(e->srv);
     (void)hipStreamSynchronize(e->stream);
     engine_free_bufs(e);
     (void)hipStreamDestroy(e->stream);
@@ -3505,6 +3703,15 @@ extern "C" int gc_engine_get_possible_moves(gc_engine* e, int n, const int8_t* b
                                             int32_t* counts) {
     if (!e || !moves || !counts || !player_white) return fail("null argument");
     if (cap <= 0) return fail("cap must be > 0");
+    if (eng_srv_use(e, n) && cap <= ENG_SRV_CAP) {
+        if (!boards || !meta) return fail("null boards/meta");
+        if (check_boards(1, boards)) return -1;
+        if (eng_srv_call(e, ENG_LIST, boards, meta, player_white[0] != 0, attack ? 1 : 0)) return -1;
+        const int c = (int)e->srv->count;
+        memcpy(moves, e->srv->moves, (size_t)2 * (c < cap ? c : cap));
+        counts[0] = c;
+        return 0;
+    }
     if (engine_reserve(e, n, cap)) return -1;
     EngineLayout o;
     if (e->rules) {
@@ -3528,21 +3735,39 @@ extern "C" int gc_engine_get_possible_moves(gc_engine* e, int n, const int8_t* b
 extern "C" int gc_engine_get_castle_moves(gc_engine* e, int n, const int8_t* boards, const uint8_t* meta,
                                           const uint8_t* player_white, uint16_t* moves, int32_t* counts) {
     if (!e || !moves || !counts || !player_white) return fail("null argument");
+    if (eng_srv_use(e, n)) {
+        if (!boards || !meta) return fail("null boards/meta");
+        if (check_boards(1, boards)) return -1;
+        if (eng_srv_call(e, ENG_CASTLE, boards, meta, player_white[0] != 0, 0)) return -1;
+        const u32 c = e->srv->count;
+        int k = 0;  // reference order (QS then KS, lib.rs:992,1011)
+        if (c & 2u) moves[k++] = A_QSW;
+        if (c & 1u) moves[k++] = A_KSW;
+        if (c & 8u) moves[k++] = A_QSB;
+        if (c & 4u) moves[k++] = A_KSB;
+        counts[0] = k;
+        return 0;
+    }
     if (engine_reserve(e, n, 2)) return -1;
     EngineLayout o;
     if (engine_upload(e, n, boards, meta, player_white, o, 2)) return -1;
-    std::vector<u64> mask((size_t)65 * n);
-    u64* dmask = nullptr;
-    if (dalloc(&dmask, (size_t)65 * n)) return -1;
-    if (e->rules) k_fmask<<<grid_for(n), BLOCK, 0, e->stream>>>(SoA{e->bb, e->meta, n}, dmask, nullptr);
-    else k_mask<<<grid_for(n), BLOCK, 0, e->stream>>>(SoA{e->bb, e->meta, n}, dmask, nullptr);
-    hipError_t le = hipGetLastError();
-    hipError_t ce = hipMemcpyAsync(mask.data(), dmask, (size_t)8 * 65 * n, hipMemcpyDeviceToHost, e->stream);
-    hipError_t se = hipStreamSynchronize(e->stream);
-    (void)hipFree(dmask);
-    if (le != hipSuccess || ce != hipSuccess || se != hipSuccess) return fail("castle mask kernel failed");
+    std::vector<u64> mask(e->rules ? (size_t)65 * n : 0);
+    if (e->rules) {
+        u64* dmask = nullptr;
+        if (dalloc(&dmask, (size_t)65 * n)) return -1;
+        k_fmask<<<grid_for(n), BLOCK, 0, e->stream>>>(SoA{e->bb, e->meta, n}, dmask, nullptr);
+        hipError_t le = hipGetLastError();
+        hipError_t ce = hipMemcpyAsync(mask.data(), dmask, (size_t)8 * 65 * n, hipMemcpyDeviceToHost, e->stream);
+        hipError_t se = hipStreamSynchronize(e->stream);
+        (void)hipFree(dmask);
+        if (le != hipSuccess || ce != hipSuccess || se != hipSuccess) return fail("castle mask kernel failed");
+    } else {  // the castle word per board into the layout's int32 row
+        k_castle_word<<<grid_for(n), BLOCK, 0, e->stream>>>(SoA{e->bb, e->meta, n}, e->i32a);
+        HIPCHK(hipGetLastError());
+        if (engine_fetch(e, o.i32a, o.i32a + (size_t)4 * n)) return -1;
+    }
     for (int i = 0; i < n; i++) {  // unpack in reference order (QS then KS, lib.rs:992,1011)
-        u64 c = mask[(size_t)65 * i + 64];
+        const u64 c = e->rules ? mask[(size_t)65 * i + 64] : (u64)reinterpret_cast<const int32_t*>(e->hio + o.i32a)[i];
         int k = 0;
         uint16_t* o = moves + 2 * (size_t)i;
         if (c & (1ull << 1)) o[k++] = A_QSW;
@@ -3560,6 +3785,16 @@ extern "C" int gc_engine_next_state(gc_engine* e, int n, const int8_t* boards, c
     if (!e || !player_white || !actions || !out_boards || !out_meta || !rewards || !status) return fail("null argument");
     for (int i = 0; i < n; i++)
         if (actions[i] > A_QSB) return fail("action out of range at index " + std::to_string(i));
+    if (eng_srv_use(e, n)) {
+        if (!boards || !meta) return fail("null boards/meta");
+        if (check_boards(1, boards)) return -1;
+        if (eng_srv_call(e, ENG_NEXT, boards, meta, player_white[0] != 0, actions[0])) return -1;
+        memcpy(out_boards, e->srv->out_board, 64);
+        memcpy(out_meta, e->srv->out_meta, 8);
+        rewards[0] = e->srv->reward;
+        status[0] = e->srv->status;
+        return 0;
+    }
     if (engine_reserve(e, n, 1)) return -1;
     // FIDE: the player argument is the side to move; reference: it only steers next_state's
     // promotion colour and rights logic (lib.rs:679-784), the state keeps current_player
@@ -3591,6 +3826,14 @@ extern "C" int gc_engine_next_state(gc_engine* e, int n, const int8_t* boards, c
 extern "C" int gc_engine_update_state(gc_engine* e, int n, const int8_t* boards, const uint8_t* meta,
                                       int8_t* out_boards, uint8_t* out_meta) {
     if (!e || !out_boards || !out_meta) return fail("null argument");
+    if (eng_srv_use(e, n)) {
+        if (!boards || !meta) return fail("null boards/meta");
+        if (check_boards(1, boards)) return -1;
+        if (eng_srv_call(e, ENG_UPDATE, boards, meta, false, 0)) return -1;
+        memcpy(out_boards, e->srv->out_board, 64);
+        memcpy(out_meta, e->srv->out_meta, 8);
+        return 0;
+    }
     if (engine_reserve(e, n, 1)) return -1;
     EngineLayout o;
     if (engine_upload(e, n, boards, meta, nullptr, o)) return -1;

@@ -195,16 +195,16 @@ def dict_to_arrays(state):
 
 def arrays_to_dict(board, meta):
     """State::to_py_object (lib.rs:355-395)."""
-    b = np.asarray(board, dtype=np.int64).reshape(8, 8)
+    m = np.asarray(meta).tolist()
     return {
-        "white_king_castle_is_possible": bool(meta[1]),
-        "white_queen_castle_is_possible": bool(meta[2]),
-        "black_king_castle_is_possible": bool(meta[3]),
-        "black_queen_castle_is_possible": bool(meta[4]),
-        "white_king_is_checked": bool(meta[5]),
-        "black_king_is_checked": bool(meta[6]),
-        "board": [[int(x) for x in row] for row in b],
-        "current_player": WHITE if meta[0] else BLACK,
+        "white_king_castle_is_possible": bool(m[1]),
+        "white_queen_castle_is_possible": bool(m[2]),
+        "black_king_castle_is_possible": bool(m[3]),
+        "black_queen_castle_is_possible": bool(m[4]),
+        "white_king_is_checked": bool(m[5]),
+        "black_king_is_checked": bool(m[6]),
+        "board": np.asarray(board).reshape(8, 8).tolist(),  # Python ints
+        "current_player": WHITE if m[0] else BLACK,
     }
 
 

@@ -135,19 +135,29 @@ class ChessEngine:
         self._white = (np.ones(1, dtype=np.uint8), np.zeros(1, dtype=np.uint8))
         self._p_moves, self._p_cnt = _lib.ptr(self._moves), _lib.ptr(self._cnt)
         self._p_white = (_lib.ptr(self._white[0]), _lib.ptr(self._white[1]))
+        self._act = np.zeros(1, dtype=np.uint16)
+        self._ob = np.zeros(64, dtype=np.int8)
+        self._om = np.zeros(8, dtype=np.uint8)
+        self._rw = np.zeros(1, dtype=np.int32)
+        self._st = np.zeros(1, dtype=np.int32)
+        self._p_act, self._p_ob, self._p_om = _lib.ptr(self._act), _lib.ptr(self._ob), _lib.ptr(self._om)
+        self._p_rw, self._p_st = _lib.ptr(self._rw), _lib.ptr(self._st)
 
     def next_state(self, state, player, move):
         b, m = C.dict_to_arrays(state)
         white = self._player(player)
-        a = C.str_to_action(move)
-        ob, om, rw, st = self._e.next_state(b, m, white, a)
-        if st[0] == -1:
+        self._act[0] = C.str_to_action(move)
+        e = self._e
+        _lib.check(e._L.gc_engine_next_state(e._h, 1, _lib.ptr(b), _lib.ptr(m), self._p_white[0 if white else 1],
+                                             self._p_act, self._p_ob, self._p_om, self._p_rw, self._p_st))
+        st = int(self._st[0])
+        if st == -1:
             raise RuntimeError("Bad move - piece is empty !")
-        if st[0] == 1:
+        if st == 1:
             raise SystemError("Both Kings are in check: this position is impossible")
-        if st[0] != 0:
+        if st != 0:
             raise ValueError(f"bad move {move!r}")
-        return C.arrays_to_dict(ob[0], om[0]), int(rw[0])
+        return C.arrays_to_dict(self._ob, self._om), int(self._rw[0])
 
     def get_possible_moves(self, state, player, attack=False):
         b, m = C.dict_to_arrays(state)
@@ -163,13 +173,17 @@ class ChessEngine:
 
     def get_castle_moves(self, state, player):
         b, m = C.dict_to_arrays(state)
-        out, cnt = self._e.castle_moves(b, m, self._player(player))
-        return C.actions_to_strs(out[0, : int(cnt[0])])
+        white = self._player(player)
+        e = self._e
+        _lib.check(e._L.gc_engine_get_castle_moves(e._h, 1, _lib.ptr(b), _lib.ptr(m), self._p_white[0 if white else 1],
+                                                   self._p_moves, self._p_cnt))
+        return C.actions_to_strs(self._moves[: int(self._cnt[0])])
 
     def update_state(self, state):
         b, m = C.dict_to_arrays(state)
-        ob, om = self._e.update_state(b, m)
-        return C.arrays_to_dict(ob[0], om[0])
+        e = self._e
+        _lib.check(e._L.gc_engine_update_state(e._h, 1, _lib.ptr(b), _lib.ptr(m), self._p_ob, self._p_om))
+        return C.arrays_to_dict(self._ob, self._om)
 
     @staticmethod
     def _player(player):
