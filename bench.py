@@ -355,10 +355,12 @@ def reference_driver(env, episodes, steps, seed):
 def single_env_leg(args, rep):
     """configs[0] / the reference's own benchmark (test_benchmark.py: 10 episodes x <= 100
     steps, published 312 us per step for the Rust v2 engine): the chess_v2.py-shaped
-    single-board env (one device launch per step: gc_env_single_call, its result in a
-    host-mapped record).  CPU baseline: the same driver and env class over the C oracle's
-    restatement of the same ops on one core.  Beside it, one ChessEngine.get_possible_moves
-    call on the start-position dict (README.md:372-374 publishes 240 us for the v2 engine)."""
+    single-board env (gc_env_single_call per step, served by a resident wave through a
+    host-mapped mailbox, its result in a host-mapped record: no launch per step).  CPU
+    baseline: the same driver and env class over the C oracle's restatement of the same ops
+    on one core.  Beside it, one ChessEngine.get_possible_moves call on the start-position
+    dict (README.md:372-374 publishes 240 us for the v2 engine), served by the engine's
+    resident wave."""
     from gym_chess_amd import codec as C
     from gym_chess_amd.engine import ChessEngine
     from gym_chess_amd.single import ChessEnv
@@ -369,7 +371,8 @@ def single_env_leg(args, rep):
     steps, dt = reference_driver(env, args.single_episodes, 100, 0x5EED)
     out = {"value": dt / steps * 1e6, "unit": "us/step", "higher_is_better": False, "steps": steps,
            "episodes": args.single_episodes, "reference_published_us_per_step": 312.0,
-           "form": "one gc_env_single_call launch per step (device bookkeeping, host-mapped record)"}
+           "form": "one gc_env_single_call per step, served by the resident single-board wave (k_single_server: "
+                   "host-mapped mailbox in, device bookkeeping, host-mapped record out; no launch per step)"}
     env.close()
     eng = ChessEngine(rp.device)
     state = dict(board=C.DEFAULT_BOARD, current_player="WHITE", white_king_castle_is_possible=True,
@@ -383,7 +386,8 @@ def single_env_leg(args, rep):
         eng.get_possible_moves(state, "WHITE")
     out["engine_get_possible_moves"] = {"value": (time.perf_counter() - t0) / calls * 1e6, "unit": "us/call",
                                         "calls": calls, "reference_published_us_per_call": 240.0,
-                                        "state": "DEFAULT_BOARD dict, WHITE"}
+                                        "state": "DEFAULT_BOARD dict, WHITE",
+                                        "form": "one-position call served by the resident engine wave (k_engine_server)"}
     if rep.rank == 0 and rep.world_size == 1 and not args.no_cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         sys.path.insert(0, os.path.join(ROOT, "tests"))
