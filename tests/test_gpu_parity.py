@@ -98,6 +98,33 @@ def test_random_positions_vs_oracle(engine, oracle, seed):
             assert (nb[i] == rb).all() and list(nm[i, :7]) == list(rm[:7]) and rw[i] == rr, i
 
 
+def test_one_position_calls_vs_oracle(engine, oracle):
+    """The engine server (k_engine_server: every n = 1 call under the reference rules, the
+    drop-in ChessEngine's shape): legal and attack-mode lists for both players, castle
+    lists, update_state and next_state of arbitrary moves, one position per call."""
+    boards, metas = random_positions(150, 31)
+    rng = np.random.RandomState(31)
+    for i in range(len(boards)):
+        b, m = boards[i:i + 1], metas[i:i + 1]
+        for attack in (False, True):
+            for white in (0, 1):
+                out, cnt = engine.possible_moves(b, m, white, attack=attack)
+                assert [int(x) for x in out[0, : cnt[0]]] == oracle.get_possible_moves(b[0], m[0], white, attack), i
+        cm, cc = engine.castle_moves(b, m, m[:, 0])
+        assert [int(x) for x in cm[0, : cc[0]]] == oracle.get_castle_moves(b[0], m[0], m[0, 0]), i
+        ob, om = engine.update_state(b, m)
+        rb, rm = oracle.update_state(b[0], m[0])
+        assert (ob[0] == rb).all() and list(om[0, :7]) == list(rm[:7]), i
+        occupied = np.nonzero(b[0])[0]
+        a = 4096 + rng.randint(4) if rng.rand() < 0.2 else int(rng.choice(occupied)) * 64 + rng.randint(64)
+        p = rng.randint(2)
+        nb, nm, rw, st = engine.next_state(b, m, p, a)
+        rc, rb, rm, rr = oracle.next_state(b[0], m[0], p, a)
+        assert st[0] == rc, i
+        if rc in (0, 1):
+            assert (nb[0] == rb).all() and list(nm[0, :7]) == list(rm[:7]) and rw[0] == rr, i
+
+
 def test_next_state_every_legal_move(engine, oracle):
     boards, metas = random_positions(150, 21)
     B, M, P, A = [], [], [], []
