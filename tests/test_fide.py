@@ -283,3 +283,68 @@ def test_fide_env_state_round_trips_keep_en_passant():
     ref = BatchedChessEnv(2, device=0, seed=1)
     with pytest.raises(Exception):
         ref.set_states(b, m, en_passant=ep)  # the reference's rules have no en passant (Q3)
+
+
+def _mask_bits(raw):
+    n = raw.shape[0]
+    bits = np.unpackbits(raw[:, :64].view(np.uint8).reshape(n, 64, 8), axis=2, bitorder="little")
+    out = np.zeros((n, 4101), dtype=bool)
+    out[:, :4096] = bits.reshape(n, 4096).astype(bool)
+    for c in range(4):
+        out[:, 4096 + c] = (raw[:, 64] >> np.uint64(c)) & np.uint64(1) != 0
+    return out
+
+
+@pytest.mark.gpu
+def test_fide_step_device_equals_host_step():
+    """VERDICT r03 missing #3: the device-buffer API step under FIDE rules (k_fenv_step_api)
+    == the host-driven FIDE step (k_fenv_step, pinned to the host build above) ply by ply on
+    the same external actions (legal, and 5 % arbitrary): outputs, states, and the mask / obs
+    / count of the new states; each pick is a legal action of its new position; then the
+    auto-reset pick loop against a host env stepping the same picks and resetting the same
+    boards."""
+    from gym_chess_amd.env import BatchedChessEnv
+
+    fens = [STANDARD[0][0], "8/8/1k6/2b5/2pP4/8/5K2/8 b - d3 0 1", STANDARD[1][0], "4k3/1P6/8/8/8/8/K7/8 w - - 0 1"]
+    n = 256
+    a = BatchedChessEnv(n, device=0, seed=5, rules="fide")
+    b = BatchedChessEnv(n, device=0, seed=5, rules="fide")
+    for e in (a, b):
+        e.set_fens([fens[i % len(fens)] for i in range(n)])
+    io = a.device_io(select=False)
+    act_buf = a.device_io(mask=False, obs=False, count=False, pick=True, select=False)
+    rng = np.random.RandomState(9)
+    for ply in range(60):
+        lists = b.possible_actions()
+        acts = np.array([l[rng.randint(len(l))] if l and rng.rand() > 0.05 else rng.randint(4101) for l in lists],
+                        dtype=np.uint16)
+        act_buf.upload_actions(acts)
+        a.step_device(io, actions=act_buf.ptr["pick"])
+        rw, dn, why = b.step(acts)
+        o = io.fetch()
+        assert (o["reward"] == rw).all() and (o["done"].astype(bool) == dn).all() and (o["reason"] == why).all(), ply
+        bb, bm = b.boards()
+        ab, am = a.boards()
+        assert (ab == bb).all() and (am == bm).all(), ply
+        assert (o["obs"] == bb).all(), ply
+        legal = b.legal_mask()
+        assert (_mask_bits(o["mask"]) == legal).all(), ply
+        assert (o["count"] == legal.sum(axis=1)).all(), ply
+        has = legal.any(axis=1)
+        assert (legal[np.arange(n)[has], o["pick"][has].astype(np.int64)]).all(), ply
+        assert (o["pick"][~has] == 0xFFFF).all(), ply
+        if dn.any():
+            a.reset(dn.astype(np.uint8))
+            b.reset(dn.astype(np.uint8))
+    # auto-reset: actions = the last pick
+    for ply in range(60):
+        picks = io.fetch("pick")["pick"]
+        a.step_device(io, autoreset=True)
+        rw, dn, why = b.step(np.where(picks == 0xFFFF, 4100, picks))  # no legal move: both invalid
+        o = io.fetch("reward", "done", "reason")
+        assert (o["reward"] == rw).all() and (o["done"].astype(bool) == dn).all(), ply
+        if dn.any():
+            b.reset(dn.astype(np.uint8))
+        bb, _ = b.boards()
+        ab, _ = a.boards()
+        assert (ab == bb).all(), ply
