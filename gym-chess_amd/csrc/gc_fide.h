@@ -422,5 +422,89 @@ GC_HD StepOut fenv_step(Pos& s, H& hist, int action, FGen& f) {
     return o;
 }
 
+// ---- the random opponent under FIDE rules (chess_v2.py:219-294 with opponent_policy set;
+// the reference-rules env_step_vs / env_open_vs of gc_env.h with the moves above) -----------
+// one ply of the env: `action` (legal) from s; the window commit, the new position's `f`,
+// the move reward and the 3-fold count (c >= 3: repetition, 0: window full)
+template <class H>
+GC_HD void fenv_ply(Pos& s, H& hist, int action, FGen& f, int* mr, int* c) {
+    RepProbe pr;
+    rep_prefetch(hist, s, pr);
+    Pos ns = s;
+    bool irrev;
+    fapply(ns, action, 0, mr, &irrev);
+    const u32 chk = fcheck_flags(ns);
+    fgen(ns, f);
+    u32 hl = hl_of(s.meta);
+    *c = rep_commit(hist, s, pr, hl, irrev);
+    ns.meta = with_hl((ns.meta & ~(u32)(M_WCHK | M_BCHK | M_DONE)) | chk | ((*c >= 3 || *c == 0) ? M_DONE : 0u), hl);
+    s = ns;
+}
+// the agent's (validated) action, then -- unless that ended the episode -- the opponent's
+// reply drawn from the policy stream (fpick_action: one draw); on o.moved `f` describes the
+// final position
+template <bool VALIDATE, class H, class S>
+GC_HD StepOut fenv_step_vs(Pos& s, H& hist, int action, FGen& f, S& scr, uint64_t seed, u32 board, u32& draw) {
+    StepOut o = {0, 0, R_NONE, 0};
+    if (VALIDATE) {
+        FGen f0;
+        fgen(s, f0);
+        if (!faction_legal(s, f0, action)) {
+            o.reward = -10;
+            o.done = (s.meta & M_DONE) ? 1 : 0;
+            o.reason = R_INVALID;
+            return o;
+        }
+    }
+    if (s.meta & M_DONE) { o.done = 1; o.reason = R_DONE_ALREADY; return o; }
+    if (mc_of(s.meta) > MOVES_MAX) { o.done = 1; o.reason = R_MOVE_CAP; return o; }
+    int mr, c;
+    fenv_ply(s, hist, action, f, &mr, &c);
+    o.reward = -10 + mr;
+    o.moved = 1;
+    if (c >= 3) { o.done = 1; o.reason = R_REPETITION; }
+    if (c == 0) { o.done = 1; o.reason = R_WINDOW_FULL; }
+    const int n = fcount(s, f, false);
+    if (f.g.in_check && n == 0) {  // 270-272
+        s.meta |= M_DONE;
+        o.done = 1;
+        o.reward += 100;
+        o.reason = R_MATE;
+    }
+    if (o.done) return o;
+    if (n == 0) {  // 120-122: the opponent has no move ("resign")
+        s.meta |= M_DONE;
+        o.done = 1;
+        o.reason = R_OPP_NO_MOVE;
+        return o;
+    }
+    hist.commit();  // the agent ply's window write lands before the reply probes it
+    const int oa = fpick_action(s, f, scr, seed, board, draw);
+    fenv_ply(s, hist, oa, f, &mr, &c);
+    o.reward -= mr;  // 283
+    if (c >= 3) { o.done = 1; o.reason = R_REPETITION; }
+    if (c == 0) { o.done = 1; o.reason = R_WINDOW_FULL; }
+    if (f.g.in_check && fcount(s, f, false) == 0) {  // 285-288
+        s.meta |= M_DONE;
+        o.done = 1;
+        o.reward -= 100;
+        o.reason = R_MATED;
+    }
+    if (s.meta & M_WHITE) s.meta += (1u << M_MC_SHIFT);  // 291-292
+    return o;
+}
+// reset() for a BLACK agent (chess_v2.py:208-216): the opponent opens from the reset
+// position (WHITE to move, `f` its generation); its 3-fold verdict is discarded and
+// move_count becomes 1; with no opening move the env is left done.  `f` then describes the
+// agent's position.
+template <class H, class S>
+GC_HD void fenv_open_vs(Pos& s, H& hist, FGen& f, S& scr, uint64_t seed, u32 board, u32& draw) {
+    if (fcount(s, f, false) == 0) { s.meta |= M_DONE; return; }
+    const int oa = fpick_action(s, f, scr, seed, board, draw);
+    int mr, c;
+    fenv_ply(s, hist, oa, f, &mr, &c);
+    s.meta = (s.meta & ~(u32)M_DONE) + (1u << M_MC_SHIFT);
+}
+
 }  // namespace fide
 }  // namespace gc

@@ -203,8 +203,10 @@ __global__ void __launch_bounds__(BLOCK) k_finit_cache(EnvDev e, EnvDev::InitCac
 }
 
 // POLICY=false: external action e.act[i] (validated); POLICY=true: the random self-play
-// driver (act[i] = this state's policy pick; A_NONE or done -> reset; pick the next action)
-template <bool POLICY>
+// driver (act[i] = this state's policy pick; A_NONE or done -> reset; pick the next action).
+// OPP: the random opponent replies inside the step (gcf::fenv_step_vs) and, for a BLACK agent,
+// opens after every reset (gcf::fenv_open_vs), as k_env_step<POLICY, true> does.
+template <bool POLICY, bool OPP = false>
 __global__ void __launch_bounds__(BLOCK) k_fenv_step(EnvDev e) {
     LDS_SCRATCH_DECL;
     int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -221,7 +223,7 @@ __global__ void __launch_bounds__(BLOCK) k_fenv_step(EnvDev e) {
         h.bump_gen();
         o.reason = R_NO_MOVES;
     } else {
-        o = gcf::fenv_step<!POLICY>(s, h, a, f);
+        o = OPP ? gcf::fenv_step_vs<!POLICY>(s, h, a, f, scr, e.seed, (u32)i, d) : gcf::fenv_step<!POLICY>(s, h, a, f);
         have = o.moved;
         nst += 1;
         if (POLICY && o.done) {
@@ -231,10 +233,13 @@ __global__ void __launch_bounds__(BLOCK) k_fenv_step(EnvDev e) {
         }
     }
     if (POLICY) {
-        if (!have) gcf::fgen(s, f);
+        if (!have) {
+            gcf::fgen(s, f);
+            if (OPP && e.agent_black) gcf::fenv_open_vs(s, h, f, scr, e.seed, (u32)i, d);
+        }
         e.act[i] = fpick(s, f, scr, e.seed, i, d);
-        e.draw[i] = d;
     }
+    e.draw[i] = d;
     h.commit();
     e.st.store(i, s);
     h.flush(g0);
@@ -244,21 +249,93 @@ __global__ void __launch_bounds__(BLOCK) k_fenv_step(EnvDev e) {
     e.reason[i] = (uint8_t)o.reason;
 }
 
+template <bool OPP = false>
 __global__ void __launch_bounds__(BLOCK) k_fenv_reset(EnvDev e, const uint8_t* __restrict__ mask, int select) {
     LDS_SCRATCH_DECL;
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= e.n) return;
     if (mask && !mask[i]) return;
+    const u32 g0 = e.hgen[i];
+    DevHist h = e.hist(i, g0);
     Pos s = fide_reset_pos(e);
-    e.hgen[i] += 1;
-    if (select) {
+    h.bump_gen();
+    if ((OPP && e.agent_black) || select) {
         gcf::FGen f;
         gcf::fgen(s, f);
         u32 d = e.draw[i];
-        e.act[i] = fpick(s, f, scr, e.seed, i, d);
+        if (OPP && e.agent_black) gcf::fenv_open_vs(s, h, f, scr, e.seed, (u32)i, d);
+        if (select) e.act[i] = fpick(s, f, scr, e.seed, i, d);
         e.draw[i] = d;
+        h.commit();
     }
+    h.flush(g0);
     e.st.store(i, s);
+}
+
+// the fused random self-play under FIDE rules with the random opponent (the paired fused
+// kernel serves opponent "none"): one lane per board, `plies` steps in one launch, the
+// per-ply trace and stats as k_env_rollout
+template <bool OPP>
+__global__ void __launch_bounds__(BLOCK) k_fenv_rollout(EnvDev e, int plies, u64* trace, uint64_t* stats) {
+    LDS_SCRATCH_DECL;
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= e.n) return;
+    Pos s = e.st.load(i);
+    u32 g0 = e.hgen[i], d = e.draw[i];
+    int a = (int)e.act[i];
+    DevHist h = e.hist(i, g0);
+    uint64_t steps = 0, rsum = 0;
+    u32 e_mate = 0, e_rep = 0, e_cap = 0, e_nomove = 0, e_err = 0;
+    StepOut o = {0, 0, R_NONE, 0};
+    for (int p = 0; p < plies; p++) {
+        o = {0, 0, R_NONE, 0};
+        gcf::FGen f;
+        bool have = false;
+        int played = a;
+        if (a == A_NONE) {
+            s = fide_reset_pos(e);
+            h.bump_gen();
+            o.reason = R_NO_MOVES;
+            e_nomove++;
+            played = -1;
+        } else {
+            o = OPP ? gcf::fenv_step_vs<false>(s, h, a, f, scr, e.seed, (u32)i, d) : gcf::fenv_step<false>(s, h, a, f);
+            have = o.moved;
+            steps++;
+            rsum += (uint64_t)(int64_t)o.reward;
+            if (o.done) {
+                e_mate += o.reason == R_MATE || o.reason == R_MATED;
+                e_rep += o.reason == R_REPETITION;
+                e_cap += o.reason == R_MOVE_CAP;
+                e_err += o.reason == R_WINDOW_FULL;
+                e_nomove += o.reason == R_OPP_NO_MOVE;
+                s = fide_reset_pos(e);
+                h.bump_gen();
+                have = false;
+            }
+        }
+        if (!have) {
+            gcf::fgen(s, f);
+            if (OPP && e.agent_black) gcf::fenv_open_vs(s, h, f, scr, e.seed, (u32)i, d);
+        }
+        if (trace) trace[(size_t)p * e.n + i] = trace_word(played, o);
+        a = fpick(s, f, scr, e.seed, i, d);
+        h.commit();
+    }
+    e.reward[i] = o.reward;
+    e.done[i] = (uint8_t)o.done;
+    e.reason[i] = (uint8_t)o.reason;
+    e.st.store(i, s);
+    h.flush(g0);
+    e.draw[i] = d;
+    e.act[i] = (uint16_t)a;
+    e.nsteps[i] += (u32)steps;
+    if (stats) {
+        uint64_t* so = stats + 8 * (size_t)i;
+        so[0] += steps; so[1] += rsum;
+        so[2 + R_MATE] += e_mate; so[2 + R_REPETITION] += e_rep; so[2 + R_MOVE_CAP] += e_cap;
+        so[2 + R_NO_MOVES] += e_nomove; so[2 + R_BOTH_CHECKED] += e_err;
+    }
 }
 
 __global__ void __launch_bounds__(BLOCK) k_fenv_select(EnvDev e) {

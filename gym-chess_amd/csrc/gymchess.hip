@@ -3461,24 +3461,32 @@ __global__ void __launch_bounds__(BLOCK) k_select(EnvDev e) {
 // gcf::fenv_step (en passant, promotion to a queen, FIDE castling), auto-reset to the start
 // position, then k_env_step_api's outputs from the new position's legal targets per own
 // square (the action-id order of the mask and of the pick; castles in word 64).
+template <bool OPP>
 __global__ void __launch_bounds__(BLOCK) k_fenv_step_api(EnvDev e, const uint16_t* __restrict__ acts,
                                                          int32_t* __restrict__ rw, uint8_t* __restrict__ dn,
                                                          uint8_t* __restrict__ rs, u64* __restrict__ mask,
                                                          int8_t* __restrict__ obs, int32_t* __restrict__ cnt,
                                                          uint16_t* __restrict__ pick_out, int autoreset) {
+    LDS_SCRATCH_DECL;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= e.n) return;
     Pos s = e.st.load(i);
     u32 g0 = e.hgen[i], d = e.draw[i], nst = e.nsteps[i];
     DevHist h = e.hist(i, g0);
     gcf::FGen f;
-    const StepOut o = gcf::fenv_step<true>(s, h, (int)acts[i], f);
+    const StepOut o = OPP ? gcf::fenv_step_vs<true>(s, h, (int)acts[i], f, scr, e.seed, (u32)i, d)
+                          : gcf::fenv_step<true>(s, h, (int)acts[i], f);
     bool have = o.moved;
     nst += 1;
-    if (autoreset && o.done) {
+    if (autoreset && o.done) {  // a BLACK agent's opponent opens (chess_v2.py:208-216)
         s = fide_reset_pos(e);
         h.bump_gen();
-        have = false;
+        gcf::fgen(s, f);
+        if (OPP && e.agent_black) {
+            h.commit();
+            gcf::fenv_open_vs(s, h, f, scr, e.seed, (u32)i, d);
+        }
+        have = true;
     }
     if (!have) gcf::fgen(s, f);
     const size_t N = (size_t)e.n;
@@ -4607,13 +4615,15 @@ static int set_window_kind(gc_env* e, bool uncapped) {
 // kernel dispatch on the env's opponent mode (a kernel-argument-uniform choice made once per
 // launch on the host, so the opponent="none" kernels carry no opponent code)
 static void launch_reset(gc_env* e, const uint8_t* mask, int select) {
-    if (e->rules) k_fenv_reset<<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d, mask, select);
+    if (e->rules && e->d.opp) k_fenv_reset<true><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d, mask, select);
+    else if (e->rules) k_fenv_reset<false><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d, mask, select);
     else if (e->d.opp) k_env_reset<true><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d, mask, select);
     else k_env_reset<false><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d, mask, select);
 }
 template <bool POLICY>
 static void launch_step(gc_env* e) {
-    if (e->rules) k_fenv_step<POLICY><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d);
+    if (e->rules && e->d.opp) k_fenv_step<POLICY, true><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d);
+    else if (e->rules) k_fenv_step<POLICY, false><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d);
     else if (e->d.opp) k_env_step<POLICY, true><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d);
     else k_env_step<POLICY, false><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d);
 }
@@ -4639,6 +4649,7 @@ static const uint16_t* sw_table(const ResetInfo& r) {
 }
 static bool pair_ok(const gc_env* e) {
     if (!e->d.opp) return true;
+    if (e->rules) return false;  // FIDE with the random opponent: the one-wave kernels (k_fenv_*)
     const EnvDev::InitCache& ic = e->d.ic;
     return ic.usable && ic.table && (!e->d.agent_black || ic.open_safe);
 }
@@ -4772,7 +4783,6 @@ extern "C" int gc_env_set_opponent(gc_env* e, int opponent, int agent_white) {
     SRV_QUIESCE(e);
     if (opponent != 0 && opponent != 1) return fail("opponent must be 0 (none) or 1 (random)");
     if (!agent_white && !opponent) return fail("player_color BLACK needs an opponent (chess_v2.py:208-212)");
-    if (opponent && e->rules) return fail("the FIDE rules mode supports opponent \"none\" only");
     HIPCHK(hipSetDevice(e->device));
     HIPCHK(hipStreamSynchronize(e->stream));
     if (set_window_kind(e, !agent_white)) return -1;
@@ -4786,13 +4796,12 @@ extern "C" int gc_env_set_opponent(gc_env* e, int opponent, int agent_white) {
     return 0;
 }
 
-// rules 0: the reference's (default); 1: FIDE (gc_fide.h; opponent "none" only).  Resets
-// every board and restarts the policy streams.
+// rules 0: the reference's (default); 1: FIDE (gc_fide.h; with the random opponent on the
+// one-wave kernels).  Resets every board and restarts the policy streams.
 extern "C" int gc_env_set_rules(gc_env* e, int rules) {
     if (!e) return fail("null env");
     SRV_QUIESCE(e);
     if (rules != 0 && rules != 1) return fail("rules must be 0 (reference) or 1 (fide)");
-    if (rules && e->d.opp) return fail("the FIDE rules mode supports opponent \"none\" only");
     HIPCHK(hipSetDevice(e->device));
     HIPCHK(hipStreamSynchronize(e->stream));
     if (rules && !e->icd_f) {  // the FIDE reset position's move set (paired kernels)
@@ -5026,9 +5035,13 @@ extern "C" int gc_env_step_device(gc_env* e, const uint16_t* d_actions, int32_t*
     HIPCHK(hipSetDevice(e->device));
     if (spill_before(e)) return -1;
     const int ar = flags & 1;
-    if (e->rules) {  // FIDE (opponent "none" only): one lane per board
-        k_fenv_step_api<<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d, d_actions, d_reward, d_done, d_reason, d_mask,
-                                                                  d_obs, d_count, d_pick, ar);
+    if (e->rules) {  // FIDE: one lane per board
+        if (e->d.opp)
+            k_fenv_step_api<true><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d, d_actions, d_reward, d_done, d_reason,
+                                                                            d_mask, d_obs, d_count, d_pick, ar);
+        else
+            k_fenv_step_api<false><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d, d_actions, d_reward, d_done, d_reason,
+                                                                             d_mask, d_obs, d_count, d_pick, ar);
         HIPCHK(hipGetLastError());
         if (spill_after(e)) return -1;
         e->policy_ready = d_pick != nullptr;
@@ -5289,6 +5302,8 @@ static int issue_rollout(gc_env* e, int n_plies, uint64_t* d_trace, bool stats) 
                 case 1: k_env_rollout2<false, 1><<<grid, bs, 0, e->stream>>>(e->slab, d.n, d.seed, d.htab, sw_table(r), r.icd, ri, st, tr); break;
                 default: k_env_rollout2<false, 2><<<grid, bs, 0, e->stream>>>(e->slab, d.n, d.seed, d.htab, sw_table(r), r.icd, ri, st, tr); break;
             }
+        } else if (e->rules) {  // FIDE with the random opponent
+            k_fenv_rollout<true><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d, k, tr, st);
         } else if (e->d.opp) {
             k_env_rollout<true><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d, k, tr, st);
         } else {

@@ -51,7 +51,7 @@ class BatchedChessEnv:
         if opponent != "none" or player_color != C.WHITE:
             _lib.check(self._L.gc_env_set_opponent(self._h, int(opponent == "random"), int(player_color == C.WHITE)))
         self.rules = rules
-        if _lib.rules_id(rules):  # FIDE (gc_fide.h): opponent "none", no fused rollout
+        if _lib.rules_id(rules):  # FIDE (gc_fide.h): either opponent mode
             _lib.check(self._L.gc_env_set_rules(self._h, _lib.rules_id(rules)))
 
     def close(self):

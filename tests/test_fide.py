@@ -348,3 +348,136 @@ def test_fide_step_device_equals_host_step():
         bb, _ = b.boards()
         ab, _ = a.boards()
         assert (ab == bb).all(), ply
+
+
+def _fide_engine_state(env):
+    """the env's states as FIDE engine inputs (meta8[7] = en-passant file + 1)"""
+    b, m = env.boards()
+    m = m.copy()
+    ep = env.en_passant()
+    m[:, 7] = np.where(ep >= 0, ep + 1, 0).astype(np.uint8)
+    return b, m
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("black", [False, True])
+def test_fide_random_opponent_steps_are_agent_then_opponent_moves(black):
+    """VERDICT r03 missing #3: the random opponent under FIDE rules (gcf::fenv_step_vs).  For
+    every board and ply, through the FIDE engine: the agent's legal move, then -- unless the
+    episode ended -- ONE legal opponent reply from that position; the reward is -10 + the
+    agent's capture value - the reply's (+100 for mating, -100 for being mated), the reasons
+    those of chess_v2.py:219-294.  A BLACK agent's boards start one white move after reset."""
+    from gym_chess_amd.engine import Engine
+    from gym_chess_amd.env import BatchedChessEnv
+
+    eng = Engine(0, rules="fide")
+    n = 96
+    env = BatchedChessEnv(n, device=0, seed=23, opponent="random", player_color="BLACK" if black else "WHITE",
+                          rules="fide")
+    start = np.array(__import__("gym_chess_amd.codec", fromlist=["DEFAULT_BOARD"]).DEFAULT_BOARD, np.int8).reshape(64)
+    if black:  # chess_v2.py:208-216: the opponent opened
+        b, m = env.boards()
+        sm = np.zeros((1, 8), np.uint8); sm[0, :5] = 1
+        kids, kc = eng.possible_moves(start[None], sm, 1)
+        children = {eng.next_state(start[None], sm, 1, int(a))[0][0].tobytes() for a in kids[0, :kc[0]]}
+        assert all(b[i].tobytes() in children for i in range(n)) and (m[:, 0] == 0).all() and (m[:, 7] == 1).all()
+    rng = np.random.RandomState(5)
+    agent_white = 0 if black else 1
+    seen = {0: 0, 1: 0, 8: 0}
+    for ply in range(80):
+        b0, m0 = _fide_engine_state(env)
+        lists = env.possible_actions()
+        live = np.array([len(x) > 0 for x in lists])
+        acts = np.array([l[rng.randint(len(l))] if l else 4100 for l in lists], dtype=np.uint16)
+        rw, dn, why = env.step(acts)
+        b1, _ = env.boards()
+        ib, im, irw, ist = eng.next_state(b0, m0, agent_white, acts)
+        for i in np.nonzero(live)[0]:
+            assert ist[i] == 0, (ply, i)
+            r = int(why[i])
+            if r in (1, 9):  # the agent mated / the opponent has no move: the board after the agent's move
+                assert (b1[i] == ib[i]).all(), (ply, i, r)
+                assert rw[i] == -10 + irw[i] + (100 if r == 1 else 0), (ply, i, r)
+            elif r in (0, 8):  # one reply of the opponent from the intermediate position
+                om_ = im[i:i + 1].copy()
+                replies, rc = eng.possible_moves(ib[i:i + 1], om_, 1 - agent_white)
+                ok = False
+                for x in replies[0, :rc[0]]:
+                    nb, _, nrw, _ = eng.next_state(ib[i:i + 1], om_, 1 - agent_white, int(x))
+                    if (nb[0] == b1[i]).all() and rw[i] == -10 + irw[i] - nrw[0] - (100 if r == 8 else 0):
+                        ok = True
+                        break
+                assert ok, (ply, i, r)
+            if r in seen:
+                seen[r] += 1
+        if dn.any():
+            env.reset(dn.astype(np.uint8))
+    assert seen[0] > n * 40
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("black", [False, True])
+def test_fide_random_opponent_fused_rollout_matches_step_random(black):
+    """The fused one-wave rollout under FIDE with the opponent (k_fenv_rollout<true>) leaves
+    every board as the per-ply launches (k_fenv_step<true, true>) do."""
+    from gym_chess_amd.env import BatchedChessEnv
+
+    kw = dict(device=0, seed=31, opponent="random", player_color="BLACK" if black else "WHITE", rules="fide")
+    a = BatchedChessEnv(512, **kw)
+    b = BatchedChessEnv(512, **kw)
+    a.rollout(300)
+    b.step_random(300)
+    ba, ma = a.boards()
+    bb, mb = b.boards()
+    assert (ba == bb).all() and (ma == mb).all()
+    assert (a.en_passant() == b.en_passant()).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("black", [False, True])
+def test_fide_random_opponent_step_device_equals_host_step(black):
+    """The device-buffer API step under FIDE with the opponent == the host-driven step on the
+    same external actions (no pick: both envs draw only the opponent's replies); then the
+    auto-reset pick loop: every output describes the env's new state, and a done board is
+    back at the start position (a BLACK agent's: one white move after it)."""
+    from gym_chess_amd import codec as C
+    from gym_chess_amd.engine import Engine
+    from gym_chess_amd.env import BatchedChessEnv
+
+    kw = dict(device=0, seed=41, opponent="random", player_color="BLACK" if black else "WHITE", rules="fide")
+    n = 200
+    a = BatchedChessEnv(n, **kw)
+    b = BatchedChessEnv(n, **kw)
+    io = a.device_io(pick=False, select=False)
+    act_buf = a.device_io(mask=False, obs=False, count=False, pick=True, select=False)
+    rng = np.random.RandomState(4)
+    for ply in range(60):
+        lists = b.possible_actions()
+        acts = np.array([l[rng.randint(len(l))] if l and rng.rand() > 0.05 else rng.randint(4101) for l in lists],
+                        dtype=np.uint16)
+        act_buf.upload_actions(acts)
+        a.step_device(io, actions=act_buf.ptr["pick"])
+        rw, dn, why = b.step(acts)
+        o = io.fetch()
+        assert (o["reward"] == rw).all() and (o["done"].astype(bool) == dn).all() and (o["reason"] == why).all(), ply
+        bb, bm = b.boards()
+        ab, am = a.boards()
+        assert (ab == bb).all() and (am == bm).all(), ply
+        assert (o["obs"] == bb).all() and (_mask_bits(o["mask"]) == b.legal_mask()).all(), ply
+        if dn.any():
+            a.reset(dn.astype(np.uint8))
+            b.reset(dn.astype(np.uint8))
+    start = np.array(C.DEFAULT_BOARD, np.int8).reshape(64)
+    eng = Engine(0, rules="fide")
+    sm = np.zeros((1, 8), np.uint8)
+    sm[0, :5] = 1
+    kids, kc = eng.possible_moves(start[None], sm, 1)
+    openings = {eng.next_state(start[None], sm, 1, int(x))[0][0].tobytes() for x in kids[0, :kc[0]]}
+    io2 = a.device_io()
+    for ply in range(40):
+        a.step_device(io2, autoreset=True)
+        o = io2.fetch()
+        ab, am = a.boards()
+        assert (o["obs"] == ab).all() and (_mask_bits(o["mask"]) == a.legal_mask()).all(), ply
+        for i in np.nonzero(o["done"])[0]:
+            assert (ab[i].tobytes() in openings) if black else (ab[i] == start).all(), (ply, i)
