@@ -3715,6 +3715,55 @@ extern "C" int gc_engine_create(int device, gc_engine** out) {
     return 0;
 }
 
+// ---- resident servers at process exit: a server wave exits after SRV_IDLE_MS without a
+// request, so a process that ends right after its last call (without destroying the env or
+// engine) could end with the wave still resident.  Every running server is registered here;
+// an atexit handler asks each to QUIT through its host-mapped mailbox and waits (host memory
+// only, no HIP call: the runtime may be tearing down) until it has marked its exit.
+struct SrvReg {
+    u32 *req_seq, *op, *exited;      // the mailbox (host-mapped)
+    const u32 *seq, *launch;         // the owner's last served sequence number and launch id
+};
+static std::mutex g_srvreg_mu;
+static std::vector<std::pair<const void*, SrvReg>> g_srvreg;
+static void srv_quit_all() {
+    std::lock_guard<std::mutex> lk(g_srvreg_mu);
+    const bool log = getenv("GC_SRV_EXIT_LOG") != nullptr;  // (tests: which servers this stopped)
+    for (auto& it : g_srvreg) {
+        const SrvReg& r = it.second;
+        if (!*r.launch || __atomic_load_n(r.exited, __ATOMIC_ACQUIRE) == *r.launch) continue;
+        __atomic_store_n(r.op, (u32)SRV_QUIT, __ATOMIC_RELAXED);
+        __atomic_store_n(r.req_seq, *r.seq + 1, __ATOMIC_RELEASE);
+        const auto t0 = std::chrono::steady_clock::now();
+        while (__atomic_load_n(r.exited, __ATOMIC_ACQUIRE) != *r.launch &&
+               std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(2 * SRV_IDLE_MS)) {
+        }
+        if (log)
+            fprintf(stderr, "gymchess: server of %p %s at exit\n", it.first,
+                    __atomic_load_n(r.exited, __ATOMIC_ACQUIRE) == *r.launch ? "stopped" : "did not answer");
+    }
+    g_srvreg.clear();
+}
+static void srv_register(const void* owner, const SrvReg& r) {
+    std::lock_guard<std::mutex> lk(g_srvreg_mu);
+    static bool hooked = false;
+    if (!hooked) {
+        std::atexit(srv_quit_all);
+        hooked = true;
+    }
+    for (auto& it : g_srvreg)
+        if (it.first == owner) return;
+    g_srvreg.emplace_back(owner, r);
+}
+static void srv_unregister(const void* owner) {
+    std::lock_guard<std::mutex> lk(g_srvreg_mu);
+    for (size_t k = 0; k < g_srvreg.size(); k++)
+        if (g_srvreg[k].first == owner) {
+            g_srvreg.erase(g_srvreg.begin() + (long)k);
+            return;
+        }
+}
+
 // ---- the engine server's host side (the single-board server's protocol, srv_call)
 static bool eng_srv_enabled() {
     static const bool off = getenv("GC_ENGINE_SERVER") && atoi(getenv("GC_ENGINE_SERVER")) == 0;  // A/B
@@ -3753,6 +3802,7 @@ static int eng_srv_call(gc_engine* e, int op, const int8_t* board, const uint8_t
         if (!e->srv_launch || __atomic_load_n(&b->exited, __ATOMIC_ACQUIRE) == e->srv_launch) {
             if (e->srv_launch) HIPCHK(hipStreamSynchronize(e->srv_stream));  // drained (idle exit)
             e->srv_launch = ++e->srv_next_launch;
+            srv_register(e, SrvReg{&b->req_seq, &b->op, &b->exited, &e->srv_seq, &e->srv_launch});
             k_engine_server<<<1, 64, 0, e->srv_stream>>>(e->srv_d, e->srv_seq, e->srv_launch);
             HIPCHK(hipGetLastError());
         }
@@ -3775,6 +3825,7 @@ extern "C" int gc_engine_destroy(gc_engine* e) {
     if (!e) return 0;
     (void)hipSetDevice(e->device);
     (void)eng_srv_stop(e);
+    srv_unregister(e);
     if (e->srv_stream) (void)hipStreamDestroy(e->srv_stream);
     if (e->srv) (void)hipHostFree(e->srv);
     (void)hipStreamSynchronize(e->stream);
@@ -4825,6 +4876,7 @@ extern "C" int gc_env_destroy(gc_env* e) {
     if (!e) return 0;
     (void)hipSetDevice(e->device);
     (void)srv_stop(e);
+    srv_unregister(e);
     (void)hipStreamSynchronize(e->stream);
     env_free(e);
     delete e;
@@ -4905,6 +4957,7 @@ static int srv_call(gc_env* e, int board, int op, int action, int flags) {
             HIPCHK(hipStreamSynchronize(e->stream));
             e->srv_launch = ++e->srv_next_launch;
             e->srv_board = board;
+            srv_register(e, SrvReg{&b->req_seq, &b->op, &b->exited, &e->srv_seq, &e->srv_launch});
             k_single_server<<<1, 64, 0, e->srv_stream>>>(e->d, board, e->srv_d, e->srec_d, e->srv_seq, e->srv_launch);
             HIPCHK(hipGetLastError());
         }

@@ -255,3 +255,28 @@ def test_single_env_server_idle_exit_and_restart():
         if o1[2]:
             dev.reset(); ref.reset()
     dev.close()
+
+
+@pytest.mark.gpu
+def test_resident_servers_stopped_at_process_exit():
+    """A process that ends right after its last server call (no close / destroy) stops the
+    resident waves (engine server, single-board server) in the library's exit handler."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "from gym_chess_amd import codec as C\n"
+            "from gym_chess_amd.engine import ChessEngine\n"
+            "from gym_chess_amd.single import ChessEnv\n"
+            "e = ChessEngine(0)\n"
+            "st = dict(board=C.DEFAULT_BOARD, current_player='WHITE', white_king_castle_is_possible=True,"
+            " white_queen_castle_is_possible=True, black_king_castle_is_possible=True, black_queen_castle_is_possible=True)\n"
+            "assert len(e.get_possible_moves(st, 'WHITE')) == 20\n"
+            "env = ChessEnv(opponent='none', log=False)\n"
+            "env.step(env.possible_actions[0])\n" % os.path.join(root, "gym-chess_amd"))
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120,
+                         env=dict(os.environ, GC_SRV_EXIT_LOG="1"))
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert "did not answer" not in out.stderr, out.stderr[-2000:]
