@@ -2782,6 +2782,7 @@ __global__ void __launch_bounds__(64) k_engine_server(EngBox* box, u32 done_seq,
     __shared__ uint8_t om[8];
     __shared__ uint16_t mv[ENG_SRV_CAP];
     __shared__ int32_t cnt, rw, st;
+    __shared__ Pos tp;  // NEXT / UPDATE: the new state, for the lanes' mailbox squares
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     const int lane = (int)threadIdx.x;
     unsigned long long idle0 = __builtin_amdgcn_s_memrealtime();
@@ -2821,17 +2822,22 @@ __global__ void __launch_bounds__(64) k_engine_server(EngBox* box, u32 done_seq,
                 if (g.castles & 2) c |= g.white ? (1 << 0) : (1 << 2);
                 cnt = c;
             }
-        } else if (lane == 0) {  // NEXT / UPDATE
-            Pos t = s;
-            if (op == ENG_NEXT) {
-                const uint16_t a = (uint16_t)arg;
-                t = next_state_one(s, &side, &a, &rw, &st, 0);
-            } else {
-                t.meta = (t.meta & ~(u32)(M_WCHK | M_BCHK)) | check_flags(t);
-                rw = 0;
-                st = 0;
+        } else {  // NEXT / UPDATE: the move and flags on lane 0, the mailbox a square per lane
+            if (lane == 0) {
+                Pos t = s;
+                if (op == ENG_NEXT) {
+                    const uint16_t a = (uint16_t)arg;
+                    t = next_state_one(s, &side, &a, &rw, &st, 0);
+                } else {
+                    t.meta = (t.meta & ~(u32)(M_WCHK | M_BCHK)) | check_flags(t);
+                    rw = 0;
+                    st = 0;
+                }
+                export_one(t, nullptr, om, 0);
+                tp = t;
             }
-            export_one(t, ob, om, 0);
+            __syncthreads();
+            ob[lane] = (int8_t)id_at(tp, lane);
         }
         __syncthreads();
         // the response: results, a system-scope fence, then resp_seq
@@ -3157,7 +3163,9 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
             for (int sq = s0; sq < s0 + 32; sq++) {
                 const bool b = (g.own >> sq) & 1;
                 const u64 v = scr.get(j & (SCRATCH_SLOTS - 1));
-                o[sq * N] = b ? v : 0ull;
+                // streamed (non-temporal): written once, read by the caller after the launch
+                // (same-box A/B: 3.105-3.121 vs 3.049-3.104e9, profiles/r04_v2)
+                __builtin_nontemporal_store(b ? v : 0ull, o + sq * N);
                 j += b ? 1 : 0;
             }
             if (role == 0) {
