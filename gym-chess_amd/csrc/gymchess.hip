@@ -3584,6 +3584,9 @@ struct gc_engine {
     struct EngBox* srv = nullptr; struct EngBox* srv_d = nullptr;
     hipStream_t srv_stream = nullptr;
     uint32_t srv_seq = 0, srv_launch = 0, srv_next_launch = 0;
+    // one call at a time per engine: ctypes releases the GIL, and a call's staging buffers
+    // and the server's mailbox are the engine's own
+    std::mutex mu;
 };
 #define ENGINE_ZC_BYTES 65536
 // byte offsets of the views for n boards and a list capacity lc (256-B aligned)
@@ -3704,6 +3707,7 @@ static void engine_export(gc_engine* e, SoA st) {
 // rules 0: the reference's (default); 1: FIDE (gc_fide.h; meta8[7] = en-passant file + 1)
 extern "C" int gc_engine_set_rules(gc_engine* e, int rules) {
     if (!e) return fail("null engine");
+    std::lock_guard<std::mutex> lk(e->mu);
     if (rules != 0 && rules != 1) return fail("rules must be 0 (reference) or 1 (fide)");
     e->rules = rules;
     return 0;
@@ -3847,6 +3851,7 @@ extern "C" int gc_engine_get_possible_moves(gc_engine* e, int n, const int8_t* b
                                             const uint8_t* player_white, int attack, uint16_t* moves, int cap,
                                             int32_t* counts) {
     if (!e || !moves || !counts || !player_white) return fail("null argument");
+    std::lock_guard<std::mutex> lk(e->mu);
     if (cap <= 0) return fail("cap must be > 0");
     if (eng_srv_use(e, n) && cap <= ENG_SRV_CAP) {
         if (!boards || !meta) return fail("null boards/meta");
@@ -3880,6 +3885,7 @@ extern "C" int gc_engine_get_possible_moves(gc_engine* e, int n, const int8_t* b
 extern "C" int gc_engine_get_castle_moves(gc_engine* e, int n, const int8_t* boards, const uint8_t* meta,
                                           const uint8_t* player_white, uint16_t* moves, int32_t* counts) {
     if (!e || !moves || !counts || !player_white) return fail("null argument");
+    std::lock_guard<std::mutex> lk(e->mu);
     if (eng_srv_use(e, n)) {
         if (!boards || !meta) return fail("null boards/meta");
         if (check_boards(1, boards)) return -1;
@@ -3928,6 +3934,7 @@ extern "C" int gc_engine_next_state(gc_engine* e, int n, const int8_t* boards, c
                                     const uint8_t* player_white, const uint16_t* actions, int8_t* out_boards,
                                     uint8_t* out_meta, int32_t* rewards, int32_t* status) {
     if (!e || !player_white || !actions || !out_boards || !out_meta || !rewards || !status) return fail("null argument");
+    std::lock_guard<std::mutex> lk(e->mu);
     for (int i = 0; i < n; i++)
         if (actions[i] > A_QSB) return fail("action out of range at index " + std::to_string(i));
     if (eng_srv_use(e, n)) {
@@ -3971,6 +3978,7 @@ extern "C" int gc_engine_next_state(gc_engine* e, int n, const int8_t* boards, c
 extern "C" int gc_engine_update_state(gc_engine* e, int n, const int8_t* boards, const uint8_t* meta,
                                       int8_t* out_boards, uint8_t* out_meta) {
     if (!e || !out_boards || !out_meta) return fail("null argument");
+    std::lock_guard<std::mutex> lk(e->mu);
     if (eng_srv_use(e, n)) {
         if (!boards || !meta) return fail("null boards/meta");
         if (check_boards(1, boards)) return -1;
@@ -4303,6 +4311,7 @@ extern "C" int gc_perft_dedup_stats(uint64_t* records, uint64_t* counted) {
 extern "C" int gc_engine_perft(gc_engine* e, int n, const int8_t* boards, const uint8_t* meta, int depth,
                                uint64_t* nodes) {
     if (!e || !nodes) return fail("null argument");
+    std::lock_guard<std::mutex> lk(e->mu);
     if (depth < 0 || depth > PERFT_MAXD) return fail("depth must be in [0, 8]");
     if (engine_reserve(e, n, 1)) return -1;
     EngineLayout o;

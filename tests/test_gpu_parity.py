@@ -125,6 +125,30 @@ def test_one_position_calls_vs_oracle(engine, oracle):
             assert (nb[0] == rb).all() and list(nm[0, :7]) == list(rm[:7]) and rw[0] == rr, i
 
 
+def test_one_position_calls_from_two_threads(engine, oracle):
+    """ctypes releases the GIL: two threads calling one engine at once (the server's mailbox
+    and the staging buffers are the engine's) get every list right."""
+    import threading
+
+    boards, metas = random_positions(80, 41)
+    refs = [oracle.get_possible_moves(boards[i], metas[i], int(metas[i, 0]), False) for i in range(80)]
+    errors = []
+
+    def work(lo, hi):
+        for _ in range(5):
+            for i in range(lo, hi):
+                out, cnt = engine.possible_moves(boards[i:i + 1], metas[i:i + 1], int(metas[i, 0]))
+                if [int(x) for x in out[0, : cnt[0]]] != refs[i]:
+                    errors.append(i)
+
+    ts = [threading.Thread(target=work, args=(0, 40)), threading.Thread(target=work, args=(40, 80))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errors, errors[:8]
+
+
 def test_next_state_every_legal_move(engine, oracle):
     boards, metas = random_positions(150, 21)
     B, M, P, A = [], [], [], []
