@@ -260,6 +260,27 @@ def test_perft_split_transpositions_merged_exactly(engine):
     assert c1 - c0 < 0.8 * (r1 - r0), (r1 - r0, c1 - c0)
 
 
+def test_perft_transpositions_over_several_chunks(engine):
+    """4 096 mid-game roots: ~5e6 depth-3 subtree roots, so the split pass runs several chunks
+    of 2^21 parents, each with its own transposition table; merged == every record counted,
+    per root."""
+    import os
+
+    from gym_chess_amd.engine import perft_dedup_stats
+
+    b, m = _midgame_roots(4096, 21, 0x5EED + 6)
+    r0, c0 = perft_dedup_stats()
+    merged = engine.perft(b, m, 5)
+    r1, c1 = perft_dedup_stats()
+    os.environ["GC_PERFT_DEDUP"] = "0"
+    try:
+        every = engine.perft(b, m, 5)
+    finally:
+        del os.environ["GC_PERFT_DEDUP"]
+    assert (merged == every).all(), np.nonzero(merged != every)[0][:4]
+    assert r1 - r0 > 2 ** 21 * 20 and c1 - c0 < 0.8 * (r1 - r0)
+
+
 def _midgame_roots(n, plies, seed):
     from gym_chess_amd.env import BatchedChessEnv
 
