@@ -216,14 +216,14 @@ def perft_leg(args, rep):
     # position occurs under; GC_PERFT_DEDUP=0 counts every record
     gather = bool(os.environ.get("GC_PERFT_GATHER"))
     dedup = not gather and os.environ.get("GC_PERFT_DEDUP", "1") != "0"
-    alg_sub = 76 if gather else (84 if dedup else 72)  # + the 4-B leader index and the 8-B count kept
+    alg_sub = 76 if gather else (80 if dedup else 72)  # + the 8-B count kept for the followers
     la, sub, kms = (b - a for a, b in zip(leaf0, leaf1))
     recs, counted = (b - a for a, b in zip(dd0, dd1))
     if recs:
         out["transpositions"] = {"records": recs, "counted": counted, "records_per_counted": recs / max(1, counted),
                                  "merged": dedup}
     if la:
-        kname = "k_perft2_perm_rec" if gather else ("k_perft2_lead" if dedup else "k_perft2_rec")
+        kname = "k_perft2_perm_rec" if gather else ("k_perft2_val" if dedup else "k_perft2_rec")
         roof = {"bound": "valu", "kernel": kname, "launches": la,
                 "subtrees": sub, "kernel_ms": kms, "share_of_perft_time": kms / 1e3 / len(rep.local) / dtm,
                 "alg_bytes_per_subtree": alg_sub, "hbm_achieved_gbs": alg_sub * sub / (kms / 1e3) / 1e9}

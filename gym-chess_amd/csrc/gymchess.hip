@@ -624,12 +624,19 @@ k_perft2_rec(const Node64* __restrict__ in, int n, unsigned long long* __restric
 // Transpositions among the depth-2 roots (round 4): a chunk's ply-3 records repeat -- m1, x,
 // m3 and m3, x, m1 reach one position -- ~1.7 records per distinct position over mid-game
 // roots.  perft2 is a function of the Pos alone, so one record per position (its leader) is
-// counted and the others (followers) add the leader's count into their own parents.
-// k_dedup: every record claims a slot of an open-addressed table keyed by a hash of its Pos
-// (entry = hash tag << 32 | record index, 0 = empty); a hash match is confirmed by comparing
-// the two whole records (written by k_expand_place, the previous launch), so a merge is exact.
-// Leaders are flagged for the order-keeping compaction (the leaf kernel still reads them in
-// move-count order); followers append (parent, leader) to a list, one atomic per wave.
+// counted and the others (followers) add the leader's count into their own parents.  With
+// the merge the chunk's records are written in expansion order (k_expand_range_rec) and:
+//   k_dedup_bin   every record claims a slot of an open-addressed table keyed by a hash of its
+//                 Pos (entry = hash tag << 32 | record index, 0 = empty) by one CAS; a tag
+//                 match is confirmed by comparing the two whole records, so a merge is exact.
+//                 A leader's move count (the leaf's lane-balancing bin) is computed here, for
+//                 leaders only, while the other waves wait on their CASes; per-block leader
+//                 histograms; followers append (parent, leader) pairs, one atomic per wave;
+//   k_place_leaders  the leaders copied into move-count order (the scanned histograms'
+//                 cursors), each one's placed index kept;
+//   k_perft2_val  the leaf over the placed leaders (dense, in order), each count kept;
+//   k_followers   each follower adds its leader's count into its own parent.
+#define DEDUP_BLOCK 1024
 __device__ __forceinline__ u64 pos_hash(const Pos& s) {
     u64 h = s.meta * 0x9E3779B97F4A7C15ull;
     const u64 f[7] = {s.k, s.q, s.r, s.b, s.n, s.p, s.w};
@@ -644,9 +651,13 @@ __device__ __forceinline__ bool pos_equal(const Pos& a, const Pos& b) {
     return ((a.k ^ b.k) | (a.q ^ b.q) | (a.r ^ b.r) | (a.b ^ b.b) | (a.n ^ b.n) | (a.p ^ b.p) | (a.w ^ b.w)) == 0 &&
            a.meta == b.meta;
 }
-__global__ void __launch_bounds__(BLOCK) k_dedup(const Node64* __restrict__ in, int n, u64* __restrict__ table,
-                                                 u32 mask, uint8_t* __restrict__ leader, u32* __restrict__ nfol,
-                                                 uint2* __restrict__ fol) {
+__global__ void __launch_bounds__(DEDUP_BLOCK) k_dedup_bin(const Node64* __restrict__ in, int n, u64* __restrict__ table,
+                                                           u32 mask, uint8_t* __restrict__ bins,
+                                                           uint8_t* __restrict__ lflag, u32* __restrict__ hist, int nblk,
+                                                           u32* __restrict__ nfol, uint2* __restrict__ fol) {
+    __shared__ u32 hb[SPLIT_BINS];
+    for (int b = threadIdx.x; b < SPLIT_BINS; b += blockDim.x) hb[b] = 0;
+    __syncthreads();
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     bool follower = false;
     u32 lead = 0, parent = 0;
@@ -657,7 +668,7 @@ __global__ void __launch_bounds__(BLOCK) k_dedup(const Node64* __restrict__ in, 
         const u64 tag = (h >> 32) | 1u;
         const u64 mine = (tag << 32) | (u32)i;
         u32 slot = (u32)h & mask;
-        for (;;) {  // (a relaxed load ahead of the CAS: 11.4 ms per chunk; the CAS alone: see DESIGN §5)
+        for (;;) {  // (a relaxed load ahead of the CAS measured the same)
             const u64 e = atomicCAS(reinterpret_cast<unsigned long long*>(table + slot), 0ull, (unsigned long long)mine);
             if (e == 0) break;  // this record leads its position
             if ((e >> 32) == tag && pos_equal(node_load(in, (u32)e), s)) {
@@ -667,38 +678,62 @@ __global__ void __launch_bounds__(BLOCK) k_dedup(const Node64* __restrict__ in, 
             }
             slot = (slot + 1) & mask;
         }
-        leader[i] = follower ? 0 : 1;
+        lflag[i] = follower ? 0 : 1;
+        if (!follower) {
+            const int b = split_bin(s, king_lines_of(s, (s.meta & M_WHITE) != 0));
+            bins[i] = (uint8_t)b;
+            atomicAdd(&hb[b], 1u);
+        }
     }
-    // wave-aggregated append of the followers
-    const u64 bal = __ballot(follower);
-    if (bal == 0) return;
-    const int lane = threadIdx.x & 63;
-    const int first = __ffsll((long long)bal) - 1;
-    u32 base = 0;
-    if (lane == first) base = atomicAdd(nfol, (u32)__popcll(bal));
-    base = __shfl(base, first);
-    if (follower) fol[base + __popcll(bal & ((1ull << lane) - 1))] = make_uint2(parent, lead);
+    const u64 bal = __ballot(follower);  // wave-aggregated append of the followers
+    if (bal) {
+        const int lane = threadIdx.x & 63;
+        const int first = __ffsll((long long)bal) - 1;
+        u32 base = 0;
+        if (lane == first) base = atomicAdd(nfol, (u32)__popcll(bal));
+        base = __shfl(base, first);
+        if (follower) fol[base + __popcll(bal & ((1ull << lane) - 1))] = make_uint2(parent, lead);
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < SPLIT_BINS; b += blockDim.x) hist[(size_t)b * nblk + blockIdx.x] = hb[b];
 }
-// the leaders (compacted, in record order) counted; their counts kept for the followers
+__global__ void __launch_bounds__(DEDUP_BLOCK) k_place_leaders(const Node64* __restrict__ in, int n,
+                                                               const uint8_t* __restrict__ bins,
+                                                               const uint8_t* __restrict__ lflag,
+                                                               const u32* __restrict__ base, int nblk,
+                                                               Node64* __restrict__ out, int32_t* __restrict__ place_of) {
+    __shared__ u32 cur[SPLIT_BINS];
+    for (int b = threadIdx.x; b < SPLIT_BINS; b += blockDim.x) cur[b] = base[(size_t)b * nblk + blockIdx.x];
+    __syncthreads();
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || !lflag[i]) return;
+    const u32 slot = atomicAdd(&cur[bins[i]], 1u);
+    const ulonglong2* x = reinterpret_cast<const ulonglong2*>(in + i);
+    ulonglong2* y = reinterpret_cast<ulonglong2*>(out + slot);
+    const ulonglong2 r0 = x[0], r1 = x[1], r2 = x[2], r3 = x[3];
+    y[0] = r0; y[1] = r1; y[2] = r2; y[3] = r3;
+    place_of[i] = (int32_t)slot;
+}
+// one lane = one placed leader (move-count order); its count kept for the followers
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(PERFT2_WPE)))
-k_perft2_lead(const Node64* __restrict__ in, const int32_t* __restrict__ idx, int n, uint64_t* __restrict__ val,
-              unsigned long long* __restrict__ parent_sum) {
+k_perft2_val(const Node64* __restrict__ in, int n, uint64_t* __restrict__ val,
+             unsigned long long* __restrict__ parent_sum) {
     __shared__ u64 lds_a[SCRATCH_SLOTS * BLOCK];
     LdsScratch sa{lds_a + threadIdx.x};
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const int j = idx[i];
-    const u32 parent = reinterpret_cast<const u32*>(in + j)[15];
-    const uint64_t c = perft2(node_load(in, j), sa);
-    val[j] = c;
+    const u32 parent = reinterpret_cast<const u32*>(in + i)[15];
+    const uint64_t c = perft2(node_load(in, i), sa);
+    val[i] = c;
     atomicAdd(parent_sum + parent, (unsigned long long)c);
 }
 __global__ void k_followers(const uint2* __restrict__ fol, const u32* __restrict__ nfol,
-                            const uint64_t* __restrict__ val, unsigned long long* __restrict__ parent_sum) {
+                            const int32_t* __restrict__ place_of, const uint64_t* __restrict__ val,
+                            unsigned long long* __restrict__ parent_sum) {
     const u32 n = *nfol;
     for (u32 i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const uint2 f = fol[i];
-        atomicAdd(parent_sum + f.x, (unsigned long long)val[f.y]);
+        atomicAdd(parent_sum + f.x, (unsigned long long)val[place_of[f.y]]);
     }
 }
 
@@ -4027,44 +4062,43 @@ static int perft_split_leaves(hipStream_t st, SoA leaf, uint64_t* leaf_out) {
     uint8_t* bins = nullptr;
     u32 *hist = nullptr, *hbase = nullptr;
     const int max_blk = (chunk + BLOCK - 1) / BLOCK;
+    const int max_dblk = (int)((cap + DEDUP_BLOCK - 1) / DEDUP_BLOCK);  // k_dedup_bin's blocks
+    const int hist_n = SPLIT_BINS * (dedup && max_dblk > max_blk ? max_dblk : max_blk);
     Node64* cr = nullptr;
-    // the transposition pass (k_dedup): table of 2x the chunk's records, leader indices,
-    // follower (parent, leader) pairs, the leaders' counts, the two list sizes
+    // the transposition pass: the records in expansion order, the table (2x the chunk's
+    // records), leader flags, placed index per record, follower (parent, leader) pairs, the
+    // placed leaders' counts, the follower count
+    Node64* cre = nullptr;
     u64* table = nullptr;
-    int32_t* lidx = nullptr;
+    uint8_t* lflag = nullptr;
+    int32_t* place_of = nullptr;
     uint2* fol = nullptr;
     uint64_t* val = nullptr;
-    u32* nsel = nullptr;  // [0] leaders, [1] followers
+    u32* nfol = nullptr;
     void* tmp = nullptr;
     size_t tmp_bytes = 0;
     int rc = 0;
     std::string err;
     auto done = [&]() {
-        void* ps[] = {kc, offs, kc2, ks, ix, is, cr, tmp, bins, hist, hbase, table, lidx, fol, val, nsel};
+        void* ps[] = {kc, offs, kc2, ks, ix, is, cr, tmp, bins, hist, hbase, cre, table, lflag, place_of, fol, val, nfol};
         for (void* q : ps) (void)hipFree(q);
         for (hipEvent_t ev : evs) (void)hipEventDestroy(ev);
     };
     if (dalloc(&kc, leaf.n) || dalloc(&offs, chunk) || dalloc(&cr, cap) ||
         (gather ? (dalloc(&kc2, cap) || dalloc(&ks, cap) || dalloc(&ix, cap) || dalloc(&is, cap))
-                : (dalloc(&bins, cap) || dalloc(&hist, (size_t)SPLIT_BINS * max_blk) ||
-                   dalloc(&hbase, (size_t)SPLIT_BINS * max_blk))) ||
-        (dedup && (dalloc(&table, 2 * cap) || dalloc(&lidx, cap) || dalloc(&fol, cap) || dalloc(&val, cap) ||
-                   dalloc(&nsel, 2)))) {
+                : (dalloc(&bins, cap) || dalloc(&hist, (size_t)hist_n) || dalloc(&hbase, (size_t)hist_n))) ||
+        (dedup && (dalloc(&cre, cap) || dalloc(&table, 2 * cap) || dalloc(&lflag, cap) || dalloc(&place_of, cap) ||
+                   dalloc(&fol, cap) || dalloc(&val, cap) || dalloc(&nfol, 1)))) {
         done();
         return -1;
     }
     {  // scratch for the largest scan and sort of a chunk
-        size_t b1 = 0, b2 = 0, b3 = 0;
+        size_t b1 = 0, b2 = 0;
         hipError_t he = hipcub::DeviceScan::ExclusiveSum(nullptr, b1, kc, offs, chunk, st);
         if (he == hipSuccess && gather)
             he = hipcub::DeviceRadixSort::SortPairs(nullptr, b2, kc2, ks, ix, is, (int)cap, 0, 10, st);
-        if (he == hipSuccess && !gather)
-            he = hipcub::DeviceScan::ExclusiveSum(nullptr, b2, hist, hbase, SPLIT_BINS * max_blk, st);
-        if (he == hipSuccess && dedup)
-            he = hipcub::DeviceSelect::Flagged(nullptr, b3, hipcub::CountingInputIterator<int32_t>(0), bins, lidx,
-                                               nsel, (int64_t)cap, st);
+        if (he == hipSuccess && !gather) he = hipcub::DeviceScan::ExclusiveSum(nullptr, b2, hist, hbase, hist_n, st);
         tmp_bytes = b1 > b2 ? b1 : b2;
-        tmp_bytes = tmp_bytes > b3 ? tmp_bytes : b3;
         if (he != hipSuccess) { done(); return fail(std::string("perft split: ") + hipGetErrorString(he)); }
         if (dalloc((char**)&tmp, tmp_bytes)) { done(); return -1; }
     }
@@ -4082,43 +4116,52 @@ static int perft_split_leaves(hipStream_t st, SoA leaf, uint64_t* leaf_out) {
         if (total > cap) { chunk /= 2; continue; }  // an unusually bushy chunk: halve and retry
         he = hipMemsetAsync(leaf_out + a, 0, (size_t)8 * c, st);  // the parents' sums
         if (he != hipSuccess) { err = std::string("perft split: ") + hipGetErrorString(he); rc = -1; break; }
-        if (total > 0 && !gather) {  // the records in move-count order, then read in order
+        unsigned long long* psum = reinterpret_cast<unsigned long long*>(leaf_out + a);
+        if (total > 0 && dedup) {  // transpositions merged, the leaders binned and placed in order
+            const int n = (int)total;
+            const int nbd = (n + DEDUP_BLOCK - 1) / DEDUP_BLOCK;
+            u32 tsize = 2;
+            while ((int64_t)tsize < 2 * total) tsize <<= 1;
+            k_expand_range_rec<<<grid_for(c), BLOCK, 0, st>>>(leaf, a, c, offs, cre);
+            he = hipMemsetAsync(table, 0, (size_t)8 * tsize, st);
+            if (he == hipSuccess) he = hipMemsetAsync(nfol, 0, 4, st);
+            if (he == hipSuccess)
+                k_dedup_bin<<<nbd, DEDUP_BLOCK, 0, st>>>(cre, n, table, tsize - 1, bins, lflag, hist, nbd, nfol, fol);
+            tb = tmp_bytes;
+            if (he == hipSuccess) he = hipcub::DeviceScan::ExclusiveSum(tmp, tb, hist, hbase, SPLIT_BINS * nbd, st);
+            u32 hb = 0, hl = 0;  // the leaders: the last bin's base + its last block's count
+            const size_t last = (size_t)SPLIT_BINS * nbd - 1;
+            if (he == hipSuccess) he = hipMemcpyAsync(&hb, hbase + last, 4, hipMemcpyDeviceToHost, st);
+            if (he == hipSuccess) he = hipMemcpyAsync(&hl, hist + last, 4, hipMemcpyDeviceToHost, st);
+            if (he == hipSuccess)
+                k_place_leaders<<<nbd, DEDUP_BLOCK, 0, st>>>(cre, n, bins, lflag, hbase, nbd, cr, place_of);
+            if (he == hipSuccess) he = hipStreamSynchronize(st);  // the leaf grid sized to the leaders
+            if (he != hipSuccess) { err = std::string("perft split dedup: ") + hipGetErrorString(he); rc = -1; break; }
+            const int lead_n = (int)(hb + hl);
+            hipEvent_t e0 = nullptr, e1 = nullptr;
+            if (hipEventCreate(&e0) == hipSuccess) evs.push_back(e0);
+            if (hipEventCreate(&e1) == hipSuccess) evs.push_back(e1);
+            if (e0 && e1) (void)hipEventRecord(e0, st);
+            k_perft2_val<<<grid_for(lead_n), BLOCK, 0, st>>>(cr, lead_n, val, psum);
+            if (e0 && e1) (void)hipEventRecord(e1, st);
+            k_followers<<<2048, BLOCK, 0, st>>>(fol, nfol, place_of, val, psum);
+            records += (uint64_t)total;
+            subtrees += (uint64_t)lead_n;
+        } else if (total > 0 && !gather) {  // the records in move-count order, then read in order
             const int nb = grid_for(c);
             k_expand_count<<<nb, BLOCK, 0, st>>>(leaf, a, c, bins, offs, hist, nb);
             tb = tmp_bytes;
             he = hipcub::DeviceScan::ExclusiveSum(tmp, tb, hist, hbase, SPLIT_BINS * nb, st);
             if (he != hipSuccess) { err = std::string("perft split scan: ") + hipGetErrorString(he); rc = -1; break; }
             k_expand_place<<<nb, BLOCK, 0, st>>>(leaf, a, c, bins, offs, hbase, nb, cr);
-            unsigned long long* psum = reinterpret_cast<unsigned long long*>(leaf_out + a);
-            int lead_n = 0;
-            u32 tsize = 2;
-            while ((int64_t)tsize < 2 * total) tsize <<= 1;
-            if (dedup) {  // bins (the records' move counts, placed) are free again: the leader flags
-                he = hipMemsetAsync(table, 0, (size_t)8 * tsize, st);
-                if (he == hipSuccess) he = hipMemsetAsync(nsel, 0, 8, st);
-                if (he == hipSuccess)
-                    k_dedup<<<grid_for((int)total), BLOCK, 0, st>>>(cr, (int)total, table, tsize - 1, bins, nsel + 1,
-                                                                    fol);
-                tb = tmp_bytes;
-                if (he == hipSuccess)
-                    he = hipcub::DeviceSelect::Flagged(tmp, tb, hipcub::CountingInputIterator<int32_t>(0), bins, lidx,
-                                                       nsel, (int64_t)total, st);
-                u32 nl = 0;  // the leaf grid sized to the leaders (one round trip per chunk)
-                if (he == hipSuccess) he = hipMemcpyAsync(&nl, nsel, 4, hipMemcpyDeviceToHost, st);
-                if (he == hipSuccess) he = hipStreamSynchronize(st);
-                if (he != hipSuccess) { err = std::string("perft split dedup: ") + hipGetErrorString(he); rc = -1; break; }
-                lead_n = (int)nl;
-            }
             hipEvent_t e0 = nullptr, e1 = nullptr;
             if (hipEventCreate(&e0) == hipSuccess) evs.push_back(e0);
             if (hipEventCreate(&e1) == hipSuccess) evs.push_back(e1);
             if (e0 && e1) (void)hipEventRecord(e0, st);
-            if (dedup) k_perft2_lead<<<grid_for(lead_n), BLOCK, 0, st>>>(cr, lidx, lead_n, val, psum);
-            else k_perft2_rec<<<grid_for((int)total), BLOCK, 0, st>>>(cr, (int)total, psum);
+            k_perft2_rec<<<grid_for((int)total), BLOCK, 0, st>>>(cr, (int)total, psum);
             if (e0 && e1) (void)hipEventRecord(e1, st);
-            if (dedup) k_followers<<<2048, BLOCK, 0, st>>>(fol, nsel + 1, val, psum);
             records += (uint64_t)total;
-            subtrees += (uint64_t)(dedup ? lead_n : total);
+            subtrees += (uint64_t)total;
         } else if (total > 0) {
             k_expand_range_rec<<<grid_for(c), BLOCK, 0, st>>>(leaf, a, c, offs, cr);
             k_count_children_rec<<<grid_for((int)total), BLOCK, 0, st>>>(cr, (int)total, kc2);

@@ -70,7 +70,7 @@ int gc_engine_perft(gc_engine* e, int n, const int8_t* boards, const uint8_t* me
  * (depth-3 subtrees split to depth-2, sorted), sorted (subtrees by move count), small
  * (unsorted nested loops), fide} */
 int gc_perft_path_counts(uint64_t* out4);
-/* diagnostics: the split pass's leaf kernel (k_perft2_rec / k_perft2_lead, one lane = one
+/* diagnostics: the split pass's leaf kernel (k_perft2_rec / k_perft2_val, one lane = one
  * depth-2 subtree) in this process -- launches, subtrees counted and summed kernel time (HIP
  * events on its stream) */
 int gc_perft_leaf_stats(uint64_t* launches, uint64_t* subtrees, double* kernel_ms);

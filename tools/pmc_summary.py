@@ -36,7 +36,7 @@ def main():
                     help="perft leaf kernel (k_perft2_rec) passes pmc_perft_{fetch,write,mix} -> pmc_perft.json")
     ap.add_argument("--rollout", action="store_true",
                     help="the headline kernel (last dispatch of --rollout-kernel) passes pmc_roll_* -> pmc_rollout.json")
-    ap.add_argument("--perft-kernel", default="k_perft2_lead",
+    ap.add_argument("--perft-kernel", default="k_perft2_val",
                     help="the split leaf kernel (k_perft2_rec: GC_PERFT_DEDUP=0, k_perft2_perm_rec: GC_PERFT_GATHER)")
     ap.add_argument("--rollout-kernel", default="k_env_rollout4",
                     help="the fused rollout's kernel: k_env_rollout4 (quads), k_env_rollout2<false, 0> (pairs)")
@@ -205,12 +205,12 @@ def bench_line(path):
 
 
 def perft_summary(a):
-    """k_perft2_lead (the split leaf pass: one lane = one distinct depth-2 subtree, bulk-counted
+    """k_perft2_val (the split leaf pass: one lane = one distinct depth-2 subtree, bulk-counted
     last ply) over the bench's perft leg.  Per launch: HBM bytes (FETCH_SIZE x2 + WRITE_SIZE),
     VALU instructions per wave, lane utilisation, VALU busy fraction.  Algorithmic bytes per
     subtree: the root's 64-byte record (7 bitboards + meta, read in order) + its count (8) added
-    into the parent's sum = 72 B, + the 4-B leader index and the 8-B count kept for the merged
-    records = 84 B; the leaves never touch memory.  (--perft-kernel k_perft2_rec: every record counted, 72 B;
+    into the parent's sum = 72 B, + the 8-B count kept for the followers = 80 B; the leaves
+    never touch memory.  (--perft-kernel k_perft2_rec: every record counted, 72 B;
     k_perft2_perm_rec: the earlier gathering form, + a 4-B permutation index.)"""
     kern = a.perft_kernel
     rows = lambda sub: per_dispatch(os.path.join(a.src, sub, "run_counter_collection.csv"), kern)  # noqa: E731
@@ -220,7 +220,7 @@ def perft_summary(a):
     out = {"kernel": kern, "launches": len(m),
            "hbm_bytes_total": tot(f, "FETCH_SIZE") * 1024 * 2 + tot(w, "WRITE_SIZE") * 1024,
            "subtrees_total": waves * 64,
-           "alg_bytes_per_subtree": 76 if "perm" in kern else (84 if "lead" in kern else 72),
+           "alg_bytes_per_subtree": 76 if "perm" in kern else (80 if "val" in kern else 72),
            "valu": {"insts_per_wave": tot(m, "SQ_INSTS_VALU") / waves,
                     "lane_utilisation": tot(m, "SQ_THREAD_CYCLES_VALU") / (tot(m, "SQ_ACTIVE_INST_VALU") * 64),
                     "wait_any_share": tot(m, "SQ_WAIT_ANY") / tot(m, "SQ_WAVE_CYCLES")},
