@@ -206,14 +206,15 @@ def perft_leg(args, rep):
            "nodes": tot, "seconds": dtm,
            "leaf_pass": {k: paths1[k] - paths0[k] for k in paths0},
            "roots_with": {"castle_right": castle, "pawn_on_7th": prom, "side_in_check": check}}
-    # the leaf kernel (k_perft2_rec: one lane = one depth-2 subtree, read in order, last ply
-    # bulk-counted): where the time goes.  It is VALU-bound -- 72 algorithmic HBM bytes per
-    # subtree (the 64-B root record in, its count added into the parent's sum) against ~1e3
-    # leaves -- so its roof is the VALU issue rate (PMC profile, tools/gpu_run.sh pmcp*).
-    # GC_PERFT_GATHER: the earlier form, gathering through a sorted permutation (+ 4 B index)
-    # Transpositions (round 4): the split pass counts one depth-2 subtree per distinct position
-    # of a chunk (k_dedup, exact: whole-record compare) and adds that count to every parent the
-    # position occurs under; GC_PERFT_DEDUP=0 counts every record
+    # the leaf kernel (k_perft2_val: one lane = one distinct depth-2 subtree, read in order,
+    # last ply bulk-counted): where the time goes.  It is VALU-bound -- 80 algorithmic HBM bytes
+    # per subtree (the 64-B root record in, its count kept and added into the parent's sum)
+    # against ~1e3 leaves -- so its roof is the VALU issue rate (PMC profile, tools/gpu_run.sh
+    # pmcp*).  Transpositions (round 4): the split pass counts one depth-2 subtree per distinct
+    # position of a chunk (k_dedup_bin, exact: whole-record compare) and adds that count to
+    # every parent the position occurs under; GC_PERFT_DEDUP=0 counts every record
+    # (k_perft2_rec, 72 B); GC_PERFT_GATHER: the round-2/3 form, gathering through a sorted
+    # permutation (+ 4 B index)
     gather = bool(os.environ.get("GC_PERFT_GATHER"))
     dedup = not gather and os.environ.get("GC_PERFT_DEDUP", "1") != "0"
     alg_sub = 76 if gather else (80 if dedup else 72)  # + the 8-B count kept for the followers

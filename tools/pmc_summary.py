@@ -33,7 +33,7 @@ def main():
     ap.add_argument("--dispatches-per-ply", type=int, default=1,
                     help="dispatches of the kernel per ply (bench.py's board-range streams, GC_STREAMS)")
     ap.add_argument("--perft", action="store_true",
-                    help="perft leaf kernel (k_perft2_rec) passes pmc_perft_{fetch,write,mix} -> pmc_perft.json")
+                    help="perft leaf kernel (--perft-kernel) passes pmc_perft_{fetch,write,mix} -> pmc_perft.json")
     ap.add_argument("--rollout", action="store_true",
                     help="the headline kernel (last dispatch of --rollout-kernel) passes pmc_roll_* -> pmc_rollout.json")
     ap.add_argument("--perft-kernel", default="k_perft2_val",
