@@ -586,12 +586,19 @@ GC_HD u64 pseudo_targets(const Pos& s, const Gen& g, int sq, int t) {
     }
 }
 
+// the squares on sq's side of the king ks (on any line through both): a pinned piece stays on
+// its own pin segment.  pinrays is the union of every pinner's segment, and two pins can share
+// a line (a rook behind the king, a queen in front); only a pawn's Q1 double push can cross its
+// king -- onto the other pin's segment, where the move exposes the king (found by a 20 000-ply
+// soak against the oracle, tools/soak.py)
+GC_HD u64 king_side(int ks, int sq) { return sq > ks ? (ks >= 63 ? 0ull : ~below(ks + 1)) : below(ks); }
+
 GC_HD u64 legal_targets(const Pos& s, const Gen& g, int sq, int t) {
     if (t == KING) return king_set(bit(sq)) & ~g.own & ~g.enemy_att;
     u64 tg = pseudo_targets(s, g, sq, t);
     if (g.ks < 0) return tg;
     tg &= g.checkmask;
-    if (g.pinned & bit(sq)) tg &= g.pinrays & line_through(g.ks, sq);
+    if (g.pinned & bit(sq)) tg &= g.pinrays & line_through(g.ks, sq) & king_side(g.ks, sq);
     return tg;
 }
 
@@ -953,14 +960,19 @@ GC_HD void sw_pawns_kl(const Pos& s, const Gen& g, const KingLines& kl, u64* t) 
     const u64 cm = g.checkmask, empty = ~g.occ, opp = g.opp, P = s.p & g.own, pr = g.pinrays;
     const u64 fp = P & ~g.pinned, pp = P & g.pinned;
     const u64 pf = pp & kl.fm(), pd = pp & kl.dm, pa = pp & kl.am;
+    // a file-pinned pawn's double push stays on its side of the king (king_side: it can jump it)
+    const int ks = sw_ksq(g);
+    const u64 hk = ks >= 63 ? 0ull : ~below(ks + 1), lk = below(ks);
     if (g.white) {  // lib.rs:935-958, p = +1: toward row 0
+        const u64 pf2 = ((((pf & hk) & ROW6) >> 16) & hk) | ((((pf & lk) & ROW6) >> 16) & lk);
         t[SW_P1] = and3(and_or(pf >> 8, pr, fp >> 8), empty, cm);
-        t[SW_P2] = and3(and_or((pf & ROW6) >> 16, pr, (fp & ROW6) >> 16), empty, cm);
+        t[SW_P2] = and3(and_or(pf2, pr, (fp & ROW6) >> 16), empty, cm);
         t[SW_PL] = and3(and_or(pa >> 7, pr, fp >> 7), opp & ~FILE_A, cm);  // row-1 col+1: anti-diagonal
         t[SW_PR] = and3(and_or(pd >> 9, pr, fp >> 9), opp & ~FILE_H, cm);  // row-1 col-1: diagonal
     } else {
+        const u64 pf2 = ((((pf & hk) & ROW1) << 16) & hk) | ((((pf & lk) & ROW1) << 16) & lk);
         t[SW_P1] = and3(and_or(pf << 8, pr, fp << 8), empty, cm);
-        t[SW_P2] = and3(and_or((pf & ROW1) << 16, pr, (fp & ROW1) << 16), empty, cm);
+        t[SW_P2] = and3(and_or(pf2, pr, (fp & ROW1) << 16), empty, cm);
         t[SW_PL] = and3(and_or(pd << 9, pr, fp << 9), opp & ~FILE_A, cm);  // row+1 col+1: diagonal
         t[SW_PR] = and3(and_or(pa << 7, pr, fp << 7), opp & ~FILE_H, cm);  // row+1 col-1: anti-diagonal
     }

@@ -269,3 +269,54 @@ def test_pin_forms_agree(seed):
     for i in range(len(boards)):
         for white in (0, 1):
             assert L.host_pins_agree(boards[i].ctypes.data, metas[i].ctypes.data, white) == 1, (i, white)
+
+
+# Two pins on one line through the king -- a rook behind it pinning one pawn, a queen in front
+# pinning another -- and the rear pawn's Q1 double push jumps the king onto the FRONT pin's
+# segment (pinrays is the union of the segments).  The reference's legality filter rejects the
+# move (the rook then checks the king); found at ply 4 591 of board 65 486, seed 1000, by the
+# 20 000-ply soak (tools/soak.py).
+TWO_PINS = (
+    "..b.kb.."
+    "..p..qp."
+    "n.np...r"
+    ".pP.pP.p"
+    "Pp..N..."
+    "..B..K.."
+    ".....P.R"
+    ".....rN."
+)
+
+
+def _two_pins_position(mirror=False):
+    from gym_chess_amd import codec as C
+
+    b = C.text_to_board(TWO_PINS)
+    m = np.zeros(8, dtype=np.uint8)
+    m[0], m[3], m[4] = 1, 1, 1
+    if mirror:  # colours swapped and the board flipped: black's pawn jumps its king
+        b = -b.reshape(8, 8)[::-1].reshape(64)
+        m[0], m[1], m[2], m[3], m[4] = 0, 1, 1, 0, 0
+    return b.astype(np.int8), m
+
+
+@pytest.mark.parametrize("mirror", [False, True])
+def test_pinned_pawn_double_push_never_crosses_its_king(oracle, mirror):
+    b, m = _two_pins_position(mirror)
+    w = int(m[0])
+    ref = oracle.get_possible_moves(b, m, w)
+    assert H.get_list(b, m, w) == ref
+    assert H.count(b, m, w) == len(ref) == H.count2(b, m, w)
+    jump = (53 * 64 + 37) if not mirror else (13 * 64 + 29)  # f2-f4 / f7-f5 over the king
+    assert jump not in ref and not H.action_legal(b, m, w, jump)
+    for d in (1, 2, 3):
+        assert H.perft(b, m, d) == oracle.perft(b, m, d)
+
+
+def test_soak_board_65486_trajectory(oracle):
+    from gym_chess_amd import codec as C
+
+    init = np.array(C.DEFAULT_BOARD, np.int8).reshape(64)
+    o = oracle.rollout_trace(1000, 65486, 4600)
+    h = H.rollout_trace(1000, 65486, 4600, init)
+    assert (o["action"] == h["action"]).all() and (o["final_board"] == h["final_board"]).all()

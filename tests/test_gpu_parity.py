@@ -149,6 +149,41 @@ def test_one_position_calls_from_two_threads(engine, oracle):
     assert not errors, errors[:8]
 
 
+@pytest.mark.parametrize("mirror", [False, True])
+def test_two_pins_double_push_never_crosses_its_king(engine, oracle, mirror):
+    """Two pins on the king's file (rook behind, queen in front): the rear pawn's Q1 double push
+    must not jump the king onto the front pin's segment (tests/test_core_host.py TWO_PINS; the
+    soak's board 65 486): lists one at a time and batched, perft, the policy's pick."""
+    from test_core_host import _two_pins_position
+
+    b, m = _two_pins_position(mirror)
+    w = int(m[0])
+    ref = oracle.get_possible_moves(b, m, w)
+    out, cnt = engine.possible_moves(b[None], m[None], w)
+    assert [int(x) for x in out[0, : cnt[0]]] == ref
+    bb, mm = np.repeat(b[None], 300, axis=0), np.repeat(m[None], 300, axis=0)
+    out, cnt = engine.possible_moves(bb, mm, w)
+    assert all([int(x) for x in out[i, : cnt[i]]] == ref for i in range(300))
+    assert (engine.perft(bb[:2], mm[:2], 3) == oracle.perft(b, m, 3)).all()
+
+
+def test_two_pins_soak_board_65486_fused_vs_oracle(oracle):
+    """The soak's failing trajectory (seed 1000, board 65 486, the divergence at ply 4 591)
+    through the headline kernel: every ply of that board == the oracle's."""
+    from gym_chess_amd.env import BatchedChessEnv
+
+    env = BatchedChessEnv(65536, device=0, seed=1000)
+    tb = env.trace_buffer(4600)
+    env.rollout_device(4600, tb)
+    env.synchronize()
+    tr = tb.fetch()
+    ref = oracle.rollout_trace(1000, 65486, 4600)
+    for key in ("action", "reward", "done", "reason"):
+        assert (tr[key][:, 65486] == ref[key]).all(), key
+    tb.close()
+    env.close()
+
+
 def test_next_state_every_legal_move(engine, oracle):
     boards, metas = random_positions(150, 21)
     B, M, P, A = [], [], [], []

@@ -1,0 +1,78 @@
+"""Diagnostic soak (not in the test suite: minutes of GPU time): long full-size fused
+rollouts against the oracle on sampled boards, for several seeds and opponent modes.
+
+Each case: 65 536 boards, `--plies` plies of the device random self-play as fused launches of
+`--chunk` plies with the per-ply trace; every ply's action / reward / done / reason of the
+sampled boards (strided + the first / last 64 + the middle) == the oracle driver's, and the
+sampled final states.  Long games reach the move cap, deep 3-fold windows and (BLACK agent)
+the spill table.
+
+    python tools/soak.py [--plies 4000] [--chunk 1000] [--seeds 5]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "gym-chess_amd"), os.path.join(ROOT, "oracle")]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--plies", type=int, default=4000)
+    ap.add_argument("--chunk", type=int, default=1000)
+    ap.add_argument("--seeds", type=int, default=5)
+    ap.add_argument("--boards", type=int, default=65536)
+    a = ap.parse_args()
+    import oracle as O
+    from gym_chess_amd.env import BatchedChessEnv
+
+    n = a.boards
+    idx = np.array(sorted(set(range(0, n, 1021)) | set(range(64)) | set(range(n - 64, n)) |
+                          set(range(n // 2 - 16, n // 2 + 16))), dtype=np.int64)
+    threads = max(1, min(16, os.cpu_count() or 1))
+    cases = [(1000 + 7919 * k, "none", "WHITE") for k in range(a.seeds)]
+    cases += [(424242, "random", "WHITE"), (434343, "random", "BLACK")]
+    for seed, opp, color in cases:
+        t0 = time.time()
+        env = BatchedChessEnv(n, device=0, seed=seed, opponent=opp, player_color=color)
+        tb = env.trace_buffer(a.chunk)
+        got = {k: [] for k in ("action", "reward", "done", "reason")}
+        for p in range(0, a.plies, a.chunk):
+            k = min(a.chunk, a.plies - p)
+            env.rollout_device(k, tb)
+            env.synchronize()
+            tr = tb.fetch(k)
+            for key in got:
+                got[key].append(tr[key][:, idx])
+        b, m = env.boards()
+        spill = env.spill_info() if color == "BLACK" else None
+        tb.close()
+        env.close()
+        kw = dict(opponent=1 if opp == "random" else 0, agent_white=color == "WHITE")
+        with ThreadPoolExecutor(threads) as ex:
+            refs = list(ex.map(lambda i: O.rollout_trace(seed, int(i), a.plies, **kw), idx))
+        bad = []
+        for key in got:
+            g = np.concatenate(got[key], axis=0)
+            w = np.stack([r[key][: a.plies] for r in refs], axis=1)
+            for p_, j in np.argwhere(g != w)[:4]:
+                bad.append((key, int(p_), int(idx[j])))
+        for j, i in enumerate(idx):
+            if not ((b[i] == refs[j]["final_board"]).all() and list(m[i]) == list(refs[j]["final_meta"])):
+                bad.append(("final", a.plies, int(i)))
+                break
+        print(json.dumps({"seed": seed, "opponent": opp, "color": color, "boards": n, "plies": a.plies,
+                          "sampled": len(idx), "mismatches": bad[:8], "spill": spill,
+                          "seconds": round(time.time() - t0, 1)}), flush=True)
+        if bad:
+            sys.exit(1)
+
+
+if __name__ == "__main__":
+    main()
