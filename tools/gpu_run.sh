@@ -48,7 +48,8 @@ for s in ${STEPS:-smoke pytest bench prof}; do
     fcp)    step fcp 300 python tools/fixed_cost_probe.py ;;  # the timed region's fixed cost, by K and wait
     anat)   step anat 120 tools/_region_anatomy ;;  # one launch's round trip by parts (build it first)
     pst)    for k in 20 1000; do PST_QUAD=1 PST_LIB=tools/_lib_pst.so step pst_$k 120 python tools/pstamp_probe.py 65536 $k; done ;;  # wave placement / phase stamps (build tools/_lib_pst.so with -DGC_PSTAMPS first)
-    sprobe) step single_probe 300 python tools/single_probe.py ;;  # the single-board server's step and segments vs the oracle
+    sprobe) step single_probe 300 python tools/single_probe.py ;;
+    soak)   step soak 800 python -u tools/soak.py --plies ${SOAK_PLIES:-20000} --chunk 2000 --seeds ${SOAK_SEEDS:-10} ;;  # long rollouts vs the oracle  # the single-board server's step and segments vs the oracle
     eprobe) step engine_probe 120 python tools/engine_probe.py &&  # ChessEngine per-call latency: server / staged in host memory / copies
             GC_ENGINE_SERVER=0 step engine_probe_zc 120 python tools/engine_probe.py &&
             GC_ENGINE_SERVER=0 GC_ENGINE_ZC=0 step engine_probe_staged 120 python tools/engine_probe.py ;;
