@@ -960,17 +960,17 @@ GC_HD void sw_pawns_kl(const Pos& s, const Gen& g, const KingLines& kl, u64* t) 
     const u64 cm = g.checkmask, empty = ~g.occ, opp = g.opp, P = s.p & g.own, pr = g.pinrays;
     const u64 fp = P & ~g.pinned, pp = P & g.pinned;
     const u64 pf = pp & kl.fm(), pd = pp & kl.dm, pa = pp & kl.am;
-    // a file-pinned pawn's double push stays on its side of the king (king_side: it can jump it)
-    const int ks = sw_ksq(g);
-    const u64 hk = ks >= 63 ? 0ull : ~below(ks + 1), lk = below(ks);
+    // a file-pinned pawn's double push stays on its side of the king (king_side): it crosses the
+    // king exactly when the king stands on the square it jumps
+    const u64 kb = bit(sw_ksq(g));
     if (g.white) {  // lib.rs:935-958, p = +1: toward row 0
-        const u64 pf2 = ((((pf & hk) & ROW6) >> 16) & hk) | ((((pf & lk) & ROW6) >> 16) & lk);
+        const u64 pf2 = ((pf & ~(kb << 8)) & ROW6) >> 16;
         t[SW_P1] = and3(and_or(pf >> 8, pr, fp >> 8), empty, cm);
         t[SW_P2] = and3(and_or(pf2, pr, (fp & ROW6) >> 16), empty, cm);
         t[SW_PL] = and3(and_or(pa >> 7, pr, fp >> 7), opp & ~FILE_A, cm);  // row-1 col+1: anti-diagonal
         t[SW_PR] = and3(and_or(pd >> 9, pr, fp >> 9), opp & ~FILE_H, cm);  // row-1 col-1: diagonal
     } else {
-        const u64 pf2 = ((((pf & hk) & ROW1) << 16) & hk) | ((((pf & lk) & ROW1) << 16) & lk);
+        const u64 pf2 = ((pf & ~(kb >> 8)) & ROW1) << 16;
         t[SW_P1] = and3(and_or(pf << 8, pr, fp << 8), empty, cm);
         t[SW_P2] = and3(and_or(pf2, pr, (fp & ROW1) << 16), empty, cm);
         t[SW_PL] = and3(and_or(pd << 9, pr, fp << 9), opp & ~FILE_A, cm);  // row+1 col+1: diagonal
