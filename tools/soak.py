@@ -28,19 +28,31 @@ def main():
     ap.add_argument("--chunk", type=int, default=1000)
     ap.add_argument("--seeds", type=int, default=5)
     ap.add_argument("--boards", type=int, default=65536)
+    ap.add_argument("--random-inits", type=int, default=0,
+                    help="instead: K random (also weird) initial boards, 4 096 boards each (tests/conftest.py)")
     a = ap.parse_args()
     import oracle as O
     from gym_chess_amd.env import BatchedChessEnv
 
     n = a.boards
-    idx = np.array(sorted(set(range(0, n, 1021)) | set(range(64)) | set(range(n - 64, n)) |
+    inits = [None]
+    if a.random_inits:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from conftest import random_positions
+
+        n = 4096
+        inits = list(random_positions(a.random_inits, 977)[0])
+    idx = np.array(sorted(set(range(0, n, 1021 if n > 8192 else 131)) | set(range(64)) | set(range(n - 64, n)) |
                           set(range(n // 2 - 16, n // 2 + 16))), dtype=np.int64)
     threads = max(1, min(16, os.cpu_count() or 1))
-    cases = [(1000 + 7919 * k, "none", "WHITE") for k in range(a.seeds)]
-    cases += [(424242, "random", "WHITE"), (434343, "random", "BLACK")]
-    for seed, opp, color in cases:
+    if a.random_inits:
+        cases = [(2000 + k, "none", "WHITE", ib) for k, ib in enumerate(inits)]
+    else:
+        cases = [(1000 + 7919 * k, "none", "WHITE", None) for k in range(a.seeds)]
+        cases += [(424242, "random", "WHITE", None), (434343, "random", "BLACK", None)]
+    for seed, opp, color, ib in cases:
         t0 = time.time()
-        env = BatchedChessEnv(n, device=0, seed=seed, opponent=opp, player_color=color)
+        env = BatchedChessEnv(n, device=0, seed=seed, opponent=opp, player_color=color, initial_board=ib)
         tb = env.trace_buffer(a.chunk)
         got = {k: [] for k in ("action", "reward", "done", "reason")}
         for p in range(0, a.plies, a.chunk):
@@ -55,6 +67,8 @@ def main():
         tb.close()
         env.close()
         kw = dict(opponent=1 if opp == "random" else 0, agent_white=color == "WHITE")
+        if ib is not None:
+            kw["init"] = ib
         with ThreadPoolExecutor(threads) as ex:
             refs = list(ex.map(lambda i: O.rollout_trace(seed, int(i), a.plies, **kw), idx))
         bad = []
