@@ -28,12 +28,17 @@ def main():
     ap.add_argument("--chunk", type=int, default=1000)
     ap.add_argument("--seeds", type=int, default=5)
     ap.add_argument("--boards", type=int, default=65536)
+    ap.add_argument("--api", action="store_true",
+                    help="instead: the API step's auto-reset pick loop (gc_env_step_device) vs the oracle driver "
+                         "in action-id order, on every sampled board until it first meets a position with no move")
     ap.add_argument("--random-inits", type=int, default=0,
                     help="instead: K random (also weird) initial boards, 4 096 boards each (tests/conftest.py)")
     a = ap.parse_args()
     import oracle as O
     from gym_chess_amd.env import BatchedChessEnv
 
+    if a.api:
+        return api_soak(a)
     n = a.boards
     inits = [None]
     if a.random_inits:
@@ -83,6 +88,47 @@ def main():
                 break
         print(json.dumps({"seed": seed, "opponent": opp, "color": color, "boards": n, "plies": a.plies,
                           "sampled": len(idx), "mismatches": bad[:8], "spill": spill,
+                          "seconds": round(time.time() - t0, 1)}), flush=True)
+        if bad:
+            sys.exit(1)
+
+
+def api_soak(a):
+    import oracle as O
+    from gym_chess_amd.env import BatchedChessEnv
+
+    n = a.boards
+    idx = np.array(sorted(set(range(0, n, 1021)) | set(range(64)) | set(range(n - 64, n))), dtype=np.int64)
+    threads = max(1, min(16, os.cpu_count() or 1))
+    for seed in (2718 + 31 * k for k in range(a.seeds)):
+        t0 = time.time()
+        with ThreadPoolExecutor(threads) as ex:
+            refs = list(ex.map(lambda i: O.rollout_trace(seed, int(i), a.plies + 1, order="action"), idx))
+        env = BatchedChessEnv(n, device=0, seed=seed)
+        io = env.device_io()
+        first = np.zeros(n, dtype=np.uint16)
+        first[idx] = [max(int(r["action"][0]), 0) for r in refs]
+        io.upload_actions(first)
+        live = np.ones(len(idx), dtype=bool)
+        bad, checked = [], 0
+        for p in range(a.plies):
+            env.step_device(io, autoreset=True)
+            o = io.fetch("reward", "done", "pick")
+            live &= np.array([r["reason"][p] != 4 and r["action"][p] >= 0 for r in refs])
+            rr = np.array([r["reward"][p] for r in refs])
+            rd = np.array([r["done"][p] for r in refs])
+            nx = np.array([r["action"][p + 1] for r in refs])
+            ok = live & (nx >= 0)
+            for j in np.nonzero(live & ((o["reward"][idx] != rr) | (o["done"][idx] != rd)))[0][:2]:
+                bad.append(("reward/done", p, int(idx[j])))
+            for j in np.nonzero(ok & (o["pick"][idx] != nx))[0][:2]:
+                bad.append(("pick", p, int(idx[j])))
+            checked += int(live.sum())
+            if bad:
+                break
+        env.close()
+        print(json.dumps({"api_seed": seed, "boards": n, "plies": a.plies, "sampled": len(idx),
+                          "board_plies_checked": checked, "mismatches": bad[:8],
                           "seconds": round(time.time() - t0, 1)}), flush=True)
         if bad:
             sys.exit(1)
