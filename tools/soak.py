@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--api", action="store_true",
                     help="instead: the API step's auto-reset pick loop (gc_env_step_device) vs the oracle driver "
                          "in action-id order, on every sampled board until it first meets a position with no move")
+    ap.add_argument("--fide", action="store_true",
+                    help="instead: rules='fide' fused rollouts vs the host build of gc_fide.h (tests/core_host)")
     ap.add_argument("--random-inits", type=int, default=0,
                     help="instead: K random (also weird) initial boards, 4 096 boards each (tests/conftest.py)")
     a = ap.parse_args()
@@ -41,6 +43,13 @@ def main():
         return api_soak(a)
     n = a.boards
     inits = [None]
+    rules = "fide" if a.fide else "reference"
+    if a.fide:
+        sys.path.insert(0, os.path.join(ROOT, "tests", "core_host"))
+        import corehost as H
+        from gym_chess_amd import codec as C
+
+        start = np.array(C.DEFAULT_BOARD, dtype=np.int8).reshape(64)
     if a.random_inits:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         from conftest import random_positions
@@ -50,14 +59,17 @@ def main():
     idx = np.array(sorted(set(range(0, n, 1021 if n > 8192 else 131)) | set(range(64)) | set(range(n - 64, n)) |
                           set(range(n // 2 - 16, n // 2 + 16))), dtype=np.int64)
     threads = max(1, min(16, os.cpu_count() or 1))
-    if a.random_inits:
+    if a.fide:
+        cases = [(0xF1DE + 7919 * k, "none", "WHITE", None) for k in range(a.seeds)]
+    elif a.random_inits:
         cases = [(2000 + k, "none", "WHITE", ib) for k, ib in enumerate(inits)]
     else:
         cases = [(1000 + 7919 * k, "none", "WHITE", None) for k in range(a.seeds)]
         cases += [(424242, "random", "WHITE", None), (434343, "random", "BLACK", None)]
     for seed, opp, color, ib in cases:
         t0 = time.time()
-        env = BatchedChessEnv(n, device=0, seed=seed, opponent=opp, player_color=color, initial_board=ib)
+        env = BatchedChessEnv(n, device=0, seed=seed, opponent=opp, player_color=color, initial_board=ib,
+                              rules=rules)
         tb = env.trace_buffer(a.chunk)
         got = {k: [] for k in ("action", "reward", "done", "reason")}
         for p in range(0, a.plies, a.chunk):
@@ -75,18 +87,21 @@ def main():
         if ib is not None:
             kw["init"] = ib
         with ThreadPoolExecutor(threads) as ex:
-            refs = list(ex.map(lambda i: O.rollout_trace(seed, int(i), a.plies, **kw), idx))
+            if a.fide:  # the host build's trace (no final state: the boards are compared by trace only)
+                refs = list(ex.map(lambda i: H.fide_rollout(seed, int(i), a.plies, start), idx))
+            else:
+                refs = list(ex.map(lambda i: O.rollout_trace(seed, int(i), a.plies, **kw), idx))
         bad = []
         for key in got:
             g = np.concatenate(got[key], axis=0)
             w = np.stack([r[key][: a.plies] for r in refs], axis=1)
             for p_, j in np.argwhere(g != w)[:4]:
                 bad.append((key, int(p_), int(idx[j])))
-        for j, i in enumerate(idx):
+        for j, i in enumerate(idx if not a.fide else []):
             if not ((b[i] == refs[j]["final_board"]).all() and list(m[i]) == list(refs[j]["final_meta"])):
                 bad.append(("final", a.plies, int(i)))
                 break
-        print(json.dumps({"seed": seed, "opponent": opp, "color": color, "boards": n, "plies": a.plies,
+        print(json.dumps({"seed": seed, "rules": rules, "opponent": opp, "color": color, "boards": n, "plies": a.plies,
                           "sampled": len(idx), "mismatches": bad[:8], "spill": spill,
                           "seconds": round(time.time() - t0, 1)}), flush=True)
         if bad:
