@@ -34,6 +34,8 @@ def main():
     ap.add_argument("--api-opp", choices=["WHITE", "BLACK"],
                     help="instead: the random opponent's API step (k_env_step_api2_vs), actions = the previous "
                          "pick, auto-reset, in lockstep with the oracle env on the sampled boards")
+    ap.add_argument("--launched", action="store_true",
+                    help="drive the cases with one launch per ply (step_random: k_env_step2) instead of fused launches")
     ap.add_argument("--fide", action="store_true",
                     help="instead: rules='fide' fused rollouts vs the host build of gc_fide.h (tests/core_host)")
     ap.add_argument("--random-inits", type=int, default=0,
@@ -77,7 +79,14 @@ def main():
                               rules=rules)
         tb = env.trace_buffer(a.chunk)
         got = {k: [] for k in ("action", "reward", "done", "reason")}
-        for p in range(0, a.plies, a.chunk):
+        for p in range(a.plies if a.launched else 0):
+            played = env.outputs()["next_action"].astype(np.int32)[idx]
+            env.step_random(1)
+            o = env.outputs()
+            got["action"].append(np.where(played == 0xFFFF, -1, played)[None])
+            for key in ("reward", "done", "reason"):
+                got[key].append(o[key][idx][None])
+        for p in range(0, 0 if a.launched else a.plies, a.chunk):
             k = min(a.chunk, a.plies - p)
             env.rollout_device(k, tb)
             env.synchronize()
@@ -106,7 +115,8 @@ def main():
             if not ((b[i] == refs[j]["final_board"]).all() and list(m[i]) == list(refs[j]["final_meta"])):
                 bad.append(("final", a.plies, int(i)))
                 break
-        print(json.dumps({"seed": seed, "rules": rules, "opponent": opp, "color": color, "boards": n, "plies": a.plies,
+        print(json.dumps({"seed": seed, "form": "launched" if a.launched else "fused", "rules": rules,
+                          "opponent": opp, "color": color, "boards": n, "plies": a.plies,
                           "sampled": len(idx), "mismatches": bad[:8], "spill": spill,
                           "seconds": round(time.time() - t0, 1)}), flush=True)
         if bad:
