@@ -3811,12 +3811,56 @@ static void srv_unregister(const void* owner) {
         }
 }
 
+// ---- one resident server per device.  A resident wave holds its hardware
+// queue until it exits, and HIP maps a process's streams onto GPU_MAX_HW_QUEUES (4 on the box)
+// queues: with more streams than that, work on a stream that shares a queue with a resident
+// server waits behind it until it idles out (SRV_IDLE_MS) -- ~50 ms per call for single-board
+// envs stepped round-robin, or env.step mixed with ChessEngine calls.  So at most one server
+// runs per device: a request to another owner's server, and every launch of this library on
+// the device (SRV_QUIESCE, devsrv_quiesce), first stops the resident one (QUIT, its stream
+// drained).  The slot's mutex is held for a whole server call (lock order: an engine's own
+// mutex, then the slot's), so a server's state is only touched under it.
+#define GC_MAX_DEVICES 64
+struct DevSrv {
+    std::recursive_mutex mu;
+    std::atomic<void*> owner{nullptr};  // the env / engine whose server may be resident
+    int (*stop)(void*) = nullptr;       // its stop (QUIT + drain)
+};
+static DevSrv g_devsrv[GC_MAX_DEVICES];
+static DevSrv& devsrv(int dev) { return g_devsrv[(unsigned)dev % GC_MAX_DEVICES]; }
+// (held: s.mu)
+static int devsrv_stop_locked(DevSrv& s) {
+    void* o = s.owner.exchange(nullptr, std::memory_order_acq_rel);
+    return o ? s.stop(o) : 0;
+}
+static int devsrv_quiesce(int dev) {
+    DevSrv& s = devsrv(dev);
+    if (!s.owner.load(std::memory_order_acquire)) return 0;
+    std::lock_guard<std::recursive_mutex> lk(s.mu);
+    return devsrv_stop_locked(s);
+}
+// (held: s.mu) the slot for `owner`: another owner's server is stopped first
+static int devsrv_claim(DevSrv& s, void* owner, int (*stop)(void*)) {
+    void* o = s.owner.load(std::memory_order_acquire);
+    if (o && o != owner && devsrv_stop_locked(s)) return -1;
+    s.stop = stop;
+    s.owner.store(owner, std::memory_order_release);
+    return 0;
+}
+static void devsrv_release(DevSrv& s, void* owner) {
+    void* o = owner;
+    s.owner.compare_exchange_strong(o, nullptr, std::memory_order_acq_rel);
+}
+
 // ---- the engine server's host side (the single-board server's protocol, srv_call)
 static bool eng_srv_enabled() {
     static const bool off = getenv("GC_ENGINE_SERVER") && atoi(getenv("GC_ENGINE_SERVER")) == 0;  // A/B
     return !off;
 }
 static int eng_srv_stop(gc_engine* e) {
+    DevSrv& s = devsrv(e->device);
+    std::lock_guard<std::recursive_mutex> lk(s.mu);
+    devsrv_release(s, e);
     if (!e->srv_launch) return 0;
     EngBox* b = e->srv;
     __atomic_store_n(&b->op, (u32)SRV_QUIT, __ATOMIC_RELAXED);
@@ -3828,8 +3872,12 @@ static int eng_srv_stop(gc_engine* e) {
     return 0;
 }
 // one op on one position; the response lands in e->srv
+static int eng_srv_stop_v(void* e) { return eng_srv_stop(static_cast<gc_engine*>(e)); }
 static int eng_srv_call(gc_engine* e, int op, const int8_t* board, const uint8_t* meta, bool white, int arg) {
     HIPCHK(hipSetDevice(e->device));
+    DevSrv& s = devsrv(e->device);
+    std::lock_guard<std::recursive_mutex> lk(s.mu);
+    if (devsrv_claim(s, e, eng_srv_stop_v)) return -1;
     if (!e->srv) {
         HIPCHK(hipHostMalloc((void**)&e->srv, sizeof(EngBox), hipHostMallocMapped | hipHostMallocCoherent));
         memset(e->srv, 0, sizeof(EngBox));
@@ -3897,7 +3945,7 @@ extern "C" int gc_engine_get_possible_moves(gc_engine* e, int n, const int8_t* b
         counts[0] = c;
         return 0;
     }
-    if (engine_reserve(e, n, cap)) return -1;
+    if (devsrv_quiesce(e->device) || engine_reserve(e, n, cap)) return -1;
     EngineLayout o;
     if (e->rules) {
         if (engine_upload(e, n, boards, meta, player_white, o, cap)) return -1;
@@ -3934,7 +3982,7 @@ extern "C" int gc_engine_get_castle_moves(gc_engine* e, int n, const int8_t* boa
         counts[0] = k;
         return 0;
     }
-    if (engine_reserve(e, n, 2)) return -1;
+    if (devsrv_quiesce(e->device) || engine_reserve(e, n, 2)) return -1;
     EngineLayout o;
     if (engine_upload(e, n, boards, meta, player_white, o, 2)) return -1;
     std::vector<u64> mask(e->rules ? (size_t)65 * n : 0);
@@ -3982,7 +4030,7 @@ extern "C" int gc_engine_next_state(gc_engine* e, int n, const int8_t* boards, c
         status[0] = e->srv->status;
         return 0;
     }
-    if (engine_reserve(e, n, 1)) return -1;
+    if (devsrv_quiesce(e->device) || engine_reserve(e, n, 1)) return -1;
     // FIDE: the player argument is the side to move; reference: it only steers next_state's
     // promotion colour and rights logic (lib.rs:679-784), the state keeps current_player
     // the import reads side only under FIDE (the player argument is the side to move there)
@@ -4022,7 +4070,7 @@ extern "C" int gc_engine_update_state(gc_engine* e, int n, const int8_t* boards,
         memcpy(out_meta, e->srv->out_meta, 8);
         return 0;
     }
-    if (engine_reserve(e, n, 1)) return -1;
+    if (devsrv_quiesce(e->device) || engine_reserve(e, n, 1)) return -1;
     EngineLayout o;
     if (engine_upload(e, n, boards, meta, nullptr, o)) return -1;
     SoA st{e->bb, e->meta, n};
@@ -4356,7 +4404,7 @@ extern "C" int gc_engine_perft(gc_engine* e, int n, const int8_t* boards, const 
     if (!e || !nodes) return fail("null argument");
     std::lock_guard<std::mutex> lk(e->mu);
     if (depth < 0 || depth > PERFT_MAXD) return fail("depth must be in [0, 8]");
-    if (engine_reserve(e, n, 1)) return -1;
+    if (devsrv_quiesce(e->device) || engine_reserve(e, n, 1)) return -1;
     EngineLayout o;
     if (engine_upload(e, n, boards, meta, nullptr, o)) return -1;
     if (perft_device(e->stream, SoA{e->bb, e->meta, n}, depth, e->u64o, e->rules)) return -1;
@@ -4426,7 +4474,8 @@ struct gc_env {
 };
 
 static int srv_stop(gc_env* e);  // (the single-board server, below)
-#define SRV_QUIESCE(e) do { if ((e)->srv_launch && srv_stop(e)) return -1; } while (0)
+// before any launch on the env's device: no resident server (its own or another owner's) holds a queue
+#define SRV_QUIESCE(e) do { if (devsrv_quiesce((e)->device)) return -1; } while (0)
 
 static void env_free(gc_env* e) {
     void* ps[] = {e->api_out, e->reset_acts, e->icd, e->icd_f, e->racts_f, e->ep, e->slab, e->d.htab, e->mbox, e->m8, e->mask,
@@ -4982,6 +5031,9 @@ static bool srv_enabled() {
 // stop the server (if one runs) and wait until it has drained: every other op on this env
 // reads or writes the board's memory through other kernels
 static int srv_stop(gc_env* e) {
+    DevSrv& s = devsrv(e->device);
+    std::lock_guard<std::recursive_mutex> lk(s.mu);
+    devsrv_release(s, e);
     if (!e->srv_launch) return 0;
     SrvBox* b = e->srv;
     __atomic_store_n(&b->op, (u32)SRV_QUIT, __ATOMIC_RELAXED);
@@ -4993,15 +5045,19 @@ static int srv_stop(gc_env* e) {
     return 0;
 }
 // one op through the server (started on demand); the record lands in e->srec
+static int srv_stop_v(void* e) { return srv_stop(static_cast<gc_env*>(e)); }
 static int srv_call(gc_env* e, int board, int op, int action, int flags) {
     HIPCHK(hipSetDevice(e->device));
+    DevSrv& s = devsrv(e->device);
+    std::lock_guard<std::recursive_mutex> lk(s.mu);
+    if (devsrv_claim(s, e, srv_stop_v)) return -1;
     if (!e->srv) {
         HIPCHK(hipHostMalloc(&e->srv, sizeof(SrvBox), hipHostMallocMapped | hipHostMallocCoherent));
         memset(e->srv, 0, sizeof(SrvBox));
         HIPCHK(hipHostGetDevicePointer((void**)&e->srv_d, e->srv, 0));
         HIPCHK(hipStreamCreateWithFlags(&e->srv_stream, hipStreamNonBlocking));
     }
-    if (e->srv_launch && e->srv_board != board && srv_stop(e)) return -1;
+    if (e->srv_launch && e->srv_board != board && (srv_stop(e) || devsrv_claim(s, e, srv_stop_v))) return -1;
     SrvBox* b = e->srv;
     const u32 seq = e->srv_seq + 1;
     __atomic_store_n(&b->op, (u32)op, __ATOMIC_RELAXED);
@@ -5051,11 +5107,12 @@ extern "C" int gc_env_single_call(gc_env* e, int board, int op, int action, int 
         return fail("action out of range [0, 4100]");
     HIPCHK(hipSetDevice(e->device));
     if (e->d.ic.spill.ent) {  // a BLACK agent: the spill table's host checks need the stream
-        if (srv_stop(e) || spill_before(e)) return -1;
+        if (devsrv_quiesce(e->device) || spill_before(e)) return -1;
     }
     if (srv_enabled() && !e->d.ic.spill.ent) {
         if (srv_call(e, board, op, action, flags)) return -1;
     } else {
+        if (devsrv_quiesce(e->device)) return -1;
         k_single<<<1, 64, 0, e->stream>>>(e->d, board, op, action, flags, e->srec_d);
         HIPCHK(hipGetLastError());
         if (spill_after(e) || gc_env_synchronize(e)) return -1;
@@ -5082,7 +5139,7 @@ extern "C" int gc_env_single_set(gc_env* e, int board, const int8_t* board64, co
     if (srv_enabled() && !e->d.ic.spill.ent) {
         if (srv_call(e, board, SOP_SET, 0, 0)) return -1;
     } else {
-        if (srv_stop(e)) return -1;
+        if (devsrv_quiesce(e->device)) return -1;
         k_single<<<1, 64, 0, e->stream>>>(e->d, board, SOP_SET, 0, 0, e->srec_d);
         HIPCHK(hipGetLastError());
         if (gc_env_synchronize(e)) return -1;

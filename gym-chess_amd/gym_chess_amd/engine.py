@@ -9,6 +9,7 @@ Reference call sites this replaces: chess_v2.py:146 (construction), 204 (update_
 419 (next_state), 579 (get_possible_moves), 590 (get_castle_moves).
 """
 import ctypes
+import threading
 
 import numpy as np
 
@@ -142,48 +143,58 @@ class ChessEngine:
         self._st = np.zeros(1, dtype=np.int32)
         self._p_act, self._p_ob, self._p_om = _lib.ptr(self._act), _lib.ptr(self._ob), _lib.ptr(self._om)
         self._p_rw, self._p_st = _lib.ptr(self._rw), _lib.ptr(self._st)
+        # the buffers above are shared by every call on this instance, and ctypes releases the
+        # GIL inside the C call: one call at a time, from the inputs' staging through the
+        # conversion of the outputs to Python objects
+        self._lock = threading.Lock()
 
     def next_state(self, state, player, move):
         b, m = C.dict_to_arrays(state)
         white = self._player(player)
-        self._act[0] = C.str_to_action(move)
+        act = C.str_to_action(move)
         e = self._e
-        _lib.check(e._L.gc_engine_next_state(e._h, 1, _lib.ptr(b), _lib.ptr(m), self._p_white[0 if white else 1],
-                                             self._p_act, self._p_ob, self._p_om, self._p_rw, self._p_st))
-        st = int(self._st[0])
+        with self._lock:
+            self._act[0] = act
+            _lib.check(e._L.gc_engine_next_state(e._h, 1, _lib.ptr(b), _lib.ptr(m), self._p_white[0 if white else 1],
+                                                 self._p_act, self._p_ob, self._p_om, self._p_rw, self._p_st))
+            st = int(self._st[0])
+            if st == 0:
+                return C.arrays_to_dict(self._ob, self._om), int(self._rw[0])
         if st == -1:
             raise RuntimeError("Bad move - piece is empty !")
         if st == 1:
             raise SystemError("Both Kings are in check: this position is impossible")
-        if st != 0:
-            raise ValueError(f"bad move {move!r}")
-        return C.arrays_to_dict(self._ob, self._om), int(self._rw[0])
+        raise ValueError(f"bad move {move!r}")
 
     def get_possible_moves(self, state, player, attack=False):
         b, m = C.dict_to_arrays(state)
         white = self._player(player)
         e = self._e
-        _lib.check(e._L.gc_engine_get_possible_moves(e._h, 1, _lib.ptr(b), _lib.ptr(m), self._p_white[0 if white else 1],
-                                                     1 if attack else 0, self._p_moves, MAX_LIST, self._p_cnt))
-        n = int(self._cnt[0])
-        if n > MAX_LIST:
-            out, cnt = e.possible_moves(b, m, white, attack, cap=n)
-            return C.actions_to_strs(out[0, :n])
-        return C.actions_to_strs(self._moves[:n])
+        with self._lock:
+            _lib.check(e._L.gc_engine_get_possible_moves(e._h, 1, _lib.ptr(b), _lib.ptr(m),
+                                                         self._p_white[0 if white else 1], 1 if attack else 0,
+                                                         self._p_moves, MAX_LIST, self._p_cnt))
+            n = int(self._cnt[0])
+            if n <= MAX_LIST:
+                return C.actions_to_strs(self._moves[:n])
+        out, cnt = e.possible_moves(b, m, white, attack, cap=n)  # fresh output arrays
+        return C.actions_to_strs(out[0, :n])
 
     def get_castle_moves(self, state, player):
         b, m = C.dict_to_arrays(state)
         white = self._player(player)
         e = self._e
-        _lib.check(e._L.gc_engine_get_castle_moves(e._h, 1, _lib.ptr(b), _lib.ptr(m), self._p_white[0 if white else 1],
-                                                   self._p_moves, self._p_cnt))
-        return C.actions_to_strs(self._moves[: int(self._cnt[0])])
+        with self._lock:
+            _lib.check(e._L.gc_engine_get_castle_moves(e._h, 1, _lib.ptr(b), _lib.ptr(m),
+                                                       self._p_white[0 if white else 1], self._p_moves, self._p_cnt))
+            return C.actions_to_strs(self._moves[: int(self._cnt[0])])
 
     def update_state(self, state):
         b, m = C.dict_to_arrays(state)
         e = self._e
-        _lib.check(e._L.gc_engine_update_state(e._h, 1, _lib.ptr(b), _lib.ptr(m), self._p_ob, self._p_om))
-        return C.arrays_to_dict(self._ob, self._om)
+        with self._lock:
+            _lib.check(e._L.gc_engine_update_state(e._h, 1, _lib.ptr(b), _lib.ptr(m), self._p_ob, self._p_om))
+            return C.arrays_to_dict(self._ob, self._om)
 
     @staticmethod
     def _player(player):

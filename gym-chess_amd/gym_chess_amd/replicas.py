@@ -220,7 +220,11 @@ class Replicas:
         self.barrier()
         out = self.run(body)
         spans = [(o[2], o[2] + o[1]) for o in out if len(o) > 2]
-        self.last_overlap = overlap(self.allgather(spans)) if len(spans) == len(out) else None
+        # every rank issues the same collective whatever its fn returned (a rank
+        # skipping it would leave the others waiting); overlap only when every replica timed one
+        got = self.allgather({"spans": spans, "complete": len(spans) == len(out)})
+        self.last_overlap = (overlap([tuple(x) for g in got for x in g["spans"]])
+                             if all(g["complete"] for g in got) else None)
         return [o[0] for o in out], self.max(max(o[1] for o in out))
 
     def allgather(self, value):

@@ -1,6 +1,7 @@
 """TEST INFRASTRUCTURE ONLY -- ctypes view of the host build of the product's bitboard core
 (gym-chess_amd/csrc/gc_core.h + gc_env.h compiled by g++), for CPU differential tests."""
 import ctypes
+import hashlib
 import os
 import subprocess
 
@@ -8,21 +9,44 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _SO = os.path.join(_HERE, "_build", "libcorehost.so")
+_STAMP = _SO + ".srchash"
+_CSRC = os.path.join(_HERE, "..", "..", "gym-chess_amd", "csrc")
+FLAGS = ["-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wno-unknown-pragmas"]
 _L = None
 P = ctypes.c_void_p
+
+
+def source_hash():
+    """sha256 prefix of core_host.cpp, the product's device headers it compiles and the flags
+    (content, not mtimes: a library built from other sources is never reused)"""
+    h = hashlib.sha256(" ".join(FLAGS).encode())
+    srcs = [os.path.join(_HERE, "core_host.cpp")] + sorted(
+        os.path.join(_CSRC, f) for f in os.listdir(_CSRC) if f.endswith(".h"))
+    for path in srcs:
+        h.update(os.path.basename(path).encode() + b"\0")
+        with open(path, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def ensure_built():
+    """(re)build libcorehost.so unless its stamp holds the current source hash"""
+    want = source_hash()
+    if os.path.exists(_SO) and os.path.exists(_STAMP) and open(_STAMP).read().strip() == want:
+        return
+    os.makedirs(os.path.dirname(_SO), exist_ok=True)
+    tmp = f"{_SO}.{os.getpid()}.tmp"  # build aside, then rename: parallel test workers never load a partial file
+    subprocess.run(["g++"] + FLAGS + ["-o", tmp, os.path.join(_HERE, "core_host.cpp")], check=True)
+    os.replace(tmp, _SO)
+    with open(f"{_STAMP}.{os.getpid()}.tmp", "w") as f:
+        f.write(want)
+    os.replace(f"{_STAMP}.{os.getpid()}.tmp", _STAMP)
 
 
 def lib():
     global _L
     if _L is None:
-        src = os.path.join(_HERE, "core_host.cpp")
-        hdr = [os.path.join(_HERE, "..", "..", "gym-chess_amd", "csrc", h) for h in ("gc_core.h", "gc_env.h", "gc_fide.h")]
-        if not os.path.exists(_SO) or os.path.getmtime(_SO) < max(os.path.getmtime(p) for p in [src] + hdr):
-            os.makedirs(os.path.dirname(_SO), exist_ok=True)
-            tmp = f"{_SO}.{os.getpid()}.tmp"  # build aside, then rename: parallel test workers never load a partial file
-            subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wno-unknown-pragmas", "-o", tmp, src],
-                           check=True)
-            os.replace(tmp, _SO)
+        ensure_built()
         L = ctypes.CDLL(_SO)
         L.host_between.restype = ctypes.c_uint64
         L.host_pins_agree.argtypes = [P, P, ctypes.c_int]

@@ -149,6 +149,52 @@ def test_one_position_calls_from_two_threads(engine, oracle):
     assert not errors, errors[:8]
 
 
+def test_chess_engine_dict_calls_from_two_threads(oracle):
+    """the drop-in ChessEngine reuses its output buffers across calls; two threads
+    sharing one instance (ctypes releases the GIL) must each get their own lists and next
+    states -- the lock covers the C call and the conversion to Python objects."""
+    import threading
+
+    from gym_chess_amd import codec as C
+    from gym_chess_amd.engine import ChessEngine
+
+    eng = ChessEngine(0)
+    boards, metas = random_positions(60, 43, weird=False)
+    states, want_lists, want_next = [], [], []
+    for i in range(60):
+        b, m = boards[i], metas[i]
+        st = C.arrays_to_dict(b, m)
+        white = int(m[0])
+        lst = oracle.get_possible_moves(b, m, white)
+        states.append((st, "WHITE" if white else "BLACK"))
+        want_lists.append(C.actions_to_strs(np.array(lst, dtype=np.uint16)))
+        if lst:
+            rc, nb, nm, rw = oracle.next_state(b, m, white, lst[0])
+            want_next.append((C.action_to_str(lst[0]), nb, rw) if rc == 0 else None)
+        else:
+            want_next.append(None)
+    errors = []
+
+    def work(lo, hi):
+        for _ in range(4):
+            for i in range(lo, hi):
+                st, pl = states[i]
+                if eng.get_possible_moves(st, pl) != want_lists[i]:
+                    errors.append(("list", i))
+                if want_next[i] is not None:
+                    mv, nb, rw = want_next[i]
+                    d, r = eng.next_state(st, pl, mv)
+                    if r != rw or list(np.asarray(d["board"]).reshape(64)) != list(nb):
+                        errors.append(("next", i))
+
+    ts = [threading.Thread(target=work, args=(0, 30)), threading.Thread(target=work, args=(30, 60))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errors, errors[:8]
+
+
 @pytest.mark.parametrize("mirror", [False, True])
 def test_two_pins_double_push_never_crosses_its_king(engine, oracle, mirror):
     """Two pins on the king's file (rook behind, queen in front): the rear pawn's Q1 double push

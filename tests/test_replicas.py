@@ -46,6 +46,12 @@ def _worker(rank, world, port, backend, out):
     # many rounds back to back: a fast rank may run one round ahead of a slow one
     acc = [r.sum(float(k * (rank + 1))) for k in range(50)]
     res["acc_ok"] = acc == [float(3 * k) for k in range(50)]
+    # ranks whose timed fn returns different shapes (rank 0 a begin time, rank 1 none) still issue
+    # the same collectives: no deadlock, no overlap claimed, the max still taken
+    _, dt = r.timed(lambda rp: (None, 0.5 + rank, time.perf_counter()) if rank == 0 else (None, 0.5 + rank))
+    res["mixed_ok"] = dt == 1.5 and r.last_overlap is None
+    _, dt = r.timed(lambda rp: (None, 0.25, time.perf_counter()))
+    res["spans_ok"] = r.last_overlap is not None and r.last_overlap["replicas"] == 2
     r.close()
     out.put((rank, res))
 
@@ -70,6 +76,7 @@ def test_two_rank_replicas(backend):
     assert res[0]["tmax"] == res[1]["tmax"] == 2.0
     assert res[0]["ssum"] == res[1]["ssum"] == res[0]["steps"] + res[1]["steps"]
     assert res[0]["acc_ok"] and res[1]["acc_ok"]
+    assert all(x["mixed_ok"] and x["spans_ok"] for x in res)
     # independence: rank 1's shard equals what a lone process with rank 1's seed computes
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
