@@ -238,6 +238,9 @@ def perft_leg(args, rep):
             except (OSError, ValueError):
                 pass
         out["roofline"] = roof
+    fx = fixture_check(args, rep, ctx[0], res[0])
+    if fx is not None:
+        out["fixture_check"] = fx
     k = min(args.oracle_perft_roots, args.perft_roots)
     if rep.rank == 0 and k > 0:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -276,6 +279,39 @@ def perft_leg(args, rep):
                                    "spread_roots_depth5": {"value": float(cn.sum()) / cdt, "roots": len(idx),
                                                            "nodes": int(cn.sum()), "seconds": cdt}}
     return out
+
+
+PERFT_FIXTURE = os.path.join(ROOT, "tests", "golden", "configs3_perft.npz")
+
+
+def fixture_check(args, rep, ctx0, nodes):
+    """configs[3] pinned at full width: rank 0's roots against the oracle's
+    fixture (tests/golden/make_perft_roots.py: the same 65 536 roots regenerated by the oracle,
+    every root's perft(4), every 64th root's perft(5)).  The timed run's per-root perft(5) must
+    equal the fixture on its stride, and a perft(4) of every root (outside the timed region)
+    must equal the fixture root by root; any difference fails the bench."""
+    import numpy as np
+
+    if rep.rank != 0 or args.perft_roots != 65536 or args.perft_depth != 5 or not os.path.exists(PERFT_FIXTURE):
+        return None
+    eng, b, m = ctx0
+    f = np.load(PERFT_FIXTURE)
+    same = bool((b == f["boards"]).all() and (m[:, :7] == f["metas"][:, :7]).all())
+    assert same, "the perft roots differ from the fixture's (tests/golden/configs3_perft.npz)"
+    s5 = f["stride5"]
+    bad5 = s5[np.nonzero(nodes[s5] != f["perft5"])[0]]
+    assert len(bad5) == 0, f"perft(5) differs from the fixture at roots {bad5[:8]}"
+    from gym_chess_amd.engine import Engine
+
+    e4 = Engine(rep.local[0].device)
+    p4 = e4.perft(b, m, 4)
+    e4.close()
+    bad4 = np.nonzero(p4 != f["perft4"])[0]
+    assert len(bad4) == 0, f"perft(4) differs from the fixture at roots {bad4[:8]}"
+    return {"fixture": os.path.relpath(PERFT_FIXTURE, ROOT), "roots_equal": 65536,
+            "perft4_roots_equal": 65536, "perft4_nodes": int(p4.sum()),
+            "perft5_roots_equal": int(len(s5)), "perft5_stride": int(s5[1] - s5[0]),
+            "perft5_stride_nodes": int(nodes[s5].sum()), "match": True}
 
 
 # algorithmic bytes per board of one API-shaped step (k_env_step_api2, the paired API step,

@@ -2009,6 +2009,12 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
 // pair_ply (and so as k_env_step<true, false> and the oracle): tests/test_gpu_parity.py and
 // tests/test_full_size.py run the fused rollouts against the oracle and the launched kernel.
 #define QUAD_BOARDS 64
+#ifndef GC_Q1_LEAPERS
+#define GC_Q1_LEAPERS 0  // the enemy's leaper attacks on Q1 in phase 1 (else Q2)
+#endif
+#ifndef GC_Q3_KINGS
+#define GC_Q3_KINGS 0    // the king sets on Q3 in phase 2 (else Q2)
+#endif
 #ifndef QUADS_WG
 #define QUADS_WG 2  // two quads per workgroup; the second's roles rotated by 2 so that every SIMD
                     // hosts a state-carrying and a stateless role of each workgroup
@@ -2139,11 +2145,18 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
         L.pin3[1][l] = g.pinned;
         L.pin3[2][l] = g.pinrays;
         L.f0[l] = g.in_check ? 1u : 0u;
-    } else if (R == 1) {  // (the leaper attacks went to Q2: phase 1 was Q1's longest)
+    } else if (R == 1) {
         my_chk = mv && mover_checked(s, ns, white, a);
         L.f1[l] = my_chk ? 1u : 0u;
-    } else if (R == 2) {  // (the leaper attacks on Q1 instead -- its SIMDs the lighter pair here -- measured neutral)
+#if GC_Q1_LEAPERS
+        L.enemy[0][l] = g.ks >= 0 ? side_attacks_leapers(ns, !g.white) : 0ull;
+#endif
+    } else if (R == 2) {
+#if GC_Q1_LEAPERS
+        L.enemy[1][l] = g.ks >= 0 ? side_attacks_orth(ns, !g.white) : 0ull;
+#else
         L.enemy[1][l] = g.ks >= 0 ? side_attacks_leapers(ns, !g.white) | side_attacks_orth(ns, !g.white) : 0ull;
+#endif
     } else {
         L.enemy[2][l] = g.ks >= 0 ? side_attacks_diag(ns, !g.white) : 0ull;
     }
@@ -2151,7 +2164,11 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
     pair_barrier();
     PST(3);
     // ---- phase 2
+#if GC_Q1_LEAPERS
+#define QUAD_ENEMY(l) (L.enemy[0][l] | L.enemy[1][l] | L.enemy[2][l])
+#else
 #define QUAD_ENEMY(l) (L.enemy[1][l] | L.enemy[2][l])
+#endif
     if (R == 0) {
         g.enemy_att = QUAD_ENEMY(l);
         gen_castles(ns, g);  // lib.rs:578-610 with the whole enemy map
@@ -2162,7 +2179,7 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
         g.checkmask = L.pin3[0][l];
         g.pinned = L.pin3[1][l];
         g.pinrays = L.pin3[2][l];
-        if (R == 2) g.enemy_att = QUAD_ENEMY(l);  // for the king sets
+        if (R == (GC_Q3_KINGS ? 3 : 2)) g.enemy_att = QUAD_ENEMY(l);  // for the king sets
     }
     const bool opp_chk = g.in_check;
     const bool both = opp_chk && my_chk;  // lib.rs:1442-1446
@@ -2196,8 +2213,10 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
         u64 T[SW_SETS];
         sw_orth(ns, g, T);
         Q.put_all<SW_ORTH, SW_DIAG>(T + SW_ORTH);
-        sw_kings(ns, g, T);
-        Q.put_all<SW_K, SW_SETS>(T + SW_K);
+        if (!GC_Q3_KINGS) {
+            sw_kings(ns, g, T);
+            Q.put_all<SW_K, SW_SETS>(T + SW_K);
+        }
         L.part[2][l] = (u32)Q.part;
 #pragma unroll
         for (int k = 0; k < 4; k++) L.cwx[0][k][l] = Q.cw[k];
@@ -2205,6 +2224,10 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
         u64 T[SW_SETS];
         sw_diag(ns, g, T);
         Q.put_all<SW_DIAG, SW_K>(T + SW_DIAG);
+        if (GC_Q3_KINGS) {
+            sw_kings(ns, g, T);
+            Q.put_all<SW_K, SW_SETS>(T + SW_K);
+        }
         L.part[3][l] = (u32)Q.part;
 #pragma unroll
         for (int k = 0; k < 4; k++) L.cwx[1][k][l] = Q.cw[k];
@@ -3241,6 +3264,383 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
         io.reward[i] = o.reward;
         io.done[i] = (uint8_t)o.done;
         io.reason[i] = (uint8_t)o.reason;
+    }
+}
+
+// ----------------------------------------------------------------------------- API step, quads
+// k_env_step_api2's contract (the same arguments, outputs, decisions and auto-reset) on FOUR
+// waves per 64 boards, as the headline rollout's quads (k_env_rollout4): the paired API step
+// ran each board's step as two long dependency chains on two waves and wrote its 34 MB
+// legal-action mask at the end, when every workgroup finished at once.
+//
+//   phase 0   Q0: applies the action (speculatively: it is validated beside it)
+//             Q1: the window probe of the pre-move board, the Philox word, the reset-table pick
+//             Q2: validates the action (quick_legal, chess_v2.py:240-242)
+//   phase 1   Q0: checkers, check mask, pins                  Q1: the mover's own check flag
+//             Q2: enemy leaper + orthogonal slider attacks    Q3: enemy diagonal slider attacks
+//             every role: zero words of its mask rows for the squares the next side does not
+//             occupy (most of the mask, written while the chains run)
+//   phase 2   Q0: castles, pawns (set-wise), knights          Q1: the 3-fold commit
+//             Q2: kings, queens                               Q3: rooks, bishops
+//             (pieces parked per ordinal in LDS with bit-sliced counts, as gen_moves)
+//   phase 3   every role: the step's outcome (identical arithmetic on the same LDS data) and
+//             its 16 mask rows of the occupied squares (a reset board: the start position's
+//             rows, from the init cache); Q2: the pick (action-id order), the count, the env's
+//             next action; Q3: the observation; Q1: the outputs, the state and the window.
+// A mask row is written only by the role that owns its square, in program order, so a row
+// zeroed in phase 1 and rewritten in phase 3 (a reset board) needs no fence.  Boards outside
+// the fast path -- > 16 own pieces, or both kings checked after the move (the move is void and
+// the pre-move board regenerates) -- take the per-piece fallback (legal_targets) in phase 3,
+// each role for its own rows.  Quad roles run only with the start position's pick table, as
+// the rollout's.
+struct ApiQuadLds {
+    u64 slots[SCRATCH_SLOTS][QUAD_BOARDS];  // parked targets per own-piece ordinal (Q0, Q2, Q3)
+    u64 ns[NBB][QUAD_BOARDS];               // Q0 -> all: the post-move board (if the action is valid)
+    u32 nmeta[QUAD_BOARDS];
+    int32_t mr[QUAD_BOARDS];                //           its capture reward
+    u32 irrev[QUAD_BOARDS];                 //           irreversible move
+    u32 valid[QUAD_BOARDS];                 // Q2 -> all: the action is legal
+    u64 pin3[3][QUAD_BOARDS];               // Q0 -> Q2, Q3: check mask, pinned, pin rays
+    u32 f0[QUAD_BOARDS];                    // Q0 -> all: the side to move is in check
+    u64 enemy[3][QUAD_BOARDS];              // Q2 ([1]), Q3 ([2]) -> Q0, Q2, Q3: the enemy map's parts
+    u32 f1[QUAD_BOARDS];                    // Q1 -> all: the mover is in check after its move
+    u64 planes[3][5][QUAD_BOARDS];          // Q0 / Q2 / Q3 -> Q2: bit-sliced per-square counts
+    u32 part[4][QUAD_BOARDS];               // move totals (Q0's holds the castles; Q3's a big board's)
+    u64 pawn5[5][QUAD_BOARDS];              // Q0 -> all: fast pawns and their origin sets
+    u32 castles[QUAD_BOARDS];               // Q0 -> all
+    u32 rep[QUAD_BOARDS];                   // Q1 -> all: 3-fold count | window length << 8
+    u32 x0[QUAD_BOARDS];                    // Q1 -> Q2: the Philox word of the draw
+    u32 ra[QUAD_BOARDS];                    // Q1 -> Q2: the start-position table pick
+};
+__shared__ ApiQuadLds g_apiq_lds[QUADS_WG];
+
+// the 16 mask rows of role R that the next side does not occupy: zero (streamed)
+template <int R>
+__device__ __forceinline__ void apiq_zero_rows(u64* __restrict__ o, size_t N, u64 own) {
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const int sq = 16 * R + k;
+        if (!((own >> sq) & 1)) __builtin_nontemporal_store(0ull, o + sq * N);
+    }
+}
+
+// The per-piece fallback of one board (apiq_run: both kings checked, or > 16 own pieces), each
+// part with its own context (gen_init) in its own scope
+template <int R>
+__device__ __noinline__ void apiq_slow_rows(Pos b, u64* __restrict__ o, size_t N) {  // (by value: no stack)
+    Gen g;
+    gen_init(b, g);
+    for (int k = 0; k < 16; k++) {
+        const int sq = 16 * R + k;
+        const u64 w = ((g.own >> sq) & 1) ? legal_targets(b, g, sq, type_at(b, sq)) : 0ull;
+        __builtin_nontemporal_store(w, o + sq * N);
+    }
+}
+__device__ __noinline__ u32 apiq_slow_castles(Pos b) {
+    Gen g;
+    gen_init(b, g);
+    return g.castles;
+}
+// -> the legal count << 16 | the pick (A_NONE without a move)
+__device__ __noinline__ u32 apiq_slow_pick(Pos b, u32 x0) {
+    Gen g;
+    gen_init(b, g);
+    const int tot = count_legal(b, g);
+    if (tot == 0) return (u32)A_NONE;
+    MoveSet ms;
+    moveset_clear(ms);
+    ms.big = true;  // (select_action's per-piece path: no parked targets read)
+    ms.total = tot;
+    return ((u32)tot << 16) | (u32)select_action(b, g, ms, NoScratch{}, (int)scale_rank(x0, (u32)tot));
+}
+
+template <int RR>
+__device__ __forceinline__ void apiq_run(uint8_t* __restrict__ slab, uint64_t seed, u64* __restrict__ htab,
+                                         const uint16_t* __restrict__ racts, const EnvDev::InitCache* __restrict__ icd,
+                                         const uint16_t* __restrict__ acts, const ApiOut& out, int nn, u32 rinfo,
+                                         int qw, int l, int i) {
+    ApiQuadLds& L = g_apiq_lds[qw];
+    const int autoreset = (rinfo >> 17) & 1;
+    rinfo &= 0x1FFFFu;
+    const bool live = i < nn;
+    const int ii = live ? i : nn - 1;  // dead lanes read a valid board, store nothing
+    const size_t N = (size_t)nn;
+    const PairIO in_io(slab, nn);
+    const PairCtx C = {seed, htab, in_io.hgen, racts, icd, (rinfo >> 16) != 0, rinfo & 0xFFFFu};
+    // every role reads the pre-move board and the action (the stateless roles decide the outcome
+    // and the fallback boards themselves); Q1 / Q2 the draw counter, Q1 the window and step counter
+    Pos s = in_io.load(ii);
+    u32 ua = acts[ii], g0 = 0, nst = 0, d = 0;
+    if (RR == 1) { g0 = in_io.hgen[ii]; nst = in_io.nsteps[ii]; }
+    if (RR == 1 || RR == 2) d = in_io.draw[ii];
+    pin(s); pin(ua); pin(g0); pin(nst); pin(d);
+    const int a = (int)ua;
+    DevHist h = DevHist{htab, in_io.hgen, g0, ii, HTAB_BITS};
+    PairScratch scr{&L.slots[0][l]};
+    if (RR < 2) __builtin_amdgcn_s_setprio(2);  // the state-carrying roles' chains are the longer
+    const bool done0 = (s.meta & M_DONE) != 0;   // chess_v2.py:245-251
+    const bool cap = mc_of(s.meta) > MOVES_MAX;  // 252-258
+    const bool white = (s.meta & M_WHITE) != 0;
+    const bool pre = live && !done0 && !cap;
+
+    // ---- phase 0
+    RepProbe pr;
+    uint16_t ra = (uint16_t)A_NONE;
+    if (RR == 0) {  // applied whatever the verdict: a board whose action is invalid keeps s
+        Pos ns = s;
+        ns.meta = (ns.meta & ~(u32)M_RIGHTS) | eff_rights(s);  // State::new
+        int mr = 0;
+        bool irrev = false;
+        apply_legal(ns, white, a, &mr, &irrev);
+        L.ns[0][l] = ns.k; L.ns[1][l] = ns.q; L.ns[2][l] = ns.r; L.ns[3][l] = ns.b;
+        L.ns[4][l] = ns.n; L.ns[5][l] = ns.p; L.ns[6][l] = ns.w;
+        L.nmeta[l] = ns.meta;
+        L.mr[l] = mr;
+        L.irrev[l] = irrev ? 1u : 0u;
+    } else if (RR == 1) {
+        if (pre) rep_prefetch(h, s, pr);
+        const u32 x0 = philox_x0(C.seed, (u32)i, d);
+        if (C.rtable) ra = C.racts[scale_rank(x0, C.rtotal)];
+        L.x0[l] = x0;
+    } else if (RR == 2) {
+        L.valid[l] = quick_legal(s, a) ? 1u : 0u;
+    }
+    pair_barrier();
+
+    // ---- phase 1
+    const bool valid = L.valid[l] != 0;
+    const bool mv = pre && valid;  // env_ply runs
+    Pos ns = s;                    // the position generated for: post-move, or s itself
+    ns.meta = (ns.meta & ~(u32)M_RIGHTS) | eff_rights(s);
+    if (mv) {
+        ns.k = L.ns[0][l]; ns.q = L.ns[1][l]; ns.r = L.ns[2][l]; ns.b = L.ns[3][l];
+        ns.n = L.ns[4][l]; ns.p = L.ns[5][l]; ns.w = L.ns[6][l];
+        ns.meta = L.nmeta[l];
+    }
+    Gen g;
+    gen_base(ns, g);
+    if (RR == 0) {
+        gen_pins(ns, g);
+        L.pin3[0][l] = g.checkmask;
+        L.pin3[1][l] = g.pinned;
+        L.pin3[2][l] = g.pinrays;
+        L.f0[l] = g.in_check ? 1u : 0u;
+    } else if (RR == 1) {
+        L.f1[l] = (mv && mover_checked(s, ns, white, a)) ? 1u : 0u;
+    } else if (RR == 2) {
+        L.enemy[1][l] = g.ks >= 0 ? side_attacks_leapers(ns, !g.white) | side_attacks_orth(ns, !g.white) : 0ull;
+    } else {
+        L.enemy[2][l] = g.ks >= 0 ? side_attacks_diag(ns, !g.white) : 0ull;
+    }
+    u64* const mrow = out.mask ? out.mask + ii : nullptr;
+    if (mrow && live) apiq_zero_rows<RR>(mrow, N, g.own);
+    pair_barrier();
+
+    // ---- phase 2
+    const bool opp_chk = L.f0[l] != 0, my_chk = L.f1[l] != 0;
+    const bool both = mv && opp_chk && my_chk;  // lib.rs:1442-1446: the move is void
+    const bool gen = live && !both;             // the next side's moves (of ns) are due
+    const bool big = popc(g.own) > SCRATCH_SLOTS;
+    g.in_check = opp_chk;
+    if (RR != 0) {
+        g.checkmask = L.pin3[0][l];
+        g.pinned = L.pin3[1][l];
+        g.pinrays = L.pin3[2][l];
+    }
+    g.enemy_att = L.enemy[1][l] | L.enemy[2][l];
+    MoveSet ms;
+    moveset_clear(ms);
+    int part = 0;
+    if (RR == 0) {  // castles (counted here), pawns, knights
+        gen_castles(ns, g);
+        if (gen && !big) {
+            part = gen_pawns(ns, g, ms, scr) + gen_knights(ns, g, ms, scr) + popc(g.castles);
+#pragma unroll
+            for (int b = 0; b < 5; b++) L.planes[0][b][l] = ms.cnt[b];
+        }
+        L.pawn5[0][l] = ms.fastp; L.pawn5[1][l] = ms.o1; L.pawn5[2][l] = ms.o2;
+        L.pawn5[3][l] = ms.ol; L.pawn5[4][l] = ms.orr;
+        L.castles[l] = g.castles;
+        L.part[0][l] = (u32)part;
+    } else if (RR == 1) {
+        int c = 0;
+        u32 hl = hl_of(s.meta);
+        if (mv && !both) {
+            pin(pr.e0.hdr); pin(pr.e0.k); pin(pr.e0.q); pin(pr.e0.r);
+            pin(pr.e0.b); pin(pr.e0.n); pin(pr.e0.p); pin(pr.e0.w);
+            c = rep_commit(h, s, pr, hl, L.irrev[l] != 0);  // table write deferred to h.commit()
+        }
+        L.rep[l] = (u32)c | (hl << 8);
+        L.ra[l] = ra;
+    } else if (RR == 2) {  // kings, queens
+        if (gen && !big) {
+            part = gen_kings(ns, g, ms, scr) + gen_sliders<QUEEN>(ns, g, ms, scr);
+#pragma unroll
+            for (int b = 0; b < 5; b++) L.planes[1][b][l] = ms.cnt[b];
+        }
+        L.part[2][l] = (u32)part;
+    } else {  // rooks, bishops; a big board's whole count
+        if (gen && !big) {
+            part = gen_sliders<ROOK>(ns, g, ms, scr) + gen_sliders<BISHOP>(ns, g, ms, scr);
+#pragma unroll
+            for (int b = 0; b < 5; b++) L.planes[2][b][l] = ms.cnt[b];
+        } else if (gen) {
+            gen_castles(ns, g);
+            part = count_legal(ns, g);
+        }
+        L.part[3][l] = (u32)part;
+    }
+    pair_barrier();
+
+    // ---- phase 3: the outcome, as k_env_step_api2 (every role: identical arithmetic)
+#ifndef GC_NO_QPRIO_DYN
+    if (RR == 0) __builtin_amdgcn_s_setprio(0);
+    if (RR == 2) __builtin_amdgcn_s_setprio(2);  // the pick: this phase's longest chain
+#endif
+    const int total = gen ? (int)(L.part[0][l] + L.part[2][l] + L.part[3][l]) : 0;
+    const u32 rpk = L.rep[l];
+    const int c = (int)(rpk & 0xFFu);
+    const u32 hl = rpk >> 8;
+    StepOut o = {0, 0, R_NONE, 0};
+    Pos fs = s;  // the state after the step
+    if (!valid) {
+        o.reward = -10;
+        o.done = done0 ? 1 : 0;
+        o.reason = R_INVALID;
+    } else if (done0) {
+        o.done = 1;
+        o.reason = R_DONE_ALREADY;
+    } else if (cap) {
+        o.done = 1;
+        o.reason = R_MOVE_CAP;
+    } else if (both) {
+        o.done = 1;
+        o.reason = R_BOTH_CHECKED;
+    } else {
+        const u32 chk = white ? ((my_chk ? M_WCHK : 0u) | (opp_chk ? M_BCHK : 0u))
+                              : ((opp_chk ? M_WCHK : 0u) | (my_chk ? M_BCHK : 0u));
+        fs = ns;
+        fs.meta = with_hl((ns.meta & ~(u32)(M_WCHK | M_BCHK | M_DONE)) | chk | ((c >= 3 || c == 0) ? M_DONE : 0u), hl);
+        o.reward = -10 + (RR == 1 ? (int)L.mr[l] : 0);  // INVALID_ACTION_REWARD + move reward (Q9; Q1 reports it)
+        o.moved = 1;
+        if (c >= 3) { o.done = 1; o.reason = R_REPETITION; }
+        if (c == 0) { o.done = 1; o.reason = R_WINDOW_FULL; }
+        if (total == 0 && opp_chk) {  // 270-272
+            fs.meta |= M_DONE;
+            o.done = 1;
+            o.reward += 100;
+            o.reason = R_MATE;
+        }
+        if (!o.done && !white) fs.meta += (1u << M_MC_SHIFT);  // 291-292
+    }
+    const bool reset = live && autoreset && o.done;
+    if (reset) fs = icd->pos;
+    // boards outside the fast path (per-piece fallback): both kings checked (the pre-move
+    // board regenerates), or more own pieces than slots
+    const bool slow = live && !reset && (both || big);
+
+    // this role's 16 mask rows (Q0: and the castles word)
+    if (mrow && live) {
+        if (reset) {
+            const u64 iown = icd->own;
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                const int sq = 16 * RR + k;
+                const u64 w = ((iown >> sq) & 1) ? icd->slots[popc(iown & below(sq))] : 0ull;
+                __builtin_nontemporal_store(w, mrow + sq * N);
+            }
+        } else if (slow) {
+            apiq_slow_rows<RR>(fs, mrow, N);
+        } else {
+            const u64 fp = L.pawn5[0][l];
+            MoveSet pm;
+            pm.o1 = L.pawn5[1][l]; pm.o2 = L.pawn5[2][l]; pm.ol = L.pawn5[3][l]; pm.orr = L.pawn5[4][l];
+            int j = popc(g.own & below(16 * RR));
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                const int sq = 16 * RR + k;
+                if ((g.own >> sq) & 1) {
+                    const u64 w = ((fp >> sq) & 1) ? fast_pawn_targets(pm, sq, g.white) : scr.get(j & (SCRATCH_SLOTS - 1));
+                    __builtin_nontemporal_store(w, mrow + sq * N);
+                    j++;
+                }
+            }
+        }
+        if (RR == 0) {
+            const u32 cs = reset ? icd->castles : slow ? apiq_slow_castles(fs) : L.castles[l];
+            const bool cwh = reset ? icd->white != 0 : slow ? (fs.meta & M_WHITE) != 0 : g.white;
+            u64 cwd = 0;
+            if (cs & 1) cwd |= cwh ? (1ull << 1) : (1ull << 3);  // QS: 4097 / 4099
+            if (cs & 2) cwd |= cwh ? (1ull << 0) : (1ull << 2);  // KS: 4096 / 4098
+            mrow[64 * N] = cwd;
+        }
+    }
+    if (!live) return;
+    if (RR == 2) {  // the pick (action-id order: the mask's), the count, the env's next action
+        int tot = total;
+        uint16_t p = (uint16_t)A_NONE;
+        if (reset) {
+            tot = (int)C.rtotal;
+            p = (uint16_t)L.ra[l];  // (the quads run only with the start position's table)
+        } else if (slow) {
+            const u32 r = apiq_slow_pick(fs, L.x0[l]);
+            tot = (int)(r >> 16);
+            p = (uint16_t)(r & 0xFFFFu);
+        } else if (tot > 0) {
+            ms.fastp = L.pawn5[0][l]; ms.o1 = L.pawn5[1][l]; ms.o2 = L.pawn5[2][l];
+            ms.ol = L.pawn5[3][l]; ms.orr = L.pawn5[4][l];
+#pragma unroll
+            for (int b = 0; b < 5; b++) ms.cnt[b] = L.planes[0][b][l] | L.planes[1][b][l] | L.planes[2][b][l];
+            ms.total = tot;
+            ms.big = false;
+            g.castles = L.castles[l];
+            p = (uint16_t)select_action_swar(ns, g, ms, scr, (int)scale_rank(L.x0[l], (u32)tot));
+        }
+        if (out.cnt) out.cnt[i] = tot;
+        if (out.pick) {
+            const PairIO io = store_io(slab, nn);
+            d += tot > 0 ? 1u : 0u;
+            out.pick[i] = p;
+            io.act[i] = p;
+            io.draw[i] = d;
+        }
+    } else if (RR == 3) {
+        if (out.obs) write_obs(fs, out.obs + 64 * (size_t)i);
+    } else if (RR == 1) {
+        if (reset) h.bump_gen();
+        out.rw[i] = o.reward;
+        out.dn[i] = (uint8_t)o.done;
+        out.rs[i] = (uint8_t)o.reason;
+        h.commit();
+        const PairIO io = store_io(slab, nn);
+        io.store(i, fs);
+        h.flush(g0);
+        io.nsteps[i] = nst + 1;
+        io.reward[i] = o.reward;
+        io.done[i] = (uint8_t)o.done;
+        io.reason[i] = (uint8_t)o.reason;
+    }
+}
+
+// 16 argument dwords, as k_env_step_api2 (all preloaded)
+__global__ void __launch_bounds__(4 * QUAD_BOARDS * QUADS_WG) __attribute__((amdgpu_waves_per_eu(4)))
+    k_env_step_api4(uint8_t* __restrict__ slab, uint64_t seed, u64* __restrict__ htab,
+                    const uint16_t* __restrict__ racts, const EnvDev::InitCache* __restrict__ icd,
+                    const uint16_t* __restrict__ acts, const ApiOut* __restrict__ outp, int nn,
+                    u32 rinfo /* autoreset << 17 | ic.table << 16 | ic.total */) {
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int qw = wv >> 2;
+    const int role = (wv & 3) ^ ((qw & 1) ? GC_QXOR : 0);  // as k_env_rollout4: every SIMD a stateful + a stateless role
+    const int l = threadIdx.x & (QUAD_BOARDS - 1);
+    const int i = (blockIdx.x * QUADS_WG + qw) * QUAD_BOARDS + l;
+    ApiOut out = *outp;
+    asm volatile("" : "+s"(out.rw), "+s"(out.dn), "+s"(out.rs), "+s"(out.mask), "+s"(out.obs), "+s"(out.cnt),
+                 "+s"(out.pick));
+    switch (role) {
+        case 0: apiq_run<0>(slab, seed, htab, racts, icd, acts, out, nn, rinfo, qw, l, i); break;
+        case 1: apiq_run<1>(slab, seed, htab, racts, icd, acts, out, nn, rinfo, qw, l, i); break;
+        case 2: apiq_run<2>(slab, seed, htab, racts, icd, acts, out, nn, rinfo, qw, l, i); break;
+        default: apiq_run<3>(slab, seed, htab, racts, icd, acts, out, nn, rinfo, qw, l, i); break;
     }
 }
 
@@ -5239,7 +5639,11 @@ extern "C" int gc_env_step_device(gc_env* e, const uint16_t* d_actions, int32_t*
         const int k0 = api_streams < e->n_sub ? api_streams : e->n_sub;
         const int k = k0 < nb ? k0 : nb;
         const u32 ri = r.rinfo | ((u32)ar << 17);
-        if (k <= 1) {
+        static const bool no_quad = getenv("GC_NO_QUAD_API") && atoi(getenv("GC_NO_QUAD_API")) != 0;  // A/B: api2
+        if (!no_quad && k <= 1) {  // four waves per 64 boards (k_env_step_api4)
+            k_env_step_api4<<<(nb + QUADS_WG - 1) / QUADS_WG, 4 * QUAD_BOARDS * QUADS_WG, 0, e->stream>>>(
+                e->slab, d.seed, d.htab, r.racts, r.icd, d_actions, e->api_out, d.n, ri);
+        } else if (k <= 1) {
             k_env_step_api2<<<(nb + PAIRS_WG - 1) / PAIRS_WG, 2 * PAIR_BOARDS * PAIRS_WG, 0, e->stream>>>(
                 e->slab, d.seed, d.htab, r.racts, r.icd, d_actions, e->api_out, d.n, ri);
         } else {

@@ -41,9 +41,6 @@ def main():
     ap.add_argument("--random-inits", type=int, default=0,
                     help="instead: K random (also weird) initial boards, 4 096 boards each (tests/conftest.py)")
     a = ap.parse_args()
-    import oracle as O
-    from gym_chess_amd.env import BatchedChessEnv
-
     if a.api:
         return api_soak(a)
     if a.api_opp:
@@ -51,20 +48,13 @@ def main():
     n = a.boards
     inits = [None]
     rules = "fide" if a.fide else "reference"
-    if a.fide:
-        sys.path.insert(0, os.path.join(ROOT, "tests", "core_host"))
-        import corehost as H
-        from gym_chess_amd import codec as C
-
-        start = np.array(C.DEFAULT_BOARD, dtype=np.int8).reshape(64)
     if a.random_inits:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         from conftest import random_positions
 
         n = 4096
         inits = list(random_positions(a.random_inits, 977)[0])
-    idx = np.array(sorted(set(range(0, n, 1021 if n > 8192 else 131)) | set(range(64)) | set(range(n - 64, n)) |
-                          set(range(n // 2 - 16, n // 2 + 16))), dtype=np.int64)
+    idx = default_sample(n)
     threads = max(1, min(16, os.cpu_count() or 1))
     if a.fide:
         cases = [(0xF1DE + 7919 * k, "none", "WHITE", None) for k in range(a.seeds)]
@@ -74,53 +64,78 @@ def main():
         cases = [(1000 + 7919 * k, "none", "WHITE", None) for k in range(a.seeds)]
         cases += [(424242, "random", "WHITE", None), (434343, "random", "BLACK", None)]
     for seed, opp, color, ib in cases:
-        t0 = time.time()
-        env = BatchedChessEnv(n, device=0, seed=seed, opponent=opp, player_color=color, initial_board=ib,
-                              rules=rules)
-        tb = env.trace_buffer(a.chunk)
-        got = {k: [] for k in ("action", "reward", "done", "reason")}
-        for p in range(a.plies if a.launched else 0):
-            played = env.outputs()["next_action"].astype(np.int32)[idx]
-            env.step_random(1)
-            o = env.outputs()
-            got["action"].append(np.where(played == 0xFFFF, -1, played)[None])
-            for key in ("reward", "done", "reason"):
-                got[key].append(o[key][idx][None])
-        for p in range(0, 0 if a.launched else a.plies, a.chunk):
-            k = min(a.chunk, a.plies - p)
-            env.rollout_device(k, tb)
-            env.synchronize()
-            tr = tb.fetch(k)
-            for key in got:
-                got[key].append(tr[key][:, idx])
-        b, m = env.boards()
-        spill = env.spill_info() if color == "BLACK" else None
-        tb.close()
-        env.close()
-        kw = dict(opponent=1 if opp == "random" else 0, agent_white=color == "WHITE")
-        if ib is not None:
-            kw["init"] = ib
-        with ThreadPoolExecutor(threads) as ex:
-            if a.fide:  # the host build's trace (no final state: the boards are compared by trace only)
-                refs = list(ex.map(lambda i: H.fide_rollout(seed, int(i), a.plies, start), idx))
-            else:
-                refs = list(ex.map(lambda i: O.rollout_trace(seed, int(i), a.plies, **kw), idx))
-        bad = []
-        for key in got:
-            g = np.concatenate(got[key], axis=0)
-            w = np.stack([r[key][: a.plies] for r in refs], axis=1)
-            for p_, j in np.argwhere(g != w)[:4]:
-                bad.append((key, int(p_), int(idx[j])))
-        for j, i in enumerate(idx if not a.fide else []):
-            if not ((b[i] == refs[j]["final_board"]).all() and list(m[i]) == list(refs[j]["final_meta"])):
-                bad.append(("final", a.plies, int(i)))
-                break
+        bad, spill, secs = fused_case(seed, opp, color, ib, a.plies, a.chunk, n, idx, rules, a.launched, threads)
         print(json.dumps({"seed": seed, "form": "launched" if a.launched else "fused", "rules": rules,
                           "opponent": opp, "color": color, "boards": n, "plies": a.plies,
                           "sampled": len(idx), "mismatches": bad[:8], "spill": spill,
-                          "seconds": round(time.time() - t0, 1)}), flush=True)
+                          "seconds": secs}), flush=True)
         if bad:
             sys.exit(1)
+
+
+def default_sample(n):
+    """strided boards + the first / last 64 + the middle 32"""
+    return np.array(sorted(set(range(0, n, 1021 if n > 8192 else 131)) | set(range(64)) | set(range(n - 64, n)) |
+                           set(range(n // 2 - 16, n // 2 + 16))), dtype=np.int64)
+
+
+def fused_case(seed, opp, color, ib, plies, chunk, n, idx, rules="reference", launched=False, threads=16):
+    """One soak case: n boards x plies of device random self-play (fused launches of `chunk`
+    plies with the per-ply trace, or one launch per ply) against the oracle driver (the host
+    build of gc_fide.h for rules="fide") on the sampled boards idx.  Returns (mismatches
+    [(what, ply, board)], the spill table's info for a BLACK agent, seconds)."""
+    import oracle as O
+    from gym_chess_amd.env import BatchedChessEnv
+
+    fide = rules == "fide"
+    if fide:
+        sys.path.insert(0, os.path.join(ROOT, "tests", "core_host"))
+        import corehost as H
+        from gym_chess_amd import codec as C
+
+        start = np.array(C.DEFAULT_BOARD, dtype=np.int8).reshape(64)
+    t0 = time.time()
+    env = BatchedChessEnv(n, device=0, seed=seed, opponent=opp, player_color=color, initial_board=ib, rules=rules)
+    tb = env.trace_buffer(chunk)
+    got = {k: [] for k in ("action", "reward", "done", "reason")}
+    for p in range(plies if launched else 0):
+        played = env.outputs()["next_action"].astype(np.int32)[idx]
+        env.step_random(1)
+        o = env.outputs()
+        got["action"].append(np.where(played == 0xFFFF, -1, played)[None])
+        for key in ("reward", "done", "reason"):
+            got[key].append(o[key][idx][None])
+    for p in range(0, 0 if launched else plies, chunk):
+        k = min(chunk, plies - p)
+        env.rollout_device(k, tb)
+        env.synchronize()
+        tr = tb.fetch(k)
+        for key in got:
+            got[key].append(tr[key][:, idx])
+        del tr
+    b, m = env.boards()
+    spill = env.spill_info() if color == "BLACK" else None
+    tb.close()
+    env.close()
+    kw = dict(opponent=1 if opp == "random" else 0, agent_white=color == "WHITE")
+    if ib is not None:
+        kw["init"] = ib
+    with ThreadPoolExecutor(threads) as ex:
+        if fide:  # the host build's trace (no final state: the boards are compared by trace only)
+            refs = list(ex.map(lambda i: H.fide_rollout(seed, int(i), plies, start), idx))
+        else:
+            refs = list(ex.map(lambda i: O.rollout_trace(seed, int(i), plies, **kw), idx))
+    bad = []
+    for key in got:
+        g = np.concatenate(got[key], axis=0)
+        w = np.stack([r[key][:plies] for r in refs], axis=1)
+        for p_, j in np.argwhere(g != w)[:4]:
+            bad.append((key, int(p_), int(idx[j])))
+    for j, i in enumerate(idx if not fide else []):
+        if not ((b[i] == refs[j]["final_board"]).all() and list(m[i]) == list(refs[j]["final_meta"])):
+            bad.append(("final", plies, int(i)))
+            break
+    return bad, spill, round(time.time() - t0, 1)
 
 
 def api_soak(a):
