@@ -12,6 +12,7 @@
 // (v_bfrev_b32 x2), line masks are computed arithmetically, so one lane = one board
 // needs no LDS and no cache traffic beyond its own state.
 #pragma once
+#include <type_traits>
 #include <stdint.h>
 
 #if defined(__HIPCC__)
@@ -775,14 +776,25 @@ struct NoScratch {  // count-only callers (perft leaves): no parking, no count p
 
 GC_HD int ordinal(u64 own, int sq) { return popc(own & below(sq)); }
 
+// a scratch type may keep its own per-piece counts (kPlanes = false: no bit-sliced planes)
+template <class S, class = void>
+struct planes_of {
+    static constexpr bool value = S::kPark;
+};
+template <class S>
+struct planes_of<S, decltype((void)S::kPlanes)> {
+    static constexpr bool value = S::kPlanes;
+};
 template <class S>
 GC_HD void park(MoveSet& ms, S& scr, u64 own, int sq, u64 tg, int& total) {
     int c = popc(tg);
     total += c;
     if (S::kPark) {
         scr.put(ordinal(own, sq), tg);
+        if (planes_of<S>::value) {
 #pragma unroll
-        for (int b = 0; b < 5; b++) ms.cnt[b] |= (u64)((c >> b) & 1) << sq;  // no VCC select
+            for (int b = 0; b < 5; b++) ms.cnt[b] |= (u64)((c >> b) & 1) << sq;  // no VCC select
+        }
     }
 }
 
@@ -844,7 +856,7 @@ GC_HD int gen_pawns(const Pos& s, const Gen& g, MoveSet& ms, S& scr, const FideE
     }
     ms.fastp = fp;
     total += popc(ms.o1) + popc(ms.o2) + popc(ms.ol) + popc(ms.orr);
-    if (S::kPark) {  // per-pawn counts o1+o2+ol+orr (0..4) as a bit-sliced sum
+    if (planes_of<S>::value) {  // per-pawn counts o1+o2+ol+orr (0..4) as a bit-sliced sum
         u64 s1 = ms.o1 ^ ms.o2, c1 = ms.o1 & ms.o2, s2 = ms.ol ^ ms.orr, c2 = ms.ol & ms.orr;
         u64 b0 = s1 ^ s2, k0 = s1 & s2;
         ms.cnt[0] |= b0;
@@ -1409,8 +1421,7 @@ GC_HD bool quick_legal(const Pos& s, int action) {
     if (action < 0 || action > A_RESIGN) return false;
     Gen g;
     gen_base(s, g);
-    if (action >= 4096) {
-        gen_pins(s, g);
+    if (action >= 4096) {  // (castles read the enemy map, not the pins)
         gen_enemy(s, g);
         return action_legal(s, g, action);
     }
@@ -1420,6 +1431,56 @@ GC_HD bool quick_legal(const Pos& s, int action) {
     if (ty == KING) return ((king_set(bit(f)) & ~g.own) >> t & 1) && !sq_attacked(s, t, !g.white);
     gen_pins(s, g);
     return (legal_targets(s, g, f, ty) >> t) & 1;
+}
+
+// quick_legal in two independent halves (the quad API step validates on two waves at once):
+// quick_legal(s, a) == quick_pseudo(s, a) && quick_safe(s, a) for every action a.
+//  * quick_pseudo: the action id is in range, castles fully (action_legal), else the from-square
+//    holds an own piece and the target is among its pseudo targets -- every piece type tested
+//    branch-free (lanes hold different types: a switch would run every case), sliders by the
+//    line and the squares strictly between; a king's step without the attack test;
+//  * quick_safe: a king step's target not attacked (sq_attacked: the map with the king still on
+//    its square, Q6); any other move inside the check mask and on its pin segment; castles and
+//    out-of-range ids true (quick_pseudo decides them).
+GC_HD bool quick_pseudo(const Pos& s, int action) {
+    if (action < 0 || action > A_RESIGN) return false;
+    Gen g;
+    gen_base(s, g);
+    if (action >= 4096) {  // (castles read the enemy map, not the pins)
+        gen_enemy(s, g);
+        return action_legal(s, g, action);
+    }
+    const int f = action >> 6, t = action & 63;
+    const u64 fb = bit(f), tb = bit(t);
+    const int ty = type_at(s, f);
+    const int df = (t & 7) - (f & 7), dr = (t >> 3) - (f >> 3);
+    const bool orth = (df == 0) != (dr == 0);
+    const bool dia = df != 0 && (df == dr || df == -dr);
+    const bool clear = (between(f, t) & g.occ) == 0;
+    const u64 empty = ~g.occ;
+    // pawns (lib.rs:935-958): one step, two from the start row (Q1: the destination only), a
+    // diagonal capture of any enemy piece
+    const u64 push = g.white ? (((fb >> 8) | ((fb & ROW6) >> 16)) & empty) : (((fb << 8) | ((fb & ROW1) << 16)) & empty);
+    const u64 pawn = push | (pawn_att_set(fb, g.white) & g.opp);
+    const u64 leap = (ty == KNIGHT ? knight_set(fb) : king_set(fb)) & ~g.own;
+    const bool ok = ty == PAWN ? (pawn & tb) != 0
+                  : (ty == KNIGHT || ty == KING) ? (leap & tb) != 0
+                  : ty == QUEEN ? (orth || dia) && clear
+                  : ty == ROOK ? orth && clear
+                  : ty == BISHOP ? dia && clear : false;
+    return ((g.own >> f) & 1) && ok && (ty == PAWN || !(g.own & tb));
+}
+GC_HD bool quick_safe(const Pos& s, int action) {
+    if (action < 0 || action >= 4096) return true;
+    const int f = action >> 6, t = action & 63;
+    Gen g;
+    gen_base(s, g);
+    if (type_at(s, f) == KING) return !sq_attacked(s, t, !g.white);
+    gen_pins(s, g);
+    if (g.ks < 0) return true;
+    u64 tg = g.checkmask;
+    if (g.pinned & bit(f)) tg &= g.pinrays & line_through(g.ks, f) & king_side(g.ks, f);
+    return (tg >> t) & 1;
 }
 
 // ---- transition: next_state (lib.rs:679-784) ------------------------------------------

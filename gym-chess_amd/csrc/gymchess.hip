@@ -3004,20 +3004,27 @@ __device__ __forceinline__ u64 bits_to_bytes(u32 b) {
     u64 y = ((u64)(b & 0xFFu) * 0x0101010101010101ull) & 0x8040201008040201ull;
     return ((y + 0x7F7F7F7F7F7F7F7Full) >> 7) & 0x0101010101010101ull;
 }
-// int8 mailbox of the position (lib.rs:41-50 ids), 8 words of 8 squares: ids summed per
-// byte from the type planes, black bytes negated in two's complement without carries
+// 4 bits of b -> the 4 bytes of a word (bit j -> byte j, value 0/1), in 32-bit arithmetic
+__device__ __forceinline__ u32 nib_to_bytes(u32 b) {
+    const u32 y = ((b & 0xFu) * 0x01010101u) & 0x08040201u;
+    return ((y + 0x7F7F7F7Fu) >> 7) & 0x01010101u;
+}
+// int8 mailbox of the position (lib.rs:41-50 ids), 16 words of 4 squares: the id's three bits
+// as three planes (K 1, Q 2, R 3, B 4, N 5, P 6), each spread to bytes and weighted, black
+// bytes negated in two's complement (no byte overflows: every byte <= 6)
+__device__ __forceinline__ u32 obs_word(u64 b0, u64 b1, u64 b2, u64 blk, int sh) {
+    const u32 v = nib_to_bytes((u32)(b0 >> sh)) + (nib_to_bytes((u32)(b1 >> sh)) << 1) +
+                  (nib_to_bytes((u32)(b2 >> sh)) << 2);
+    const u32 b = nib_to_bytes((u32)(blk >> sh));
+    return (v ^ (b * 0xFFu)) + b;
+}
 __device__ void write_obs(const Pos& s, int8_t* __restrict__ out) {
     u64* o = reinterpret_cast<u64*>(out);
-    const u64 occ = occ_of(s), blk = occ & ~s.w;
+    const u64 b0 = s.k | s.r | s.n, b1 = s.q | s.r | s.p, b2 = s.b | s.n | s.p;
+    const u64 blk = occ_of(s) & ~s.w;
 #pragma unroll
-    for (int r = 0; r < 8; r++) {
-        const int sh = 8 * r;
-        u64 v = bits_to_bytes((u32)(s.k >> sh)) * KING + bits_to_bytes((u32)(s.q >> sh)) * QUEEN +
-                bits_to_bytes((u32)(s.r >> sh)) * ROOK + bits_to_bytes((u32)(s.b >> sh)) * BISHOP +
-                bits_to_bytes((u32)(s.n >> sh)) * KNIGHT + bits_to_bytes((u32)(s.p >> sh)) * PAWN;
-        u64 b = bits_to_bytes((u32)(blk >> sh));
-        o[r] = (v ^ (b * 0xFFull)) + b;  // -id = ~id + 1 per black byte (no byte overflows)
-    }
+    for (int r = 0; r < 8; r++)
+        o[r] = (u64)obs_word(b0, b1, b2, blk, 8 * r) | ((u64)obs_word(b0, b1, b2, blk, 8 * r + 4) << 32);
 }
 
 template <bool OPP>
@@ -3275,20 +3282,21 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
 //
 //   phase 0   Q0: applies the action (speculatively: it is validated beside it)
 //             Q1: the window probe of the pre-move board, the Philox word, the reset-table pick
-//             Q2: validates the action (quick_legal, chess_v2.py:240-242)
+//             Q2, Q3: validate the action (chess_v2.py:240-242), quick_legal in two halves:
+//                 Q3 the move's shape (quick_pseudo), Q2 the king's safety (quick_safe)
 //   phase 1   Q0: checkers, check mask, pins                  Q1: the mover's own check flag
 //             Q2: enemy leaper + orthogonal slider attacks    Q3: enemy diagonal slider attacks
-//             every role: zero words of its mask rows for the squares the next side does not
-//             occupy (most of the mask, written while the chains run)
-//   phase 2   Q0: castles, pawns (set-wise), knights          Q1: the 3-fold commit
-//             Q2: kings, queens                               Q3: rooks, bishops
+//   phase 2   Q0: castles, pawns (set-wise; every pawn's targets parked too)
+//             Q1: knights, kings, then the 3-fold commit (its probe lands meanwhile)
+//             Q2: queens, bishops                             Q3: rooks
 //             (pieces parked per ordinal in LDS with bit-sliced counts, as gen_moves)
 //   phase 3   every role: the step's outcome (identical arithmetic on the same LDS data) and
-//             its 16 mask rows of the occupied squares (a reset board: the start position's
+//             its 16 mask rows, each written once, whole (a reset board: the start position's
 //             rows, from the init cache); Q2: the pick (action-id order), the count, the env's
 //             next action; Q3: the observation; Q1: the outputs, the state and the window.
-// A mask row is written only by the role that owns its square, in program order, so a row
-// zeroed in phase 1 and rewritten in phase 3 (a reset board) needs no fence.  Boards outside
+// A mask row is written only by the role that owns its square.  (Zeroing the unoccupied
+// squares' rows in phase 1 instead, GC_APIQ_EARLY: partial rows written twice, 28.4 vs 18.5 us
+// per launch.)  Boards outside
 // the fast path -- > 16 own pieces, or both kings checked after the move (the move is void and
 // the pre-move board regenerates) -- take the per-piece fallback (legal_targets) in phase 3,
 // each role for its own rows.  Quad roles run only with the start position's pick table, as
@@ -3299,20 +3307,30 @@ struct ApiQuadLds {
     u32 nmeta[QUAD_BOARDS];
     int32_t mr[QUAD_BOARDS];                //           its capture reward
     u32 irrev[QUAD_BOARDS];                 //           irreversible move
-    u32 valid[QUAD_BOARDS];                 // Q2 -> all: the action is legal
+    u32 valid[2][QUAD_BOARDS];              // Q3 ([0]: its shape), Q2 ([1]: king safety) -> all
     u64 pin3[3][QUAD_BOARDS];               // Q0 -> Q2, Q3: check mask, pinned, pin rays
     u32 f0[QUAD_BOARDS];                    // Q0 -> all: the side to move is in check
     u64 enemy[3][QUAD_BOARDS];              // Q2 ([1]), Q3 ([2]) -> Q0, Q2, Q3: the enemy map's parts
     u32 f1[QUAD_BOARDS];                    // Q1 -> all: the mover is in check after its move
-    u64 planes[3][5][QUAD_BOARDS];          // Q0 / Q2 / Q3 -> Q2: bit-sliced per-square counts
+    u64 cbw[4][2][QUAD_BOARDS];             // per role -> Q2: its pieces' move counts, a byte per ordinal
     u32 part[4][QUAD_BOARDS];               // move totals (Q0's holds the castles; Q3's a big board's)
-    u64 pawn5[5][QUAD_BOARDS];              // Q0 -> all: fast pawns and their origin sets
     u32 castles[QUAD_BOARDS];               // Q0 -> all
     u32 rep[QUAD_BOARDS];                   // Q1 -> all: 3-fold count | window length << 8
     u32 x0[QUAD_BOARDS];                    // Q1 -> Q2: the Philox word of the draw
     u32 ra[QUAD_BOARDS];                    // Q1 -> Q2: the start-position table pick
 };
 __shared__ ApiQuadLds g_apiq_lds[QUADS_WG];
+#ifndef GC_APIQ_EARLY
+#define GC_APIQ_EARLY 0  // 1: rows of unoccupied squares zeroed in phase 1 (partial rows written twice:
+                         // 28.4 us per launch; non-temporal or not alike), 0: every row once in phase 3 (18.5)
+#endif
+#ifndef GC_APIQ_NT
+#define GC_APIQ_NT 1     // the mask rows as non-temporal stores
+#endif
+__device__ __forceinline__ void apiq_store(u64* p, u64 v) {
+    if (GC_APIQ_NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
 
 // the 16 mask rows of role R that the next side does not occupy: zero (streamed)
 template <int R>
@@ -3320,8 +3338,43 @@ __device__ __forceinline__ void apiq_zero_rows(u64* __restrict__ o, size_t N, u6
 #pragma unroll
     for (int k = 0; k < 16; k++) {
         const int sq = 16 * R + k;
-        if (!((own >> sq) & 1)) __builtin_nontemporal_store(0ull, o + sq * N);
+        if (!((own >> sq) & 1)) apiq_store(o + sq * N, 0ull);
     }
+}
+
+// Parked targets by own-piece ordinal in LDS (slot j of lane l at base[j * 64]), and each piece's
+// move count as byte j of two words: the pick in action-id order (ascending from-square, the
+// ordinals' order, then target) finds the piece by byte prefix sums instead of the bit-sliced
+// per-square count planes (5 more 64-bit updates per piece, kPlanes)
+struct OrdScratch {
+    static constexpr bool kPark = true;
+    static constexpr bool kPlanes = false;
+    u64* base;
+    u64 c0, c1;
+    __device__ void put(int j, u64 v) {
+        base[j * QUAD_BOARDS] = v;
+        const u64 add = (u64)popc(v) << (8 * (j & 7));
+        c0 |= j < 8 ? add : 0ull;
+        c1 |= j < 8 ? 0ull : add;
+    }
+    __device__ u64 get(int j) const { return base[j * QUAD_BOARDS]; }
+};
+// the k-th (< normal) non-castle move in action-id order from the ordinal byte counts
+__device__ __forceinline__ int ord_pick(const OrdScratch& scr, u64 own, u64 c0, u64 c1, int normal, int k) {
+    int j;
+    if (normal < 256) {
+        const u64 cw[4] = {c0, c1, 0ull, 0ull};
+        j = sw_locate(cw, k);
+    } else {  // (never in play: byte prefix sums would overflow)
+#pragma unroll 1
+        for (j = 0; j < SCRATCH_SLOTS - 1; j++) {
+            const int c = (int)(((j < 8 ? c0 : c1) >> (8 * (j & 7))) & 0xFF);
+            if (k < c) break;
+            k -= c;
+        }
+    }
+    const int sq = kth_set_bit(own, j);
+    return sq * 64 + kth_set_bit(scr.get(j), k);
 }
 
 // The per-piece fallback of one board (apiq_run: both kings checked, or > 16 own pieces), each
@@ -3333,7 +3386,7 @@ __device__ __noinline__ void apiq_slow_rows(Pos b, u64* __restrict__ o, size_t N
     for (int k = 0; k < 16; k++) {
         const int sq = 16 * R + k;
         const u64 w = ((g.own >> sq) & 1) ? legal_targets(b, g, sq, type_at(b, sq)) : 0ull;
-        __builtin_nontemporal_store(w, o + sq * N);
+        apiq_store(o + sq * N, w);
     }
 }
 __device__ __noinline__ u32 apiq_slow_castles(Pos b) {
@@ -3369,15 +3422,28 @@ __device__ __forceinline__ void apiq_run(uint8_t* __restrict__ slab, uint64_t se
     const PairCtx C = {seed, htab, in_io.hgen, racts, icd, (rinfo >> 16) != 0, rinfo & 0xFFFFu};
     // every role reads the pre-move board and the action (the stateless roles decide the outcome
     // and the fallback boards themselves); Q1 / Q2 the draw counter, Q1 the window and step counter
+#ifdef GC_PSTAMPS
+    const unsigned long long pst_entry = __builtin_amdgcn_s_memrealtime();
+    if (l == 0) {
+        for (int k = 0; k < 8; k++) gc_pst[threadIdx.x >> 6][k] = 0;
+        gc_pst[threadIdx.x >> 6][8] = __builtin_amdgcn_s_memtime();
+    }
+#endif
     Pos s = in_io.load(ii);
     u32 ua = acts[ii], g0 = 0, nst = 0, d = 0;
     if (RR == 1) { g0 = in_io.hgen[ii]; nst = in_io.nsteps[ii]; }
     if (RR == 1 || RR == 2) d = in_io.draw[ii];
     pin(s); pin(ua); pin(g0); pin(nst); pin(d);
+    PST(7);  // (GC_PSTAMPS: segment 7 = the entry loads; 0-6 phase 0, wait A, ..., phase 3)
+#ifdef GC_PSTAMPS
+    const unsigned long long pst_rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
     const int a = (int)ua;
     DevHist h = DevHist{htab, in_io.hgen, g0, ii, HTAB_BITS};
-    PairScratch scr{&L.slots[0][l]};
-    if (RR < 2) __builtin_amdgcn_s_setprio(2);  // the state-carrying roles' chains are the longer
+    OrdScratch scr{&L.slots[0][l], 0ull, 0ull};
+    // issue priority: the state-carrying roles' chains are the longer; Q2 (a validation half,
+    // on Q0's SIMDs) level with Q0 in phase 0
+    if (RR != 3) __builtin_amdgcn_s_setprio(2);
     const bool done0 = (s.meta & M_DONE) != 0;   // chess_v2.py:245-251
     const bool cap = mc_of(s.meta) > MOVES_MAX;  // 252-258
     const bool white = (s.meta & M_WHITE) != 0;
@@ -3403,12 +3469,17 @@ __device__ __forceinline__ void apiq_run(uint8_t* __restrict__ slab, uint64_t se
         if (C.rtable) ra = C.racts[scale_rank(x0, C.rtotal)];
         L.x0[l] = x0;
     } else if (RR == 2) {
-        L.valid[l] = quick_legal(s, a) ? 1u : 0u;
+        L.valid[1][l] = quick_safe(s, a) ? 1u : 0u;
+    } else {
+        L.valid[0][l] = quick_pseudo(s, a) ? 1u : 0u;
     }
+    PST(0);
     pair_barrier();
+    PST(1);
 
     // ---- phase 1
-    const bool valid = L.valid[l] != 0;
+    if (RR == 2) __builtin_amdgcn_s_setprio(0);
+    const bool valid = (L.valid[0][l] & L.valid[1][l]) != 0;
     const bool mv = pre && valid;  // env_ply runs
     Pos ns = s;                    // the position generated for: post-move, or s itself
     ns.meta = (ns.meta & ~(u32)M_RIGHTS) | eff_rights(s);
@@ -3433,8 +3504,10 @@ __device__ __forceinline__ void apiq_run(uint8_t* __restrict__ slab, uint64_t se
         L.enemy[2][l] = g.ks >= 0 ? side_attacks_diag(ns, !g.white) : 0ull;
     }
     u64* const mrow = out.mask ? out.mask + ii : nullptr;
-    if (mrow && live) apiq_zero_rows<RR>(mrow, N, g.own);
+    if (GC_APIQ_EARLY && mrow && live) apiq_zero_rows<RR>(mrow, N, g.own);
+    PST(2);
     pair_barrier();
+    PST(3);
 
     // ---- phase 2
     const bool opp_chk = L.f0[l] != 0, my_chk = L.f1[l] != 0;
@@ -3451,18 +3524,26 @@ __device__ __forceinline__ void apiq_run(uint8_t* __restrict__ slab, uint64_t se
     MoveSet ms;
     moveset_clear(ms);
     int part = 0;
-    if (RR == 0) {  // castles (counted here), pawns, knights
+    if (RR == 0) {  // castles (counted here), pawns: the fast ones' targets parked as well
         gen_castles(ns, g);
         if (gen && !big) {
-            part = gen_pawns(ns, g, ms, scr) + gen_knights(ns, g, ms, scr) + popc(g.castles);
-#pragma unroll
-            for (int b = 0; b < 5; b++) L.planes[0][b][l] = ms.cnt[b];
+            part = gen_pawns(ns, g, ms, scr) + popc(g.castles);
+            for (u64 fp = ms.fastp; fp; fp &= fp - 1) {
+                const int sq = ctz(fp);
+                scr.put(ordinal(g.own, sq), fast_pawn_targets(ms, sq, g.white));
+            }
         }
-        L.pawn5[0][l] = ms.fastp; L.pawn5[1][l] = ms.o1; L.pawn5[2][l] = ms.o2;
-        L.pawn5[3][l] = ms.ol; L.pawn5[4][l] = ms.orr;
+        L.cbw[0][0][l] = scr.c0;
+        L.cbw[0][1][l] = scr.c1;
         L.castles[l] = g.castles;
         L.part[0][l] = (u32)part;
-    } else if (RR == 1) {
+    } else if (RR == 1) {  // knights, kings (while the probe lands), the 3-fold commit
+        if (gen && !big) {
+            part = gen_knights(ns, g, ms, scr) + gen_kings(ns, g, ms, scr);
+        }
+        L.cbw[1][0][l] = scr.c0;
+        L.cbw[1][1][l] = scr.c1;
+        L.part[1][l] = (u32)part;
         int c = 0;
         u32 hl = hl_of(s.meta);
         if (mv && !both) {
@@ -3472,32 +3553,34 @@ __device__ __forceinline__ void apiq_run(uint8_t* __restrict__ slab, uint64_t se
         }
         L.rep[l] = (u32)c | (hl << 8);
         L.ra[l] = ra;
-    } else if (RR == 2) {  // kings, queens
+    } else if (RR == 2) {  // queens, bishops
         if (gen && !big) {
-            part = gen_kings(ns, g, ms, scr) + gen_sliders<QUEEN>(ns, g, ms, scr);
-#pragma unroll
-            for (int b = 0; b < 5; b++) L.planes[1][b][l] = ms.cnt[b];
+            part = gen_sliders<QUEEN>(ns, g, ms, scr) + gen_sliders<BISHOP>(ns, g, ms, scr);
         }
+        L.cbw[2][0][l] = scr.c0;
+        L.cbw[2][1][l] = scr.c1;
         L.part[2][l] = (u32)part;
-    } else {  // rooks, bishops; a big board's whole count
+    } else {  // rooks; a big board's whole count
         if (gen && !big) {
-            part = gen_sliders<ROOK>(ns, g, ms, scr) + gen_sliders<BISHOP>(ns, g, ms, scr);
-#pragma unroll
-            for (int b = 0; b < 5; b++) L.planes[2][b][l] = ms.cnt[b];
+            part = gen_sliders<ROOK>(ns, g, ms, scr);
         } else if (gen) {
             gen_castles(ns, g);
             part = count_legal(ns, g);
         }
+        L.cbw[3][0][l] = scr.c0;
+        L.cbw[3][1][l] = scr.c1;
         L.part[3][l] = (u32)part;
     }
+    PST(4);
     pair_barrier();
+    PST(5);
 
     // ---- phase 3: the outcome, as k_env_step_api2 (every role: identical arithmetic)
 #ifndef GC_NO_QPRIO_DYN
     if (RR == 0) __builtin_amdgcn_s_setprio(0);
     if (RR == 2) __builtin_amdgcn_s_setprio(2);  // the pick: this phase's longest chain
 #endif
-    const int total = gen ? (int)(L.part[0][l] + L.part[2][l] + L.part[3][l]) : 0;
+    const int total = gen ? (int)(L.part[0][l] + L.part[1][l] + L.part[2][l] + L.part[3][l]) : 0;
     const u32 rpk = L.rep[l];
     const int c = (int)(rpk & 0xFFu);
     const u32 hl = rpk >> 8;
@@ -3547,23 +3630,21 @@ __device__ __forceinline__ void apiq_run(uint8_t* __restrict__ slab, uint64_t se
             for (int k = 0; k < 16; k++) {
                 const int sq = 16 * RR + k;
                 const u64 w = ((iown >> sq) & 1) ? icd->slots[popc(iown & below(sq))] : 0ull;
-                __builtin_nontemporal_store(w, mrow + sq * N);
+                apiq_store(mrow + sq * N, w);
             }
         } else if (slow) {
             apiq_slow_rows<RR>(fs, mrow, N);
-        } else {
-            const u64 fp = L.pawn5[0][l];
-            MoveSet pm;
-            pm.o1 = L.pawn5[1][l]; pm.o2 = L.pawn5[2][l]; pm.ol = L.pawn5[3][l]; pm.orr = L.pawn5[4][l];
+        } else {  // every own piece's targets are parked (pawns too): one LDS read per row
             int j = popc(g.own & below(16 * RR));
 #pragma unroll
             for (int k = 0; k < 16; k++) {
                 const int sq = 16 * RR + k;
-                if ((g.own >> sq) & 1) {
-                    const u64 w = ((fp >> sq) & 1) ? fast_pawn_targets(pm, sq, g.white) : scr.get(j & (SCRATCH_SLOTS - 1));
-                    __builtin_nontemporal_store(w, mrow + sq * N);
-                    j++;
+                const bool own = (g.own >> sq) & 1;
+                if (own || !GC_APIQ_EARLY) {  // (without the early zeros: every row, each once)
+                    const u64 w = scr.get(j & (SCRATCH_SLOTS - 1));
+                    apiq_store(mrow + sq * N, own ? w : 0ull);
                 }
+                j += own ? 1 : 0;
             }
         }
         if (RR == 0) {
@@ -3575,8 +3656,10 @@ __device__ __forceinline__ void apiq_run(uint8_t* __restrict__ slab, uint64_t se
             mrow[64 * N] = cwd;
         }
     }
-    if (!live) return;
-    if (RR == 2) {  // the pick (action-id order: the mask's), the count, the env's next action
+#ifdef GC_PSTAMPS
+    const unsigned long long pst_rt1 = __builtin_amdgcn_s_memrealtime();
+#endif
+    if (live && RR == 2) {  // the pick (action-id order: the mask's), the count, the env's next action
         int tot = total;
         uint16_t p = (uint16_t)A_NONE;
         if (reset) {
@@ -3586,15 +3669,17 @@ __device__ __forceinline__ void apiq_run(uint8_t* __restrict__ slab, uint64_t se
             const u32 r = apiq_slow_pick(fs, L.x0[l]);
             tot = (int)(r >> 16);
             p = (uint16_t)(r & 0xFFFFu);
-        } else if (tot > 0) {
-            ms.fastp = L.pawn5[0][l]; ms.o1 = L.pawn5[1][l]; ms.o2 = L.pawn5[2][l];
-            ms.ol = L.pawn5[3][l]; ms.orr = L.pawn5[4][l];
-#pragma unroll
-            for (int b = 0; b < 5; b++) ms.cnt[b] = L.planes[0][b][l] | L.planes[1][b][l] | L.planes[2][b][l];
-            ms.total = tot;
-            ms.big = false;
-            g.castles = L.castles[l];
-            p = (uint16_t)select_action_swar(ns, g, ms, scr, (int)scale_rank(L.x0[l], (u32)tot));
+        } else if (tot > 0) {  // castles last (KS 4096 / 4098 before QS 4097 / 4099)
+            const u32 cs = L.castles[l];
+            const int normal = tot - popc(cs);
+            int k = (int)scale_rank(L.x0[l], (u32)tot);
+            if (k < normal) {
+                p = (uint16_t)ord_pick(scr, g.own, L.cbw[0][0][l] | L.cbw[1][0][l] | L.cbw[2][0][l] | L.cbw[3][0][l],
+                                       L.cbw[0][1][l] | L.cbw[1][1][l] | L.cbw[2][1][l] | L.cbw[3][1][l], normal, k);
+            } else {
+                k -= normal;
+                p = (cs & 2) && k == 0 ? (uint16_t)(g.white ? A_KSW : A_KSB) : (uint16_t)(g.white ? A_QSW : A_QSB);
+            }
         }
         if (out.cnt) out.cnt[i] = tot;
         if (out.pick) {
@@ -3604,9 +3689,9 @@ __device__ __forceinline__ void apiq_run(uint8_t* __restrict__ slab, uint64_t se
             io.act[i] = p;
             io.draw[i] = d;
         }
-    } else if (RR == 3) {
+    } else if (live && RR == 3) {
         if (out.obs) write_obs(fs, out.obs + 64 * (size_t)i);
-    } else if (RR == 1) {
+    } else if (live && RR == 1) {
         if (reset) h.bump_gen();
         out.rw[i] = o.reward;
         out.dn[i] = (uint8_t)o.done;
@@ -3620,6 +3705,17 @@ __device__ __forceinline__ void apiq_run(uint8_t* __restrict__ slab, uint64_t se
         io.done[i] = (uint8_t)o.done;
         io.reason[i] = (uint8_t)o.reason;
     }
+#ifdef GC_PSTAMPS
+    PST(6);
+    if (g_pst_out != nullptr && l == 0) {  // (tools/api_pstamp_probe.py)
+        const size_t w = (size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+        for (int k = 0; k < 8; k++) g_pst_out[w * 12 + k] = gc_pst[threadIdx.x >> 6][k];
+        g_pst_out[w * 12 + 8] = pst_entry;
+        g_pst_out[w * 12 + 9] = pst_rt0;
+        g_pst_out[w * 12 + 10] = pst_rt1;
+        g_pst_out[w * 12 + 11] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
 }
 
 // 16 argument dwords, as k_env_step_api2 (all preloaded)
@@ -6279,6 +6375,26 @@ extern "C" int gc_debug_pstamps(gc_env* e, int n_plies, uint64_t* out /* waves *
     unsigned long long* z = nullptr;
     HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_pst_out), &z, sizeof(z)));
     (void)hipFree(d);
+    return 0;
+}
+#endif
+
+#ifdef GC_PSTAMPS
+// the quad API step's per-wave stamps (tools/api_pstamp_probe.py): buffer on (`on` != 0, sized
+// for the env's k_env_step_api4 waves, zeroed) or copied out and off
+static unsigned long long* g_api_pst = nullptr;
+extern "C" int gc_debug_api_pstamps(gc_env* e, int on, uint64_t* out /* waves * 12 */) {
+    const size_t waves = (size_t)((e->n + QUAD_BOARDS * QUADS_WG - 1) / (QUAD_BOARDS * QUADS_WG)) * 4 * QUADS_WG;
+    HIPCHK(hipStreamSynchronize(e->stream));
+    if (on) {
+        if (!g_api_pst && dalloc(&g_api_pst, waves * 12)) return -1;
+        HIPCHK(hipMemset(g_api_pst, 0, waves * 96));
+        HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_pst_out), &g_api_pst, sizeof(g_api_pst)));
+        return 0;
+    }
+    if (g_api_pst && out) HIPCHK(hipMemcpy(out, g_api_pst, waves * 96, hipMemcpyDeviceToHost));
+    unsigned long long* z = nullptr;
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_pst_out), &z, sizeof(z)));
     return 0;
 }
 #endif

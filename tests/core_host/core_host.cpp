@@ -186,9 +186,12 @@ extern "C" int host_quick_legal_agree(const int8_t* b, const uint8_t* m, int whi
     int n = 0;
     for (int a = -1; a <= A_RESIGN + 1; a++) {
         bool q = quick_legal(s, a), r = action_legal(s, g, a);
-        if (q != r) return -1 - a;
+        bool split = quick_pseudo(s, a) && quick_safe(s, a);  // the quad API step's two halves
+        if (q != r || split != r) return -1 - a;
         n += r;
     }
+    for (int a : {5000, 8191, 65535})
+        if (quick_legal(s, a) || (quick_pseudo(s, a) && quick_safe(s, a))) return -1 - a;
     return n;
 }
 extern "C" uint64_t host_between(int a, int b) { return between(a, b); }

@@ -239,14 +239,15 @@ def test_swar_pick_agrees(seed):
     assert ranks > 10000
 
 
-@pytest.mark.parametrize("seed", [13])
-def test_quick_legal_agrees(seed):
+@pytest.mark.parametrize("seed,weird", [(13, True), (14, False)])
+def test_quick_legal_agrees(seed, weird):
     """quick_legal (the paired API step's validation: no enemy map, a king target's attack
-    test alone) == action_legal over gen_init for all 4 101 action ids (and -1, 4101) on fuzz
-    positions, both sides to move."""
+    test alone) and its two halves quick_pseudo && quick_safe (the quad API step's, on two
+    waves) == action_legal over gen_init for all 4 101 action ids (and -1, 4101, larger ids)
+    on fuzz positions, both sides to move."""
     from conftest import random_positions
 
-    boards, metas = random_positions(600, seed)
+    boards, metas = random_positions(600, seed, weird=weird)
     L = H.lib()
     legal = 0
     for i in range(len(boards)):

@@ -16,7 +16,7 @@ mkdir -p gpurun_out
 MODE=${MODE:-step}
 if [ -n "${PARITY:-}" ]; then
   for lib in $LIBS; do
-    so=${lib%%@*}; ev=""; [ "$so" != "$lib" ] && ev=${lib#*@}
+    so=${lib%%@*}; ev=""; [ "$so" != "$lib" ] && ev=$(echo "${lib#*@}" | tr "@" " ")
     env $ev timeout -k 10 300 python tools/ab_parity.py $so > gpurun_out/ab_parity.log 2>&1 || { echo "PARITY FAILED $lib"; tail -20 gpurun_out/ab_parity.log; exit 3; }
     echo "parity ok: $lib $(tail -1 gpurun_out/ab_parity.log)"
   done
@@ -32,7 +32,7 @@ esac
 for r in $(seq ${REPS:-3}); do
   for lib in $LIBS; do
     for k in $KS; do
-      so=${lib%%@*}; ev=""; [ "$so" != "$lib" ] && ev=${lib#*@}
+      so=${lib%%@*}; ev=""; [ "$so" != "$lib" ] && ev=$(echo "${lib#*@}" | tr "@" " ")
       env $ev timeout -k 10 240 python tools/ab_lib.py $so --steps $k $ARGS > gpurun_out/ab_one.log 2>&1 || { echo "STOP $lib rc=$?"; tail -5 gpurun_out/ab_one.log; exit 3; }
       python - "$lib" "$MODE" >> gpurun_out/ab.jsonl <<'PY'
 import json, sys
