@@ -1083,7 +1083,7 @@ GC_HD SliderGens slider_gens_kl(const Pos& s, const Gen& g, const KingLines& kl)
 }
 GC_HD SliderGens slider_gens(const Pos& s, const Gen& g) { return slider_gens_kl(s, g, king_lines(g.ks, g.white)); }
 // pawns (set-wise, pinned ones included), knights, kings (count_moves without the sliders)
-GC_HD int count_nonsliders_kl(const Pos& s, const Gen& g, const KingLines& kl) {
+GC_HD int count_nonsliders_kl(const Pos& s, const Gen& g, const KingLines& kl, bool kl_king = false) {
     const u64 own = g.own, tm = ~own & g.checkmask;
     int total = popc(g.castles);
     // pawns (lib.rs:935-958; Q1: the double push tests only the destination): sw_pawns' sets
@@ -1101,8 +1101,8 @@ GC_HD int count_nonsliders_kl(const Pos& s, const Gen& g, const KingLines& kl) {
     const u64 K = s.k & own, ok = ~own & ~g.enemy_att;
     if (K & (K - 1)) {
         for (u64 x = K; x; x &= x - 1) total += popc(king_set(x & (0 - x)) & ok);
-    } else {
-        total += popc(king_set(K) & ok);
+    } else {  // (kl_king: the lone king is the tracked one, its steps are kl.king)
+        total += popc((kl_king && kl.ks >= 0 && K == bit(kl.ks) ? kl.king : king_set(K)) & ok);
     }
     return total;
 }
@@ -1136,7 +1136,10 @@ GC_HD void ray_fill_pair(u64 ge, u64 go, u64 empty, u64 wrap, u64& ae, u64& ao) 
 }
 // kh: the king lines of the side to move if its tracked king sits on kh.ks (perft: computed
 // once per subtree root); otherwise (a king captured, Q7) they are recomputed here
-GC_HD int count_position_kl(const Pos& s, const KingLines& kh) {
+// ktab (the round-5 LDS-table A/B, GC_PERFT_LDS): king neighbourhoods by square from a table in
+// LDS for the enemy king's attacks, and the own king's steps from the per-root KingLines, instead
+// of the set-wise shifts
+GC_HD int count_position_kl(const Pos& s, const KingLines& kh, const u64* ktab = nullptr) {
     Gen g;
     gen_base_ks(s, g, kh);  // the tracked king from the hint while the side's kings are the hint's
     KingLines kl = kh;
@@ -1161,10 +1164,19 @@ GC_HD int count_position_kl(const Pos& s, const KingLines& kh) {
     GC_PAIR(7, true, eBQ, G.a, ~FILE_H)
 #undef GC_PAIR
     if (g.ks >= 0) {  // gen_enemy (no king: no map, no castling)
-        g.enemy_att = att | side_attacks_leapers(s, !g.white);
+        if (ktab) {
+            const u64 ek = s.k & g.opp;
+            const u64 ekatt = (ek & (ek - 1)) == 0 && ek ? ktab[ctz(ek)] : king_set(ek);
+            g.enemy_att = att | (pawn_att_set(s.p & g.opp, !g.white) & ~ek) | knight_set(s.n & g.opp) | ekatt;
+        } else {
+            g.enemy_att = att | side_attacks_leapers(s, !g.white);
+        }
         gen_castles(s, g);
     }
-    return n + count_nonsliders_kl(s, g, kl);
+#ifndef GC_KL_KING
+#define GC_KL_KING 1  // the own king's steps from the per-root KingLines (perft 1.566 -> 1.583e12 same-box)
+#endif
+    return n + count_nonsliders_kl(s, g, kl, ktab != nullptr || GC_KL_KING);
 }
 GC_HD int count_position(const Pos& s) { return count_position_kl(s, king_lines_of(s, (s.meta & M_WHITE) != 0)); }
 

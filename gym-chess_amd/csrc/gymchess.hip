@@ -651,6 +651,12 @@ __device__ __forceinline__ bool pos_equal(const Pos& a, const Pos& b) {
     return ((a.k ^ b.k) | (a.q ^ b.q) | (a.r ^ b.r) | (a.b ^ b.b) | (a.n ^ b.n) | (a.p ^ b.p) | (a.w ^ b.w)) == 0 &&
            a.meta == b.meta;
 }
+// DEDUP_R records per thread (block b: records [b, b + 1) * DEDUP_BLOCK * DEDUP_R, the r-th
+// DEDUP_BLOCK of them on pass r): their loads, hashes and CASes issued back to back, so DEDUP_R
+// table round trips are in flight per lane instead of one
+#ifndef DEDUP_R
+#define DEDUP_R 1
+#endif
 __global__ void __launch_bounds__(DEDUP_BLOCK) k_dedup_bin(const Node64* __restrict__ in, int n, u64* __restrict__ table,
                                                            u32 mask, uint8_t* __restrict__ bins,
                                                            uint8_t* __restrict__ lflag, u32* __restrict__ hist, int nblk,
@@ -658,41 +664,61 @@ __global__ void __launch_bounds__(DEDUP_BLOCK) k_dedup_bin(const Node64* __restr
     __shared__ u32 hb[SPLIT_BINS];
     for (int b = threadIdx.x; b < SPLIT_BINS; b += blockDim.x) hb[b] = 0;
     __syncthreads();
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    bool follower = false;
-    u32 lead = 0, parent = 0;
-    if (i < n) {
-        const Pos s = node_load(in, i);
-        parent = reinterpret_cast<const u32*>(in + i)[15];
-        const u64 h = pos_hash(s);
-        const u64 tag = (h >> 32) | 1u;
-        const u64 mine = (tag << 32) | (u32)i;
-        u32 slot = (u32)h & mask;
-        for (;;) {  // (a relaxed load ahead of the CAS measured the same)
-            const u64 e = atomicCAS(reinterpret_cast<unsigned long long*>(table + slot), 0ull, (unsigned long long)mine);
-            if (e == 0) break;  // this record leads its position
-            if ((e >> 32) == tag && pos_equal(node_load(in, (u32)e), s)) {
-                follower = true;
-                lead = (u32)e;
-                break;
-            }
-            slot = (slot + 1) & mask;
-        }
-        lflag[i] = follower ? 0 : 1;
-        if (!follower) {
-            const int b = split_bin(s, king_lines_of(s, (s.meta & M_WHITE) != 0));
-            bins[i] = (uint8_t)b;
-            atomicAdd(&hb[b], 1u);
-        }
+    const size_t i0 = (size_t)blockIdx.x * DEDUP_BLOCK * DEDUP_R + threadIdx.x;
+    Pos s[DEDUP_R];
+    u64 tag[DEDUP_R], e[DEDUP_R];
+    u32 slot[DEDUP_R];
+#pragma unroll
+    for (int r = 0; r < DEDUP_R; r++) {
+        const size_t i = i0 + (size_t)r * DEDUP_BLOCK;
+        s[r] = node_load(in, i < (size_t)n ? i : (size_t)n - 1);
     }
-    const u64 bal = __ballot(follower);  // wave-aggregated append of the followers
-    if (bal) {
-        const int lane = threadIdx.x & 63;
-        const int first = __ffsll((long long)bal) - 1;
-        u32 base = 0;
-        if (lane == first) base = atomicAdd(nfol, (u32)__popcll(bal));
-        base = __shfl(base, first);
-        if (follower) fol[base + __popcll(bal & ((1ull << lane) - 1))] = make_uint2(parent, lead);
+#pragma unroll
+    for (int r = 0; r < DEDUP_R; r++) {  // every CAS issued before any result is needed
+        const size_t i = i0 + (size_t)r * DEDUP_BLOCK;
+        const u64 h = pos_hash(s[r]);
+        tag[r] = (h >> 32) | 1u;
+        slot[r] = (u32)h & mask;
+        e[r] = i < (size_t)n ? atomicCAS(reinterpret_cast<unsigned long long*>(table + slot[r]), 0ull,
+                                         (unsigned long long)((tag[r] << 32) | (u32)i))
+                             : 0ull;
+    }
+#pragma unroll
+    for (int r = 0; r < DEDUP_R; r++) {
+        const size_t i = i0 + (size_t)r * DEDUP_BLOCK;
+        bool follower = false;
+        u32 lead = 0, parent = 0;
+        if (i < (size_t)n) {
+            parent = reinterpret_cast<const u32*>(in + i)[15];
+            const u64 mine = (tag[r] << 32) | (u32)i;
+            u64 x = e[r];
+            u32 sl = slot[r];
+            for (;;) {  // (a relaxed load ahead of the CAS measured the same)
+                if (x == 0) break;  // this record leads its position
+                if ((x >> 32) == tag[r] && pos_equal(node_load(in, (u32)x), s[r])) {
+                    follower = true;
+                    lead = (u32)x;
+                    break;
+                }
+                sl = (sl + 1) & mask;
+                x = atomicCAS(reinterpret_cast<unsigned long long*>(table + sl), 0ull, (unsigned long long)mine);
+            }
+            lflag[i] = follower ? 0 : 1;
+            if (!follower) {
+                const int b = split_bin(s[r], king_lines_of(s[r], (s[r].meta & M_WHITE) != 0));
+                bins[i] = (uint8_t)b;
+                atomicAdd(&hb[b], 1u);
+            }
+        }
+        const u64 bal = __ballot(follower);  // wave-aggregated append of the followers
+        if (bal) {
+            const int lane = threadIdx.x & 63;
+            const int first = __ffsll((long long)bal) - 1;
+            u32 base = 0;
+            if (lane == first) base = atomicAdd(nfol, (u32)__popcll(bal));
+            base = __shfl(base, first);
+            if (follower) fol[base + __popcll(bal & ((1ull << lane) - 1))] = make_uint2(parent, lead);
+        }
     }
     __syncthreads();
     for (int b = threadIdx.x; b < SPLIT_BINS; b += blockDim.x) hist[(size_t)b * nblk + blockIdx.x] = hb[b];
@@ -705,14 +731,16 @@ __global__ void __launch_bounds__(DEDUP_BLOCK) k_place_leaders(const Node64* __r
     __shared__ u32 cur[SPLIT_BINS];
     for (int b = threadIdx.x; b < SPLIT_BINS; b += blockDim.x) cur[b] = base[(size_t)b * nblk + blockIdx.x];
     __syncthreads();
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n || !lflag[i]) return;
-    const u32 slot = atomicAdd(&cur[bins[i]], 1u);
-    const ulonglong2* x = reinterpret_cast<const ulonglong2*>(in + i);
-    ulonglong2* y = reinterpret_cast<ulonglong2*>(out + slot);
-    const ulonglong2 r0 = x[0], r1 = x[1], r2 = x[2], r3 = x[3];
-    y[0] = r0; y[1] = r1; y[2] = r2; y[3] = r3;
-    place_of[i] = (int32_t)slot;
+    for (int r = 0; r < DEDUP_R; r++) {  // k_dedup_bin's blocks: DEDUP_BLOCK * DEDUP_R records
+        const size_t i = (size_t)blockIdx.x * DEDUP_BLOCK * DEDUP_R + (size_t)r * DEDUP_BLOCK + threadIdx.x;
+        if (i >= (size_t)n || !lflag[i]) continue;
+        const u32 slot = atomicAdd(&cur[bins[i]], 1u);
+        const ulonglong2* x = reinterpret_cast<const ulonglong2*>(in + i);
+        ulonglong2* y = reinterpret_cast<ulonglong2*>(out + slot);
+        const ulonglong2 r0 = x[0], r1 = x[1], r2 = x[2], r3 = x[3];
+        y[0] = r0; y[1] = r1; y[2] = r2; y[3] = r3;
+        place_of[i] = (int32_t)slot;
+    }
 }
 // one lane = one placed leader (move-count order); its count kept for the followers
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(PERFT2_WPE)))
@@ -720,10 +748,22 @@ k_perft2_val(const Node64* __restrict__ in, int n, uint64_t* __restrict__ val,
              unsigned long long* __restrict__ parent_sum) {
     __shared__ u64 lds_a[SCRATCH_SLOTS * BLOCK];
     LdsScratch sa{lds_a + threadIdx.x};
+#ifndef GC_PERFT_LDS
+#define GC_PERFT_LDS 0  // A/B: the leaf's king neighbourhoods from an LDS table (count_position_kl's ktab)
+#endif
+#if GC_PERFT_LDS
+    __shared__ u64 ktab[64];
+    if (threadIdx.x < 64) ktab[threadIdx.x] = king_set(bit((int)threadIdx.x));
+    __syncthreads();
+#endif
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const u32 parent = reinterpret_cast<const u32*>(in + i)[15];
+#if GC_PERFT_LDS
+    const uint64_t c = perft2(node_load(in, i), sa, ktab);
+#else
     const uint64_t c = perft2(node_load(in, i), sa);
+#endif
     val[i] = c;
     atomicAdd(parent_sum + parent, (unsigned long long)c);
 }
@@ -3324,6 +3364,10 @@ __shared__ ApiQuadLds g_apiq_lds[QUADS_WG];
 #define GC_APIQ_EARLY 0  // 1: rows of unoccupied squares zeroed in phase 1 (partial rows written twice:
                          // 28.4 us per launch; non-temporal or not alike), 0: every row once in phase 3 (18.5)
 #endif
+#ifndef GC_APIQ_SPLIT
+#define GC_APIQ_SPLIT 0  // phase 2's pieces: 0 Q0 pawns | Q1 knights, kings | Q2 queens, bishops | Q3 rooks;
+                         // 1: bishops on Q3; 2: knights on Q0
+#endif
 #ifndef GC_APIQ_NT
 #define GC_APIQ_NT 1     // the mask rows as non-temporal stores
 #endif
@@ -3443,7 +3487,10 @@ __device__ __forceinline__ void apiq_run(uint8_t* __restrict__ slab, uint64_t se
     OrdScratch scr{&L.slots[0][l], 0ull, 0ull};
     // issue priority: the state-carrying roles' chains are the longer; Q2 (a validation half,
     // on Q0's SIMDs) level with Q0 in phase 0
-    if (RR != 3) __builtin_amdgcn_s_setprio(2);
+#ifndef GC_APIQ_Q3P
+#define GC_APIQ_Q3P 0  // A/B: Q3 (the other validation half, the observation) at priority 2 in phases 0 and 3
+#endif
+    if (RR != 3 || GC_APIQ_Q3P) __builtin_amdgcn_s_setprio(2);
     const bool done0 = (s.meta & M_DONE) != 0;   // chess_v2.py:245-251
     const bool cap = mc_of(s.meta) > MOVES_MAX;  // 252-258
     const bool white = (s.meta & M_WHITE) != 0;
@@ -3478,7 +3525,7 @@ __device__ __forceinline__ void apiq_run(uint8_t* __restrict__ slab, uint64_t se
     PST(1);
 
     // ---- phase 1
-    if (RR == 2) __builtin_amdgcn_s_setprio(0);
+    if (RR == 2 || (GC_APIQ_Q3P && RR == 3)) __builtin_amdgcn_s_setprio(0);
     const bool valid = (L.valid[0][l] & L.valid[1][l]) != 0;
     const bool mv = pre && valid;  // env_ply runs
     Pos ns = s;                    // the position generated for: post-move, or s itself
@@ -3532,6 +3579,7 @@ __device__ __forceinline__ void apiq_run(uint8_t* __restrict__ slab, uint64_t se
                 const int sq = ctz(fp);
                 scr.put(ordinal(g.own, sq), fast_pawn_targets(ms, sq, g.white));
             }
+            if (GC_APIQ_SPLIT == 2) part += gen_knights(ns, g, ms, scr);
         }
         L.cbw[0][0][l] = scr.c0;
         L.cbw[0][1][l] = scr.c1;
@@ -3539,7 +3587,7 @@ __device__ __forceinline__ void apiq_run(uint8_t* __restrict__ slab, uint64_t se
         L.part[0][l] = (u32)part;
     } else if (RR == 1) {  // knights, kings (while the probe lands), the 3-fold commit
         if (gen && !big) {
-            part = gen_knights(ns, g, ms, scr) + gen_kings(ns, g, ms, scr);
+            part = (GC_APIQ_SPLIT == 2 ? 0 : gen_knights(ns, g, ms, scr)) + gen_kings(ns, g, ms, scr);
         }
         L.cbw[1][0][l] = scr.c0;
         L.cbw[1][1][l] = scr.c1;
@@ -3555,14 +3603,14 @@ __device__ __forceinline__ void apiq_run(uint8_t* __restrict__ slab, uint64_t se
         L.ra[l] = ra;
     } else if (RR == 2) {  // queens, bishops
         if (gen && !big) {
-            part = gen_sliders<QUEEN>(ns, g, ms, scr) + gen_sliders<BISHOP>(ns, g, ms, scr);
+            part = gen_sliders<QUEEN>(ns, g, ms, scr) + (GC_APIQ_SPLIT == 1 ? 0 : gen_sliders<BISHOP>(ns, g, ms, scr));
         }
         L.cbw[2][0][l] = scr.c0;
         L.cbw[2][1][l] = scr.c1;
         L.part[2][l] = (u32)part;
     } else {  // rooks; a big board's whole count
         if (gen && !big) {
-            part = gen_sliders<ROOK>(ns, g, ms, scr);
+            part = gen_sliders<ROOK>(ns, g, ms, scr) + (GC_APIQ_SPLIT == 1 ? gen_sliders<BISHOP>(ns, g, ms, scr) : 0);
         } else if (gen) {
             gen_castles(ns, g);
             part = count_legal(ns, g);
@@ -3578,7 +3626,7 @@ __device__ __forceinline__ void apiq_run(uint8_t* __restrict__ slab, uint64_t se
     // ---- phase 3: the outcome, as k_env_step_api2 (every role: identical arithmetic)
 #ifndef GC_NO_QPRIO_DYN
     if (RR == 0) __builtin_amdgcn_s_setprio(0);
-    if (RR == 2) __builtin_amdgcn_s_setprio(2);  // the pick: this phase's longest chain
+    if (RR == 2 || (GC_APIQ_Q3P && RR == 3)) __builtin_amdgcn_s_setprio(2);  // the pick: this phase's longest chain
 #endif
     const int total = gen ? (int)(L.part[0][l] + L.part[1][l] + L.part[2][l] + L.part[3][l]) : 0;
     const u32 rpk = L.rep[l];
@@ -4606,7 +4654,7 @@ static int perft_split_leaves(hipStream_t st, SoA leaf, uint64_t* leaf_out) {
     uint8_t* bins = nullptr;
     u32 *hist = nullptr, *hbase = nullptr;
     const int max_blk = (chunk + BLOCK - 1) / BLOCK;
-    const int max_dblk = (int)((cap + DEDUP_BLOCK - 1) / DEDUP_BLOCK);  // k_dedup_bin's blocks
+    const int max_dblk = (int)((cap + DEDUP_BLOCK * DEDUP_R - 1) / (DEDUP_BLOCK * DEDUP_R));  // k_dedup_bin's blocks
     const int hist_n = SPLIT_BINS * (dedup && max_dblk > max_blk ? max_dblk : max_blk);
     Node64* cr = nullptr;
     // the transposition pass: the records in expansion order, the table (2x the chunk's
@@ -4663,7 +4711,7 @@ static int perft_split_leaves(hipStream_t st, SoA leaf, uint64_t* leaf_out) {
         unsigned long long* psum = reinterpret_cast<unsigned long long*>(leaf_out + a);
         if (total > 0 && dedup) {  // transpositions merged, the leaders binned and placed in order
             const int n = (int)total;
-            const int nbd = (n + DEDUP_BLOCK - 1) / DEDUP_BLOCK;
+            const int nbd = (n + DEDUP_BLOCK * DEDUP_R - 1) / (DEDUP_BLOCK * DEDUP_R);
             u32 tsize = 2;
             while ((int64_t)tsize < 2 * total) tsize <<= 1;
             k_expand_range_rec<<<grid_for(c), BLOCK, 0, st>>>(leaf, a, c, offs, cre);

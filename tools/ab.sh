@@ -40,7 +40,7 @@ lib, mode = sys.argv[1], sys.argv[2]
 d = json.loads([l for l in open("gpurun_out/ab_one.log") if l.startswith("{")][-1])
 if mode == "perft":
     p = d["perft"]
-    print(json.dumps({"lib": lib, "k": 0, "value": p["value"], "aux": p["roofline"]["kernel_ms"]}))
+    print(json.dumps({"lib": lib, "k": 0, "value": p["value"], "aux": p["roofline"]["kernel_ms"], "nodes": p["nodes"]}))
 elif mode == "api":
     p = d["api_step"]
     print(json.dumps({"lib": lib, "k": 0, "value": p["value"], "aux": p["roofline"]["avg_launch_us"]}))
@@ -59,5 +59,7 @@ for r in rows:
 for (lib, k), rs in sorted(g.items()):
     v = sorted(x["value"] / 1e9 for x in rs)
     e = sorted(x["aux"] for x in rs)
-    print(f"{lib:55s} K={k:5d}: value {' '.join(f'{x:.3f}' for x in v)} e9 | aux {' '.join(f'{x:.3f}' for x in e)}")
+    nodes = sorted(set(x.get("nodes") for x in rs if x.get("nodes") is not None))
+    print(f"{lib:55s} K={k:5d}: value {' '.join(f'{x:.3f}' for x in v)} e9 | aux {' '.join(f'{x:.3f}' for x in e)}"
+          + (f" | nodes {nodes}" if nodes else ""))
 PY
