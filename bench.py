@@ -314,8 +314,7 @@ def fixture_check(args, rep, ctx0, nodes):
             "perft5_stride_nodes": int(nodes[s5].sum()), "match": True}
 
 
-# algorithmic bytes per board of one API-shaped step (k_env_step_api2, the paired API step,
-# DESIGN.md §5): state 120 r/w, action 2, draw / step counter / window generation 24 r/w, window probe 64 + entry
+# algorithmic bytes per board of one API-shaped step (k_env_step_api4 / _api2): state 120 r/w, action 2, draw / step counter / window generation 24 r/w, window probe 64 + entry
 # write 64, outputs reward / done / reason to the caller and the env 12, the legal-action mask
 # 520 (65 words), observation 64, legal count 4, the pick 2 + the env's act 2
 ALG_BYTES_API = 120 + 2 + 24 + 128 + 12 + 520 + 64 + 4 + 4
@@ -325,8 +324,8 @@ def api_step_leg(args, rep, n, **env_kw):
     """The reference's call shape (chess_v2.py:219-294 + possible_actions 333-335) on device
     buffers: per step an external action per board in (here: the previous step's random-policy
     pick, so no host round trip), reward / done / reason, the int8 observation, the legal-action
-    mask and count out, auto-reset of finished boards.  One launch of k_env_step_api2 (the
-    paired API step) per step."""
+    mask and count out, auto-reset of finished boards.  One launch of k_env_step_api4 (the quad
+    API step; the random opponent's: k_env_step_api2_vs, paired) per step."""
     from gym_chess_amd.env import BatchedChessEnv
 
     def setup(rp):
@@ -358,8 +357,12 @@ def api_step_leg(args, rep, n, **env_kw):
         env.close()
     avg = kms / 1e3 / args.api_steps
     ach = n * ALG_BYTES_API / avg / 1e9
+    # the quad API step (k_env_step_api4) serves opponent "none" (GC_NO_QUAD_API=1: the paired one);
+    # the random opponent's runs on the paired driver
+    kern = "k_env_step_api2_vs" if env_kw else (
+        "k_env_step_api2" if os.environ.get("GC_NO_QUAD_API", "0") not in ("", "0") else "k_env_step_api4")
     out = {"value": rep.world_size * n * args.api_steps / dt, "unit": "env_steps/s", "steps": args.api_steps,
-           "roofline": {"bound": "hbm", "kernel": "k_env_step_api2" + ("_vs" if env_kw else ""), "achieved": ach,
+           "roofline": {"bound": "hbm", "kernel": kern, "achieved": ach,
                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "avg_launch_us": avg * 1e6,
                         "alg_bytes_per_board": ALG_BYTES_API}}
     if env_kw:

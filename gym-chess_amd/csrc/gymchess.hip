@@ -3328,7 +3328,7 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
 //             Q2: enemy leaper + orthogonal slider attacks    Q3: enemy diagonal slider attacks
 //   phase 2   Q0: castles, pawns (set-wise; every pawn's targets parked too)
 //             Q1: knights, kings, then the 3-fold commit (its probe lands meanwhile)
-//             Q2: queens, bishops                             Q3: rooks
+//             Q2: queens                                      Q3: rooks, bishops
 //             (pieces parked per ordinal in LDS with bit-sliced counts, as gen_moves)
 //   phase 3   every role: the step's outcome (identical arithmetic on the same LDS data) and
 //             its 16 mask rows, each written once, whole (a reset board: the start position's
@@ -3365,8 +3365,8 @@ __shared__ ApiQuadLds g_apiq_lds[QUADS_WG];
                          // 28.4 us per launch; non-temporal or not alike), 0: every row once in phase 3 (18.5)
 #endif
 #ifndef GC_APIQ_SPLIT
-#define GC_APIQ_SPLIT 0  // phase 2's pieces: 0 Q0 pawns | Q1 knights, kings | Q2 queens, bishops | Q3 rooks;
-                         // 1: bishops on Q3; 2: knights on Q0
+#define GC_APIQ_SPLIT 1  // phase 2's pieces: 1 Q0 pawns | Q1 knights, kings | Q2 queens | Q3 rooks, bishops
+                         // (same-box 17.13 us per launch); 0: bishops on Q2 (17.34); 2: 0 with knights on Q0 (17.60)
 #endif
 #ifndef GC_APIQ_NT
 #define GC_APIQ_NT 1     // the mask rows as non-temporal stores
@@ -4640,8 +4640,11 @@ static uint64_t g_leaf_launches = 0, g_leaf_subtrees = 0, g_leaf_records = 0;
 static double g_leaf_ms = 0.0;
 
 static int perft_split_leaves(hipStream_t st, SoA leaf, uint64_t* leaf_out) {
-    const int64_t cap = (int64_t)1 << 27;  // children per chunk (7.5 GiB of boards)
-    int chunk = 1 << 21;
+    // parents per chunk 2^21 and up to 2^27 children (7.5 GiB of boards); GC_PERFT_CHUNK=k
+    // (A/B): 2^k parents, 2^(k+6) children
+    static const int chunk_log2 = getenv("GC_PERFT_CHUNK") ? atoi(getenv("GC_PERFT_CHUNK")) : 21;
+    const int64_t cap = (int64_t)1 << (chunk_log2 + 6);
+    int chunk = 1 << chunk_log2;
     std::vector<hipEvent_t> evs;  // pairs around the leaf launches
     uint64_t subtrees = 0, records = 0;  // subtrees counted by the leaf kernel, of records made
     // GC_PERFT_GATHER (A/B): the round-2/3 form -- records in expansion order, a radix sort by
