@@ -221,8 +221,10 @@ def perft_leg(args, rep):
     la, sub, kms = (b - a for a, b in zip(leaf0, leaf1))
     recs, counted = (b - a for a, b in zip(dd0, dd1))
     if recs:
+        # the leaf's own rate beside nodes/s: the transposition merge raises
+        # nodes/s by counting each distinct depth-2 subtree once, not by a faster leaf
         out["transpositions"] = {"records": recs, "counted": counted, "records_per_counted": recs / max(1, counted),
-                                 "merged": dedup}
+                                 "merged": dedup, "records_per_s": recs / dtm, "counted_subtrees_per_s": counted / dtm}
     if la:
         kname = "k_perft2_perm_rec" if gather else ("k_perft2_val" if dedup else "k_perft2_rec")
         roof = {"bound": "valu", "kernel": kname, "launches": la,
