@@ -742,6 +742,73 @@ __global__ void __launch_bounds__(DEDUP_BLOCK) k_place_leaders(const Node64* __r
         place_of[i] = (int32_t)slot;
     }
 }
+// The transposition pass by sorting (round 5, GC_PERFT_SORTDEDUP, the default): every record's
+// 32-bit hash tag and index sorted by the tag (hipCUB radix sort: ~2 ms for 2^26 pairs), so equal
+// positions are adjacent and the pass reads sequentially -- where k_dedup_bin made one random
+// CAS per record into a 1 GiB table (~1 TB/s of random line traffic, 12 ms per chunk).
+//   k_dedup_keys   per record, in order: the tag, the index, the parent, the leaf's move-count bin
+//   (sort)         by the tag (stable: a run's members in record order)
+//   k_dedup_runs   one lane per run of equal tags: the members compared whole with the run's
+//                  first (and, after a tag collision, with the run's other leaders), so a merge is
+//                  exact; each group's first member leads
+//   k_leader_hist  per-block leader histograms by bin (k_place_leaders' blocks)
+//   k_followers2   each follower adds its leader's count into its own parent
+__global__ void __launch_bounds__(BLOCK) k_dedup_keys(const Node64* __restrict__ in, int n, u32* __restrict__ keys,
+                                                      u32* __restrict__ vals, uint8_t* __restrict__ bins,
+                                                      u32* __restrict__ parent_of) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const Pos s = node_load(in, i);
+    keys[i] = (u32)(pos_hash(s) >> 32);
+    vals[i] = (u32)i;
+    parent_of[i] = reinterpret_cast<const u32*>(in + i)[15];
+    bins[i] = (uint8_t)split_bin(s, king_lines_of(s, (s.meta & M_WHITE) != 0));
+}
+__global__ void __launch_bounds__(BLOCK) k_dedup_runs(const Node64* __restrict__ in, int n, const u32* __restrict__ keys,
+                                                      const u32* __restrict__ vals, uint8_t* __restrict__ lflag,
+                                                      u32* __restrict__ lead) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const u32 k = keys[p];
+    if (p > 0 && keys[p - 1] == k) return;  // not a run's first member
+    int q = p + 1;
+    while (q < n && keys[q] == k) q++;
+    const u32 r0 = vals[p];
+    lflag[r0] = 1;
+    if (q == p + 1) return;  // a lone position
+    const Pos s0 = node_load(in, r0);
+    for (int j = p + 1; j < q; j++) {
+        const u32 r = vals[j];
+        const Pos sj = node_load(in, r);
+        u32 ld = pos_equal(sj, s0) ? r0 : r;
+        for (int t = p + 1; t < j && ld == r; t++) {  // a tag collision: the run's other leaders
+            const u32 rt = vals[t];
+            if (lflag[rt] && pos_equal(node_load(in, rt), sj)) ld = rt;
+        }
+        lflag[r] = ld == r ? 1 : 0;
+        lead[r] = ld;
+    }
+}
+__global__ void __launch_bounds__(DEDUP_BLOCK) k_leader_hist(int n, const uint8_t* __restrict__ lflag,
+                                                             const uint8_t* __restrict__ bins, u32* __restrict__ hist,
+                                                             int nblk) {
+    __shared__ u32 hb[SPLIT_BINS];
+    for (int b = threadIdx.x; b < SPLIT_BINS; b += blockDim.x) hb[b] = 0;
+    __syncthreads();
+    for (int r = 0; r < DEDUP_R; r++) {  // k_place_leaders' blocks: DEDUP_BLOCK * DEDUP_R records
+        const size_t i = (size_t)blockIdx.x * DEDUP_BLOCK * DEDUP_R + (size_t)r * DEDUP_BLOCK + threadIdx.x;
+        if (i < (size_t)n && lflag[i]) atomicAdd(&hb[bins[i]], 1u);
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < SPLIT_BINS; b += blockDim.x) hist[(size_t)b * nblk + blockIdx.x] = hb[b];
+}
+__global__ void k_followers2(int n, const uint8_t* __restrict__ lflag, const u32* __restrict__ lead,
+                             const u32* __restrict__ parent_of, const int32_t* __restrict__ place_of,
+                             const uint64_t* __restrict__ val, unsigned long long* __restrict__ parent_sum) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        if (!lflag[i]) atomicAdd(parent_sum + parent_of[i], (unsigned long long)val[place_of[lead[i]]]);
+}
+
 // one lane = one placed leader (move-count order); its count kept for the followers
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(PERFT2_WPE)))
 k_perft2_val(const Node64* __restrict__ in, int n, uint64_t* __restrict__ val,
@@ -4653,6 +4720,9 @@ static int perft_split_leaves(hipStream_t st, SoA leaf, uint64_t* leaf_out) {
     // GC_PERFT_DEDUP=0 (per call; A/B and tests): every record counted, transpositions too
     const char* dd = getenv("GC_PERFT_DEDUP");
     const bool dedup = !gather && !(dd && dd[0] == '0');
+    // GC_PERFT_SORTDEDUP=0 (A/B): the transposition pass by one CAS per record (k_dedup_bin)
+    const char* sd = getenv("GC_PERFT_SORTDEDUP");
+    const bool sortdedup = !(sd && sd[0] == '0');
     int32_t *kc = nullptr, *offs = nullptr, *kc2 = nullptr, *ks = nullptr, *ix = nullptr, *is = nullptr;
     uint8_t* bins = nullptr;
     u32 *hist = nullptr, *hbase = nullptr;
@@ -4693,7 +4763,13 @@ static int perft_split_leaves(hipStream_t st, SoA leaf, uint64_t* leaf_out) {
         if (he == hipSuccess && gather)
             he = hipcub::DeviceRadixSort::SortPairs(nullptr, b2, kc2, ks, ix, is, (int)cap, 0, 10, st);
         if (he == hipSuccess && !gather) he = hipcub::DeviceScan::ExclusiveSum(nullptr, b2, hist, hbase, hist_n, st);
+        size_t b3 = 0;  // the sorting transposition pass (keys / values in the table's memory)
+        if (he == hipSuccess && dedup) {
+            u32* kk = reinterpret_cast<u32*>(table);
+            he = hipcub::DeviceRadixSort::SortPairs(nullptr, b3, kk, kk + cap, kk + 2 * cap, kk + 3 * cap, (int)cap, 0, 32, st);
+        }
         tmp_bytes = b1 > b2 ? b1 : b2;
+        tmp_bytes = tmp_bytes > b3 ? tmp_bytes : b3;
         if (he != hipSuccess) { done(); return fail(std::string("perft split: ") + hipGetErrorString(he)); }
         if (dalloc((char**)&tmp, tmp_bytes)) { done(); return -1; }
     }
@@ -4718,10 +4794,26 @@ static int perft_split_leaves(hipStream_t st, SoA leaf, uint64_t* leaf_out) {
             u32 tsize = 2;
             while ((int64_t)tsize < 2 * total) tsize <<= 1;
             k_expand_range_rec<<<grid_for(c), BLOCK, 0, st>>>(leaf, a, c, offs, cre);
-            he = hipMemsetAsync(table, 0, (size_t)8 * tsize, st);
-            if (he == hipSuccess) he = hipMemsetAsync(nfol, 0, 4, st);
-            if (he == hipSuccess)
-                k_dedup_bin<<<nbd, DEDUP_BLOCK, 0, st>>>(cre, n, table, tsize - 1, bins, lflag, hist, nbd, nfol, fol);
+            // keys / values of the sort in the table's memory (16 B per record), parents and
+            // leaders in the follower pairs' (8 B)
+            u32* const keys = reinterpret_cast<u32*>(table);
+            u32* const keys2 = keys + cap;
+            u32* const vals = keys + 2 * cap;
+            u32* const vals2 = keys + 3 * cap;
+            u32* const parent_of = reinterpret_cast<u32*>(fol);
+            u32* const lead = parent_of + cap;
+            if (sortdedup) {
+                k_dedup_keys<<<grid_for(n), BLOCK, 0, st>>>(cre, n, keys, vals, bins, parent_of);
+                tb = tmp_bytes;
+                he = hipcub::DeviceRadixSort::SortPairs(tmp, tb, keys, keys2, vals, vals2, n, 0, 32, st);
+                if (he == hipSuccess) k_dedup_runs<<<grid_for(n), BLOCK, 0, st>>>(cre, n, keys2, vals2, lflag, lead);
+                if (he == hipSuccess) k_leader_hist<<<nbd, DEDUP_BLOCK, 0, st>>>(n, lflag, bins, hist, nbd);
+            } else {
+                he = hipMemsetAsync(table, 0, (size_t)8 * tsize, st);
+                if (he == hipSuccess) he = hipMemsetAsync(nfol, 0, 4, st);
+                if (he == hipSuccess)
+                    k_dedup_bin<<<nbd, DEDUP_BLOCK, 0, st>>>(cre, n, table, tsize - 1, bins, lflag, hist, nbd, nfol, fol);
+            }
             tb = tmp_bytes;
             if (he == hipSuccess) he = hipcub::DeviceScan::ExclusiveSum(tmp, tb, hist, hbase, SPLIT_BINS * nbd, st);
             u32 hb = 0, hl = 0;  // the leaders: the last bin's base + its last block's count
@@ -4739,7 +4831,8 @@ static int perft_split_leaves(hipStream_t st, SoA leaf, uint64_t* leaf_out) {
             if (e0 && e1) (void)hipEventRecord(e0, st);
             k_perft2_val<<<grid_for(lead_n), BLOCK, 0, st>>>(cr, lead_n, val, psum);
             if (e0 && e1) (void)hipEventRecord(e1, st);
-            k_followers<<<2048, BLOCK, 0, st>>>(fol, nfol, place_of, val, psum);
+            if (sortdedup) k_followers2<<<2048, BLOCK, 0, st>>>(n, lflag, lead, parent_of, place_of, val, psum);
+            else k_followers<<<2048, BLOCK, 0, st>>>(fol, nfol, place_of, val, psum);
             records += (uint64_t)total;
             subtrees += (uint64_t)lead_n;
         } else if (total > 0 && !gather) {  // the records in move-count order, then read in order
