@@ -211,13 +211,16 @@ def perft_leg(args, rep):
     # per subtree (the 64-B root record in, its count kept and added into the parent's sum)
     # against ~1e3 leaves -- so its roof is the VALU issue rate (PMC profile, tools/gpu_run.sh
     # pmcp*).  Transpositions (round 4): the split pass counts one depth-2 subtree per distinct
-    # position of a chunk (k_dedup_bin, exact: whole-record compare) and adds that count to
-    # every parent the position occurs under; GC_PERFT_DEDUP=0 counts every record
-    # (k_perft2_rec, 72 B); GC_PERFT_GATHER: the round-2/3 form, gathering through a sorted
-    # permutation (+ 4 B index)
+    # position of a chunk (exact: whole-record compare) and adds that count to every parent the
+    # position occurs under -- round 5: the records sorted by hash tag, each leader's leaf lane
+    # adding its count into its followers' parents (72 B: record + parent add; the count kept
+    # for a follower pass, GC_PERFT_FUSE=0 or the CAS table GC_PERFT_SORTDEDUP=0: 80 B);
+    # GC_PERFT_DEDUP=0 counts every record (k_perft2_rec, 72 B); GC_PERFT_GATHER: the
+    # round-2/3 form, gathering through a sorted permutation (+ 4 B index)
     gather = bool(os.environ.get("GC_PERFT_GATHER"))
     dedup = not gather and os.environ.get("GC_PERFT_DEDUP", "1") != "0"
-    alg_sub = 76 if gather else (80 if dedup else 72)  # + the 8-B count kept for the followers
+    fused = dedup and os.environ.get("GC_PERFT_SORTDEDUP", "1") != "0" and os.environ.get("GC_PERFT_FUSE", "1") != "0"
+    alg_sub = 76 if gather else (72 if fused or not dedup else 80)
     la, sub, kms = (b - a for a, b in zip(leaf0, leaf1))
     recs, counted = (b - a for a, b in zip(dd0, dd1))
     if recs:

@@ -761,15 +761,42 @@ __global__ void __launch_bounds__(BLOCK) k_dedup_keys(const Node64* __restrict__
     const Pos s = node_load(in, i);
     keys[i] = (u32)(pos_hash(s) >> 32);
     vals[i] = (u32)i;
-    parent_of[i] = reinterpret_cast<const u32*>(in + i)[15];
+    if (parent_of) parent_of[i] = reinterpret_cast<const u32*>(in + i)[15];
     bins[i] = (uint8_t)split_bin(s, king_lines_of(s, (s.meta & M_WHITE) != 0));
 }
+#ifndef GC_DEDUP_PAR
+#define GC_DEDUP_PAR 1  // k_dedup_runs: one lane per sorted record (0: one lane per run, members in a loop)
+#endif
 __global__ void __launch_bounds__(BLOCK) k_dedup_runs(const Node64* __restrict__ in, int n, const u32* __restrict__ keys,
                                                       const u32* __restrict__ vals, uint8_t* __restrict__ lflag,
                                                       u32* __restrict__ lead) {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= n) return;
     const u32 k = keys[p];
+#if GC_DEDUP_PAR
+    // every lane settles its own record: the run's first member (earliest in record order, the
+    // sort being stable) leads; a later member follows the earliest member equal to it -- the
+    // run's first, or after a tag collision an earlier member found by the ordered scan
+    const u32 r = vals[p];
+    int p0 = p;
+    while (p0 > 0 && keys[p0 - 1] == k) p0--;
+    u32 ld = r;
+    if (p0 < p) {
+        const Pos s = node_load(in, r);
+        const u32 r0 = vals[p0];
+        if (pos_equal(s, node_load(in, r0))) {
+            ld = r0;
+        } else {
+            for (int t = p0 + 1; t < p; t++) {
+                const u32 rt = vals[t];
+                if (pos_equal(node_load(in, rt), s)) { ld = rt; break; }
+            }
+        }
+    }
+    lflag[r] = ld == r ? 1 : 0;
+    if (ld != r) lead[r] = ld;
+#else
+    if (p > 0 && keys[p - 1] == k) return;  // not a run's first member
     if (p > 0 && keys[p - 1] == k) return;  // not a run's first member
     int q = p + 1;
     while (q < n && keys[q] == k) q++;
@@ -788,6 +815,7 @@ __global__ void __launch_bounds__(BLOCK) k_dedup_runs(const Node64* __restrict__
         lflag[r] = ld == r ? 1 : 0;
         lead[r] = ld;
     }
+#endif
 }
 __global__ void __launch_bounds__(DEDUP_BLOCK) k_leader_hist(int n, const uint8_t* __restrict__ lflag,
                                                              const uint8_t* __restrict__ bins, u32* __restrict__ hist,
@@ -809,10 +837,78 @@ __global__ void k_followers2(int n, const uint8_t* __restrict__ lflag, const u32
         if (!lflag[i]) atomicAdd(parent_sum + parent_of[i], (unsigned long long)val[place_of[lead[i]]]);
 }
 
-// one lane = one placed leader (move-count order); its count kept for the followers
+// The followers credited by their leader's lane in the leaf (GC_PERFT_FUSE, the default): no
+// follower pass, no kept counts.  k_dedup_runs_f writes, per record, a lead word (bit 31: it leads,
+// low bits: its sorted position) and, in sorted order, each member's leader position and parent;
+// the leaf lane of the leader at sorted position pL walks its run (keys2[pL] onwards) and adds its
+// count into the parent of every member whose leader is pL.
+__global__ void __launch_bounds__(BLOCK) k_dedup_runs_f(const Node64* __restrict__ in, int n,
+                                                        const u32* __restrict__ keys, const u32* __restrict__ vals,
+                                                        u32* __restrict__ leadw, u32* __restrict__ fld_s,
+                                                        u32* __restrict__ fpar_s) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const u32 k = keys[p];
+    const u32 r = vals[p];
+    int p0 = p;
+    while (p0 > 0 && keys[p0 - 1] == k) p0--;
+    u32 lp = (u32)p, parent = 0;
+    if (p0 < p) {  // a later member: the earliest equal member leads (as k_dedup_runs)
+        const Pos s = node_load(in, r);
+        parent = reinterpret_cast<const u32*>(in + r)[15];
+        if (pos_equal(s, node_load(in, vals[p0]))) {
+            lp = (u32)p0;
+        } else {
+            for (int t = p0 + 1; t < p; t++)
+                if (pos_equal(node_load(in, vals[t]), s)) { lp = (u32)t; break; }
+        }
+    }
+    leadw[r] = lp == (u32)p ? (0x80000000u | (u32)p) : 0u;
+    fld_s[p] = lp;
+    fpar_s[p] = parent;
+}
+__global__ void __launch_bounds__(DEDUP_BLOCK) k_leader_hist_f(int n, const u32* __restrict__ leadw,
+                                                               const uint8_t* __restrict__ bins, u32* __restrict__ hist,
+                                                               int nblk) {
+    __shared__ u32 hb[SPLIT_BINS];
+    for (int b = threadIdx.x; b < SPLIT_BINS; b += blockDim.x) hb[b] = 0;
+    __syncthreads();
+    for (int r = 0; r < DEDUP_R; r++) {  // k_place_leaders' blocks: DEDUP_BLOCK * DEDUP_R records
+        const size_t i = (size_t)blockIdx.x * DEDUP_BLOCK * DEDUP_R + (size_t)r * DEDUP_BLOCK + threadIdx.x;
+        if (i < (size_t)n && (leadw[i] >> 31)) atomicAdd(&hb[bins[i]], 1u);
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < SPLIT_BINS; b += blockDim.x) hist[(size_t)b * nblk + blockIdx.x] = hb[b];
+}
+__global__ void __launch_bounds__(DEDUP_BLOCK) k_place_leaders_f(const Node64* __restrict__ in, int n,
+                                                                 const uint8_t* __restrict__ bins,
+                                                                 const u32* __restrict__ leadw,
+                                                                 const u32* __restrict__ base, int nblk,
+                                                                 Node64* __restrict__ out, u32* __restrict__ spos) {
+    __shared__ u32 cur[SPLIT_BINS];
+    for (int b = threadIdx.x; b < SPLIT_BINS; b += blockDim.x) cur[b] = base[(size_t)b * nblk + blockIdx.x];
+    __syncthreads();
+    for (int r = 0; r < DEDUP_R; r++) {
+        const size_t i = (size_t)blockIdx.x * DEDUP_BLOCK * DEDUP_R + (size_t)r * DEDUP_BLOCK + threadIdx.x;
+        if (i >= (size_t)n) continue;
+        const u32 w = leadw[i];
+        if (!(w >> 31)) continue;
+        const u32 slot = atomicAdd(&cur[bins[i]], 1u);
+        const ulonglong2* x = reinterpret_cast<const ulonglong2*>(in + i);
+        ulonglong2* y = reinterpret_cast<ulonglong2*>(out + slot);
+        const ulonglong2 r0 = x[0], r1 = x[1], r2 = x[2], r3 = x[3];
+        y[0] = r0; y[1] = r1; y[2] = r2; y[3] = r3;
+        spos[slot] = w & 0x7FFFFFFFu;
+    }
+}
+
+// one lane = one placed leader (move-count order); its count kept for the followers (FUSE: added
+// into the followers' parents by this lane)
+template <bool FUSE>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(PERFT2_WPE)))
 k_perft2_val(const Node64* __restrict__ in, int n, uint64_t* __restrict__ val,
-             unsigned long long* __restrict__ parent_sum) {
+             unsigned long long* __restrict__ parent_sum, int nrec, const u32* __restrict__ keys,
+             const u32* __restrict__ fld_s, const u32* __restrict__ fpar_s, const u32* __restrict__ spos) {
     __shared__ u64 lds_a[SCRATCH_SLOTS * BLOCK];
     LdsScratch sa{lds_a + threadIdx.x};
 #ifndef GC_PERFT_LDS
@@ -831,8 +927,15 @@ k_perft2_val(const Node64* __restrict__ in, int n, uint64_t* __restrict__ val,
 #else
     const uint64_t c = perft2(node_load(in, i), sa);
 #endif
-    val[i] = c;
     atomicAdd(parent_sum + parent, (unsigned long long)c);
+    if (!FUSE) {
+        val[i] = c;
+    } else {
+        const u32 pl = spos[i];
+        const u32 k = keys[pl];
+        for (int j = (int)pl + 1; j < nrec && keys[j] == k; j++)
+            if (fld_s[j] == pl) atomicAdd(parent_sum + fpar_s[j], (unsigned long long)c);
+    }
 }
 __global__ void k_followers(const uint2* __restrict__ fol, const u32* __restrict__ nfol,
                             const int32_t* __restrict__ place_of, const uint64_t* __restrict__ val,
@@ -4723,6 +4826,10 @@ static int perft_split_leaves(hipStream_t st, SoA leaf, uint64_t* leaf_out) {
     // GC_PERFT_SORTDEDUP=0 (A/B): the transposition pass by one CAS per record (k_dedup_bin)
     const char* sd = getenv("GC_PERFT_SORTDEDUP");
     const bool sortdedup = !(sd && sd[0] == '0');
+    // GC_PERFT_FUSE=0 (A/B, sorting pass only): the followers added by a pass of their own
+    // (k_followers2) instead of by their leader's leaf lane
+    const char* sf = getenv("GC_PERFT_FUSE");
+    const bool fuse = sortdedup && !(sf && sf[0] == '0');
     int32_t *kc = nullptr, *offs = nullptr, *kc2 = nullptr, *ks = nullptr, *ix = nullptr, *is = nullptr;
     uint8_t* bins = nullptr;
     u32 *hist = nullptr, *hbase = nullptr;
@@ -4802,7 +4909,15 @@ static int perft_split_leaves(hipStream_t st, SoA leaf, uint64_t* leaf_out) {
             u32* const vals2 = keys + 3 * cap;
             u32* const parent_of = reinterpret_cast<u32*>(fol);
             u32* const lead = parent_of + cap;
-            if (sortdedup) {
+            u32* const leadw = parent_of;                              // FUSE: per record
+            u32* const spos = reinterpret_cast<u32*>(place_of);        // FUSE: per placed leader
+            if (fuse) {  // after the sort, the unsorted keys / values hold the members' leaders / parents
+                k_dedup_keys<<<grid_for(n), BLOCK, 0, st>>>(cre, n, keys, vals, bins, nullptr);
+                tb = tmp_bytes;
+                he = hipcub::DeviceRadixSort::SortPairs(tmp, tb, keys, keys2, vals, vals2, n, 0, 32, st);
+                if (he == hipSuccess) k_dedup_runs_f<<<grid_for(n), BLOCK, 0, st>>>(cre, n, keys2, vals2, leadw, keys, vals);
+                if (he == hipSuccess) k_leader_hist_f<<<nbd, DEDUP_BLOCK, 0, st>>>(n, leadw, bins, hist, nbd);
+            } else if (sortdedup) {
                 k_dedup_keys<<<grid_for(n), BLOCK, 0, st>>>(cre, n, keys, vals, bins, parent_of);
                 tb = tmp_bytes;
                 he = hipcub::DeviceRadixSort::SortPairs(tmp, tb, keys, keys2, vals, vals2, n, 0, 32, st);
@@ -4820,7 +4935,9 @@ static int perft_split_leaves(hipStream_t st, SoA leaf, uint64_t* leaf_out) {
             const size_t last = (size_t)SPLIT_BINS * nbd - 1;
             if (he == hipSuccess) he = hipMemcpyAsync(&hb, hbase + last, 4, hipMemcpyDeviceToHost, st);
             if (he == hipSuccess) he = hipMemcpyAsync(&hl, hist + last, 4, hipMemcpyDeviceToHost, st);
-            if (he == hipSuccess)
+            if (he == hipSuccess && fuse)
+                k_place_leaders_f<<<nbd, DEDUP_BLOCK, 0, st>>>(cre, n, bins, leadw, hbase, nbd, cr, spos);
+            else if (he == hipSuccess)
                 k_place_leaders<<<nbd, DEDUP_BLOCK, 0, st>>>(cre, n, bins, lflag, hbase, nbd, cr, place_of);
             if (he == hipSuccess) he = hipStreamSynchronize(st);  // the leaf grid sized to the leaders
             if (he != hipSuccess) { err = std::string("perft split dedup: ") + hipGetErrorString(he); rc = -1; break; }
@@ -4829,10 +4946,13 @@ static int perft_split_leaves(hipStream_t st, SoA leaf, uint64_t* leaf_out) {
             if (hipEventCreate(&e0) == hipSuccess) evs.push_back(e0);
             if (hipEventCreate(&e1) == hipSuccess) evs.push_back(e1);
             if (e0 && e1) (void)hipEventRecord(e0, st);
-            k_perft2_val<<<grid_for(lead_n), BLOCK, 0, st>>>(cr, lead_n, val, psum);
+            if (fuse)
+                k_perft2_val<true><<<grid_for(lead_n), BLOCK, 0, st>>>(cr, lead_n, val, psum, n, keys2, keys, vals, spos);
+            else
+                k_perft2_val<false><<<grid_for(lead_n), BLOCK, 0, st>>>(cr, lead_n, val, psum, 0, nullptr, nullptr, nullptr, nullptr);
             if (e0 && e1) (void)hipEventRecord(e1, st);
-            if (sortdedup) k_followers2<<<2048, BLOCK, 0, st>>>(n, lflag, lead, parent_of, place_of, val, psum);
-            else k_followers<<<2048, BLOCK, 0, st>>>(fol, nfol, place_of, val, psum);
+            if (!fuse && sortdedup) k_followers2<<<2048, BLOCK, 0, st>>>(n, lflag, lead, parent_of, place_of, val, psum);
+            else if (!fuse) k_followers<<<2048, BLOCK, 0, st>>>(fol, nfol, place_of, val, psum);
             records += (uint64_t)total;
             subtrees += (uint64_t)lead_n;
         } else if (total > 0 && !gather) {  // the records in move-count order, then read in order

@@ -318,25 +318,28 @@ def test_perft_split_leaves_matches_depth3_subtrees(engine):
     assert (split == whole).all() and split.sum() > 200 * 10**6, np.nonzero(split != whole)[0][:4]
 
 
-@pytest.mark.parametrize("form", ["sort", "cas"])
+@pytest.mark.parametrize("form", ["fused", "sort", "cas"])
 def test_perft_split_transpositions_merged_exactly(engine, form):
     """The split pass's transposition pass (one leaf count per distinct depth-2 root of a chunk,
     the other records adding the leader's count to their own parents) == every record counted
-    (GC_PERFT_DEDUP=0), per root; the merge happened (counted < records).  Both forms: the
-    records sorted by hash tag (k_dedup_keys / k_dedup_runs, the default) and one CAS per record
-    into a table (k_dedup_bin, GC_PERFT_SORTDEDUP=0)."""
+    (GC_PERFT_DEDUP=0), per root; the merge happened (counted < records).  Every form: the
+    records sorted by hash tag with the followers credited by their leader's leaf lane
+    (k_dedup_runs_f, the default) or by a pass of their own (k_dedup_runs + k_followers2,
+    GC_PERFT_FUSE=0), and one CAS per record into a table (k_dedup_bin, GC_PERFT_SORTDEDUP=0)."""
     import os
 
     from gym_chess_amd.engine import perft_dedup_stats
 
     b, m = _midgame_roots(200, 21, 0x5EED + 5)
     r0, c0 = perft_dedup_stats()
-    if form == "cas":
-        os.environ["GC_PERFT_SORTDEDUP"] = "0"
+    knob = {"fused": None, "sort": "GC_PERFT_FUSE", "cas": "GC_PERFT_SORTDEDUP"}[form]
+    if knob:
+        os.environ[knob] = "0"
     try:
         merged = engine.perft(b, m, 5)
     finally:
-        os.environ.pop("GC_PERFT_SORTDEDUP", None)
+        if knob:
+            os.environ.pop(knob, None)
     r1, c1 = perft_dedup_stats()
     os.environ["GC_PERFT_DEDUP"] = "0"
     try:
