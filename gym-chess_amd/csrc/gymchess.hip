@@ -3242,7 +3242,7 @@ __global__ void __launch_bounds__(BLOCK) k_env_step_api(EnvDev e, const uint16_t
                                                         int32_t* __restrict__ rw, uint8_t* __restrict__ dn,
                                                         uint8_t* __restrict__ rs, u64* __restrict__ mask,
                                                         int8_t* __restrict__ obs, int32_t* __restrict__ cnt,
-                                                        uint16_t* __restrict__ pick_out, int autoreset) {
+                                                        uint16_t* __restrict__ pick_out, int autoreset, size_t mstride) {
     LDS_SCRATCH_DECL;
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= e.n) return;
@@ -3271,7 +3271,7 @@ __global__ void __launch_bounds__(BLOCK) k_env_step_api(EnvDev e, const uint16_t
     dn[i] = (uint8_t)o.done;
     rs[i] = (uint8_t)o.reason;
     if (cnt) cnt[i] = ms.total;
-    if (mask) write_mask(s, g, ms, scr, mask + i, (size_t)e.n);
+    if (mask) write_mask(s, g, ms, scr, mask + i, mstride);
     if (obs) write_obs(s, obs + 64 * (size_t)i);
     if (pick_out) {
         uint16_t p = pick_mask_order(s, g, ms, scr, e.seed, i, pc.draw);
@@ -3305,6 +3305,7 @@ struct ApiOut {
     int8_t* obs;
     int32_t* cnt;
     uint16_t* pick;
+    size_t ms;  // the mask's row stride in words (gc_env_set_mask_stride; default n)
 };
 __device__ __forceinline__ void ic_moves(const EnvDev::InitCache& ic, Gen& g, MoveSet& ms) {
     g.white = ic.white;
@@ -3331,7 +3332,7 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
     rinfo &= 0x1FFFFu;
     ApiOut out;
     PAIR_PROLOGUE_ACT(acts, out = *outp; asm volatile("" : "+s"(out.rw), "+s"(out.dn), "+s"(out.rs), "+s"(out.mask),
-                                                                  "+s"(out.obs), "+s"(out.cnt), "+s"(out.pick));)
+                                                                  "+s"(out.obs), "+s"(out.cnt), "+s"(out.pick), "+s"(out.ms));)
     PairScratch scr{&L.slots[0][l]};
 #ifdef GC_API_PRIO  // diagnostic: issue priority 2 for W0 (1) or W1 (2)
     if ((GC_API_PRIO == 1 && role == 0) || (GC_API_PRIO == 2 && role == 1)) __builtin_amdgcn_s_setprio(2);
@@ -3430,7 +3431,7 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
     }
     if (out.mask && live) {
         u64* o = out.mask + i;
-        const size_t N = (size_t)nn;
+        const size_t N = out.ms;
         if (!ms.big) {  // W1 squares 0..31, W0 32..63 and the castles word
             const int s0 = role ? 0 : 32;
             int j = popc(g.own & below(s0));
@@ -3631,7 +3632,7 @@ __device__ __forceinline__ void apiq_run(uint8_t* __restrict__ slab, uint64_t se
     rinfo &= 0x1FFFFu;
     const bool live = i < nn;
     const int ii = live ? i : nn - 1;  // dead lanes read a valid board, store nothing
-    const size_t N = (size_t)nn;
+    const size_t N = out.ms;  // the mask rows' stride
     const PairIO in_io(slab, nn);
     const PairCtx C = {seed, htab, in_io.hgen, racts, icd, (rinfo >> 16) != 0, rinfo & 0xFFFFu};
     // every role reads the pre-move board and the action (the stateless roles decide the outcome
@@ -3949,7 +3950,7 @@ __global__ void __launch_bounds__(4 * QUAD_BOARDS * QUADS_WG) __attribute__((amd
     const int i = (blockIdx.x * QUADS_WG + qw) * QUAD_BOARDS + l;
     ApiOut out = *outp;
     asm volatile("" : "+s"(out.rw), "+s"(out.dn), "+s"(out.rs), "+s"(out.mask), "+s"(out.obs), "+s"(out.cnt),
-                 "+s"(out.pick));
+                 "+s"(out.pick), "+s"(out.ms));
     switch (role) {
         case 0: apiq_run<0>(slab, seed, htab, racts, icd, acts, out, nn, rinfo, qw, l, i); break;
         case 1: apiq_run<1>(slab, seed, htab, racts, icd, acts, out, nn, rinfo, qw, l, i); break;
@@ -3982,7 +3983,7 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
     rinfo &= 0x1FFFFu;
     ApiOut out;
     PAIR_PROLOGUE_ACT(acts, out = *outp; asm volatile("" : "+s"(out.rw), "+s"(out.dn), "+s"(out.rs), "+s"(out.mask),
-                                                                  "+s"(out.obs), "+s"(out.cnt), "+s"(out.pick));)
+                                                                  "+s"(out.obs), "+s"(out.cnt), "+s"(out.pick), "+s"(out.ms));)
     PairScratch scr{&L.slots[0][l]};
     const uint16_t* const sw_tab = C.racts + RESET_ACTS_MAX;  // the start position's picks in move-set order
     const bool done0 = (s.meta & M_DONE) != 0;              // chess_v2.py:245-251
@@ -4147,7 +4148,7 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
     }
     if (out.mask && live) {
         u64* om = out.mask + i;
-        const size_t N = (size_t)nn;
+        const size_t N = out.ms;
         if (!ms.big) {  // W1 squares 0..31, W0 32..63 and the castles word
             const int q0 = role ? 0 : 32;
             int j = popc(g.own & below(q0));
@@ -4223,7 +4224,7 @@ __global__ void __launch_bounds__(BLOCK) k_fenv_step_api(EnvDev e, const uint16_
                                                          int32_t* __restrict__ rw, uint8_t* __restrict__ dn,
                                                          uint8_t* __restrict__ rs, u64* __restrict__ mask,
                                                          int8_t* __restrict__ obs, int32_t* __restrict__ cnt,
-                                                         uint16_t* __restrict__ pick_out, int autoreset) {
+                                                         uint16_t* __restrict__ pick_out, int autoreset, size_t mstride) {
     LDS_SCRATCH_DECL;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= e.n) return;
@@ -4246,7 +4247,7 @@ __global__ void __launch_bounds__(BLOCK) k_fenv_step_api(EnvDev e, const uint16_
         have = true;
     }
     if (!have) gcf::fgen(s, f);
-    const size_t N = (size_t)e.n;
+    const size_t N = mstride;
     u64 cw = 0;  // bit c = action 4096 + c
     if (f.g.castles & 1) cw |= f.g.white ? (1ull << 1) : (1ull << 3);
     if (f.g.castles & 2) cw |= f.g.white ? (1ull << 0) : (1ull << 2);
@@ -5192,6 +5193,7 @@ struct gc_env {
     int rules = 0;              // 0 reference, 1 FIDE (gc_fide.h)
     int8_t* ep = nullptr;       // FIDE ingest: en-passant files
     ApiOut* api_out = nullptr;  // the paired API step's output pointers (device copy of api_host)
+    int64_t mask_stride = 0;    // gc_env_step_device's mask row stride in words (0: n)
     ApiOut api_host{};
     uint16_t* reset_acts = nullptr;
     EnvDev::InitCache* icd = nullptr;  // device copy of d.ic (the paired kernels read it from HBM)
@@ -5953,6 +5955,16 @@ extern "C" int gc_env_step(gc_env* e, const uint16_t* actions, int32_t* reward, 
     return 0;
 }
 
+// the row stride (in 64-bit words, >= n; 0 = n) of gc_env_step_device's d_mask from the next call
+// on: with n a multiple of a large power of two, rows n words apart alias on the same HBM
+// channels, so a caller may pad them (gym_chess_amd.env.DeviceIO does)
+extern "C" int gc_env_set_mask_stride(gc_env* e, int64_t words) {
+    if (!e) return fail("null env");
+    if (words != 0 && words < (int64_t)e->n) return fail("mask stride below the board count");
+    e->mask_stride = words;
+    return 0;
+}
+
 // step() with device buffers (k_env_step_api): asynchronous on the env's stream
 // (gc_env_get_stream); every pointer is device memory of n entries (mask: n*65 words, obs:
 // n*64 bytes); mask / obs / count / pick may be NULL.
@@ -5965,13 +5977,14 @@ extern "C" int gc_env_step_device(gc_env* e, const uint16_t* d_actions, int32_t*
     HIPCHK(hipSetDevice(e->device));
     if (spill_before(e)) return -1;
     const int ar = flags & 1;
+    const size_t ms = e->mask_stride ? (size_t)e->mask_stride : (size_t)e->n;  // the mask rows' stride
     if (e->rules) {  // FIDE: one lane per board
         if (e->d.opp)
             k_fenv_step_api<true><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d, d_actions, d_reward, d_done, d_reason,
-                                                                            d_mask, d_obs, d_count, d_pick, ar);
+                                                                            d_mask, d_obs, d_count, d_pick, ar, ms);
         else
             k_fenv_step_api<false><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d, d_actions, d_reward, d_done, d_reason,
-                                                                             d_mask, d_obs, d_count, d_pick, ar);
+                                                                             d_mask, d_obs, d_count, d_pick, ar, ms);
         HIPCHK(hipGetLastError());
         if (spill_after(e)) return -1;
         e->policy_ready = d_pick != nullptr;
@@ -5982,7 +5995,7 @@ extern "C" int gc_env_step_device(gc_env* e, const uint16_t* d_actions, int32_t*
         const EnvDev& d = e->d;
         const ResetInfo r = reset_info(e);
         const int nb = (e->n + PAIR_BOARDS - 1) / PAIR_BOARDS;
-        const ApiOut o = {d_reward, d_done, d_reason, d_mask, d_obs, d_count, d_pick};
+        const ApiOut o = {d_reward, d_done, d_reason, d_mask, d_obs, d_count, d_pick, ms};
         if (!e->api_out) {
             if (dalloc(&e->api_out, 1)) return -1;
             e->api_host = {};
@@ -6023,7 +6036,7 @@ extern "C" int gc_env_step_device(gc_env* e, const uint16_t* d_actions, int32_t*
         const EnvDev& d = e->d;
         const ResetInfo r = reset_info(e);
         const int nb = (e->n + PAIR_BOARDS - 1) / PAIR_BOARDS;
-        const ApiOut o = {d_reward, d_done, d_reason, d_mask, d_obs, d_count, d_pick};
+        const ApiOut o = {d_reward, d_done, d_reason, d_mask, d_obs, d_count, d_pick, ms};
         if (!e->api_out) {
             if (dalloc(&e->api_out, 1)) return -1;
             e->api_host = {};
@@ -6042,10 +6055,10 @@ extern "C" int gc_env_step_device(gc_env* e, const uint16_t* d_actions, int32_t*
                                                                       e->api_out, d.n, r.rinfo | ((u32)ar << 17));
     } else if (e->d.opp)
         k_env_step_api<true><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d, d_actions, d_reward, d_done, d_reason,
-                                                                      d_mask, d_obs, d_count, d_pick, ar);
+                                                                      d_mask, d_obs, d_count, d_pick, ar, ms);
     else
         k_env_step_api<false><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d, d_actions, d_reward, d_done, d_reason,
-                                                                       d_mask, d_obs, d_count, d_pick, ar);
+                                                                       d_mask, d_obs, d_count, d_pick, ar, ms);
     HIPCHK(hipGetLastError());
     if (spill_after(e)) return -1;
     e->policy_ready = d_pick != nullptr;

@@ -18,6 +18,7 @@ rules="fide" plays FIDE chess (gym-chess_amd/csrc/gc_fide.h, SURVEY.md §8f row 
 reference env's rewards and bookkeeping; an action promotes to a queen.
 """
 import ctypes
+import os
 
 import numpy as np
 
@@ -43,6 +44,7 @@ class BatchedChessEnv:
         _lib.check(self._L.gc_env_create(self.device, self.num_boards, ctypes.c_uint64(self.seed),
                                          _lib.ptr(ib) if ib is not None else None, ctypes.byref(h)))
         self._h = h
+        self._mask_stride = 0  # gc_env_set_mask_stride's value (0: num_boards)
         if opponent not in ("none", "random"):
             raise ValueError(f"Unrecognized opponent policy {opponent} (batched env: 'none' or 'random'; "
                              "drive both sides yourself for a custom opponent)")
@@ -271,10 +273,11 @@ class BatchedChessEnv:
         return int(self._L.gc_env_device_bytes(self._h))
 
     # ------------------------------------------------------------------ device-buffer step
-    def device_io(self, mask=True, obs=True, count=True, pick=True, select=True):
+    def device_io(self, mask=True, obs=True, count=True, pick=True, select=True, mask_stride=None):
         """Device buffers for step_device (gc_device_alloc on this env's device); with pick and
-        select, the pick buffer starts as the random policy's actions for the current states."""
-        return DeviceIO(self, mask=mask, obs=obs, count=count, pick=pick, select=select)
+        select, the pick buffer starts as the random policy's actions for the current states.
+        mask_stride: the mask's row stride in words (>= N; None = DeviceIO.default_mask_stride)."""
+        return DeviceIO(self, mask=mask, obs=obs, count=count, pick=pick, select=select, mask_stride=mask_stride)
 
     def step_device(self, io, actions=None, autoreset=False):
         """step() on device buffers (gc_env_step_device), asynchronous on the env's stream.
@@ -284,6 +287,9 @@ class BatchedChessEnv:
         if not a:
             raise ValueError("no actions: pass a device pointer or allocate io with pick=True")
         p = io.ptr
+        if io.mask_stride != self._mask_stride:
+            _lib.check(self._L.gc_env_set_mask_stride(self._h, io.mask_stride))
+            self._mask_stride = io.mask_stride
         _lib.check(self._L.gc_env_step_device(self._h, a, p["reward"], p["done"], p["reason"], p.get("mask"),
                                               p.get("obs"), p.get("count"), p.get("pick"), int(bool(autoreset))))
 
@@ -355,22 +361,39 @@ class TraceBuffer:
 
 class DeviceIO:
     """Device buffers of one env's step_device outputs: reward i32, done u8, reason u8 and
-    optionally mask u64[65][N] (word-major), obs i8[N][64], count i32, pick u16 (the random policy's next
-    action, which step_device uses as the actions when given none).  fetch() copies them to
-    host arrays; upload_actions() fills the pick buffer from the host."""
+    optionally mask u64[65][stride] (word-major: word f of board i at f * stride + i, stride >= N),
+    obs i8[N][64], count i32, pick u16 (the random policy's next action, which step_device uses
+    as the actions when given none).  fetch() copies them to host arrays; upload_actions() fills
+    the pick buffer from the host."""
 
     _SPEC = {"reward": (np.int32, ()), "done": (np.uint8, ()), "reason": (np.uint8, ()),
              "mask": (np.uint64, (65,)), "obs": (np.int8, (64,)), "count": (np.int32, ()), "pick": (np.uint16, ())}
 
-    def __init__(self, env, mask=True, obs=True, count=True, pick=True, select=True):
+    @staticmethod
+    def default_mask_stride(n):
+        """N plus GC_MASK_PAD words (default MASK_PAD) once N is a multiple of 512: packed rows of
+        such an N sit a multiple of 4 KiB apart and fall on the same HBM channels.  Measured on
+        the quad API step at N = 65 536 (same box): packed 17.0 us per launch, padded by 8 words
+        16.4, by 64 16.2, by 256-4096 15.6-15.8 -- 512 (4 KiB) kept."""
+        pad = int(os.environ.get("GC_MASK_PAD", DeviceIO.MASK_PAD))
+        return n + pad if n % 512 == 0 else n
+
+    MASK_PAD = 512
+
+    def __init__(self, env, mask=True, obs=True, count=True, pick=True, select=True, mask_stride=None):
         self.env = env
+        n = env.num_boards
+        self.mask_stride = int(self.default_mask_stride(n) if mask_stride is None else mask_stride)
+        if self.mask_stride < n:
+            raise ValueError(f"mask_stride {self.mask_stride} < num_boards {n}")
         want = {"reward": True, "done": True, "reason": True, "mask": mask, "obs": obs, "count": count, "pick": pick}
         self.ptr = {}
         for k, on in want.items():
             if not on:
                 continue
             dt, sh = self._SPEC[k]
-            nb = env.num_boards * int(np.prod(sh, dtype=np.int64)) * np.dtype(dt).itemsize
+            rows = self.mask_stride if k == "mask" else n
+            nb = rows * int(np.prod(sh, dtype=np.int64)) * np.dtype(dt).itemsize
             v = ctypes.c_void_p()
             _lib.check(env._L.gc_device_alloc(env.device, ctypes.c_uint64(nb), ctypes.byref(v)))
             self.ptr[k] = v.value
@@ -387,14 +410,16 @@ class DeviceIO:
         _lib.check(self.env._L.gc_env_copy(self.env._h, self.ptr["pick"], _lib.ptr(a), ctypes.c_uint64(a.nbytes), 1))
 
     def fetch(self, *keys):
-        """host copies; the mask comes back as [N][65] (the device buffer is word-major [65][N])"""
+        """host copies; the mask comes back as [N][65] (the device buffer is word-major
+        [65][mask_stride])"""
         out = {}
+        n = self.env.num_boards
         for k in keys or self.ptr:
             dt, sh = self._SPEC[k]
-            shape = (65, self.env.num_boards) if k == "mask" else (self.env.num_boards,) + sh
+            shape = (65, self.mask_stride) if k == "mask" else (n,) + sh
             a = np.zeros(shape, dtype=dt)
             _lib.check(self.env._L.gc_env_copy(self.env._h, _lib.ptr(a), self.ptr[k], ctypes.c_uint64(a.nbytes), 2))
-            out[k] = np.ascontiguousarray(a.T) if k == "mask" else a
+            out[k] = np.ascontiguousarray(a[:, :n].T) if k == "mask" else a
         return out
 
     def close(self):

@@ -200,3 +200,27 @@ def test_step_device_random_opponent_vs_oracle(oracle, color, autoreset):
                 ors[i].reset()
                 ors[i].pick()
         prev = env.outputs()["next_action"].astype(np.int64) if ends.any() else out["pick"].astype(np.int64)
+
+
+@pytest.mark.parametrize("kind", ["quad", "opponent", "fide"])
+def test_step_device_mask_stride(kind):
+    """A padded mask row stride (gc_env_set_mask_stride) moves only the rows: two envs stepped
+    alike, one with packed rows and one with N + 37 and N + 512 words between rows, give equal
+    masks and outputs -- on the quad API step, the random opponent's paired step and the FIDE
+    one-lane step."""
+    from gym_chess_amd.env import BatchedChessEnv
+
+    n = 1024
+    kw = {"quad": {}, "opponent": {"opponent": "random"}, "fide": {"rules": "fide"}}[kind]
+    envs = [BatchedChessEnv(n, device=0, seed=31, **kw) for _ in range(3)]
+    ios = [e.device_io(mask_stride=st) for e, st in zip(envs, (n, n + 37, n + 512))]
+    assert [io.mask_stride for io in ios] == [n, n + 37, n + 512]
+    for ply in range(40):
+        outs = []
+        for e, io in zip(envs, ios):
+            e.step_device(io, autoreset=True)
+            outs.append(io.fetch())
+        for o in outs[1:]:
+            for k in outs[0]:
+                assert (o[k] == outs[0][k]).all(), (ply, k)
+        assert outs[0]["mask"].shape == (n, 65)
