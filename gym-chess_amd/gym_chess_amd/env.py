@@ -371,12 +371,13 @@ class DeviceIO:
 
     @staticmethod
     def default_mask_stride(n):
-        """N plus GC_MASK_PAD words (default MASK_PAD) once N is a multiple of 512: packed rows of
-        such an N sit a multiple of 4 KiB apart and fall on the same HBM channels.  Measured on
-        the quad API step at N = 65 536 (same box): packed 17.0 us per launch, padded by 8 words
-        16.4, by 64 16.2, by 256-4096 15.6-15.8 -- 512 (4 KiB) kept."""
+        """From N = 4096 on: N rounded up to a multiple of 512, plus GC_MASK_PAD words (default
+        MASK_PAD).  Packed rows of N = 65 536 sit 512 KiB apart and fall on the same HBM
+        channels; measured on the quad API step (same box): packed 17.0 us per launch, padded by
+        8 words 16.4, by 64 16.2, by 256-4096 15.6-15.8 -- 512 (4 KiB) kept; N = 65 472 packed
+        (511.5 KiB apart) 16.8 against 16.2 for 65 536 padded."""
         pad = int(os.environ.get("GC_MASK_PAD", DeviceIO.MASK_PAD))
-        return n + pad if n % 512 == 0 else n
+        return (n + 511) // 512 * 512 + pad if n >= 4096 and pad else n
 
     MASK_PAD = 512
 
