@@ -2252,8 +2252,9 @@ struct QuadLds {
     Pos rp;                          // the reset position (read at a reset: no registers held for it)
 };
 // one set of the next side's moves into LDS, its count into the packed byte counts and the total
-struct QuadSets {
-    QuadLds& L;
+template <class LT>
+struct QuadSetsT {
+    LT& L;
     int l;
     u64 cw[4];
     int part;
@@ -2269,6 +2270,7 @@ struct QuadSets {
         for (int j = LO; j < HI; j++) put(j, t[j - LO]);
     }
 };
+using QuadSets = QuadSetsT<QuadLds>;
 
 // Q0's choice of the next action, left for the start of the next ply: Q2 makes the pick from
 // the move sets in phase 3 while Q0 and Q1 settle the outcome (the pick was phase 3's longest
@@ -3956,6 +3958,511 @@ __global__ void __launch_bounds__(4 * QUAD_BOARDS * QUADS_WG) __attribute__((amd
         case 1: apiq_run<1>(slab, seed, htab, racts, icd, acts, out, nn, rinfo, qw, l, i); break;
         case 2: apiq_run<2>(slab, seed, htab, racts, icd, acts, out, nn, rinfo, qw, l, i); break;
         default: apiq_run<3>(slab, seed, htab, racts, icd, acts, out, nn, rinfo, qw, l, i); break;
+    }
+}
+
+// ----------------------------------------------------------------------------- API step, quads, random opponent
+// k_env_step_api2_vs<false>'s contract (a WHITE agent against the random opponent: the agent's
+// validated action, the reply inside the step, chess_v2.py:219-294 with opponent_policy set) on
+// four waves per 64 boards.  The agent's ply runs as k_env_step_api4's
+// phases 0-2 with the opponent's moves made as the rollout's move sets; the reply is picked and
+// applied in phase 3; phases 4-6 are k_env_step_api4's phases 1-3 for the position the mask
+// describes -- the reply played, or (no reply) the state after the agent's half as it stands:
+//
+//   phase 0   Q0: applies the agent's action              Q1: its window probe, two Philox words
+//             Q2, Q3: validate it (quick_safe / quick_pseudo)     and the reset table's picks
+//   phase 1   the opponent's position: Q0 pins, Q1 the agent's own check, Q2 / Q3 the enemy map
+//   phase 2   Q0 castles, pawn and knight sets | Q1 the agent ply's 3-fold commit
+//             Q2 rook / queen direction sets, king sets | Q3 bishop / queen ones
+//   phase 3   every role: the agent ply's outcome (same arithmetic from LDS); Q2 picks the reply
+//             (draw d, move-set order) and applies it; Q1 writes the agent ply's window entry and
+//             probes the pre-reply board
+//   phase 4   the mask's position: Q0 pins, Q1 the opponent's own check, Q2 / Q3 the enemy map
+//   phase 5   Q0 castles, pawns | Q1 knights, kings, the reply's 3-fold commit | Q2 queens
+//             Q3 rooks, bishops (pieces parked by ordinal, as k_env_step_api4)
+//   phase 6   every role: the reply's outcome, its 16 mask rows; Q2 the agent's pick (the next
+//             draw, action-id order), count and next action; Q3 the observation; Q1 the outputs,
+//             the state and the window
+//
+// Same draws in the same order as k_env_step_api2_vs (and the one-wave k_env_step_api<true>).
+// A BLACK agent (whose reset opens with the opponent's move) stays on k_env_step_api2_vs<true>.
+struct ApiQvSetCounts {
+    u64 cwx[2][4][QUAD_BOARDS];  // Q2 / Q3 -> Q2: their sets' byte counts (phase 2)
+    u64 cw0[QUAD_BOARDS];        // Q0 -> Q2: its sets' (words 0, 1: pawns, knights)
+    u64 cw1[QUAD_BOARDS];
+};
+struct ApiQuadVsLds {
+    union {
+        u64 sets[SW_SETS][QUAD_BOARDS];         // phases 2-3: the opponent's move sets
+        u64 slots[SCRATCH_SLOTS][QUAD_BOARDS];  // phases 5-6: parked targets per own-piece ordinal
+    };
+    u64 ns[NBB][QUAD_BOARDS];    // Q0 -> all (phase 0): the agent's post-move board
+    u32 nmeta[QUAD_BOARDS];
+    int32_t mr[QUAD_BOARDS];     //   its capture reward
+    u32 irrev[QUAD_BOARDS];      //   irreversible move
+    u64 ns2[NBB][QUAD_BOARDS];   // Q2 -> all (phase 3): the mask's position (the reply played, or the kept state)
+    u32 nmeta2[QUAD_BOARDS];
+    int32_t mr2[QUAD_BOARDS];    //   the reply's capture reward
+    u32 irrev2[QUAD_BOARDS];
+    u32 oa[QUAD_BOARDS];         // Q2 -> Q1: the reply
+    u32 valid[2][QUAD_BOARDS];   // Q3 ([0]: the move's shape), Q2 ([1]: king safety) -> all
+    u64 pin3[3][QUAD_BOARDS];    // Q0 -> Q2, Q3: check mask, pinned, pin rays (phases 1 and 4)
+    u32 f0[QUAD_BOARDS];         // Q0 -> all: the side to move is in check
+    u64 enemy[3][QUAD_BOARDS];   // Q2 ([1]), Q3 ([2]) -> all: the enemy map's parts
+    u32 f1[QUAD_BOARDS];         // Q1 -> all: the mover is in check after its move
+    union {
+        ApiQvSetCounts sc;                  // phases 2-3
+        u64 cbw[4][2][QUAD_BOARDS];         // phases 5-6: per role, its pieces' move counts by ordinal
+    };
+    u32 part[4][QUAD_BOARDS];    // move totals (Q0's holds the castles; phase 5: Q3's a big board's)
+    u32 castles[QUAD_BOARDS];    // Q0 -> all
+    u32 rep[QUAD_BOARDS];        // Q1 -> all: the agent ply's 3-fold count | window length << 8
+    u32 rep2[QUAD_BOARDS];       // Q1 -> all: the reply's
+    u32 x0[QUAD_BOARDS];         // Q1 -> Q2: the Philox words of draws d, d + 1
+    u32 x1[QUAD_BOARDS];
+    u32 ra[2][QUAD_BOARDS];      // Q1 -> Q2: the start-position table picks for x0 / x1
+};
+__shared__ ApiQuadVsLds g_apiqv_lds[QUADS_WG];
+
+template <int RR>
+__device__ __forceinline__ void apiqv_run(uint8_t* __restrict__ slab, uint64_t seed, u64* __restrict__ htab,
+                                          const uint16_t* __restrict__ racts, const EnvDev::InitCache* __restrict__ icd,
+                                          const uint16_t* __restrict__ acts, const ApiOut& out, int nn, u32 rinfo,
+                                          int qw, int l, int i) {
+    ApiQuadVsLds& L = g_apiqv_lds[qw];
+    const int autoreset = (rinfo >> 17) & 1;
+    rinfo &= 0x1FFFFu;
+    const bool live = i < nn;
+    const int ii = live ? i : nn - 1;  // dead lanes read a valid board, store nothing
+    const size_t N = out.ms;           // the mask rows' stride
+    const PairIO in_io(slab, nn);
+    const PairCtx C = {seed, htab, in_io.hgen, racts, icd, (rinfo >> 16) != 0, rinfo & 0xFFFFu};
+    Pos s = in_io.load(ii);
+    u32 ua = acts[ii], g0 = 0, nst = 0, d = 0;
+    if (RR == 1) { g0 = in_io.hgen[ii]; nst = in_io.nsteps[ii]; }
+    if (RR == 1 || RR == 2) d = in_io.draw[ii];
+    pin(s); pin(ua); pin(g0); pin(nst); pin(d);
+    const int a = (int)ua;
+    DevHist h = DevHist{htab, in_io.hgen, g0, ii, HTAB_BITS};
+    OrdScratch scr{&L.slots[0][l], 0ull, 0ull};
+    if (RR != 3) __builtin_amdgcn_s_setprio(2);
+    const bool done0 = (s.meta & M_DONE) != 0;   // chess_v2.py:245-251
+    const bool cap = mc_of(s.meta) > MOVES_MAX;  // 252-258
+    const bool white = (s.meta & M_WHITE) != 0;  // the agent's colour
+    const bool pre = live && !done0 && !cap;
+
+    // ---- phase 0: the agent's action applied (speculatively) and validated; Q1's loads issued
+    RepProbe pr;
+    uint16_t ra0 = (uint16_t)A_NONE, ra1 = (uint16_t)A_NONE;
+    if (RR == 0) {
+        Pos ns = s;
+        ns.meta = (ns.meta & ~(u32)M_RIGHTS) | eff_rights(s);  // State::new
+        int mr = 0;
+        bool irrev = false;
+        apply_legal(ns, white, a, &mr, &irrev);
+        L.ns[0][l] = ns.k; L.ns[1][l] = ns.q; L.ns[2][l] = ns.r; L.ns[3][l] = ns.b;
+        L.ns[4][l] = ns.n; L.ns[5][l] = ns.p; L.ns[6][l] = ns.w;
+        L.nmeta[l] = ns.meta;
+        L.mr[l] = mr;
+        L.irrev[l] = irrev ? 1u : 0u;
+    } else if (RR == 1) {
+        if (pre) rep_prefetch(h, s, pr);
+        const u32 x0 = philox_x0(C.seed, (u32)i, d), x1 = philox_x0(C.seed, (u32)i, d + 1);
+        if (C.rtable) {
+            ra0 = C.racts[scale_rank(x0, C.rtotal)];
+            ra1 = C.racts[scale_rank(x1, C.rtotal)];
+        }
+        L.x0[l] = x0;
+        L.x1[l] = x1;
+    } else if (RR == 2) {
+        L.valid[1][l] = quick_safe(s, a) ? 1u : 0u;
+    } else {
+        L.valid[0][l] = quick_pseudo(s, a) ? 1u : 0u;
+    }
+    pair_barrier();
+
+    // ---- phase 1: the opponent's position
+    if (RR == 2) __builtin_amdgcn_s_setprio(0);
+    const bool valid = (L.valid[0][l] & L.valid[1][l]) != 0;
+    const bool mv = pre && valid;  // the agent's env_ply runs
+    Pos ns = s;
+    ns.meta = (ns.meta & ~(u32)M_RIGHTS) | eff_rights(s);
+    if (mv) {
+        ns.k = L.ns[0][l]; ns.q = L.ns[1][l]; ns.r = L.ns[2][l]; ns.b = L.ns[3][l];
+        ns.n = L.ns[4][l]; ns.p = L.ns[5][l]; ns.w = L.ns[6][l];
+        ns.meta = L.nmeta[l];
+    }
+    Gen g;
+    gen_base(ns, g);
+    if (RR == 0) {
+        gen_pins(ns, g);
+        L.pin3[0][l] = g.checkmask;
+        L.pin3[1][l] = g.pinned;
+        L.pin3[2][l] = g.pinrays;
+        L.f0[l] = g.in_check ? 1u : 0u;
+    } else if (RR == 1) {
+        L.f1[l] = (mv && mover_checked(s, ns, white, a)) ? 1u : 0u;
+    } else if (RR == 2) {
+        L.enemy[1][l] = g.ks >= 0 ? side_attacks_leapers(ns, !g.white) | side_attacks_orth(ns, !g.white) : 0ull;
+    } else {
+        L.enemy[2][l] = g.ks >= 0 ? side_attacks_diag(ns, !g.white) : 0ull;
+    }
+    pair_barrier();
+
+    // ---- phase 2: the opponent's move sets (as the rollout's quads); Q1 the agent ply's commit
+    const bool opp_chk = L.f0[l] != 0, my_chk = L.f1[l] != 0;
+    const bool both = mv && opp_chk && my_chk;  // lib.rs:1442-1446: the move is void
+    const bool gen = mv && !both;               // the opponent's moves are due
+    g.in_check = opp_chk;
+    if (RR != 0) {
+        g.checkmask = L.pin3[0][l];
+        g.pinned = L.pin3[1][l];
+        g.pinrays = L.pin3[2][l];
+    }
+    g.enemy_att = L.enemy[1][l] | L.enemy[2][l];
+    QuadSetsT<ApiQuadVsLds> Q{L, l, {0, 0, 0, 0}, 0};
+    const int mr = L.mr[l];
+    const bool irrev = L.irrev[l] != 0;
+    if (RR == 0) {
+        gen_castles(ns, g);
+        if (gen) {
+            u64 T[SW_SETS];
+            sw_pawns(ns, g, T);
+            Q.put_all<SW_P1, SW_N>(T + SW_P1);
+            sw_knights(ns, g, T);
+            Q.put_all<SW_N, SW_ORTH>(T + SW_N);
+            Q.part += popc(g.castles);
+        }
+        L.sc.cw0[l] = Q.cw[0];
+        L.sc.cw1[l] = Q.cw[1];
+        L.castles[l] = g.castles;
+        L.part[0][l] = (u32)Q.part;
+    } else if (RR == 1) {
+        int c = 0;
+        u32 hl = hl_of(s.meta);
+        if (gen) {
+            pin(pr.e0.hdr); pin(pr.e0.k); pin(pr.e0.q); pin(pr.e0.r);
+            pin(pr.e0.b); pin(pr.e0.n); pin(pr.e0.p); pin(pr.e0.w);
+            c = rep_commit(h, s, pr, hl, irrev);  // table write deferred to h.commit()
+        }
+        L.rep[l] = (u32)c | (hl << 8);
+        L.ra[0][l] = ra0;
+        L.ra[1][l] = ra1;
+    } else if (RR == 2) {  // unconditional: ignored unless the opponent's moves are due
+        u64 T[SW_SETS];
+        sw_orth(ns, g, T);
+        Q.put_all<SW_ORTH, SW_DIAG>(T + SW_ORTH);
+        sw_kings(ns, g, T);
+        Q.put_all<SW_K, SW_SETS>(T + SW_K);
+        L.part[2][l] = (u32)Q.part;
+#pragma unroll
+        for (int k = 0; k < 4; k++) L.sc.cwx[0][k][l] = Q.cw[k];
+    } else {
+        u64 T[SW_SETS];
+        sw_diag(ns, g, T);
+        Q.put_all<SW_DIAG, SW_K>(T + SW_DIAG);
+        L.part[3][l] = (u32)Q.part;
+#pragma unroll
+        for (int k = 0; k < 4; k++) L.sc.cwx[1][k][l] = Q.cw[k];
+    }
+    pair_barrier();
+
+    // ---- phase 3: the agent ply's outcome (k_env_step_api2_vs half A); Q2 picks and plays the reply
+    if (RR == 0) __builtin_amdgcn_s_setprio(0);
+    if (RR == 2) __builtin_amdgcn_s_setprio(2);
+    const int tot_opp = gen ? (int)(L.part[0][l] + L.part[2][l] + L.part[3][l]) : 0;
+    StepOut o = {0, 0, R_NONE, 0};
+    bool cont = false;  // the opponent replies
+    Pos s1 = s;         // the state after the agent's half
+    {
+        const u32 rpk = L.rep[l];
+        const int c = (int)(rpk & 0xFFu);
+        const u32 hl = rpk >> 8;
+        if (!valid) {
+            o.reward = -10;
+            o.done = done0 ? 1 : 0;
+            o.reason = R_INVALID;
+        } else if (done0) {
+            o.done = 1;
+            o.reason = R_DONE_ALREADY;
+        } else if (cap) {
+            o.done = 1;
+            o.reason = R_MOVE_CAP;
+        } else if (both) {
+            o.done = 1;
+            o.reason = R_BOTH_CHECKED;
+        } else {
+            const u32 chk = white ? ((my_chk ? M_WCHK : 0u) | (opp_chk ? M_BCHK : 0u))
+                                  : ((opp_chk ? M_WCHK : 0u) | (my_chk ? M_BCHK : 0u));
+            s1 = ns;
+            s1.meta = with_hl((ns.meta & ~(u32)(M_WCHK | M_BCHK | M_DONE)) | chk | ((c >= 3 || c == 0) ? M_DONE : 0u), hl);
+            o.reward = -10 + mr;  // Q9
+            o.moved = 1;
+            if (c >= 3) { o.done = 1; o.reason = R_REPETITION; }
+            if (c == 0) { o.done = 1; o.reason = R_WINDOW_FULL; }
+            if (tot_opp == 0 && opp_chk) {  // 270-272
+                s1.meta |= M_DONE;
+                o.done = 1;
+                o.reward += 100;
+                o.reason = R_MATE;
+            }
+            if (!o.done && tot_opp == 0) {  // 120-122: the opponent's policy "resigns"
+                s1.meta |= M_DONE;
+                o.done = 1;
+                o.reason = R_OPP_NO_MOVE;
+            }
+            cont = !o.done;
+        }
+    }
+    if (RR == 2) {  // the reply (move-set order, draw d) played on the state after the agent's half
+        Pos p = s1;
+        p.meta = (p.meta & ~(u32)M_RIGHTS) | eff_rights(s1);
+        int mr2 = 0;
+        bool irrev2 = false;
+        int oa = A_NONE;
+        if (cont) {
+            u64 cw[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) cw[k] = Q.cw[k] | L.sc.cwx[1][k][l];
+            cw[0] |= L.sc.cw0[l];
+            cw[1] |= L.sc.cw1[l];
+            g.castles = L.castles[l];
+            oa = sw_pick_lds(L, l, g, cw, tot_opp, (int)scale_rank(L.x0[l], (u32)tot_opp));
+            apply_legal(p, (s1.meta & M_WHITE) != 0, oa, &mr2, &irrev2);
+        }
+        L.ns2[0][l] = p.k; L.ns2[1][l] = p.q; L.ns2[2][l] = p.r; L.ns2[3][l] = p.b;
+        L.ns2[4][l] = p.n; L.ns2[5][l] = p.p; L.ns2[6][l] = p.w;
+        L.nmeta2[l] = p.meta;
+        L.mr2[l] = mr2;
+        L.irrev2[l] = irrev2 ? 1u : 0u;
+        L.oa[l] = (u32)oa;
+    } else if (RR == 1 && live) {
+        h.commit();  // the agent ply's window write lands before the reply probes the table
+        if (cont) rep_prefetch(h, s1, pr);
+    }
+    pair_barrier();
+
+    // ---- phase 4: the mask's position (the agent to move after a reply)
+    if (RR == 0) __builtin_amdgcn_s_setprio(2);
+    if (RR == 2) __builtin_amdgcn_s_setprio(0);
+    Pos P;
+    P.k = L.ns2[0][l]; P.q = L.ns2[1][l]; P.r = L.ns2[2][l]; P.b = L.ns2[3][l];
+    P.n = L.ns2[4][l]; P.p = L.ns2[5][l]; P.w = L.ns2[6][l];
+    P.meta = L.nmeta2[l];
+    gen_base(P, g);
+    if (RR == 0) {
+        gen_pins(P, g);
+        L.pin3[0][l] = g.checkmask;
+        L.pin3[1][l] = g.pinned;
+        L.pin3[2][l] = g.pinrays;
+        L.f0[l] = g.in_check ? 1u : 0u;
+    } else if (RR == 1) {
+        L.f1[l] = (cont && mover_checked(s1, P, (s1.meta & M_WHITE) != 0, (int)L.oa[l])) ? 1u : 0u;
+    } else if (RR == 2) {
+        L.enemy[1][l] = g.ks >= 0 ? side_attacks_leapers(P, !g.white) | side_attacks_orth(P, !g.white) : 0ull;
+    } else {
+        L.enemy[2][l] = g.ks >= 0 ? side_attacks_diag(P, !g.white) : 0ull;
+    }
+    pair_barrier();
+
+    // ---- phase 5: the mask position's moves, parked by ordinal; Q1 the reply's commit
+    const bool chk2 = L.f0[l] != 0, mchk2 = L.f1[l] != 0;  // the agent in check; the opponent, after its reply
+    const bool both2 = cont && chk2 && mchk2;
+    const bool gen2 = live && !both2;
+    const bool big = popc(g.own) > SCRATCH_SLOTS;
+    g.in_check = chk2;
+    if (RR != 0) {
+        g.checkmask = L.pin3[0][l];
+        g.pinned = L.pin3[1][l];
+        g.pinrays = L.pin3[2][l];
+    }
+    g.enemy_att = L.enemy[1][l] | L.enemy[2][l];
+    MoveSet ms;
+    moveset_clear(ms);
+    int part = 0;
+    if (RR == 0) {  // castles (counted here), pawns: the fast ones' targets parked as well
+        gen_castles(P, g);
+        if (gen2 && !big) {
+            part = gen_pawns(P, g, ms, scr) + popc(g.castles);
+            for (u64 fp = ms.fastp; fp; fp &= fp - 1) {
+                const int sq = ctz(fp);
+                scr.put(ordinal(g.own, sq), fast_pawn_targets(ms, sq, g.white));
+            }
+        }
+        L.cbw[0][0][l] = scr.c0;
+        L.cbw[0][1][l] = scr.c1;
+        L.castles[l] = g.castles;
+        L.part[0][l] = (u32)part;
+    } else if (RR == 1) {  // knights, kings (while the probe lands), the reply's 3-fold commit
+        if (gen2 && !big) part = gen_knights(P, g, ms, scr) + gen_kings(P, g, ms, scr);
+        L.cbw[1][0][l] = scr.c0;
+        L.cbw[1][1][l] = scr.c1;
+        L.part[1][l] = (u32)part;
+        int c = 0;
+        u32 hl = hl_of(s1.meta);
+        if (cont && !both2) {
+            pin(pr.e0.hdr); pin(pr.e0.k); pin(pr.e0.q); pin(pr.e0.r);
+            pin(pr.e0.b); pin(pr.e0.n); pin(pr.e0.p); pin(pr.e0.w);
+            c = rep_commit(h, s1, pr, hl, L.irrev2[l] != 0);  // table write deferred to h.commit()
+        }
+        L.rep2[l] = (u32)c | (hl << 8);
+    } else if (RR == 2) {  // queens
+        if (gen2 && !big) part = gen_sliders<QUEEN>(P, g, ms, scr);
+        L.cbw[2][0][l] = scr.c0;
+        L.cbw[2][1][l] = scr.c1;
+        L.part[2][l] = (u32)part;
+    } else {  // rooks, bishops; a big board's whole count
+        if (gen2 && !big) {
+            part = gen_sliders<ROOK>(P, g, ms, scr) + gen_sliders<BISHOP>(P, g, ms, scr);
+        } else if (gen2) {
+            gen_castles(P, g);
+            part = count_legal(P, g);
+        }
+        L.cbw[3][0][l] = scr.c0;
+        L.cbw[3][1][l] = scr.c1;
+        L.part[3][l] = (u32)part;
+    }
+    pair_barrier();
+
+    // ---- phase 6: the reply's outcome (k_env_step_api2_vs half B), the mask rows, the outputs
+    if (RR == 0) __builtin_amdgcn_s_setprio(0);
+    if (RR == 2) __builtin_amdgcn_s_setprio(2);
+    const int total = gen2 ? (int)(L.part[0][l] + L.part[1][l] + L.part[2][l] + L.part[3][l]) : 0;
+    Pos fs = s1;         // the state after the step
+    bool alone = false;  // the state stays (the reply left both kings checked): its moves were not made
+    if (cont) {
+        if (both2) {  // the engine raises, the env ends
+            o.reason = R_BOTH_CHECKED;
+            o.done = 1;
+            alone = true;
+        } else {
+            const u32 rpk = L.rep2[l];
+            const int c = (int)(rpk & 0xFFu);
+            const u32 hl = rpk >> 8;
+            const bool ow = (s1.meta & M_WHITE) != 0;  // the opponent's colour
+            const u32 chk = ow ? ((mchk2 ? M_WCHK : 0u) | (chk2 ? M_BCHK : 0u))
+                               : ((chk2 ? M_WCHK : 0u) | (mchk2 ? M_BCHK : 0u));
+            fs = P;
+            fs.meta = with_hl((P.meta & ~(u32)(M_WCHK | M_BCHK | M_DONE)) | chk | ((c >= 3 || c == 0) ? M_DONE : 0u), hl);
+            o.reward -= (int)L.mr2[l];  // 283
+            if (c >= 3) { o.done = 1; o.reason = R_REPETITION; }
+            if (c == 0) { o.done = 1; o.reason = R_WINDOW_FULL; }
+            if (total == 0 && chk2) {  // 285-288
+                fs.meta |= M_DONE;
+                o.done = 1;
+                o.reward -= 100;
+                o.reason = R_MATED;
+            }
+            if (fs.meta & M_WHITE) fs.meta += (1u << M_MC_SHIFT);  // 291-292
+        }
+    }
+    const bool reset = live && autoreset && o.done;  // chess_v2.py:183-206
+    if (reset) fs = icd->pos;
+    // boards outside the fast path (per-piece fallback): the state kept after a void reply, or
+    // more own pieces than slots
+    const bool slow = live && !reset && (alone || big);
+    u64* const mrow = out.mask ? out.mask + ii : nullptr;
+    if (mrow && live) {
+        if (reset) {
+            const u64 iown = icd->own;
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                const int sq = 16 * RR + k;
+                const u64 w = ((iown >> sq) & 1) ? icd->slots[popc(iown & below(sq))] : 0ull;
+                apiq_store(mrow + sq * N, w);
+            }
+        } else if (slow) {
+            apiq_slow_rows<RR>(fs, mrow, N);
+        } else {  // every own piece's targets are parked (pawns too): one LDS read per row
+            int j = popc(g.own & below(16 * RR));
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                const int sq = 16 * RR + k;
+                const bool own = (g.own >> sq) & 1;
+                const u64 w = scr.get(j & (SCRATCH_SLOTS - 1));
+                apiq_store(mrow + sq * N, own ? w : 0ull);
+                j += own ? 1 : 0;
+            }
+        }
+        if (RR == 0) {
+            const u32 cs = reset ? icd->castles : slow ? apiq_slow_castles(fs) : L.castles[l];
+            const bool cwh = reset ? icd->white != 0 : slow ? (fs.meta & M_WHITE) != 0 : g.white;
+            u64 cwd = 0;
+            if (cs & 1) cwd |= cwh ? (1ull << 1) : (1ull << 3);  // QS: 4097 / 4099
+            if (cs & 2) cwd |= cwh ? (1ull << 0) : (1ull << 2);  // KS: 4096 / 4098
+            mrow[64 * N] = cwd;
+        }
+    }
+    if (live && RR == 2) {  // the agent's pick (the next draw, action-id order), the count, the env's next action
+        const u32 nd = cont ? 1u : 0u;  // draws taken by the reply
+        const u32 xp = cont ? L.x1[l] : L.x0[l];
+        int tot = total;
+        uint16_t p = (uint16_t)A_NONE;
+        if (reset) {
+            tot = (int)C.rtotal;
+            p = (uint16_t)L.ra[nd][l];  // (the quads run only with the start position's table)
+        } else if (slow) {
+            const u32 r = apiq_slow_pick(fs, xp);
+            tot = (int)(r >> 16);
+            p = (uint16_t)(r & 0xFFFFu);
+        } else if (tot > 0) {  // castles last (KS 4096 / 4098 before QS 4097 / 4099)
+            const u32 cs = L.castles[l];
+            const int normal = tot - popc(cs);
+            int k = (int)scale_rank(xp, (u32)tot);
+            if (k < normal) {
+                p = (uint16_t)ord_pick(scr, g.own, L.cbw[0][0][l] | L.cbw[1][0][l] | L.cbw[2][0][l] | L.cbw[3][0][l],
+                                       L.cbw[0][1][l] | L.cbw[1][1][l] | L.cbw[2][1][l] | L.cbw[3][1][l], normal, k);
+            } else {
+                k -= normal;
+                p = (cs & 2) && k == 0 ? (uint16_t)(g.white ? A_KSW : A_KSB) : (uint16_t)(g.white ? A_QSW : A_QSB);
+            }
+        }
+        if (out.cnt) out.cnt[i] = tot;
+        const PairIO io = store_io(slab, nn);
+        u32 dn = d + nd;
+        if (out.pick) {
+            dn += tot > 0 ? 1u : 0u;
+            out.pick[i] = p;
+            io.act[i] = p;
+        }
+        io.draw[i] = dn;
+    } else if (live && RR == 3) {
+        if (out.obs) write_obs(fs, out.obs + 64 * (size_t)i);
+    } else if (live && RR == 1) {
+        if (reset) h.bump_gen();
+        out.rw[i] = o.reward;
+        out.dn[i] = (uint8_t)o.done;
+        out.rs[i] = (uint8_t)o.reason;
+        h.commit();
+        const PairIO io = store_io(slab, nn);
+        io.store(i, fs);
+        h.flush(g0);
+        io.nsteps[i] = nst + 1;
+        io.reward[i] = o.reward;
+        io.done[i] = (uint8_t)o.done;
+        io.reason[i] = (uint8_t)o.reason;
+    }
+}
+
+// 16 argument dwords, as k_env_step_api2_vs (all preloaded)
+__global__ void __launch_bounds__(4 * QUAD_BOARDS * QUADS_WG) __attribute__((amdgpu_waves_per_eu(4)))
+    k_env_step_api4_vs(uint8_t* __restrict__ slab, uint64_t seed, u64* __restrict__ htab,
+                       const uint16_t* __restrict__ racts, const EnvDev::InitCache* __restrict__ icd,
+                       const uint16_t* __restrict__ acts, const ApiOut* __restrict__ outp, int nn,
+                       u32 rinfo /* autoreset << 17 | ic.table << 16 | ic.total */) {
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int qw = wv >> 2;
+    const int role = (wv & 3) ^ ((qw & 1) ? GC_QXOR : 0);  // as k_env_rollout4: every SIMD a stateful + a stateless role
+    const int l = threadIdx.x & (QUAD_BOARDS - 1);
+    const int i = (blockIdx.x * QUADS_WG + qw) * QUAD_BOARDS + l;
+    ApiOut out = *outp;
+    asm volatile("" : "+s"(out.rw), "+s"(out.dn), "+s"(out.rs), "+s"(out.mask), "+s"(out.obs), "+s"(out.cnt),
+                 "+s"(out.pick), "+s"(out.ms));
+    switch (role) {
+        case 0: apiqv_run<0>(slab, seed, htab, racts, icd, acts, out, nn, rinfo, qw, l, i); break;
+        case 1: apiqv_run<1>(slab, seed, htab, racts, icd, acts, out, nn, rinfo, qw, l, i); break;
+        case 2: apiqv_run<2>(slab, seed, htab, racts, icd, acts, out, nn, rinfo, qw, l, i); break;
+        default: apiqv_run<3>(slab, seed, htab, racts, icd, acts, out, nn, rinfo, qw, l, i); break;
     }
 }
 
@@ -6047,7 +6554,12 @@ extern "C" int gc_env_step_device(gc_env* e, const uint16_t* d_actions, int32_t*
             HIPCHK(hipStreamSynchronize(e->stream));
         }
         const dim3 grid((nb + PAIRS_WG - 1) / PAIRS_WG), block(2 * PAIR_BOARDS * PAIRS_WG);
-        if (d.agent_black)
+        const char* nq = getenv("GC_NO_QUAD_API");  // A/B and tests (read per call): api2_vs
+        const bool no_quad_vs = nq && atoi(nq) != 0;
+        if (!d.agent_black && !no_quad_vs)  // a WHITE agent: four waves per 64 boards (k_env_step_api4_vs)
+            k_env_step_api4_vs<<<(nb + QUADS_WG - 1) / QUADS_WG, 4 * QUAD_BOARDS * QUADS_WG, 0, e->stream>>>(
+                e->slab, d.seed, d.htab, r.racts, r.icd, d_actions, e->api_out, d.n, r.rinfo | ((u32)ar << 17));
+        else if (d.agent_black)
             k_env_step_api2_vs<true><<<grid, block, 0, e->stream>>>(e->slab, d.seed, d.htab, r.racts, r.icd, d_actions,
                                                                      e->api_out, d.n, r.rinfo | ((u32)ar << 17));
         else

@@ -95,19 +95,22 @@ def test_obs_of_weird_boards(oracle):
     assert (o["reason"] == 6).all() and (o["obs"] == boards).all()
 
 
-@pytest.mark.parametrize("autoreset", [False, True])
-def test_step_device_weird_boards_equal_host_step(oracle, autoreset):
+@pytest.mark.parametrize("opponent,autoreset", [("none", False), ("none", True), ("random", False)])
+def test_step_device_weird_boards_equal_host_step(oracle, autoreset, opponent):
     """Fuzz positions (several / no kings, pawns on back ranks, > 16 pieces, rights without
-    rooks): the device-buffer step (the paired kernel: quick_legal validation, regen of kept
-    states, the lone regeneration of a both-checked board) == the host step ply by ply, with
-    the mask / obs / count of every board; with auto-reset, the reset boards' too."""
+    rooks): the device-buffer step (the quad kernels: quick_legal validation, regen of kept
+    states, the per-piece fallback of a both-checked or > 16-piece board; with the random
+    opponent its reply too) == the host step ply by ply, with the mask / obs / count of every
+    board; with auto-reset, the reset boards' too (the host reset takes a policy draw that the
+    device's does not, so the random opponent's auto-reset form is checked against the paired
+    kernel below and against the oracle in test_step_device_random_opponent_vs_oracle)."""
     from conftest import random_positions
     from gym_chess_amd.env import BatchedChessEnv
 
     n = 1000
     boards, metas = random_positions(n, 4242)
-    a = BatchedChessEnv(n, device=0, seed=5)
-    b = BatchedChessEnv(n, device=0, seed=5)
+    a = BatchedChessEnv(n, device=0, seed=5, opponent=opponent)
+    b = BatchedChessEnv(n, device=0, seed=5, opponent=opponent)
     assert a.paired()
     a.set_states(boards, metas)
     b.set_states(boards, metas)
@@ -224,3 +227,50 @@ def test_step_device_mask_stride(kind):
             for k in outs[0]:
                 assert (o[k] == outs[0][k]).all(), (ply, k)
         assert outs[0]["mask"].shape == (n, 65)
+
+
+@pytest.mark.parametrize("start", ["weird", "settled"])
+def test_quad_opponent_api_equals_paired(start):
+    """The random opponent's quad API step (k_env_step_api4_vs, a WHITE agent) == the paired one
+    (k_env_step_api2_vs, GC_NO_QUAD_API=1) ply by ply with auto-reset: outputs, picks, mask, obs,
+    count and states -- on fuzz positions (> 16 pieces, both kings checked, no kings) and on
+    boards settled by 300 plies of play."""
+    import os
+
+    from conftest import random_positions
+    from gym_chess_amd.env import BatchedChessEnv
+
+    n = 1000 if start == "weird" else 4096
+    envs = [BatchedChessEnv(n, device=0, seed=77, opponent="random") for _ in range(2)]
+    if start == "weird":
+        boards, metas = random_positions(n, 5151)
+        for e in envs:
+            e.set_states(boards, metas)
+    else:
+        for e in envs:
+            e.rollout(300)
+    ios = [e.device_io() for e in envs]
+    acts = envs[0].device_io(mask=False, obs=False, count=False, pick=True, select=False)
+    rng = np.random.RandomState(4)
+    reasons = set()
+    for ply in range(40):
+        lists = envs[0].possible_actions()
+        a = np.array([l[rng.randint(len(l))] if l and rng.rand() > 0.1 else rng.randint(4101) for l in lists],
+                     dtype=np.uint16)
+        acts.upload_actions(a)
+        outs = []
+        for k, (e, io) in enumerate(zip(envs, ios)):
+            if k:
+                os.environ["GC_NO_QUAD_API"] = "1"
+            try:
+                e.step_device(io, actions=acts.ptr["pick"], autoreset=True)
+                outs.append(io.fetch())
+            finally:
+                os.environ.pop("GC_NO_QUAD_API", None)
+        for key in outs[0]:
+            assert (outs[0][key] == outs[1][key]).all(), (ply, key, np.nonzero(outs[0][key] != outs[1][key])[0][:4])
+        b0, m0 = envs[0].boards()
+        b1, m1 = envs[1].boards()
+        assert (b0 == b1).all() and (m0 == m1).all(), ply
+        reasons |= set(int(x) for x in outs[0]["reason"])
+    assert {0, 6}.issubset(reasons), reasons
