@@ -330,7 +330,7 @@ def api_step_leg(args, rep, n, **env_kw):
     buffers: per step an external action per board in (here: the previous step's random-policy
     pick, so no host round trip), reward / done / reason, the int8 observation, the legal-action
     mask and count out, auto-reset of finished boards.  One launch of k_env_step_api4 (the quad
-    API step; the random opponent's: k_env_step_api2_vs, paired) per step."""
+    API step; the random opponent's: k_env_step_api4_vs) per step."""
     from gym_chess_amd.env import BatchedChessEnv
 
     def setup(rp):
@@ -362,10 +362,11 @@ def api_step_leg(args, rep, n, **env_kw):
         env.close()
     avg = kms / 1e3 / args.api_steps
     ach = n * ALG_BYTES_API / avg / 1e9
-    # the quad API step (k_env_step_api4) serves opponent "none" (GC_NO_QUAD_API=1: the paired one);
-    # the random opponent's runs on the paired driver
-    kern = "k_env_step_api2_vs" if env_kw else (
-        "k_env_step_api2" if os.environ.get("GC_NO_QUAD_API", "0") not in ("", "0") else "k_env_step_api4")
+    # the quad API steps (k_env_step_api4; the random opponent's with a WHITE agent:
+    # k_env_step_api4_vs) -- GC_NO_QUAD_API=1: the paired ones
+    paired = os.environ.get("GC_NO_QUAD_API", "0") not in ("", "0")
+    kern = ("k_env_step_api2_vs" if paired else "k_env_step_api4_vs") if env_kw else (
+        "k_env_step_api2" if paired else "k_env_step_api4")
     out = {"value": rep.world_size * n * args.api_steps / dt, "unit": "env_steps/s", "steps": args.api_steps,
            "roofline": {"bound": "hbm", "kernel": kern, "achieved": ach,
                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "avg_launch_us": avg * 1e6,
@@ -658,7 +659,7 @@ def main():
         e.close()
     if args.api_steps > 0:
         extra["api_step"] = api_step_leg(args, rep, n)
-        # the random opponent answering inside each step (chess_v2.py:275-288), paired driver
+        # the random opponent answering inside each step (chess_v2.py:275-288)
         extra["api_step"]["opponent_random"] = api_step_leg(args, rep, n, opponent="random")
     if args.single_episodes > 0:
         extra["single_env"] = single_env_leg(args, rep)

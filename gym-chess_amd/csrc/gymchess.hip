@@ -3239,6 +3239,20 @@ __device__ void write_obs(const Pos& s, int8_t* __restrict__ out) {
         o[r] = (u64)obs_word(b0, b1, b2, blk, 8 * r) | ((u64)obs_word(b0, b1, b2, blk, 8 * r + 4) << 32);
 }
 
+#ifdef GC_OBS_DIAG  // diagnostic (not parity): the observation words stored word-major (coalesced), to time the scattered stores
+__device__ void write_obs_diag(const Pos& s, int8_t* __restrict__ out, int i, int nn) {
+    u64* o = reinterpret_cast<u64*>(out);
+    const u64 b0 = s.k | s.r | s.n, b1 = s.q | s.r | s.p, b2 = s.b | s.n | s.p;
+    const u64 blk = occ_of(s) & ~s.w;
+#pragma unroll
+    for (int r = 0; r < 8; r++)
+        o[(size_t)r * nn + i] = (u64)obs_word(b0, b1, b2, blk, 8 * r) | ((u64)obs_word(b0, b1, b2, blk, 8 * r + 4) << 32);
+}
+#define WRITE_OBS_Q3(fs, base, i, nn) write_obs_diag(fs, base, i, nn)
+#else
+#define WRITE_OBS_Q3(fs, base, i, nn) write_obs(fs, (base) + 64 * (size_t)(i))
+#endif
+
 template <bool OPP>
 __global__ void __launch_bounds__(BLOCK) k_env_step_api(EnvDev e, const uint16_t* __restrict__ acts,
                                                         int32_t* __restrict__ rw, uint8_t* __restrict__ dn,
@@ -3911,7 +3925,7 @@ __device__ __forceinline__ void apiq_run(uint8_t* __restrict__ slab, uint64_t se
             io.draw[i] = d;
         }
     } else if (live && RR == 3) {
-        if (out.obs) write_obs(fs, out.obs + 64 * (size_t)i);
+        if (out.obs) WRITE_OBS_Q3(fs, out.obs, i, nn);
     } else if (live && RR == 1) {
         if (reset) h.bump_gen();
         out.rw[i] = o.reward;
@@ -4030,6 +4044,13 @@ __device__ __forceinline__ void apiqv_run(uint8_t* __restrict__ slab, uint64_t s
                                           const uint16_t* __restrict__ acts, const ApiOut& out, int nn, u32 rinfo,
                                           int qw, int l, int i) {
     ApiQuadVsLds& L = g_apiqv_lds[qw];
+#ifdef GC_PSTAMPS  // (tools/api_pstamp_probe.py vs: segments 0-6 = the phases' work, 7 = entry loads + barrier waits)
+    const unsigned long long pst_entry = __builtin_amdgcn_s_memrealtime();
+    if (l == 0) {
+        for (int k = 0; k < 8; k++) gc_pst[threadIdx.x >> 6][k] = 0;
+        gc_pst[threadIdx.x >> 6][8] = __builtin_amdgcn_s_memtime();
+    }
+#endif
     const int autoreset = (rinfo >> 17) & 1;
     rinfo &= 0x1FFFFu;
     const bool live = i < nn;
@@ -4042,6 +4063,10 @@ __device__ __forceinline__ void apiqv_run(uint8_t* __restrict__ slab, uint64_t s
     if (RR == 1) { g0 = in_io.hgen[ii]; nst = in_io.nsteps[ii]; }
     if (RR == 1 || RR == 2) d = in_io.draw[ii];
     pin(s); pin(ua); pin(g0); pin(nst); pin(d);
+    PST(7);
+#ifdef GC_PSTAMPS
+    const unsigned long long pst_rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
     const int a = (int)ua;
     DevHist h = DevHist{htab, in_io.hgen, g0, ii, HTAB_BITS};
     OrdScratch scr{&L.slots[0][l], 0ull, 0ull};
@@ -4079,7 +4104,9 @@ __device__ __forceinline__ void apiqv_run(uint8_t* __restrict__ slab, uint64_t s
     } else {
         L.valid[0][l] = quick_pseudo(s, a) ? 1u : 0u;
     }
+    PST(0);
     pair_barrier();
+    PST(7);
 
     // ---- phase 1: the opponent's position
     if (RR == 2) __builtin_amdgcn_s_setprio(0);
@@ -4107,7 +4134,9 @@ __device__ __forceinline__ void apiqv_run(uint8_t* __restrict__ slab, uint64_t s
     } else {
         L.enemy[2][l] = g.ks >= 0 ? side_attacks_diag(ns, !g.white) : 0ull;
     }
+    PST(1);
     pair_barrier();
+    PST(7);
 
     // ---- phase 2: the opponent's move sets (as the rollout's quads); Q1 the agent ply's commit
     const bool opp_chk = L.f0[l] != 0, my_chk = L.f1[l] != 0;
@@ -4165,7 +4194,9 @@ __device__ __forceinline__ void apiqv_run(uint8_t* __restrict__ slab, uint64_t s
 #pragma unroll
         for (int k = 0; k < 4; k++) L.sc.cwx[1][k][l] = Q.cw[k];
     }
+    PST(2);
     pair_barrier();
+    PST(7);
 
     // ---- phase 3: the agent ply's outcome (k_env_step_api2_vs half A); Q2 picks and plays the reply
     if (RR == 0) __builtin_amdgcn_s_setprio(0);
@@ -4240,7 +4271,9 @@ __device__ __forceinline__ void apiqv_run(uint8_t* __restrict__ slab, uint64_t s
         h.commit();  // the agent ply's window write lands before the reply probes the table
         if (cont) rep_prefetch(h, s1, pr);
     }
+    PST(3);
     pair_barrier();
+    PST(7);
 
     // ---- phase 4: the mask's position (the agent to move after a reply)
     if (RR == 0) __builtin_amdgcn_s_setprio(2);
@@ -4263,7 +4296,9 @@ __device__ __forceinline__ void apiqv_run(uint8_t* __restrict__ slab, uint64_t s
     } else {
         L.enemy[2][l] = g.ks >= 0 ? side_attacks_diag(P, !g.white) : 0ull;
     }
+    PST(4);
     pair_barrier();
+    PST(7);
 
     // ---- phase 5: the mask position's moves, parked by ordinal; Q1 the reply's commit
     const bool chk2 = L.f0[l] != 0, mchk2 = L.f1[l] != 0;  // the agent in check; the opponent, after its reply
@@ -4322,7 +4357,9 @@ __device__ __forceinline__ void apiqv_run(uint8_t* __restrict__ slab, uint64_t s
         L.cbw[3][1][l] = scr.c1;
         L.part[3][l] = (u32)part;
     }
+    PST(5);
     pair_barrier();
+    PST(7);
 
     // ---- phase 6: the reply's outcome (k_env_step_api2_vs half B), the mask rows, the outputs
     if (RR == 0) __builtin_amdgcn_s_setprio(0);
@@ -4427,7 +4464,7 @@ __device__ __forceinline__ void apiqv_run(uint8_t* __restrict__ slab, uint64_t s
         }
         io.draw[i] = dn;
     } else if (live && RR == 3) {
-        if (out.obs) write_obs(fs, out.obs + 64 * (size_t)i);
+        if (out.obs) WRITE_OBS_Q3(fs, out.obs, i, nn);
     } else if (live && RR == 1) {
         if (reset) h.bump_gen();
         out.rw[i] = o.reward;
@@ -4442,6 +4479,17 @@ __device__ __forceinline__ void apiqv_run(uint8_t* __restrict__ slab, uint64_t s
         io.done[i] = (uint8_t)o.done;
         io.reason[i] = (uint8_t)o.reason;
     }
+#ifdef GC_PSTAMPS
+    PST(6);
+    if (g_pst_out != nullptr && l == 0) {
+        const size_t w = (size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+        for (int k = 0; k < 8; k++) g_pst_out[w * 12 + k] = gc_pst[threadIdx.x >> 6][k];
+        g_pst_out[w * 12 + 8] = pst_entry;
+        g_pst_out[w * 12 + 9] = pst_rt0;
+        g_pst_out[w * 12 + 10] = pst_rt0;
+        g_pst_out[w * 12 + 11] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
 }
 
 // 16 argument dwords, as k_env_step_api2_vs (all preloaded)

@@ -1,9 +1,10 @@
-"""Diagnostic only: where one quad API step (k_env_step_api4) spends its time, per role -- the
+"""Diagnostic only: where one quad API step (k_env_step_api4; with "vs": k_env_step_api4_vs, its
+seven phases' work and the entry + waits together) spends its time, per role -- the
 cycles of each segment (entry loads, phase 0, wait A, phase 1, wait B, phase 2, wait C,
 phase 3 with its stores; s_memtime) and the launch anatomy (wave start / end on the 100 MHz
 clock).  Build: tools/build_variants.sh pst "-DGC_PSTAMPS" -> tools/_lib_pst.so.
 
-    python tools/api_pstamp_probe.py [boards] [steps before the stamped one]
+    python tools/api_pstamp_probe.py [boards] [steps before the stamped one] [vs]
 """
 import ctypes
 import os
@@ -21,7 +22,8 @@ from gym_chess_amd.env import BatchedChessEnv  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 warm = int(sys.argv[2]) if len(sys.argv) > 2 else 100
-env = BatchedChessEnv(n, device=0, seed=0x5EED + 14)
+vs = len(sys.argv) > 3 and sys.argv[3] == "vs"  # the random opponent's quad step (k_env_step_api4_vs)
+env = BatchedChessEnv(n, device=0, seed=0x5EED + 14, **({"opponent": "random"} if vs else {}))
 env.rollout(1000)
 io = env.device_io()
 for _ in range(warm):
@@ -49,6 +51,8 @@ for k in range(5):
 w = np.arange(len(raw)) % 8
 role = (w & 3) ^ (((w >> 2) & 1) << 1)
 names = ["phase 0", "wait A", "phase 1", "wait B", "phase 2", "wait C", "phase 3", "entry"]
+if vs:  # k_env_step_api4_vs: seven phases' work, the entry loads and every barrier wait together
+    names = [f"phase {k}" for k in range(7)] + ["entry+waits"]
 for r in range(4):
     s = st[role == r]
     tot = s.sum(axis=1).mean()
