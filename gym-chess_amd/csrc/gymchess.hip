@@ -838,14 +838,19 @@ __global__ void k_followers2(int n, const uint8_t* __restrict__ lflag, const u32
 }
 
 // The followers credited by their leader's lane in the leaf (GC_PERFT_FUSE, the default): no
-// follower pass, no kept counts.  k_dedup_runs_f writes, per record, a lead word (bit 31: it leads,
-// low bits: its sorted position) and, in sorted order, each member's leader position and parent;
-// the leaf lane of the leader at sorted position pL walks its run (keys2[pL] onwards) and adds its
-// count into the parent of every member whose leader is pL.
+// follower pass, no kept counts.  k_dedup_runs_f writes, per record, a lead word (bit 31: it leads;
+// bits 27-30: how many later members its run holds, GC_RUN_CAP = that many or more; bits 0-26: its sorted
+// position) and, in sorted order, each member's (leader position, parent) pair; the leaf lane of
+// the leader at sorted position pL walks the later members of its run -- none for a lone position,
+// which then reads nothing more -- and adds its count into the parent of every member it leads.
+#define RUN_LEN_SHIFT 27
+#ifndef GC_RUN_CAP
+#define GC_RUN_CAP 15  // the lead word's run length saturates here (a test build lowers it: the tag walk then runs)
+#endif
+static_assert(GC_RUN_CAP >= 1 && GC_RUN_CAP <= 15, "GC_RUN_CAP: 4 bits");
 __global__ void __launch_bounds__(BLOCK) k_dedup_runs_f(const Node64* __restrict__ in, int n,
                                                         const u32* __restrict__ keys, const u32* __restrict__ vals,
-                                                        u32* __restrict__ leadw, u32* __restrict__ fld_s,
-                                                        u32* __restrict__ fpar_s) {
+                                                        u32* __restrict__ leadw, uint2* __restrict__ fw) {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= n) return;
     const u32 k = keys[p];
@@ -863,9 +868,14 @@ __global__ void __launch_bounds__(BLOCK) k_dedup_runs_f(const Node64* __restrict
                 if (pos_equal(node_load(in, vals[t]), s)) { lp = (u32)t; break; }
         }
     }
-    leadw[r] = lp == (u32)p ? (0x80000000u | (u32)p) : 0u;
-    fld_s[p] = lp;
-    fpar_s[p] = parent;
+    u32 w = 0u;
+    if (lp == (u32)p) {  // a leader: the later members of its run (the walk's length in the leaf)
+        int q = p + 1;
+        while (q < n && q - p <= GC_RUN_CAP && keys[q] == k) q++;
+        w = 0x80000000u | ((u32)(q - p - 1) << RUN_LEN_SHIFT) | (u32)p;
+    }
+    leadw[r] = w;
+    fw[p] = make_uint2(lp, parent);
 }
 __global__ void __launch_bounds__(DEDUP_BLOCK) k_leader_hist_f(int n, const u32* __restrict__ leadw,
                                                                const uint8_t* __restrict__ bins, u32* __restrict__ hist,
@@ -908,7 +918,7 @@ template <bool FUSE>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(PERFT2_WPE)))
 k_perft2_val(const Node64* __restrict__ in, int n, uint64_t* __restrict__ val,
              unsigned long long* __restrict__ parent_sum, int nrec, const u32* __restrict__ keys,
-             const u32* __restrict__ fld_s, const u32* __restrict__ fpar_s, const u32* __restrict__ spos) {
+             const uint2* __restrict__ fw, const u32* __restrict__ spos) {
     __shared__ u64 lds_a[SCRATCH_SLOTS * BLOCK];
     LdsScratch sa{lds_a + threadIdx.x};
 #ifndef GC_PERFT_LDS
@@ -931,10 +941,20 @@ k_perft2_val(const Node64* __restrict__ in, int n, uint64_t* __restrict__ val,
     if (!FUSE) {
         val[i] = c;
     } else {
-        const u32 pl = spos[i];
-        const u32 k = keys[pl];
-        for (int j = (int)pl + 1; j < nrec && keys[j] == k; j++)
-            if (fld_s[j] == pl) atomicAdd(parent_sum + fpar_s[j], (unsigned long long)c);
+        const u32 w = spos[i];
+        const u32 pl = w & ((1u << RUN_LEN_SHIFT) - 1u);
+        const int rl = (int)(w >> RUN_LEN_SHIFT);  // later members of the run (GC_RUN_CAP: that many or more)
+        for (int j = (int)pl + 1; j <= (int)pl + rl; j++) {  // (nothing read for a lone position)
+            const uint2 f = fw[j];
+            if (f.x == pl) atomicAdd(parent_sum + f.y, (unsigned long long)c);
+        }
+        if (rl == GC_RUN_CAP) {  // a longer run: the rest by its tag
+            const u32 k = keys[pl];
+            for (int j = (int)pl + GC_RUN_CAP + 1; j < nrec && keys[j] == k; j++) {
+                const uint2 f = fw[j];
+                if (f.x == pl) atomicAdd(parent_sum + f.y, (unsigned long long)c);
+            }
+        }
     }
 }
 __global__ void k_followers(const uint2* __restrict__ fol, const u32* __restrict__ nfol,
@@ -5460,18 +5480,19 @@ static int perft_split_leaves(hipStream_t st, SoA leaf, uint64_t* leaf_out) {
             // keys / values of the sort in the table's memory (16 B per record), parents and
             // leaders in the follower pairs' (8 B)
             u32* const keys = reinterpret_cast<u32*>(table);
-            u32* const keys2 = keys + cap;
-            u32* const vals = keys + 2 * cap;
+            u32* const vals = keys + cap;
+            u32* const keys2 = keys + 2 * cap;
             u32* const vals2 = keys + 3 * cap;
+            uint2* const fw = reinterpret_cast<uint2*>(table);  // FUSE, after the sort: over keys | vals
             u32* const parent_of = reinterpret_cast<u32*>(fol);
             u32* const lead = parent_of + cap;
             u32* const leadw = parent_of;                              // FUSE: per record
             u32* const spos = reinterpret_cast<u32*>(place_of);        // FUSE: per placed leader
-            if (fuse) {  // after the sort, the unsorted keys / values hold the members' leaders / parents
+            if (fuse) {  // after the sort, the unsorted keys / values hold the members' (leader, parent) pairs
                 k_dedup_keys<<<grid_for(n), BLOCK, 0, st>>>(cre, n, keys, vals, bins, nullptr);
                 tb = tmp_bytes;
                 he = hipcub::DeviceRadixSort::SortPairs(tmp, tb, keys, keys2, vals, vals2, n, 0, 32, st);
-                if (he == hipSuccess) k_dedup_runs_f<<<grid_for(n), BLOCK, 0, st>>>(cre, n, keys2, vals2, leadw, keys, vals);
+                if (he == hipSuccess) k_dedup_runs_f<<<grid_for(n), BLOCK, 0, st>>>(cre, n, keys2, vals2, leadw, fw);
                 if (he == hipSuccess) k_leader_hist_f<<<nbd, DEDUP_BLOCK, 0, st>>>(n, leadw, bins, hist, nbd);
             } else if (sortdedup) {
                 k_dedup_keys<<<grid_for(n), BLOCK, 0, st>>>(cre, n, keys, vals, bins, parent_of);
@@ -5503,9 +5524,9 @@ static int perft_split_leaves(hipStream_t st, SoA leaf, uint64_t* leaf_out) {
             if (hipEventCreate(&e1) == hipSuccess) evs.push_back(e1);
             if (e0 && e1) (void)hipEventRecord(e0, st);
             if (fuse)
-                k_perft2_val<true><<<grid_for(lead_n), BLOCK, 0, st>>>(cr, lead_n, val, psum, n, keys2, keys, vals, spos);
+                k_perft2_val<true><<<grid_for(lead_n), BLOCK, 0, st>>>(cr, lead_n, val, psum, n, keys2, fw, spos);
             else
-                k_perft2_val<false><<<grid_for(lead_n), BLOCK, 0, st>>>(cr, lead_n, val, psum, 0, nullptr, nullptr, nullptr, nullptr);
+                k_perft2_val<false><<<grid_for(lead_n), BLOCK, 0, st>>>(cr, lead_n, val, psum, 0, nullptr, nullptr, nullptr);
             if (e0 && e1) (void)hipEventRecord(e1, st);
             if (!fuse && sortdedup) k_followers2<<<2048, BLOCK, 0, st>>>(n, lflag, lead, parent_of, place_of, val, psum);
             else if (!fuse) k_followers<<<2048, BLOCK, 0, st>>>(fol, nfol, place_of, val, psum);
