@@ -179,58 +179,67 @@ def api_soak(a):
             sys.exit(1)
 
 
-def api_opp_soak(a):
+def api_opp_case(seed, color, plies, n, idx):
+    """The random opponent's device API step (auto-reset, actions = the previous picks) against
+    the oracle env on the boards idx: every step's reward / done / reason and pick, the states
+    every 500 plies.  -> (mismatches, board steps checked, spill info, seconds)"""
     import oracle as O
     from gym_chess_amd.env import BatchedChessEnv
 
+    t0 = time.time()
+    env = BatchedChessEnv(n, device=0, seed=seed, opponent="random", player_color=color)
+    io = env.device_io(mask=False, obs=False, count=False)
+    ors = {int(i): O.OracleEnv(opponent=1, agent_white=color == "WHITE", seed=seed, board=int(i)) for i in idx}
+    for o in ors.values():
+        o.pick()
+    prev = io.fetch("pick")["pick"].astype(np.int64)
+    bad, steps = [], 0
+    for p in range(plies):
+        acts = np.where(prev == 0xFFFF, 0, prev).astype(np.uint16)
+        io.upload_actions(acts)
+        env.step_device(io, autoreset=True)
+        out = io.fetch("reward", "done", "reason", "pick")
+        for i, o in ors.items():
+            rc, rw, dn, why = o.step(int(acts[i]))
+            if rc == 1:
+                dn, why = 1, 5
+            if (rw, dn, why) != (int(out["reward"][i]), int(out["done"][i]), int(out["reason"][i])):
+                bad.append(("step", p, i))
+                break
+            if dn:
+                o.reset()
+            legal = sorted(o.moves())
+            want = legal[O.policy_index(seed, i, o.draw, len(legal))] if legal else 0xFFFF
+            if int(out["pick"][i]) != want:
+                bad.append(("pick", p, i))
+                break
+            if legal:
+                o.pick()
+            steps += 1
+        if p % 500 == 499 or p == plies - 1:
+            b, m = env.boards()
+            for i, o in ors.items():
+                ob, om = o.state()
+                if not ((b[i] == ob).all() and list(m[i]) == list(om)):
+                    bad.append(("state", p, i))
+                    break
+        if bad:
+            break
+        prev = out["pick"].astype(np.int64)
+    spill = env.spill_info() if color == "BLACK" else None
+    io.close()
+    env.close()
+    return bad, steps, spill, round(time.time() - t0, 1)
+
+
+def api_opp_soak(a):
     n, color = a.boards, a.api_opp
     idx = np.array(sorted(set(range(0, n, 1021)) | set(range(64)) | set(range(n - 64, n))), dtype=np.int64)
     for seed in (0x0A11 + 97 * k for k in range(a.seeds)):
-        t0 = time.time()
-        env = BatchedChessEnv(n, device=0, seed=seed, opponent="random", player_color=color)
-        io = env.device_io(mask=False, obs=False, count=False)
-        ors = {int(i): O.OracleEnv(opponent=1, agent_white=color == "WHITE", seed=seed, board=int(i)) for i in idx}
-        for o in ors.values():
-            o.pick()
-        prev = io.fetch("pick")["pick"].astype(np.int64)
-        bad, steps = [], 0
-        for p in range(a.plies):
-            acts = np.where(prev == 0xFFFF, 0, prev).astype(np.uint16)
-            io.upload_actions(acts)
-            env.step_device(io, autoreset=True)
-            out = io.fetch("reward", "done", "reason", "pick")
-            for i, o in ors.items():
-                rc, rw, dn, why = o.step(int(acts[i]))
-                if rc == 1:
-                    dn, why = 1, 5
-                if (rw, dn, why) != (int(out["reward"][i]), int(out["done"][i]), int(out["reason"][i])):
-                    bad.append(("step", p, i))
-                    break
-                if dn:
-                    o.reset()
-                legal = sorted(o.moves())
-                want = legal[O.policy_index(seed, i, o.draw, len(legal))] if legal else 0xFFFF
-                if int(out["pick"][i]) != want:
-                    bad.append(("pick", p, i))
-                    break
-                if legal:
-                    o.pick()
-                steps += 1
-            if p % 500 == 499 or p == a.plies - 1:
-                b, m = env.boards()
-                for i, o in ors.items():
-                    ob, om = o.state()
-                    if not ((b[i] == ob).all() and list(m[i]) == list(om)):
-                        bad.append(("state", p, i))
-                        break
-            if bad:
-                break
-            prev = out["pick"].astype(np.int64)
-        spill = env.spill_info() if color == "BLACK" else None
-        env.close()
+        bad, steps, spill, secs = api_opp_case(seed, color, a.plies, n, idx)
         print(json.dumps({"api_opp_seed": seed, "color": color, "boards": n, "plies": a.plies,
                           "sampled": len(idx), "board_steps_checked": steps, "mismatches": bad[:8],
-                          "spill": spill, "seconds": round(time.time() - t0, 1)}), flush=True)
+                          "spill": spill, "seconds": secs}), flush=True)
         if bad:
             sys.exit(1)
 
