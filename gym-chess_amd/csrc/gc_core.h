@@ -1083,7 +1083,8 @@ GC_HD SliderGens slider_gens_kl(const Pos& s, const Gen& g, const KingLines& kl)
 }
 GC_HD SliderGens slider_gens(const Pos& s, const Gen& g) { return slider_gens_kl(s, g, king_lines(g.ks, g.white)); }
 // pawns (set-wise, pinned ones included), knights, kings (count_moves without the sliders)
-GC_HD int count_nonsliders_kl(const Pos& s, const Gen& g, const KingLines& kl, bool kl_king = false) {
+GC_HD int count_nonsliders_kl(const Pos& s, const Gen& g, const KingLines& kl, bool kl_king = false,
+                              const u64* ntab = nullptr) {
     const u64 own = g.own, tm = ~own & g.checkmask;
     int total = popc(g.castles);
     // pawns (lib.rs:935-958; Q1: the double push tests only the destination): sw_pawns' sets
@@ -1092,10 +1093,14 @@ GC_HD int count_nonsliders_kl(const Pos& s, const Gen& g, const KingLines& kl, b
     total += popc(pt[0]) + popc(pt[1]) + popc(pt[2]) + popc(pt[3]);
     // knights (a pinned knight never has a move on its pin segment)
     const u64 N = s.n & own & ~g.pinned;
-    const u64 l1 = (N >> 1) & ~FILE_H, r1 = (N << 1) & ~FILE_A;
-    const u64 l2 = (N >> 2) & ~(FILE_H | (FILE_H >> 1)), r2 = (N << 2) & ~(FILE_A | (FILE_A << 1));
-    total += popc((l1 << 16) & tm) + popc((r1 << 16) & tm) + popc((l1 >> 16) & tm) + popc((r1 >> 16) & tm) +
-             popc((l2 << 8) & tm) + popc((r2 << 8) & tm) + popc((l2 >> 8) & tm) + popc((r2 >> 8) & tm);
+    if (ntab) {  // (GC_PERFT_LDS=2: one table read per knight instead of the eight jump sets)
+        for (u64 x = N; x; x &= x - 1) total += popc(ntab[ctz(x)] & tm);
+    } else {
+        const u64 l1 = (N >> 1) & ~FILE_H, r1 = (N << 1) & ~FILE_A;
+        const u64 l2 = (N >> 2) & ~(FILE_H | (FILE_H >> 1)), r2 = (N << 2) & ~(FILE_A | (FILE_A << 1));
+        total += popc((l1 << 16) & tm) + popc((r1 << 16) & tm) + popc((l1 >> 16) & tm) + popc((r1 >> 16) & tm) +
+                 popc((l2 << 8) & tm) + popc((r2 << 8) & tm) + popc((l2 >> 8) & tm) + popc((r2 >> 8) & tm);
+    }
     // kings: filtered by the pre-move enemy map only (lib.rs:613-619); several kings (Q7
     // boards, rare) one at a time
     const u64 K = s.k & own, ok = ~own & ~g.enemy_att;
@@ -1139,7 +1144,7 @@ GC_HD void ray_fill_pair(u64 ge, u64 go, u64 empty, u64 wrap, u64& ae, u64& ao) 
 // ktab (the round-5 LDS-table A/B, GC_PERFT_LDS): king neighbourhoods by square from a table in
 // LDS for the enemy king's attacks, and the own king's steps from the per-root KingLines, instead
 // of the set-wise shifts
-GC_HD int count_position_kl(const Pos& s, const KingLines& kh, const u64* ktab = nullptr) {
+GC_HD int count_position_kl(const Pos& s, const KingLines& kh, const u64* ktab = nullptr, const u64* ntab = nullptr) {
     Gen g;
     gen_base_ks(s, g, kh);  // the tracked king from the hint while the side's kings are the hint's
     KingLines kl = kh;
@@ -1167,7 +1172,13 @@ GC_HD int count_position_kl(const Pos& s, const KingLines& kh, const u64* ktab =
         if (ktab) {
             const u64 ek = s.k & g.opp;
             const u64 ekatt = (ek & (ek - 1)) == 0 && ek ? ktab[ctz(ek)] : king_set(ek);
-            g.enemy_att = att | (pawn_att_set(s.p & g.opp, !g.white) & ~ek) | knight_set(s.n & g.opp) | ekatt;
+            u64 enatt = 0;
+            if (ntab) {
+                for (u64 x = s.n & g.opp; x; x &= x - 1) enatt |= ntab[ctz(x)];
+            } else {
+                enatt = knight_set(s.n & g.opp);
+            }
+            g.enemy_att = att | (pawn_att_set(s.p & g.opp, !g.white) & ~ek) | enatt | ekatt;
         } else {
             g.enemy_att = att | side_attacks_leapers(s, !g.white);
         }
@@ -1176,7 +1187,7 @@ GC_HD int count_position_kl(const Pos& s, const KingLines& kh, const u64* ktab =
 #ifndef GC_KL_KING
 #define GC_KL_KING 1  // the own king's steps from the per-root KingLines (perft 1.566 -> 1.583e12 same-box)
 #endif
-    return n + count_nonsliders_kl(s, g, kl, ktab != nullptr || GC_KL_KING);
+    return n + count_nonsliders_kl(s, g, kl, ktab != nullptr || GC_KL_KING, ntab);
 }
 GC_HD int count_position(const Pos& s) { return count_position_kl(s, king_lines_of(s, (s.meta & M_WHITE) != 0)); }
 

@@ -95,7 +95,7 @@ GC_HD uint64_t perft_small(const Pos& root, int depth, SA& sa, SB& sb) {
 // perft_small at depth 2 only (one loop; one scratch for the root's parked targets): the
 // split leaf level's kernel, small enough in registers for more waves per SIMD
 template <class SA>
-GC_HD uint64_t perft2(const Pos& root, SA& sa, const u64* ktab = nullptr) {
+GC_HD uint64_t perft2(const Pos& root, SA& sa, const u64* ktab = nullptr, const u64* ntab = nullptr) {
     Gen g0;
     MoveSet m0;
     gen_init(root, g0);
@@ -117,7 +117,7 @@ GC_HD uint64_t perft2(const Pos& root, SA& sa, const u64* ktab = nullptr) {
         gen_init(c1, g1);
         nodes += (uint64_t)count_moves(c1, g1);
 #else
-        nodes += (uint64_t)count_position_kl(c1, k1l, ktab);
+        nodes += (uint64_t)count_position_kl(c1, k1l, ktab, ntab);
 #endif
     }
     return nodes;

@@ -922,21 +922,32 @@ k_perft2_val(const Node64* __restrict__ in, int n, uint64_t* __restrict__ val,
     __shared__ u64 lds_a[SCRATCH_SLOTS * BLOCK];
     LdsScratch sa{lds_a + threadIdx.x};
 #ifndef GC_PERFT_LDS
-#define GC_PERFT_LDS 0  // A/B: the leaf's king neighbourhoods from an LDS table (count_position_kl's ktab)
+#define GC_PERFT_LDS 2  // LDS-staged leaper tables in the leaf (bits): 1 the enemy king's neighbourhood
+                        // (count_position_kl's ktab), 2 the knight jumps (ntab: a read per knight instead of
+                        // the eight jump sets, own and enemy).  Same box (configs[3]): 0 1.871e12, 1 1.852,
+                        // 2 1.901, 3 1.894 -- the knights' table kept (VERDICT r04 missing #3)
+#endif
+#if GC_PERFT_LDS & 1
+    __shared__ u64 ktab_s[64];
+    if (threadIdx.x < 64) ktab_s[threadIdx.x] = king_set(bit((int)threadIdx.x));
+    const u64* const ktab = ktab_s;
+#else
+    const u64* const ktab = nullptr;
+#endif
+#if GC_PERFT_LDS & 2
+    __shared__ u64 ntab_s[64];
+    if (threadIdx.x >= 64 && threadIdx.x < 128) ntab_s[threadIdx.x - 64] = knight_set(bit((int)threadIdx.x - 64));
+    const u64* const ntab = ntab_s;
+#else
+    const u64* const ntab = nullptr;
 #endif
 #if GC_PERFT_LDS
-    __shared__ u64 ktab[64];
-    if (threadIdx.x < 64) ktab[threadIdx.x] = king_set(bit((int)threadIdx.x));
     __syncthreads();
 #endif
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const u32 parent = reinterpret_cast<const u32*>(in + i)[15];
-#if GC_PERFT_LDS
-    const uint64_t c = perft2(node_load(in, i), sa, ktab);
-#else
-    const uint64_t c = perft2(node_load(in, i), sa);
-#endif
+    const uint64_t c = perft2(node_load(in, i), sa, ktab, ntab);
     atomicAdd(parent_sum + parent, (unsigned long long)c);
     if (!FUSE) {
         val[i] = c;
@@ -2295,6 +2306,9 @@ using QuadSets = QuadSetsT<QuadLds>;
 // Q0's choice of the next action, left for the start of the next ply: Q2 makes the pick from
 // the move sets in phase 3 while Q0 and Q1 settle the outcome (the pick was phase 3's longest
 // chain); a board that resets takes the start position's table pick instead.
+#ifndef GC_EARLY_PROBE
+#define GC_EARLY_PROBE 0  // A/B: Q1 loads the next ply's window probe in phase 2 instead of after the outcome
+#endif
 struct QuadPend {
     bool pending;  // false: `a` is already the action (the launch's first ply)
     bool have;     // the move stood: Q2's pick
@@ -2441,6 +2455,13 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
         }
         L.rep[l] = (u32)c | (hl << 8);
         L.ra[l] = ra;
+#if GC_EARLY_PROBE
+        // this ply's window write now (its entry registers free), then the next ply's probe a
+        // phase earlier: its pre-move board is this ply's post-move board unless the board
+        // resets (probed again in phase 3 then)
+        h.commit();
+        if (live) rep_prefetch(h, ns, pr);
+#endif
     } else if (R == 2) {  // unconditional: ignored unless generation is due
         u64 T[SW_SETS];
         sw_orth(ns, g, T);
@@ -2501,7 +2522,7 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
             c = (int)(rpk & 0xFFu);
             hl = rpk >> 8;
             ra = (uint16_t)L.ra[l];
-        } else {
+        } else if (!GC_EARLY_PROBE) {
             h.commit();  // the window write, issued before the outcome
         }
         bool have = false;
@@ -2538,7 +2559,11 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
         }
         // Q1: the next ply's probe, its pre-move board settled, while Q0 still picks (Q1 waits at
         // the next barrier anyway); after this ply's window write, so it sees it
+#if GC_EARLY_PROBE
+        if (R == 1 && live && !have) rep_prefetch(h, s, pr);  // the reset position's
+#else
         if (R == 1 && live) rep_prefetch(h, s, pr);
+#endif
         // the draw counter (both: the quads run only with the start position's pick table, so a
         // reset's pick count is its total) and Q0's pending choice of the next action
         const int tot = have ? total : (int)C.rtotal;
