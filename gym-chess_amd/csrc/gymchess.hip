@@ -2260,6 +2260,21 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
 #define QUADS_WG 2  // two quads per workgroup; the second's roles rotated by 2 so that every SIMD
                     // hosts a state-carrying and a stateless role of each workgroup
 #endif
+#ifndef GC_Q_LEAPER_LDS
+#define GC_Q_LEAPER_LDS 0  // A/B: Q2's enemy knight / king attacks from LDS tables (a read per piece)
+#endif
+#if GC_Q_LEAPER_LDS
+__shared__ u64 g_q_ntab[64], g_q_ktab[64];
+// side_attacks_leapers with the knights' and the kings' neighbourhoods read from the tables
+__device__ __forceinline__ u64 side_attacks_leapers_lds(const Pos& s, bool white) {
+    const u64 occ = occ_of(s);
+    const u64 mine = white ? s.w : (occ & ~s.w);
+    u64 a = pawn_att_set(s.p & mine, white) & ~(s.k & mine);
+    for (u64 x = s.n & mine; x; x &= x - 1) a |= g_q_ntab[ctz(x)];
+    for (u64 x = s.k & mine; x; x &= x - 1) a |= g_q_ktab[ctz(x)];
+    return a;
+}
+#endif
 struct QuadLds {
     u64 sets[SW_SETS][QUAD_BOARDS];  // the next side's move sets (Q0: pawns / knights / kings, Q2, Q3)
     u64 ns[NBB][QUAD_BOARDS];        // Q0 -> all: the post-move board (phase 0)
@@ -2400,6 +2415,8 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
     } else if (R == 2) {
 #if GC_Q1_LEAPERS
         L.enemy[1][l] = g.ks >= 0 ? side_attacks_orth(ns, !g.white) : 0ull;
+#elif GC_Q_LEAPER_LDS
+        L.enemy[1][l] = g.ks >= 0 ? side_attacks_leapers_lds(ns, !g.white) | side_attacks_orth(ns, !g.white) : 0ull;
 #else
         L.enemy[1][l] = g.ks >= 0 ? side_attacks_leapers(ns, !g.white) | side_attacks_orth(ns, !g.white) : 0ull;
 #endif
@@ -2603,6 +2620,12 @@ __device__ __forceinline__ void quad_run(uint8_t* __restrict__ slab, int nn, uin
         pin(s); pin(ua); pin(g0); pin(nst); pin(d);
     }
     if (RR == 0 && l == 0) L.rp = icd->pos;  // read after ply 0's first barrier
+#if GC_Q_LEAPER_LDS
+    if (qw == 0 && RR == 3) {  // (read after ply 0's first barrier too)
+        g_q_ntab[l] = knight_set(bit(l));
+        g_q_ktab[l] = king_set(bit(l));
+    }
+#endif
     int a = (int)ua;
     DevHist h = DevHist{htab, in_io.hgen, g0, ii, HTAB_BITS};
     RepProbe pr;  // Q1: the window probe of the coming ply's pre-move board
