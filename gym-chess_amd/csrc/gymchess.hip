@@ -4138,7 +4138,13 @@ __device__ __forceinline__ void apiqv_run(uint8_t* __restrict__ slab, uint64_t s
     const int a = (int)ua;
     DevHist h = DevHist{htab, in_io.hgen, g0, ii, HTAB_BITS};
     OrdScratch scr{&L.slots[0][l], 0ull, 0ull};
+#ifndef GC_APIQV_Q3P
+#define GC_APIQV_Q3P 0  // A/B: Q3 over Q1 (their SIMDs' pair) in phases 0, 5 and 6, where Q3's chain is the longer
+                        // (same box: 20.9 vs 20.7 us per launch -- off)
+#endif
     if (RR != 3) __builtin_amdgcn_s_setprio(2);
+    if (GC_APIQV_Q3P && RR == 1) __builtin_amdgcn_s_setprio(0);
+    if (GC_APIQV_Q3P && RR == 3) __builtin_amdgcn_s_setprio(2);
     const bool done0 = (s.meta & M_DONE) != 0;   // chess_v2.py:245-251
     const bool cap = mc_of(s.meta) > MOVES_MAX;  // 252-258
     const bool white = (s.meta & M_WHITE) != 0;  // the agent's colour
@@ -4178,6 +4184,8 @@ __device__ __forceinline__ void apiqv_run(uint8_t* __restrict__ slab, uint64_t s
 
     // ---- phase 1: the opponent's position
     if (RR == 2) __builtin_amdgcn_s_setprio(0);
+    if (GC_APIQV_Q3P && RR == 1) __builtin_amdgcn_s_setprio(2);
+    if (GC_APIQV_Q3P && RR == 3) __builtin_amdgcn_s_setprio(0);
     const bool valid = (L.valid[0][l] & L.valid[1][l]) != 0;
     const bool mv = pre && valid;  // the agent's env_ply runs
     Pos ns = s;
@@ -4369,6 +4377,8 @@ __device__ __forceinline__ void apiqv_run(uint8_t* __restrict__ slab, uint64_t s
     PST(7);
 
     // ---- phase 5: the mask position's moves, parked by ordinal; Q1 the reply's commit
+    if (GC_APIQV_Q3P && RR == 1) __builtin_amdgcn_s_setprio(0);
+    if (GC_APIQV_Q3P && RR == 3) __builtin_amdgcn_s_setprio(2);
     const bool chk2 = L.f0[l] != 0, mchk2 = L.f1[l] != 0;  // the agent in check; the opponent, after its reply
     const bool both2 = cont && chk2 && mchk2;
     const bool gen2 = live && !both2;
