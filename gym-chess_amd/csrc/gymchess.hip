@@ -868,13 +868,12 @@ __global__ void __launch_bounds__(BLOCK) k_dedup_runs_f(const Node64* __restrict
                 if (pos_equal(node_load(in, vals[t]), s)) { lp = (u32)t; break; }
         }
     }
-    u32 w = 0u;
-    if (lp == (u32)p) {  // a leader: the later members of its run (the walk's length in the leaf)
+    if (lp == (u32)p) {  // a leader: the later members of its run (the walk's length in the leaf);
+        // a follower's word stays as zeroed before the pass (no scattered write for it)
         int q = p + 1;
         while (q < n && q - p <= GC_RUN_CAP && keys[q] == k) q++;
-        w = 0x80000000u | ((u32)(q - p - 1) << RUN_LEN_SHIFT) | (u32)p;
+        leadw[r] = 0x80000000u | ((u32)(q - p - 1) << RUN_LEN_SHIFT) | (u32)p;
     }
-    leadw[r] = w;
     fw[p] = make_uint2(lp, parent);
 }
 __global__ void __launch_bounds__(DEDUP_BLOCK) k_leader_hist_f(int n, const u32* __restrict__ leadw,
@@ -5550,6 +5549,7 @@ static int perft_split_leaves(hipStream_t st, SoA leaf, uint64_t* leaf_out) {
                 k_dedup_keys<<<grid_for(n), BLOCK, 0, st>>>(cre, n, keys, vals, bins, nullptr);
                 tb = tmp_bytes;
                 he = hipcub::DeviceRadixSort::SortPairs(tmp, tb, keys, keys2, vals, vals2, n, 0, 32, st);
+                if (he == hipSuccess) he = hipMemsetAsync(leadw, 0, (size_t)4 * n, st);
                 if (he == hipSuccess) k_dedup_runs_f<<<grid_for(n), BLOCK, 0, st>>>(cre, n, keys2, vals2, leadw, fw);
                 if (he == hipSuccess) k_leader_hist_f<<<nbd, DEDUP_BLOCK, 0, st>>>(n, leadw, bins, hist, nbd);
             } else if (sortdedup) {
