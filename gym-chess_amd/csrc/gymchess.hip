@@ -4101,11 +4101,12 @@ struct ApiQuadVsLds {
     u32 rep2[QUAD_BOARDS];       // Q1 -> all: the reply's
     u32 x0[QUAD_BOARDS];         // Q1 -> Q2: the Philox words of draws d, d + 1
     u32 x1[QUAD_BOARDS];
-    u32 ra[2][QUAD_BOARDS];      // Q1 -> Q2: the start-position table picks for x0 / x1
+    u32 x2[QUAD_BOARDS];         // (BLACK: d + 2, after a reply and a reset's opening)
+    u32 ra[2][QUAD_BOARDS];      // Q1 -> all: the table picks for x0 / x1 (WHITE: a reset board's pick; BLACK: the opening)
 };
 __shared__ ApiQuadVsLds g_apiqv_lds[QUADS_WG];
 
-template <int RR>
+template <int RR, bool BLACK>
 __device__ __forceinline__ void apiqv_run(uint8_t* __restrict__ slab, uint64_t seed, u64* __restrict__ htab,
                                           const uint16_t* __restrict__ racts, const EnvDev::InitCache* __restrict__ icd,
                                           const uint16_t* __restrict__ acts, const ApiOut& out, int nn, u32 rinfo,
@@ -4135,7 +4136,8 @@ __device__ __forceinline__ void apiqv_run(uint8_t* __restrict__ slab, uint64_t s
     const unsigned long long pst_rt0 = __builtin_amdgcn_s_memrealtime();
 #endif
     const int a = (int)ua;
-    DevHist h = DevHist{htab, in_io.hgen, g0, ii, HTAB_BITS};
+    DevHist h = DevHist{htab, in_io.hgen, g0, ii, BLACK ? HTAB_BITS_UNCAPPED : HTAB_BITS};
+    if (BLACK && RR == 1) h.sp = icd->spill;  // a BLACK agent's windows may spill
     OrdScratch scr{&L.slots[0][l], 0ull, 0ull};
 #ifndef GC_APIQV_Q3P
 #define GC_APIQV_Q3P 0  // A/B: Q3 over Q1 (their SIMDs' pair) in phases 0, 5 and 6, where Q3's chain is the longer
@@ -4166,12 +4168,16 @@ __device__ __forceinline__ void apiqv_run(uint8_t* __restrict__ slab, uint64_t s
     } else if (RR == 1) {
         if (pre) rep_prefetch(h, s, pr);
         const u32 x0 = philox_x0(C.seed, (u32)i, d), x1 = philox_x0(C.seed, (u32)i, d + 1);
+        // WHITE: a reset board's pick in action-id order; BLACK: the opponent's opening after a
+        // reset, in move-set order (chess_v2.py:208-216), for the draw it would take
+        const uint16_t* const tab = BLACK ? C.racts + RESET_ACTS_MAX : C.racts;
         if (C.rtable) {
-            ra0 = C.racts[scale_rank(x0, C.rtotal)];
-            ra1 = C.racts[scale_rank(x1, C.rtotal)];
+            ra0 = tab[scale_rank(x0, C.rtotal)];
+            ra1 = tab[scale_rank(x1, C.rtotal)];
         }
         L.x0[l] = x0;
         L.x1[l] = x1;
+        if (BLACK) L.x2[l] = philox_x0(C.seed, (u32)i, d + 2);
     } else if (RR == 2) {
         L.valid[1][l] = quick_safe(s, a) ? 1u : 0u;
     } else {
@@ -4471,13 +4477,41 @@ __device__ __forceinline__ void apiqv_run(uint8_t* __restrict__ slab, uint64_t s
         }
     }
     const bool reset = live && autoreset && o.done;  // chess_v2.py:183-206
+    u32 nd = cont ? 1u : 0u;                         // draws taken by the reply (and the opening)
     if (reset) fs = icd->pos;
-    // boards outside the fast path (per-piece fallback): the state kept after a void reply, or
-    // more own pieces than slots
-    const bool slow = live && !reset && (alone || big);
+    if (BLACK && reset) {  // the opponent opens as WHITE (208-216), its pick read in phase 0
+        const int op = (int)L.ra[nd][l];
+        Pos p = fs;
+        p.meta = (p.meta & ~(u32)M_RIGHTS) | eff_rights(fs);  // State::new
+        int mro = 0;
+        bool irro = false;
+        apply_legal(p, true, op, &mro, &irro);
+        const bool mchk = mover_checked(fs, p, true, op);
+        Gen gk;
+        gen_base(p, gk);
+        const bool ochk = gk.ks >= 0 && sq_attacked(p, gk.ks, true);  // the agent's king, after the opening
+        u32 hl = hl_of(fs.meta);
+        int c = 1;
+        if (RR == 1) {  // the window: the reply's write, the reset's new generation, the opening's entry
+            h.commit();
+            h.bump_gen();
+            RepProbe po;
+            rep_prefetch(h, fs, po);
+            c = rep_commit(h, fs, po, hl, irro);
+        }
+        const u32 chk = (mchk ? M_WCHK : 0u) | (ochk ? M_BCHK : 0u);
+        fs = p;
+        fs.meta = with_hl((p.meta & ~(u32)(M_WCHK | M_BCHK | M_DONE)) | chk | ((c >= 3 || c == 0) ? M_DONE : 0u), hl);
+        fs.meta = (fs.meta & ~(u32)M_DONE) + (1u << M_MC_SHIFT);
+        nd += 1;
+    }
+    // boards outside the fast path (per-piece fallback): the state kept after a void reply, more
+    // own pieces than slots, or (BLACK) the position after a reset's opening
+    const bool slow = live && ((!reset && (alone || big)) || (BLACK && reset));
+    const bool cached = reset && !BLACK;  // the start position's rows, count and pick
     u64* const mrow = out.mask ? out.mask + ii : nullptr;
     if (mrow && live) {
-        if (reset) {
+        if (cached) {
             const u64 iown = icd->own;
 #pragma unroll
             for (int k = 0; k < 16; k++) {
@@ -4499,8 +4533,8 @@ __device__ __forceinline__ void apiqv_run(uint8_t* __restrict__ slab, uint64_t s
             }
         }
         if (RR == 0) {
-            const u32 cs = reset ? icd->castles : slow ? apiq_slow_castles(fs) : L.castles[l];
-            const bool cwh = reset ? icd->white != 0 : slow ? (fs.meta & M_WHITE) != 0 : g.white;
+            const u32 cs = cached ? icd->castles : slow ? apiq_slow_castles(fs) : L.castles[l];
+            const bool cwh = cached ? icd->white != 0 : slow ? (fs.meta & M_WHITE) != 0 : g.white;
             u64 cwd = 0;
             if (cs & 1) cwd |= cwh ? (1ull << 1) : (1ull << 3);  // QS: 4097 / 4099
             if (cs & 2) cwd |= cwh ? (1ull << 0) : (1ull << 2);  // KS: 4096 / 4098
@@ -4508,11 +4542,10 @@ __device__ __forceinline__ void apiqv_run(uint8_t* __restrict__ slab, uint64_t s
         }
     }
     if (live && RR == 2) {  // the agent's pick (the next draw, action-id order), the count, the env's next action
-        const u32 nd = cont ? 1u : 0u;  // draws taken by the reply
-        const u32 xp = cont ? L.x1[l] : L.x0[l];
+        const u32 xp = nd == 0 ? L.x0[l] : nd == 1 ? L.x1[l] : L.x2[l];
         int tot = total;
         uint16_t p = (uint16_t)A_NONE;
-        if (reset) {
+        if (cached) {
             tot = (int)C.rtotal;
             p = (uint16_t)L.ra[nd][l];  // (the quads run only with the start position's table)
         } else if (slow) {
@@ -4543,7 +4576,7 @@ __device__ __forceinline__ void apiqv_run(uint8_t* __restrict__ slab, uint64_t s
     } else if (live && RR == 3) {
         if (out.obs) WRITE_OBS_Q3(fs, out.obs, i, nn);
     } else if (live && RR == 1) {
-        if (reset) h.bump_gen();
+        if (reset && !BLACK) h.bump_gen();  // (BLACK: bumped before the opening's entry)
         out.rw[i] = o.reward;
         out.dn[i] = (uint8_t)o.done;
         out.rs[i] = (uint8_t)o.reason;
@@ -4570,6 +4603,7 @@ __device__ __forceinline__ void apiqv_run(uint8_t* __restrict__ slab, uint64_t s
 }
 
 // 16 argument dwords, as k_env_step_api2_vs (all preloaded)
+template <bool BLACK>
 __global__ void __launch_bounds__(4 * QUAD_BOARDS * QUADS_WG) __attribute__((amdgpu_waves_per_eu(4)))
     k_env_step_api4_vs(uint8_t* __restrict__ slab, uint64_t seed, u64* __restrict__ htab,
                        const uint16_t* __restrict__ racts, const EnvDev::InitCache* __restrict__ icd,
@@ -4584,10 +4618,10 @@ __global__ void __launch_bounds__(4 * QUAD_BOARDS * QUADS_WG) __attribute__((amd
     asm volatile("" : "+s"(out.rw), "+s"(out.dn), "+s"(out.rs), "+s"(out.mask), "+s"(out.obs), "+s"(out.cnt),
                  "+s"(out.pick), "+s"(out.ms));
     switch (role) {
-        case 0: apiqv_run<0>(slab, seed, htab, racts, icd, acts, out, nn, rinfo, qw, l, i); break;
-        case 1: apiqv_run<1>(slab, seed, htab, racts, icd, acts, out, nn, rinfo, qw, l, i); break;
-        case 2: apiqv_run<2>(slab, seed, htab, racts, icd, acts, out, nn, rinfo, qw, l, i); break;
-        default: apiqv_run<3>(slab, seed, htab, racts, icd, acts, out, nn, rinfo, qw, l, i); break;
+        case 0: apiqv_run<0, BLACK>(slab, seed, htab, racts, icd, acts, out, nn, rinfo, qw, l, i); break;
+        case 1: apiqv_run<1, BLACK>(slab, seed, htab, racts, icd, acts, out, nn, rinfo, qw, l, i); break;
+        case 2: apiqv_run<2, BLACK>(slab, seed, htab, racts, icd, acts, out, nn, rinfo, qw, l, i); break;
+        default: apiqv_run<3, BLACK>(slab, seed, htab, racts, icd, acts, out, nn, rinfo, qw, l, i); break;
     }
 }
 
@@ -6683,8 +6717,16 @@ extern "C" int gc_env_step_device(gc_env* e, const uint16_t* d_actions, int32_t*
         const dim3 grid((nb + PAIRS_WG - 1) / PAIRS_WG), block(2 * PAIR_BOARDS * PAIRS_WG);
         const char* nq = getenv("GC_NO_QUAD_API");  // A/B and tests (read per call): api2_vs
         const bool no_quad_vs = nq && atoi(nq) != 0;
-        if (!d.agent_black && !no_quad_vs)  // a WHITE agent: four waves per 64 boards (k_env_step_api4_vs)
-            k_env_step_api4_vs<<<(nb + QUADS_WG - 1) / QUADS_WG, 4 * QUAD_BOARDS * QUADS_WG, 0, e->stream>>>(
+        // a BLACK agent stays on the paired kernel unless GC_QUAD_API_BLACK=1 (read per call): its
+        // resets open with the opponent's move, which the quads generate through the per-piece
+        // fallback on every role (46.9 vs 41.6 us per launch, tools/api_color_probe.py)
+        const char* qb = getenv("GC_QUAD_API_BLACK");
+        const bool quad_black = qb && atoi(qb) != 0;
+        if (!no_quad_vs && d.agent_black && quad_black)  // four waves per 64 boards (k_env_step_api4_vs)
+            k_env_step_api4_vs<true><<<(nb + QUADS_WG - 1) / QUADS_WG, 4 * QUAD_BOARDS * QUADS_WG, 0, e->stream>>>(
+                e->slab, d.seed, d.htab, r.racts, r.icd, d_actions, e->api_out, d.n, r.rinfo | ((u32)ar << 17));
+        else if (!no_quad_vs && !d.agent_black)
+            k_env_step_api4_vs<false><<<(nb + QUADS_WG - 1) / QUADS_WG, 4 * QUAD_BOARDS * QUADS_WG, 0, e->stream>>>(
                 e->slab, d.seed, d.htab, r.racts, r.icd, d_actions, e->api_out, d.n, r.rinfo | ((u32)ar << 17));
         else if (d.agent_black)
             k_env_step_api2_vs<true><<<grid, block, 0, e->stream>>>(e->slab, d.seed, d.htab, r.racts, r.icd, d_actions,

@@ -229,19 +229,21 @@ def test_step_device_mask_stride(kind):
         assert outs[0]["mask"].shape == (n, 65)
 
 
+@pytest.mark.parametrize("color", ["WHITE", "BLACK"])
 @pytest.mark.parametrize("start", ["weird", "settled"])
-def test_quad_opponent_api_equals_paired(start):
-    """The random opponent's quad API step (k_env_step_api4_vs, a WHITE agent) == the paired one
+def test_quad_opponent_api_equals_paired(start, color):
+    """The random opponent's quad API step (k_env_step_api4_vs) == the paired one
     (k_env_step_api2_vs, GC_NO_QUAD_API=1) ply by ply with auto-reset: outputs, picks, mask, obs,
     count and states -- on fuzz positions (> 16 pieces, both kings checked, no kings) and on
-    boards settled by 300 plies of play."""
+    boards settled by 300 plies of play; a BLACK agent's resets open with the opponent's move
+    (its quad form is opt-in, GC_QUAD_API_BLACK=1)."""
     import os
 
     from conftest import random_positions
     from gym_chess_amd.env import BatchedChessEnv
 
     n = 1000 if start == "weird" else 4096
-    envs = [BatchedChessEnv(n, device=0, seed=77, opponent="random") for _ in range(2)]
+    envs = [BatchedChessEnv(n, device=0, seed=77, opponent="random", player_color=color) for _ in range(2)]
     if start == "weird":
         boards, metas = random_positions(n, 5151)
         for e in envs:
@@ -260,13 +262,13 @@ def test_quad_opponent_api_equals_paired(start):
         acts.upload_actions(a)
         outs = []
         for k, (e, io) in enumerate(zip(envs, ios)):
-            if k:
-                os.environ["GC_NO_QUAD_API"] = "1"
+            os.environ["GC_NO_QUAD_API" if k else "GC_QUAD_API_BLACK"] = "1"
             try:
                 e.step_device(io, actions=acts.ptr["pick"], autoreset=True)
                 outs.append(io.fetch())
             finally:
                 os.environ.pop("GC_NO_QUAD_API", None)
+                os.environ.pop("GC_QUAD_API_BLACK", None)
         for key in outs[0]:
             assert (outs[0][key] == outs[1][key]).all(), (ply, key, np.nonzero(outs[0][key] != outs[1][key])[0][:4])
         b0, m0 = envs[0].boards()
