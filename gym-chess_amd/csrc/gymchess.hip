@@ -990,6 +990,7 @@ __global__ void k_sum_children(const T* __restrict__ offs, const T* __restrict__
 }
 
 // ----------------------------------------------------------------------------- env kernels
+struct OpenCache;  // (k_init_open_cache)
 struct EnvDev {
     SoA st;
     u64* htab;       // [N/64][HTAB][64][8] repetition tables (gc_env.h; DevHist::entry)
@@ -1024,6 +1025,10 @@ struct EnvDev {
         // not the start position's: the env's spill table, carried in this device-memory
         // block because the paired kernels' arguments are full (rewritten when it grows)
         SpillTab spill;
+        // a BLACK agent's resets: the position after each opening of the move-set-order table
+        // (k_init_open_cache; null until a BLACK agent is set), the agent's picks per opening
+        const OpenCache* open;
+        const uint16_t* open_acts;  // [opening][RESET_ACTS_MAX], action-id order
         // the fused rollout's completion word (gc_env_wait_rollout): workgroups finished
         // (device), launches finished (device), the last count written to host-mapped memory
         struct DoneWord {
@@ -1141,6 +1146,61 @@ __global__ void __launch_bounds__(BLOCK) k_init_cache(EnvDev e, EnvDev::InitCach
         if (g2.in_check && mover_checked(c.pos, ns, c.white != 0, a)) c.open_safe = 0;
     }
     *out = c;
+}
+
+// The position after the k-th opening of the reset position's move-set-order table (the
+// opponent's WHITE opening of a BLACK agent's reset, chess_v2.py:208-216), settled as the env
+// settles it -- check flags, the window after it (the reset position's entry unless the opening
+// is irreversible: length 1 or 0), the move count -- and the agent's moves there, as InitCache.
+struct OpenCache {
+    Pos pos;
+    u64 own;
+    u64 slots[SCRATCH_SLOTS];
+    int total;
+    u32 castles;
+    int white;
+    int usable;  // 0: > 16 own pieces (the per-piece fallback)
+    int table;   // open_acts holds all `total` actions
+    int irrev;   // the opening is irreversible (the window restarts empty)
+};
+__global__ void __launch_bounds__(BLOCK) k_init_open_cache(EnvDev e, const EnvDev::InitCache* ic,
+                                                           const uint16_t* sw_tab, OpenCache* out,
+                                                           uint16_t* acts) {
+    LDS_SCRATCH_DECL;
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= ic->total || !ic->table) return;
+    const Pos s0 = ic->pos;
+    const int op = (int)sw_tab[k];
+    Pos p = s0;
+    p.meta = (p.meta & ~(u32)M_RIGHTS) | eff_rights(s0);  // State::new
+    int mr = 0;
+    bool irrev = false;
+    apply_legal(p, true, op, &mr, &irrev);
+    const bool mchk = mover_checked(s0, p, true, op);
+    Gen g;
+    MoveSet ms;
+    gen_init(p, g);
+    const u32 chk = (mchk ? M_WCHK : 0u) | (g.in_check ? M_BCHK : 0u);
+    const u32 hl = irrev ? 0u : hl_of(s0.meta) + 1u;  // rep_commit on a fresh window: count 1
+    OpenCache c = {};
+    c.pos = p;
+    c.pos.meta = with_hl((p.meta & ~(u32)(M_WCHK | M_BCHK | M_DONE)) | chk, hl) + (1u << M_MC_SHIFT);
+    gen_moves(p, g, ms, scr);
+    c.own = g.own;
+    for (int j = 0; j < SCRATCH_SLOTS; j++) c.slots[j] = ms.big ? 0 : scr.get(j);
+    for (u64 fp = ms.big ? 0 : ms.fastp; fp; fp &= fp - 1) {
+        const int sq = ctz(fp);
+        c.slots[ordinal(g.own, sq)] = fast_pawn_targets(ms, sq, g.white);
+    }
+    c.total = ms.total;
+    c.castles = g.castles;
+    c.white = g.white;
+    c.usable = !ms.big;
+    c.table = c.usable && ms.total > 0 && ms.total <= RESET_ACTS_MAX;
+    c.irrev = irrev ? 1 : 0;
+    for (int j = 0; c.table && j < ms.total; j++)
+        acts[(size_t)k * RESET_ACTS_MAX + j] = (uint16_t)select_action(p, g, ms, scr, j);
+    out[k] = c;
 }
 
 // the API step's `pick` output: uniform over the legal actions, the k-th in action-id order
@@ -4479,44 +4539,34 @@ __device__ __forceinline__ void apiqv_run(uint8_t* __restrict__ slab, uint64_t s
     const bool reset = live && autoreset && o.done;  // chess_v2.py:183-206
     u32 nd = cont ? 1u : 0u;                         // draws taken by the reply (and the opening)
     if (reset) fs = icd->pos;
-    if (BLACK && reset) {  // the opponent opens as WHITE (208-216), its pick read in phase 0
-        const int op = (int)L.ra[nd][l];
-        Pos p = fs;
-        p.meta = (p.meta & ~(u32)M_RIGHTS) | eff_rights(fs);  // State::new
-        int mro = 0;
-        bool irro = false;
-        apply_legal(p, true, op, &mro, &irro);
-        const bool mchk = mover_checked(fs, p, true, op);
-        Gen gk;
-        gen_base(p, gk);
-        const bool ochk = gk.ks >= 0 && sq_attacked(p, gk.ks, true);  // the agent's king, after the opening
-        u32 hl = hl_of(fs.meta);
-        int c = 1;
+    const OpenCache* oc = nullptr;  // BLACK, a reset: the position after the opening
+    if (BLACK && reset) {  // the opponent opens as WHITE (208-216): the opening of draw nd, settled beforehand
+        oc = icd->open + scale_rank(nd == 0 ? L.x0[l] : L.x1[l], C.rtotal);
         if (RR == 1) {  // the window: the reply's write, the reset's new generation, the opening's entry
             h.commit();
             h.bump_gen();
             RepProbe po;
             rep_prefetch(h, fs, po);
-            c = rep_commit(h, fs, po, hl, irro);
+            u32 hl = hl_of(fs.meta);
+            (void)rep_commit(h, fs, po, hl, oc->irrev != 0);  // (count 1, length as the cache's)
         }
-        const u32 chk = (mchk ? M_WCHK : 0u) | (ochk ? M_BCHK : 0u);
-        fs = p;
-        fs.meta = with_hl((p.meta & ~(u32)(M_WCHK | M_BCHK | M_DONE)) | chk | ((c >= 3 || c == 0) ? M_DONE : 0u), hl);
-        fs.meta = (fs.meta & ~(u32)M_DONE) + (1u << M_MC_SHIFT);
+        fs = oc->pos;
         nd += 1;
     }
     // boards outside the fast path (per-piece fallback): the state kept after a void reply, more
-    // own pieces than slots, or (BLACK) the position after a reset's opening
-    const bool slow = live && ((!reset && (alone || big)) || (BLACK && reset));
+    // own pieces than slots, or (BLACK) an opening's position with more own pieces than slots
+    const bool slow = live && ((!reset && (alone || big)) || (BLACK && reset && !oc->usable));
     const bool cached = reset && !BLACK;  // the start position's rows, count and pick
+    const bool ocached = BLACK && reset && oc->usable;  // the opening's
     u64* const mrow = out.mask ? out.mask + ii : nullptr;
     if (mrow && live) {
-        if (cached) {
-            const u64 iown = icd->own;
+        if (cached || ocached) {
+            const u64 iown = cached ? icd->own : oc->own;
+            const u64* const islots = cached ? icd->slots : oc->slots;
 #pragma unroll
             for (int k = 0; k < 16; k++) {
                 const int sq = 16 * RR + k;
-                const u64 w = ((iown >> sq) & 1) ? icd->slots[popc(iown & below(sq))] : 0ull;
+                const u64 w = ((iown >> sq) & 1) ? islots[popc(iown & below(sq))] : 0ull;
                 apiq_store(mrow + sq * N, w);
             }
         } else if (slow) {
@@ -4533,8 +4583,8 @@ __device__ __forceinline__ void apiqv_run(uint8_t* __restrict__ slab, uint64_t s
             }
         }
         if (RR == 0) {
-            const u32 cs = cached ? icd->castles : slow ? apiq_slow_castles(fs) : L.castles[l];
-            const bool cwh = cached ? icd->white != 0 : slow ? (fs.meta & M_WHITE) != 0 : g.white;
+            const u32 cs = cached ? icd->castles : ocached ? oc->castles : slow ? apiq_slow_castles(fs) : L.castles[l];
+            const bool cwh = cached ? icd->white != 0 : ocached ? oc->white != 0 : slow ? (fs.meta & M_WHITE) != 0 : g.white;
             u64 cwd = 0;
             if (cs & 1) cwd |= cwh ? (1ull << 1) : (1ull << 3);  // QS: 4097 / 4099
             if (cs & 2) cwd |= cwh ? (1ull << 0) : (1ull << 2);  // KS: 4096 / 4098
@@ -4548,6 +4598,13 @@ __device__ __forceinline__ void apiqv_run(uint8_t* __restrict__ slab, uint64_t s
         if (cached) {
             tot = (int)C.rtotal;
             p = (uint16_t)L.ra[nd][l];  // (the quads run only with the start position's table)
+        } else if (ocached && oc->table) {
+            tot = oc->total;
+            p = icd->open_acts[(size_t)(oc - icd->open) * RESET_ACTS_MAX + scale_rank(xp, (u32)tot)];
+        } else if (ocached) {  // (never with a standard start: more moves than the table holds)
+            const u32 r = apiq_slow_pick(fs, xp);
+            tot = (int)(r >> 16);
+            p = (uint16_t)(r & 0xFFFFu);
         } else if (slow) {
             const u32 r = apiq_slow_pick(fs, xp);
             tot = (int)(r >> 16);
@@ -5867,6 +5924,8 @@ struct gc_env {
     EnvDev::InitCache* icd = nullptr;  // device copy of d.ic (the paired kernels read it from HBM)
     EnvDev::InitCache* icd_f = nullptr;  // the same for the FIDE reset position (gc_env_set_rules)
     uint16_t* racts_f = nullptr;
+    OpenCache* open_cache = nullptr;     // a BLACK agent's openings (k_init_open_cache, gc_env_set_opponent)
+    uint16_t* open_acts = nullptr;
     EnvDev::InitCache ic_f = {};
     uint8_t* slab = nullptr;  // per-board fields (Slab): bb, meta, hgen, draw, nsteps, reward, act, done, reason
     hipGraphExec_t graph_exec = nullptr;  // GC_GRAPH: a captured chunk of step launches
@@ -5908,7 +5967,7 @@ static int srv_stop(gc_env* e);  // (the single-board server, below)
 #define SRV_QUIESCE(e) do { if (devsrv_quiesce((e)->device)) return -1; } while (0)
 
 static void env_free(gc_env* e) {
-    void* ps[] = {e->api_out, e->reset_acts, e->icd, e->icd_f, e->racts_f, e->ep, e->slab, e->d.htab, e->mbox, e->m8, e->mask,
+    void* ps[] = {e->api_out, e->reset_acts, e->icd, e->icd_f, e->racts_f, e->open_cache, e->open_acts, e->ep, e->slab, e->d.htab, e->mbox, e->m8, e->mask,
                   e->list, e->counts, e->lmask, e->stats};
     for (void* p : ps) if (p) (void)hipFree(p);
     for (auto& v : e->ev) if (v) (void)hipEventDestroy(v);
@@ -6378,6 +6437,18 @@ extern "C" int gc_env_set_opponent(gc_env* e, int opponent, int agent_white) {
     if (set_window_kind(e, !agent_white)) return -1;
     e->d.opp = opponent;
     e->d.agent_black = agent_white ? 0 : 1;
+    if (!agent_white && e->d.ic.table && !e->open_cache) {  // the openings of a BLACK agent's resets
+        if (dalloc(&e->open_cache, RESET_ACTS_MAX) || dalloc(&e->open_acts, (size_t)RESET_ACTS_MAX * RESET_ACTS_MAX))
+            return -1;
+        k_init_open_cache<<<(RESET_ACTS_MAX + BLOCK - 1) / BLOCK, BLOCK, 0, e->stream>>>(
+            e->d, e->icd, e->reset_acts + RESET_ACTS_MAX, e->open_cache, e->open_acts);
+        HIPCHK(hipGetLastError());
+        e->d.ic.open = e->open_cache;
+        e->d.ic.open_acts = e->open_acts;
+        HIPCHK(hipMemcpyAsync(&e->icd->open, &e->d.ic.open, sizeof(e->d.ic.open) + sizeof(e->d.ic.open_acts),
+                              hipMemcpyHostToDevice, e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream));
+    }
     HIPCHK(hipMemsetAsync(e->d.draw, 0, (size_t)4 * e->n, e->stream));  // fresh policy streams
     launch_reset(e, nullptr, 1);
     HIPCHK(hipGetLastError());
@@ -6717,12 +6788,10 @@ extern "C" int gc_env_step_device(gc_env* e, const uint16_t* d_actions, int32_t*
         const dim3 grid((nb + PAIRS_WG - 1) / PAIRS_WG), block(2 * PAIR_BOARDS * PAIRS_WG);
         const char* nq = getenv("GC_NO_QUAD_API");  // A/B and tests (read per call): api2_vs
         const bool no_quad_vs = nq && atoi(nq) != 0;
-        // a BLACK agent stays on the paired kernel unless GC_QUAD_API_BLACK=1 (read per call): its
-        // resets open with the opponent's move, which the quads generate through the per-piece
-        // fallback on every role (46.9 vs 41.6 us per launch, tools/api_color_probe.py)
-        const char* qb = getenv("GC_QUAD_API_BLACK");
-        const bool quad_black = qb && atoi(qb) != 0;
-        if (!no_quad_vs && d.agent_black && quad_black)  // four waves per 64 boards (k_env_step_api4_vs)
+        // (a BLACK agent's resets open with the opponent's move: the openings' positions and moves
+        // are cached, k_init_open_cache -- 33.9 vs 41.1 us per launch for the paired kernel,
+        // tools/api_color_probe.py; through the per-piece fallback instead: 46.9)
+        if (!no_quad_vs && d.agent_black && d.ic.open)  // four waves per 64 boards (k_env_step_api4_vs)
             k_env_step_api4_vs<true><<<(nb + QUADS_WG - 1) / QUADS_WG, 4 * QUAD_BOARDS * QUADS_WG, 0, e->stream>>>(
                 e->slab, d.seed, d.htab, r.racts, r.icd, d_actions, e->api_out, d.n, r.rinfo | ((u32)ar << 17));
         else if (!no_quad_vs && !d.agent_black)

@@ -236,7 +236,7 @@ def test_quad_opponent_api_equals_paired(start, color):
     (k_env_step_api2_vs, GC_NO_QUAD_API=1) ply by ply with auto-reset: outputs, picks, mask, obs,
     count and states -- on fuzz positions (> 16 pieces, both kings checked, no kings) and on
     boards settled by 300 plies of play; a BLACK agent's resets open with the opponent's move
-    (its quad form is opt-in, GC_QUAD_API_BLACK=1)."""
+    (the quads take the opening's position and moves from k_init_open_cache)."""
     import os
 
     from conftest import random_positions
@@ -262,13 +262,13 @@ def test_quad_opponent_api_equals_paired(start, color):
         acts.upload_actions(a)
         outs = []
         for k, (e, io) in enumerate(zip(envs, ios)):
-            os.environ["GC_NO_QUAD_API" if k else "GC_QUAD_API_BLACK"] = "1"
+            if k:
+                os.environ["GC_NO_QUAD_API"] = "1"
             try:
                 e.step_device(io, actions=acts.ptr["pick"], autoreset=True)
                 outs.append(io.fetch())
             finally:
                 os.environ.pop("GC_NO_QUAD_API", None)
-                os.environ.pop("GC_QUAD_API_BLACK", None)
         for key in outs[0]:
             assert (outs[0][key] == outs[1][key]).all(), (ply, key, np.nonzero(outs[0][key] != outs[1][key])[0][:4])
         b0, m0 = envs[0].boards()

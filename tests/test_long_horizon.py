@@ -6,8 +6,8 @@ test had met the position).  Each case runs the device's random self-play as fus
 the oracle driver (oracle/gc_oracle.c restating chess_v2.py:219-294 over lib.rs).
 Cases: opponent "none" (the headline kernel k_env_rollout4), the random opponent for a WHITE
 agent and for a BLACK agent (whose unbounded windows go through the spill table); and the
-random opponent's device API step (k_env_step_api4_vs for a WHITE agent, k_env_step_api2_vs for
-a BLACK one) stepped with its own picks, auto-reset on.
+random opponent's device API step (k_env_step_api4_vs, both colours) stepped with its own picks,
+auto-reset on.
 Reference: test_benchmark.py:9-43 (the driver), chess_v2.py:116-127 (the random policy),
 chess_v2.py:192, 402-407 (3-fold), lib.rs:460-784 (moves, next_state)."""
 import os

@@ -1,6 +1,5 @@
 """Diagnostic only: the random opponent's API step per launch (HIP events) for a WHITE and a
-BLACK agent, quad (k_env_step_api4_vs; BLACK opt-in, GC_QUAD_API_BLACK=1) and paired
-(GC_NO_QUAD_API=1) kernels, 65 536 boards.
+BLACK agent, quad (k_env_step_api4_vs) and paired (GC_NO_QUAD_API=1) kernels, 65 536 boards.
 
     python tools/api_color_probe.py [boards] [steps]
 """
@@ -15,7 +14,8 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 300
 for color in ("WHITE", "BLACK"):
     for paired in (False, True):
-        os.environ["GC_NO_QUAD_API" if paired else "GC_QUAD_API_BLACK"] = "1"
+        if paired:
+            os.environ["GC_NO_QUAD_API"] = "1"
         env = BatchedChessEnv(n, device=0, seed=99, opponent="random", player_color=color)
         env.rollout(200)
         io = env.device_io()
@@ -31,4 +31,3 @@ for color in ("WHITE", "BLACK"):
         io.close()
         env.close()
         os.environ.pop("GC_NO_QUAD_API", None)
-        os.environ.pop("GC_QUAD_API_BLACK", None)
