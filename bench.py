@@ -370,7 +370,14 @@ def api_step_leg(args, rep, n, **env_kw):
     out = {"value": rep.world_size * n * args.api_steps / dt, "unit": "env_steps/s", "steps": args.api_steps,
            "roofline": {"bound": "hbm", "kernel": kern, "achieved": ach,
                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "avg_launch_us": avg * 1e6,
-                        "alg_bytes_per_board": ALG_BYTES_API}}
+                        "alg_bytes_per_board": ALG_BYTES_API, "traffic": None}}
+    pa = load_pmc(os.path.join(ROOT, "profiles", "pmc_api_latest.json"))
+    kp = (pa or {}).get("kernels", {}).get(kern)
+    if kp:  # HBM bytes per launch by PMC (tools/api_pmc.sh), scaled to this run's boards
+        out["roofline"]["traffic"] = kp["bytes_per_board"] * n
+        out["roofline"]["pmc_source"] = {"file": "profiles/pmc_api_latest.json", "profile": pa.get("profile"),
+                                         "bytes_per_board": kp["bytes_per_board"],
+                                         "note": "FETCH_SIZE x2 + WRITE_SIZE per launch of the bench's API legs"}
     if env_kw:
         out["env"] = env_kw
     return out
