@@ -843,11 +843,14 @@ __global__ void k_followers2(int n, const uint8_t* __restrict__ lflag, const u32
 // position) and, in sorted order, each member's (leader position, parent) pair; the leaf lane of
 // the leader at sorted position pL walks the later members of its run -- none for a lone position,
 // which then reads nothing more -- and adds its count into the parent of every member it leads.
-#define RUN_LEN_SHIFT 27
-#ifndef GC_RUN_CAP
-#define GC_RUN_CAP 15  // the lead word's run length saturates here (a test build lowers it: the tag walk then runs)
+#ifndef RUN_LEN_SHIFT
+#define RUN_LEN_SHIFT 27  // sorted positions below 2^27 (chunks of up to 2^21 parents), run lengths in bits 27-30
 #endif
-static_assert(GC_RUN_CAP >= 1 && GC_RUN_CAP <= 15, "GC_RUN_CAP: 4 bits");
+#ifndef GC_RUN_CAP
+#define GC_RUN_CAP ((1 << (31 - RUN_LEN_SHIFT)) - 1)  // the lead word's run length saturates here (a test
+                                                      // build lowers it: the tag walk then runs)
+#endif
+static_assert(GC_RUN_CAP >= 1 && GC_RUN_CAP < (1 << (31 - RUN_LEN_SHIFT)), "GC_RUN_CAP: the bits above RUN_LEN_SHIFT");
 __global__ void __launch_bounds__(BLOCK) k_dedup_runs_f(const Node64* __restrict__ in, int n,
                                                         const u32* __restrict__ keys, const u32* __restrict__ vals,
                                                         u32* __restrict__ leadw, uint2* __restrict__ fw) {
@@ -5553,7 +5556,9 @@ static int perft_split_leaves(hipStream_t st, SoA leaf, uint64_t* leaf_out) {
     // GC_PERFT_FUSE=0 (A/B, sorting pass only): the followers added by a pass of their own
     // (k_followers2) instead of by their leader's leaf lane
     const char* sf = getenv("GC_PERFT_FUSE");
-    const bool fuse = sortdedup && !(sf && sf[0] == '0');
+    // (the lead word holds a sorted position in RUN_LEN_SHIFT bits: chunks of more records take
+    // the follower pass)
+    const bool fuse = sortdedup && !(sf && sf[0] == '0') && cap <= ((int64_t)1 << RUN_LEN_SHIFT);
     int32_t *kc = nullptr, *offs = nullptr, *kc2 = nullptr, *ks = nullptr, *ix = nullptr, *is = nullptr;
     uint8_t* bins = nullptr;
     u32 *hist = nullptr, *hbase = nullptr;
