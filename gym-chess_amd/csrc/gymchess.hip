@@ -2489,6 +2489,10 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
     pair_barrier();
     PST(3);
     // ---- phase 2
+#ifdef GC_QPRIO_P2  // A/B: Q2 (phase 2's longest chain, its SIMD shared with Q0) raised over Q0 from phase 2 on
+    if (R == 0) __builtin_amdgcn_s_setprio(0);
+    if (R == 2) __builtin_amdgcn_s_setprio(2);
+#endif
 #if GC_Q1_LEAPERS
 #define QUAD_ENEMY(l) (L.enemy[0][l] | L.enemy[1][l] | L.enemy[2][l])
 #else
