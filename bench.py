@@ -98,6 +98,8 @@ def parse():
                     help="configs[0]: the reference benchmark driver on the single-board env (0 = skip)")
     ap.add_argument("--concurrent-ms", type=float, default=0.0,
                     help="replicas' common-interval leg (>= this many ms per replica); always on (250 ms) for N > 1")
+    ap.add_argument("--configs1-roots", type=int, default=4096,
+                    help="configs[1]: start-position roots of the perft(3) leg (0 = skip)")
     ap.add_argument("--perft-depth", type=int, default=5)
     ap.add_argument("--perft-subsample", type=int, default=256,
                     help="roots of the fixed strided subsample checked (and CPU-timed) one ply shallower")
@@ -207,20 +209,16 @@ def perft_leg(args, rep):
            "leaf_pass": {k: paths1[k] - paths0[k] for k in paths0},
            "roots_with": {"castle_right": castle, "pawn_on_7th": prom, "side_in_check": check}}
     # the leaf kernel (k_perft2_val: one lane = one distinct depth-2 subtree, read in order,
-    # last ply bulk-counted): where the time goes.  It is VALU-bound -- 80 algorithmic HBM bytes
-    # per subtree (the 64-B root record in, its count kept and added into the parent's sum)
-    # against ~1e3 leaves -- so its roof is the VALU issue rate (PMC profile, tools/gpu_run.sh
-    # pmcp*).  Transpositions (round 4): the split pass counts one depth-2 subtree per distinct
-    # position of a chunk (exact: whole-record compare) and adds that count to every parent the
-    # position occurs under -- round 5: the records sorted by hash tag, each leader's leaf lane
-    # adding its count into its followers' parents (72 B: record + parent add; the count kept
-    # for a follower pass, GC_PERFT_FUSE=0 or the CAS table GC_PERFT_SORTDEDUP=0: 80 B);
-    # GC_PERFT_DEDUP=0 counts every record (k_perft2_rec, 72 B); GC_PERFT_GATHER: the
-    # round-2/3 form, gathering through a sorted permutation (+ 4 B index)
-    gather = bool(os.environ.get("GC_PERFT_GATHER"))
-    dedup = not gather and os.environ.get("GC_PERFT_DEDUP", "1") != "0"
-    fused = dedup and os.environ.get("GC_PERFT_SORTDEDUP", "1") != "0" and os.environ.get("GC_PERFT_FUSE", "1") != "0"
-    alg_sub = 76 if gather else (72 if fused or not dedup else 80)
+    # last ply bulk-counted): where the time goes.  It is VALU-bound -- 72 algorithmic HBM bytes
+    # per subtree (the 64-B root record in, its count added into the parent's sum) against ~1e3
+    # leaves -- so its roof is the VALU issue rate (PMC profile, tools/gpu_run.sh pmcp*).
+    # Transpositions (round 4): the split pass counts one depth-2 subtree per distinct position
+    # of a chunk (exact: whole-record compare) and adds that count to every parent the position
+    # occurs under -- since round 5 the records sorted by hash tag, each leader's leaf lane
+    # adding its count into its followers' parents.  GC_PERFT_DEDUP=0 counts every record
+    # (k_perft2_rec, 72 B).
+    dedup = os.environ.get("GC_PERFT_DEDUP", "1") != "0"
+    alg_sub = 72
     la, sub, kms = (b - a for a, b in zip(leaf0, leaf1))
     recs, counted = (b - a for a, b in zip(dd0, dd1))
     if recs:
@@ -229,7 +227,7 @@ def perft_leg(args, rep):
         out["transpositions"] = {"records": recs, "counted": counted, "records_per_counted": recs / max(1, counted),
                                  "merged": dedup, "records_per_s": recs / dtm, "counted_subtrees_per_s": counted / dtm}
     if la:
-        kname = "k_perft2_perm_rec" if gather else ("k_perft2_val" if dedup else "k_perft2_rec")
+        kname = "k_perft2_val" if dedup else "k_perft2_rec"
         roof = {"bound": "valu", "kernel": kname, "launches": la,
                 "subtrees": sub, "kernel_ms": kms, "share_of_perft_time": kms / 1e3 / len(rep.local) / dtm,
                 "alg_bytes_per_subtree": alg_sub, "hbm_achieved_gbs": alg_sub * sub / (kms / 1e3) / 1e9}
@@ -283,6 +281,61 @@ def perft_leg(args, rep):
                                    f"across threads)",
                                    "spread_roots_depth5": {"value": float(cn.sum()) / cdt, "roots": len(idx),
                                                            "nodes": int(cn.sum()), "seconds": cdt}}
+    return out
+
+
+def perft_startpos_leg(args, rep, depth=3, reps=20):
+    """configs[1]: --configs1-roots copies of the start position, perft(3) through the engine
+    C-ABI (gc_engine_perft; 8 982 leaves per root under the reference rules), timed
+    over `reps` calls after a warm call; every root's count must equal the oracle's.  CPU
+    baseline: the oracle's perft(3) of the start position on a bounded sample of roots."""
+    import numpy as np
+
+    from gym_chess_amd import codec as C
+    from gym_chess_amd.engine import Engine
+
+    n = args.configs1_roots
+    b = np.tile(np.asarray(C.DEFAULT_BOARD, np.int8).reshape(1, 64), (n, 1))
+    m = np.zeros((n, 8), np.uint8)
+    m[:, 0:5] = 1  # WHITE to move, all four castle rights (chess_v2.py:183-206)
+
+    def prep(rp):
+        eng = Engine(rp.device)
+        eng.perft(b, m, depth)  # load the kernels
+        return eng
+
+    ctx = rep.run(prep)
+
+    def run(rp):
+        eng = ctx[rep.local.index(rp)]
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            nodes = eng.perft(b, m, depth)
+        return nodes, time.perf_counter() - t0
+
+    res, dt = rep.timed(run)
+    for eng in ctx:
+        eng.close()
+    tot = rep.sum(float(sum(float(r.sum()) for r in res))) * reps
+    out = {"value": tot / dt, "unit": "perft_nodes/s", "roots_per_gpu": n, "depth": depth, "calls": reps,
+           "nodes_per_call": int(res[0].sum()), "ms_per_call": dt * 1e3 / reps,
+           "form": "one gc_engine_perft call per repetition (host arrays in, per-root counts out: PCIe included)"}
+    if rep.rank == 0:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O
+
+        threads = max(1, min(16, os.cpu_count() or 1))
+        t0 = time.perf_counter()
+        cn = O.perft_by_children(b, m, depth, threads=threads)
+        cdt = time.perf_counter() - t0
+        assert (cn == cn[0]).all() and (res[0] == cn[0]).all(), "configs[1] perft differs from the oracle"
+        out["oracle_nodes_per_root"] = int(cn[0])
+        out["match"] = True
+        if rep.world_size == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = {"value": float(cn.sum()) / cdt, "unit": "perft_nodes/s", "cores": threads,
+                                   "kind": "port",
+                                   "sample": f"all {n} start-position roots x perft({depth}) ({int(cn.sum())} nodes, "
+                                             f"{cdt:.2f} s) with the C oracle, children handed out across threads"}
     return out
 
 
@@ -362,17 +415,20 @@ def api_step_leg(args, rep, n, **env_kw):
         env.close()
     avg = kms / 1e3 / args.api_steps
     ach = n * ALG_BYTES_API / avg / 1e9
-    # the quad API steps (k_env_step_api4; the random opponent's with a WHITE agent:
-    # k_env_step_api4_vs) -- GC_NO_QUAD_API=1: the paired ones
+    # the quad API steps (k_env_step_api4; the random opponent's: k_env_step_api4_vs<BLACK>) --
+    # GC_NO_QUAD_API=1: the opponent's paired one
     paired = os.environ.get("GC_NO_QUAD_API", "0") not in ("", "0")
-    kern = ("k_env_step_api2_vs" if paired else "k_env_step_api4_vs") if env_kw else (
-        "k_env_step_api2" if paired else "k_env_step_api4")
+    black = env_kw.get("player_color") == "BLACK"
+    kern = (("k_env_step_api2_vs" if paired else "k_env_step_api4_vs") + ("<true>" if black else "<false>")
+            if env_kw else "k_env_step_api4")
     out = {"value": rep.world_size * n * args.api_steps / dt, "unit": "env_steps/s", "steps": args.api_steps,
            "roofline": {"bound": "hbm", "kernel": kern, "achieved": ach,
                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "avg_launch_us": avg * 1e6,
                         "alg_bytes_per_board": ALG_BYTES_API, "traffic": None}}
     pa = load_pmc(os.path.join(ROOT, "profiles", "pmc_api_latest.json"))
     kp = (pa or {}).get("kernels", {}).get(kern)
+    if kp is None and kern.endswith("<false>"):  # summaries before round 6 dropped the template argument
+        kp = (pa or {}).get("kernels", {}).get(kern[:-len("<false>")])
     if kp:  # HBM bytes per launch by PMC (tools/api_pmc.sh), scaled to this run's boards
         out["roofline"]["traffic"] = kp["bytes_per_board"] * n
         out["roofline"]["pmc_source"] = {"file": "profiles/pmc_api_latest.json", "profile": pa.get("profile"),
@@ -668,6 +724,11 @@ def main():
         extra["api_step"] = api_step_leg(args, rep, n)
         # the random opponent answering inside each step (chess_v2.py:275-288)
         extra["api_step"]["opponent_random"] = api_step_leg(args, rep, n, opponent="random")
+        # a BLACK agent: the opponent opens every reset game (chess_v2.py:208-216), windows unbounded
+        extra["api_step"]["opponent_random_black"] = api_step_leg(args, rep, n, opponent="random",
+                                                                  player_color="BLACK")
+    if args.configs1_roots > 0:
+        extra["perft_startpos"] = perft_startpos_leg(args, rep)
     if args.single_episodes > 0:
         extra["single_env"] = single_env_leg(args, rep)
     if args.variant_steps > 0:

@@ -1141,10 +1141,10 @@ GC_HD void ray_fill_pair(u64 ge, u64 go, u64 empty, u64 wrap, u64& ae, u64& ao) 
 }
 // kh: the king lines of the side to move if its tracked king sits on kh.ks (perft: computed
 // once per subtree root); otherwise (a king captured, Q7) they are recomputed here
-// ktab (the round-5 LDS-table A/B, GC_PERFT_LDS): king neighbourhoods by square from a table in
-// LDS for the enemy king's attacks, and the own king's steps from the per-root KingLines, instead
-// of the set-wise shifts
-GC_HD int count_position_kl(const Pos& s, const KingLines& kh, const u64* ktab = nullptr, const u64* ntab = nullptr) {
+// ntab (the perft leaf's LDS table, round 5): the own knights' jumps by square instead of the
+// eight shifted jump sets.  The own king's steps come from the per-root KingLines (perft 1.566 ->
+// 1.583e12 same-box); the enemy king's neighbourhood from a table was measured slower.
+GC_HD int count_position_kl(const Pos& s, const KingLines& kh, const u64* ntab = nullptr) {
     Gen g;
     gen_base_ks(s, g, kh);  // the tracked king from the hint while the side's kings are the hint's
     KingLines kl = kh;
@@ -1169,25 +1169,10 @@ GC_HD int count_position_kl(const Pos& s, const KingLines& kh, const u64* ktab =
     GC_PAIR(7, true, eBQ, G.a, ~FILE_H)
 #undef GC_PAIR
     if (g.ks >= 0) {  // gen_enemy (no king: no map, no castling)
-        if (ktab) {
-            const u64 ek = s.k & g.opp;
-            const u64 ekatt = (ek & (ek - 1)) == 0 && ek ? ktab[ctz(ek)] : king_set(ek);
-            u64 enatt = 0;
-            if (ntab) {
-                for (u64 x = s.n & g.opp; x; x &= x - 1) enatt |= ntab[ctz(x)];
-            } else {
-                enatt = knight_set(s.n & g.opp);
-            }
-            g.enemy_att = att | (pawn_att_set(s.p & g.opp, !g.white) & ~ek) | enatt | ekatt;
-        } else {
-            g.enemy_att = att | side_attacks_leapers(s, !g.white);
-        }
+        g.enemy_att = att | side_attacks_leapers(s, !g.white);
         gen_castles(s, g);
     }
-#ifndef GC_KL_KING
-#define GC_KL_KING 1  // the own king's steps from the per-root KingLines (perft 1.566 -> 1.583e12 same-box)
-#endif
-    return n + count_nonsliders_kl(s, g, kl, ktab != nullptr || GC_KL_KING, ntab);
+    return n + count_nonsliders_kl(s, g, kl, true, ntab);
 }
 GC_HD int count_position(const Pos& s) { return count_position_kl(s, king_lines_of(s, (s.meta & M_WHITE) != 0)); }
 

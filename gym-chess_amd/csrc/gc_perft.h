@@ -95,7 +95,7 @@ GC_HD uint64_t perft_small(const Pos& root, int depth, SA& sa, SB& sb) {
 // perft_small at depth 2 only (one loop; one scratch for the root's parked targets): the
 // split leaf level's kernel, small enough in registers for more waves per SIMD
 template <class SA>
-GC_HD uint64_t perft2(const Pos& root, SA& sa, const u64* ktab = nullptr, const u64* ntab = nullptr) {
+GC_HD uint64_t perft2(const Pos& root, SA& sa, const u64* ntab = nullptr) {
     Gen g0;
     MoveSet m0;
     gen_init(root, g0);
@@ -112,13 +112,7 @@ GC_HD uint64_t perft2(const Pos& root, SA& sa, const u64* ktab = nullptr, const 
     MoveWalk w0(g0);
     for (int k1 = 0; k1 < m0.total; k1++) {
         Pos c1 = child_of(root, g0.white, w0.next(g0, m0, sa));
-#ifdef GC_PERFT_UNFUSED  // A/B: the map and the count in two passes
-        Gen g1;
-        gen_init(c1, g1);
-        nodes += (uint64_t)count_moves(c1, g1);
-#else
-        nodes += (uint64_t)count_position_kl(c1, k1l, ktab, ntab);
-#endif
+        nodes += (uint64_t)count_position_kl(c1, k1l, ntab);
     }
     return nodes;
 }

@@ -451,30 +451,6 @@ __device__ __forceinline__ void node_store(Node64* __restrict__ v, size_t j, con
     x[2] = make_ulonglong2(s.n, s.p);
     x[3] = make_ulonglong2(s.w, (u64)s.meta | ((u64)parent << 32));
 }
-// one lane = one depth-2 subtree, visited in move-count order (perm); its count goes straight
-// into its parent's total (a 64-bit atomic into the chunk's parent sums, zeroed by the
-// caller: <= 2^21 parents, 16 MiB, cache-resident) -- no per-subtree value array, no
-// scattered value write, no summing pass
-__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(PERFT2_WPE)))
-k_perft2_perm_rec(const Node64* __restrict__ in, int n, const int32_t* __restrict__ perm,
-                  unsigned long long* __restrict__ parent_sum) {
-    __shared__ u64 lds_a[SCRATCH_SLOTS * BLOCK];
-    LdsScratch sa{lds_a + threadIdx.x};
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int j = perm[i];
-    const u32 parent = reinterpret_cast<const u32*>(in + j)[15];
-    atomicAdd(parent_sum + parent, (unsigned long long)perft2(node_load(in, j), sa));
-}
-__global__ void k_count_children_rec(const Node64* __restrict__ in, int n, int32_t* __restrict__ cnt) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    Pos s = node_load(in, i);
-    Gen g;
-    gen_init(s, g);
-    cnt[i] = count_moves(s, g);
-}
-
 __global__ void k_iota(int32_t* __restrict__ v, int n) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) v[i] = i;
@@ -625,18 +601,10 @@ k_perft2_rec(const Node64* __restrict__ in, int n, unsigned long long* __restric
 // m3 and m3, x, m1 reach one position -- ~1.7 records per distinct position over mid-game
 // roots.  perft2 is a function of the Pos alone, so one record per position (its leader) is
 // counted and the others (followers) add the leader's count into their own parents.  With
-// the merge the chunk's records are written in expansion order (k_expand_range_rec) and:
-//   k_dedup_bin   every record claims a slot of an open-addressed table keyed by a hash of its
-//                 Pos (entry = hash tag << 32 | record index, 0 = empty) by one CAS; a tag
-//                 match is confirmed by comparing the two whole records, so a merge is exact.
-//                 A leader's move count (the leaf's lane-balancing bin) is computed here, for
-//                 leaders only, while the other waves wait on their CASes; per-block leader
-//                 histograms; followers append (parent, leader) pairs, one atomic per wave;
-//   k_place_leaders  the leaders copied into move-count order (the scanned histograms'
-//                 cursors), each one's placed index kept;
-//   k_perft2_val  the leaf over the placed leaders (dense, in order), each count kept;
-//   k_followers   each follower adds its leader's count into its own parent.
-#define DEDUP_BLOCK 1024
+// the merge the chunk's records are written in expansion order (k_expand_range_rec) and grouped
+// by sorting (below).  (Round 4's first form -- one CAS per record into an open-addressed table,
+// ~1 TB/s of random line traffic, 12.5 ms per chunk -- and round 5's sort with a follower pass of
+// its own were measured slower and removed in round 6.)
 __device__ __forceinline__ u64 pos_hash(const Pos& s) {
     u64 h = s.meta * 0x9E3779B97F4A7C15ull;
     const u64 f[7] = {s.k, s.q, s.r, s.b, s.n, s.p, s.w};
@@ -651,194 +619,29 @@ __device__ __forceinline__ bool pos_equal(const Pos& a, const Pos& b) {
     return ((a.k ^ b.k) | (a.q ^ b.q) | (a.r ^ b.r) | (a.b ^ b.b) | (a.n ^ b.n) | (a.p ^ b.p) | (a.w ^ b.w)) == 0 &&
            a.meta == b.meta;
 }
-// DEDUP_R records per thread (block b: records [b, b + 1) * DEDUP_BLOCK * DEDUP_R, the r-th
-// DEDUP_BLOCK of them on pass r): their loads, hashes and CASes issued back to back, so DEDUP_R
-// table round trips are in flight per lane instead of one
-#ifndef DEDUP_R
-#define DEDUP_R 1
-#endif
-__global__ void __launch_bounds__(DEDUP_BLOCK) k_dedup_bin(const Node64* __restrict__ in, int n, u64* __restrict__ table,
-                                                           u32 mask, uint8_t* __restrict__ bins,
-                                                           uint8_t* __restrict__ lflag, u32* __restrict__ hist, int nblk,
-                                                           u32* __restrict__ nfol, uint2* __restrict__ fol) {
-    __shared__ u32 hb[SPLIT_BINS];
-    for (int b = threadIdx.x; b < SPLIT_BINS; b += blockDim.x) hb[b] = 0;
-    __syncthreads();
-    const size_t i0 = (size_t)blockIdx.x * DEDUP_BLOCK * DEDUP_R + threadIdx.x;
-    Pos s[DEDUP_R];
-    u64 tag[DEDUP_R], e[DEDUP_R];
-    u32 slot[DEDUP_R];
-#pragma unroll
-    for (int r = 0; r < DEDUP_R; r++) {
-        const size_t i = i0 + (size_t)r * DEDUP_BLOCK;
-        s[r] = node_load(in, i < (size_t)n ? i : (size_t)n - 1);
-    }
-#pragma unroll
-    for (int r = 0; r < DEDUP_R; r++) {  // every CAS issued before any result is needed
-        const size_t i = i0 + (size_t)r * DEDUP_BLOCK;
-        const u64 h = pos_hash(s[r]);
-        tag[r] = (h >> 32) | 1u;
-        slot[r] = (u32)h & mask;
-        e[r] = i < (size_t)n ? atomicCAS(reinterpret_cast<unsigned long long*>(table + slot[r]), 0ull,
-                                         (unsigned long long)((tag[r] << 32) | (u32)i))
-                             : 0ull;
-    }
-#pragma unroll
-    for (int r = 0; r < DEDUP_R; r++) {
-        const size_t i = i0 + (size_t)r * DEDUP_BLOCK;
-        bool follower = false;
-        u32 lead = 0, parent = 0;
-        if (i < (size_t)n) {
-            parent = reinterpret_cast<const u32*>(in + i)[15];
-            const u64 mine = (tag[r] << 32) | (u32)i;
-            u64 x = e[r];
-            u32 sl = slot[r];
-            for (;;) {  // (a relaxed load ahead of the CAS measured the same)
-                if (x == 0) break;  // this record leads its position
-                if ((x >> 32) == tag[r] && pos_equal(node_load(in, (u32)x), s[r])) {
-                    follower = true;
-                    lead = (u32)x;
-                    break;
-                }
-                sl = (sl + 1) & mask;
-                x = atomicCAS(reinterpret_cast<unsigned long long*>(table + sl), 0ull, (unsigned long long)mine);
-            }
-            lflag[i] = follower ? 0 : 1;
-            if (!follower) {
-                const int b = split_bin(s[r], king_lines_of(s[r], (s[r].meta & M_WHITE) != 0));
-                bins[i] = (uint8_t)b;
-                atomicAdd(&hb[b], 1u);
-            }
-        }
-        const u64 bal = __ballot(follower);  // wave-aggregated append of the followers
-        if (bal) {
-            const int lane = threadIdx.x & 63;
-            const int first = __ffsll((long long)bal) - 1;
-            u32 base = 0;
-            if (lane == first) base = atomicAdd(nfol, (u32)__popcll(bal));
-            base = __shfl(base, first);
-            if (follower) fol[base + __popcll(bal & ((1ull << lane) - 1))] = make_uint2(parent, lead);
-        }
-    }
-    __syncthreads();
-    for (int b = threadIdx.x; b < SPLIT_BINS; b += blockDim.x) hist[(size_t)b * nblk + blockIdx.x] = hb[b];
-}
-__global__ void __launch_bounds__(DEDUP_BLOCK) k_place_leaders(const Node64* __restrict__ in, int n,
-                                                               const uint8_t* __restrict__ bins,
-                                                               const uint8_t* __restrict__ lflag,
-                                                               const u32* __restrict__ base, int nblk,
-                                                               Node64* __restrict__ out, int32_t* __restrict__ place_of) {
-    __shared__ u32 cur[SPLIT_BINS];
-    for (int b = threadIdx.x; b < SPLIT_BINS; b += blockDim.x) cur[b] = base[(size_t)b * nblk + blockIdx.x];
-    __syncthreads();
-    for (int r = 0; r < DEDUP_R; r++) {  // k_dedup_bin's blocks: DEDUP_BLOCK * DEDUP_R records
-        const size_t i = (size_t)blockIdx.x * DEDUP_BLOCK * DEDUP_R + (size_t)r * DEDUP_BLOCK + threadIdx.x;
-        if (i >= (size_t)n || !lflag[i]) continue;
-        const u32 slot = atomicAdd(&cur[bins[i]], 1u);
-        const ulonglong2* x = reinterpret_cast<const ulonglong2*>(in + i);
-        ulonglong2* y = reinterpret_cast<ulonglong2*>(out + slot);
-        const ulonglong2 r0 = x[0], r1 = x[1], r2 = x[2], r3 = x[3];
-        y[0] = r0; y[1] = r1; y[2] = r2; y[3] = r3;
-        place_of[i] = (int32_t)slot;
-    }
-}
-// The transposition pass by sorting (round 5, GC_PERFT_SORTDEDUP, the default): every record's
-// 32-bit hash tag and index sorted by the tag (hipCUB radix sort: ~2 ms for 2^26 pairs), so equal
-// positions are adjacent and the pass reads sequentially -- where k_dedup_bin made one random
-// CAS per record into a 1 GiB table (~1 TB/s of random line traffic, 12 ms per chunk).
-//   k_dedup_keys   per record, in order: the tag, the index, the parent, the leaf's move-count bin
-//   (sort)         by the tag (stable: a run's members in record order)
-//   k_dedup_runs   one lane per run of equal tags: the members compared whole with the run's
-//                  first (and, after a tag collision, with the run's other leaders), so a merge is
-//                  exact; each group's first member leads
-//   k_leader_hist  per-block leader histograms by bin (k_place_leaders' blocks)
-//   k_followers2   each follower adds its leader's count into its own parent
+// The transposition pass by sorting (round 5): every record's 32-bit hash tag and index sorted
+// by the tag (hipCUB radix sort: ~2 ms for 2^26 pairs), so equal positions are adjacent and the
+// pass reads sequentially.
+//   k_dedup_keys     per record, in order: the tag, the index, the leaf's move-count bin
+//   (sort)           by the tag (stable: a run's members in record order)
+//   k_dedup_runs_f   one lane per sorted record: the members compared whole with the run's
+//                    first (and, after a tag collision, with the run's earlier members), so a
+//                    merge is exact; each group's first member leads
+//   k_leader_hist_f  per-block leader histograms by bin (k_place_leaders_f's blocks)
+//   k_place_leaders_f  the leaders copied into move-count order
+//   k_perft2_val     the leaf over the placed leaders, each lane crediting its followers
+#define DEDUP_BLOCK 1024
+#define DEDUP_R 1  // records per thread of the histogram / placement passes (2 or 4: no gain, round 5)
 __global__ void __launch_bounds__(BLOCK) k_dedup_keys(const Node64* __restrict__ in, int n, u32* __restrict__ keys,
-                                                      u32* __restrict__ vals, uint8_t* __restrict__ bins,
-                                                      u32* __restrict__ parent_of) {
+                                                      u32* __restrict__ vals, uint8_t* __restrict__ bins) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const Pos s = node_load(in, i);
     keys[i] = (u32)(pos_hash(s) >> 32);
     vals[i] = (u32)i;
-    if (parent_of) parent_of[i] = reinterpret_cast<const u32*>(in + i)[15];
     bins[i] = (uint8_t)split_bin(s, king_lines_of(s, (s.meta & M_WHITE) != 0));
 }
-#ifndef GC_DEDUP_PAR
-#define GC_DEDUP_PAR 1  // k_dedup_runs: one lane per sorted record (0: one lane per run, members in a loop)
-#endif
-__global__ void __launch_bounds__(BLOCK) k_dedup_runs(const Node64* __restrict__ in, int n, const u32* __restrict__ keys,
-                                                      const u32* __restrict__ vals, uint8_t* __restrict__ lflag,
-                                                      u32* __restrict__ lead) {
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= n) return;
-    const u32 k = keys[p];
-#if GC_DEDUP_PAR
-    // every lane settles its own record: the run's first member (earliest in record order, the
-    // sort being stable) leads; a later member follows the earliest member equal to it -- the
-    // run's first, or after a tag collision an earlier member found by the ordered scan
-    const u32 r = vals[p];
-    int p0 = p;
-    while (p0 > 0 && keys[p0 - 1] == k) p0--;
-    u32 ld = r;
-    if (p0 < p) {
-        const Pos s = node_load(in, r);
-        const u32 r0 = vals[p0];
-        if (pos_equal(s, node_load(in, r0))) {
-            ld = r0;
-        } else {
-            for (int t = p0 + 1; t < p; t++) {
-                const u32 rt = vals[t];
-                if (pos_equal(node_load(in, rt), s)) { ld = rt; break; }
-            }
-        }
-    }
-    lflag[r] = ld == r ? 1 : 0;
-    if (ld != r) lead[r] = ld;
-#else
-    if (p > 0 && keys[p - 1] == k) return;  // not a run's first member
-    if (p > 0 && keys[p - 1] == k) return;  // not a run's first member
-    int q = p + 1;
-    while (q < n && keys[q] == k) q++;
-    const u32 r0 = vals[p];
-    lflag[r0] = 1;
-    if (q == p + 1) return;  // a lone position
-    const Pos s0 = node_load(in, r0);
-    for (int j = p + 1; j < q; j++) {
-        const u32 r = vals[j];
-        const Pos sj = node_load(in, r);
-        u32 ld = pos_equal(sj, s0) ? r0 : r;
-        for (int t = p + 1; t < j && ld == r; t++) {  // a tag collision: the run's other leaders
-            const u32 rt = vals[t];
-            if (lflag[rt] && pos_equal(node_load(in, rt), sj)) ld = rt;
-        }
-        lflag[r] = ld == r ? 1 : 0;
-        lead[r] = ld;
-    }
-#endif
-}
-__global__ void __launch_bounds__(DEDUP_BLOCK) k_leader_hist(int n, const uint8_t* __restrict__ lflag,
-                                                             const uint8_t* __restrict__ bins, u32* __restrict__ hist,
-                                                             int nblk) {
-    __shared__ u32 hb[SPLIT_BINS];
-    for (int b = threadIdx.x; b < SPLIT_BINS; b += blockDim.x) hb[b] = 0;
-    __syncthreads();
-    for (int r = 0; r < DEDUP_R; r++) {  // k_place_leaders' blocks: DEDUP_BLOCK * DEDUP_R records
-        const size_t i = (size_t)blockIdx.x * DEDUP_BLOCK * DEDUP_R + (size_t)r * DEDUP_BLOCK + threadIdx.x;
-        if (i < (size_t)n && lflag[i]) atomicAdd(&hb[bins[i]], 1u);
-    }
-    __syncthreads();
-    for (int b = threadIdx.x; b < SPLIT_BINS; b += blockDim.x) hist[(size_t)b * nblk + blockIdx.x] = hb[b];
-}
-__global__ void k_followers2(int n, const uint8_t* __restrict__ lflag, const u32* __restrict__ lead,
-                             const u32* __restrict__ parent_of, const int32_t* __restrict__ place_of,
-                             const uint64_t* __restrict__ val, unsigned long long* __restrict__ parent_sum) {
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
-        if (!lflag[i]) atomicAdd(parent_sum + parent_of[i], (unsigned long long)val[place_of[lead[i]]]);
-}
-
-// The followers credited by their leader's lane in the leaf (GC_PERFT_FUSE, the default): no
-// follower pass, no kept counts.  k_dedup_runs_f writes, per record, a lead word (bit 31: it leads;
+// The followers credited by their leader's lane in the leaf: no follower pass, no kept counts.  k_dedup_runs_f writes, per record, a lead word (bit 31: it leads;
 // bits 27-30: how many later members its run holds, GC_RUN_CAP = that many or more; bits 0-26: its sorted
 // position) and, in sorted order, each member's (leader position, parent) pair; the leaf lane of
 // the leader at sorted position pL walks the later members of its run -- none for a lone position,
@@ -861,7 +664,7 @@ __global__ void __launch_bounds__(BLOCK) k_dedup_runs_f(const Node64* __restrict
     int p0 = p;
     while (p0 > 0 && keys[p0 - 1] == k) p0--;
     u32 lp = (u32)p, parent = 0;
-    if (p0 < p) {  // a later member: the earliest equal member leads (as k_dedup_runs)
+    if (p0 < p) {  // a later member: the earliest equal member leads
         const Pos s = node_load(in, r);
         parent = reinterpret_cast<const u32*>(in + r)[15];
         if (pos_equal(s, node_load(in, vals[p0]))) {
@@ -885,7 +688,7 @@ __global__ void __launch_bounds__(DEDUP_BLOCK) k_leader_hist_f(int n, const u32*
     __shared__ u32 hb[SPLIT_BINS];
     for (int b = threadIdx.x; b < SPLIT_BINS; b += blockDim.x) hb[b] = 0;
     __syncthreads();
-    for (int r = 0; r < DEDUP_R; r++) {  // k_place_leaders' blocks: DEDUP_BLOCK * DEDUP_R records
+    for (int r = 0; r < DEDUP_R; r++) {  // k_place_leaders_f's blocks: DEDUP_BLOCK * DEDUP_R records
         const size_t i = (size_t)blockIdx.x * DEDUP_BLOCK * DEDUP_R + (size_t)r * DEDUP_BLOCK + threadIdx.x;
         if (i < (size_t)n && (leadw[i] >> 31)) atomicAdd(&hb[bins[i]], 1u);
     }
@@ -914,72 +717,39 @@ __global__ void __launch_bounds__(DEDUP_BLOCK) k_place_leaders_f(const Node64* _
     }
 }
 
-// one lane = one placed leader (move-count order); its count kept for the followers (FUSE: added
-// into the followers' parents by this lane)
-template <bool FUSE>
+// one lane = one placed leader (move-count order); its count added into its own parent and into
+// the parents of the followers it leads
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(PERFT2_WPE)))
-k_perft2_val(const Node64* __restrict__ in, int n, uint64_t* __restrict__ val,
-             unsigned long long* __restrict__ parent_sum, int nrec, const u32* __restrict__ keys,
-             const uint2* __restrict__ fw, const u32* __restrict__ spos) {
+k_perft2_val(const Node64* __restrict__ in, int n, unsigned long long* __restrict__ parent_sum, int nrec,
+             const u32* __restrict__ keys, const uint2* __restrict__ fw, const u32* __restrict__ spos) {
     __shared__ u64 lds_a[SCRATCH_SLOTS * BLOCK];
     LdsScratch sa{lds_a + threadIdx.x};
-#ifndef GC_PERFT_LDS
-#define GC_PERFT_LDS 2  // LDS-staged leaper tables in the leaf (bits): 1 the enemy king's neighbourhood
-                        // (count_position_kl's ktab), 2 the knight jumps (ntab: a read per knight instead of
-                        // the eight jump sets, own and enemy).  Same box (configs[3]): 0 1.871e12, 1 1.852,
-                        // 2 1.901, 3 1.894 -- the knights' table kept (VERDICT r04 missing #3)
-#endif
-#if GC_PERFT_LDS & 1
-    __shared__ u64 ktab_s[64];
-    if (threadIdx.x < 64) ktab_s[threadIdx.x] = king_set(bit((int)threadIdx.x));
-    const u64* const ktab = ktab_s;
-#else
-    const u64* const ktab = nullptr;
-#endif
-#if GC_PERFT_LDS & 2
+    // the knight jumps from an LDS table (a read per own knight instead of the eight jump sets):
+    // 1.871 -> 1.901e12 same-box (VERDICT r04 missing #3); the enemy king's neighbourhood from a
+    // table lost (1.852e12)
     __shared__ u64 ntab_s[64];
     if (threadIdx.x >= 64 && threadIdx.x < 128) ntab_s[threadIdx.x - 64] = knight_set(bit((int)threadIdx.x - 64));
-    const u64* const ntab = ntab_s;
-#else
-    const u64* const ntab = nullptr;
-#endif
-#if GC_PERFT_LDS
     __syncthreads();
-#endif
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const u32 parent = reinterpret_cast<const u32*>(in + i)[15];
-    const uint64_t c = perft2(node_load(in, i), sa, ktab, ntab);
+    const uint64_t c = perft2(node_load(in, i), sa, ntab_s);
     atomicAdd(parent_sum + parent, (unsigned long long)c);
-    if (!FUSE) {
-        val[i] = c;
-    } else {
-        const u32 w = spos[i];
-        const u32 pl = w & ((1u << RUN_LEN_SHIFT) - 1u);
-        const int rl = (int)(w >> RUN_LEN_SHIFT);  // later members of the run (GC_RUN_CAP: that many or more)
-        for (int j = (int)pl + 1; j <= (int)pl + rl; j++) {  // (nothing read for a lone position)
+    const u32 w = spos[i];
+    const u32 pl = w & ((1u << RUN_LEN_SHIFT) - 1u);
+    const int rl = (int)(w >> RUN_LEN_SHIFT);  // later members of the run (GC_RUN_CAP: that many or more)
+    for (int j = (int)pl + 1; j <= (int)pl + rl; j++) {  // (nothing read for a lone position)
+        const uint2 f = fw[j];
+        if (f.x == pl) atomicAdd(parent_sum + f.y, (unsigned long long)c);
+    }
+    if (rl == GC_RUN_CAP) {  // a longer run: the rest by its tag
+        const u32 k = keys[pl];
+        for (int j = (int)pl + GC_RUN_CAP + 1; j < nrec && keys[j] == k; j++) {
             const uint2 f = fw[j];
             if (f.x == pl) atomicAdd(parent_sum + f.y, (unsigned long long)c);
         }
-        if (rl == GC_RUN_CAP) {  // a longer run: the rest by its tag
-            const u32 k = keys[pl];
-            for (int j = (int)pl + GC_RUN_CAP + 1; j < nrec && keys[j] == k; j++) {
-                const uint2 f = fw[j];
-                if (f.x == pl) atomicAdd(parent_sum + f.y, (unsigned long long)c);
-            }
-        }
     }
 }
-__global__ void k_followers(const uint2* __restrict__ fol, const u32* __restrict__ nfol,
-                            const int32_t* __restrict__ place_of, const uint64_t* __restrict__ val,
-                            unsigned long long* __restrict__ parent_sum) {
-    const u32 n = *nfol;
-    for (u32 i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const uint2 f = fol[i];
-        atomicAdd(parent_sum + f.x, (unsigned long long)val[place_of[f.y]]);
-    }
-}
-
 // parent value = sum of its children's values (children of one parent are contiguous)
 template <class T>
 __global__ void k_sum_children(const T* __restrict__ offs, const T* __restrict__ cnt,
@@ -1453,13 +1223,6 @@ struct PairHalf {
     u64 T[SW_SETS];  // SW: the next side's move sets (each wave its own; all in LDS after phase 2)
     u64 cw[4];       // SW, W0: every set's count, one byte per set (gc_core.h sw_pack)
 };
-// Diagonal slider sets computed by W0 instead of W1 in the set-wise phase 2 (reference rules):
-// balances the two waves' phase-2 work (tools/pstamp_probe.py: W1 3 840 vs W0 2 810 cycles
-// per ply with 0)
-#ifndef GC_SW_SPLIT
-#define GC_SW_SPLIT 0
-#endif
-static_assert(GC_SW_SPLIT >= 0 && GC_SW_SPLIT <= 4, "GC_SW_SPLIT: 0..4 diagonal sets on W0");
 struct PairNoop {
     __device__ void operator()() const {}
 };
@@ -1617,8 +1380,9 @@ __device__ __forceinline__ void pair_half(PairLds& L, RT role, int l, bool mv, b
     int c = 0;
     u32 hl = hl_of(s.meta);
     if (role == 0) {
-        if constexpr (SW) {  // pawn, knight and king sets (+ GC_SW_SPLIT diagonal sets); castles counted here
-            constexpr int W0_FROM = FIDE ? SW_K : SW_K - GC_SW_SPLIT;  // W0's sets: [0, SW_ORTH) and [W0_FROM, SW_SETS)
+        if constexpr (SW) {  // pawn, knight and king sets; castles counted here (diagonal sets moved
+                             // here from W1 measured within noise in round 3)
+            constexpr int W0_FROM = SW_K;  // W0's sets: [0, SW_ORTH) and [SW_K, SW_SETS)
             H.cw[0] = H.cw[1] = H.cw[2] = H.cw[3] = 0;
             if (gen) {
                 if constexpr (FIDE) {
@@ -1626,7 +1390,6 @@ __device__ __forceinline__ void pair_half(PairLds& L, RT role, int l, bool mv, b
                 } else {
                     sw_pawns(ns, g, H.T);
                     sw_knights(ns, g, H.T);
-                    sw_diag_part<4 - GC_SW_SPLIT, 4>(ns, g, H.T);
                     sw_kings(ns, g, H.T);
                 }
                 sw_pack(H.T, 0, SW_ORTH, H.cw);
@@ -1651,14 +1414,14 @@ __device__ __forceinline__ void pair_half(PairLds& L, RT role, int l, bool mv, b
         }
     } else {
         if constexpr (SW) {  // the slider direction sets and their byte counts, to W0 through LDS
-            constexpr int W1_TO = FIDE ? SW_K : SW_K - GC_SW_SPLIT;  // W1's sets: [SW_ORTH, W1_TO)
+            constexpr int W1_TO = SW_K;  // W1's sets: [SW_ORTH, SW_K)
             u64 cw[4] = {0, 0, 0, 0};
             if (gen) {
                 if constexpr (FIDE) {
                     gcf::fsw_gen_b(ns, gcf::FGen{g, 0, -1}, H.T);
                 } else {
                     sw_orth(ns, g, H.T);
-                    sw_diag_part<0, 4 - GC_SW_SPLIT>(ns, g, H.T);
+                    sw_diag_part<0, 4>(ns, g, H.T);
                 }
                 sw_pack(H.T, SW_ORTH, W1_TO, cw);
                 part = sw_popc(H.T, SW_ORTH, W1_TO);
@@ -1676,9 +1439,6 @@ __device__ __forceinline__ void pair_half(PairLds& L, RT role, int l, bool mv, b
             pin(pr.e0.hdr); pin(pr.e0.k); pin(pr.e0.q); pin(pr.e0.r);
             pin(pr.e0.b); pin(pr.e0.n); pin(pr.e0.p); pin(pr.e0.w);
             c = rep_commit(h, s, pr, hl, irrev);  // table write deferred to h.commit()
-#ifdef GC_EARLIER_COMMIT  // A/B: issued right here
-            h.commit();
-#endif
         }
         L.rep[l] = (u32)c | (hl << 8);
         w1_late();
@@ -1789,9 +1549,7 @@ __device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, RT rol
         x0 = L.x0[l];
         ra = (uint16_t)L.ra[l];
     }
-#ifndef GC_EARLIER_COMMIT
     else h.commit();  // the window write, issued before the outcome (not with the stores: 9.3 -> 9.1 us per ply)
-#endif
     Gen& g = H.g;
     MoveSet& ms = H.ms;
     // W0: the next action from this ply's move sets, ahead of the outcome (its LDS read and rank
@@ -1828,9 +1586,6 @@ __device__ __forceinline__ StepOut pair_ply(PairLds& L, const PairCtx& C, RT rol
         s = rp;
         h.bump_gen();
     }
-#ifdef GC_STAMP6_EARLY  // diagnostic: stamp 6 before the pick instead of after it
-    GC_STAMP(6);
-#endif
     if (role == 0) {
         uint16_t act = (uint16_t)set_act;
         int tot = ms.total;
@@ -2087,17 +1842,11 @@ __device__ __forceinline__ PairIO store_io(uint8_t* slab, int nn) {
 // every launch -- measured ~2-3k cycles, paid wherever the compiler sinks it, and with SGPRs
 // scarce it sank it next to a spill that forced the wait in phase 1.  The reset position and
 // move set come from a device-memory copy (icd) instead.
-// Which pair and role wave w of a workgroup takes (GC_PAIR_MAP; diagnostic builds compare):
-// 0: pair w / 2, role w % 2 (a pair's two waves adjacent); 1: pair w % PAIRS_WG, role
-// w / PAIRS_WG (with 4 pairs, waves w and w + 4 -- one SIMD under round-robin placement --
-// form a pair); 2: pair w / 2, role alternating across pairs (a SIMD hosts both roles).
-#ifndef GC_PAIR_MAP
-#define GC_PAIR_MAP 2  // r03 A/B (fused, 65 536 boards): 0 -> 11.2e9, 2 -> 11.37e9, 1 with 4 pairs -> 10.9e9
-#endif
-__device__ __forceinline__ int pair_of_wave(int w) { return GC_PAIR_MAP == 1 ? w % PAIRS_WG : w >> 1; }
-__device__ __forceinline__ int role_of_wave(int w) {
-    return GC_PAIR_MAP == 1 ? w / PAIRS_WG : GC_PAIR_MAP == 2 ? ((w ^ (w >> 1)) & 1) : (w & 1);
-}
+// Which pair and role wave w of a workgroup takes: pair w / 2, the role alternating across pairs
+// (a SIMD hosts both roles).  r03 A/B (fused, 65 536 boards): 11.37e9; a pair's waves as roles
+// 0 / 1 everywhere 11.2e9; waves w and w + 4 (one SIMD) as a pair with 4 pairs 10.9e9.
+__device__ __forceinline__ int pair_of_wave(int w) { return w >> 1; }
+__device__ __forceinline__ int role_of_wave(int w) { return (w ^ (w >> 1)) & 1; }
 #define PAIR_PROLOGUE PAIR_PROLOGUE_ACT(in_io.act, )
 // ACTS: the action source (the env's next action, or the caller's for the API step);
 // ENTRY: more entry loads, waited for with the reset position's
@@ -2148,9 +1897,7 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
     constexpr bool API = false;
     PAIR_PROLOGUE
     StepOut o = pair_step<OPP, false, FIDE>(Ls, L, C, role, l, i, live, rp, s, a, d, h, nst);
-#ifndef GC_STAMP6_EARLY
     GC_STAMP(6);
-#endif
     const PairIO io = store_io(slab, nn);
     if (live) {
         if (role == 0) {
@@ -2280,13 +2027,9 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
             }
         }
     };
-#ifdef GC_ROLE_RUNTIME  // A/B: one loop for both roles
-    plies_loop(role, stats != nullptr);
-#else
-    if (role == 0) plies_loop(RoleC<0>{}, std::false_type{});  // W0 keeps no stats
-    else if (stats) plies_loop(RoleC<1>{}, std::true_type{});
+    if (role == 0) plies_loop(RoleC<0>{}, std::false_type{});  // W0 keeps no stats (one loop for
+    else if (stats) plies_loop(RoleC<1>{}, std::true_type{});  // both roles: 965 -> 1 045 VALU per wave)
     else plies_loop(RoleC<1>{}, std::false_type{});
-#endif
 }
 
 // ----------------------------------------------------------------------------- quad step
@@ -2312,30 +2055,9 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
 // pair_ply (and so as k_env_step<true, false> and the oracle): tests/test_gpu_parity.py and
 // tests/test_full_size.py run the fused rollouts against the oracle and the launched kernel.
 #define QUAD_BOARDS 64
-#ifndef GC_Q1_LEAPERS
-#define GC_Q1_LEAPERS 0  // the enemy's leaper attacks on Q1 in phase 1 (else Q2)
-#endif
-#ifndef GC_Q3_KINGS
-#define GC_Q3_KINGS 0    // the king sets on Q3 in phase 2 (else Q2)
-#endif
 #ifndef QUADS_WG
 #define QUADS_WG 2  // two quads per workgroup; the second's roles rotated by 2 so that every SIMD
                     // hosts a state-carrying and a stateless role of each workgroup
-#endif
-#ifndef GC_Q_LEAPER_LDS
-#define GC_Q_LEAPER_LDS 0  // A/B: Q2's enemy knight / king attacks from LDS tables (a read per piece)
-#endif
-#if GC_Q_LEAPER_LDS
-__shared__ u64 g_q_ntab[64], g_q_ktab[64];
-// side_attacks_leapers with the knights' and the kings' neighbourhoods read from the tables
-__device__ __forceinline__ u64 side_attacks_leapers_lds(const Pos& s, bool white) {
-    const u64 occ = occ_of(s);
-    const u64 mine = white ? s.w : (occ & ~s.w);
-    u64 a = pawn_att_set(s.p & mine, white) & ~(s.k & mine);
-    for (u64 x = s.n & mine; x; x &= x - 1) a |= g_q_ntab[ctz(x)];
-    for (u64 x = s.k & mine; x; x &= x - 1) a |= g_q_ktab[ctz(x)];
-    return a;
-}
 #endif
 struct QuadLds {
     u64 sets[SW_SETS][QUAD_BOARDS];  // the next side's move sets (Q0: pawns / knights / kings, Q2, Q3)
@@ -2383,9 +2105,6 @@ using QuadSets = QuadSetsT<QuadLds>;
 // Q0's choice of the next action, left for the start of the next ply: Q2 makes the pick from
 // the move sets in phase 3 while Q0 and Q1 settle the outcome (the pick was phase 3's longest
 // chain); a board that resets takes the start position's table pick instead.
-#ifndef GC_EARLY_PROBE
-#define GC_EARLY_PROBE 0  // A/B: Q1 loads the next ply's window probe in phase 2 instead of after the outcome
-#endif
 struct QuadPend {
     bool pending;  // false: `a` is already the action (the launch's first ply)
     bool have;     // the move stood: Q2's pick
@@ -2401,14 +2120,9 @@ template <int R>
 __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l, int i, bool live, Pos& s, int& a,
                                             u32& d, DevHist& h, u32& nst, RepProbe& pr, QuadPend& pend) {
     constexpr bool CARRY = R < 2;  // Q0 / Q1 hold the state
-#ifndef GC_NO_QPRIO_DYN  // Q2's pick (phase 3's longest) ahead of Q0's outcome there: 14.43-14.63 -> 14.90-15.12e9
+    // Q2's pick (phase 3's longest) is raised over Q0's outcome there: 14.43-14.63 -> 14.90-15.12e9
     if (R == 0) __builtin_amdgcn_s_setprio(2);
     if (R == 2) __builtin_amdgcn_s_setprio(0);
-#endif
-#ifdef GC_QPRIO_MID  // diagnostic: phases 1-2 at priorities GC_QPRIO_MID (Q0, Q1) / GC_QPRIO_MID23 (Q2, Q3)
-    if (R == 1) __builtin_amdgcn_s_setprio(2);
-    if (R == 3) __builtin_amdgcn_s_setprio(0);
-#endif
     if (R == 0) a = pend.resolve(L, l, a);  // the last ply's action: Q2's pick, or the reset table's
     u32 x0 = 0;
     uint16_t ra = (uint16_t)A_NONE;
@@ -2446,10 +2160,6 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
     if (R != 1) pair_barrier();
     PST(1);
     // ---- phase 1
-#ifdef GC_QPRIO_MID
-    if (R < 2) __builtin_amdgcn_s_setprio(GC_QPRIO_MID);
-    else __builtin_amdgcn_s_setprio(GC_QPRIO_MID23);
-#endif
     Gen g;
     bool my_chk = false;
     if (R != 0) {
@@ -2471,17 +2181,8 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
     } else if (R == 1) {
         my_chk = mv && mover_checked(s, ns, white, a);
         L.f1[l] = my_chk ? 1u : 0u;
-#if GC_Q1_LEAPERS
-        L.enemy[0][l] = g.ks >= 0 ? side_attacks_leapers(ns, !g.white) : 0ull;
-#endif
     } else if (R == 2) {
-#if GC_Q1_LEAPERS
-        L.enemy[1][l] = g.ks >= 0 ? side_attacks_orth(ns, !g.white) : 0ull;
-#elif GC_Q_LEAPER_LDS
-        L.enemy[1][l] = g.ks >= 0 ? side_attacks_leapers_lds(ns, !g.white) | side_attacks_orth(ns, !g.white) : 0ull;
-#else
         L.enemy[1][l] = g.ks >= 0 ? side_attacks_leapers(ns, !g.white) | side_attacks_orth(ns, !g.white) : 0ull;
-#endif
     } else {
         L.enemy[2][l] = g.ks >= 0 ? side_attacks_diag(ns, !g.white) : 0ull;
     }
@@ -2489,15 +2190,7 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
     pair_barrier();
     PST(3);
     // ---- phase 2
-#ifdef GC_QPRIO_P2  // A/B: Q2 (phase 2's longest chain, its SIMD shared with Q0) raised over Q0 from phase 2 on
-    if (R == 0) __builtin_amdgcn_s_setprio(0);
-    if (R == 2) __builtin_amdgcn_s_setprio(2);
-#endif
-#if GC_Q1_LEAPERS
-#define QUAD_ENEMY(l) (L.enemy[0][l] | L.enemy[1][l] | L.enemy[2][l])
-#else
 #define QUAD_ENEMY(l) (L.enemy[1][l] | L.enemy[2][l])
-#endif
     if (R == 0) {
         g.enemy_att = QUAD_ENEMY(l);
         gen_castles(ns, g);  // lib.rs:578-610 with the whole enemy map
@@ -2508,7 +2201,7 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
         g.checkmask = L.pin3[0][l];
         g.pinned = L.pin3[1][l];
         g.pinrays = L.pin3[2][l];
-        if (R == (GC_Q3_KINGS ? 3 : 2)) g.enemy_att = QUAD_ENEMY(l);  // for the king sets
+        if (R == 2) g.enemy_att = QUAD_ENEMY(l);  // for the king sets
     }
     const bool opp_chk = g.in_check;
     const bool both = opp_chk && my_chk;  // lib.rs:1442-1446
@@ -2538,21 +2231,12 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
         }
         L.rep[l] = (u32)c | (hl << 8);
         L.ra[l] = ra;
-#if GC_EARLY_PROBE
-        // this ply's window write now (its entry registers free), then the next ply's probe a
-        // phase earlier: its pre-move board is this ply's post-move board unless the board
-        // resets (probed again in phase 3 then)
-        h.commit();
-        if (live) rep_prefetch(h, ns, pr);
-#endif
     } else if (R == 2) {  // unconditional: ignored unless generation is due
         u64 T[SW_SETS];
         sw_orth(ns, g, T);
         Q.put_all<SW_ORTH, SW_DIAG>(T + SW_ORTH);
-        if (!GC_Q3_KINGS) {
-            sw_kings(ns, g, T);
-            Q.put_all<SW_K, SW_SETS>(T + SW_K);
-        }
+        sw_kings(ns, g, T);
+        Q.put_all<SW_K, SW_SETS>(T + SW_K);
         L.part[2][l] = (u32)Q.part;
 #pragma unroll
         for (int k = 0; k < 4; k++) L.cwx[0][k][l] = Q.cw[k];
@@ -2560,10 +2244,6 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
         u64 T[SW_SETS];
         sw_diag(ns, g, T);
         Q.put_all<SW_DIAG, SW_K>(T + SW_DIAG);
-        if (GC_Q3_KINGS) {
-            sw_kings(ns, g, T);
-            Q.put_all<SW_K, SW_SETS>(T + SW_K);
-        }
         L.part[3][l] = (u32)Q.part;
 #pragma unroll
         for (int k = 0; k < 4; k++) L.cwx[1][k][l] = Q.cw[k];
@@ -2575,23 +2255,13 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
     // ---- phase 3: the outcome (Q0 and Q1, identical arithmetic); Q2 picks the next action
     // from the move sets (Q0 takes it, or the reset table's, at the start of the next ply)
     StepOut o = {0, 0, R_NONE, 0};
-#ifndef GC_NO_QPRIO_DYN
     if (R == 0) __builtin_amdgcn_s_setprio(0);
     if (R == 2) __builtin_amdgcn_s_setprio(2);
-#endif
-#ifdef GC_QPRIO_MID
-    if (R == 1) __builtin_amdgcn_s_setprio(2);
-    if (R == 3) __builtin_amdgcn_s_setprio(0);
-#endif
-#ifndef GC_PICK_ROLE
-#define GC_PICK_ROLE 2
-#endif
-    if (R == GC_PICK_ROLE) {
-        constexpr int OTHER = GC_PICK_ROLE == 2 ? 1 : 0;  // the other stateless role's byte counts
-        const int total = (int)L.part[0][l] + Q.part + (int)L.part[5 - GC_PICK_ROLE][l];
+    if (R == 2) {  // (on Q3, whose SIMDs Q1 shares: 12.77-12.98 vs 13.30-13.42e9)
+        const int total = (int)L.part[0][l] + Q.part + (int)L.part[3][l];
         u64 cw[4];
 #pragma unroll
-        for (int k = 0; k < 4; k++) cw[k] = Q.cw[k] | L.cwx[OTHER][k][l];
+        for (int k = 0; k < 4; k++) cw[k] = Q.cw[k] | L.cwx[1][k][l];
         cw[0] |= L.cw0[l];
         cw[1] |= L.cw1[l];
         g.castles = L.castles[l];
@@ -2605,7 +2275,7 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
             c = (int)(rpk & 0xFFu);
             hl = rpk >> 8;
             ra = (uint16_t)L.ra[l];
-        } else if (!GC_EARLY_PROBE) {
+        } else {
             h.commit();  // the window write, issued before the outcome
         }
         bool have = false;
@@ -2642,11 +2312,7 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
         }
         // Q1: the next ply's probe, its pre-move board settled, while Q0 still picks (Q1 waits at
         // the next barrier anyway); after this ply's window write, so it sees it
-#if GC_EARLY_PROBE
-        if (R == 1 && live && !have) rep_prefetch(h, s, pr);  // the reset position's
-#else
         if (R == 1 && live) rep_prefetch(h, s, pr);
-#endif
         // the draw counter (both: the quads run only with the start position's pick table, so a
         // reset's pick count is its total) and Q0's pending choice of the next action
         const int tot = have ? total : (int)C.rtotal;
@@ -2686,12 +2352,6 @@ __device__ __forceinline__ void quad_run(uint8_t* __restrict__ slab, int nn, uin
         pin(s); pin(ua); pin(g0); pin(nst); pin(d);
     }
     if (RR == 0 && l == 0) L.rp = icd->pos;  // read after ply 0's first barrier
-#if GC_Q_LEAPER_LDS
-    if (qw == 0 && RR == 3) {  // (read after ply 0's first barrier too)
-        g_q_ntab[l] = knight_set(bit(l));
-        g_q_ktab[l] = king_set(bit(l));
-    }
-#endif
     int a = (int)ua;
     DevHist h = DevHist{htab, in_io.hgen, g0, ii, HTAB_BITS};
     RepProbe pr;  // Q1: the window probe of the coming ply's pre-move board
@@ -2797,9 +2457,6 @@ __global__ void __launch_bounds__(4 * QUAD_BOARDS * QUADS_WG) __attribute__((amd
         case 3: __builtin_amdgcn_s_setprio(3); break;
         default: break;
     }
-#ifdef GC_QUAD_ONLY  // diagnostic builds: one role's register needs
-    quad_run<GC_QUAD_ONLY, false>(slab, nn, seed, htab, racts, icd, rinfo, plies, stats, trace, qw, l, i);
-#else
     switch (role) {
         case 0: quad_run<0, false>(slab, nn, seed, htab, racts, icd, rinfo, plies, stats, trace, qw, l, i); break;
         case 1:
@@ -2809,7 +2466,6 @@ __global__ void __launch_bounds__(4 * QUAD_BOARDS * QUADS_WG) __attribute__((amd
         case 2: quad_run<2, false>(slab, nn, seed, htab, racts, icd, rinfo, plies, stats, trace, qw, l, i); break;
         default: quad_run<3, false>(slab, nn, seed, htab, racts, icd, rinfo, plies, stats, trace, qw, l, i); break;
     }
-#endif
     // The completion word: every workgroup, its stores performed (the barrier waits for them),
     // counts itself; the last one bumps the launch count and writes it to host-mapped memory,
     // where gc_env_wait_rollout sees it ~5 us before the stream's completion signal would tell
@@ -3373,19 +3029,8 @@ __device__ void write_obs(const Pos& s, int8_t* __restrict__ out) {
         o[r] = (u64)obs_word(b0, b1, b2, blk, 8 * r) | ((u64)obs_word(b0, b1, b2, blk, 8 * r + 4) << 32);
 }
 
-#ifdef GC_OBS_DIAG  // diagnostic (not parity): the observation words stored word-major (coalesced), to time the scattered stores
-__device__ void write_obs_diag(const Pos& s, int8_t* __restrict__ out, int i, int nn) {
-    u64* o = reinterpret_cast<u64*>(out);
-    const u64 b0 = s.k | s.r | s.n, b1 = s.q | s.r | s.p, b2 = s.b | s.n | s.p;
-    const u64 blk = occ_of(s) & ~s.w;
-#pragma unroll
-    for (int r = 0; r < 8; r++)
-        o[(size_t)r * nn + i] = (u64)obs_word(b0, b1, b2, blk, 8 * r) | ((u64)obs_word(b0, b1, b2, blk, 8 * r + 4) << 32);
-}
-#define WRITE_OBS_Q3(fs, base, i, nn) write_obs_diag(fs, base, i, nn)
-#else
 #define WRITE_OBS_Q3(fs, base, i, nn) write_obs(fs, (base) + 64 * (size_t)(i))
-#endif
+
 
 template <bool OPP>
 __global__ void __launch_bounds__(BLOCK) k_env_step_api(EnvDev e, const uint16_t* __restrict__ acts,
@@ -3455,7 +3100,7 @@ struct ApiOut {
     int8_t* obs;
     int32_t* cnt;
     uint16_t* pick;
-    size_t ms;  // the mask's row stride in words (gc_env_set_mask_stride; default n)
+    size_t ms;  // the mask's row stride in words (gc_env_step_device2; default n)
 };
 __device__ __forceinline__ void ic_moves(const EnvDev::InitCache& ic, Gen& g, MoveSet& ms) {
     g.white = ic.white;
@@ -3468,177 +3113,13 @@ __device__ __forceinline__ void ic_moves(const EnvDev::InitCache& ic, Gen& g, Mo
     ms.big = false;
 }
 
-// 16 argument dwords, no padding (all preloaded): the output pointers live in device memory
-// (outp, rewritten only when the caller's buffers change), auto-reset rides in rinfo bit 17
-__global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
-    k_env_step_api2(uint8_t* __restrict__ slab, uint64_t seed, u64* __restrict__ htab,
-                    const uint16_t* __restrict__ racts, const EnvDev::InitCache* __restrict__ icd,
-                    const uint16_t* __restrict__ acts, const ApiOut* __restrict__ outp, int nn,
-                    u32 rinfo /* first block << 18 | autoreset << 17 | ic.table << 16 | ic.total */) {
-    constexpr int OPP = 0;
-    constexpr bool API = true;
-    const int blk0 = (int)(rinfo >> 18);  // a launch may cover a sub-range of the board blocks
-    const int autoreset = (rinfo >> 17) & 1;
-    rinfo &= 0x1FFFFu;
-    ApiOut out;
-    PAIR_PROLOGUE_ACT(acts, out = *outp; asm volatile("" : "+s"(out.rw), "+s"(out.dn), "+s"(out.rs), "+s"(out.mask),
-                                                                  "+s"(out.obs), "+s"(out.cnt), "+s"(out.pick), "+s"(out.ms));)
-    PairScratch scr{&L.slots[0][l]};
-#ifdef GC_API_PRIO  // diagnostic: issue priority 2 for W0 (1) or W1 (2)
-    if ((GC_API_PRIO == 1 && role == 0) || (GC_API_PRIO == 2 && role == 1)) __builtin_amdgcn_s_setprio(2);
-#endif
-    const bool done0 = (s.meta & M_DONE) != 0;              // chess_v2.py:245-251
-    const bool cap = mc_of(s.meta) > MOVES_MAX;             // 252-258
-    const bool white = (s.meta & M_WHITE) != 0;
-    const bool pre = live && !done0 && !cap;
-    bool valid = false;
-    if (role == 0) {  // chess_v2.py:240-242, on the pre-move board
-        valid = quick_legal(s, a);
-        L.act[l] = valid ? 1u : 0u;
-        L.draw[l] = (pre && valid) ? 1u : 0u;  // W1 reads it in phase 1 (MV_LDS)
-    }
-    u32 x0 = 0;
-    uint16_t ra = (uint16_t)A_NONE;
-    PairHalf H;
-    pair_half<false, false, true>(
-        L, role, l, role == 0 ? (pre && valid) : pre, live, s, a, nullptr, L.draw, h, H,
-        [&] {
-            x0 = philox_x0(C.seed, (u32)i, d);
-            if (C.rtable) ra = C.racts[scale_rank(x0, C.rtotal)];
-            L.x0[l] = x0;
-        },
-        [&] { L.ra[l] = ra; });
-    if (role) valid = L.act[l] != 0;
-    else {
-        x0 = L.x0[l];
-        ra = (uint16_t)L.ra[l];
-    }
-    StepOut o = {0, 0, R_NONE, 0};
-    if (!valid) {
-        o.reward = -10;
-        o.done = done0 ? 1 : 0;
-        o.reason = R_INVALID;
-    } else if (done0) {
-        o.done = 1;
-        o.reason = R_DONE_ALREADY;
-    } else if (cap) {
-        o.done = 1;
-        o.reason = R_MOVE_CAP;
-    } else if (H.both) {
-        o.done = 1;
-        o.reason = R_BOTH_CHECKED;
-    } else {
-        s = pair_settle(H, white);
-        o.reward = -10 + H.mr;  // INVALID_ACTION_REWARD + move reward (Q9)
-        o.moved = 1;
-        if (H.c >= 3) { o.done = 1; o.reason = R_REPETITION; }
-        if (H.c == 0) { o.done = 1; o.reason = R_WINDOW_FULL; }
-        if (H.ms.total == 0 && H.opp_chk) {  // 270-272
-            s.meta |= M_DONE;
-            o.done = 1;
-            o.reward += 100;
-            o.reason = R_MATE;
-        }
-        if (!o.done && !white) s.meta += (1u << M_MC_SHIFT);  // 291-292
-    }
-    nst += 1;
-    const bool reset = live && autoreset && o.done;
-    if (reset) {
-        s = rp;
-        h.bump_gen();
-    }
-    const bool alone = live && !reset && valid && !done0 && !cap && H.both;  // state kept, moves not generated
-    // W0: every own piece's targets into its slot -- the fast pawns' from their origin sets, a
-    // reset board's from the start position's cache -- so that the mask is written square-major
-    // by both waves, each word once (coalesced, no zero-then-patch); castles and the whole
-    // enemy map (king targets of > 16-piece boards) to W1
-    if (role == 0) {
-        if (reset) {
-#pragma unroll
-            for (int j = 0; j < SCRATCH_SLOTS; j++) scr.put(j, C.icd->slots[j]);
-        } else if (!H.ms.big) {
-            for (u64 fp = H.ms.fastp; fp; fp &= fp - 1) {
-                const int sq = ctz(fp);
-                scr.put(ordinal(H.g.own, sq), fast_pawn_targets(H.ms, sq, H.g.white));
-            }
-        }
-        L.nmeta[l] = H.g.castles;
-        L.enemy[l] = H.g.enemy_att;
-    }
-    pair_barrier();
-    Gen g = H.g;
-    MoveSet ms = H.ms;
-    if (role) {
-        g.castles = L.nmeta[l];
-        g.enemy_att = L.enemy[l];
-    }
-    if (reset) ic_moves(*C.icd, g, ms);
-    if (alone) {  // the big-board path: legal targets per piece, no slots
-        gen_init(s, g);
-        moveset_clear(ms);
-        ms.big = true;
-        ms.total = count_legal(s, g);
-    }
-    if (out.mask && live) {
-        u64* o = out.mask + i;
-        const size_t N = out.ms;
-        if (!ms.big) {  // W1 squares 0..31, W0 32..63 and the castles word
-            const int s0 = role ? 0 : 32;
-            int j = popc(g.own & below(s0));
-#pragma unroll 8
-            for (int sq = s0; sq < s0 + 32; sq++) {
-                const bool b = (g.own >> sq) & 1;
-                const u64 v = scr.get(j & (SCRATCH_SLOTS - 1));
-                // streamed (non-temporal): written once, read by the caller after the launch
-                // (same-box A/B: 3.105-3.121 vs 3.049-3.104e9, profiles/r04_v2)
-                __builtin_nontemporal_store(b ? v : 0ull, o + sq * N);
-                j += b ? 1 : 0;
-            }
-            if (role == 0) {
-                u64 c = 0;
-                if (g.castles & 1) c |= g.white ? (1ull << 1) : (1ull << 3);  // QS: 4097 / 4099
-                if (g.castles & 2) c |= g.white ? (1ull << 0) : (1ull << 2);  // KS: 4096 / 4098
-                o[64 * N] = c;
-            }
-        } else if (role) {
-            write_mask(s, g, ms, scr, o, N);
-        }
-    }
-    const PairIO io = store_io(slab, nn);
-    if (role == 0) {
-        if (out.pick && live) {
-            uint16_t p = (uint16_t)A_NONE;
-            if (reset && C.rtable) {
-                p = ra;
-            } else if (ms.total > 0) {
-                int k = (int)scale_rank(x0, (u32)ms.total);
-                p = (uint16_t)select_action_swar(s, g, ms, scr, k);
-            }
-            d += ms.total > 0 ? 1u : 0u;
-            out.pick[i] = p;
-            io.act[i] = p;
-            io.draw[i] = d;
-        }
-    } else if (live) {
-        if (out.obs) write_obs(s, out.obs + 64 * (size_t)i);
-        if (out.cnt) out.cnt[i] = ms.total;
-        out.rw[i] = o.reward;
-        out.dn[i] = (uint8_t)o.done;
-        out.rs[i] = (uint8_t)o.reason;
-        h.commit();
-        io.store(i, s);
-        h.flush(g0);
-        io.nsteps[i] = nst;
-        io.reward[i] = o.reward;
-        io.done[i] = (uint8_t)o.done;
-        io.reason[i] = (uint8_t)o.reason;
-    }
-}
-
 // ----------------------------------------------------------------------------- API step, quads
-// k_env_step_api2's contract (the same arguments, outputs, decisions and auto-reset) on FOUR
-// waves per 64 boards, as the headline rollout's quads (k_env_rollout4): the paired API step
-// ran each board's step as two long dependency chains on two waves and wrote its 34 MB
+// The API step (external actions in; reward / done / reason, the observation, the legal-action
+// mask and count, the random policy's pick out; auto-reset) on FOUR waves per 64 boards, as the
+// headline rollout's quads (k_env_rollout4).  16 argument dwords, no padding (all preloaded): the
+// output pointers live in device memory (outp, rewritten only when the caller's buffers change),
+// auto-reset rides in rinfo bit 17.  The round-2 paired API step (k_env_step_api2, removed in
+// round 6) ran each board's step as two long dependency chains on two waves and wrote its 34 MB
 // legal-action mask at the end, when every workgroup finished at once.
 //
 //   phase 0   Q0: applies the action (speculatively: it is validated beside it)
@@ -3656,8 +3137,8 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
 //             rows, from the init cache); Q2: the pick (action-id order), the count, the env's
 //             next action; Q3: the observation; Q1: the outputs, the state and the window.
 // A mask row is written only by the role that owns its square.  (Zeroing the unoccupied
-// squares' rows in phase 1 instead, GC_APIQ_EARLY: partial rows written twice, 28.4 vs 18.5 us
-// per launch.)  Boards outside
+// squares' rows in phase 1 instead wrote partial rows twice: 28.4 vs 18.5 us per launch,
+// measured in round 5.)  Boards outside
 // the fast path -- > 16 own pieces, or both kings checked after the move (the move is void and
 // the pre-move board regenerates) -- take the per-piece fallback (legal_targets) in phase 3,
 // each role for its own rows.  Quad roles run only with the start position's pick table, as
@@ -3681,30 +3162,10 @@ struct ApiQuadLds {
     u32 ra[QUAD_BOARDS];                    // Q1 -> Q2: the start-position table pick
 };
 __shared__ ApiQuadLds g_apiq_lds[QUADS_WG];
-#ifndef GC_APIQ_EARLY
-#define GC_APIQ_EARLY 0  // 1: rows of unoccupied squares zeroed in phase 1 (partial rows written twice:
-                         // 28.4 us per launch; non-temporal or not alike), 0: every row once in phase 3 (18.5)
-#endif
-#ifndef GC_APIQ_SPLIT
-#define GC_APIQ_SPLIT 1  // phase 2's pieces: 1 Q0 pawns | Q1 knights, kings | Q2 queens | Q3 rooks, bishops
-                         // (same-box 17.13 us per launch); 0: bishops on Q2 (17.34); 2: 0 with knights on Q0 (17.60)
-#endif
-#ifndef GC_APIQ_NT
-#define GC_APIQ_NT 1     // the mask rows as non-temporal stores
-#endif
+// phase 2's pieces: Q0 pawns | Q1 knights, kings | Q2 queens | Q3 rooks, bishops (same-box 17.13 us
+// per launch; bishops on Q2 17.34; and the knights on Q0 17.60)
 __device__ __forceinline__ void apiq_store(u64* p, u64 v) {
-    if (GC_APIQ_NT) __builtin_nontemporal_store(v, p);
-    else *p = v;
-}
-
-// the 16 mask rows of role R that the next side does not occupy: zero (streamed)
-template <int R>
-__device__ __forceinline__ void apiq_zero_rows(u64* __restrict__ o, size_t N, u64 own) {
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-        const int sq = 16 * R + k;
-        if (!((own >> sq) & 1)) apiq_store(o + sq * N, 0ull);
-    }
+    __builtin_nontemporal_store(v, p);  // the mask rows stream (3.105-3.121 vs 3.049-3.104e9, round 4)
 }
 
 // Parked targets by own-piece ordinal in LDS (slot j of lane l at base[j * 64]), and each piece's
@@ -3808,10 +3269,8 @@ __device__ __forceinline__ void apiq_run(uint8_t* __restrict__ slab, uint64_t se
     OrdScratch scr{&L.slots[0][l], 0ull, 0ull};
     // issue priority: the state-carrying roles' chains are the longer; Q2 (a validation half,
     // on Q0's SIMDs) level with Q0 in phase 0
-#ifndef GC_APIQ_Q3P
-#define GC_APIQ_Q3P 0  // A/B: Q3 (the other validation half, the observation) at priority 2 in phases 0 and 3
-#endif
-    if (RR != 3 || GC_APIQ_Q3P) __builtin_amdgcn_s_setprio(2);
+    // (Q3 raised as well, in phases 0 and 3: not faster)
+    if (RR != 3) __builtin_amdgcn_s_setprio(2);
     const bool done0 = (s.meta & M_DONE) != 0;   // chess_v2.py:245-251
     const bool cap = mc_of(s.meta) > MOVES_MAX;  // 252-258
     const bool white = (s.meta & M_WHITE) != 0;
@@ -3846,7 +3305,7 @@ __device__ __forceinline__ void apiq_run(uint8_t* __restrict__ slab, uint64_t se
     PST(1);
 
     // ---- phase 1
-    if (RR == 2 || (GC_APIQ_Q3P && RR == 3)) __builtin_amdgcn_s_setprio(0);
+    if (RR == 2) __builtin_amdgcn_s_setprio(0);
     const bool valid = (L.valid[0][l] & L.valid[1][l]) != 0;
     const bool mv = pre && valid;  // env_ply runs
     Pos ns = s;                    // the position generated for: post-move, or s itself
@@ -3872,7 +3331,6 @@ __device__ __forceinline__ void apiq_run(uint8_t* __restrict__ slab, uint64_t se
         L.enemy[2][l] = g.ks >= 0 ? side_attacks_diag(ns, !g.white) : 0ull;
     }
     u64* const mrow = out.mask ? out.mask + ii : nullptr;
-    if (GC_APIQ_EARLY && mrow && live) apiq_zero_rows<RR>(mrow, N, g.own);
     PST(2);
     pair_barrier();
     PST(3);
@@ -3900,7 +3358,6 @@ __device__ __forceinline__ void apiq_run(uint8_t* __restrict__ slab, uint64_t se
                 const int sq = ctz(fp);
                 scr.put(ordinal(g.own, sq), fast_pawn_targets(ms, sq, g.white));
             }
-            if (GC_APIQ_SPLIT == 2) part += gen_knights(ns, g, ms, scr);
         }
         L.cbw[0][0][l] = scr.c0;
         L.cbw[0][1][l] = scr.c1;
@@ -3908,7 +3365,7 @@ __device__ __forceinline__ void apiq_run(uint8_t* __restrict__ slab, uint64_t se
         L.part[0][l] = (u32)part;
     } else if (RR == 1) {  // knights, kings (while the probe lands), the 3-fold commit
         if (gen && !big) {
-            part = (GC_APIQ_SPLIT == 2 ? 0 : gen_knights(ns, g, ms, scr)) + gen_kings(ns, g, ms, scr);
+            part = gen_knights(ns, g, ms, scr) + gen_kings(ns, g, ms, scr);
         }
         L.cbw[1][0][l] = scr.c0;
         L.cbw[1][1][l] = scr.c1;
@@ -3924,14 +3381,14 @@ __device__ __forceinline__ void apiq_run(uint8_t* __restrict__ slab, uint64_t se
         L.ra[l] = ra;
     } else if (RR == 2) {  // queens, bishops
         if (gen && !big) {
-            part = gen_sliders<QUEEN>(ns, g, ms, scr) + (GC_APIQ_SPLIT == 1 ? 0 : gen_sliders<BISHOP>(ns, g, ms, scr));
+            part = gen_sliders<QUEEN>(ns, g, ms, scr);
         }
         L.cbw[2][0][l] = scr.c0;
         L.cbw[2][1][l] = scr.c1;
         L.part[2][l] = (u32)part;
     } else {  // rooks; a big board's whole count
         if (gen && !big) {
-            part = gen_sliders<ROOK>(ns, g, ms, scr) + (GC_APIQ_SPLIT == 1 ? gen_sliders<BISHOP>(ns, g, ms, scr) : 0);
+            part = gen_sliders<ROOK>(ns, g, ms, scr) + gen_sliders<BISHOP>(ns, g, ms, scr);
         } else if (gen) {
             gen_castles(ns, g);
             part = count_legal(ns, g);
@@ -3944,11 +3401,9 @@ __device__ __forceinline__ void apiq_run(uint8_t* __restrict__ slab, uint64_t se
     pair_barrier();
     PST(5);
 
-    // ---- phase 3: the outcome, as k_env_step_api2 (every role: identical arithmetic)
-#ifndef GC_NO_QPRIO_DYN
+    // ---- phase 3: the outcome (every role: identical arithmetic)
     if (RR == 0) __builtin_amdgcn_s_setprio(0);
-    if (RR == 2 || (GC_APIQ_Q3P && RR == 3)) __builtin_amdgcn_s_setprio(2);  // the pick: this phase's longest chain
-#endif
+    if (RR == 2) __builtin_amdgcn_s_setprio(2);  // the pick: this phase's longest chain
     const int total = gen ? (int)(L.part[0][l] + L.part[1][l] + L.part[2][l] + L.part[3][l]) : 0;
     const u32 rpk = L.rep[l];
     const int c = (int)(rpk & 0xFFu);
@@ -4009,10 +3464,8 @@ __device__ __forceinline__ void apiq_run(uint8_t* __restrict__ slab, uint64_t se
             for (int k = 0; k < 16; k++) {
                 const int sq = 16 * RR + k;
                 const bool own = (g.own >> sq) & 1;
-                if (own || !GC_APIQ_EARLY) {  // (without the early zeros: every row, each once)
-                    const u64 w = scr.get(j & (SCRATCH_SLOTS - 1));
-                    apiq_store(mrow + sq * N, own ? w : 0ull);
-                }
+                const u64 w = scr.get(j & (SCRATCH_SLOTS - 1));
+                apiq_store(mrow + sq * N, own ? w : 0ull);
                 j += own ? 1 : 0;
             }
         }
@@ -4087,7 +3540,7 @@ __device__ __forceinline__ void apiq_run(uint8_t* __restrict__ slab, uint64_t se
 #endif
 }
 
-// 16 argument dwords, as k_env_step_api2 (all preloaded)
+// 16 argument dwords, as k_env_step_api4 (all preloaded)
 __global__ void __launch_bounds__(4 * QUAD_BOARDS * QUADS_WG) __attribute__((amdgpu_waves_per_eu(4)))
     k_env_step_api4(uint8_t* __restrict__ slab, uint64_t seed, u64* __restrict__ htab,
                     const uint16_t* __restrict__ racts, const EnvDev::InitCache* __restrict__ icd,
@@ -4206,13 +3659,8 @@ __device__ __forceinline__ void apiqv_run(uint8_t* __restrict__ slab, uint64_t s
     DevHist h = DevHist{htab, in_io.hgen, g0, ii, BLACK ? HTAB_BITS_UNCAPPED : HTAB_BITS};
     if (BLACK && RR == 1) h.sp = icd->spill;  // a BLACK agent's windows may spill
     OrdScratch scr{&L.slots[0][l], 0ull, 0ull};
-#ifndef GC_APIQV_Q3P
-#define GC_APIQV_Q3P 0  // A/B: Q3 over Q1 (their SIMDs' pair) in phases 0, 5 and 6, where Q3's chain is the longer
-                        // (same box: 20.9 vs 20.7 us per launch -- off)
-#endif
+    // (Q3 over Q1 in phases 0, 5 and 6, where Q3's chain is the longer: 20.9 vs 20.7 us per launch)
     if (RR != 3) __builtin_amdgcn_s_setprio(2);
-    if (GC_APIQV_Q3P && RR == 1) __builtin_amdgcn_s_setprio(0);
-    if (GC_APIQV_Q3P && RR == 3) __builtin_amdgcn_s_setprio(2);
     const bool done0 = (s.meta & M_DONE) != 0;   // chess_v2.py:245-251
     const bool cap = mc_of(s.meta) > MOVES_MAX;  // 252-258
     const bool white = (s.meta & M_WHITE) != 0;  // the agent's colour
@@ -4256,8 +3704,6 @@ __device__ __forceinline__ void apiqv_run(uint8_t* __restrict__ slab, uint64_t s
 
     // ---- phase 1: the opponent's position
     if (RR == 2) __builtin_amdgcn_s_setprio(0);
-    if (GC_APIQV_Q3P && RR == 1) __builtin_amdgcn_s_setprio(2);
-    if (GC_APIQV_Q3P && RR == 3) __builtin_amdgcn_s_setprio(0);
     const bool valid = (L.valid[0][l] & L.valid[1][l]) != 0;
     const bool mv = pre && valid;  // the agent's env_ply runs
     Pos ns = s;
@@ -4449,8 +3895,6 @@ __device__ __forceinline__ void apiqv_run(uint8_t* __restrict__ slab, uint64_t s
     PST(7);
 
     // ---- phase 5: the mask position's moves, parked by ordinal; Q1 the reply's commit
-    if (GC_APIQV_Q3P && RR == 1) __builtin_amdgcn_s_setprio(0);
-    if (GC_APIQV_Q3P && RR == 3) __builtin_amdgcn_s_setprio(2);
     const bool chk2 = L.f0[l] != 0, mchk2 = L.f1[l] != 0;  // the agent in check; the opponent, after its reply
     const bool both2 = cont && chk2 && mchk2;
     const bool gen2 = live && !both2;
@@ -4598,6 +4042,9 @@ __device__ __forceinline__ void apiqv_run(uint8_t* __restrict__ slab, uint64_t s
             mrow[64 * N] = cwd;
         }
     }
+#ifdef GC_PSTAMPS
+    const unsigned long long pst_rt1 = __builtin_amdgcn_s_memrealtime();  // the mask rows issued
+#endif
     if (live && RR == 2) {  // the agent's pick (the next draw, action-id order), the count, the env's next action
         const u32 xp = nd == 0 ? L.x0[l] : nd == 1 ? L.x1[l] : L.x2[l];
         int tot = total;
@@ -4660,7 +4107,7 @@ __device__ __forceinline__ void apiqv_run(uint8_t* __restrict__ slab, uint64_t s
         for (int k = 0; k < 8; k++) g_pst_out[w * 12 + k] = gc_pst[threadIdx.x >> 6][k];
         g_pst_out[w * 12 + 8] = pst_entry;
         g_pst_out[w * 12 + 9] = pst_rt0;
-        g_pst_out[w * 12 + 10] = pst_rt0;
+        g_pst_out[w * 12 + 10] = pst_rt1;
         g_pst_out[w * 12 + 11] = __builtin_amdgcn_s_memrealtime();
     }
 #endif
@@ -5535,79 +4982,60 @@ extern "C" int gc_engine_update_state(gc_engine* e, int n, const int8_t* boards,
 // one remaining loop has (nearly) equal trip counts across a wave -- with depth-3 subtrees
 // the inner loop's trip count varied per lane (PMC: ~60 % lane utilisation).
 // leaf-kernel time of the split pass (gc_perft_leaf_stats): HIP events around every
-// k_perft2_perm launch, on the stream it runs on; summed once the pass has synchronised
+// leaf launch (k_perft2_val / k_perft2_rec), on the stream it runs on; summed once the pass has synchronised
 static std::mutex g_leaf_mu;
 static uint64_t g_leaf_launches = 0, g_leaf_subtrees = 0, g_leaf_records = 0;
 static double g_leaf_ms = 0.0;
 
 static int perft_split_leaves(hipStream_t st, SoA leaf, uint64_t* leaf_out) {
     // parents per chunk 2^21 and up to 2^27 children (7.5 GiB of boards); GC_PERFT_CHUNK=k
-    // (A/B): 2^k parents, 2^(k+6) children
+    // (A/B): 2^k parents, 2^(k+6) children (2^20 / 2^22 measured 1.92 / 1.83 vs 1.93e12)
     static const int chunk_log2 = getenv("GC_PERFT_CHUNK") ? atoi(getenv("GC_PERFT_CHUNK")) : 21;
+    // (the lead word holds a sorted position in RUN_LEN_SHIFT bits)
+    if (chunk_log2 < 10 || chunk_log2 + 6 > RUN_LEN_SHIFT)
+        return fail("GC_PERFT_CHUNK must be in [10, 21] (2^k parents per chunk)");
     const int64_t cap = (int64_t)1 << (chunk_log2 + 6);
     int chunk = 1 << chunk_log2;
     std::vector<hipEvent_t> evs;  // pairs around the leaf launches
     uint64_t subtrees = 0, records = 0;  // subtrees counted by the leaf kernel, of records made
-    // GC_PERFT_GATHER (A/B): the round-2/3 form -- records in expansion order, a radix sort by
-    // move count, the leaf kernel gathering through the permutation
-    static const bool gather = getenv("GC_PERFT_GATHER") != nullptr;
-    // GC_PERFT_DEDUP=0 (per call; A/B and tests): every record counted, transpositions too
+    // GC_PERFT_DEDUP=0 (per call; tests): every record counted, transpositions too
     const char* dd = getenv("GC_PERFT_DEDUP");
-    const bool dedup = !gather && !(dd && dd[0] == '0');
-    // GC_PERFT_SORTDEDUP=0 (A/B): the transposition pass by one CAS per record (k_dedup_bin)
-    const char* sd = getenv("GC_PERFT_SORTDEDUP");
-    const bool sortdedup = !(sd && sd[0] == '0');
-    // GC_PERFT_FUSE=0 (A/B, sorting pass only): the followers added by a pass of their own
-    // (k_followers2) instead of by their leader's leaf lane
-    const char* sf = getenv("GC_PERFT_FUSE");
-    // (the lead word holds a sorted position in RUN_LEN_SHIFT bits: chunks of more records take
-    // the follower pass)
-    const bool fuse = sortdedup && !(sf && sf[0] == '0') && cap <= ((int64_t)1 << RUN_LEN_SHIFT);
-    int32_t *kc = nullptr, *offs = nullptr, *kc2 = nullptr, *ks = nullptr, *ix = nullptr, *is = nullptr;
+    const bool dedup = !(dd && dd[0] == '0');
+    int32_t *kc = nullptr, *offs = nullptr;
     uint8_t* bins = nullptr;
     u32 *hist = nullptr, *hbase = nullptr;
     const int max_blk = (chunk + BLOCK - 1) / BLOCK;
-    const int max_dblk = (int)((cap + DEDUP_BLOCK * DEDUP_R - 1) / (DEDUP_BLOCK * DEDUP_R));  // k_dedup_bin's blocks
+    const int max_dblk = (int)((cap + DEDUP_BLOCK * DEDUP_R - 1) / (DEDUP_BLOCK * DEDUP_R));  // the histograms' blocks
     const int hist_n = SPLIT_BINS * (dedup && max_dblk > max_blk ? max_dblk : max_blk);
     Node64* cr = nullptr;
-    // the transposition pass: the records in expansion order, the table (2x the chunk's
-    // records), leader flags, placed index per record, follower (parent, leader) pairs, the
-    // placed leaders' counts, the follower count
+    // the transposition pass: the records in expansion order; the sort's keys / values (16 B per
+    // record), reused after it for the members' (leader, parent) pairs; the lead words; the
+    // placed leaders' sorted positions
     Node64* cre = nullptr;
-    u64* table = nullptr;
-    uint8_t* lflag = nullptr;
-    int32_t* place_of = nullptr;
-    uint2* fol = nullptr;
-    uint64_t* val = nullptr;
-    u32* nfol = nullptr;
+    u32* kv = nullptr;
+    u32* leadw = nullptr;
+    u32* spos = nullptr;
     void* tmp = nullptr;
     size_t tmp_bytes = 0;
     int rc = 0;
     std::string err;
     auto done = [&]() {
-        void* ps[] = {kc, offs, kc2, ks, ix, is, cr, tmp, bins, hist, hbase, cre, table, lflag, place_of, fol, val, nfol};
+        void* ps[] = {kc, offs, cr, tmp, bins, hist, hbase, cre, kv, leadw, spos};
         for (void* q : ps) (void)hipFree(q);
         for (hipEvent_t ev : evs) (void)hipEventDestroy(ev);
     };
-    if (dalloc(&kc, leaf.n) || dalloc(&offs, chunk) || dalloc(&cr, cap) ||
-        (gather ? (dalloc(&kc2, cap) || dalloc(&ks, cap) || dalloc(&ix, cap) || dalloc(&is, cap))
-                : (dalloc(&bins, cap) || dalloc(&hist, (size_t)hist_n) || dalloc(&hbase, (size_t)hist_n))) ||
-        (dedup && (dalloc(&cre, cap) || dalloc(&table, 2 * cap) || dalloc(&lflag, cap) || dalloc(&place_of, cap) ||
-                   dalloc(&fol, cap) || dalloc(&val, cap) || dalloc(&nfol, 1)))) {
+    if (dalloc(&kc, leaf.n) || dalloc(&offs, chunk) || dalloc(&cr, cap) || dalloc(&bins, cap) ||
+        dalloc(&hist, (size_t)hist_n) || dalloc(&hbase, (size_t)hist_n) ||
+        (dedup && (dalloc(&cre, cap) || dalloc(&kv, 4 * cap) || dalloc(&leadw, cap) || dalloc(&spos, cap)))) {
         done();
         return -1;
     }
     {  // scratch for the largest scan and sort of a chunk
-        size_t b1 = 0, b2 = 0;
+        size_t b1 = 0, b2 = 0, b3 = 0;
         hipError_t he = hipcub::DeviceScan::ExclusiveSum(nullptr, b1, kc, offs, chunk, st);
-        if (he == hipSuccess && gather)
-            he = hipcub::DeviceRadixSort::SortPairs(nullptr, b2, kc2, ks, ix, is, (int)cap, 0, 10, st);
-        if (he == hipSuccess && !gather) he = hipcub::DeviceScan::ExclusiveSum(nullptr, b2, hist, hbase, hist_n, st);
-        size_t b3 = 0;  // the sorting transposition pass (keys / values in the table's memory)
-        if (he == hipSuccess && dedup) {
-            u32* kk = reinterpret_cast<u32*>(table);
-            he = hipcub::DeviceRadixSort::SortPairs(nullptr, b3, kk, kk + cap, kk + 2 * cap, kk + 3 * cap, (int)cap, 0, 32, st);
-        }
+        if (he == hipSuccess) he = hipcub::DeviceScan::ExclusiveSum(nullptr, b2, hist, hbase, hist_n, st);
+        if (he == hipSuccess && dedup)
+            he = hipcub::DeviceRadixSort::SortPairs(nullptr, b3, kv, kv + cap, kv + 2 * cap, kv + 3 * cap, (int)cap, 0, 32, st);
         tmp_bytes = b1 > b2 ? b1 : b2;
         tmp_bytes = tmp_bytes > b3 ? tmp_bytes : b3;
         if (he != hipSuccess) { done(); return fail(std::string("perft split: ") + hipGetErrorString(he)); }
@@ -5631,49 +5059,25 @@ static int perft_split_leaves(hipStream_t st, SoA leaf, uint64_t* leaf_out) {
         if (total > 0 && dedup) {  // transpositions merged, the leaders binned and placed in order
             const int n = (int)total;
             const int nbd = (n + DEDUP_BLOCK * DEDUP_R - 1) / (DEDUP_BLOCK * DEDUP_R);
-            u32 tsize = 2;
-            while ((int64_t)tsize < 2 * total) tsize <<= 1;
             k_expand_range_rec<<<grid_for(c), BLOCK, 0, st>>>(leaf, a, c, offs, cre);
-            // keys / values of the sort in the table's memory (16 B per record), parents and
-            // leaders in the follower pairs' (8 B)
-            u32* const keys = reinterpret_cast<u32*>(table);
-            u32* const vals = keys + cap;
-            u32* const keys2 = keys + 2 * cap;
-            u32* const vals2 = keys + 3 * cap;
-            uint2* const fw = reinterpret_cast<uint2*>(table);  // FUSE, after the sort: over keys | vals
-            u32* const parent_of = reinterpret_cast<u32*>(fol);
-            u32* const lead = parent_of + cap;
-            u32* const leadw = parent_of;                              // FUSE: per record
-            u32* const spos = reinterpret_cast<u32*>(place_of);        // FUSE: per placed leader
-            if (fuse) {  // after the sort, the unsorted keys / values hold the members' (leader, parent) pairs
-                k_dedup_keys<<<grid_for(n), BLOCK, 0, st>>>(cre, n, keys, vals, bins, nullptr);
-                tb = tmp_bytes;
-                he = hipcub::DeviceRadixSort::SortPairs(tmp, tb, keys, keys2, vals, vals2, n, 0, 32, st);
-                if (he == hipSuccess) he = hipMemsetAsync(leadw, 0, (size_t)4 * n, st);
-                if (he == hipSuccess) k_dedup_runs_f<<<grid_for(n), BLOCK, 0, st>>>(cre, n, keys2, vals2, leadw, fw);
-                if (he == hipSuccess) k_leader_hist_f<<<nbd, DEDUP_BLOCK, 0, st>>>(n, leadw, bins, hist, nbd);
-            } else if (sortdedup) {
-                k_dedup_keys<<<grid_for(n), BLOCK, 0, st>>>(cre, n, keys, vals, bins, parent_of);
-                tb = tmp_bytes;
-                he = hipcub::DeviceRadixSort::SortPairs(tmp, tb, keys, keys2, vals, vals2, n, 0, 32, st);
-                if (he == hipSuccess) k_dedup_runs<<<grid_for(n), BLOCK, 0, st>>>(cre, n, keys2, vals2, lflag, lead);
-                if (he == hipSuccess) k_leader_hist<<<nbd, DEDUP_BLOCK, 0, st>>>(n, lflag, bins, hist, nbd);
-            } else {
-                he = hipMemsetAsync(table, 0, (size_t)8 * tsize, st);
-                if (he == hipSuccess) he = hipMemsetAsync(nfol, 0, 4, st);
-                if (he == hipSuccess)
-                    k_dedup_bin<<<nbd, DEDUP_BLOCK, 0, st>>>(cre, n, table, tsize - 1, bins, lflag, hist, nbd, nfol, fol);
-            }
+            u32* const keys = kv;
+            u32* const vals = kv + cap;
+            u32* const keys2 = kv + 2 * cap;
+            u32* const vals2 = kv + 3 * cap;
+            uint2* const fw = reinterpret_cast<uint2*>(kv);  // after the sort: over keys | vals
+            k_dedup_keys<<<grid_for(n), BLOCK, 0, st>>>(cre, n, keys, vals, bins);
+            tb = tmp_bytes;
+            he = hipcub::DeviceRadixSort::SortPairs(tmp, tb, keys, keys2, vals, vals2, n, 0, 32, st);
+            if (he == hipSuccess) he = hipMemsetAsync(leadw, 0, (size_t)4 * n, st);
+            if (he == hipSuccess) k_dedup_runs_f<<<grid_for(n), BLOCK, 0, st>>>(cre, n, keys2, vals2, leadw, fw);
+            if (he == hipSuccess) k_leader_hist_f<<<nbd, DEDUP_BLOCK, 0, st>>>(n, leadw, bins, hist, nbd);
             tb = tmp_bytes;
             if (he == hipSuccess) he = hipcub::DeviceScan::ExclusiveSum(tmp, tb, hist, hbase, SPLIT_BINS * nbd, st);
             u32 hb = 0, hl = 0;  // the leaders: the last bin's base + its last block's count
             const size_t last = (size_t)SPLIT_BINS * nbd - 1;
             if (he == hipSuccess) he = hipMemcpyAsync(&hb, hbase + last, 4, hipMemcpyDeviceToHost, st);
             if (he == hipSuccess) he = hipMemcpyAsync(&hl, hist + last, 4, hipMemcpyDeviceToHost, st);
-            if (he == hipSuccess && fuse)
-                k_place_leaders_f<<<nbd, DEDUP_BLOCK, 0, st>>>(cre, n, bins, leadw, hbase, nbd, cr, spos);
-            else if (he == hipSuccess)
-                k_place_leaders<<<nbd, DEDUP_BLOCK, 0, st>>>(cre, n, bins, lflag, hbase, nbd, cr, place_of);
+            if (he == hipSuccess) k_place_leaders_f<<<nbd, DEDUP_BLOCK, 0, st>>>(cre, n, bins, leadw, hbase, nbd, cr, spos);
             if (he == hipSuccess) he = hipStreamSynchronize(st);  // the leaf grid sized to the leaders
             if (he != hipSuccess) { err = std::string("perft split dedup: ") + hipGetErrorString(he); rc = -1; break; }
             const int lead_n = (int)(hb + hl);
@@ -5681,16 +5085,11 @@ static int perft_split_leaves(hipStream_t st, SoA leaf, uint64_t* leaf_out) {
             if (hipEventCreate(&e0) == hipSuccess) evs.push_back(e0);
             if (hipEventCreate(&e1) == hipSuccess) evs.push_back(e1);
             if (e0 && e1) (void)hipEventRecord(e0, st);
-            if (fuse)
-                k_perft2_val<true><<<grid_for(lead_n), BLOCK, 0, st>>>(cr, lead_n, val, psum, n, keys2, fw, spos);
-            else
-                k_perft2_val<false><<<grid_for(lead_n), BLOCK, 0, st>>>(cr, lead_n, val, psum, 0, nullptr, nullptr, nullptr);
+            k_perft2_val<<<grid_for(lead_n), BLOCK, 0, st>>>(cr, lead_n, psum, n, keys2, fw, spos);
             if (e0 && e1) (void)hipEventRecord(e1, st);
-            if (!fuse && sortdedup) k_followers2<<<2048, BLOCK, 0, st>>>(n, lflag, lead, parent_of, place_of, val, psum);
-            else if (!fuse) k_followers<<<2048, BLOCK, 0, st>>>(fol, nfol, place_of, val, psum);
             records += (uint64_t)total;
             subtrees += (uint64_t)lead_n;
-        } else if (total > 0 && !gather) {  // the records in move-count order, then read in order
+        } else if (total > 0) {  // every record, in move-count order, then read in order
             const int nb = grid_for(c);
             k_expand_count<<<nb, BLOCK, 0, st>>>(leaf, a, c, bins, offs, hist, nb);
             tb = tmp_bytes;
@@ -5705,22 +5104,6 @@ static int perft_split_leaves(hipStream_t st, SoA leaf, uint64_t* leaf_out) {
             if (e0 && e1) (void)hipEventRecord(e1, st);
             records += (uint64_t)total;
             subtrees += (uint64_t)total;
-        } else if (total > 0) {
-            k_expand_range_rec<<<grid_for(c), BLOCK, 0, st>>>(leaf, a, c, offs, cr);
-            k_count_children_rec<<<grid_for((int)total), BLOCK, 0, st>>>(cr, (int)total, kc2);
-            k_iota<<<grid_for((int)total), BLOCK, 0, st>>>(ix, (int)total);
-            tb = tmp_bytes;
-            he = hipcub::DeviceRadixSort::SortPairs(tmp, tb, kc2, ks, ix, is, (int)total, 0, 10, st);
-            if (he != hipSuccess) { err = std::string("perft split sort: ") + hipGetErrorString(he); rc = -1; break; }
-            hipEvent_t e0 = nullptr, e1 = nullptr;
-            if (hipEventCreate(&e0) == hipSuccess) evs.push_back(e0);
-            if (hipEventCreate(&e1) == hipSuccess) evs.push_back(e1);
-            if (e0 && e1) (void)hipEventRecord(e0, st);
-            k_perft2_perm_rec<<<grid_for((int)total), BLOCK, 0, st>>>(
-                cr, (int)total, is, reinterpret_cast<unsigned long long*>(leaf_out + a));
-            if (e0 && e1) (void)hipEventRecord(e1, st);
-            subtrees += (uint64_t)total;
-            records += (uint64_t)total;
         }
         he = hipGetLastError();
         if (he != hipSuccess) { err = std::string("perft split kernels: ") + hipGetErrorString(he); rc = -1; break; }
@@ -5927,7 +5310,6 @@ struct gc_env {
     int rules = 0;              // 0 reference, 1 FIDE (gc_fide.h)
     int8_t* ep = nullptr;       // FIDE ingest: en-passant files
     ApiOut* api_out = nullptr;  // the paired API step's output pointers (device copy of api_host)
-    int64_t mask_stride = 0;    // gc_env_step_device's mask row stride in words (0: n)
     ApiOut api_host{};
     uint16_t* reset_acts = nullptr;
     EnvDev::InitCache* icd = nullptr;  // device copy of d.ic (the paired kernels read it from HBM)
@@ -6703,29 +6085,23 @@ extern "C" int gc_env_step(gc_env* e, const uint16_t* actions, int32_t* reward, 
     return 0;
 }
 
-// the row stride (in 64-bit words, >= n; 0 = n) of gc_env_step_device's d_mask from the next call
-// on: with n a multiple of a large power of two, rows n words apart alias on the same HBM
-// channels, so a caller may pad them (gym_chess_amd.env.DeviceIO does)
-extern "C" int gc_env_set_mask_stride(gc_env* e, int64_t words) {
-    if (!e) return fail("null env");
-    if (words != 0 && words < (int64_t)e->n) return fail("mask stride below the board count");
-    e->mask_stride = words;
-    return 0;
-}
-
-// step() with device buffers (k_env_step_api): asynchronous on the env's stream
-// (gc_env_get_stream); every pointer is device memory of n entries (mask: n*65 words, obs:
-// n*64 bytes); mask / obs / count / pick may be NULL.
-extern "C" int gc_env_step_device(gc_env* e, const uint16_t* d_actions, int32_t* d_reward, uint8_t* d_done,
-                                  uint8_t* d_reason, uint64_t* d_mask, int8_t* d_obs, int32_t* d_count,
-                                  uint16_t* d_pick, int flags) {
+// step() with device buffers (k_env_step_api4 and its siblings): asynchronous on the env's
+// stream (gc_env_get_stream); every pointer is device memory of n entries (mask: 65 rows of
+// mask_stride words, word f of board i at f * mask_stride + i; obs: n*64 bytes); mask / obs /
+// count / pick may be NULL.  The stride travels with each call: with n a multiple
+// of a large power of two, packed rows n words apart alias on the same HBM channels, so a caller
+// may pad them (gym_chess_amd.env.DeviceIO does); gc_env_step_device is the packed form.
+extern "C" int gc_env_step_device2(gc_env* e, const uint16_t* d_actions, int32_t* d_reward, uint8_t* d_done,
+                                   uint8_t* d_reason, uint64_t* d_mask, int8_t* d_obs, int32_t* d_count,
+                                   uint16_t* d_pick, int flags, int64_t mask_stride) {
     if (!e || !d_actions || !d_reward || !d_done || !d_reason) return fail("null argument");
     SRV_QUIESCE(e);
     if (flags & ~1) return fail("flags: bit 0 = auto-reset");
+    if (mask_stride != 0 && mask_stride < (int64_t)e->n) return fail("mask stride below the board count");
     HIPCHK(hipSetDevice(e->device));
     if (spill_before(e)) return -1;
     const int ar = flags & 1;
-    const size_t ms = e->mask_stride ? (size_t)e->mask_stride : (size_t)e->n;  // the mask rows' stride
+    const size_t ms = mask_stride ? (size_t)mask_stride : (size_t)e->n;  // the mask rows' stride
     if (e->rules) {  // FIDE: one lane per board
         if (e->d.opp)
             k_fenv_step_api<true><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d, d_actions, d_reward, d_done, d_reason,
@@ -6753,33 +6129,10 @@ extern "C" int gc_env_step_device(gc_env* e, const uint16_t* d_actions, int32_t*
             HIPCHK(hipMemcpyAsync(e->api_out, &e->api_host, sizeof o, hipMemcpyHostToDevice, e->stream));
             HIPCHK(hipStreamSynchronize(e->stream));  // api_host may change again before a lazy copy ran
         }
-        // GC_API_STREAMS=k (diagnostic): over k board-range streams as gc_env_step_random, so a
-        // range's store tail (the mask: 520 B per board) could overlap the other's generation --
-        // measured 47 vs 21 us per step at k = 2 (the ranges' launches did not overlap): one stream
-        static const int api_streams = getenv("GC_API_STREAMS") ? atoi(getenv("GC_API_STREAMS")) : 1;
-        const int k0 = api_streams < e->n_sub ? api_streams : e->n_sub;
-        const int k = k0 < nb ? k0 : nb;
-        const u32 ri = r.rinfo | ((u32)ar << 17);
-        static const bool no_quad = getenv("GC_NO_QUAD_API") && atoi(getenv("GC_NO_QUAD_API")) != 0;  // A/B: api2
-        if (!no_quad && k <= 1) {  // four waves per 64 boards (k_env_step_api4)
-            k_env_step_api4<<<(nb + QUADS_WG - 1) / QUADS_WG, 4 * QUAD_BOARDS * QUADS_WG, 0, e->stream>>>(
-                e->slab, d.seed, d.htab, r.racts, r.icd, d_actions, e->api_out, d.n, ri);
-        } else if (k <= 1) {
-            k_env_step_api2<<<(nb + PAIRS_WG - 1) / PAIRS_WG, 2 * PAIR_BOARDS * PAIRS_WG, 0, e->stream>>>(
-                e->slab, d.seed, d.htab, r.racts, r.icd, d_actions, e->api_out, d.n, ri);
-        } else {
-            const int per = ((nb + k - 1) / k + PAIRS_WG - 1) / PAIRS_WG * PAIRS_WG;  // whole workgroups
-            HIPCHK(hipEventRecord(e->fork_ev, e->stream));
-            for (int j = 0; j < k; j++) {
-                const int b0 = j * per, nbj = nb - b0 < per ? nb - b0 : per;
-                if (nbj <= 0) continue;
-                HIPCHK(hipStreamWaitEvent(e->sub[j], e->fork_ev, 0));
-                k_env_step_api2<<<(nbj + PAIRS_WG - 1) / PAIRS_WG, 2 * PAIR_BOARDS * PAIRS_WG, 0, e->sub[j]>>>(
-                    e->slab, d.seed, d.htab, r.racts, r.icd, d_actions, e->api_out, d.n, ri | ((u32)b0 << 18));
-                HIPCHK(hipEventRecord(e->sub_ev[j], e->sub[j]));
-                HIPCHK(hipStreamWaitEvent(e->stream, e->sub_ev[j], 0));
-            }
-        }
+        // (over two board-range streams, so a range's store tail could overlap the other's
+        // generation: measured 47 vs 21 us per step with the paired kernel, round 3)
+        k_env_step_api4<<<(nb + QUADS_WG - 1) / QUADS_WG, 4 * QUAD_BOARDS * QUADS_WG, 0, e->stream>>>(
+            e->slab, d.seed, d.htab, r.racts, r.icd, d_actions, e->api_out, d.n, r.rinfo | ((u32)ar << 17));
     } else if (e->d.opp && pair_ok(e) && !one_wave) {  // the random opponent on the paired driver
         const EnvDev& d = e->d;
         const ResetInfo r = reset_info(e);
@@ -6822,6 +6175,12 @@ extern "C" int gc_env_step_device(gc_env* e, const uint16_t* d_actions, int32_t*
     if (spill_after(e)) return -1;
     e->policy_ready = d_pick != nullptr;
     return 0;
+}
+
+extern "C" int gc_env_step_device(gc_env* e, const uint16_t* d_actions, int32_t* d_reward, uint8_t* d_done,
+                                  uint8_t* d_reason, uint64_t* d_mask, int8_t* d_obs, int32_t* d_count,
+                                  uint16_t* d_pick, int flags) {
+    return gc_env_step_device2(e, d_actions, d_reward, d_done, d_reason, d_mask, d_obs, d_count, d_pick, flags, 0);
 }
 
 extern "C" int gc_env_get_stream(gc_env* e, void** stream) {

@@ -81,7 +81,7 @@ SIGNATURES = {
     "gc_env_paired": (_I, [_P]),
     "gc_env_rollout_waves": (_I, [_P]),
     "gc_env_step_device": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I]),
-    "gc_env_set_mask_stride": (_I, [_P, ctypes.c_int64]),
+    "gc_env_step_device2": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, ctypes.c_int64]),
     "gc_env_get_stream": (_I, [_P, _P]),
     "gc_device_alloc": (_I, [_I, _U64, _P]),
     "gc_device_free": (_I, [_I, _P]),

@@ -44,7 +44,6 @@ class BatchedChessEnv:
         _lib.check(self._L.gc_env_create(self.device, self.num_boards, ctypes.c_uint64(self.seed),
                                          _lib.ptr(ib) if ib is not None else None, ctypes.byref(h)))
         self._h = h
-        self._mask_stride = 0  # gc_env_set_mask_stride's value (0: num_boards)
         if opponent not in ("none", "random"):
             raise ValueError(f"Unrecognized opponent policy {opponent} (batched env: 'none' or 'random'; "
                              "drive both sides yourself for a custom opponent)")
@@ -287,11 +286,9 @@ class BatchedChessEnv:
         if not a:
             raise ValueError("no actions: pass a device pointer or allocate io with pick=True")
         p = io.ptr
-        if io.mask_stride != self._mask_stride:
-            _lib.check(self._L.gc_env_set_mask_stride(self._h, io.mask_stride))
-            self._mask_stride = io.mask_stride
-        _lib.check(self._L.gc_env_step_device(self._h, a, p["reward"], p["done"], p["reason"], p.get("mask"),
-                                              p.get("obs"), p.get("count"), p.get("pick"), int(bool(autoreset))))
+        _lib.check(self._L.gc_env_step_device2(self._h, a, p["reward"], p["done"], p["reason"], p.get("mask"),
+                                               p.get("obs"), p.get("count"), p.get("pick"), int(bool(autoreset)),
+                                               io.mask_stride))
 
     def stream(self):
         """the env's hipStream_t (for callers ordering their own device work with it)"""
@@ -338,14 +335,19 @@ class TraceBuffer:
 
     def fetch(self, plies=None):
         """host copy of the first `plies` plies as dict(action, reward, done, reason) [ply][board]"""
-        k = self.plies if plies is None else int(plies)
-        w = np.zeros((k, self.env.num_boards), dtype=np.uint64)
-        if w.size:
-            _lib.check(self.env._L.gc_env_copy(self.env._h, _lib.ptr(w), self.ptr, ctypes.c_uint64(w.nbytes), 2))
+        w = self.raw(plies)
         return dict(action=(w & np.uint64(0xFFFF)).astype(np.uint16).view(np.int16),
                     reward=((w >> np.uint64(16)) & np.uint64(0xFFFF)).astype(np.uint16).view(np.int16),
                     done=((w >> np.uint64(32)) & np.uint64(0xFF)).astype(np.uint8),
                     reason=((w >> np.uint64(40)) & np.uint64(0xFF)).astype(np.uint8))
+
+    def raw(self, plies=None):
+        """host copy of the first `plies` plies as the packed words, uint64 [ply][board]"""
+        k = self.plies if plies is None else int(plies)
+        w = np.zeros((k, self.env.num_boards), dtype=np.uint64)
+        if w.size:
+            _lib.check(self.env._L.gc_env_copy(self.env._h, _lib.ptr(w), self.ptr, ctypes.c_uint64(w.nbytes), 2))
+        return w
 
     def close(self):
         if self.ptr:

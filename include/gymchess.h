@@ -165,11 +165,13 @@ int gc_env_step(gc_env* e, const uint16_t* actions, int32_t* reward, uint8_t* do
 int gc_env_step_device(gc_env* e, const uint16_t* d_actions, int32_t* d_reward, uint8_t* d_done,
                        uint8_t* d_reason, uint64_t* d_mask, int8_t* d_obs, int32_t* d_count,
                        uint16_t* d_pick, int flags);
-/* The row stride of gc_env_step_device's d_mask, in words (>= n; 0 = n, the default): word f of
- * board i at d_mask[f * stride + i].  Applies from the next call.  With n a multiple of a large
- * power of two, packed rows (512 KiB apart at n = 65 536) fall on the same HBM channels; a
- * padded stride spreads them. */
-int gc_env_set_mask_stride(gc_env* e, int64_t words);
+/* gc_env_step_device with the mask's row stride in words (>= n; 0 = n, the packed form above):
+ * word f of board i at d_mask[f * mask_stride + i].  With n a multiple of a large power of two,
+ * packed rows (512 KiB apart at n = 65 536) fall on the same HBM channels; a padded stride
+ * spreads them.  The stride is an argument of every call (no state kept on the env). */
+int gc_env_step_device2(gc_env* e, const uint16_t* d_actions, int32_t* d_reward, uint8_t* d_done,
+                        uint8_t* d_reason, uint64_t* d_mask, int8_t* d_obs, int32_t* d_count,
+                        uint16_t* d_pick, int flags, int64_t mask_stride);
 int gc_env_get_stream(gc_env* e, void** stream);
 /* device memory helpers for callers without an allocator; kind 0 h2h 1 h2d 2 d2h 3 d2d
  * (synchronous on the env's stream) */

@@ -777,6 +777,60 @@ void oracle_rollout_batch(const int8_t *init, uint64_t seed, uint32_t b_begin, u
     oracle_rollout_batch2(init, seed, b_begin, n_boards, plies, 0, 1, threads, stats8);
 }
 
+/* Full-width trajectory digests: one 64-bit digest per board of its whole
+ * rollout_board trajectory -- every ply's outputs packed as the device's trace word (action i16 |
+ * reward i16 << 16 | done << 32 | reason << 40, gymchess.hip trace_word), folded in ply order by
+ * d = (d ^ w) * FNV_PRIME, then the final state's 64 board bytes as eight little-endian words and
+ * its 8 meta bytes as one.  Boards handed out across pthreads. */
+#define DIGEST_PRIME 0x100000001B3ull
+static uint64_t digest_fold(uint64_t d, uint64_t w) { return (d ^ w) * DIGEST_PRIME; }
+uint64_t oracle_trace_word(int action, int reward, int done, int reason) {
+    return (uint64_t)(uint16_t)(int16_t)action | ((uint64_t)(uint16_t)(int16_t)reward << 16) |
+           ((uint64_t)(done & 0xFF) << 32) | ((uint64_t)(reason & 0xFF) << 40);
+}
+typedef struct {
+    const int8_t *init; uint64_t seed; int plies, opp, agent_black; uint32_t b_begin, n; atomic_uint *next;
+    uint64_t *out;
+} DJob;
+static void *djob_run(void *arg) {
+    DJob *j = (DJob *)arg;
+    int16_t *a = (int16_t *)malloc((size_t)j->plies * 2), *r = (int16_t *)malloc((size_t)j->plies * 2);
+    uint8_t *dn = (uint8_t *)malloc((size_t)j->plies), *why = (uint8_t *)malloc((size_t)j->plies);
+    for (;;) {
+        uint32_t k = atomic_fetch_add(j->next, 1u);
+        if (k >= j->n) break;
+        OStats st;
+        memset(&st, 0, sizeof(st));
+        int8_t fb[64];
+        uint8_t fm[8];
+        uint32_t draw;
+        rollout_board(j->init, j->seed, j->b_begin + k, j->plies, j->opp, j->agent_black, -1, a, r, dn, why, fb, fm, &draw,
+                      &st);
+        uint64_t d = 0, w;
+        for (int p = 0; p < j->plies; p++) d = digest_fold(d, oracle_trace_word(a[p], r[p], dn[p], why[p]));
+        for (int q = 0; q < 8; q++) { memcpy(&w, fb + 8 * q, 8); d = digest_fold(d, w); }
+        memcpy(&w, fm, 8);
+        j->out[k] = digest_fold(d, w);
+    }
+    free(a); free(r); free(dn); free(why);
+    return NULL;
+}
+void oracle_rollout_digests(const int8_t *init, uint64_t seed, uint32_t b_begin, uint32_t n_boards, int plies, int opp,
+                            int agent_white, int threads, uint64_t *out) {
+    if (threads < 1) threads = 1;
+    atomic_uint next;
+    atomic_init(&next, 0u);
+    DJob *jobs = (DJob *)calloc((size_t)threads, sizeof(DJob));
+    pthread_t *th = (pthread_t *)calloc((size_t)threads, sizeof(pthread_t));
+    for (int t = 0; t < threads; t++) {
+        jobs[t] = (DJob){init, seed, plies, opp, !agent_white, b_begin, n_boards, &next, out};
+        pthread_create(&th[t], NULL, djob_run, &jobs[t]);
+    }
+    for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+    free(jobs);
+    free(th);
+}
+
 /* Trajectory with an opponent mode (0 none, 1 random) and agent colour; order -1 or 1: the
  * policy's move-set order, 0: action-id order (the API step's `pick` output). */
 void oracle_rollout_trace3(const int8_t *init, uint64_t seed, uint32_t board, int plies, int opp, int agent_white,

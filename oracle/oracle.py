@@ -98,6 +98,10 @@ def lib():
         L.oracle_env_window.restype = i32
         L.oracle_env_set_board.argtypes = [P, P, P]
         L.oracle_env_set_board.restype = None
+        L.oracle_rollout_digests.argtypes = [P, u64, u32, u32, i32, i32, i32, i32, P]
+        L.oracle_rollout_digests.restype = None
+        L.oracle_trace_word.argtypes = [i32, i32, i32, i32]
+        L.oracle_trace_word.restype = u64
         _lib = L
     return _lib
 
@@ -221,6 +225,21 @@ def rollout_batch(seed, b_begin, n_boards, plies, threads=1, init=DEFAULT_BOARD,
     lib().oracle_rollout_batch2(_p(init), seed, b_begin, n_boards, plies, int(opponent), int(bool(agent_white)), threads,
                                 _p(st))
     return st
+
+
+DIGEST_PRIME = 0x100000001B3
+
+
+def rollout_digests(seed, n_boards, plies, opponent=0, agent_white=True, threads=1, init=DEFAULT_BOARD, b_begin=0):
+    """Per board b_begin + k, a 64-bit digest of rollout_trace's whole trajectory: every ply's
+    outputs packed as the device's trace word, folded d = (d ^ w) * DIGEST_PRIME in ply order, then
+    the final board (eight little-endian words) and meta (one word) -- gc_oracle.c
+    oracle_rollout_digests; the device side is tests/test_full_width_digest.py's trace_digest."""
+    init = np.ascontiguousarray(init, dtype=np.int8).reshape(64)
+    out = np.zeros(n_boards, dtype=np.uint64)
+    lib().oracle_rollout_digests(_p(init), seed, b_begin, n_boards, plies, int(opponent), int(bool(agent_white)),
+                                 threads, _p(out))
+    return out
 
 
 class OracleEnv:

@@ -207,7 +207,7 @@ def test_step_device_random_opponent_vs_oracle(oracle, color, autoreset):
 
 @pytest.mark.parametrize("kind", ["quad", "opponent", "fide"])
 def test_step_device_mask_stride(kind):
-    """A padded mask row stride (gc_env_set_mask_stride) moves only the rows: two envs stepped
+    """A padded mask row stride (gc_env_step_device2's argument) moves only the rows: envs stepped
     alike, one with packed rows and one with N + 37 and N + 512 words between rows, give equal
     masks and outputs -- on the quad API step, the random opponent's paired step and the FIDE
     one-lane step."""

@@ -28,7 +28,7 @@ out = {"boards": 65536, "note": "rocprofv3 PMC of the API legs of bench.py (100 
 for k, cs in res.items():
     if "FETCH_SIZE" in cs and "WRITE_SIZE" in cs:
         b = cs["FETCH_SIZE"] * 1024 * 2 + cs["WRITE_SIZE"] * 1024
-        name = k.replace("void ", "").split("<")[0]
+        name = k.replace("void ", "").split("(")[0].replace(" ", "")  # k_env_step_api4_vs<true> / <false> apart
         out["kernels"][name] = {"bytes_per_launch": b, "bytes_per_board": b / 65536,
                                 "fetch_bytes": cs["FETCH_SIZE"] * 2048, "write_bytes": cs["WRITE_SIZE"] * 1024}
 json.dump(out, open("gpurun_out/pmc_api.json", "w"), indent=1)
