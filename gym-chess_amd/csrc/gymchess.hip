@@ -2059,8 +2059,29 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
 #define QUADS_WG 2  // two quads per workgroup; the second's roles rotated by 2 so that every SIMD
                     // hosts a state-carrying and a stateless role of each workgroup
 #endif
+// The 3-fold window's occupancy in LDS (GC_OCC; Q1's, a bit per table slot: 64 B per board).
+// The table is open-addressed with linear probing and entries leave it only all at once (a
+// generation bump), so a board whose home slot is free is not in the window -- its probe would
+// stop at once and insert there.  While a board's bitmap mirrors its window (OccQ::valid: since the
+// window was last emptied inside this launch -- a reset or an irreversible move), Q1 tests the
+// next board's home slot in LDS and loads nothing when it is free (~80 % of plies: the window is
+// short and a repetition is rare); a taken home slot (the board again, or another on its slot)
+// is probed in the table as before, and so is every board of a window that predates the launch.
+// Exact: the fast path makes the same decision rep_commit makes on a free first probe.  It
+// removes the probe's line from most plies (the window's bytes).  Where the
+// work goes (tools/pstamp_probe.py: the ply's chain is Q2's, phases 1-3): the bitmap is cleared
+// and the next board looked up in phase 1 (Q1 computes only the mover's check flag there), this
+// ply's entry is added in phase 2 beside the commit; in phase 3 every lane issues ONE load as
+// before -- a slow lane its home entry, a fast lane the env's init block, one line that every
+// lane of the chip reads (it stays in L2) -- so the registers merge no loaded data and the wait
+// stays at phase 2's commit; the fast lane's header is replaced after it.  (v1, all of it in
+// phase 3: Q1's phase 3 2 589 vs 1 447 cycles, -5 % at K = 1 000; v2, a load issued only by the
+// slow lanes: the merge of the loaded registers waited for it at the end of phase 3.)
+#ifndef GC_OCC
+#define GC_OCC 1
+#endif
 struct QuadLds {
-    u64 sets[SW_SETS][QUAD_BOARDS];  // the next side's move sets (Q0: pawns / knights / kings, Q2, Q3)
+    u64 sets[SW_SETS][QUAD_BOARDS];  // the next side's move sets (Q0: pawns / knights, Q2, Q3)
     u64 ns[NBB][QUAD_BOARDS];        // Q0 -> all: the post-move board (phase 0)
     u32 nmeta[QUAD_BOARDS];
     int32_t mr[QUAD_BOARDS];         //           its capture reward
@@ -2069,17 +2090,24 @@ struct QuadLds {
     u32 f0[QUAD_BOARDS];             // Q0 -> Q1: the side to move is in check
     u64 enemy[3][QUAD_BOARDS];       // Q2 / Q3 -> Q0, Q2: the enemy map's leaper + orthogonal ([1]), diagonal ([2]) parts
     u32 f1[QUAD_BOARDS];             // Q1 -> Q0: the mover is in check after its move
-    u64 cwx[2][4][QUAD_BOARDS];      // Q2 / Q3 -> Q0: their sets' byte counts (all four words)
+    u64 cwx[2][4][QUAD_BOARDS];      // Q2 ([0]) / Q3 ([1]) -> Q2: their sets' byte counts (all four words)
+    u64 cw0[2][QUAD_BOARDS];         // Q0 -> Q2: its sets' byte counts (words 0, 1: pawns, knights)
     u32 part[4][QUAD_BOARDS];        // partial move totals (Q0's holds the castles)
     u32 rep[QUAD_BOARDS];            // Q1 -> Q0: 3-fold count | window length << 8
-    u32 x0[QUAD_BOARDS];             // Q1 -> Q0: the Philox word of the next draw
+    u32 x0[QUAD_BOARDS];             // Q1 -> Q2: the Philox word of the next draw
     u32 ra[QUAD_BOARDS];             // Q1 -> Q0: the start-position table pick
     u32 act[QUAD_BOARDS];            // Q0 -> Q1: this ply's action (phase 0)
     u32 pick[QUAD_BOARDS];           // Q2 -> Q0: the policy's pick from this ply's move sets (phase 3)
     u32 castles[QUAD_BOARDS];        // Q0 -> Q2: the castles (phase 2)
-    u64 cw0[QUAD_BOARDS];            // Q0 -> Q2: its sets' byte counts (words 0, 1: pawns, knights)
-    u64 cw1[QUAD_BOARDS];
+#if GC_OCC
+    u64 occ[HTAB / 64][QUAD_BOARDS];  // Q1: the window's taken table slots, a bit per slot
+    u32 nkey[QUAD_BOARDS];            // Q1, phase 1 -> 3: the next board's key if the move stands
+    u32 rkey0;                        // the reset position's key
+#endif
     Pos rp;                          // the reset position (read at a reset: no registers held for it)
+#ifdef GC_LDS_PAD  // diagnostic builds: LDS per quad grown by this many bytes
+    u64 pad[GC_LDS_PAD / 8];
+#endif
 };
 // one set of the next side's moves into LDS, its count into the packed byte counts and the total
 template <class LT>
@@ -2115,10 +2143,17 @@ struct QuadPend {
 };
 
 // One ply of board i for role R of its quad (RoleC<0..3>).  Q0 / Q1: in/out as pair_ply (s, a,
-// d, h, nst); both return the same s and a.  Q2 / Q3: s, a, d, h, nst unused.
+// d, h, nst); both return the same s and a.  Q2 / Q3: s, a, d, h, nst unused.  oq (Q1, GC_OCC):
+// the occupancy bitmap mirrors the window (valid), and is to be cleared before use (clr: a reset)
+struct OccQ {
+    bool valid;  // the bitmap mirrors the window
+    bool clr;    // it is to be cleared first (the window was emptied: a reset, an irreversible move)
+    bool probe;  // the next board, if the move stands, is probed in the table
+    bool fast;   // the probe in flight is the init block's line: its header reads as a free slot
+};
 template <int R>
 __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l, int i, bool live, Pos& s, int& a,
-                                            u32& d, DevHist& h, u32& nst, RepProbe& pr, QuadPend& pend) {
+                                            u32& d, DevHist& h, u32& nst, RepProbe& pr, QuadPend& pend, OccQ& oq) {
     constexpr bool CARRY = R < 2;  // Q0 / Q1 hold the state
     // Q2's pick (phase 3's longest) is raised over Q0's outcome there: 14.43-14.63 -> 14.90-15.12e9
     if (R == 0) __builtin_amdgcn_s_setprio(2);
@@ -2181,6 +2216,18 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
     } else if (R == 1) {
         my_chk = mv && mover_checked(s, ns, white, a);
         L.f1[l] = my_chk ? 1u : 0u;
+#if GC_OCC
+        if (oq.clr) {  // the window was emptied
+#pragma unroll
+            for (int w = 0; w < HTAB / 64; w++) L.occ[w][l] = 0ull;
+            oq.clr = false;
+        }
+        // the next ply's pre-move board if this move stands (ns): its key, and whether its home
+        // slot is taken in the window before this ply's entry (phase 2 adds that one)
+        const u32 nk = board_key(ns);
+        L.nkey[l] = nk;
+        oq.probe = !oq.valid || ((L.occ[(nk & (HTAB - 1)) >> 6][l] >> (nk & 63)) & 1) != 0;
+#endif
     } else if (R == 2) {
         L.enemy[1][l] = g.ks >= 0 ? side_attacks_leapers(ns, !g.white) | side_attacks_orth(ns, !g.white) : 0ull;
     } else {
@@ -2220,14 +2267,27 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
             Q.put_all<SW_N, SW_ORTH>(T + SW_N);
             Q.part += popc(g.castles);
         }
-        L.cw0[l] = Q.cw[0];
-        L.cw1[l] = Q.cw[1];
+        L.cw0[0][l] = Q.cw[0];
+        L.cw0[1][l] = Q.cw[1];
         L.castles[l] = g.castles;
     } else if (R == 1) {
         if (mv && !both) {
             pin(pr.e0.hdr); pin(pr.e0.k); pin(pr.e0.q); pin(pr.e0.r);
             pin(pr.e0.b); pin(pr.e0.n); pin(pr.e0.p); pin(pr.e0.w);
+#if GC_OCC
+            if (oq.fast) pr.e0.hdr = (u64)(h.gen() ^ 1u);  // (after the wait: no loaded register merged)
+#endif
             c = rep_commit(h, s, pr, hl, irrev);  // table write deferred to h.commit()
+#if GC_OCC
+            if (irrev) {  // the window is cleared: from the next ply on the bitmap mirrors it again
+                oq.valid = true;
+                oq.clr = true;
+                oq.probe = false;
+            } else if (h.wkind == 2) {  // this ply's new entry: its slot, and the next board's home?
+                L.occ[h.wpos >> 6][l] |= 1ull << (h.wpos & 63);
+                oq.probe = oq.probe || (u32)h.wpos == (L.nkey[l] & (HTAB - 1));
+            }
+#endif
         }
         L.rep[l] = (u32)c | (hl << 8);
         L.ra[l] = ra;
@@ -2262,8 +2322,8 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
         u64 cw[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) cw[k] = Q.cw[k] | L.cwx[1][k][l];
-        cw[0] |= L.cw0[l];
-        cw[1] |= L.cw1[l];
+        cw[0] |= L.cw0[0][l];
+        cw[1] |= L.cw0[1][l];
         g.castles = L.castles[l];
         // (a board whose generation is not due reads stale sets here: its pick is not taken)
         L.pick[l] = total > 0 ? (u32)sw_pick_lds(L, l, g, cw, total, (int)scale_rank(L.x0[l], (u32)total)) : (u32)A_NONE;
@@ -2312,7 +2372,23 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
         }
         // Q1: the next ply's probe, its pre-move board settled, while Q0 still picks (Q1 waits at
         // the next barrier anyway); after this ply's window write, so it sees it
+#if GC_OCC
+        if (R == 1) {  // (the verdict is phases 1-2's; a reset's window is empty, its bitmap cleared next ply)
+            pr.key = have ? L.nkey[l] : L.rkey0;
+            if (!have) {
+                oq.valid = true;
+                oq.clr = true;
+            }
+            oq.fast = !(live && have && oq.probe);
+            // one load per lane: the home entry, or the init block's line (a free slot, see above)
+            const ulonglong2* src = oq.fast ? reinterpret_cast<const ulonglong2*>(C.icd)
+                                            : reinterpret_cast<const ulonglong2*>(h.htab + h.entry((int)(pr.key & (HTAB - 1))) * 8);
+            const ulonglong2 e0 = src[0], e1 = src[1], e2 = src[2], e3 = src[3];
+            pr.e0 = RepEntry{e0.x, e0.y, e1.x, e1.y, e2.x, e2.y, e3.x, e3.y};
+        }
+#else
         if (R == 1 && live) rep_prefetch(h, s, pr);
+#endif
         // the draw counter (both: the quads run only with the start position's pick table, so a
         // reset's pick count is its total) and Q0's pending choice of the next action
         const int tot = have ? total : (int)C.rtotal;
@@ -2351,11 +2427,23 @@ __device__ __forceinline__ void quad_run(uint8_t* __restrict__ slab, int nn, uin
         d = in_io.draw[ii];
         pin(s); pin(ua); pin(g0); pin(nst); pin(d);
     }
-    if (RR == 0 && l == 0) L.rp = icd->pos;  // read after ply 0's first barrier
+    // the reset position (and its key) into LDS by Q3, which has no work in phase 0 (on Q0 the
+    // wait for its load sat in front of ply 0's apply); read after ply 0's first barrier
+    if (RR == 3 && l == 0) {
+        const Pos rp = icd->pos;
+        L.rp = rp;
+#if GC_OCC
+        L.rkey0 = board_key(rp);
+#endif
+    }
     int a = (int)ua;
     DevHist h = DevHist{htab, in_io.hgen, g0, ii, HTAB_BITS};
     RepProbe pr;  // Q1: the window probe of the coming ply's pre-move board
     if (RR == 1 && live) rep_prefetch(h, s, pr);
+    // Q1: the occupancy bitmap starts empty, so it mirrors a board's window only once that is
+    // empty (from the launch's start, or at a reset / an irreversible move); until then the board
+    // is probed in the table
+    OccQ oq{RR == 1 && hl_of(s.meta) == 0, RR == 1, true, false};
     QuadPend pend{false, false, 0};  // Q0: the first ply's action is the env's
 #ifdef GC_PSTAMPS
     const unsigned long long g_pst_entry = __builtin_amdgcn_s_memrealtime();
@@ -2366,11 +2454,13 @@ __device__ __forceinline__ void quad_run(uint8_t* __restrict__ slab, int nn, uin
     }
     const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();
 #endif
-    uint64_t steps = 0, rsum = 0;
-    u32 e_mate = 0, e_rep = 0, e_cap = 0, e_nomove = 0, e_err = 0;
+    // per-launch stats (ST), packed: a launch runs <= ROLLOUT_MAX_PLIES plies, so every count fits
+    // 16 bits and the reward sum 32 -- four registers instead of nine
+    u32 sa = 0, sb = 0, sc = 0;  // steps | errors << 16, mates | 3-folds << 16, move caps | no-moves << 16
+    int32_t rsum = 0;
     StepOut o = {0, 0, R_NONE, 0};
     for (int p = 0; p < plies; p++) {
-        o = quad_ply<RR>(L, C, l, i, live, s, a, d, h, nst, pr, pend);
+        o = quad_ply<RR>(L, C, l, i, live, s, a, d, h, nst, pr, pend, oq);
         const int played = a;  // (Q0: resolved at the ply's start; Q1: read after its barrier A)
 #ifdef GC_PSTAMPS
         if (p == 0) rt1 = __builtin_amdgcn_s_memrealtime();
@@ -2379,16 +2469,14 @@ __device__ __forceinline__ void quad_run(uint8_t* __restrict__ slab, int nn, uin
             if (trace && live) trace[(size_t)p * nn + i] = trace_word(played == A_NONE ? -1 : played, o);
             if (!ST) {
             } else if (played == A_NONE) {
-                e_nomove++;
+                sc += 1u << 16;
             } else {
-                steps++;
-                rsum += (uint64_t)(int64_t)o.reward;
+                sa += 1u;
+                rsum += o.reward;
                 if (o.done) {
-                    e_mate += o.reason == R_MATE || o.reason == R_MATED;
-                    e_rep += o.reason == R_REPETITION;
-                    e_cap += o.reason == R_MOVE_CAP;
-                    e_err += o.reason == R_BOTH_CHECKED || o.reason == R_WINDOW_FULL;
-                    e_nomove += o.reason == R_OPP_NO_MOVE;
+                    sb += (o.reason == R_MATE || o.reason == R_MATED ? 1u : 0u) | (o.reason == R_REPETITION ? 1u << 16 : 0u);
+                    sc += (o.reason == R_MOVE_CAP ? 1u : 0u) | (o.reason == R_OPP_NO_MOVE ? 1u << 16 : 0u);
+                    sa += o.reason == R_BOTH_CHECKED || o.reason == R_WINDOW_FULL ? 1u << 16 : 0u;
                 }
             }
             h.commit();  // this ply's window write lands before the next ply's probe
@@ -2421,9 +2509,9 @@ __device__ __forceinline__ void quad_run(uint8_t* __restrict__ slab, int nn, uin
         io.reason[i] = (uint8_t)o.reason;
         if (ST) {
             uint64_t* so = stats + 8 * (size_t)i;
-            so[0] += steps; so[1] += rsum;
-            so[2 + R_MATE] += e_mate; so[2 + R_REPETITION] += e_rep; so[2 + R_MOVE_CAP] += e_cap;
-            so[2 + R_NO_MOVES] += e_nomove; so[2 + R_BOTH_CHECKED] += e_err;
+            so[0] += sa & 0xFFFFu; so[1] += (uint64_t)(int64_t)rsum;
+            so[2 + R_MATE] += sb & 0xFFFFu; so[2 + R_REPETITION] += sb >> 16; so[2 + R_MOVE_CAP] += sc & 0xFFFFu;
+            so[2 + R_NO_MOVES] += sc >> 16; so[2 + R_BOTH_CHECKED] += sa >> 16;
         }
     }
 }

@@ -142,8 +142,9 @@ def test_step_device_weird_boards_equal_host_step(oracle, autoreset, opponent):
 @pytest.mark.parametrize("color", ["WHITE", "BLACK"])
 @pytest.mark.parametrize("autoreset", [False, True])
 def test_step_device_random_opponent_vs_oracle(oracle, color, autoreset):
-    """The random opponent's device-buffer step on the paired driver (k_env_step_api2_vs: the
-    agent's half-ply, the reply, a BLACK agent's opening after a reset) in lockstep with the
+    """The random opponent's device-buffer step -- the quad kernel k_env_step_api4_vs for both
+    agent colours (gc_env_step_device2's dispatch; a BLACK agent's reset opening taken from the
+    openings cache, k_init_open_cache): the agent's half-ply, the reply -- in lockstep with the
     oracle env (chess_v2.py:219-294 with the opponent policy): rewards / done / reasons,
     states, observation, mask, count; and every pick == the k-th legal action in action-id
     order for the oracle's draw counter.  Actions: mostly the previous pick, some other legal

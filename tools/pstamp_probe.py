@@ -40,6 +40,8 @@ print(f"launch anatomy ({plies} plies, us from the first wave's start): last wav
 if quad:  # k_env_rollout4: 8 waves per workgroup, roles (w & 3) ^ 2 * quad
     w = np.arange(waves) % 8
     role = (w & 3) ^ (((w >> 2) & 1) << 1)
+    if os.environ.get("PST_WG") == "1":  # one quad per workgroup (QUADS_WG=1): roles 0-3 in order
+        role = w & 3
     names = ["phase 0", "wait A", "phase 1", "wait B", "phase 2", "wait C", "phase 3", "wait D"]
     roles = (0, 1, 2, 3)
 else:

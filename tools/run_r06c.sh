@@ -1,0 +1,11 @@
+#!/bin/bash
+# Round-6 session C: phase stamps of the baseline, the lean Q0 and the pins on Q1; parity gate
+# and same-box A/B of lean Q0 / pins on Q1 / both.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+for v in pst pstlean pstpins; do
+  PST_QUAD=1 PST_LIB=tools/_lib_$v.so timeout -k 10 120 python tools/pstamp_probe.py 65536 1000 > gpurun_out/r06c_$v.log 2>&1 || { echo "PST $v rc=$?"; tail -5 gpurun_out/r06c_$v.log; exit 3; }
+  echo "== $v"; cat gpurun_out/r06c_$v.log
+done
+PARITY=1 LIBS="gym-chess_amd/gym_chess_amd/libgymchess.so tools/_lib_lean.so tools/_lib_pins1.so tools/_lib_leanpins.so" REPS=${REPS:-3} bash tools/ab.sh || exit 4
