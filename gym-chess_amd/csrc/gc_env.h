@@ -148,11 +148,7 @@ struct RepProbe {
 template <class H>
 GC_HD void rep_prefetch(H& h, const Pos& s, RepProbe& pr) {
     pr.key = board_key(s);
-#ifdef GC_DIAG_NOPROBE  // diagnostic builds only (timing, not parity): no probe load, every slot reads as free
-    pr.e0 = RepEntry{0xFFFFFFFFull, 0, 0, 0, 0, 0, 0, 0};
-#else
     pr.e0 = h.load((int)(pr.key & ((1u << h.bits()) - 1)));
-#endif
 }
 
 // Returns how many times the board has been the pre-move board so far, this one included;

@@ -2080,6 +2080,7 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
 #ifndef GC_OCC
 #define GC_OCC 1
 #endif
+
 struct QuadLds {
     u64 sets[SW_SETS][QUAD_BOARDS];  // the next side's move sets (Q0: pawns / knights, Q2, Q3)
     u64 ns[NBB][QUAD_BOARDS];        // Q0 -> all: the post-move board (phase 0)
@@ -2105,9 +2106,6 @@ struct QuadLds {
     u32 rkey0;                        // the reset position's key
 #endif
     Pos rp;                          // the reset position (read at a reset: no registers held for it)
-#ifdef GC_LDS_PAD  // diagnostic builds: LDS per quad grown by this many bytes
-    u64 pad[GC_LDS_PAD / 8];
-#endif
 };
 // one set of the next side's moves into LDS, its count into the packed byte counts and the total
 template <class LT>
@@ -5222,13 +5220,12 @@ static std::atomic<unsigned long long> g_perft_path[4];  // split, sorted, small
 // Leaf level: perft(node, rem) of every node of `leaf` (rem <= 3, or few nodes) into out.
 static int perft_leaf(hipStream_t st, SoA ls, int rem, uint64_t* out, int fide) {
     if (ls.n == 0) return 0;
-    static const bool unsorted = getenv("GC_PERFT_UNSORTED") != nullptr;  // A/B switch
     const char* sp = getenv("GC_PERFT_SPLIT");  // per call: tests compare both paths
-    if (!fide && rem == 3 && ls.n >= 65536 && !unsorted && !(sp && sp[0] == '0')) {
+    if (!fide && rem == 3 && ls.n >= 65536 && !(sp && sp[0] == '0')) {
         g_perft_path[0]++;
         return perft_split_leaves(st, ls, out);
     }
-    if (!fide && rem >= 2 && ls.n >= 65536 && !unsorted) {  // subtrees by root move count
+    if (!fide && rem >= 2 && ls.n >= 65536) {  // subtrees by root move count
         int32_t *kc = nullptr, *ks = nullptr, *ix = nullptr, *is = nullptr;
         void* tmp = nullptr;
         size_t tb = 0;
@@ -5407,8 +5404,6 @@ struct gc_env {
     uint16_t* open_acts = nullptr;
     EnvDev::InitCache ic_f = {};
     uint8_t* slab = nullptr;  // per-board fields (Slab): bb, meta, hgen, draw, nsteps, reward, act, done, reason
-    hipGraphExec_t graph_exec = nullptr;  // GC_GRAPH: a captured chunk of step launches
-    int graph_chunk = 0;
     // Board-range streams of gc_env_step_random (gc_env_set_streams): ply p+1 of one range
     // depends only on ply p of the same range, so the ranges' launches interleave and the
     // launch ramp / tail of one range's ply overlaps another range's waves.
@@ -5455,7 +5450,6 @@ static void env_free(gc_env* e) {
         if (e->sub[j]) (void)hipStreamDestroy(e->sub[j]);
     }
     if (e->fork_ev) (void)hipEventDestroy(e->fork_ev);
-    if (e->graph_exec) (void)hipGraphExecDestroy(e->graph_exec);
     if (e->d.ic.spill.ent) (void)hipFree(e->d.ic.spill.ent);
     if (e->d.ic.spill.ctr) (void)hipFree(e->d.ic.spill.ctr);
     if (e->sp_ctr_h) (void)hipHostFree(e->sp_ctr_h);
@@ -5728,7 +5722,6 @@ static int set_window_kind(gc_env* e, bool uncapped) {
         (void)hipFree(e->d.htab);
         e->d.htab = t;
         e->d.hbits = bits;
-        if (e->graph_exec) { (void)hipGraphExecDestroy(e->graph_exec); e->graph_exec = nullptr; }
     }
     if (uncapped && !e->d.ic.spill.ent) {  // a BLACK agent's windows may outgrow the table
         if (spill_alloc(e, spill_bits_for(e->n))) return -1;
@@ -5951,7 +5944,6 @@ extern "C" int gc_env_set_rules(gc_env* e, int rules) {
         HIPCHK(hipMemcpyAsync(&e->ic_f, e->icd_f, sizeof(EnvDev::InitCache), hipMemcpyDeviceToHost, e->stream));
         HIPCHK(hipStreamSynchronize(e->stream));
     }
-    if (e->graph_exec && rules != e->rules) { (void)hipGraphExecDestroy(e->graph_exec); e->graph_exec = nullptr; }
     e->rules = rules;
     HIPCHK(hipMemsetAsync(e->d.draw, 0, (size_t)4 * e->n, e->stream));
     launch_reset(e, nullptr, 1);
@@ -6202,8 +6194,7 @@ extern "C" int gc_env_step_device2(gc_env* e, const uint16_t* d_actions, int32_t
         e->policy_ready = d_pick != nullptr;
         return 0;
     }
-    static const bool one_wave = getenv("GC_STEP1") != nullptr;  // A/B switch to the one-wave kernel
-    if (!e->d.opp && e->d.ic.usable && e->d.ic.table && !one_wave) {
+    if (!e->d.opp && e->d.ic.usable && e->d.ic.table) {
         const EnvDev& d = e->d;
         const ResetInfo r = reset_info(e);
         const int nb = (e->n + PAIR_BOARDS - 1) / PAIR_BOARDS;
@@ -6221,7 +6212,7 @@ extern "C" int gc_env_step_device2(gc_env* e, const uint16_t* d_actions, int32_t
         // generation: measured 47 vs 21 us per step with the paired kernel, round 3)
         k_env_step_api4<<<(nb + QUADS_WG - 1) / QUADS_WG, 4 * QUAD_BOARDS * QUADS_WG, 0, e->stream>>>(
             e->slab, d.seed, d.htab, r.racts, r.icd, d_actions, e->api_out, d.n, r.rinfo | ((u32)ar << 17));
-    } else if (e->d.opp && pair_ok(e) && !one_wave) {  // the random opponent on the paired driver
+    } else if (e->d.opp && pair_ok(e)) {  // the random opponent on the paired driver
         const EnvDev& d = e->d;
         const ResetInfo r = reset_info(e);
         const int nb = (e->n + PAIR_BOARDS - 1) / PAIR_BOARDS;
@@ -6343,28 +6334,10 @@ extern "C" int gc_env_step_random(gc_env* e, int n_plies) {
     }
     return spill_after(e);
 }
+// (a hipGraph of the plies' launches was measured slower: 11.4 vs 9.8 us per ply, round 2)
 static int step_random(gc_env* e, int n_plies) {
-    static const bool one_wave = getenv("GC_STEP1") != nullptr;  // A/B switch to k_env_step<true, false>
-    static const int graph_chunk = getenv("GC_GRAPH") ? atoi(getenv("GC_GRAPH")) : 0;
-    const bool pair = pair_ok(e) && !one_wave;  // the paired kernel (pair_ok: all but rare opponent setups)
+    const bool pair = pair_ok(e);  // the paired kernel (pair_ok: all but rare opponent setups)
     int p = 0;
-    if (pair && graph_chunk > 0) {
-        if (!e->graph_exec || e->graph_chunk != graph_chunk) {  // captured once per env
-            if (e->graph_exec) (void)hipGraphExecDestroy(e->graph_exec);
-            e->graph_exec = nullptr;
-            hipGraph_t g = nullptr;
-            HIPCHK(hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
-            int rc = issue_plies(e, graph_chunk);  // fork / join of the board-range streams is captured too
-            hipError_t ce = hipStreamEndCapture(e->stream, &g);
-            if (rc) return rc;
-            HIPCHK(ce);
-            hipError_t ge = hipGraphInstantiate(&e->graph_exec, g, nullptr, nullptr, 0);
-            (void)hipGraphDestroy(g);
-            if (ge != hipSuccess) return fail(std::string("graph instantiate: ") + hipGetErrorString(ge));
-            e->graph_chunk = graph_chunk;
-        }
-        for (; p + graph_chunk <= n_plies; p += graph_chunk) HIPCHK(hipGraphLaunch(e->graph_exec, e->stream));
-    }
     if (p < n_plies) {
         if (pair) return issue_plies(e, n_plies - p);
         for (; p < n_plies; p++) {
@@ -6385,19 +6358,13 @@ extern "C" int gc_env_set_streams(gc_env* e, int k) {
         if (!e->sub_ev[j]) HIPCHK(hipEventCreateWithFlags(&e->sub_ev[j], hipEventDisableTiming));
     }
     if (!e->fork_ev) HIPCHK(hipEventCreateWithFlags(&e->fork_ev, hipEventDisableTiming));
-    if (e->graph_exec && k != e->n_sub) {  // a captured chunk holds the old fork / join
-        HIPCHK(hipStreamSynchronize(e->stream));
-        (void)hipGraphExecDestroy(e->graph_exec);
-        e->graph_exec = nullptr;
-    }
     e->n_sub = k;
     return 0;
 }
 
 extern "C" int gc_env_paired(gc_env* e) {
     if (!e) return fail("null env");
-    static const bool one_wave = getenv("GC_STEP1") != nullptr;
-    return pair_ok(e) && !one_wave ? 1 : 0;
+    return pair_ok(e) ? 1 : 0;
 }
 
 // The quads take a reset board's pick from the start position's table only (Q1 reads it in
@@ -6411,9 +6378,7 @@ static bool use_quad(const gc_env* e) {
 
 extern "C" int gc_env_rollout_waves(gc_env* e) {
     if (!e) return fail("null env");
-    static const bool one_wave = getenv("GC_STEP1") != nullptr;
-    const bool pair = pair_ok(e) && (!one_wave || e->rules);
-    return pair ? (use_quad(e) ? 4 : 2) : 1;
+    return pair_ok(e) ? (use_quad(e) ? 4 : 2) : 1;
 }
 
 extern "C" int gc_env_select_random(gc_env* e) {
@@ -6432,8 +6397,7 @@ extern "C" int gc_env_select_random(gc_env* e) {
 // trace_word) when d_trace is not NULL; with `stats`, per-board stats accumulate into e->stats.
 static int issue_rollout(gc_env* e, int n_plies, uint64_t* d_trace, bool stats) {
     uint64_t* const st = stats ? e->stats : nullptr;
-    static const bool one_wave = getenv("GC_STEP1") != nullptr;
-    const bool pair = pair_ok(e) && (!one_wave || e->rules);
+    const bool pair = pair_ok(e);
     const EnvDev& d = e->d;
     const ResetInfo r = reset_info(e);
     const int grid = (e->n + PAIR_BOARDS * PAIRS_WG - 1) / (PAIR_BOARDS * PAIRS_WG), bs = 2 * PAIR_BOARDS * PAIRS_WG;
@@ -6891,8 +6855,7 @@ extern "C" int gc_debug_stamps(gc_env* e, int n_plies, uint64_t* out /* (n/64)*8
     HIPCHK(hipStreamSynchronize(e->stream));
     HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_out), &d, sizeof(d)));
     for (int p = 0; p < n_plies; p++) {
-        if (getenv("GC_STEP1")) k_env_step<true, false><<<grid_for(e->n), BLOCK, 0, e->stream>>>(e->d);
-        else launch_step2(e, e->stream);
+        launch_step2(e, e->stream);
     }
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(out, d, cnt * 8, hipMemcpyDeviceToHost, e->stream));
