@@ -61,7 +61,8 @@ ALG_BYTES_PER_BOARD = 120 + 4 + 24 + 6 + 64 + 64
 
 # the PMC profiles the traffic / VALU figures come from (rocprofv3 passes, tools/gpu_run.sh
 # pmc*; tools/pmc_summary.py); counters cannot be read from inside this process
-PMC_FILE = os.path.join(ROOT, "profiles", "pmc_rollout_latest.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_rollout_latest.json")  # the driver's K = 20 launch
+PMC_FILE_LONG = os.path.join(ROOT, "profiles", "pmc_rollout_long_latest.json")  # a K = 1 000 launch
 PMC_STEP_FILE = os.path.join(ROOT, "profiles", "pmc_traffic_latest.json")
 
 
@@ -659,6 +660,9 @@ def main():
     ctx = rep.run(setup)
     envs = [c[0] for c in ctx]
     rollout_kernel = ROLLOUT_KERNEL[envs[0].rollout_waves()]
+    occ = rollout_kernel == "k_env_rollout4" and args.steps >= envs[0].rollout_occ_min_plies()
+    if rollout_kernel == "k_env_rollout4":  # <true>: with the window's occupancy filter
+        rollout_kernel += "<true>" if occ else "<false>"
 
     def step(rp):
         env, tb = ctx[rep.local.index(rp)][:2]
@@ -698,18 +702,31 @@ def main():
     alg = alg_bytes_fused(mean_window)
     launch_s = sum(kern_ms) / len(kern_ms) / 1e3
     achieved = n * args.steps * alg / launch_s / 1e9
-    pm = load_pmc(PMC_FILE)
+    # the PMC passes of the same kernel variant (the filter halves the window's bytes)
+    pmc_file = PMC_FILE_LONG if occ and os.path.exists(PMC_FILE_LONG) else PMC_FILE
+    pm = load_pmc(pmc_file)
     traffic = pmc_src = valu = None
     if pm:
         # per launch of THIS run: the profiled launch's bytes per board per ply x boards x steps
         bpp = pm.get("bytes_per_board_ply")
         traffic = bpp * n * args.steps if bpp else None
         valu = pm.get("valu")
-        pmc_src = {"file": os.path.relpath(PMC_FILE, ROOT), "profile": pm.get("profile"),
+        pmc_src = {"file": os.path.relpath(pmc_file, ROOT), "profile": pm.get("profile"), "kernel": pm.get("kernel"),
                    "plies_per_launch": pm.get("plies_per_launch"), "bytes_per_board_ply": pm.get("bytes_per_board_ply"),
-                   "note": "rocprofv3 PMC passes of the driver-shaped bench command (not this process); traffic = "
+                   "note": "rocprofv3 PMC passes of the bench command at that launch length (not this process); traffic = "
                            "its FETCH_SIZE x2 + WRITE_SIZE per board per ply (MI355X guide, gfx950 correction) x boards "
                            "x this launch's steps"}
+
+    # what bounds the kernel: "bound" stays the roofline the contract prices it
+    # against (HBM), but at frac ~0.4 the launch is not bandwidth-limited -- half its wave cycles
+    # wait on the ply's dependency chain (workgroup barriers, LDS and the window's line) while the
+    # SIMDs issue well under their peak
+    limiter = None
+    if valu:
+        limiter = {"kind": "dependency-chain latency (4 barriers per ply, role chains Q2 > Q1)",
+                   "wait_any_share": valu.get("wait_any_share"), "issue_frac": valu.get("issue_frac"),
+                   "hbm_frac": achieved / HBM_PEAK_GBS,
+                   "pmc_bytes_vs_alg": (pm.get("bytes_per_board_ply") or 0) / alg if alg else None}
 
     extra = {}
     if rep.world_size > 1 or args.concurrent_ms > 0:
@@ -774,7 +791,7 @@ def main():
                          "kernel": rollout_kernel, "avg_launch_us": launch_s * 1e6,
                          "plies_per_launch": args.steps, "alg_bytes_per_board_ply": alg,
                          "alg_bytes_rule": "SURVEY 8(d) fused rollout ply: 173 + 8h", "mean_window": mean_window,
-                         "valu": valu, "pmc_source": pmc_src},
+                         "valu": valu, "pmc_source": pmc_src, "limiter": limiter},
             "cpu_baseline": cpu,
             **extra,
         }

@@ -2059,7 +2059,7 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
 #define QUADS_WG 2  // two quads per workgroup; the second's roles rotated by 2 so that every SIMD
                     // hosts a state-carrying and a stateless role of each workgroup
 #endif
-// The 3-fold window's occupancy in LDS (GC_OCC; Q1's, a bit per table slot: 64 B per board).
+// The 3-fold window's occupancy in LDS (k_env_rollout4<true>; Q1's, a bit per table slot: 64 B per board).
 // The table is open-addressed with linear probing and entries leave it only all at once (a
 // generation bump), so a board whose home slot is free is not in the window -- its probe would
 // stop at once and insert there.  While a board's bitmap mirrors its window (OccQ::valid: since the
@@ -2077,9 +2077,6 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
 // stays at phase 2's commit; the fast lane's header is replaced after it.  (v1, all of it in
 // phase 3: Q1's phase 3 2 589 vs 1 447 cycles, -5 % at K = 1 000; v2, a load issued only by the
 // slow lanes: the merge of the loaded registers waited for it at the end of phase 3.)
-#ifndef GC_OCC
-#define GC_OCC 1
-#endif
 
 struct QuadLds {
     u64 sets[SW_SETS][QUAD_BOARDS];  // the next side's move sets (Q0: pawns / knights, Q2, Q3)
@@ -2100,11 +2097,9 @@ struct QuadLds {
     u32 act[QUAD_BOARDS];            // Q0 -> Q1: this ply's action (phase 0)
     u32 pick[QUAD_BOARDS];           // Q2 -> Q0: the policy's pick from this ply's move sets (phase 3)
     u32 castles[QUAD_BOARDS];        // Q0 -> Q2: the castles (phase 2)
-#if GC_OCC
-    u64 occ[HTAB / 64][QUAD_BOARDS];  // Q1: the window's taken table slots, a bit per slot
-    u32 nkey[QUAD_BOARDS];            // Q1, phase 1 -> 3: the next board's key if the move stands
-    u32 rkey0;                        // the reset position's key
-#endif
+    u64 occ[HTAB / 64][QUAD_BOARDS];  // (OCC) Q1: the window's taken table slots, a bit per slot
+    u32 nkey[QUAD_BOARDS];            // (OCC) Q1, phase 1 -> 3: the next board's key if the move stands
+    u32 rkey0;                        // (OCC) the reset position's key
     Pos rp;                          // the reset position (read at a reset: no registers held for it)
 };
 // one set of the next side's moves into LDS, its count into the packed byte counts and the total
@@ -2141,7 +2136,7 @@ struct QuadPend {
 };
 
 // One ply of board i for role R of its quad (RoleC<0..3>).  Q0 / Q1: in/out as pair_ply (s, a,
-// d, h, nst); both return the same s and a.  Q2 / Q3: s, a, d, h, nst unused.  oq (Q1, GC_OCC):
+// d, h, nst); both return the same s and a.  Q2 / Q3: s, a, d, h, nst unused.  oq (Q1, OCC):
 // the occupancy bitmap mirrors the window (valid), and is to be cleared before use (clr: a reset)
 struct OccQ {
     bool valid;  // the bitmap mirrors the window
@@ -2149,7 +2144,7 @@ struct OccQ {
     bool probe;  // the next board, if the move stands, is probed in the table
     bool fast;   // the probe in flight is the init block's line: its header reads as a free slot
 };
-template <int R>
+template <int R, bool OCC>
 __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l, int i, bool live, Pos& s, int& a,
                                             u32& d, DevHist& h, u32& nst, RepProbe& pr, QuadPend& pend, OccQ& oq) {
     constexpr bool CARRY = R < 2;  // Q0 / Q1 hold the state
@@ -2214,7 +2209,7 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
     } else if (R == 1) {
         my_chk = mv && mover_checked(s, ns, white, a);
         L.f1[l] = my_chk ? 1u : 0u;
-#if GC_OCC
+        if constexpr (OCC) {
         if (oq.clr) {  // the window was emptied
 #pragma unroll
             for (int w = 0; w < HTAB / 64; w++) L.occ[w][l] = 0ull;
@@ -2225,7 +2220,7 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
         const u32 nk = board_key(ns);
         L.nkey[l] = nk;
         oq.probe = !oq.valid || ((L.occ[(nk & (HTAB - 1)) >> 6][l] >> (nk & 63)) & 1) != 0;
-#endif
+        }
     } else if (R == 2) {
         L.enemy[1][l] = g.ks >= 0 ? side_attacks_leapers(ns, !g.white) | side_attacks_orth(ns, !g.white) : 0ull;
     } else {
@@ -2272,12 +2267,10 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
         if (mv && !both) {
             pin(pr.e0.hdr); pin(pr.e0.k); pin(pr.e0.q); pin(pr.e0.r);
             pin(pr.e0.b); pin(pr.e0.n); pin(pr.e0.p); pin(pr.e0.w);
-#if GC_OCC
-            if (oq.fast) pr.e0.hdr = (u64)(h.gen() ^ 1u);  // (after the wait: no loaded register merged)
-#endif
+            if (OCC && oq.fast) pr.e0.hdr = (u64)(h.gen() ^ 1u);  // (after the wait: no loaded register merged)
             c = rep_commit(h, s, pr, hl, irrev);  // table write deferred to h.commit()
-#if GC_OCC
-            if (irrev) {  // the window is cleared: from the next ply on the bitmap mirrors it again
+            if (!OCC) {
+            } else if (irrev) {  // the window is cleared: from the next ply on the bitmap mirrors it again
                 oq.valid = true;
                 oq.clr = true;
                 oq.probe = false;
@@ -2285,7 +2278,6 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
                 L.occ[h.wpos >> 6][l] |= 1ull << (h.wpos & 63);
                 oq.probe = oq.probe || (u32)h.wpos == (L.nkey[l] & (HTAB - 1));
             }
-#endif
         }
         L.rep[l] = (u32)c | (hl << 8);
         L.ra[l] = ra;
@@ -2370,8 +2362,7 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
         }
         // Q1: the next ply's probe, its pre-move board settled, while Q0 still picks (Q1 waits at
         // the next barrier anyway); after this ply's window write, so it sees it
-#if GC_OCC
-        if (R == 1) {  // (the verdict is phases 1-2's; a reset's window is empty, its bitmap cleared next ply)
+        if (R == 1 && OCC) {  // (the verdict is phases 1-2's; a reset's window is empty, its bitmap cleared next ply)
             pr.key = have ? L.nkey[l] : L.rkey0;
             if (!have) {
                 oq.valid = true;
@@ -2383,10 +2374,9 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
                                             : reinterpret_cast<const ulonglong2*>(h.htab + h.entry((int)(pr.key & (HTAB - 1))) * 8);
             const ulonglong2 e0 = src[0], e1 = src[1], e2 = src[2], e3 = src[3];
             pr.e0 = RepEntry{e0.x, e0.y, e1.x, e1.y, e2.x, e2.y, e3.x, e3.y};
+        } else if (R == 1 && live) {
+            rep_prefetch(h, s, pr);
         }
-#else
-        if (R == 1 && live) rep_prefetch(h, s, pr);
-#endif
         // the draw counter (both: the quads run only with the start position's pick table, so a
         // reset's pick count is its total) and Q0's pending choice of the next action
         const int tot = have ? total : (int)C.rtotal;
@@ -2405,7 +2395,7 @@ __shared__ QuadLds g_quad_lds[QUADS_WG];
 // One role's whole launch (its K plies and its stores), inlined into the kernel's switch on the
 // role: a non-inlined function takes generic pointers -- flat memory instructions, which count
 // in lgkmcnt too, so every barrier's lgkmcnt(0) waited for the window probe in flight.
-template <int RR, bool ST>
+template <int RR, bool ST, bool OCC>
 __device__ __forceinline__ void quad_run(uint8_t* __restrict__ slab, int nn, uint64_t seed, u64* __restrict__ htab,
                                       const uint16_t* __restrict__ racts, const EnvDev::InitCache* __restrict__ icd,
                                       u32 rinfo, int plies, uint64_t* __restrict__ stats, u64* __restrict__ trace,
@@ -2430,9 +2420,7 @@ __device__ __forceinline__ void quad_run(uint8_t* __restrict__ slab, int nn, uin
     if (RR == 3 && l == 0) {
         const Pos rp = icd->pos;
         L.rp = rp;
-#if GC_OCC
-        L.rkey0 = board_key(rp);
-#endif
+        if (OCC) L.rkey0 = board_key(rp);
     }
     int a = (int)ua;
     DevHist h = DevHist{htab, in_io.hgen, g0, ii, HTAB_BITS};
@@ -2458,7 +2446,7 @@ __device__ __forceinline__ void quad_run(uint8_t* __restrict__ slab, int nn, uin
     int32_t rsum = 0;
     StepOut o = {0, 0, R_NONE, 0};
     for (int p = 0; p < plies; p++) {
-        o = quad_ply<RR>(L, C, l, i, live, s, a, d, h, nst, pr, pend, oq);
+        o = quad_ply<RR, OCC>(L, C, l, i, live, s, a, d, h, nst, pr, pend, oq);
         const int played = a;  // (Q0: resolved at the ply's start; Q1: read after its barrier A)
 #ifdef GC_PSTAMPS
         if (p == 0) rt1 = __builtin_amdgcn_s_memrealtime();
@@ -2516,6 +2504,7 @@ __device__ __forceinline__ void quad_run(uint8_t* __restrict__ slab, int nn, uin
 
 // The fused K-ply rollout on quads (k_env_rollout2's contract: same arguments, state, trace
 // and stats).  Q0 writes the next action and draw counter, Q1 the rest, as W0 / W1 there.
+template <bool OCC>
 __global__ void __launch_bounds__(4 * QUAD_BOARDS * QUADS_WG) __attribute__((amdgpu_waves_per_eu(4)))
     k_env_rollout4(uint8_t* __restrict__ slab, int nn, uint64_t seed, u64* __restrict__ htab,
                    const uint16_t* __restrict__ racts, const EnvDev::InitCache* __restrict__ icd, u32 rinfo,
@@ -2544,13 +2533,13 @@ __global__ void __launch_bounds__(4 * QUAD_BOARDS * QUADS_WG) __attribute__((amd
         default: break;
     }
     switch (role) {
-        case 0: quad_run<0, false>(slab, nn, seed, htab, racts, icd, rinfo, plies, stats, trace, qw, l, i); break;
+        case 0: quad_run<0, false, OCC>(slab, nn, seed, htab, racts, icd, rinfo, plies, stats, trace, qw, l, i); break;
         case 1:
-            if (stats) quad_run<1, true>(slab, nn, seed, htab, racts, icd, rinfo, plies, stats, trace, qw, l, i);
-            else quad_run<1, false>(slab, nn, seed, htab, racts, icd, rinfo, plies, stats, trace, qw, l, i);
+            if (stats) quad_run<1, true, OCC>(slab, nn, seed, htab, racts, icd, rinfo, plies, stats, trace, qw, l, i);
+            else quad_run<1, false, OCC>(slab, nn, seed, htab, racts, icd, rinfo, plies, stats, trace, qw, l, i);
             break;
-        case 2: quad_run<2, false>(slab, nn, seed, htab, racts, icd, rinfo, plies, stats, trace, qw, l, i); break;
-        default: quad_run<3, false>(slab, nn, seed, htab, racts, icd, rinfo, plies, stats, trace, qw, l, i); break;
+        case 2: quad_run<2, false, OCC>(slab, nn, seed, htab, racts, icd, rinfo, plies, stats, trace, qw, l, i); break;
+        default: quad_run<3, false, OCC>(slab, nn, seed, htab, racts, icd, rinfo, plies, stats, trace, qw, l, i); break;
     }
     // The completion word: every workgroup, its stores performed (the barrier waits for them),
     // counts itself; the last one bumps the launch count and writes it to host-mapped memory,
@@ -6376,6 +6365,20 @@ static bool use_quad(const gc_env* e) {
     return !no_quad && !e->rules && pair_opp(e) == 0 && e->d.ic.table;
 }
 
+// The occupancy filter (k_env_rollout4<true>, above) costs Q1 ~700 cycles of phase 1 and the
+// ply ~3 % more cycles (tools/pstamp_probe.py); what it buys is half the ply's HBM bytes, and
+// with them the clock a long launch holds under the power limit (r06h stamps: 2.27 vs 2.18 GHz
+// over 1 000 plies).  Same box, always / never (profiles/r06_v1/ab_summary.txt, run_r06j):
+// K = 20 12.44 / 12.91e9, 100 14.75 / 15.22, 300 15.06 / 15.66, 700 15.35 / 15.44, 1 000
+// 15.41 / 15.15, 2 000 15.73 / 15.28 -- so it runs for launches of GC_OCC_MIN_PLIES (768, the
+// crossover) plies or more
+static int occ_min_plies() {
+    static const int v = getenv("GC_OCC_MIN_PLIES") ? atoi(getenv("GC_OCC_MIN_PLIES")) : 768;
+    return v;
+}
+
+extern "C" int gc_env_rollout_occ_min_plies(void) { return occ_min_plies(); }
+
 extern "C" int gc_env_rollout_waves(gc_env* e) {
     if (!e) return fail("null env");
     return pair_ok(e) ? (use_quad(e) ? 4 : 2) : 1;
@@ -6409,8 +6412,12 @@ static int issue_rollout(gc_env* e, int n_plies, uint64_t* d_trace, bool stats) 
         e->done_expect = 0;
         if (pair && use_quad(e)) {
             const int qg = (e->n + QUAD_BOARDS * QUADS_WG - 1) / (QUAD_BOARDS * QUADS_WG);
-            k_env_rollout4<<<qg, 4 * QUAD_BOARDS * QUADS_WG, 0, e->stream>>>(e->slab, d.n, d.seed, d.htab, sw_table(r),
-                                                                             r.icd, ri, st, tr);
+            if (k >= occ_min_plies())
+                k_env_rollout4<true><<<qg, 4 * QUAD_BOARDS * QUADS_WG, 0, e->stream>>>(e->slab, d.n, d.seed, d.htab,
+                                                                                      sw_table(r), r.icd, ri, st, tr);
+            else
+                k_env_rollout4<false><<<qg, 4 * QUAD_BOARDS * QUADS_WG, 0, e->stream>>>(e->slab, d.n, d.seed, d.htab,
+                                                                                       sw_table(r), r.icd, ri, st, tr);
             e->done_expect = ++e->done_issued;
         } else if (pair) {
             switch (e->rules ? 3 : pair_opp(e)) {

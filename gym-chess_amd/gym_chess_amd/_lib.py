@@ -80,6 +80,7 @@ SIGNATURES = {
     "gc_env_set_streams": (_I, [_P, _I]),
     "gc_env_paired": (_I, [_P]),
     "gc_env_rollout_waves": (_I, [_P]),
+    "gc_env_rollout_occ_min_plies": (_I, []),
     "gc_env_step_device": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I]),
     "gc_env_step_device2": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, ctypes.c_int64]),
     "gc_env_get_stream": (_I, [_P, _P]),

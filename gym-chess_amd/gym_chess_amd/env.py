@@ -198,6 +198,11 @@ class BatchedChessEnv:
             _lib.check(r)
         return int(r)
 
+    def rollout_occ_min_plies(self):
+        """the fewest plies per quad launch that run with the window's occupancy filter
+        (gc_env_rollout_occ_min_plies; shorter launches probe the table every ply)"""
+        return int(self._L.gc_env_rollout_occ_min_plies())
+
     def step_random(self, n_plies=1):
         _lib.check(self._L.gc_env_step_random(self._h, int(n_plies)))
 

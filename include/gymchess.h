@@ -198,6 +198,10 @@ int gc_env_paired(gc_env* e);
  * 4 (k_env_rollout4: self-play under the reference rules, unless GC_NO_QUAD is set), 2 (the
  * paired k_env_rollout2) or 1 (the one-wave kernels); -1 on error.  Results are the same. */
 int gc_env_rollout_waves(gc_env* e);
+/* the fewest plies per launch of k_env_rollout4 that run with the 3-fold window's occupancy
+ * filter in LDS (shorter launches probe the window's table every ply); the filter needs a
+ * board's window emptied inside the launch before it applies.  Results are the same. */
+int gc_env_rollout_occ_min_plies(void);
 /* re-pick policy actions for the current states (after set_states / external steps) */
 int gc_env_select_random(gc_env* e);
 /* Same driver fused into ONE launch of n_plies plies (state kept in registers).  Optional

@@ -2,7 +2,7 @@
 # Same-box A/B of libgymchess.so builds, interleaved REPS times (one gpurun call).
 #   LIBS="tools/_lib_a.so gym-chess_amd/gym_chess_amd/libgymchess.so" bash tools/ab.sh
 #   an entry lib.so@VAR=VALUE runs that build with an environment switch
-# MODE=step  (default) the headline fused rollout at K = 20 (the driver's shape) and K = 1000
+# MODE=step  (default) the headline fused rollout at K = 20 (the driver's shape) and K = 1000 (KS: other K)
 # MODE=perft the perft leg (configs[3]: 65 536 mid-game roots, perft(5)) and its leaf kernel time
 # MODE=api   the API-shaped device step (gc_env_step_device); apiv: its random-opponent form
 # PARITY=1   first run tools/ab_parity.py for every build (rollout / step parity subset vs the oracle)
@@ -23,7 +23,7 @@ if [ -n "${PARITY:-}" ]; then
 fi
 NOLEG="--no-cpu-baseline --launched-steps 0 --api-steps 0 --single-episodes 0 --variant-steps 0"
 case $MODE in
-  step)  KS="20 1000"; ARGS="--warmup 5 $NOLEG --perft-roots 0" ;;
+  step)  KS=${KS:-"20 1000"}; ARGS="--warmup 5 $NOLEG --perft-roots 0" ;;
   perft) KS="5"; ARGS="--warmup 5 --settle 0 --no-cpu-baseline --launched-steps 0 --api-steps 0 --single-episodes 0 --variant-steps 0 --oracle-perft-roots 0" ;;
   api|apiv) KS="5"; ARGS="--warmup 5 --settle 0 --no-cpu-baseline --launched-steps 0 --api-steps 200 --single-episodes 0 --variant-steps 0 --perft-roots 0" ;;
   *) echo "unknown MODE $MODE"; exit 2 ;;

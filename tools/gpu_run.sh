@@ -21,6 +21,7 @@ PMCB="python bench.py --no-cpu-baseline --steps 20 --launched-steps 20 --api-ste
 # the headline: the driver's own shape (--steps 20 --warmup 5), the fused launch of 20 steps is
 # the LAST k_env_rollout4 dispatch of the process
 PMCR="python bench.py --no-cpu-baseline --steps 20 --warmup 5 --launched-steps 0 --api-steps 0 --single-episodes 0 --perft-roots 0 --variant-steps 0"
+PMCRL="python bench.py --no-cpu-baseline --steps 1000 --warmup 5 --launched-steps 0 --api-steps 0 --single-episodes 0 --perft-roots 0 --variant-steps 0"  # the K = 1 000 line
 MIXC="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAVE_CYCLES GRBM_GUI_ACTIVE"
 # perft passes: the bench's perft leg (65 536 mid-game FEN roots, perft(5)) without the step legs
 PERFTB="python bench.py --no-cpu-baseline --steps 5 --warmup 5 --settle 0 --launched-steps 0 --api-steps 0 --single-episodes 0 --variant-steps 0 --oracle-perft-roots 0"
@@ -41,6 +42,9 @@ for s in ${STEPS:-smoke pytest bench prof}; do
     pmcrf)  step pmcrf 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_roll_fetch -o run --output-format csv -- $PMCR ;;
     pmcrw)  step pmcrw 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_roll_write -o run --output-format csv -- $PMCR ;;
     pmcrm)  step pmcrm 300 rocprofv3 --pmc $MIXC -d $OUT/pmc_roll_mix -o run --output-format csv -- $PMCR ;;
+    pmcrl)  step pmcr_longf 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_roll_long_fetch -o run --output-format csv -- $PMCRL &&
+            step pmcr_longw 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_roll_long_write -o run --output-format csv -- $PMCRL &&
+            step pmcr_longm 300 rocprofv3 --pmc $MIXC -d $OUT/pmc_roll_long_mix -o run --output-format csv -- $PMCRL ;;
     perftab) step perft_dedup 300 $PERFTB --perft-roots 65536 &&  # the perft leg, transpositions merged / not
             GC_PERFT_DEDUP=0 step perft_every 300 $PERFTB --perft-roots 65536 ;;
     profp)  step profp 300 rocprofv3 --kernel-trace --stats -d $OUT/profp -o run --output-format csv -- $PERFTB &&
@@ -69,6 +73,7 @@ if [ -n "${PROFILE_TAG:-}" ]; then
   [ -d $OUT/pmc_fetch ] && python tools/pmc_summary.py $OUT $OUT/summary/$PROFILE_TAG --kernel "k_env_step2<false, 0>" --dispatches-per-ply ${GC_STREAMS:-2} > /dev/null
   [ -d $OUT/pmc_perft_fetch ] && python tools/pmc_summary.py $OUT $OUT/summary/$PROFILE_TAG --perft > /dev/null
   [ -d $OUT/pmc_roll_fetch ] && python tools/pmc_summary.py $OUT $OUT/summary/$PROFILE_TAG --rollout > /dev/null
+  [ -d $OUT/pmc_roll_long_fetch ] && python tools/pmc_summary.py $OUT $OUT/summary/$PROFILE_TAG --rollout --roll-tag _long > /dev/null
   for f in short1 short2 short3 long; do [ -f $OUT/$f.log ] && grep '^{' $OUT/$f.log | tail -1 > $OUT/summary/$PROFILE_TAG/$f.json; done
   for f in bench pmcf; do [ -f $OUT/$f.log ] && grep '^{' $OUT/$f.log | tail -1 > $OUT/summary/$PROFILE_TAG/$f.json; done
   rm -rf $OUT/prof $OUT/profs $OUT/pmc_*

@@ -40,6 +40,8 @@ def main():
                     help="the split leaf kernel (k_perft2_rec: GC_PERFT_DEDUP=0, k_perft2_perm_rec: GC_PERFT_GATHER)")
     ap.add_argument("--rollout-kernel", default="k_env_rollout4",
                     help="the fused rollout's kernel: k_env_rollout4 (quads), k_env_rollout2<false, 0> (pairs)")
+    ap.add_argument("--roll-tag", default="",
+                    help="the rollout passes' directory tag: pmc_roll<TAG>_* -> pmc_rollout<TAG>.json (_long: K = 1000)")
     ap.add_argument("--calib", action="store_true",
                     help="tools/_valu_calib under the mix counters (pmc_calib + calib.log) -> valu_calib.json")
     a = ap.parse_args()
@@ -168,17 +170,18 @@ def rollout_summary(a):
     board per ply; VALU instructions per wave, lane utilisation, INT64 share, issue fraction
     (calibrated, tools/valu_calib.hip); SQ_WAIT_ANY share of wave cycles."""
     kern = a.rollout_kernel
-    f = per_dispatch(os.path.join(a.src, "pmc_roll_fetch", "run_counter_collection.csv"), kern)[-1]
-    w = per_dispatch(os.path.join(a.src, "pmc_roll_write", "run_counter_collection.csv"), kern)[-1]
-    bl = bench_line(os.path.join(a.src, "pmcrf.log")) or {}
+    t = a.roll_tag
+    f = per_dispatch(os.path.join(a.src, f"pmc_roll{t}_fetch", "run_counter_collection.csv"), kern)[-1]
+    w = per_dispatch(os.path.join(a.src, f"pmc_roll{t}_write", "run_counter_collection.csv"), kern)[-1]
+    bl = bench_line(os.path.join(a.src, f"pmcr{t}f.log")) or {}
     plies = bl.get("steps", 20)
     fetch, write = f["FETCH_SIZE"] * 1024 * 2, w["WRITE_SIZE"] * 1024
     out = {"kernel": kern, "boards": a.boards, "plies_per_launch": plies, "fetch_bytes_corrected": fetch,
            "write_bytes": write, "bytes_per_launch": fetch + write,
            "bytes_per_board_ply": (fetch + write) / a.boards / plies,
            "mean_window": bl.get("roofline", {}).get("mean_window"),
-           "note": "the timed launch of the driver-shaped bench command (--steps 20 --warmup 5); FETCH_SIZE x2"}
-    mp = os.path.join(a.src, "pmc_roll_mix", "run_counter_collection.csv")
+           "note": f"the timed launch of the bench command (--steps {plies} --warmup 5); FETCH_SIZE x2"}
+    mp = os.path.join(a.src, f"pmc_roll{t}_mix", "run_counter_collection.csv")
     if os.path.exists(mp):
         m = per_dispatch(mp, kern)[-1]
         waves = m["SQ_WAVES"]
@@ -190,7 +193,7 @@ def rollout_summary(a):
             out["valu"].update(valu_issue(m, cal))
     out["profile"] = os.path.basename(a.dst.rstrip("/"))
     os.makedirs(a.dst, exist_ok=True)
-    json.dump(out, open(os.path.join(a.dst, "pmc_rollout.json"), "w"), indent=1)
+    json.dump(out, open(os.path.join(a.dst, f"pmc_rollout{t}.json"), "w"), indent=1)
     print(json.dumps(out, indent=1))
 
 

@@ -32,7 +32,8 @@ def main():
                     help="instead: the API step's auto-reset pick loop (gc_env_step_device) vs the oracle driver "
                          "in action-id order, on every sampled board until it first meets a position with no move")
     ap.add_argument("--api-opp", choices=["WHITE", "BLACK"],
-                    help="instead: the random opponent's API step (k_env_step_api2_vs), actions = the previous "
+                    help="instead: the random opponent's API step (the quad kernel k_env_step_api4_vs, either "
+                         "colour), actions = the previous "
                          "pick, auto-reset, in lockstep with the oracle env on the sampled boards")
     ap.add_argument("--launched", action="store_true",
                     help="drive the cases with one launch per ply (step_random: k_env_step2) instead of fused launches")
