@@ -1930,6 +1930,19 @@ __device__ __forceinline__ u64 trace_word(int played, const StepOut& o) {
 }
 #define ROLLOUT_MAX_PLIES 16383  // plies per launch: rinfo bits 18..31
 
+#ifdef GC_PSTAMPS
+// the wave's start (s_memrealtime) with its placement in bits 44+: cu | sh | se | simd | xcc
+// (tools/pstamp_probe.py splits them; as GC_STAMPS_REAL)
+__device__ __forceinline__ unsigned long long pst_entry_where() {
+    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+    unsigned hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)\n\ts_getreg_b32 %1, hwreg(HW_REG_XCC_ID)" : "=s"(hw), "=s"(xcc));
+    const unsigned long long where = ((hw >> 8) & 0xF) | (((hw >> 12) & 1) << 4) | (((hw >> 13) & 3) << 5) |
+                                     (((hw >> 4) & 3) << 7) | ((unsigned long long)(xcc & 0xF) << 9);
+    return (t & ((1ull << 44) - 1)) | (where << 44);
+}
+#endif
+
 // Fused K-ply random self-play on the paired step: the state stays in registers for the K
 // plies (K env.step() calls of every board in one launch); every ply's outputs go to the
 // optional trace [ply][N] (trace_word), the last ply's outputs, the state, window and counters
@@ -1945,15 +1958,7 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
     const int plies = (int)(rinfo >> 18);
     rinfo &= 0x1FFFFu;
 #ifdef GC_PSTAMPS
-    unsigned long long g_pst_entry = __builtin_amdgcn_s_memrealtime();  // wave start, before the entry loads
-    {  // the wave's placement in bits 44+: cu | sh | se | simd | xcc (as GC_STAMPS_REAL)
-        unsigned hw, xcc;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)\n\ts_getreg_b32 %1, hwreg(HW_REG_XCC_ID)"
-                     : "=s"(hw), "=s"(xcc));
-        const unsigned long long where = ((hw >> 8) & 0xF) | (((hw >> 12) & 1) << 4) | (((hw >> 13) & 3) << 5) |
-                                         (((hw >> 4) & 3) << 7) | ((unsigned long long)(xcc & 0xF) << 9);
-        g_pst_entry = (g_pst_entry & ((1ull << 44) - 1)) | (where << 44);
-    }
+    const unsigned long long g_pst_entry = pst_entry_where();  // wave start, before the entry loads
 #endif
     PAIR_PROLOGUE
     uint64_t steps = 0, rsum = 0;
@@ -2432,7 +2437,7 @@ __device__ __forceinline__ void quad_run(uint8_t* __restrict__ slab, int nn, uin
     OccQ oq{RR == 1 && hl_of(s.meta) == 0, RR == 1, true, false};
     QuadPend pend{false, false, 0};  // Q0: the first ply's action is the env's
 #ifdef GC_PSTAMPS
-    const unsigned long long g_pst_entry = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long g_pst_entry = pst_entry_where();
     unsigned long long rt1 = 0;
     if (l == 0) {
         for (int k = 0; k < 8; k++) gc_pst[threadIdx.x >> 6][k] = 0;

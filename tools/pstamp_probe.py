@@ -55,7 +55,32 @@ for r in roles:
     print(f"[{'Q' if quad else 'W'}{r}] {len(s)} waves, {tot:.0f} cycles per ply")
     for k in range(len(names)):
         print(f"   {names[k]:>8}: {s[:, k].mean():7.0f}  ({s[:, k].mean() / tot:5.1%})")
-if quad:
+if quad:  # where the slow waves run (k_env_rollout4): wave end and per-ply time by XCD and by CU
+    xcc = where >> 9
+    cu_key = where & 0x7F | (xcc << 7)
+    end = us[:, 3]
+    per = (us[:, 3] - us[:, 2]) / max(plies - 1, 1)
+    print("wave end by XCD (mean / max us):", " ".join(f"{x}:{end[xcc == x].mean():.1f}/{end[xcc == x].max():.1f}"
+                                                        for x in np.unique(xcc)))
+    print("per-ply us by XCD (mean / max):", " ".join(f"{x}:{per[xcc == x].mean():.3f}/{per[xcc == x].max():.3f}"
+                                                       for x in np.unique(xcc)))
+    _, cu_inv, cu_cnt = np.unique(cu_key, return_inverse=True, return_counts=True)
+    print(f"CUs used {len(cu_cnt)}, waves per CU: " + ", ".join(f"{c}x{k}" for c, k in zip(*np.unique(cu_cnt, return_counts=True))))
+    print("end percentiles (us):", " ".join(f"p{q}:{np.percentile(end, q):.1f}" for q in (0, 10, 25, 50, 75, 90, 99, 100)))
+    wg = np.arange(waves) // 8
+    wg_end = np.array([end[wg == g].max() for g in range(wg.max() + 1)])
+    wg_per = np.array([per[wg == g].mean() for g in range(wg.max() + 1)])
+    print("workgroup end percentiles (us):", " ".join(f"p{q}:{np.percentile(wg_end, q):.1f}" for q in (0, 10, 50, 90, 100)))
+    # per CU: the mean per-ply time of its waves; the spread across CUs says whether the tail is
+    # the place (a slow CU / XCD) or the boards (a workgroup's own work)
+    cu_per = np.array([per[cu_inv == c].mean() for c in range(len(cu_cnt))])
+    print("per-ply us by CU: " + " ".join(f"p{q}:{np.percentile(cu_per, q):.3f}" for q in (0, 10, 50, 90, 100)))
+    # the two workgroups of a CU: how alike their per-ply times are (same place, different boards)
+    pairs = {}
+    for g in range(wg.max() + 1):
+        pairs.setdefault(int(cu_key[wg == g][0]), []).append(g)
+    d = [abs(wg_per[a[0]] - wg_per[a[1]]) for a in pairs.values() if len(a) == 2]
+    print(f"CUs with two workgroups: {len(d)}; |per-ply difference| mean {np.mean(d):.3f} us, max {np.max(d):.3f}")
     sys.exit(0)
 
 # where the slow waves run: wave end by XCD, by CU load and by SIMD load

@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--chunk", type=int, default=1000)
     ap.add_argument("--seeds", type=int, default=5)
     ap.add_argument("--boards", type=int, default=65536)
+    ap.add_argument("--seed-base", type=int, default=1000, help="the opponent-none cases' seeds: base + 7919 k")
     ap.add_argument("--api", action="store_true",
                     help="instead: the API step's auto-reset pick loop (gc_env_step_device) vs the oracle driver "
                          "in action-id order, on every sampled board until it first meets a position with no move")
@@ -62,7 +63,7 @@ def main():
     elif a.random_inits:
         cases = [(2000 + k, "none", "WHITE", ib) for k, ib in enumerate(inits)]
     else:
-        cases = [(1000 + 7919 * k, "none", "WHITE", None) for k in range(a.seeds)]
+        cases = [(a.seed_base + 7919 * k, "none", "WHITE", None) for k in range(a.seeds)]
         cases += [(424242, "random", "WHITE", None), (434343, "random", "BLACK", None)]
     for seed, opp, color, ib in cases:
         bad, spill, secs = fused_case(seed, opp, color, ib, a.plies, a.chunk, n, idx, rules, a.launched, threads)
