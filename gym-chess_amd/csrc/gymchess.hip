@@ -2149,13 +2149,33 @@ struct OccQ {
     bool probe;  // the next board, if the move stands, is probed in the table
     bool fast;   // the probe in flight is the init block's line: its header reads as a free slot
 };
+// The two workgroups of a CU (blocks b and b + half: tools/pstamp_probe.py reads each wave's
+// HW_ID) start together on the same SIMDs, and at equal priority the SQ issues the older wave
+// first -- so block b ran its plies at 4.21 us and block b + half at 5.01 (every CU; same roles on
+// every SIMD), and the launch ended with the later ones.  They take turns instead: on alternate
+// plies one workgroup's roles run one level above the other's (s_setprio 3 / 1 over 2 / 0): 0.14
+// us apart, the launch 4 858 vs 5 636 us by stamps; same box 16.01 vs 15.43e9 at K = 1 000, 13.25
+// vs 13.19e9 at K = 20 (run_r06p).  (Round 3's feedback form, progress words per CU, levelled them
+// too but cost more than it gave.)
+#ifndef GC_WG_FAIR
+#define GC_WG_FAIR 1  // 0: A/B
+#endif
+// s_setprio(x), one level up on the plies where this workgroup has its turn (GC_WG_FAIR)
+#define QSETPRIO(x, up)                                       \
+    do {                                                      \
+        if (GC_WG_FAIR && (up)) __builtin_amdgcn_s_setprio((x) + 1); \
+        else __builtin_amdgcn_s_setprio(x);                   \
+    } while (0)
 template <int R, bool OCC>
 __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l, int i, bool live, Pos& s, int& a,
-                                            u32& d, DevHist& h, u32& nst, RepProbe& pr, QuadPend& pend, OccQ& oq) {
+                                            u32& d, DevHist& h, u32& nst, RepProbe& pr, QuadPend& pend, OccQ& oq,
+                                            bool up = false) {
     constexpr bool CARRY = R < 2;  // Q0 / Q1 hold the state
     // Q2's pick (phase 3's longest) is raised over Q0's outcome there: 14.43-14.63 -> 14.90-15.12e9
-    if (R == 0) __builtin_amdgcn_s_setprio(2);
-    if (R == 2) __builtin_amdgcn_s_setprio(0);
+    if (R == 0) QSETPRIO(2, up);
+    if (R == 2) QSETPRIO(0, up);
+    if (GC_WG_FAIR && R == 1) QSETPRIO(2, up);
+    if (GC_WG_FAIR && R == 3) QSETPRIO(0, up);
     if (R == 0) a = pend.resolve(L, l, a);  // the last ply's action: Q2's pick, or the reset table's
     u32 x0 = 0;
     uint16_t ra = (uint16_t)A_NONE;
@@ -2310,8 +2330,8 @@ __device__ __forceinline__ StepOut quad_ply(QuadLds& L, const PairCtx& C, int l,
     // ---- phase 3: the outcome (Q0 and Q1, identical arithmetic); Q2 picks the next action
     // from the move sets (Q0 takes it, or the reset table's, at the start of the next ply)
     StepOut o = {0, 0, R_NONE, 0};
-    if (R == 0) __builtin_amdgcn_s_setprio(0);
-    if (R == 2) __builtin_amdgcn_s_setprio(2);
+    if (R == 0) QSETPRIO(0, up);
+    if (R == 2) QSETPRIO(2, up);
     if (R == 2) {  // (on Q3, whose SIMDs Q1 shares: 12.77-12.98 vs 13.30-13.42e9)
         const int total = (int)L.part[0][l] + Q.part + (int)L.part[3][l];
         u64 cw[4];
@@ -2436,6 +2456,7 @@ __device__ __forceinline__ void quad_run(uint8_t* __restrict__ slab, int nn, uin
     // is probed in the table
     OccQ oq{RR == 1 && hl_of(s.meta) == 0, RR == 1, true, false};
     QuadPend pend{false, false, 0};  // Q0: the first ply's action is the env's
+    const int wg_half = ((nn + QUAD_BOARDS * QUADS_WG - 1) / (QUAD_BOARDS * QUADS_WG)) >> 1;
 #ifdef GC_PSTAMPS
     const unsigned long long g_pst_entry = pst_entry_where();
     unsigned long long rt1 = 0;
@@ -2451,7 +2472,9 @@ __device__ __forceinline__ void quad_run(uint8_t* __restrict__ slab, int nn, uin
     int32_t rsum = 0;
     StepOut o = {0, 0, R_NONE, 0};
     for (int p = 0; p < plies; p++) {
-        o = quad_ply<RR, OCC>(L, C, l, i, live, s, a, d, h, nst, pr, pend, oq);
+        // (GC_WG_FAIR, above: this workgroup's turn one level up)
+        const bool up = GC_WG_FAIR && ((((int)blockIdx.x >= wg_half) ? 1 : 0) ^ (p & 1));
+        o = quad_ply<RR, OCC>(L, C, l, i, live, s, a, d, h, nst, pr, pend, oq, up);
         const int played = a;  // (Q0: resolved at the ply's start; Q1: read after its barrier A)
 #ifdef GC_PSTAMPS
         if (p == 0) rt1 = __builtin_amdgcn_s_memrealtime();
@@ -6373,12 +6396,12 @@ static bool use_quad(const gc_env* e) {
 // The occupancy filter (k_env_rollout4<true>, above) costs Q1 ~700 cycles of phase 1 and the
 // ply ~3 % more cycles (tools/pstamp_probe.py); what it buys is half the ply's HBM bytes, and
 // with them the clock a long launch holds under the power limit (r06h stamps: 2.27 vs 2.18 GHz
-// over 1 000 plies).  Same box, always / never (profiles/r06_v1/ab_summary.txt, run_r06j):
-// K = 20 12.44 / 12.91e9, 100 14.75 / 15.22, 300 15.06 / 15.66, 700 15.35 / 15.44, 1 000
-// 15.41 / 15.15, 2 000 15.73 / 15.28 -- so it runs for launches of GC_OCC_MIN_PLIES (768, the
-// crossover) plies or more
+// over 1 000 plies).  Same box, always / never, the workgroups taking turns (profiles/r06_v1/
+// ab_summary.txt, run_r06q): K = 20 12.86 / 13.27e9, 100 15.29 / 15.48, 300 15.73 / 15.90, 500
+// 15.79 / 15.91, 700 15.91 / 15.43, 1 000 15.94 / 15.12, 2 000 16.26 / 15.62 -- so it runs for
+// launches of GC_OCC_MIN_PLIES (600, the crossover) plies or more
 static int occ_min_plies() {
-    static const int v = getenv("GC_OCC_MIN_PLIES") ? atoi(getenv("GC_OCC_MIN_PLIES")) : 768;
+    static const int v = getenv("GC_OCC_MIN_PLIES") ? atoi(getenv("GC_OCC_MIN_PLIES")) : 600;
     return v;
 }
 

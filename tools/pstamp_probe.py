@@ -81,6 +81,23 @@ if quad:  # where the slow waves run (k_env_rollout4): wave end and per-ply time
         pairs.setdefault(int(cu_key[wg == g][0]), []).append(g)
     d = [abs(wg_per[a[0]] - wg_per[a[1]]) for a in pairs.values() if len(a) == 2]
     print(f"CUs with two workgroups: {len(d)}; |per-ply difference| mean {np.mean(d):.3f} us, max {np.max(d):.3f}")
+    # which of a CU's two workgroups is the slow one: the later-dispatched (higher index, later
+    # start)?  and the SIMDs its waves sit on
+    first = np.array([us[wg == g, 0].min() for g in range(wg.max() + 1)])
+    slow_later = slow_higher = 0
+    for a in pairs.values():
+        if len(a) != 2:
+            continue
+        f, sl = (a[0], a[1]) if wg_per[a[0]] <= wg_per[a[1]] else (a[1], a[0])
+        slow_later += first[sl] > first[f]
+        slow_higher += sl > f
+    nwg = wg.max() + 1
+    print(f"slow workgroup of a CU: started later in {slow_later} of {len(pairs)}, higher index in {slow_higher}; "
+          f"per-ply us by index half: {wg_per[:nwg // 2].mean():.3f} / {wg_per[nwg // 2:].mean():.3f}")
+    simd = (where >> 7) & 3
+    for g in list(pairs.values())[:3]:
+        print("  CU sample:", [(int(x), f"{wg_per[x]:.3f}", f"start {first[x]:.2f}",
+                               "simds " + "".join(str(int(v)) for v in simd[wg == x])) for x in g])
     sys.exit(0)
 
 # where the slow waves run: wave end by XCD, by CU load and by SIMD load
