@@ -1140,6 +1140,9 @@ __global__ void __launch_bounds__(BLOCK) k_env_step(EnvDev e) {
 // same order of decisions; tests/test_gpu_parity.py compares both with the oracle).
 #define PAIR_BOARDS 64
 #ifndef PAIRS_WG
+#ifndef GC_PAIR_FAIR
+#define GC_PAIR_FAIR 1  // 0: A/B (k_env_rollout2's workgroups taking turns)
+#endif
 #define PAIRS_WG 2  // board pairs (64 boards, two waves) per workgroup: 1 -> 9.8 us per ply, 2 -> 9.3, 4 -> 10.6
 #endif
 struct PairLds {
@@ -1974,9 +1977,16 @@ __global__ void __launch_bounds__(2 * PAIR_BOARDS * PAIRS_WG) PAIR_ATTR
 #endif
     // one loop per role (RoleC): each wave runs only its own role's code; and one with the
     // per-board stats (gc_env_rollout), one without (the device form: no counters per ply)
+    // a CU's two workgroups take turns one priority level up, ply by ply (k_env_rollout4's
+    // GC_WG_FAIR: blocks b and b + half; at equal priority the SQ issues the older wave first)
+    const int wg_half = ((nn + PAIR_BOARDS * PAIRS_WG - 1) / (PAIR_BOARDS * PAIRS_WG)) >> 1;
     auto plies_loop = [&](auto R, auto ST) {
         for (int p = 0; p < plies; p++) {
             int played = a;
+            if (GC_PAIR_FAIR) {
+                if ((((int)blockIdx.x >= wg_half) ? 1 : 0) ^ (p & 1)) __builtin_amdgcn_s_setprio(1);
+                else __builtin_amdgcn_s_setprio(0);
+            }
             o = pair_step<OPP, true, FIDE>(Ls, L, C, R, l, i, live, rp, s, a, d, h, nst);
 #ifdef GC_PSTAMPS
             if (p == 0) rt1 = __builtin_amdgcn_s_memrealtime();

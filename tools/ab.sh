@@ -4,6 +4,7 @@
 #   an entry lib.so@VAR=VALUE runs that build with an environment switch
 # MODE=step  (default) the headline fused rollout at K = 20 (the driver's shape) and K = 1000 (KS: other K)
 # MODE=perft the perft leg (configs[3]: 65 536 mid-game roots, perft(5)) and its leaf kernel time
+# MODE=var   the fused variants on the paired kernel: the random opponent (K=1), FIDE rules (K=2)
 # MODE=api   the API-shaped device step (gc_env_step_device); apiv: its random-opponent form
 # PARITY=1   first run tools/ab_parity.py for every build (rollout / step parity subset vs the oracle)
 # PYTEST=1   first run the whole -m gpu suite on the in-tree build
@@ -25,6 +26,7 @@ NOLEG="--no-cpu-baseline --launched-steps 0 --api-steps 0 --single-episodes 0 --
 case $MODE in
   step)  KS=${KS:-"20 1000"}; ARGS="--warmup 5 $NOLEG --perft-roots 0" ;;
   perft) KS="5"; ARGS="--warmup 5 --settle 0 --no-cpu-baseline --launched-steps 0 --api-steps 0 --single-episodes 0 --variant-steps 0 --oracle-perft-roots 0" ;;
+  var)   KS="5"; ARGS="--warmup 5 --no-cpu-baseline --launched-steps 0 --api-steps 0 --single-episodes 0 --variant-steps 300 --perft-roots 0 --configs1-roots 0" ;;
   api|apiv) KS="5"; ARGS="--warmup 5 --settle 0 --no-cpu-baseline --launched-steps 0 --api-steps 200 --single-episodes 0 --variant-steps 0 --perft-roots 0" ;;
   *) echo "unknown MODE $MODE"; exit 2 ;;
 esac
@@ -41,6 +43,10 @@ d = json.loads([l for l in open("gpurun_out/ab_one.log") if l.startswith("{")][-
 if mode == "perft":
     p = d["perft"]
     print(json.dumps({"lib": lib, "k": 0, "value": p["value"], "aux": p["roofline"]["kernel_ms"], "nodes": p["nodes"]}))
+elif mode == "var":  # the fused variants (k_env_rollout2): k = 1 the random opponent, 2 FIDE rules
+    v = d["variants"]
+    print(json.dumps({"lib": lib, "k": 1, "value": v["opponent_random"]["value"], "aux": 0}))
+    print(json.dumps({"lib": lib, "k": 2, "value": v["rules_fide"]["value"], "aux": 0}))
 elif mode in ("api", "apiv"):
     p = d["api_step"] if mode == "api" else d["api_step"]["opponent_random"]
     print(json.dumps({"lib": lib, "k": 0, "value": p["value"], "aux": p["roofline"]["avg_launch_us"]}))
