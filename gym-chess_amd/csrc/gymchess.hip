@@ -4838,6 +4838,10 @@ static int devsrv_stop_locked(DevSrv& s) {
     void* o = s.owner.exchange(nullptr, std::memory_order_acq_rel);
     return o ? s.stop(o) : 0;
 }
+// (Lock-free when no server is resident.  Callers on other threads may claim the slot between
+// this check and their own launch: that launch then queues behind the new server until the
+// server stops -- at the next call of another owner, or by itself after SRV_IDLE_MS without a
+// request -- a delay, never a wrong result.)
 static int devsrv_quiesce(int dev) {
     DevSrv& s = devsrv(dev);
     if (!s.owner.load(std::memory_order_acquire)) return 0;
