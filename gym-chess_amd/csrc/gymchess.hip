@@ -4593,47 +4593,12 @@ __global__ void __launch_bounds__(BLOCK) k_fenv_step_api(EnvDev e, const uint16_
 // ----------------------------------------------------------------------------- host side
 static inline int grid_for(int n) { return (n + BLOCK - 1) / BLOCK; }
 
-#define GC_MAX_POOL_DEVICES 64
 template <class T>
 static int dalloc(T** p, size_t count) {
     if (count == 0) count = 1;
     hipError_t e = hipMalloc((void**)p, count * sizeof(T));
     if (e != hipSuccess) return fail(std::string("hipMalloc: ") + hipGetErrorString(e));
     return 0;
-}
-// Stream-ordered temporaries (the perft levels' counts, offsets, children and sort buffers):
-// hipMallocAsync from the current device's default pool, freed in stream order -- no device
-// synchronisation per free, and the pool keeps up to POOL_KEEP bytes for the next call (a
-// perft(3) of 4 096 roots made twelve hipMalloc / hipFree pairs per call before)
-static const uint64_t POOL_KEEP = (uint64_t)1 << 30;
-static int pool_keep_once() {
-    static std::mutex mu;
-    static bool done[GC_MAX_POOL_DEVICES] = {};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return 0;
-    std::lock_guard<std::mutex> lk(mu);
-    if (dev < 0 || dev >= GC_MAX_POOL_DEVICES || done[dev]) return 0;
-    done[dev] = true;
-    hipMemPool_t pool;
-    if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
-        uint64_t keep = POOL_KEEP;
-        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
-    }
-    return 0;
-}
-template <class T>
-static int dalloc_s(T** p, size_t count, hipStream_t st) {
-    pool_keep_once();
-    if (count == 0) count = 1;
-    hipError_t e = hipMallocAsync((void**)p, count * sizeof(T), st);
-    if (e != hipSuccess) {
-        *p = nullptr;
-        return fail(std::string("hipMallocAsync: ") + hipGetErrorString(e));
-    }
-    return 0;
-}
-static void dfree_s(void* p, hipStream_t st) {
-    if (p) (void)hipFreeAsync(p, st);
 }
 
 struct gc_engine {
@@ -5296,22 +5261,20 @@ static int perft_leaf(hipStream_t st, SoA ls, int rem, uint64_t* out, int fide) 
         void* tmp = nullptr;
         size_t tb = 0;
         hipError_t he = hipSuccess;
-        if (dalloc_s(&kc, ls.n, st) || dalloc_s(&ks, ls.n, st) || dalloc_s(&ix, ls.n, st) || dalloc_s(&is, ls.n, st))
-            he = hipErrorOutOfMemory;
+        if (dalloc(&kc, ls.n) || dalloc(&ks, ls.n) || dalloc(&ix, ls.n) || dalloc(&is, ls.n)) he = hipErrorOutOfMemory;
         if (he == hipSuccess) {
             k_count_children<int32_t><<<grid_for(ls.n), BLOCK, 0, st>>>(ls, kc);
             k_iota<<<grid_for(ls.n), BLOCK, 0, st>>>(ix, ls.n);
             he = hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kc, ks, ix, is, ls.n, 0, 10, st);
         }
-        if (he == hipSuccess && dalloc_s((char**)&tmp, tb, st) == 0)
+        if (he == hipSuccess && dalloc((char**)&tmp, tb) == 0)
             he = hipcub::DeviceRadixSort::SortPairs(tmp, tb, kc, ks, ix, is, ls.n, 0, 10, st);
         bool ok = he == hipSuccess && tmp;
         if (ok) {
             k_perft_small_perm<<<grid_for(ls.n), BLOCK, 0, st>>>(ls, is, rem, out);
-            he = hipGetLastError();
+            he = hipStreamSynchronize(st);  // before the temporaries are freed
         }
-        // (freed in stream order: the pass above still reads them)
-        dfree_s(tmp, st); dfree_s(kc, st); dfree_s(ks, st); dfree_s(ix, st); dfree_s(is, st);
+        (void)hipFree(tmp); (void)hipFree(kc); (void)hipFree(ks); (void)hipFree(ix); (void)hipFree(is);
         if (he != hipSuccess) return fail(std::string("perft sort: ") + hipGetErrorString(he));
         if (ok) { g_perft_path[1]++; return 0; }
     }
@@ -5346,16 +5309,17 @@ static int perft_nodes(hipStream_t st, SoA nodes, int rem, uint64_t* out, int fi
     size_t tmp_bytes = 0;
     int64_t held = 0;  // children the buffers below can hold
     std::string err;
-    auto release = [&]() {  // in stream order: the work queued on st before still reads them
+    auto release = [&]() {
+        (void)hipStreamSynchronize(st);  // nothing in flight may still use the buffers
         void* ps[] = {cnt, offs, cb, cm, cval, tmp};
-        for (void* q : ps) dfree_s(q, st);
+        for (void* q : ps) (void)hipFree(q);
         cb = nullptr; cm = nullptr; cval = nullptr;
     };
-    if (dalloc_s(&cnt, n, st) || dalloc_s(&offs, n, st)) { release(); return -1; }
+    if (dalloc(&cnt, n) || dalloc(&offs, n)) { release(); return -1; }
     if (fide) k_fcount_children<<<grid_for(n), BLOCK, 0, st>>>(nodes, cnt);
     else k_count_children<int64_t><<<grid_for(n), BLOCK, 0, st>>>(nodes, cnt);
     hipError_t he = hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, cnt, offs, n, st);
-    if (he != hipSuccess || dalloc_s((char**)&tmp, tmp_bytes ? tmp_bytes : 1, st)) {
+    if (he != hipSuccess || dalloc((char**)&tmp, tmp_bytes ? tmp_bytes : 1)) {
         release();
         return he != hipSuccess ? fail(std::string("perft scan: ") + hipGetErrorString(he)) : -1;
     }
@@ -5372,14 +5336,12 @@ static int perft_nodes(hipStream_t st, SoA nodes, int rem, uint64_t* out, int fi
         const int64_t total = lo + lc;
         if (total > cap && c > 1) { chunk = (c + 1) / 2; continue; }  // halve the chunk and rescan
         if (total >= ((int64_t)1 << 31)) { err = "perft: one node has too many children"; break; }
-        if (total > held) {  // (re)allocate the child buffers for this chunk (stream order)
-            dfree_s(cb, st); dfree_s(cm, st); dfree_s(cval, st);
+        if (total > held) {  // (re)allocate the child buffers for this chunk
+            (void)hipStreamSynchronize(st);
+            (void)hipFree(cb); (void)hipFree(cm); (void)hipFree(cval);
             cb = nullptr; cm = nullptr; cval = nullptr;
             held = 0;
-            if (dalloc_s(&cb, (size_t)NBB * total, st) || dalloc_s(&cm, total, st) || dalloc_s(&cval, total, st)) {
-                err = g_err;
-                break;
-            }
+            if (dalloc(&cb, (size_t)NBB * total) || dalloc(&cm, total) || dalloc(&cval, total)) { err = g_err; break; }
             held = total;
         }
         if (total > 0) {
