@@ -2162,11 +2162,11 @@ struct OccQ {
 // The two workgroups of a CU (blocks b and b + half: tools/pstamp_probe.py reads each wave's
 // HW_ID) start together on the same SIMDs, and at equal priority the SQ issues the older wave
 // first -- so block b ran its plies at 4.21 us and block b + half at 5.01 (every CU; same roles on
-// every SIMD), and the launch ended with the later ones.  They take turns instead: on alternate
-// plies one workgroup's roles run one level above the other's (s_setprio 3 / 1 over 2 / 0): 0.14
-// us apart, the launch 4 858 vs 5 636 us by stamps; same box 16.01 vs 15.43e9 at K = 1 000, 13.25
-// vs 13.19e9 at K = 20 (run_r06p).  (Round 3's feedback form, progress words per CU, levelled them
-// too but cost more than it gave.)
+// every SIMD), and the launch ended with the later ones.  They take turns instead: for turns of
+// GC_TURN_SHIFT (below) plies one workgroup's roles run one level above the other's (s_setprio 3 /
+// 1 over 2 / 0).  One-ply turns: 0.14 us apart, the launch 4 858 vs 5 636 us by stamps; same box
+// 16.01 vs 15.43e9 at K = 1 000, 13.25 vs 13.19e9 at K = 20 (run_r06p).  (Round 3's feedback form,
+// progress words per CU, levelled them too but cost more than it gave.)
 #ifndef GC_WG_FAIR
 #define GC_WG_FAIR 1  // 0: A/B
 #endif
@@ -2483,7 +2483,11 @@ __device__ __forceinline__ void quad_run(uint8_t* __restrict__ slab, int nn, uin
     StepOut o = {0, 0, R_NONE, 0};
     for (int p = 0; p < plies; p++) {
         // (GC_WG_FAIR, above: this workgroup's turn one level up)
-        const bool up = GC_WG_FAIR && ((((int)blockIdx.x >= wg_half) ? 1 : 0) ^ (p & 1));
+#ifndef GC_TURN_SHIFT
+#define GC_TURN_SHIFT 2  // turns of 4 plies: same box at K = 20, 8 repeats, 13.32 vs 13.01e9 (events
+                         // 4.53 vs 4.66 us per ply; 8-ply turns 13.22); at K = 1 000 level (run_r06v, w)
+#endif
+        const bool up = GC_WG_FAIR && ((((int)blockIdx.x >= wg_half) ? 1 : 0) ^ ((p >> GC_TURN_SHIFT) & 1));
         o = quad_ply<RR, OCC>(L, C, l, i, live, s, a, d, h, nst, pr, pend, oq, up);
         const int played = a;  // (Q0: resolved at the ply's start; Q1: read after its barrier A)
 #ifdef GC_PSTAMPS
